@@ -1,0 +1,836 @@
+// C-ABI entry points of libfactmx.so (declared in include/factmx.h).
+//
+// Composite ops (Linear fwd/bwd, the whole MS-TCN stack, the MHA core) are
+// orchestrated here in C++ so one Python call launches the whole sequence on
+// the caller's stream; kernels live in gemm_f32.hip, rowops.hip, segments.hip.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "fx_common.h"
+
+namespace fx {
+
+// ---- kernels implemented in the other translation units -------------------
+long long colsum_workspace_floats(int M, int N);
+int launch_layernorm_fwd(const float* x, long long ldx, const float* r, long long ldr, const float* w,
+                         const float* b, float eps, int rows, int cols, int relu, float* y, long long ldy,
+                         float* mean, float* rstd, float* xhat, long long ldxh, hipStream_t s);
+long long layernorm_bwd_ws_floats(int rows, int cols);
+int launch_layernorm_bwd(const float* dy, long long lddy, const float* y, long long ldy, const float* xhat,
+                         long long ldxh, const float* w, const float* rstd, int rows, int cols, int relu,
+                         float* dx, long long lddx, float* dw, float* db, float* ws, hipStream_t s);
+int launch_softmax_rows(const float* x, long long ldx, int rows, int cols, float scale, float* p, long long ldp,
+                        hipStream_t s);
+int launch_softmax_rows_bwd(const float* p, long long ldp, const float* dp, long long lddp, const float* extra,
+                            long long lde, int rows, int cols, float scale, float* dl, long long ldd,
+                            hipStream_t s);
+int launch_pf_fwd(const float* x, long long ldx, int rows, int cols, int n, float* out, long long ldo,
+                  hipStream_t s);
+int launch_pf_bwd(const float* out, long long ldo, const float* dout, long long lddo, const float* dcl,
+                  long long lddc, int rows, int cols, int n, float* dx, long long lddx, hipStream_t s);
+int launch_l2n_fwd(const float* x, long long ldx, int rows, int cols, float* y, long long ldy, float* nrm,
+                   hipStream_t s);
+int launch_l2n_bwd(const float* y, long long ldy, const float* nrm, const float* dy, long long lddy, int rows,
+                   int cols, float* dx, long long lddx, hipStream_t s);
+int launch_segments(const float* x, long long ldx, int col0, int ncls, int T, int32_t* pred, int32_t* seg_id,
+                    int32_t* seg_start, int32_t* seg_end, int32_t* num_seg, hipStream_t s);
+int launch_seg_reduce(const float* x, long long ldx, const int32_t* st, const int32_t* en, int S, int cols, int mean,
+                      float* y, long long ldy, int accumulate, hipStream_t s);
+int launch_seg_mean_bwd(const float* dy, long long lddy, const int32_t* sid, const int32_t* st, const int32_t* en,
+                        int T, int cols, float* dx, long long lddx, int accumulate, hipStream_t s);
+
+// ---- error state ------------------------------------------------------------
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+// ---- profiling (opt-in diagnostic used by bench.py) ---------------------------
+namespace {
+struct ProfState {
+  int kind = -1;
+  int max_events = 0;
+  std::vector<hipEvent_t> ev;
+  std::vector<double> flops, bytes;
+  int used = 0;
+  hipEvent_t pending = nullptr;
+};
+std::mutex g_prof_mu;
+ProfState g_prof;
+}  // namespace
+
+void prof_begin(int kind, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  if (g_prof.kind != kind || g_prof.used >= g_prof.max_events) return;
+  (void)hipEventRecord(g_prof.ev[2 * g_prof.used], s);
+}
+
+void prof_end(int kind, hipStream_t s, double flops, double bytes) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  if (g_prof.kind != kind || g_prof.used >= g_prof.max_events) return;
+  (void)hipEventRecord(g_prof.ev[2 * g_prof.used + 1], s);
+  g_prof.flops[g_prof.used] = flops;
+  g_prof.bytes[g_prof.used] = bytes;
+  g_prof.used++;
+}
+
+// ---- helpers -------------------------------------------------------------------
+namespace {
+
+__global__ void relu_bwd_kernel(const float* dy, long long lddy, const float* y, long long ldy, int rows, int cols,
+                                float* dz, long long lddz) {
+  const long long total = (long long)rows * cols;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / cols, c = i % cols;
+    dz[r * lddz + c] = y[r * ldy + c] > 0.f ? dy[r * lddy + c] : 0.f;
+  }
+}
+
+__global__ void add2_kernel(const float* a, long long lda, const float* b, long long ldb, int rows, int cols,
+                            float* o, long long ldo, int accumulate) {
+  const long long total = (long long)rows * cols;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / cols, c = i % cols;
+    const float v = a[r * lda + c] + (b ? b[r * ldb + c] : 0.f);
+    o[r * ldo + c] = accumulate ? o[r * ldo + c] + v : v;
+  }
+}
+
+struct PackArgs {
+  const float* w[32];
+  float* wf[32];
+  float* wb[32];
+  int F;
+};
+
+// Conv1d weight (F_out=F, F_in=F, 3) -> Wf[n][j*F+c] (forward B) and Wb[c][j*F+n] (dX B)
+__global__ void pack_conv_kernel(PackArgs p) {
+  const int l = blockIdx.y;
+  const int F = p.F;
+  const long long total = 3LL * F * F;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int n = (int)(i / (3 * F));
+    const int rem = (int)(i % (3 * F));
+    const int c = rem / 3, j = rem % 3;
+    const float v = p.w[l][i];
+    p.wf[l][(long long)n * 3 * F + j * F + c] = v;
+    p.wb[l][(long long)c * 3 * F + j * F + n] = v;
+  }
+}
+
+int ew_grid(long long total) { return (int)std::min<long long>(std::max<long long>(cdiv(total, 256), 1), 4096); }
+
+int relu_bwd(const float* dy, long long lddy, const float* y, long long ldy, int rows, int cols, float* dz,
+             long long lddz, hipStream_t s) {
+  if ((long long)rows * cols == 0) return FX_OK;
+  hipLaunchKernelGGL(relu_bwd_kernel, dim3(ew_grid((long long)rows * cols)), dim3(256), 0, s, dy, lddy, y, ldy, rows,
+                     cols, dz, lddz);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+int add2(const float* a, long long lda, const float* b, long long ldb, int rows, int cols, float* o, long long ldo,
+         int accumulate, hipStream_t s) {
+  if ((long long)rows * cols == 0) return FX_OK;
+  hipLaunchKernelGGL(add2_kernel, dim3(ew_grid((long long)rows * cols)), dim3(256), 0, s, a, lda, b, ldb, rows, cols,
+                     o, ldo, accumulate);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+// split-K factor for small-output / long-K products (dW over frames, token x frame)
+int pick_split(int M, int N, int K, int batch = 1) {
+  const long long tiles = (long long)cdiv(M, 64) * cdiv(N, 64) * batch;
+  const int nkt = cdiv(K, 32);
+  if (tiles >= 160 || nkt < 8) return 1;
+  int sp = (int)std::min<long long>(nkt / 4, cdiv(320, tiles));
+  return std::max(sp, 1);
+}
+
+long long split_ws(int M, int N, int K, int batch = 1) {
+  const int sp = pick_split(M, N, K, batch);
+  return sp > 1 ? (long long)sp * M * N * batch : 0;
+}
+
+// y = (x [+pos on the first pos_cols columns]) . w^T (+b) (+relu);  w (N,K) with row stride ldw
+int linear_fwd(const float* x, long long ldx, int M, int K, const float* w, const float* b, float* y, long long ldy,
+               int N, int relu, hipStream_t s, long long ldw = -1, const float* pos = nullptr,
+               long long ldpos = 0, int pos_cols = 0) {
+  fx_gemm_desc d = gemm_desc(M, N, K, op_rows(x, ldx), op_rows(w, ldw < 0 ? K : ldw), y, ldy);
+  d.a.pos = pos;
+  d.a.ld_pos = ldpos;
+  d.a.pos_cols = pos ? pos_cols : 0;
+  d.bias = b;
+  d.relu = relu;
+  return launch_gemm(d, s);
+}
+
+// dx (+)= dy . w  [* (gate > 0)];  w (N,K)
+int linear_dx(const float* dy, long long lddy, const float* w, int M, int K, int N, float* dx, long long lddx,
+              int accumulate, const float* gate, long long ld_gate, float* ws, hipStream_t s, long long ldw = -1) {
+  fx_gemm_desc d = gemm_desc(M, K, N, op_rows(dy, lddy), op_cols(w, ldw < 0 ? K : ldw), dx, lddx);
+  d.beta = accumulate ? 1.f : 0.f;
+  d.gate = gate;
+  d.ld_gate = ld_gate;
+  d.split_k = pick_split(M, K, N);
+  d.workspace = ws;
+  return launch_gemm(d, s);
+}
+
+// dw (+)= dy^T . x ; dy (M,N), x (M,K) -> dw (N,K) with row stride lddw
+int linear_dw(const float* dy, long long lddy, const float* x, long long ldx, int M, int K, int N, float* dw,
+              int accumulate, float* ws, hipStream_t s, long long lddw = -1) {
+  fx_gemm_desc d = gemm_desc(N, K, M, op_cols(dy, lddy), op_cols(x, ldx), dw, lddw < 0 ? K : lddw);
+  d.beta = accumulate ? 1.f : 0.f;
+  d.split_k = pick_split(N, K, M);
+  d.workspace = ws;
+  return launch_gemm(d, s);
+}
+
+// ---- MS-TCN layout of saved activations / workspace --------------------------------
+struct MstcnLayout {
+  long long rowsF;
+  // saved
+  long long h, z, xh, rs, total_saved;
+  // workspace
+  long long wf, wb, buf0, buf1, buf2, split, colsum, total_ws;
+};
+
+MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
+  MstcnLayout L{};
+  const long long F = p->F;
+  const int NL = p->num_layers;
+  L.rowsF = (long long)rows * F;
+  L.h = 0;                                   // h_0 .. h_NL
+  L.z = L.h + (NL + 1) * L.rowsF;            // z_0 .. z_{NL-1}
+  L.xh = L.z + NL * L.rowsF;                 // LN xhat_i
+  L.rs = L.xh + (p->layernorm ? NL * L.rowsF : 0);
+  L.total_saved = L.rs + (p->layernorm ? (long long)NL * rows : 0);
+  const long long wsz = 3 * F * F;
+  L.wf = 0;
+  L.wb = L.wf + NL * wsz;
+  L.buf0 = L.wb + NL * wsz;
+  L.buf1 = L.buf0 + L.rowsF;
+  L.buf2 = L.buf1 + L.rowsF;
+  L.split = L.buf2 + L.rowsF;
+  long long sp = 0;
+  sp = std::max(sp, split_ws(p->F, 3 * p->F, rows));          // conv dW
+  sp = std::max(sp, split_ws(p->F, p->F, rows));              // pointwise dW
+  sp = std::max(sp, split_ws(p->cout, p->F, rows));           // out dW
+  if (p->in_map) sp = std::max(sp, split_ws(p->F, p->cin, rows));  // in dW
+  sp = std::max(sp, split_ws(rows, p->F, p->cout));           // dH_L
+  if (p->in_map) sp = std::max(sp, split_ws(rows, p->cin, p->F));
+  sp = std::max(sp, layernorm_bwd_ws_floats(rows, p->F));
+  L.colsum = L.split + sp;
+  long long cs = colsum_workspace_floats(rows, std::max(std::max(p->F, p->cout), p->cin));
+  L.total_ws = L.colsum + cs;
+  return L;
+}
+
+int pack_conv_weights(const fx_mstcn_params* p, float* ws, const MstcnLayout& L, hipStream_t s) {
+  PackArgs a{};
+  a.F = p->F;
+  const long long wsz = 3LL * p->F * p->F;
+  for (int l = 0; l < p->num_layers; ++l) {
+    a.w[l] = p->w_dil[l];
+    a.wf[l] = ws + L.wf + l * wsz;
+    a.wb[l] = ws + L.wb + l * wsz;
+  }
+  hipLaunchKernelGGL(pack_conv_kernel, dim3(std::min<int>(cdiv(wsz, 256), 512), p->num_layers), dim3(256), 0, s, a);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+int layer_dilation(const fx_mstcn_params* p, int i) {
+  long long d = p->dil0 > 0 ? p->dil0 : 1;
+  const int f = p->dil_factor > 0 ? p->dil_factor : 2;
+  for (int k = 0; k < i; ++k) d *= f;
+  return (int)d;
+}
+
+fx_operand conv_operand(const float* h, long long ld, int cin, int dil, int dir, int T, bool trans) {
+  fx_operand o = trans ? op_cols(h, ld) : op_rows(h, ld);
+  o.conv_taps = 3;
+  o.conv_cin = cin;
+  o.conv_dil = dil;
+  o.conv_dir = dir;
+  o.seq_len = T;
+  return o;
+}
+
+}  // namespace
+}  // namespace fx
+
+using namespace fx;
+
+extern "C" {
+
+int fx_version(void) { return FX_ABI_VERSION; }
+const char* fx_last_error(void) { return g_last_error.c_str(); }
+
+int fx_gemm(const fx_gemm_desc* desc, void* stream) {
+  FX_REQUIRE(desc, "fx_gemm: null descriptor");
+  return launch_gemm(*desc, (hipStream_t)stream);
+}
+
+long long fx_gemm_workspace_floats(const fx_gemm_desc* desc) { return desc ? gemm_workspace_floats(*desc) : 0; }
+
+// ---------------------------------------------------------------- Linear
+int fx_linear_fwd(const float* x, long long ldx, const float* pos, long long ldpos, int pos_cols, int M, int K,
+                  const float* w, long long ldw, const float* b, float* y, long long ldy, int N, int relu,
+                  void* stream) {
+  return linear_fwd(x, ldx, M, K, w, b, y, ldy, N, relu, (hipStream_t)stream, ldw, pos, ldpos, pos_cols);
+}
+
+long long fx_linear_bwd_workspace_floats(int M, int K, int N) {
+  return (long long)M * N + split_ws(M, K, N) + split_ws(N, K, M) + colsum_workspace_floats(M, N);
+}
+
+int fx_linear_bwd(const float* dy, long long lddy, const float* x, long long ldx, const float* w, long long ldw,
+                  const float* relu_out, long long ld_relu, int M, int K, int N, float* dx, long long lddx,
+                  float* dw, long long lddw, float* db, int accumulate, float* workspace, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  FX_REQUIRE(workspace || (!relu_out && split_ws(M, K, N) == 0 && split_ws(N, K, M) == 0 && !db),
+             "fx_linear_bwd: workspace required");
+  float* wz = workspace;
+  float* wsx = wz + (long long)M * N;
+  float* wsw = wsx + split_ws(M, K, N);
+  float* wsc = wsw + split_ws(N, K, M);
+  const float* g = dy;
+  long long ldg = lddy;
+  if (relu_out) {
+    FX_TRY(relu_bwd(dy, lddy, relu_out, ld_relu, M, N, wz, N, s));
+    g = wz;
+    ldg = N;
+  }
+  if (dx) FX_TRY(linear_dx(g, ldg, w, M, K, N, dx, lddx, accumulate, nullptr, 0, wsx, s, ldw));
+  if (dw) FX_TRY(linear_dw(g, ldg, x, ldx, M, K, N, dw, accumulate, wsw, s, lddw));
+  if (db) FX_TRY(launch_colsum(g, ldg, M, N, db, accumulate, wsc, s));
+  return FX_OK;
+}
+
+// ---------------------------------------------------------------- MS-TCN
+long long fx_mstcn_saved_floats(const fx_mstcn_params* p, int rows) { return mstcn_layout(p, rows).total_saved; }
+long long fx_mstcn_workspace_floats(const fx_mstcn_params* p, int rows) { return mstcn_layout(p, rows).total_ws; }
+
+int fx_mstcn_fwd(const fx_mstcn_params* p, const float* x, long long ldx, int T, int nvid, float* y, long long ldy,
+                 float* saved, float* workspace, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  FX_REQUIRE(p && p->num_layers >= 0 && p->num_layers <= 32, "mstcn: 0..32 layers");
+  FX_REQUIRE(p->in_map || p->cin == p->F, "mstcn: in_map=0 needs cin == F");
+  const int rows = T * nvid;
+  const int F = p->F;
+  const MstcnLayout L = mstcn_layout(p, rows);
+  FX_TRY(pack_conv_weights(p, workspace, L, s));
+  float* h0 = saved + L.h;
+  if (p->in_map) {
+    FX_TRY(linear_fwd(x, ldx, rows, p->cin, p->w_in, p->b_in, h0, F, F, 0, s));
+  } else {
+    FX_CHECK_HIP(hipMemcpy2DAsync(h0, F * sizeof(float), x, ldx * sizeof(float), F * sizeof(float), rows,
+                                  hipMemcpyDeviceToDevice, s));
+  }
+  for (int i = 0; i < p->num_layers; ++i) {
+    const float* hi = saved + L.h + i * L.rowsF;
+    float* hn = saved + L.h + (i + 1) * L.rowsF;
+    float* zi = saved + L.z + i * L.rowsF;
+    // z = relu(dilated_conv(h) + b)      (basic.py:158)
+    fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(hi, F, F, layer_dilation(p, i), 1, T, false),
+                               op_rows(workspace + L.wf + (long long)i * 3 * F * F, 3 * F), zi, F);
+    d.bias = p->b_dil[i];
+    d.relu = 1;
+    prof_begin(0, s);
+    FX_TRY(launch_gemm(d, s));
+    prof_end(0, s, 2.0 * rows * F * 3.0 * F, 4.0 * (2.0 * rows * F + 3.0 * F * F));
+    // h' = h + z . Wpw^T + b   [then LN]   (basic.py:159-169)
+    float* u = p->layernorm ? workspace + L.buf0 : hn;
+    fx_gemm_desc e = gemm_desc(rows, F, F, op_rows(zi, F), op_rows(p->w_pw[i], F), u, F);
+    e.bias = p->b_pw[i];
+    e.resid = hi;
+    e.ld_resid = F;
+    FX_TRY(launch_gemm(e, s));
+    if (p->layernorm)
+      FX_TRY(launch_layernorm_fwd(u, F, nullptr, 0, p->ln_w[i], p->ln_b[i], 1e-5f, rows, F, 0, hn, F, nullptr,
+                                  saved + L.rs + (long long)i * rows, saved + L.xh + i * L.rowsF, F, s));
+  }
+  const float* hL = saved + L.h + p->num_layers * L.rowsF;
+  return linear_fwd(hL, F, rows, F, p->w_out, p->b_out, y, ldy, p->cout, 0, s);
+}
+
+int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float* x, long long ldx, int T, int nvid,
+                 const float* dy, long long lddy, float* dx, long long lddx, const float* saved, float* workspace,
+                 void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int rows = T * nvid;
+  const int F = p->F;
+  const MstcnLayout L = mstcn_layout(p, rows);
+  float* ws = workspace;
+  FX_TRY(pack_conv_weights(p, ws, L, s));
+  float* spl = ws + L.split;
+  float* csw = ws + L.colsum;
+  float* dH = ws + L.buf0;   // gradient w.r.t. the current layer output
+  float* dU = ws + L.buf1;   // gradient at the residual sum (pre-LN)
+  float* dZ = ws + L.buf2;   // gradient at the conv output (pre-ReLU)
+  // output map
+  const float* hL = saved + L.h + p->num_layers * L.rowsF;
+  FX_TRY(linear_dw(dy, lddy, hL, F, rows, F, p->cout, g->w_out, 0, spl, s));
+  FX_TRY(launch_colsum(dy, lddy, rows, p->cout, g->b_out, 0, csw, s));
+  FX_TRY(linear_dx(dy, lddy, p->w_out, rows, F, p->cout, dH, F, 0, nullptr, 0, spl, s));
+  for (int i = p->num_layers - 1; i >= 0; --i) {
+    const float* hi = saved + L.h + i * L.rowsF;
+    const float* zi = saved + L.z + i * L.rowsF;
+    const float* gU = dH;
+    if (p->layernorm) {
+      FX_TRY(launch_layernorm_bwd(dH, F, nullptr, 0, saved + L.xh + i * L.rowsF, F, p->ln_w[i],
+                                  saved + L.rs + (long long)i * rows, rows, F, 0, dU, F, g->ln_w[i], g->ln_b[i],
+                                  spl, s));
+      gU = dU;
+    }
+    // pointwise: dW_pw = dU^T z, db_pw = colsum(dU), dZ = (dU . W_pw) * (z > 0)
+    FX_TRY(linear_dw(gU, F, zi, F, rows, F, F, g->w_pw[i], 0, spl, s));
+    FX_TRY(launch_colsum(gU, F, rows, F, g->b_pw[i], 0, csw, s));
+    FX_TRY(linear_dx(gU, F, p->w_pw[i], rows, F, F, dZ, F, 0, zi, F, spl, s));
+    // conv: dW (tap-major columns stored straight into (F,F,3)), db, dH_i = dU + conv^T(dZ)
+    {
+      fx_gemm_desc d = gemm_desc(F, 3 * F, rows, op_cols(dZ, F), conv_operand(hi, F, F, layer_dilation(p, i), 1, T, true),
+                                 g->w_dil[i], 3 * F);
+      d.c_tap_cin = F;
+      d.split_k = pick_split(F, 3 * F, rows);
+      d.workspace = spl;
+      FX_TRY(launch_gemm(d, s));
+    }
+    FX_TRY(launch_colsum(dZ, F, rows, F, g->b_dil[i], 0, csw, s));
+    {
+      float* dHn = (gU == dH) ? dU : dH;  // write into the buffer not holding gU
+      fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dZ, F, F, layer_dilation(p, i), -1, T, false),
+                                 op_rows(ws + L.wb + (long long)i * 3 * F * F, 3 * F), dHn, F);
+      d.resid = gU;
+      d.ld_resid = F;
+      FX_TRY(launch_gemm(d, s));
+      if (dHn != dH) std::swap(dH, dU);  // dH now holds dH_i
+    }
+  }
+  if (p->in_map) {
+    if (g->w_in) FX_TRY(linear_dw(dH, F, x, ldx, rows, p->cin, F, g->w_in, 0, spl, s));
+    if (g->b_in) FX_TRY(launch_colsum(dH, F, rows, F, g->b_in, 0, csw, s));
+    if (dx) FX_TRY(linear_dx(dH, F, p->w_in, rows, p->cin, F, dx, lddx, 0, nullptr, 0, spl, s));
+  } else if (dx) {
+    FX_CHECK_HIP(hipMemcpy2DAsync(dx, lddx * sizeof(float), dH, F * sizeof(float), F * sizeof(float), rows,
+                                  hipMemcpyDeviceToDevice, s));
+  }
+  return FX_OK;
+}
+
+// ---------------------------------------------------------------- row ops
+int fx_layernorm_fwd(const float* x, long long ldx, const float* r, long long ldr, const float* w, const float* b,
+                     float eps, int rows, int cols, int relu, float* y, long long ldy, float* xhat, long long ldxh,
+                     float* rstd, void* stream) {
+  return launch_layernorm_fwd(x, ldx, r, ldr, w, b, eps, rows, cols, relu, y, ldy, nullptr, rstd, xhat, ldxh,
+                              (hipStream_t)stream);
+}
+
+long long fx_layernorm_bwd_workspace_floats(int rows, int cols) { return layernorm_bwd_ws_floats(rows, cols); }
+
+int fx_layernorm_bwd(const float* dy, long long lddy, const float* y, long long ldy, const float* xhat,
+                     long long ldxh, const float* w, const float* rstd, int rows, int cols, int relu, float* dx,
+                     long long lddx, float* dw, float* db, float* workspace, void* stream) {
+  return launch_layernorm_bwd(dy, lddy, y, ldy, xhat, ldxh, w, rstd, rows, cols, relu, dx, lddx, dw, db, workspace,
+                              (hipStream_t)stream);
+}
+
+int fx_softmax_rows(const float* logits, long long ldl, int rows, int cols, float scale, float* probs,
+                    long long ldp, void* stream) {
+  return launch_softmax_rows(logits, ldl, rows, cols, scale, probs, ldp, (hipStream_t)stream);
+}
+
+int fx_softmax_rows_bwd(const float* probs, long long ldp, const float* dprobs, long long lddp,
+                        const float* dlogit_extra, long long lde, int rows, int cols, float scale, float* dlogit,
+                        long long ldd, void* stream) {
+  return launch_softmax_rows_bwd(probs, ldp, dprobs, lddp, dlogit_extra, lde, rows, cols, scale, dlogit, ldd,
+                                 (hipStream_t)stream);
+}
+
+int fx_process_feature_fwd(const float* x, long long ldx, int rows, int cols, int n, float* out, long long ldo,
+                           void* stream) {
+  return launch_pf_fwd(x, ldx, rows, cols, n, out, ldo, (hipStream_t)stream);
+}
+
+int fx_process_feature_bwd(const float* out, long long ldo, const float* dout, long long lddo, const float* dclogit,
+                           long long lddc, int rows, int cols, int n, float* dx, long long lddx, void* stream) {
+  return launch_pf_bwd(out, ldo, dout, lddo, dclogit, lddc, rows, cols, n, dx, lddx, (hipStream_t)stream);
+}
+
+int fx_l2norm_fwd(const float* x, long long ldx, int rows, int cols, float* y, long long ldy, float* norm,
+                  void* stream) {
+  return launch_l2n_fwd(x, ldx, rows, cols, y, ldy, norm, (hipStream_t)stream);
+}
+
+int fx_l2norm_bwd(const float* y, long long ldy, const float* norm, const float* dy, long long lddy, int rows,
+                  int cols, float* dx, long long lddx, void* stream) {
+  return launch_l2n_bwd(y, ldy, norm, dy, lddy, rows, cols, dx, lddx, (hipStream_t)stream);
+}
+
+int fx_relu_bwd(const float* dy, long long lddy, const float* y, long long ldy, int rows, int cols, float* dz,
+                long long lddz, void* stream) {
+  return relu_bwd(dy, lddy, y, ldy, rows, cols, dz, lddz, (hipStream_t)stream);
+}
+
+int fx_add(const float* a, long long lda, const float* b, long long ldb, int rows, int cols, float* out,
+           long long ldo, int accumulate, void* stream) {
+  return add2(a, lda, b, ldb, rows, cols, out, ldo, accumulate, (hipStream_t)stream);
+}
+
+// ---------------------------------------------------------------- MHA core
+long long fx_mha_core_workspace_floats(int Lq, int Lk, int E, int nhead) {
+  const int hd = E / std::max(nhead, 1);
+  long long ws = (long long)nhead * Lq * Lk;  // dS
+  long long sp = 0;
+  sp = std::max(sp, split_ws(Lq, hd, Lk, nhead));
+  sp = std::max(sp, split_ws(Lk, hd, Lq, nhead));
+  sp = std::max(sp, split_ws(Lq, Lk, hd, nhead));
+  return ws + 2 * sp;
+}
+
+int fx_mha_core_fwd(const float* q, long long ldq, const float* k, long long ldk, const float* v, long long ldv,
+                    int Lq, int Lk, int E, int nhead, float* probs, float* o, long long ldo, float* workspace,
+                    void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  FX_REQUIRE(nhead > 0 && E % nhead == 0, "mha: E must be divisible by nhead");
+  const int hd = E / nhead;
+  const float scale = 1.0f / std::sqrt((float)hd);
+  // S_h = (Q_h K_h^T) * scale  -> probs buffer, then row softmax in place
+  fx_gemm_desc d = gemm_desc(Lq, Lk, hd, op_rows(q, ldq), op_rows(k, ldk), probs, Lk);
+  d.batch = nhead;
+  d.a.batch_stride = hd;
+  d.b.batch_stride = hd;
+  d.c_batch_stride = (long long)Lq * Lk;
+  d.alpha = scale;
+  FX_TRY(launch_gemm(d, s));
+  FX_TRY(launch_softmax_rows(probs, Lk, nhead * Lq, Lk, 1.f, probs, Lk, s));
+  // O_h = P_h V_h
+  fx_gemm_desc e = gemm_desc(Lq, hd, Lk, op_rows(probs, Lk), op_cols(v, ldv), o, ldo);
+  e.batch = nhead;
+  e.a.batch_stride = (long long)Lq * Lk;
+  e.b.batch_stride = hd;
+  e.c_batch_stride = hd;
+  e.split_k = workspace ? pick_split(Lq, hd, Lk, nhead) : 1;
+  e.workspace = workspace;
+  return launch_gemm(e, s);
+}
+
+int fx_mha_core_bwd(const float* q, long long ldq, const float* k, long long ldk, const float* v, long long ldv,
+                    const float* probs, const float* dout, long long lddo, int Lq, int Lk, int E, int nhead,
+                    float* dq, long long lddq, float* dk, long long lddk, float* dv, long long lddv,
+                    float* workspace, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  FX_REQUIRE(nhead > 0 && E % nhead == 0, "mha: E must be divisible by nhead");
+  const int hd = E / nhead;
+  const float scale = 1.0f / std::sqrt((float)hd);
+  float* dS = workspace;
+  float* spl = workspace + (long long)nhead * Lq * Lk;
+  // dP_h = dO_h V_h^T
+  fx_gemm_desc d = gemm_desc(Lq, Lk, hd, op_rows(dout, lddo), op_rows(v, ldv), dS, Lk);
+  d.batch = nhead;
+  d.a.batch_stride = hd;
+  d.b.batch_stride = hd;
+  d.c_batch_stride = (long long)Lq * Lk;
+  FX_TRY(launch_gemm(d, s));
+  // dS = softmax_bwd(P, dP)
+  FX_TRY(launch_softmax_rows_bwd(probs, Lk, dS, Lk, nullptr, 0, nhead * Lq, Lk, 1.f, dS, Lk, s));
+  // dQ_h = scale * dS_h K_h
+  if (dq) {
+    fx_gemm_desc e = gemm_desc(Lq, hd, Lk, op_rows(dS, Lk), op_cols(k, ldk), dq, lddq);
+    e.batch = nhead;
+    e.a.batch_stride = (long long)Lq * Lk;
+    e.b.batch_stride = hd;
+    e.c_batch_stride = hd;
+    e.alpha = scale;
+    e.split_k = pick_split(Lq, hd, Lk, nhead);
+    e.workspace = spl;
+    FX_TRY(launch_gemm(e, s));
+  }
+  // dK_h = scale * dS_h^T Q_h
+  if (dk) {
+    fx_gemm_desc e = gemm_desc(Lk, hd, Lq, op_cols(dS, Lk), op_cols(q, ldq), dk, lddk);
+    e.batch = nhead;
+    e.a.batch_stride = (long long)Lq * Lk;
+    e.b.batch_stride = hd;
+    e.c_batch_stride = hd;
+    e.alpha = scale;
+    e.split_k = pick_split(Lk, hd, Lq, nhead);
+    e.workspace = spl;
+    FX_TRY(launch_gemm(e, s));
+  }
+  // dV_h = P_h^T dO_h
+  if (dv) {
+    fx_gemm_desc e = gemm_desc(Lk, hd, Lq, op_cols(probs, Lk), op_cols(dout, lddo), dv, lddv);
+    e.batch = nhead;
+    e.a.batch_stride = (long long)Lq * Lk;
+    e.b.batch_stride = hd;
+    e.c_batch_stride = hd;
+    e.split_k = pick_split(Lk, hd, Lq, nhead);
+    e.workspace = spl;
+    FX_TRY(launch_gemm(e, s));
+  }
+  return FX_OK;
+}
+
+// ---------------------------------------------------------------- X2Y_map
+// Single-head cross attention of basic.py:349-389 (kq_pos=True).
+// saved: xin (Nx*xdim, X+Xpos when Xpos), yin (Ny*ydim), xk, xv (Nx*Hd), yq, feat (Ny*Hd)
+namespace {
+struct X2YLayout {
+  long long xin, yin, xk, xv, yq, feat, total;
+};
+X2YLayout x2y_layout(int Nx, int xdim, int Ny, int ydim, int Hd) {
+  X2YLayout L{};
+  L.xin = 0;
+  L.yin = L.xin + (long long)Nx * xdim;
+  L.xk = L.yin + (long long)Ny * ydim;
+  L.xv = L.xk + (long long)Nx * Hd;
+  L.yq = L.xv + (long long)Nx * Hd;
+  L.feat = L.yq + (long long)Ny * Hd;
+  L.total = L.feat + (long long)Ny * Hd;
+  return L;
+}
+long long x2y_split_ws(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim) {
+  long long sp = 0;
+  sp = std::max(sp, split_ws(Ny, Nx, Hd));             // logits
+  sp = std::max(sp, split_ws(Ny, Hd, Nx));             // feat, dyq
+  sp = std::max(sp, split_ws(Nx, Hd, Ny));             // dxv, dxk
+  sp = std::max(sp, split_ws(Ny, ydim + Hd, outdim));  // dcat
+  sp = std::max(sp, split_ws(outdim, ydim, Ny));       // dW_y pieces
+  sp = std::max(sp, split_ws(outdim, Hd, Ny));
+  sp = std::max(sp, split_ws(Hd, xdim, Nx));           // dW_k / dW_v
+  sp = std::max(sp, split_ws(Hd, ydim, Ny));           // dW_q
+  sp = std::max(sp, split_ws(Nx, xdim, Hd));           // dX
+  sp = std::max(sp, split_ws(Ny, ydim, Hd));           // dY
+  return sp;
+}
+}  // namespace
+
+long long fx_x2y_saved_floats(int Nx, int xdim, int Ny, int ydim, int Hd) {
+  return x2y_layout(Nx, xdim, Ny, ydim, Hd).total;
+}
+
+long long fx_x2y_workspace_floats(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim) {
+  long long w = (long long)Ny * (ydim + Hd) + (long long)Ny * Nx + 2LL * Nx * Hd + (long long)Ny * Hd +
+                (long long)Nx * xdim + (long long)Ny * ydim;
+  return w + x2y_split_ws(Nx, xdim, Ny, ydim, Hd, outdim) +
+         colsum_workspace_floats(std::max(Nx, Ny), std::max(Hd, outdim));
+}
+
+int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpos, long long ldxp, int xpos_cols,
+               const float* Y, long long ldy, int Ny, int ydim, const float* Ypos, long long ldyp, int ypos_cols,
+               const float* wk, const float* bk, const float* wv, const float* bv, const float* wq, const float* bq,
+               const float* wy, const float* by, int Hd, int outdim, float* out, long long ldo, float* logit,
+               float* attn, float* saved, float* workspace, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const X2YLayout L = x2y_layout(Nx, xdim, Ny, ydim, Hd);
+  float* xk = saved + L.xk;
+  float* xv = saved + L.xv;
+  float* yq = saved + L.yq;
+  float* feat = saved + L.feat;
+  // keep X+Xpos / Y+Ypos for the weight gradients (basic.py:357-369)
+  const float* xin = X;
+  long long ldxin = ldx;
+  if (Xpos) {
+    FX_CHECK_HIP(hipMemcpy2DAsync(saved + L.xin, xdim * sizeof(float), X, ldx * sizeof(float), xdim * sizeof(float), Nx,
+                                  hipMemcpyDeviceToDevice, s));
+    FX_TRY(add2(Xpos, ldxp, nullptr, 0, Nx, xpos_cols, saved + L.xin, xdim, 1, s));
+    xin = saved + L.xin;
+    ldxin = xdim;
+  }
+  const float* yin = Y;
+  long long ldyin = ldy;
+  if (Ypos) {
+    FX_CHECK_HIP(hipMemcpy2DAsync(saved + L.yin, ydim * sizeof(float), Y, ldy * sizeof(float), ydim * sizeof(float), Ny,
+                                  hipMemcpyDeviceToDevice, s));
+    FX_TRY(add2(Ypos, ldyp, nullptr, 0, Ny, ypos_cols, saved + L.yin, ydim, 1, s));
+    yin = saved + L.yin;
+    ldyin = ydim;
+  }
+  FX_TRY(linear_fwd(xin, ldxin, Nx, xdim, wk, bk, xk, Hd, Hd, 0, s));
+  FX_TRY(linear_fwd(X, ldx, Nx, xdim, wv, bv, xv, Hd, Hd, 0, s));
+  FX_TRY(linear_fwd(yin, ldyin, Ny, ydim, wq, bq, yq, Hd, Hd, 0, s));
+  const float scale = 1.0f / std::sqrt((float)Hd);
+  {
+    fx_gemm_desc d = gemm_desc(Ny, Nx, Hd, op_rows(yq, Hd), op_rows(xk, Hd), logit, Nx);
+    d.alpha = scale;
+    d.split_k = pick_split(Ny, Nx, Hd);
+    d.workspace = workspace;
+    FX_TRY(launch_gemm(d, s));
+  }
+  FX_TRY(launch_softmax_rows(logit, Nx, Ny, Nx, 1.f, attn, Nx, s));
+  {
+    fx_gemm_desc d = gemm_desc(Ny, Hd, Nx, op_rows(attn, Nx), op_cols(xv, Hd), feat, Hd);
+    d.split_k = pick_split(Ny, Hd, Nx);
+    d.workspace = workspace;
+    FX_TRY(launch_gemm(d, s));
+  }
+  // Y_W(cat[Y, feat]) with the concatenation folded into the A-operand loader
+  fx_operand a = op_rows(Y, ldy);
+  a.ptr1 = feat;
+  a.ld1 = Hd;
+  a.k_split = ydim;
+  fx_gemm_desc d = gemm_desc(Ny, outdim, ydim + Hd, a, op_rows(wy, ydim + Hd), out, ldo);
+  d.bias = by;
+  return launch_gemm(d, s);
+}
+
+int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, const float* Y, long long ldy, int Ny,
+               int ydim, int ypos_cols, const float* wk, const float* wv, const float* wq, const float* wy, int Hd,
+               int outdim, const float* attn, const float* saved, const float* dout, long long lddo,
+               const float* dlogit, const float* dattn, float* dX, float* dXpos, float* dY, float* dYpos, float* dwk,
+               float* dbk, float* dwv, float* dbv, float* dwq, float* dbq, float* dwy, float* dby, int has_xpos,
+               int has_ypos, float* workspace, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const X2YLayout L = x2y_layout(Nx, xdim, Ny, ydim, Hd);
+  const float* xk = saved + L.xk;
+  const float* xv = saved + L.xv;
+  const float* yq = saved + L.yq;
+  const float* feat = saved + L.feat;
+  const float* xin = has_xpos ? saved + L.xin : X;
+  const long long ldxin = has_xpos ? xdim : ldx;
+  const float* yin = has_ypos ? saved + L.yin : Y;
+  const long long ldyin = has_ypos ? ydim : ldy;
+  const int cw = ydim + Hd;
+  float* dcat = workspace;
+  float* dL = dcat + (long long)Ny * cw;
+  float* dxv = dL + (long long)Ny * Nx;
+  float* dxk = dxv + (long long)Nx * Hd;
+  float* dyq = dxk + (long long)Nx * Hd;
+  float* dXk = dyq + (long long)Ny * Hd;
+  float* dYq = dXk + (long long)Nx * xdim;
+  float* spl = dYq + (long long)Ny * ydim;
+  float* csw = spl + x2y_split_ws(Nx, xdim, Ny, ydim, Hd, outdim);
+  const float scale = 1.0f / std::sqrt((float)Hd);
+  // Y_W: dcat = dout . Wy, dWy = dout^T [Y, feat], dby
+  FX_TRY(linear_dx(dout, lddo, wy, Ny, cw, outdim, dcat, cw, 0, nullptr, 0, spl, s));
+  FX_TRY(linear_dw(dout, lddo, Y, ldy, Ny, ydim, outdim, dwy, 0, spl, s, cw));
+  FX_TRY(linear_dw(dout, lddo, feat, Hd, Ny, Hd, outdim, dwy + ydim, 0, spl, s, cw));
+  FX_TRY(launch_colsum(dout, lddo, Ny, outdim, dby, 0, csw, s));
+  const float* dfeat = dcat + ydim;
+  // dP = dfeat . xv^T (+ dattn) ; dxv = attn^T . dfeat
+  {
+    fx_gemm_desc d = gemm_desc(Ny, Nx, Hd, op_rows(dfeat, cw), op_rows(xv, Hd), dL, Nx);
+    d.resid = dattn;
+    d.ld_resid = Nx;
+    d.split_k = pick_split(Ny, Nx, Hd);
+    d.workspace = spl;
+    FX_TRY(launch_gemm(d, s));
+  }
+  {
+    fx_gemm_desc d = gemm_desc(Nx, Hd, Ny, op_cols(attn, Nx), op_cols(dfeat, cw), dxv, Hd);
+    d.split_k = pick_split(Nx, Hd, Ny);
+    d.workspace = spl;
+    FX_TRY(launch_gemm(d, s));
+  }
+  // dlogit = softmax_bwd(attn, dP) + dlogit_direct   (in place)
+  FX_TRY(launch_softmax_rows_bwd(attn, Nx, dL, Nx, dlogit, Nx, Ny, Nx, 1.f, dL, Nx, s));
+  {
+    fx_gemm_desc d = gemm_desc(Ny, Hd, Nx, op_rows(dL, Nx), op_cols(xk, Hd), dyq, Hd);
+    d.alpha = scale;
+    d.split_k = pick_split(Ny, Hd, Nx);
+    d.workspace = spl;
+    FX_TRY(launch_gemm(d, s));
+  }
+  {
+    fx_gemm_desc d = gemm_desc(Nx, Hd, Ny, op_cols(dL, Nx), op_cols(yq, Hd), dxk, Hd);
+    d.alpha = scale;
+    d.split_k = pick_split(Nx, Hd, Ny);
+    d.workspace = spl;
+    FX_TRY(launch_gemm(d, s));
+  }
+  // projections
+  FX_TRY(linear_dw(dxk, Hd, xin, ldxin, Nx, xdim, Hd, dwk, 0, spl, s));
+  FX_TRY(launch_colsum(dxk, Hd, Nx, Hd, dbk, 0, csw, s));
+  FX_TRY(linear_dw(dxv, Hd, X, ldx, Nx, xdim, Hd, dwv, 0, spl, s));
+  FX_TRY(launch_colsum(dxv, Hd, Nx, Hd, dbv, 0, csw, s));
+  FX_TRY(linear_dw(dyq, Hd, yin, ldyin, Ny, ydim, Hd, dwq, 0, spl, s));
+  FX_TRY(launch_colsum(dyq, Hd, Ny, Hd, dbq, 0, csw, s));
+  if (dX || dXpos) {
+    FX_TRY(linear_dx(dxk, Hd, wk, Nx, xdim, Hd, dXk, xdim, 0, nullptr, 0, spl, s));
+    if (dXpos)
+      FX_CHECK_HIP(hipMemcpy2DAsync(dXpos, xpos_cols * sizeof(float), dXk, xdim * sizeof(float),
+                                    xpos_cols * sizeof(float), Nx, hipMemcpyDeviceToDevice, s));
+    if (dX) {
+      fx_gemm_desc d = gemm_desc(Nx, xdim, Hd, op_rows(dxv, Hd), op_cols(wv, xdim), dX, xdim);
+      d.resid = dXk;
+      d.ld_resid = xdim;
+      d.split_k = pick_split(Nx, xdim, Hd);
+      d.workspace = spl;
+      FX_TRY(launch_gemm(d, s));
+    }
+  }
+  if (dY || dYpos) {
+    FX_TRY(linear_dx(dyq, Hd, wq, Ny, ydim, Hd, dYq, ydim, 0, nullptr, 0, spl, s));
+    if (dYpos)
+      FX_CHECK_HIP(hipMemcpy2DAsync(dYpos, ypos_cols * sizeof(float), dYq, ydim * sizeof(float),
+                                    ypos_cols * sizeof(float), Ny, hipMemcpyDeviceToDevice, s));
+    if (dY) FX_TRY(add2(dYq, ydim, dcat, cw, Ny, ydim, dY, ydim, 0, s));
+  }
+  return FX_OK;
+}
+
+// ---------------------------------------------------------------- segments
+int fx_segments_from_probs(const float* x, long long ldx, int col0, int ncls, int T, int32_t* pred, int32_t* seg_id,
+                           int32_t* seg_start, int32_t* seg_end, int32_t* num_seg, void* stream) {
+  return launch_segments(x, ldx, col0, ncls, T, pred, seg_id, seg_start, seg_end, num_seg, (hipStream_t)stream);
+}
+
+int fx_seg_mean_fwd(const float* x, long long ldx, const int32_t* seg_start, const int32_t* seg_end, int S, int cols,
+                    float* y, long long ldy, void* stream) {
+  return launch_seg_reduce(x, ldx, seg_start, seg_end, S, cols, 1, y, ldy, 0, (hipStream_t)stream);
+}
+
+int fx_seg_mean_bwd(const float* dy, long long lddy, const int32_t* seg_id, const int32_t* seg_start,
+                    const int32_t* seg_end, int T, int cols, float* dx, long long lddx, int accumulate, void* stream) {
+  return launch_seg_mean_bwd(dy, lddy, seg_id, seg_start, seg_end, T, cols, dx, lddx, accumulate, (hipStream_t)stream);
+}
+
+int fx_seg_sum_rows(const float* dx, long long lddx, const int32_t* seg_start, const int32_t* seg_end, int S, int cols,
+                    float* dy, long long lddy, int accumulate, void* stream) {
+  return launch_seg_reduce(dx, lddx, seg_start, seg_end, S, cols, 0, dy, lddy, accumulate, (hipStream_t)stream);
+}
+
+// ---------------------------------------------------------------- profiling
+int fx_prof_enable(int kind, int max_events) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  for (auto& e : g_prof.ev) (void)hipEventDestroy(e);
+  g_prof = ProfState{};
+  g_prof.ev.resize(2 * (size_t)max_events);
+  for (auto& e : g_prof.ev) FX_CHECK_HIP(hipEventCreate(&e));
+  g_prof.flops.assign(max_events, 0.0);
+  g_prof.bytes.assign(max_events, 0.0);
+  g_prof.max_events = max_events;
+  g_prof.kind = kind;
+  return FX_OK;
+}
+
+int fx_prof_collect(int kind, double* total_ms, double* total_flops, double* total_bytes, int* count) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  FX_REQUIRE(g_prof.kind == kind, "prof: kind not enabled");
+  double ms = 0, fl = 0, by = 0;
+  for (int i = 0; i < g_prof.used; ++i) {
+    FX_CHECK_HIP(hipEventSynchronize(g_prof.ev[2 * i + 1]));
+    float t = 0.f;
+    FX_CHECK_HIP(hipEventElapsedTime(&t, g_prof.ev[2 * i], g_prof.ev[2 * i + 1]));
+    ms += t;
+    fl += g_prof.flops[i];
+    by += g_prof.bytes[i];
+  }
+  *total_ms = ms;
+  *total_flops = fl;
+  *total_bytes = by;
+  *count = g_prof.used;
+  return FX_OK;
+}
+
+void fx_prof_disable(void) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  for (auto& e : g_prof.ev) (void)hipEventDestroy(e);
+  g_prof = ProfState{};
+}
+
+}  // extern "C"

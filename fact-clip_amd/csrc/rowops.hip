@@ -1,0 +1,429 @@
+// Row-wise kernels: LayerNorm (+residual, +ReLU), softmax, process_feature,
+// L2 normalisation, and their backwards.  One wave64 per row for rows up to
+// 1024 channels (values held in registers, 16 per lane max); a 256-thread
+// workgroup per row (global re-reads, L2 resident) for longer rows such as
+// attention over T frames.  All reductions are wave shuffles + LDS.
+#include <algorithm>
+
+#include "fx_common.h"
+
+namespace fx {
+namespace {
+
+constexpr int MAXPL = 16;  // values per lane in the wave-per-row path (cols <= 1024)
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------- LayerNorm
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const float* x, long long ldx, const float* r,
+                                                     long long ldr, const float* w, const float* b,
+                                                     float eps, int rows, int cols, int relu, float* y,
+                                                     long long ldy, float* mean_out, float* rstd_out,
+                                                     float* xhat, long long ldxh) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float v[MAXPL];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXPL; ++i) {
+    const int c = i * 64 + lane;
+    v[i] = 0.f;
+    if (c < cols) {
+      v[i] = x[(long long)row * ldx + c] + (r ? r[(long long)row * ldr + c] : 0.f);
+      s += v[i];
+    }
+  }
+  const float mu = wave_sum(s) / cols;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXPL; ++i) {
+    const int c = i * 64 + lane;
+    if (c < cols) {
+      const float d = v[i] - mu;
+      q += d * d;
+    }
+  }
+  const float rs = rsqrtf(wave_sum(q) / cols + eps);
+#pragma unroll
+  for (int i = 0; i < MAXPL; ++i) {
+    const int c = i * 64 + lane;
+    if (c < cols) {
+      const float h = (v[i] - mu) * rs;
+      if (xhat) xhat[(long long)row * ldxh + c] = h;
+      float o = h * w[c] + b[c];
+      if (relu) o = fmaxf(o, 0.f);
+      y[(long long)row * ldy + c] = o;
+    }
+  }
+  if (lane == 0) {
+    if (mean_out) mean_out[row] = mu;
+    if (rstd_out) rstd_out[row] = rs;
+  }
+}
+
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy_eff * w
+// per-block partial dw/db sums over the block's rows -> ws[blk][2*cols]
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const float* dy, long long lddy, const float* y,
+                                                     long long ldy, const float* xhat, long long ldxh,
+                                                     const float* w, const float* rstd, int rows,
+                                                     int cols, int relu, float* dx, long long lddx,
+                                                     float* ws) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float pw[MAXPL], pb[MAXPL];
+#pragma unroll
+  for (int i = 0; i < MAXPL; ++i) pw[i] = pb[i] = 0.f;
+  for (int row = blockIdx.x * 4 + wv; row < rows; row += gridDim.x * 4) {
+    float g[MAXPL], h[MAXPL];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXPL; ++i) {
+      const int c = i * 64 + lane;
+      g[i] = h[i] = 0.f;
+      if (c < cols) {
+        float d = dy[(long long)row * lddy + c];
+        if (relu && !(y[(long long)row * ldy + c] > 0.f)) d = 0.f;
+        h[i] = xhat[(long long)row * ldxh + c];
+        pw[i] += d * h[i];
+        pb[i] += d;
+        g[i] = d * w[c];
+        s1 += g[i];
+        s2 += g[i] * h[i];
+      }
+    }
+    s1 = wave_sum(s1) / cols;
+    s2 = wave_sum(s2) / cols;
+    const float rs = rstd[row];
+#pragma unroll
+    for (int i = 0; i < MAXPL; ++i) {
+      const int c = i * 64 + lane;
+      if (c < cols) dx[(long long)row * lddx + c] = rs * (g[i] - s1 - h[i] * s2);
+    }
+  }
+  if (!ws) return;
+  __shared__ float red[4][2][64];
+#pragma unroll
+  for (int i = 0; i < MAXPL; ++i) {
+    if (i * 64 >= cols) break;
+    red[wv][0][lane] = pw[i];
+    red[wv][1][lane] = pb[i];
+    __syncthreads();
+    if (wv == 0) {
+      const int c = i * 64 + lane;
+      if (c < cols) {
+        ws[(long long)blockIdx.x * 2 * cols + c] = red[0][0][lane] + red[1][0][lane] + red[2][0][lane] + red[3][0][lane];
+        ws[(long long)blockIdx.x * 2 * cols + cols + c] =
+            red[0][1][lane] + red[1][1][lane] + red[2][1][lane] + red[3][1][lane];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void ln_bwd_reduce(const float* ws, int nblk, int cols, float* dw, float* db) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float a = 0.f, b = 0.f;
+  for (int k = 0; k < nblk; ++k) {
+    a += ws[(long long)k * 2 * cols + c];
+    b += ws[(long long)k * 2 * cols + cols + c];
+  }
+  if (dw) dw[c] += a;
+  if (db) db[c] += b;
+}
+
+// ---------------------------------------------------------------- softmax
+// wave per row (cols <= 1024)
+__global__ __launch_bounds__(256) void softmax_wave_kernel(const float* x, long long ldx, int rows, int cols,
+                                                           float scale, float* p, long long ldp) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float v[MAXPL];
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < MAXPL; ++i) {
+    const int c = i * 64 + lane;
+    v[i] = -INFINITY;
+    if (c < cols) {
+      v[i] = scale * x[(long long)row * ldx + c];
+      m = fmaxf(m, v[i]);
+    }
+  }
+  m = wave_max(m);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXPL; ++i) {
+    const int c = i * 64 + lane;
+    if (c < cols) {
+      v[i] = __expf(v[i] - m);
+      s += v[i];
+    }
+  }
+  const float inv = 1.f / wave_sum(s);
+#pragma unroll
+  for (int i = 0; i < MAXPL; ++i) {
+    const int c = i * 64 + lane;
+    if (c < cols) p[(long long)row * ldp + c] = v[i] * inv;
+  }
+}
+
+__device__ __forceinline__ float block_reduce(float v, bool is_max, float* sh) {
+  v = is_max ? wave_max(v) : wave_sum(v);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) sh[wv] = v;
+  __syncthreads();
+  float r = sh[0];
+  for (int i = 1; i < (int)(blockDim.x >> 6); ++i) r = is_max ? fmaxf(r, sh[i]) : r + sh[i];
+  return r;
+}
+
+// block per row (long rows)
+__global__ __launch_bounds__(256) void softmax_block_kernel(const float* x, long long ldx, int rows, int cols,
+                                                            float scale, float* p, long long ldp) {
+  __shared__ float sh[4];
+  const int row = blockIdx.x;
+  const float* xr = x + (long long)row * ldx;
+  float m = -INFINITY;
+  for (int c = threadIdx.x; c < cols; c += 256) m = fmaxf(m, scale * xr[c]);
+  m = block_reduce(m, true, sh);
+  float s = 0.f;
+  for (int c = threadIdx.x; c < cols; c += 256) s += __expf(scale * xr[c] - m);
+  s = block_reduce(s, false, sh);
+  const float inv = 1.f / s;
+  float* pr = p + (long long)row * ldp;
+  for (int c = threadIdx.x; c < cols; c += 256) pr[c] = __expf(scale * xr[c] - m) * inv;
+}
+
+// dlogit = scale * p * (dp - sum(dp * p)) + extra
+__global__ __launch_bounds__(256) void softmax_bwd_block_kernel(const float* p, long long ldp, const float* dp,
+                                                                long long lddp, const float* extra,
+                                                                long long lde, int cols, float scale,
+                                                                float* dl, long long ldd) {
+  __shared__ float sh[4];
+  const int row = blockIdx.x;
+  const float* pr = p + (long long)row * ldp;
+  const float* dr = dp + (long long)row * lddp;
+  float s = 0.f;
+  for (int c = threadIdx.x; c < cols; c += 256) s += pr[c] * dr[c];
+  s = block_reduce(s, false, sh);
+  float* out = dl + (long long)row * ldd;
+  for (int c = threadIdx.x; c < cols; c += 256) {
+    float v = scale * pr[c] * (dr[c] - s);
+    if (extra) v += extra[(long long)row * lde + c];
+    out[c] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void softmax_bwd_wave_kernel(const float* p, long long ldp, const float* dp,
+                                                               long long lddp, const float* extra,
+                                                               long long lde, int rows, int cols,
+                                                               float scale, float* dl, long long ldd) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float pv[MAXPL], dv[MAXPL];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXPL; ++i) {
+    const int c = i * 64 + lane;
+    pv[i] = dv[i] = 0.f;
+    if (c < cols) {
+      pv[i] = p[(long long)row * ldp + c];
+      dv[i] = dp[(long long)row * lddp + c];
+      s += pv[i] * dv[i];
+    }
+  }
+  s = wave_sum(s);
+#pragma unroll
+  for (int i = 0; i < MAXPL; ++i) {
+    const int c = i * 64 + lane;
+    if (c < cols) {
+      float v = scale * pv[i] * (dv[i] - s);
+      if (extra) v += extra[(long long)row * lde + c];
+      dl[(long long)row * ldd + c] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- process_feature
+__global__ __launch_bounds__(256) void pf_fwd_kernel(const float* x, long long ldx, int rows, int cols, int n,
+                                                     float* out, long long ldo) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + (long long)row * ldx;
+  float* orow = out + (long long)row * ldo;
+  const int f = cols - n;
+  for (int c = lane; c < f; c += 64) orow[c] = xr[c];
+  float m = -INFINITY;
+  for (int c = lane; c < n; c += 64) m = fmaxf(m, xr[f + c]);
+  m = wave_max(m);
+  float s = 0.f;
+  for (int c = lane; c < n; c += 64) s += __expf(xr[f + c] - m);
+  const float inv = 1.f / wave_sum(s);
+  for (int c = lane; c < n; c += 64) orow[f + c] = __expf(xr[f + c] - m) * inv;
+}
+
+__global__ __launch_bounds__(256) void pf_bwd_kernel(const float* out, long long ldo, const float* dout,
+                                                     long long lddo, const float* dcl, long long lddc,
+                                                     int rows, int cols, int n, float* dx, long long lddx) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int f = cols - n;
+  const float* orow = out + (long long)row * ldo;
+  const float* drow = dout + (long long)row * lddo;
+  float* xrow = dx + (long long)row * lddx;
+  for (int c = lane; c < f; c += 64) xrow[c] = drow[c];
+  float s = 0.f;
+  for (int c = lane; c < n; c += 64) s += orow[f + c] * drow[f + c];
+  s = wave_sum(s);
+  for (int c = lane; c < n; c += 64) {
+    float v = orow[f + c] * (drow[f + c] - s);
+    if (dcl) v += dcl[(long long)row * lddc + c];
+    xrow[f + c] = v;
+  }
+}
+
+// ---------------------------------------------------------------- L2 normalise
+__global__ __launch_bounds__(256) void l2n_fwd_kernel(const float* x, long long ldx, int rows, int cols, float* y,
+                                                      long long ldy, float* nrm) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float s = 0.f;
+  for (int c = lane; c < cols; c += 64) {
+    const float v = x[(long long)row * ldx + c];
+    s += v * v;
+  }
+  const float n = fmaxf(sqrtf(wave_sum(s)), 1e-12f);
+  const float inv = 1.f / n;
+  for (int c = lane; c < cols; c += 64) y[(long long)row * ldy + c] = x[(long long)row * ldx + c] * inv;
+  if (lane == 0) nrm[row] = n;
+}
+
+// y = x / max(|x|, eps):  dx = (dy - y * <dy, y>) / n   (n > eps; else dx = dy / eps)
+__global__ __launch_bounds__(256) void l2n_bwd_kernel(const float* y, long long ldy, const float* nrm,
+                                                      const float* dy, long long lddy, int rows, int cols,
+                                                      float* dx, long long lddx) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float n = nrm[row];
+  float s = 0.f;
+  for (int c = lane; c < cols; c += 64) s += y[(long long)row * ldy + c] * dy[(long long)row * lddy + c];
+  s = wave_sum(s);
+  const bool clamped = !(n > 1e-12f);
+  const float inv = 1.f / n;
+  for (int c = lane; c < cols; c += 64) {
+    const float g = dy[(long long)row * lddy + c];
+    dx[(long long)row * lddx + c] = clamped ? g * inv : (g - y[(long long)row * ldy + c] * s) * inv;
+  }
+}
+
+}  // namespace
+
+int launch_layernorm_fwd(const float* x, long long ldx, const float* r, long long ldr, const float* w,
+                         const float* b, float eps, int rows, int cols, int relu, float* y, long long ldy,
+                         float* mean, float* rstd, float* xhat, long long ldxh, hipStream_t s) {
+  FX_REQUIRE(cols > 0 && cols <= 64 * MAXPL, "layernorm: cols must be in (0, 1024]");
+  if (rows == 0) return FX_OK;
+  hipLaunchKernelGGL(ln_fwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, r, ldr, w, b, eps, rows, cols,
+                     relu, y, ldy, mean, rstd, xhat, ldxh);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+long long layernorm_bwd_ws_floats(int rows, int cols) {
+  const int nblk = std::min(cdiv(rows, 4), 256);
+  return (long long)nblk * 2 * cols;
+}
+
+int launch_layernorm_bwd(const float* dy, long long lddy, const float* y, long long ldy, const float* xhat,
+                         long long ldxh, const float* w, const float* rstd, int rows, int cols, int relu,
+                         float* dx, long long lddx, float* dw, float* db, float* ws, hipStream_t s) {
+  FX_REQUIRE(cols > 0 && cols <= 64 * MAXPL, "layernorm: cols must be in (0, 1024]");
+  if (rows == 0) return FX_OK;
+  const int nblk = std::min(cdiv(rows, 4), 256);
+  const bool want = dw || db;
+  FX_REQUIRE(!want || ws, "layernorm bwd: workspace required for dw/db");
+  hipLaunchKernelGGL(ln_bwd_kernel, dim3(nblk), dim3(256), 0, s, dy, lddy, y, ldy, xhat, ldxh, w, rstd, rows,
+                     cols, relu, dx, lddx, want ? ws : nullptr);
+  if (want) hipLaunchKernelGGL(ln_bwd_reduce, dim3(cdiv(cols, 256)), dim3(256), 0, s, ws, nblk, cols, dw, db);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+int launch_softmax_rows(const float* x, long long ldx, int rows, int cols, float scale, float* p, long long ldp,
+                        hipStream_t s) {
+  if (rows == 0 || cols == 0) return FX_OK;
+  if (cols <= 64 * MAXPL)
+    hipLaunchKernelGGL(softmax_wave_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, rows, cols, scale, p, ldp);
+  else
+    hipLaunchKernelGGL(softmax_block_kernel, dim3(rows), dim3(256), 0, s, x, ldx, rows, cols, scale, p, ldp);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+int launch_softmax_rows_bwd(const float* p, long long ldp, const float* dp, long long lddp, const float* extra,
+                            long long lde, int rows, int cols, float scale, float* dl, long long ldd,
+                            hipStream_t s) {
+  if (rows == 0 || cols == 0) return FX_OK;
+  if (cols <= 64 * MAXPL)
+    hipLaunchKernelGGL(softmax_bwd_wave_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, p, ldp, dp, lddp, extra, lde,
+                       rows, cols, scale, dl, ldd);
+  else
+    hipLaunchKernelGGL(softmax_bwd_block_kernel, dim3(rows), dim3(256), 0, s, p, ldp, dp, lddp, extra, lde, cols,
+                       scale, dl, ldd);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+int launch_pf_fwd(const float* x, long long ldx, int rows, int cols, int n, float* out, long long ldo,
+                  hipStream_t s) {
+  FX_REQUIRE(n > 0 && n <= cols, "process_feature: need 0 < n <= cols");
+  if (rows == 0) return FX_OK;
+  hipLaunchKernelGGL(pf_fwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, rows, cols, n, out, ldo);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+int launch_pf_bwd(const float* out, long long ldo, const float* dout, long long lddo, const float* dcl,
+                  long long lddc, int rows, int cols, int n, float* dx, long long lddx, hipStream_t s) {
+  FX_REQUIRE(n > 0 && n <= cols, "process_feature: need 0 < n <= cols");
+  if (rows == 0) return FX_OK;
+  hipLaunchKernelGGL(pf_bwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, out, ldo, dout, lddo, dcl, lddc, rows,
+                     cols, n, dx, lddx);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+int launch_l2n_fwd(const float* x, long long ldx, int rows, int cols, float* y, long long ldy, float* nrm,
+                   hipStream_t s) {
+  if (rows == 0) return FX_OK;
+  hipLaunchKernelGGL(l2n_fwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, rows, cols, y, ldy, nrm);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+int launch_l2n_bwd(const float* y, long long ldy, const float* nrm, const float* dy, long long lddy, int rows,
+                   int cols, float* dx, long long lddx, hipStream_t s) {
+  if (rows == 0) return FX_OK;
+  hipLaunchKernelGGL(l2n_bwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, y, ldy, nrm, dy, lddy, rows, cols, dx,
+                     lddx);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+}  // namespace fx

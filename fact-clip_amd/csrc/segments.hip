@@ -1,0 +1,137 @@
+// Temporal down/up-sampling on device (UpdateBlockTDU.temporal_downsample,
+// blocks.py:417-437; TemporalDownsampleUpsample, basic.py:595-651;
+// parse_label, utils/utils.py:25-48).
+//
+// The reference copies the argmax to the host, run-length-encodes it in numpy
+// and copies index tensors back.  Here: argmax (many workgroups) -> one
+// 1024-thread workgroup does the boundary scan and writes seg_id / starts /
+// ends / S; the host reads S once (the reference also synchronises here).
+// Segment pooling is a deterministic, frame-ordered sum per segment.
+#include "fx_common.h"
+
+namespace fx {
+namespace {
+
+__global__ __launch_bounds__(256) void argmax_rows_kernel(const float* x, long long ldx, int col0, int ncls, int T,
+                                                          int32_t* pred) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= T) return;
+  const float* xr = x + (long long)t * ldx + col0;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int c = lane; c < ncls; c += 64) {
+    const float v = xr[c];
+    if (v > best) {  // lanes visit increasing c: keeps the first max per lane
+      best = v;
+      bi = c;
+    }
+  }
+  // reduce (max value, then smallest index) across the wave == torch first-max argmax
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > best || (ov == best && oi < bi)) {
+      best = ov;
+      bi = oi;
+    }
+  }
+  if (lane == 0) pred[t] = (bi == 0x7fffffff) ? 0 : bi;
+}
+
+constexpr int SCAN_THREADS = 1024;
+
+__global__ __launch_bounds__(SCAN_THREADS) void boundary_scan_kernel(const int32_t* pred, int T, int32_t* seg_id,
+                                                                     int32_t* seg_start, int32_t* seg_end,
+                                                                     int32_t* num_seg) {
+  __shared__ int32_t sums[SCAN_THREADS];
+  const int tid = threadIdx.x;
+  const int per = (T + SCAN_THREADS - 1) / SCAN_THREADS;
+  const int b = tid * per, e = min(T, b + per);
+  int cnt = 0;
+  for (int t = b; t < e; ++t) cnt += (t == 0 || pred[t] != pred[t - 1]) ? 1 : 0;
+  sums[tid] = cnt;
+  __syncthreads();
+  // Hillis-Steele inclusive scan over 1024 partial counts
+  for (int off = 1; off < SCAN_THREADS; off <<= 1) {
+    const int v = tid >= off ? sums[tid - off] : 0;
+    __syncthreads();
+    sums[tid] += v;
+    __syncthreads();
+  }
+  int sid = sums[tid] - cnt - 1;  // segment index before this chunk's first frame
+  for (int t = b; t < e; ++t) {
+    if (t == 0 || pred[t] != pred[t - 1]) {
+      ++sid;
+      seg_start[sid] = t;
+      if (sid > 0) seg_end[sid - 1] = t - 1;
+    }
+    seg_id[t] = sid;
+  }
+  if (tid == SCAN_THREADS - 1) {
+    const int S = sums[tid];
+    num_seg[0] = S;
+    if (S > 0) seg_end[S - 1] = T - 1;
+  }
+}
+
+// y[s, c] = (sum_{t=start..end} x[t, c]) * (mean ? 1/len : 1)  (+ y if accumulate)
+__global__ __launch_bounds__(256) void seg_reduce_kernel(const float* x, long long ldx, const int32_t* st,
+                                                         const int32_t* en, int S, int cols, int mean, float* y,
+                                                         long long ldy, int accumulate) {
+  const int s = blockIdx.x;
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (s >= S || c >= cols) return;
+  const int a = st[s], b = en[s];
+  float acc = 0.f;
+  for (int t = a; t <= b; ++t) acc += x[(long long)t * ldx + c];
+  if (mean) acc = acc / (float)(b - a + 1);
+  float* yp = y + (long long)s * ldy + c;
+  *yp = accumulate ? *yp + acc : acc;
+}
+
+// dx[t, c] (+)= dy[seg_id[t], c] / len
+__global__ __launch_bounds__(256) void seg_mean_bwd_kernel(const float* dy, long long lddy, const int32_t* sid,
+                                                           const int32_t* st, const int32_t* en, int T, int cols,
+                                                           float* dx, long long lddx, int accumulate) {
+  const int t = blockIdx.x;
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (t >= T || c >= cols) return;
+  const int s = sid[t];
+  const float v = dy[(long long)s * lddy + c] / (float)(en[s] - st[s] + 1);
+  float* p = dx + (long long)t * lddx + c;
+  *p = accumulate ? *p + v : v;
+}
+
+}  // namespace
+
+int launch_segments(const float* x, long long ldx, int col0, int ncls, int T, int32_t* pred, int32_t* seg_id,
+                    int32_t* seg_start, int32_t* seg_end, int32_t* num_seg, hipStream_t s) {
+  FX_REQUIRE(T > 0 && ncls > 0, "segments: need T > 0 and ncls > 0");
+  hipLaunchKernelGGL(argmax_rows_kernel, dim3(cdiv(T, 4)), dim3(256), 0, s, x, ldx, col0, ncls, T, pred);
+  hipLaunchKernelGGL(boundary_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, s, pred, T, seg_id, seg_start, seg_end,
+                     num_seg);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+int launch_seg_reduce(const float* x, long long ldx, const int32_t* st, const int32_t* en, int S, int cols, int mean,
+                      float* y, long long ldy, int accumulate, hipStream_t s) {
+  if (S == 0 || cols == 0) return FX_OK;
+  hipLaunchKernelGGL(seg_reduce_kernel, dim3(S, cdiv(cols, 256)), dim3(256), 0, s, x, ldx, st, en, S, cols, mean, y,
+                     ldy, accumulate);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+int launch_seg_mean_bwd(const float* dy, long long lddy, const int32_t* sid, const int32_t* st, const int32_t* en,
+                        int T, int cols, float* dx, long long lddx, int accumulate, hipStream_t s) {
+  if (T == 0 || cols == 0) return FX_OK;
+  hipLaunchKernelGGL(seg_mean_bwd_kernel, dim3(T, cdiv(cols, 256)), dim3(256), 0, s, dy, lddy, sid, st, en, T, cols,
+                     dx, lddx, accumulate);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+}  // namespace fx

@@ -1,0 +1,643 @@
+"""Autograd functions over the libfactmx C ABI.
+
+Every function here launches hand-written HIP kernels through ``native`` on
+PyTorch's current stream; tensors are fp32 row-major (rows, channels).  There
+is no eager/CPU fallback: a missing library raises FactmxNativeError.
+"""
+import ctypes
+import math
+
+import torch
+
+from . import native as nx
+
+_f32 = torch.float32
+
+
+def _empty(*shape, device):
+    return torch.empty(*shape, device=device, dtype=_f32)
+
+
+def _ws(n, device):
+    return torch.empty(max(int(n), 1), device=device, dtype=_f32)
+
+
+def _2d(t):
+    """(N, 1, C) or (N, C) -> (N, C) view with unit column stride."""
+    if t.dim() == 3:
+        assert t.shape[1] == 1, t.shape
+        t = t[:, 0, :]
+    if t.stride(-1) != 1:
+        t = t.contiguous()
+    return t
+
+
+def _w2d(w):
+    return w.reshape(w.shape[0], -1) if w.dim() == 3 else w
+
+
+def _check(status, what):
+    if status != 0:
+        nx.check(status, what)
+
+
+# ---------------------------------------------------------------------------
+# raw launch helpers (no autograd)
+# ---------------------------------------------------------------------------
+
+def lin_fwd(x, w, b, relu=0, out=None):
+    lib = nx.load()
+    w2 = _w2d(w)
+    M, K = x.shape
+    N = w2.shape[0]
+    y = out if out is not None else _empty(M, N, device=x.device)
+    _check(lib.fx_linear_fwd(nx.ptr(x), nx.ld(x), None, 0, 0, M, K, nx.ptr(w2), nx.ld(w2), nx.ptr(b),
+                             nx.ptr(y), nx.ld(y), N, int(relu), nx.stream()), "fx_linear_fwd")
+    return y
+
+
+def lin_bwd(dy, x, w, need_dx=True, need_dw=True, need_db=True, relu_out=None):
+    lib = nx.load()
+    w2 = _w2d(w)
+    M, K = x.shape
+    N = w2.shape[0]
+    dev = dy.device
+    dx = _empty(M, K, device=dev) if need_dx else None
+    dw = _empty(N, K, device=dev) if need_dw else None
+    db = _empty(N, device=dev) if need_db else None
+    ws = _ws(lib.fx_linear_bwd_workspace_floats(M, K, N), dev)
+    _check(lib.fx_linear_bwd(nx.ptr(dy), nx.ld(dy), nx.ptr(x), nx.ld(x), nx.ptr(w2), nx.ld(w2),
+                             nx.ptr(relu_out), nx.ld(relu_out), M, K, N, nx.ptr(dx), nx.ld(dx),
+                             nx.ptr(dw), nx.ld(dw), nx.ptr(db), 0, nx.ptr(ws), nx.stream()), "fx_linear_bwd")
+    if dw is not None and w.dim() == 3:
+        dw = dw.reshape(w.shape)
+    return dx, dw, db
+
+
+# ---------------------------------------------------------------------------
+# Linear / Conv1d(k=1)
+# ---------------------------------------------------------------------------
+
+class LinearFn(torch.autograd.Function):
+    """nn.Linear / Conv1d(k=1) on (rows, K): basic.py:139,177,182; blocks.py:154,158,402,414."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, relu):
+        y = lin_fwd(x, w, b, relu)
+        ctx.relu = relu
+        ctx.save_for_backward(x, w, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx, dw, db = lin_bwd(dy, x, w, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+                             ctx.needs_input_grad[2], relu_out=y if ctx.relu else None)
+        return dx, dw, db, None
+
+
+def linear(x, w, b, relu=False):
+    return LinearFn.apply(_2d(x), w, b, int(relu))
+
+
+# ---------------------------------------------------------------------------
+# LayerNorm (+ fused residual, + fused ReLU)
+# ---------------------------------------------------------------------------
+
+class LayerNormFn(torch.autograd.Function):
+    """post-norm ``LN(x + r)`` (basic.py:444-450, 504-522; blocks.py:155-156 with ReLU)."""
+
+    @staticmethod
+    def forward(ctx, x, r, w, b, eps, relu):
+        lib = nx.load()
+        rows, cols = x.shape
+        y = _empty(rows, cols, device=x.device)
+        xhat = _empty(rows, cols, device=x.device)
+        rstd = _empty(rows, device=x.device)
+        _check(lib.fx_layernorm_fwd(nx.ptr(x), nx.ld(x), nx.ptr(r), nx.ld(r), nx.ptr(w), nx.ptr(b), float(eps),
+                                    rows, cols, int(relu), nx.ptr(y), cols, nx.ptr(xhat), cols, nx.ptr(rstd),
+                                    nx.stream()), "fx_layernorm_fwd")
+        ctx.relu = relu
+        ctx.has_r = r is not None
+        ctx.save_for_backward(y, xhat, rstd, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = nx.load()
+        y, xhat, rstd, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        rows, cols = y.shape
+        dev = dy.device
+        dx = _empty(rows, cols, device=dev)
+        dw = torch.zeros(cols, device=dev, dtype=_f32)
+        db = torch.zeros(cols, device=dev, dtype=_f32)
+        ws = _ws(lib.fx_layernorm_bwd_workspace_floats(rows, cols), dev)
+        _check(lib.fx_layernorm_bwd(nx.ptr(dy), cols, nx.ptr(y), cols, nx.ptr(xhat), cols, nx.ptr(w), nx.ptr(rstd),
+                                    rows, cols, int(ctx.relu), nx.ptr(dx), cols, nx.ptr(dw), nx.ptr(db), nx.ptr(ws),
+                                    nx.stream()), "fx_layernorm_bwd")
+        return dx, (dx if ctx.has_r else None), dw, db, None, None
+
+
+def layer_norm(x, w, b, eps=1e-5, residual=None, relu=False):
+    return LayerNormFn.apply(_2d(x), None if residual is None else _2d(residual), w, b, eps, int(relu))
+
+
+# ---------------------------------------------------------------------------
+# process_feature (class-logit softmax tail)
+# ---------------------------------------------------------------------------
+
+class ProcessFeatureFn(torch.autograd.Function):
+    """``Block.process_feature`` (blocks.py:195-202): out = [x[:, :-n], softmax(x[:, -n:])]."""
+
+    @staticmethod
+    def forward(ctx, x, n):
+        lib = nx.load()
+        rows, cols = x.shape
+        out = _empty(rows, cols, device=x.device)
+        _check(lib.fx_process_feature_fwd(nx.ptr(x), nx.ld(x), rows, cols, n, nx.ptr(out), cols, nx.stream()),
+               "fx_process_feature_fwd")
+        ctx.n = n
+        ctx.save_for_backward(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = nx.load()
+        (out,) = ctx.saved_tensors
+        dout = dout.contiguous()
+        rows, cols = out.shape
+        dx = _empty(rows, cols, device=out.device)
+        _check(lib.fx_process_feature_bwd(nx.ptr(out), cols, nx.ptr(dout), cols, None, 0, rows, cols, ctx.n,
+                                          nx.ptr(dx), cols, nx.stream()), "fx_process_feature_bwd")
+        return dx, None
+
+
+def process_feature(x, n):
+    """Returns (feature-with-probs, clogit view) exactly like the reference."""
+    x2 = _2d(x)
+    out = ProcessFeatureFn.apply(x2, n)
+    return out, x2[:, -n:]
+
+
+# ---------------------------------------------------------------------------
+# L2 normalisation
+# ---------------------------------------------------------------------------
+
+class L2NormFn(torch.autograd.Function):
+    """``F.normalize(dim=-1, eps=1e-12)`` (blocks.py:174)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        lib = nx.load()
+        rows, cols = x.shape
+        y = _empty(rows, cols, device=x.device)
+        nrm = _empty(rows, device=x.device)
+        _check(lib.fx_l2norm_fwd(nx.ptr(x), nx.ld(x), rows, cols, nx.ptr(y), cols, nx.ptr(nrm), nx.stream()),
+               "fx_l2norm_fwd")
+        ctx.save_for_backward(y, nrm)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = nx.load()
+        y, nrm = ctx.saved_tensors
+        dy = dy.contiguous()
+        rows, cols = y.shape
+        dx = _empty(rows, cols, device=y.device)
+        _check(lib.fx_l2norm_bwd(nx.ptr(y), cols, nx.ptr(nrm), nx.ptr(dy), cols, rows, cols, nx.ptr(dx), cols,
+                                 nx.stream()), "fx_l2norm_bwd")
+        return dx
+
+
+def l2_normalize(x):
+    return L2NormFn.apply(_2d(x))
+
+
+# ---------------------------------------------------------------------------
+# Multi-head attention (nn.MultiheadAttention math)
+# ---------------------------------------------------------------------------
+
+class MHAFn(torch.autograd.Function):
+    """``nn.MultiheadAttention`` forward/backward as used by SALayer/SCALayer
+    (basic.py:442, 500, 513): in-projections, per-head softmax(QK^T/sqrt(hd))V, out_proj."""
+
+    @staticmethod
+    def forward(ctx, q_in, k_in, v_in, wq, bq, wk, bk, wv, bv, wo, bo, nhead):
+        lib = nx.load()
+        dev = q_in.device
+        Lq, Lk = q_in.shape[0], k_in.shape[0]
+        E = wq.shape[0]
+        q = lin_fwd(q_in, wq, bq)
+        k = lin_fwd(k_in, wk, bk)
+        v = lin_fwd(v_in, wv, bv)
+        probs = _empty(nhead, Lq, Lk, device=dev)
+        o = _empty(Lq, E, device=dev)
+        ws = _ws(lib.fx_mha_core_workspace_floats(Lq, Lk, E, nhead), dev)
+        _check(lib.fx_mha_core_fwd(nx.ptr(q), E, nx.ptr(k), E, nx.ptr(v), E, Lq, Lk, E, nhead, nx.ptr(probs),
+                                   nx.ptr(o), E, nx.ptr(ws), nx.stream()), "fx_mha_core_fwd")
+        out = lin_fwd(o, wo, bo)
+        ctx.nhead = nhead
+        ctx.save_for_backward(q_in, k_in, v_in, wq, wk, wv, wo, q, k, v, probs, o)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = nx.load()
+        q_in, k_in, v_in, wq, wk, wv, wo, q, k, v, probs, o = ctx.saved_tensors
+        nd = ctx.needs_input_grad
+        dout = dout.contiguous()
+        dev = dout.device
+        Lq, Lk = q_in.shape[0], k_in.shape[0]
+        E = wq.shape[0]
+        nh = ctx.nhead
+        d_o, dwo, dbo = lin_bwd(dout, o, wo, True, nd[9], nd[10])
+        dq = _empty(Lq, E, device=dev)
+        dk = _empty(Lk, E, device=dev)
+        dv = _empty(Lk, E, device=dev)
+        ws = _ws(lib.fx_mha_core_workspace_floats(Lq, Lk, E, nh), dev)
+        _check(lib.fx_mha_core_bwd(nx.ptr(q), E, nx.ptr(k), E, nx.ptr(v), E, nx.ptr(probs), nx.ptr(d_o), E, Lq, Lk,
+                                   E, nh, nx.ptr(dq), E, nx.ptr(dk), E, nx.ptr(dv), E, nx.ptr(ws), nx.stream()),
+               "fx_mha_core_bwd")
+        dq_in, dwq, dbq = lin_bwd(dq, q_in, wq, nd[0], nd[3], nd[4])
+        dk_in, dwk, dbk = lin_bwd(dk, k_in, wk, nd[1], nd[5], nd[6])
+        dv_in, dwv, dbv = lin_bwd(dv, v_in, wv, nd[2], nd[7], nd[8])
+        return dq_in, dk_in, dv_in, dwq, dbq, dwk, dbk, dwv, dbv, dwo, dbo, None
+
+
+def mha(mod, query, key, value):
+    """Run an nn.MultiheadAttention module's parameters through MHAFn (dropout must be off)."""
+    E = mod.embed_dim
+    if mod._qkv_same_embed_dim:
+        W = mod.in_proj_weight
+        wq, wk, wv = W[:E], W[E:2 * E], W[2 * E:]
+    else:
+        wq, wk, wv = mod.q_proj_weight, mod.k_proj_weight, mod.v_proj_weight
+    b = mod.in_proj_bias
+    return MHAFn.apply(_2d(query), _2d(key), _2d(value), wq, b[:E], wk, b[E:2 * E], wv, b[2 * E:],
+                       mod.out_proj.weight, mod.out_proj.bias, mod.num_heads)
+
+
+# ---------------------------------------------------------------------------
+# X2Y_map
+# ---------------------------------------------------------------------------
+
+class X2YFn(torch.autograd.Function):
+    """``X2Y_map.forward`` (basic.py:349-389): returns (Y_out, attn_logit, attn)."""
+
+    @staticmethod
+    def forward(ctx, X, Y, Xpos, Ypos, wk, bk, wv, bv, wq, bq, wy, by):
+        lib = nx.load()
+        dev = X.device
+        Nx, xdim = X.shape
+        Ny, ydim = Y.shape
+        Hd, outdim = wk.shape[0], wy.shape[0]
+        out = _empty(Ny, outdim, device=dev)
+        logit = _empty(Ny, Nx, device=dev)
+        attn = _empty(Ny, Nx, device=dev)
+        saved = _ws(lib.fx_x2y_saved_floats(Nx, xdim, Ny, ydim, Hd), dev)
+        ws = _ws(lib.fx_x2y_workspace_floats(Nx, xdim, Ny, ydim, Hd, outdim), dev)
+        xpc = 0 if Xpos is None else Xpos.shape[1]
+        ypc = 0 if Ypos is None else Ypos.shape[1]
+        _check(lib.fx_x2y_fwd(nx.ptr(X), nx.ld(X), Nx, xdim, nx.ptr(Xpos), nx.ld(Xpos), xpc,
+                              nx.ptr(Y), nx.ld(Y), Ny, ydim, nx.ptr(Ypos), nx.ld(Ypos), ypc,
+                              nx.ptr(wk), nx.ptr(bk), nx.ptr(wv), nx.ptr(bv), nx.ptr(wq), nx.ptr(bq),
+                              nx.ptr(wy), nx.ptr(by), Hd, outdim, nx.ptr(out), outdim, nx.ptr(logit), nx.ptr(attn),
+                              nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_x2y_fwd")
+        ctx.dims = (Nx, xdim, Ny, ydim, Hd, outdim, xpc, ypc)
+        ctx.has_pos = (Xpos is not None, Ypos is not None)
+        ctx.save_for_backward(X, Y, wk, wv, wq, wy, attn, saved)
+        ctx.mark_non_differentiable(attn)
+        return out, logit, attn
+
+    @staticmethod
+    def backward(ctx, dout, dlogit, dattn):
+        lib = nx.load()
+        X, Y, wk, wv, wq, wy, attn, saved = ctx.saved_tensors
+        Nx, xdim, Ny, ydim, Hd, outdim, xpc, ypc = ctx.dims
+        hx, hy = ctx.has_pos
+        nd = ctx.needs_input_grad
+        dev = X.device
+        dout = torch.zeros(Ny, outdim, device=dev) if dout is None else dout.contiguous()
+        dlogit = None if dlogit is None else dlogit.contiguous()
+        dattn = None if dattn is None else dattn.contiguous()
+        dX = _empty(Nx, xdim, device=dev) if nd[0] else None
+        dY = _empty(Ny, ydim, device=dev) if nd[1] else None
+        dXp = _empty(Nx, xpc, device=dev) if (hx and nd[2]) else None
+        dYp = _empty(Ny, ypc, device=dev) if (hy and nd[3]) else None
+        g = [_empty(*t.shape, device=dev) for t in (wk, wk[:, 0], wv, wv[:, 0], wq, wq[:, 0], wy, wy[:, 0])]
+        ws = _ws(lib.fx_x2y_workspace_floats(Nx, xdim, Ny, ydim, Hd, outdim), dev)
+        _check(lib.fx_x2y_bwd(nx.ptr(X), nx.ld(X), Nx, xdim, xpc, nx.ptr(Y), nx.ld(Y), Ny, ydim, ypc,
+                              nx.ptr(wk), nx.ptr(wv), nx.ptr(wq), nx.ptr(wy), Hd, outdim, nx.ptr(attn), nx.ptr(saved),
+                              nx.ptr(dout), outdim, nx.ptr(dlogit), nx.ptr(dattn), nx.ptr(dX), nx.ptr(dXp),
+                              nx.ptr(dY), nx.ptr(dYp), *[nx.ptr(t) for t in g], int(hx), int(hy), nx.ptr(ws),
+                              nx.stream()), "fx_x2y_bwd")
+        return (dX, dY, dXp, dYp) + tuple(g)
+
+
+def x2y(mod, X, Y, Xpos, Ypos):
+    return X2YFn.apply(_2d(X), _2d(Y), None if Xpos is None else _2d(Xpos), None if Ypos is None else _2d(Ypos),
+                       mod.X_K.weight, mod.X_K.bias, mod.X_V.weight, mod.X_V.bias, mod.Y_Q.weight, mod.Y_Q.bias,
+                       mod.Y_W.weight, mod.Y_W.bias)
+
+
+# ---------------------------------------------------------------------------
+# MS-TCN stack
+# ---------------------------------------------------------------------------
+
+def _ptr_array(ts):
+    arr = (ctypes.c_void_p * max(len(ts), 1))(*[nx.ptr(t) for t in ts])
+    return arr
+
+
+class MSTCNFn(torch.autograd.Function):
+    """Whole ``MSTCN.forward`` (basic.py:200-220) in one C call (eval-mode dropout)."""
+
+    @staticmethod
+    def forward(ctx, x, meta, *params):
+        lib = nx.load()
+        T, nvid, cin, F, cout, nl, ln, in_map, d0, dfac = meta
+        it = iter(params)
+        w_in = b_in = None
+        if in_map:
+            w_in, b_in = next(it), next(it)
+        layers = []
+        for _ in range(nl):
+            lw = [next(it), next(it), next(it), next(it)]
+            lw += [next(it), next(it)] if ln else [None, None]
+            layers.append(lw)
+        w_out, b_out = next(it), next(it)
+        keep = []
+        prm = nx.MstcnParams()
+        prm.cin, prm.F, prm.cout, prm.num_layers, prm.layernorm, prm.in_map = cin, F, cout, nl, int(ln), int(in_map)
+        prm.dil0, prm.dil_factor = d0, dfac
+        prm.w_in, prm.b_in = nx.ptr(w_in), nx.ptr(b_in)
+        for field, k in (("w_dil", 0), ("b_dil", 1), ("w_pw", 2), ("b_pw", 3), ("ln_w", 4), ("ln_b", 5)):
+            arr = _ptr_array([lw[k] for lw in layers])
+            keep.append(arr)
+            setattr(prm, field, ctypes.cast(arr, ctypes.c_void_p))
+        prm.w_out, prm.b_out = nx.ptr(w_out), nx.ptr(b_out)
+        rows = x.shape[0]
+        dev = x.device
+        y = _empty(rows, cout, device=dev)
+        saved = _ws(lib.fx_mstcn_saved_floats(ctypes.byref(prm), rows), dev)
+        ws = _ws(lib.fx_mstcn_workspace_floats(ctypes.byref(prm), rows), dev)
+        _check(lib.fx_mstcn_fwd(ctypes.byref(prm), nx.ptr(x), nx.ld(x), T, nvid, nx.ptr(y), cout, nx.ptr(saved),
+                                nx.ptr(ws), nx.stream()), "fx_mstcn_fwd")
+        ctx.meta = meta
+        ctx.prm = prm
+        ctx.keep = keep
+        ctx.layers_shapes = [(lw[0].shape, lw[2].shape) for lw in layers]
+        ctx.save_for_backward(x, saved, *params)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = nx.load()
+        x, saved, *params = ctx.saved_tensors
+        T, nvid, cin, F, cout, nl, ln, in_map, d0, dfac = ctx.meta
+        dev = x.device
+        dy = dy.contiguous()
+        grads = [_empty(*p_.shape, device=dev) for p_ in params]
+        # LayerNorm gains/biases are accumulated by the kernel -> zero them
+        off = 2 if in_map else 0
+        per = 6 if ln else 4
+        if ln:
+            for i in range(nl):
+                grads[off + i * per + 4].zero_()
+                grads[off + i * per + 5].zero_()
+        it = iter(grads)
+        g = nx.MstcnGrads()
+        if in_map:
+            g.w_in, g.b_in = nx.ptr(next(it)), nx.ptr(next(it))
+        lg = [[next(it) for _ in range(per)] for _ in range(nl)]
+        keep = []
+        for field, k in (("w_dil", 0), ("b_dil", 1), ("w_pw", 2), ("b_pw", 3), ("ln_w", 4), ("ln_b", 5)):
+            arr = _ptr_array([(l_[k] if k < len(l_) else None) for l_ in lg])
+            keep.append(arr)
+            setattr(g, field, ctypes.cast(arr, ctypes.c_void_p))
+        g.w_out, g.b_out = nx.ptr(next(it)), nx.ptr(next(it))
+        dx = _empty(*x.shape, device=dev) if ctx.needs_input_grad[0] else None
+        ws = _ws(lib.fx_mstcn_workspace_floats(ctypes.byref(ctx.prm), x.shape[0]), dev)
+        _check(lib.fx_mstcn_bwd(ctypes.byref(ctx.prm), ctypes.byref(g), nx.ptr(x), nx.ld(x), T, nvid, nx.ptr(dy),
+                                cout, nx.ptr(dx), nx.ld(dx), nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_mstcn_bwd")
+        return (dx, None) + tuple(grads)
+
+
+def mstcn(mod, x, T, nvid=1):
+    """Run a factmx.models.basic.MSTCN through MSTCNFn."""
+    x2 = _2d(x)
+    params = []
+    if mod.in_map:
+        params += [mod.conv_1x1.weight, mod.conv_1x1.bias]
+    for lyr in mod.layers:
+        params += [lyr.conv_dilated.weight, lyr.conv_dilated.bias, lyr.conv_1x1.weight, lyr.conv_1x1.bias]
+        if lyr.norm is not None:
+            params += [lyr.norm.weight, lyr.norm.bias]
+    params += [mod.conv_out.weight, mod.conv_out.bias]
+    ln = mod.layers[0].norm is not None if len(mod.layers) else False
+    meta = (T, nvid, x2.shape[1], mod.hid_dim, mod.out_dim, mod.num_layers, bool(ln), bool(mod.in_map),
+            mod.dilation0, mod.dilation_factor)
+    return MSTCNFn.apply(x2, meta, *params)
+
+
+# ---------------------------------------------------------------------------
+# generic dilated Conv1d(k=3) (MSTCN2 / standalone DilatedResidualLayer pieces)
+# ---------------------------------------------------------------------------
+
+def _conv_operand(t, cin, dil, direction, T, trans):
+    o = nx.Operand()
+    o.ptr, o.ld = nx.ptr(t), nx.ld(t)
+    o.trans = int(trans)
+    o.conv_taps, o.conv_cin, o.conv_dil, o.conv_dir, o.seq_len = 3, cin, dil, direction, T
+    return o
+
+
+def _rows_operand(t, trans=False):
+    o = nx.Operand()
+    o.ptr, o.ld = nx.ptr(t), nx.ld(t)
+    o.trans = int(trans)
+    o.conv_dir = 1
+    return o
+
+
+def gemm(M, N, K, a, b, c, ldc, bias=None, relu=0, resid=None, alpha=1.0, beta=0.0, gate=None, c_tap_cin=0,
+         split=1):
+    lib = nx.load()
+    d = nx.GemmDesc()
+    d.M, d.N, d.K, d.batch = M, N, K, 1
+    d.a, d.b = a, b
+    d.c, d.ldc = nx.ptr(c), ldc
+    d.alpha, d.beta = alpha, beta
+    d.bias = nx.ptr(bias)
+    d.resid, d.ld_resid = nx.ptr(resid), nx.ld(resid)
+    d.gate, d.ld_gate = nx.ptr(gate), nx.ld(gate)
+    d.relu, d.c_tap_cin = relu, c_tap_cin
+    d.split_k = split
+    ws = None
+    if split > 1:
+        ws = _ws(lib.fx_gemm_workspace_floats(ctypes.byref(d)), c.device)
+        d.workspace = nx.ptr(ws)
+    _check(lib.fx_gemm(ctypes.byref(d), nx.stream()), "fx_gemm")
+    return ws
+
+
+class Conv3Fn(torch.autograd.Function):
+    """Conv1d(k=3, dilation d, padding d) on (T*nvid, C) rows as an implicit GEMM (basic.py:138, 237-245)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, dil, T):
+        rows, cin = x.shape
+        cout = w.shape[0]
+        wf = w.permute(0, 2, 1).reshape(cout, 3 * cin).contiguous()       # [n][tap][c]
+        y = _empty(rows, cout, device=x.device)
+        gemm(rows, cout, 3 * cin, _conv_operand(x, cin, dil, 1, T, False), _rows_operand(wf), y, cout, bias=b)
+        ctx.dil, ctx.T = dil, T
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        rows, cin = x.shape
+        cout = w.shape[0]
+        dev = x.device
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            wb = w.permute(1, 2, 0).reshape(cin, 3 * cout).contiguous()   # [c][tap][n]
+            dx = _empty(rows, cin, device=dev)
+            gemm(rows, cin, 3 * cout, _conv_operand(dy, cout, ctx.dil, -1, ctx.T, False), _rows_operand(wb), dx, cin)
+        if ctx.needs_input_grad[1]:
+            dw = _empty(*w.shape, device=dev)
+            split = max(1, min(16, rows // 256))
+            gemm(cout, 3 * cin, rows, _rows_operand(dy, trans=True), _conv_operand(x, cin, ctx.dil, 1, ctx.T, True),
+                 dw, 3 * cin, c_tap_cin=cin, split=split)
+        if ctx.needs_input_grad[2]:
+            db = _colsum(dy)
+        return dx, dw, db, None, None
+
+
+def _colsum(t):
+    """Column sums (bias gradient) through fx_linear_bwd with dx/dw disabled."""
+    lib = nx.load()
+    M, N = t.shape
+    db = _empty(N, device=t.device)
+    ws = _ws(lib.fx_linear_bwd_workspace_floats(M, 1, N), t.device)
+    dummy_x = torch.empty(M, 1, device=t.device, dtype=_f32)
+    dummy_w = torch.empty(N, 1, device=t.device, dtype=_f32)
+    _check(lib.fx_linear_bwd(nx.ptr(t), nx.ld(t), nx.ptr(dummy_x), 1, nx.ptr(dummy_w), 1, None, 0, M, 1, N, None, 0,
+                             None, 0, nx.ptr(db), 0, nx.ptr(ws), nx.stream()), "colsum")
+    return db
+
+
+def conv3(x, w, b, dil, T):
+    return Conv3Fn.apply(_2d(x), w, b, dil, T)
+
+
+# ---------------------------------------------------------------------------
+# Temporal down/up-sampling
+# ---------------------------------------------------------------------------
+
+def segments_from_probs(x2d, col0, ncls):
+    """Device argmax + run-length boundaries; returns (S, seg_id, start, end) with one host read of S."""
+    lib = nx.load()
+    T = x2d.shape[0]
+    dev = x2d.device
+    pred = torch.empty(T, device=dev, dtype=torch.int32)
+    seg_id = torch.empty(T, device=dev, dtype=torch.int32)
+    st = torch.empty(T, device=dev, dtype=torch.int32)
+    en = torch.empty(T, device=dev, dtype=torch.int32)
+    ns = torch.empty(1, device=dev, dtype=torch.int32)
+    _check(lib.fx_segments_from_probs(nx.ptr(x2d), nx.ld(x2d), col0, ncls, T, nx.ptr(pred), nx.ptr(seg_id),
+                                      nx.ptr(st), nx.ptr(en), nx.ptr(ns), nx.stream()), "fx_segments_from_probs")
+    S = int(ns.item())
+    return S, seg_id, st[:S], en[:S]
+
+
+class SegMeanFn(torch.autograd.Function):
+    """``feature_frame2seg`` (basic.py:615-625): index_add over frames / segment length."""
+
+    @staticmethod
+    def forward(ctx, x, seg_id, st, en):
+        lib = nx.load()
+        S = st.shape[0]
+        T, C = x.shape
+        y = _empty(S, C, device=x.device)
+        _check(lib.fx_seg_mean_fwd(nx.ptr(x), nx.ld(x), nx.ptr(st), nx.ptr(en), S, C, nx.ptr(y), C, nx.stream()),
+               "fx_seg_mean_fwd")
+        ctx.save_for_backward(seg_id, st, en)
+        ctx.T = T
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = nx.load()
+        seg_id, st, en = ctx.saved_tensors
+        dy = dy.contiguous()
+        C = dy.shape[1]
+        dx = _empty(ctx.T, C, device=dy.device)
+        _check(lib.fx_seg_mean_bwd(nx.ptr(dy), C, nx.ptr(seg_id), nx.ptr(st), nx.ptr(en), ctx.T, C, nx.ptr(dx), C, 0,
+                                   nx.stream()), "fx_seg_mean_bwd")
+        return dx, None, None, None
+
+
+def seg_sum_rows(x, st, en):
+    lib = nx.load()
+    S = st.shape[0]
+    C = x.shape[1]
+    y = _empty(S, C, device=x.device)
+    _check(lib.fx_seg_sum_rows(nx.ptr(x), nx.ld(x), nx.ptr(st), nx.ptr(en), S, C, nx.ptr(y), C, 0, nx.stream()),
+           "fx_seg_sum_rows")
+    return y
+
+
+class SegMergeFn(torch.autograd.Function):
+    """``temporal_upsample`` (blocks.py:439-447): relu(sf_merge(cat[seg[seg_id], frame])).
+    The segment->frame gather is the A-operand row gather of the GEMM."""
+
+    @staticmethod
+    def forward(ctx, seg, frame, seg_id, st, en, w, b):
+        T = frame.shape[0]
+        Fs, H = seg.shape[1], frame.shape[1]
+        N = w.shape[0]
+        y = _empty(T, N, device=frame.device)
+        a = _rows_operand(seg)
+        a.rows0 = nx.ptr(seg_id)
+        a.ptr1, a.ld1, a.k_split = nx.ptr(frame), nx.ld(frame), Fs
+        gemm(T, N, Fs + H, a, _rows_operand(w), y, N, bias=b, relu=1)
+        ctx.save_for_backward(seg, frame, st, en, w, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = nx.load()
+        seg, frame, st, en, w, y = ctx.saved_tensors
+        dy = dy.contiguous()
+        T, N = y.shape
+        Fs = seg.shape[1]
+        dev = dy.device
+        dz = _empty(T, N, device=dev)
+        _check(lib.fx_relu_bwd(nx.ptr(dy), N, nx.ptr(y), N, T, N, nx.ptr(dz), N, nx.stream()), "fx_relu_bwd")
+        dzs = seg_sum_rows(dz, st, en)                        # gather backward folded before the GEMM
+        dseg, dws, _ = lin_bwd(dzs, seg, w[:, :Fs], True, True, False)
+        dframe, dwf, db = lin_bwd(dz, frame, w[:, Fs:], True, True, True)
+        dw = torch.cat([dws, dwf], 1)
+        return dseg, dframe, None, None, None, dw, db
+
+
+# ---------------------------------------------------------------------------
+# elementwise
+# ---------------------------------------------------------------------------
+
+def add_(a, b):
+    """a += b on device (same shape)."""
+    lib = nx.load()
+    rows, cols = a.shape
+    _check(lib.fx_add(nx.ptr(b), nx.ld(b), None, 0, rows, cols, nx.ptr(a), nx.ld(a), 1, nx.stream()), "fx_add")
+    return a
+
+
+def mha_scale(hd):
+    return 1.0 / math.sqrt(hd)

@@ -1,0 +1,482 @@
+"""Layer modules of FACT with the reference's Python surface, HIP underneath.
+
+Class names, constructor signatures, sub-module creation order (so a seeded
+init is identical) and state_dict keys follow fact_clip/models/basic.py.  The
+forwards run through ``factmx.functional`` (hand-written HIP kernels behind the
+libfactmx C ABI).  Tensors at the module boundary keep the reference's
+sequence-first (N, 1, C) layout; internally everything is (N, C) row-major.
+
+Dropout: the fused kernels run eval-mode dropout.  Dropout on materialised
+tensors (residual branches, FFN, projection head, channel masking) is applied
+with torch's GPU dropout; a non-zero dropout *inside* a fused kernel (MS-TCN
+layer output, attention probabilities, X2Y concat) raises in training mode.
+"""
+import copy
+import math
+import random
+from typing import Optional
+
+import torch
+import torch.nn as nn
+from torch import Tensor
+
+from .. import functional as fxf
+
+
+def _as3d(t2d):
+    return t2d.unsqueeze(1)
+
+
+def _no_fused_dropout(module, p, where):
+    if module.training and p > 0:
+        raise NotImplementedError(f"dropout={p} inside the fused {where} kernel is not implemented; "
+                                  "use dropout 0 (parity/benchmark configs do)")
+
+
+def _dropout(x, p, training):
+    return torch.nn.functional.dropout(x, p, training) if (training and p > 0) else x
+
+
+def time_mask(feature, T, num_masks, p, replace_with_zero=False, clone=False):
+    """basic.py:10-36 (training augmentation, host RNG; torch ops on the device tensor)."""
+    if clone:
+        feature = feature.clone()
+    n = feature.shape[0]
+    for _ in range(num_masks):
+        t = min(int(p * n), random.randrange(0, T))
+        t0 = random.randrange(0, n - t)
+        if t0 == t0 + t:
+            return feature
+        feature[t0:t0 + t] = 0 if replace_with_zero else feature.mean()
+    return feature
+
+
+def torch_class_label_to_segment_label(label):
+    """basic.py:38-54, vectorised on the label's device (no per-frame host sync)."""
+    change = torch.ones_like(label, dtype=torch.bool)
+    change[1:] = label[1:] != label[:-1]
+    segment_label = torch.cumsum(change.to(torch.int64), 0) - 1
+    transcript = label[change]
+    return transcript.to(torch.int64), segment_label.to(label.dtype)
+
+
+def logit2prob(clogit, dim=-1, class_sep=None):
+    """basic.py:56-65."""
+    if class_sep is None or class_sep <= 0:
+        return torch.softmax(clogit, dim=dim)
+    return torch.cat([torch.softmax(clogit[..., :class_sep], dim=dim),
+                      torch.softmax(clogit[..., class_sep:], dim=dim)], dim=dim)
+
+
+class PositionalEncoding(nn.Module):
+    """basic.py:67-129: sinusoid table buffer ``pe`` (max_len, 1, d), zeros when ``empty``."""
+
+    def __init__(self, d_model, max_len=5000, empty=False):
+        super().__init__()
+        self.d_model = d_model
+        self.max_len = max_len
+        self.empty = empty
+        self._build(d_model, max_len)
+
+    def _build(self, d_model, max_len):
+        pe = torch.zeros(max_len, d_model)
+        if not self.empty:
+            pos = torch.arange(0, max_len, dtype=torch.float).unsqueeze(1)
+            div = torch.exp(torch.arange(0, d_model, 2).float() * (-math.log(10000.0) / d_model))
+            pe[:, 0::2] = torch.sin(pos * div)
+            pe[:, 1::2] = torch.cos(pos * div)
+        self.register_buffer("pe", pe.unsqueeze(1))
+
+    def __repr__(self):
+        return "PositionalEncoding(EMPTY)" if self.empty else f"PositionalEncoding(Dim={self.d_model}, MaxLen={self.max_len})"
+
+    def forward(self, x):
+        if x.size(0) > self.pe.shape[0]:
+            dev = self.pe.device
+            self._build(self.d_model, x.size(0) + 10)
+            self.pe = self.pe.to(dev)
+        return self.pe[:x.size(0), :]
+
+
+def add_positional_encoding(tensor, pos):
+    """basic.py:313-320 (pos added to the first d channels)."""
+    if pos is None:
+        return tensor
+    d = pos.size(-1)
+    if pos.dim() != tensor.dim():          # (N,1,d) positions against a (N,C) working tensor
+        pos = pos.reshape(*tensor.shape[:-1], d)
+    tensor = tensor.clone()
+    tensor[..., :d] = tensor[..., :d] + pos
+    return tensor
+
+
+def _pos_or_none(pe_module_or_tensor):
+    return pe_module_or_tensor
+
+
+class DilatedResidualLayer(nn.Module):
+    """basic.py:131-171; forward runs the one-layer fused MS-TCN kernel path."""
+
+    def __init__(self, dilation, nchannels, dropout=0.5, layernorm=True, layernorm_eps=1e-5, ngroup=1):
+        super().__init__()
+        if ngroup != 1:
+            raise NotImplementedError("grouped dilated conv (f_ngp != 1) is not implemented")
+        self.dilation = dilation
+        self.nchannels = nchannels
+        self.dropout_rate = dropout
+        self.conv_dilated = nn.Conv1d(nchannels, nchannels, 3, padding=dilation, dilation=dilation, groups=ngroup)
+        self.conv_1x1 = nn.Conv1d(nchannels, nchannels, 1)
+        self.dropout = nn.Dropout(dropout)
+        self.use_layernorm = layernorm
+        self.norm = nn.LayerNorm(nchannels, eps=layernorm_eps) if layernorm else None
+
+    def __repr__(self):
+        return (f"DilatedResidualLayer(Conv(d={self.dilation},h={self.nchannels}), 1x1(h={self.nchannels}), "
+                f"Dropout={self.dropout_rate}, ln={self.use_layernorm})")
+
+    def forward(self, x, mask=None):
+        """x: (B=1, C, T) as in the reference."""
+        assert mask is None
+        _no_fused_dropout(self, self.dropout_rate, "dilated residual layer")
+        T = x.shape[-1]
+        h = x[0].t().contiguous()
+        z = fxf.conv3(h, self.conv_dilated.weight, self.conv_dilated.bias, self.dilation, T)
+        z = torch.relu(z)
+        y = fxf.linear(z, self.conv_1x1.weight, self.conv_1x1.bias) + h
+        if self.norm is not None:
+            y = fxf.layer_norm(y, self.norm.weight, self.norm.bias, self.norm.eps)
+        return y.t().unsqueeze(0)
+
+
+class MSTCN(nn.Module):
+    """basic.py:173-220; the whole stack is one fused HIP call (fx_mstcn_fwd/bwd)."""
+
+    def __init__(self, in_dim, hid_dim, out_dim, num_layers, dropout=0.5, dilation_factor=2, ln=True, ngroup=1,
+                 in_map=False):
+        super().__init__()
+        if in_map:
+            self.conv_1x1 = nn.Conv1d(in_dim, hid_dim, 1)
+        else:
+            assert in_dim == hid_dim
+        self.layers = nn.ModuleList([DilatedResidualLayer(dilation_factor ** i, hid_dim, dropout, layernorm=ln,
+                                                          ngroup=ngroup) for i in range(num_layers)])
+        self.conv_out = nn.Conv1d(hid_dim, out_dim, 1)
+        self.in_dim, self.hid_dim, self.out_dim = in_dim, hid_dim, out_dim
+        self.in_map = in_map
+        self.num_layers = num_layers
+        self.dropout_rate = dropout
+        self.dilation_factor = dilation_factor
+        self.dilation0 = 1
+        self.string = (f"MSTCN(h:{in_dim}->{hid_dim}x{num_layers}->{out_dim}, d={dilation_factor}, ng={ngroup}, "
+                       f"dropout={dropout}, in_map={in_map})")
+
+    def __repr__(self):
+        return self.string
+
+    def forward(self, x, mask=None):
+        """x: (T, 1, C) -> (T, 1, out_dim)."""
+        assert mask is None
+        _no_fused_dropout(self, self.dropout_rate, "MS-TCN")
+        out = fxf.mstcn(self, x, T=x.shape[0])
+        self.output = _as3d(out)
+        return self.output
+
+
+class MSTCN2(nn.Module):
+    """basic.py:222-281 (MS-TCN++): dual-dilation implicit-GEMM convs, 1x1 fusion, ReLU, residual."""
+
+    def __init__(self, dim, num_f_maps, out_dim, num_layers, dropout=0.5, dilation_factor=2, ngroup=1, ln=False,
+                 in_map=True):
+        super().__init__()
+        assert ln is False or ln == 0
+        if ngroup != 1:
+            raise NotImplementedError("grouped dilated conv (f_ngp != 1) is not implemented")
+        self.num_layers = num_layers
+        self.in_map = in_map
+        if in_map:
+            self.conv_1x1_in = nn.Conv1d(dim, num_f_maps, 1)
+        else:
+            assert dim == num_f_maps
+        self.conv_dilated_1 = nn.ModuleList(
+            nn.Conv1d(num_f_maps, num_f_maps, 3, padding=dilation_factor ** (num_layers - 1 - i),
+                      dilation=dilation_factor ** (num_layers - 1 - i), groups=ngroup) for i in range(num_layers))
+        self.conv_dilated_2 = nn.ModuleList(
+            nn.Conv1d(num_f_maps, num_f_maps, 3, padding=dilation_factor ** i, dilation=dilation_factor ** i,
+                      groups=ngroup) for i in range(num_layers))
+        self.conv_fusion = nn.ModuleList(nn.Conv1d(2 * num_f_maps, num_f_maps, 1) for _ in range(num_layers))
+        self.dropout = nn.Dropout(dropout)
+        self.conv_out = nn.Conv1d(num_f_maps, out_dim, 1)
+        self.dilation_factor = dilation_factor
+        self.string = (f"MSTCN2(h:{dim}->{num_f_maps}x{num_layers}->{out_dim}, d={dilation_factor}, ng={ngroup}, "
+                       f"dropout={dropout}, in_map={in_map})")
+
+    def __repr__(self):
+        return self.string
+
+    def forward(self, x):
+        T = x.shape[0]
+        f = fxf.linear(x, self.conv_1x1_in.weight, self.conv_1x1_in.bias) if self.in_map else fxf._2d(x)
+        L = self.num_layers
+        for i in range(L):
+            f_in = f
+            a = fxf.conv3(f, self.conv_dilated_1[i].weight, self.conv_dilated_1[i].bias,
+                          self.dilation_factor ** (L - 1 - i), T)
+            b = fxf.conv3(f, self.conv_dilated_2[i].weight, self.conv_dilated_2[i].bias, self.dilation_factor ** i, T)
+            f = fxf.linear(torch.cat([a, b], 1), self.conv_fusion[i].weight, self.conv_fusion[i].bias, relu=True)
+            if i != L - 1:
+                f = _dropout(f, self.dropout.p, self.training)
+            f = f + f_in
+        return _as3d(fxf.linear(f, self.conv_out.weight, self.conv_out.bias))
+
+
+class ActionUpdate_GRU(nn.Module):
+    """basic.py:283-308 (transcript-conditioned action branch; not on the FACT_CLIP path)."""
+
+    def __init__(self, in_dim, hid_dim, out_dim, n_layers, dropout=0.5, layer_norm_eps=1e-5, out_map=False):
+        super().__init__()
+        self.in_dim, self.hid_dim, self.n_layers = in_dim, hid_dim, n_layers
+        self.gru = nn.GRU(in_dim, hid_dim // 2, n_layers, dropout=dropout, bidirectional=True)
+        self.layernorm = nn.LayerNorm(hid_dim, eps=layer_norm_eps)
+        if out_map:
+            self.out_map = nn.Linear(hid_dim, out_dim)
+        else:
+            assert hid_dim == out_dim
+            self.out_map = nn.Identity()
+
+    def forward(self, tgt, memory, pos=None, query_pos=None):
+        out, _ = self.gru(tgt)
+        out = _as3d(fxf.layer_norm(out, self.layernorm.weight, self.layernorm.bias, self.layernorm.eps))
+        if isinstance(self.out_map, nn.Linear):
+            out = _as3d(fxf.linear(out, self.out_map.weight, self.out_map.bias))
+        return out
+
+
+def _get_clones(module, N):
+    return nn.ModuleList([copy.deepcopy(module) for _ in range(N)])
+
+
+class X2Y_map(nn.Module):
+    """basic.py:335-389: single-head cross attention; fused fx_x2y_fwd/bwd."""
+
+    def __init__(self, x_dim, y_dim, y_outdim, head_dim, dropout=0.5, kq_pos=False):
+        super().__init__()
+        self.kq_pos = kq_pos
+        self.X_K = nn.Linear(x_dim, head_dim)
+        self.X_V = nn.Linear(x_dim, head_dim)
+        self.Y_Q = nn.Linear(y_dim, head_dim)
+        self.Y_W = nn.Linear(y_dim + head_dim, y_outdim)
+        self.dropout = nn.Dropout(dropout)
+
+    def forward(self, X_feature, Y_feature, X_pos=None, Y_pos=None, X_pad_mask=None, Y_pad_mask=None):
+        assert X_pad_mask is None and Y_pad_mask is None
+        _no_fused_dropout(self, self.dropout.p, "X2Y concat")
+        xp = X_pos if (X_pos is not None and self.kq_pos) else None
+        yp = Y_pos if (Y_pos is not None and self.kq_pos) else None
+        out, logit, attn = fxf.x2y(self, X_feature, Y_feature, xp, yp)
+        self.attn_logit = logit.unsqueeze(0)          # (B=1, Y, X)
+        self.attn = attn.unsqueeze(0).unsqueeze(1)    # (B=1, nhead=1, Y, X)
+        return _as3d(out)
+
+
+class SALayer(nn.Module):
+    """basic.py:391-452: self attention + FFN, post-norm."""
+
+    def __init__(self, q_dim, nhead, dim_feedforward=2048, kv_dim=None, dropout=0.1, attn_dropout=0.1,
+                 activation="relu", vpos=False):
+        super().__init__()
+        if activation != "relu":
+            raise NotImplementedError(activation)
+        kv_dim = q_dim if kv_dim is None else kv_dim
+        self.multihead_attn = nn.MultiheadAttention(q_dim, nhead, kdim=kv_dim, vdim=kv_dim, dropout=attn_dropout)
+        self.linear1 = nn.Linear(q_dim, dim_feedforward)
+        self.dropout = nn.Dropout(dropout)
+        self.linear2 = nn.Linear(dim_feedforward, q_dim)
+        self.norm1 = nn.LayerNorm(q_dim)
+        self.norm2 = nn.LayerNorm(q_dim)
+        self.dropout1 = nn.Dropout(dropout)
+        self.dropout2 = nn.Dropout(dropout)
+        self.q_dim, self.kv_dim, self.nhead, self.dim_feedforward = q_dim, kv_dim, nhead, dim_feedforward
+        self.use_vpos = vpos
+        self.dropout_rate = (dropout, attn_dropout)
+
+    def __repr__(self):
+        return (f"SALayer( q({self.q_dim})xkv({self.kv_dim})->{self.q_dim}, head:{self.nhead}, "
+                f"ffdim:{self.dim_feedforward}, dropout:{self.dropout_rate}, vpos:{self.use_vpos} )")
+
+    def forward(self, tgt, key, value, query_pos: Optional[Tensor] = None, key_pos: Optional[Tensor] = None,
+                value_pos: Optional[Tensor] = None):
+        _no_fused_dropout(self, self.multihead_attn.dropout, "attention")
+        query = add_positional_encoding(tgt, query_pos)
+        key = add_positional_encoding(key, key_pos)
+        if self.use_vpos:
+            value = add_positional_encoding(value, value_pos)
+        t2 = fxf.mha(self.multihead_attn, query, key, value)
+        t2 = _dropout(t2, self.dropout1.p, self.training)
+        t = fxf.layer_norm(t2, self.norm1.weight, self.norm1.bias, self.norm1.eps, residual=tgt)
+        h = fxf.linear(t, self.linear1.weight, self.linear1.bias, relu=True)
+        h = _dropout(h, self.dropout.p, self.training)
+        t2 = _dropout(fxf.linear(h, self.linear2.weight, self.linear2.bias), self.dropout2.p, self.training)
+        return _as3d(fxf.layer_norm(t2, self.norm2.weight, self.norm2.bias, self.norm2.eps, residual=t))
+
+
+class SCALayer(nn.Module):
+    """basic.py:454-523: self attention over action tokens, cross attention onto frames, FFN."""
+
+    def __init__(self, action_dim, frame_dim, nhead, dim_feedforward=2048, dropout=0.1, attn_dropout=0.1,
+                 activation="relu", normalize_before=False, sa_value_w_pos=False, ca_value_w_pos=False):
+        super().__init__()
+        if activation != "relu":
+            raise NotImplementedError(activation)
+        self.self_attn = nn.MultiheadAttention(action_dim, nhead, dropout=attn_dropout)
+        self.multihead_attn = nn.MultiheadAttention(action_dim, nhead, kdim=frame_dim, vdim=frame_dim,
+                                                    dropout=attn_dropout)
+        self.linear1 = nn.Linear(action_dim, dim_feedforward)
+        self.dropout = nn.Dropout(dropout)
+        self.linear2 = nn.Linear(dim_feedforward, action_dim)
+        self.norm1 = nn.LayerNorm(action_dim)
+        self.norm2 = nn.LayerNorm(action_dim)
+        self.norm3 = nn.LayerNorm(action_dim)
+        self.dropout1 = nn.Dropout(dropout)
+        self.dropout2 = nn.Dropout(dropout)
+        self.dropout3 = nn.Dropout(dropout)
+        self.normalize_before = normalize_before
+        assert not normalize_before
+        self.sa_value_w_pos = sa_value_w_pos
+        self.ca_value_w_pos = ca_value_w_pos
+        self.string = (f"SCALayer( adim:{action_dim}, fdim:{frame_dim}, head:{nhead}, ffdim:{dim_feedforward}, "
+                       f"dropout:{(dropout, attn_dropout)}, svpos:{sa_value_w_pos}, cvpos:{ca_value_w_pos} )")
+
+    def __repr__(self):
+        return self.string
+
+    def forward(self, tgt, memory, pos: Optional[Tensor] = None, query_pos: Optional[Tensor] = None):
+        _no_fused_dropout(self, self.self_attn.dropout, "attention")
+        q = add_positional_encoding(tgt, query_pos)
+        t2 = fxf.mha(self.self_attn, q, q, q if self.sa_value_w_pos else tgt)
+        t = fxf.layer_norm(_dropout(t2, self.dropout1.p, self.training), self.norm1.weight, self.norm1.bias,
+                           self.norm1.eps, residual=tgt)
+        query = add_positional_encoding(t, query_pos)
+        key = add_positional_encoding(memory, pos)
+        t2 = fxf.mha(self.multihead_attn, query, key, key if self.ca_value_w_pos else memory)
+        t = fxf.layer_norm(_dropout(t2, self.dropout2.p, self.training), self.norm2.weight, self.norm2.bias,
+                           self.norm2.eps, residual=t)
+        h = _dropout(fxf.linear(t, self.linear1.weight, self.linear1.bias, relu=True), self.dropout.p, self.training)
+        t2 = _dropout(fxf.linear(h, self.linear2.weight, self.linear2.bias), self.dropout3.p, self.training)
+        return _as3d(fxf.layer_norm(t2, self.norm3.weight, self.norm3.bias, self.norm3.eps, residual=t))
+
+
+class SCADecoder(nn.Module):
+    """basic.py:525-557."""
+
+    def __init__(self, in_dim, hid_dim, out_dim, decoder_layer, num_layers, norm=None, in_map=False):
+        super().__init__()
+        self.in_map = in_map
+        if in_map:
+            self.in_linear = nn.Linear(in_dim, hid_dim)
+        else:
+            assert hid_dim == in_dim
+        self.layers = _get_clones(decoder_layer, num_layers)
+        self.out_linear = nn.Linear(hid_dim, out_dim)
+        self.num_layers = num_layers
+        self.norm = norm
+
+    def forward(self, tgt, memory, pos: Optional[Tensor] = None, query_pos: Optional[Tensor] = None):
+        out = _as3d(fxf.linear(tgt, self.in_linear.weight, self.in_linear.bias)) if self.in_map else tgt
+        for layer in self.layers:
+            out = layer(out, memory, pos=pos, query_pos=query_pos)
+        if self.norm is not None:
+            out = fxf.layer_norm(out, self.norm.weight, self.norm.bias, self.norm.eps)
+        return _as3d(fxf.linear(out, self.out_linear.weight, self.out_linear.bias))
+
+
+class SADecoder(nn.Module):
+    """basic.py:561-593."""
+
+    def __init__(self, in_dim, hid_dim, out_dim, decoder_layer, num_layers, norm=None, in_map=False):
+        super().__init__()
+        self.in_map = in_map
+        if in_map:
+            self.in_linear = nn.Linear(in_dim, hid_dim)
+        else:
+            assert in_dim == hid_dim
+        self.layers = _get_clones(decoder_layer, num_layers)
+        self.out_linear = nn.Linear(hid_dim, out_dim)
+        self.num_layers = num_layers
+        self.norm = norm
+
+    def forward(self, tgt, pos: Optional[Tensor] = None):
+        out = _as3d(fxf.linear(tgt, self.in_linear.weight, self.in_linear.bias)) if self.in_map else tgt
+        for layer in self.layers:
+            out = layer(out, out, out, query_pos=pos, key_pos=pos, value_pos=pos)
+        if self.norm is not None:
+            out = fxf.layer_norm(out, self.norm.weight, self.norm.bias, self.norm.eps)
+        return _as3d(fxf.linear(out, self.out_linear.weight, self.out_linear.bias))
+
+
+class Segment:
+    """utils/utils.py:4-23 (host view of one run)."""
+
+    def __init__(self, action, start, end):
+        assert start >= 0
+        self.action, self.start, self.end = action, start, end
+        self.len = end - start + 1
+
+    def __repr__(self):
+        return "<%r %d-%d>" % (self.action, self.start, self.end)
+
+
+class TemporalDownsampleUpsample:
+    """basic.py:595-651 with device-resident segment tables.
+
+    ``from_probs`` builds it from frame probabilities with the HIP argmax +
+    boundary-scan kernels (bit-exact run-length encoding of the argmax); the
+    host sees only S.  ``seg_label`` / ``seg_lens`` are int64 device tensors as
+    in the reference; ``segs`` materialises the Segment list lazily."""
+
+    def __init__(self, seg_id, starts, ends, pred=None):
+        self.seg_id32 = seg_id
+        self.start32, self.end32 = starts, ends
+        self.num_seg = int(starts.shape[0])
+        self.seg_label = seg_id.to(torch.int64)
+        self.seg_lens = (ends - starts + 1).to(torch.int64)
+        self._pred = pred
+        self._segs = None
+
+    @classmethod
+    def from_probs(cls, frame2d, col0, ncls):
+        S, seg_id, st, en = fxf.segments_from_probs(frame2d, col0, ncls)
+        return cls(seg_id, st, en)
+
+    @property
+    def segs(self):
+        if self._segs is None:
+            st = self.start32.cpu().tolist()
+            en = self.end32.cpu().tolist()
+            self._segs = [Segment(None, s, e) for s, e in zip(st, en)]
+        return self._segs
+
+    def cuda(self):
+        return self
+
+    def to(self, device):
+        return self
+
+    def centers(self):
+        return torch.div(self.start32 + self.end32, 2, rounding_mode="floor").to(torch.int64)
+
+    def feature_frame2seg(self, frame_feature, normalize=True):
+        assert normalize
+        return _as3d(fxf.SegMeanFn.apply(fxf._2d(frame_feature), self.seg_id32, self.start32, self.end32))
+
+    def attn_frame2seg(self, frame_attn):
+        b, f, a = frame_attn.shape
+        out = torch.zeros(b, self.num_seg, a, device=frame_attn.device, dtype=frame_attn.dtype)
+        out.index_add_(1, self.seg_label, frame_attn)
+        return out / self.seg_lens[:, None]
+
+    def feature_seg2frame(self, seg_feature):
+        return seg_feature[self.seg_label]
+
+    def attn_seg2frame(self, seg_attn):
+        assert seg_attn.shape[0] == 1
+        return seg_attn[0, self.seg_label].unsqueeze(0)

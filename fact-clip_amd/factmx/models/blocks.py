@@ -1,0 +1,435 @@
+"""FACT / FACT_CLIP with the reference's Python surface (fact_clip/models/blocks.py).
+
+Same constructors, attribute names read by losses / eval / scripts
+(``frame_clogit``, ``action_clogit``, ``a2f_attn``, ``f2a_attn``,
+``*_attn_logit``, ``seg_clogit``, ``tdu``, ``action_feature``,
+``projected_frame_embeddings``, ``fact_loss``, ``contrastive_loss``),
+state_dict keys and ``forward(seq_list, label_list, compute_loss)``
+contract.  Compute runs on the HIP kernels through factmx.functional.
+"""
+import torch
+import torch.nn as nn
+
+from .. import functional as fxf
+from ..configs.utils import update_from
+from ..utils import utils
+from . import basic
+from . import loss as loss_mod
+from .basic import time_mask, torch_class_label_to_segment_label
+from .loss import MatchCriterion
+
+
+def _frame_pos(pe_module, seq):
+    """frame_pe(seq) (blocks.py:59/613); None when the table is empty (fpos=False), which is
+    numerically identical to adding zeros and lets the kernels skip the add."""
+    return None if pe_module.empty else pe_module(seq)
+
+
+class FeatureProjection(nn.Module):
+    """blocks.py:141-175: Linear -> LayerNorm -> ReLU -> Dropout -> Linear -> L2-normalise."""
+
+    def __init__(self, feature_dim, clip_dim=512, hidden_dim=512, dropout=0.1):
+        super().__init__()
+        self.feature_dim = feature_dim
+        self.clip_dim = clip_dim
+        self.projection = nn.Sequential(nn.Linear(feature_dim, hidden_dim), nn.LayerNorm(hidden_dim), nn.ReLU(),
+                                        nn.Dropout(dropout), nn.Linear(hidden_dim, clip_dim))
+
+    def forward(self, feature):
+        lin0, ln, _, drop, lin1 = self.projection
+        shp = feature.shape
+        h = fxf.linear(feature, lin0.weight, lin0.bias)
+        h = fxf.layer_norm(h, ln.weight, ln.bias, ln.eps, relu=True)
+        h = basic._dropout(h, drop.p, self.training)
+        h = fxf.linear(h, lin1.weight, lin1.bias)
+        y = fxf.l2_normalize(h)
+        return y.reshape(*shp[:-1], self.clip_dim)
+
+
+class Block(nn.Module):
+    """blocks.py:180-281."""
+
+    def __repr__(self):
+        return (f"{type(self).__name__}(\n  f:{self.frame_branch},\n  a:{self.action_branch},\n"
+                f"  a2f:{getattr(self, 'a2f_layer', None)},\n  f2a:{getattr(self, 'f2a_layer', None)}\n)")
+
+    def process_feature(self, feature, nclass):
+        out, clogit = fxf.process_feature(feature, nclass)
+        return out.unsqueeze(1), clogit.unsqueeze(1)
+
+    def create_fbranch(self, cfg, in_dim=None, f_inmap=False):
+        if in_dim is None:
+            in_dim = cfg.f_dim
+        if cfg.f == "m":
+            return basic.MSTCN(in_dim, cfg.f_dim, cfg.hid_dim, cfg.f_layers, dropout=cfg.dropout, ln=cfg.f_ln,
+                               ngroup=cfg.f_ngp, in_map=f_inmap)
+        if cfg.f == "m2":
+            return basic.MSTCN2(in_dim, cfg.f_dim, cfg.hid_dim, cfg.f_layers, dropout=cfg.dropout, ln=cfg.f_ln,
+                                ngroup=cfg.f_ngp, in_map=f_inmap)
+        raise ValueError(f"frame branch type {cfg.f!r} (the reference builds only 'm' / 'm2')")
+
+    def create_abranch(self, cfg):
+        if cfg.a == "sa":
+            layer = basic.SALayer(cfg.a_dim, cfg.a_nhead, dim_feedforward=cfg.a_ffdim, dropout=cfg.dropout,
+                                  attn_dropout=cfg.dropout)
+            return basic.SADecoder(cfg.a_dim, cfg.a_dim, cfg.hid_dim, layer, cfg.a_layers, in_map=False)
+        if cfg.a == "sca":
+            layer = basic.SCALayer(cfg.a_dim, cfg.hid_dim, cfg.a_nhead, cfg.a_ffdim, dropout=cfg.dropout,
+                                   attn_dropout=cfg.dropout)
+            norm = torch.nn.LayerNorm(cfg.a_dim)
+            return basic.SCADecoder(cfg.a_dim, cfg.a_dim, cfg.hid_dim, layer, cfg.a_layers, norm=norm, in_map=False)
+        if cfg.a in ("gru", "gru_om"):
+            assert self.cfg.FACT.trans
+            return basic.ActionUpdate_GRU(cfg.a_dim, cfg.a_dim, cfg.hid_dim, cfg.a_layers, dropout=cfg.dropout,
+                                          out_map=(cfg.a == "gru_om"))
+        raise ValueError(cfg.a)
+
+    def create_cross_attention(self, cfg, outdim, kq_pos=True):
+        return basic.X2Y_map(cfg.hid_dim, cfg.hid_dim, outdim, head_dim=cfg.hid_dim, dropout=cfg.dropout,
+                             kq_pos=kq_pos)
+
+    @staticmethod
+    def _abranch_prob(action_clogit, a2f_attn):
+        """Per-frame class distribution of the most-attended non-null token (blocks.py:246-258)."""
+        acl = action_clogit.squeeze(1)
+        a2f = a2f_attn.squeeze(0)
+        null_cid = acl.shape[-1] - 1
+        loc = torch.nonzero(acl.argmax(1) != null_cid)[:, 0]
+        if loc.numel() == 0:
+            return None
+        qtk_prob = torch.softmax(acl[:, :-1], dim=1)
+        return qtk_prob[loc[a2f[:, loc].argmax(-1)]]
+
+    @staticmethod
+    def _eval(action_clogit, a2f_attn, frame_clogit, weight):
+        fprob = torch.softmax(frame_clogit.squeeze(1), dim=-1)
+        ab = Block._abranch_prob(action_clogit, a2f_attn)
+        if ab is None:
+            return fprob.argmax(1)
+        return ((1 - weight) * ab + weight * fprob).argmax(1)
+
+    @staticmethod
+    def _eval_w_transcript(transcript, a2f_attn, frame_clogit, weight):
+        fprob = torch.softmax(frame_clogit.squeeze(1), dim=-1)[:, transcript]
+        n = len(transcript)
+        aprob = torch.softmax(a2f_attn[0, :, :n], dim=-1)
+        return transcript[((1 - weight) * aprob + weight * fprob).argmax(1)]
+
+    def eval(self, transcript=None):
+        if not self.cfg.FACT.trans:
+            return self._eval(self.action_clogit, self.a2f_attn, self.frame_clogit, self.cfg.FACT.mwt)
+        return self._eval_w_transcript(transcript, self.a2f_attn, self.frame_clogit, self.cfg.FACT.mwt)
+
+
+class InputBlock(Block):
+    """blocks.py:284-320."""
+
+    def __init__(self, cfg, in_dim, nclass):
+        super().__init__()
+        self.cfg = cfg
+        self.nclass = nclass
+        bcfg = cfg.Bi
+        self.frame_branch = self.create_fbranch(bcfg, in_dim, f_inmap=True)
+        self.action_branch = self.create_abranch(bcfg)
+
+    def forward(self, frame_feature, action_feature, frame_pos, action_pos, action_clogit=None):
+        frame_feature = self.frame_branch(frame_feature)
+        frame_feature, frame_clogit = self.process_feature(frame_feature, self.nclass)
+        action_feature = self.action_branch(action_feature, frame_feature, pos=frame_pos, query_pos=action_pos)
+        action_feature, action_clogit = self.process_feature(action_feature, self.nclass + 1)
+        self.frame_clogit = frame_clogit
+        self.action_clogit = action_clogit
+        self.action_feature = action_feature[:, :, :-(self.nclass + 1)]
+        return frame_feature, action_feature
+
+    def compute_loss(self, criterion, match=None):
+        fl = criterion.frame_loss(self.frame_clogit.squeeze(1))
+        atk = criterion.action_token_loss(match, self.action_clogit)
+        sm = loss_mod.smooth_loss(self.frame_clogit.transpose(0, 1))
+        return fl + atk + self.cfg.Loss.sw * sm
+
+
+class UpdateBlock(Block):
+    """blocks.py:322-382."""
+
+    def __init__(self, cfg, nclass):
+        super().__init__()
+        self.cfg = cfg
+        self.nclass = nclass
+        bcfg = cfg.Bu
+        self.frame_branch = self.create_fbranch(bcfg)
+        self.f2a_layer = self.create_cross_attention(bcfg, bcfg.a_dim)
+        self.action_branch = self.create_abranch(bcfg)
+        self.a2f_layer = self.create_cross_attention(bcfg, bcfg.f_dim)
+
+    def forward(self, frame_feature, action_feature, frame_pos, action_pos):
+        action_feature = self.f2a_layer(frame_feature, action_feature, X_pos=frame_pos, Y_pos=action_pos)
+        action_feature = self.action_branch(action_feature, action_pos)
+        action_feature, action_clogit = self.process_feature(action_feature, self.nclass + 1)
+        frame_feature = self.a2f_layer(action_feature, frame_feature, X_pos=action_pos, Y_pos=frame_pos)
+        frame_feature = self.frame_branch(frame_feature)
+        frame_feature, frame_clogit = self.process_feature(frame_feature, self.nclass)
+        self.frame_clogit = frame_clogit
+        self.action_clogit = action_clogit
+        self.action_feature = action_feature[:, :, :-(self.nclass + 1)]
+        self.f2a_attn = self.f2a_layer.attn[0]
+        self.a2f_attn = self.a2f_layer.attn[0]
+        self.f2a_attn_logit = self.f2a_layer.attn_logit[0].unsqueeze(0)
+        self.a2f_attn_logit = self.a2f_layer.attn_logit[0].unsqueeze(0)
+        return frame_feature, action_feature
+
+    def compute_loss(self, criterion, match=None):
+        fl = criterion.frame_loss(self.frame_clogit.squeeze(1))
+        atk = criterion.action_token_loss(match, self.action_clogit)
+        f2a_t = self.f2a_attn_logit.transpose(1, 2)
+        f2a = criterion.cross_attn_loss(match, f2a_t, dim=1)
+        a2f = criterion.cross_attn_loss(match, self.a2f_attn_logit, dim=2)
+        sm = (loss_mod.smooth_loss(self.a2f_attn_logit) + loss_mod.smooth_loss(f2a_t)
+              + loss_mod.smooth_loss(self.frame_clogit.transpose(0, 1)))
+        return atk + f2a + a2f + fl + self.cfg.Loss.sw * sm
+
+
+class UpdateBlockTDU(Block):
+    """blocks.py:385-497: segment-level update with device-side temporal down/up-sampling."""
+
+    def __init__(self, cfg, nclass):
+        super().__init__()
+        self.cfg = cfg
+        self.nclass = nclass
+        bcfg = cfg.BU
+        self.frame_branch = self.create_fbranch(bcfg)
+        self.seg_update = nn.GRU(bcfg.hid_dim, bcfg.hid_dim // 2, bcfg.s_layers, bidirectional=True)
+        self.seg_combine = nn.Linear(bcfg.hid_dim, bcfg.hid_dim)
+        self.f2a_layer = self.create_cross_attention(bcfg, bcfg.a_dim)
+        self.action_branch = self.create_abranch(bcfg)
+        self.a2f_layer = self.create_cross_attention(bcfg, bcfg.f_dim)
+        self.sf_merge = nn.Sequential(nn.Linear(bcfg.hid_dim + bcfg.f_dim, bcfg.f_dim), nn.ReLU())
+
+    def temporal_downsample(self, frame_feature):
+        f2 = fxf._2d(frame_feature)
+        tdu = basic.TemporalDownsampleUpsample.from_probs(f2, f2.shape[1] - self.nclass, self.nclass)
+        seg = tdu.feature_frame2seg(frame_feature)
+        seg, _ = self.seg_update(seg)
+        seg = torch.relu(seg)
+        seg = fxf.linear(seg, self.seg_combine.weight, self.seg_combine.bias).unsqueeze(1)
+        seg, seg_clogit = self.process_feature(seg, self.nclass)
+        return tdu, seg, seg_clogit
+
+    def temporal_upsample(self, tdu, seg_feature, frame_feature):
+        lin = self.sf_merge[0]
+        y = fxf.SegMergeFn.apply(fxf._2d(seg_feature), fxf._2d(frame_feature), tdu.seg_id32, tdu.start32, tdu.end32,
+                                 lin.weight, lin.bias)
+        return y.unsqueeze(1)
+
+    def forward(self, frame_feature, action_feature, frame_pos, action_pos):
+        tdu, seg_feature, seg_clogit = self.temporal_downsample(frame_feature)
+        seg_pos = None if frame_pos is None else frame_pos[tdu.centers()]
+        action_feature = self.f2a_layer(seg_feature, action_feature, X_pos=seg_pos, Y_pos=action_pos)
+        action_feature = self.action_branch(action_feature, action_pos)
+        action_feature, action_clogit = self.process_feature(action_feature, self.nclass + 1)
+        seg_feature = self.a2f_layer(action_feature, seg_feature, X_pos=action_pos, Y_pos=seg_pos)
+        frame_feature = self.temporal_upsample(tdu, seg_feature, frame_feature)
+        frame_feature = self.frame_branch(frame_feature)
+        frame_feature, frame_clogit = self.process_feature(frame_feature, self.nclass)
+        self.frame_clogit = frame_clogit
+        self.seg_clogit = seg_clogit
+        self.tdu = tdu
+        self.action_clogit = action_clogit
+        self.action_feature = action_feature[:, :, :-(self.nclass + 1)]
+        self.f2a_attn_logit = self.f2a_layer.attn_logit[0].unsqueeze(0)
+        self.f2a_attn = tdu.attn_seg2frame(self.f2a_layer.attn[0].transpose(2, 1)).transpose(2, 1)
+        self.a2f_attn_logit = self.a2f_layer.attn_logit[0].unsqueeze(0)
+        self.a2f_attn = tdu.attn_seg2frame(self.a2f_layer.attn[0])
+        return frame_feature, action_feature
+
+    def compute_loss(self, criterion, match=None):
+        fl = criterion.frame_loss(self.frame_clogit.squeeze(1))
+        sl = criterion.frame_loss_tdu(self.seg_clogit, self.tdu)
+        atk = criterion.action_token_loss(match, self.action_clogit)
+        f2a = criterion.cross_attn_loss_tdu(match, self.f2a_attn_logit.transpose(1, 2), self.tdu, dim=1)
+        a2f = criterion.cross_attn_loss_tdu(match, self.a2f_attn_logit, self.tdu, dim=2)
+        sm = loss_mod.smooth_loss(self.frame_clogit.transpose(0, 1))
+        return (fl + sl) / 2 + atk + f2a + a2f + self.cfg.Loss.sw * sm
+
+
+def _build_blocks(cfg, in_dim, n_classes):
+    base = cfg.Bi
+    blocks = []
+    for t in cfg.FACT.block:
+        if t == "i":
+            blocks.append(InputBlock(cfg, in_dim, n_classes))
+        elif t == "u":
+            update_from(cfg.Bu, base, inplace=True)
+            base = cfg.Bu
+            blocks.append(UpdateBlock(cfg, n_classes))
+        elif t == "U":
+            update_from(cfg.BU, base, inplace=True)
+            base = cfg.BU
+            blocks.append(UpdateBlockTDU(cfg, n_classes))
+        else:
+            raise ValueError(t)
+    return nn.ModuleList(blocks)
+
+
+class _FACTBase(nn.Module):
+    def _init_common(self, cfg, n_classes):
+        self.cfg = cfg
+        self.num_classes = n_classes
+        bcfg = cfg.Bi
+        self.frame_pe = basic.PositionalEncoding(bcfg.hid_dim, max_len=10000, empty=(not cfg.FACT.fpos))
+        self.channel_masking_dropout = nn.Dropout2d(p=cfg.FACT.cmr)
+        if not cfg.FACT.trans:
+            self.action_query = nn.Parameter(torch.randn([cfg.FACT.ntoken, 1, bcfg.a_dim]))
+        else:
+            self.action_pe = basic.PositionalEncoding(bcfg.a_dim, max_len=1000)
+            self.action_embed = nn.Embedding(n_classes, bcfg.a_dim)
+
+    def _run_blocks(self, seq, transcript):
+        frame_feature = seq
+        frame_pe = _frame_pos(self.frame_pe, seq)
+        if self.cfg.FACT.cmr and self.training:
+            frame_feature = self.channel_masking_dropout(frame_feature.permute([1, 2, 0])).permute([2, 0, 1])
+        if self.cfg.TM.use and self.training:
+            frame_feature = time_mask(frame_feature, self.cfg.TM.t, self.cfg.TM.m, self.cfg.TM.p,
+                                      replace_with_zero=True)
+        if not self.cfg.FACT.trans:
+            action_pe = self.action_query
+            action_feature = torch.zeros_like(action_pe)
+        else:
+            action_pe = self.action_pe(transcript)
+            action_feature = self.action_embed(transcript).unsqueeze(1) + action_pe
+            action_pe = torch.zeros_like(action_pe)
+        block_output = []
+        for block in self.block_list:
+            frame_feature, action_feature = block(frame_feature, action_feature, frame_pe, action_pe)
+            block_output.append([frame_feature, action_feature])
+        return block_output
+
+    def _fact_loss(self, label):
+        mc: MatchCriterion = self.mcriterion
+        mc.set_label(label)
+        last = self.block_list[-1]
+        match = mc.match(basic.logit2prob(last.action_clogit, dim=-1), last.a2f_attn)
+        self.loss_list = [blk.compute_loss(mc, match) for blk in self.block_list]
+        return sum(self.loss_list) / len(self.loss_list)
+
+    def save_model(self, fname):
+        torch.save(self.state_dict(), fname)
+
+
+class FACT(_FACTBase):
+    """blocks.py:19-135 (vanilla FACT)."""
+
+    def __init__(self, cfg, in_dim, n_classes):
+        super().__init__()
+        self._init_common(cfg, n_classes)
+        self.block_list = _build_blocks(cfg, in_dim, n_classes)
+        self.mcriterion = None
+
+    def _forward_one_video(self, seq, transcript=None):
+        return self._run_blocks(seq, transcript)
+
+    def _loss_one_video(self, label):
+        return self._fact_loss(label)
+
+    def forward(self, seq_list, label_list, compute_loss=False):
+        save_list, losses = [], []
+        for seq, label in zip(seq_list, label_list):
+            trans = torch_class_label_to_segment_label(label)[0]
+            self._forward_one_video(seq.unsqueeze(1), trans)
+            save = {"pred": utils.to_numpy(self.block_list[-1].eval(trans))}
+            save_list.append(save)
+            if compute_loss:
+                lo = self._loss_one_video(label)
+                losses.append(lo)
+                save["loss"] = {"loss": lo.item()}
+        if compute_loss:
+            return sum(losses) / len(losses), save_list
+        return save_list
+
+
+class FACT_CLIP(_FACTBase):
+    """blocks.py:504-920: FACT + CLIP projection head + InfoNCE; zero-shot eval via text similarity."""
+
+    def __init__(self, cfg, in_dim, n_classes, text_embeddings=None):
+        super().__init__()
+        self._init_common(cfg, n_classes)
+        # feature width from Bi.hid_dim, evaluated before the block loop (blocks.py:568)
+        frame_feature_dim = cfg.Bi.hid_dim - n_classes
+        self.frame_projection = FeatureProjection(feature_dim=frame_feature_dim, clip_dim=512,
+                                                  hidden_dim=cfg.CLIP.projection_hidden_dim,
+                                                  dropout=cfg.CLIP.projection_dropout)
+        if text_embeddings is not None:
+            self.register_buffer("text_embeddings", text_embeddings)
+        else:
+            self.text_embeddings = None
+        self.block_list = _build_blocks(cfg, in_dim, n_classes)
+        self.mcriterion = None
+
+    def _forward_one_video(self, seq, transcript=None):
+        out = self._run_blocks(seq, transcript)
+        frame_feature = out[-1][0]
+        feat_dim = frame_feature.shape[-1] - self.num_classes
+        self.projected_frame_embeddings = self.frame_projection(frame_feature[:, :, :feat_dim])
+        return out
+
+    def _loss_one_video(self, label):
+        fact_loss = self._fact_loss(label)
+        if self.text_embeddings is None or not hasattr(self, "projected_frame_embeddings"):
+            return fact_loss
+        mc = self.mcriterion
+        text = self.text_embeddings
+        labels = mc.class_label
+        emb = self.projected_frame_embeddings
+        hold = list(getattr(self.cfg, "holdout_classes", []) or [])
+        if hold:
+            n = text.shape[0]
+            seen = torch.tensor([i for i in range(n) if i not in set(hold)], device=text.device)
+            text = text[seen]
+            remap = torch.full((n,), -1, device=text.device, dtype=torch.long)
+            remap[seen] = torch.arange(len(seen), device=text.device)
+            labels = remap[labels]
+            valid = labels != -1
+            if not bool(valid.all()):
+                if int(valid.sum()) == 0:
+                    return fact_loss
+                labels = labels[valid]
+                emb = emb.reshape(-1, emb.shape[-1])[valid].unsqueeze(1)
+        con = loss_mod.infonce_contrastive_loss(emb, text, labels, temperature=self.cfg.CLIP.temp)
+        total = self.cfg.CLIP.fact_loss_weight * fact_loss + self.cfg.CLIP.contrastive_weight * con
+        self.fact_loss = fact_loss
+        self.contrastive_loss = con
+        return total
+
+    def eval_with_clip(self, transcript=None):
+        """blocks.py:788-887."""
+        if self.text_embeddings is None or not hasattr(self, "projected_frame_embeddings"):
+            return self.block_list[-1].eval(transcript)
+        emb = self.projected_frame_embeddings.squeeze(1)
+        clip_prob = torch.softmax(emb @ self.text_embeddings.t() / self.cfg.CLIP.temp, dim=-1)
+        last = self.block_list[-1]
+        ab = Block._abranch_prob(last.action_clogit, last.a2f_attn)
+        if ab is None:
+            return clip_prob.argmax(1)
+        w = self.cfg.FACT.mwt
+        return ((1 - w) * ab + w * clip_prob).argmax(1)
+
+    def forward(self, seq_list, label_list, compute_loss=False):
+        save_list, losses = [], []
+        for seq, label in zip(seq_list, label_list):
+            trans = torch_class_label_to_segment_label(label)[0]
+            self._forward_one_video(seq.unsqueeze(1), trans)
+            save = {"pred": utils.to_numpy(self.eval_with_clip(trans))}
+            save_list.append(save)
+            if compute_loss:
+                lo = self._loss_one_video(label)
+                losses.append(lo)
+                ld = {"loss": lo.item()}
+                if hasattr(self, "fact_loss"):
+                    ld["fact_loss"] = self.fact_loss.item()
+                if hasattr(self, "contrastive_loss"):
+                    ld["contrastive_loss"] = self.contrastive_loss.item()
+                save["loss"] = ld
+        if compute_loss:
+            return sum(losses) / len(losses), save_list
+        return save_list

@@ -1,0 +1,188 @@
+"""Matching and losses with the reference's surface (fact_clip/models/loss.py).
+
+Label bookkeeping is vectorised on the label's device (the reference loops over
+frames in Python).  The Hungarian assignment stays on the host (scipy, as in
+the reference); its cost matrix (tokens x GT segments) is built on the device
+and copied once.  Loss arithmetic runs as device tensor ops; fusing it into
+HIP kernels is the next step on the roadmap.
+"""
+import numpy as np
+import torch
+import torch.nn.functional as F
+from scipy.optimize import linear_sum_assignment
+
+from . import basic
+from .basic import torch_class_label_to_segment_label, logit2prob  # noqa: F401  (re-exported like loss.py:20,38)
+
+
+def smooth_loss(logit, is_logit=True):
+    """loss.py:8-18: mean of clamp((d/dt log_softmax)^2, 0, 16) over (B, T-1, C)."""
+    lp = F.log_softmax(logit, dim=2) if is_logit else logit
+    step = lp[:, 1:] - lp[:, :-1]
+    return torch.clamp(step * step, min=0, max=16).mean()
+
+
+def _onehot(idx, n):
+    return F.one_hot(idx.to(torch.int64), n).to(torch.float32)
+
+
+def _zoom(tdu, onehot):
+    """Mean of a frame-level (T, K) table over each TDU segment -> (S, K)."""
+    z = torch.zeros(tdu.num_seg, onehot.shape[1], dtype=onehot.dtype, device=onehot.device)
+    z.index_add_(0, tdu.seg_label, onehot)
+    return z / tdu.seg_lens[:, None]
+
+
+def _weighted_xent(logits, target, weight):
+    """Mean cross-entropy with class weights: sum w[y] * nll / sum w[y] (F.cross_entropy semantics)."""
+    return F.cross_entropy(logits, target, weight=weight)
+
+
+class MatchCriterion:
+    """loss.py:49-277."""
+
+    def __init__(self, cfg, nclasses, bg_ids=[], class_weight=None):
+        self.cfg = cfg
+        self.nclasses = nclasses
+        self.bg_ids = list(bg_ids) if bg_ids is not None else []
+        self._class_weight = class_weight
+
+    def set_label(self, label):
+        self.class_label = label
+        self.transcript, self.seg_label = torch_class_label_to_segment_label(label)
+        self.onehot_class_label = _onehot(label, self.nclasses)
+        self.onehot_seg_label = _onehot(self.seg_label, len(self.transcript))
+        dev = label.device
+        cw = torch.ones(self.nclasses + 1, device=dev)
+        cw[-1] = self.cfg.Loss.nullw
+        sw = torch.ones(len(self.transcript), dtype=torch.float32, device=dev)
+        if self._class_weight is not None:
+            cw[:self.nclasses] = torch.as_tensor(self._class_weight[:self.nclasses], dtype=torch.float32, device=dev)
+            sw = torch.as_tensor(self._class_weight, dtype=torch.float32, device=dev)[self.transcript]
+        else:
+            for i in self.bg_ids:
+                cw[i] = self.cfg.Loss.bgw
+                sw[self.transcript == i] = self.cfg.Loss.bgw
+        self.cweight, self.sweight = cw, sw
+
+    def _label_to_onehot(self, label, nclass):
+        return _onehot(label, nclass)
+
+    @classmethod
+    def a2f_soft_iou(cls, a2f_attn, onehot_seg_label):
+        """loss.py:91-106 on the device: overlap / sum_t min(attn + onehot, 1)."""
+        a = a2f_attn[0]                                      # (T, A)
+        overlap = a.t() @ onehot_seg_label                   # (A, S)
+        union = torch.minimum(a[:, :, None] + onehot_seg_label[:, None, :], torch.ones((), device=a.device)).sum(0)
+        return torch.nan_to_num(overlap / union, nan=0.0)
+
+    def match(self, clogit, a2f_attn):
+        """loss.py:108-153: Hungarian (o2o) / one-to-many / sequential matching."""
+        assert clogit.shape[1] == 1
+        mcfg = self.cfg.Loss
+        S = self.onehot_seg_label.shape[-1]
+        if mcfg.match == "seq":
+            A = clogit.shape[0]
+            assert A >= S, (A, S)
+            idx = torch.arange(S, dtype=torch.int64)
+            return idx, idx
+        with torch.no_grad():
+            cost = torch.zeros(clogit.shape[0], S, device=clogit.device)
+            if mcfg.pc > 0:
+                cost = cost - mcfg.pc * clogit.squeeze(1)[:, self.transcript]
+            if mcfg.a2fc > 0:
+                cost = cost - mcfg.a2fc * self.a2f_soft_iou(a2f_attn, self.onehot_seg_label)
+            cost = cost.double().cpu().numpy()
+        if mcfg.match == "o2o":
+            ai, si = linear_sum_assignment(cost)
+        elif mcfg.match == "o2m":
+            ai, si = self._one_to_many_match(cost)
+        else:
+            raise ValueError(mcfg.match)
+        return torch.as_tensor(np.asarray(ai), dtype=torch.int64), torch.as_tensor(np.asarray(si), dtype=torch.int64)
+
+    def _one_to_many_match(self, cost):
+        """loss.py:155-193."""
+        tr = self.transcript.cpu().numpy()
+        actions = np.unique(tr)
+        per_action = np.stack([cost[:, tr == a].sum(1) for a in actions], axis=1)
+        aid, cid = linear_sum_assignment(per_action)
+        rest = [a for a in range(cost.shape[0]) if a not in set(aid.tolist())]
+        rest_c = per_action[rest].argmin(1) if rest else np.zeros(0, dtype=np.int64)
+        token_cls = np.zeros(cost.shape[0])
+        token_cls[np.array(aid.tolist() + rest, dtype=np.int64)] = np.array(
+            [actions[i] for i in cid.tolist() + list(rest_c)])
+        pairs = {}
+        for a in actions:
+            segs = np.where(tr == a)[0]
+            toks = np.where(token_cls == a)[0]
+            pick = cost[toks][:, segs].argmin(0)
+            for s, k in zip(segs, pick):
+                pairs[s] = toks[k]
+        return list(pairs.values()), list(pairs.keys())
+
+    def action_token_loss(self, match, action_clogit, is_logit=True):
+        """loss.py:195-207."""
+        aind, sind = match
+        A, C = action_clogit.shape[0], action_clogit.shape[-1]
+        dev = action_clogit.device
+        tgt = torch.full((A,), C - 1, dtype=torch.int64, device=dev)
+        tgt[aind.to(dev)] = self.transcript[sind.to(dev)]
+        x = action_clogit.squeeze(1)
+        if is_logit:
+            return _weighted_xent(x, tgt, self.cweight)
+        return F.nll_loss(x, tgt, weight=self.cweight)
+
+    def _attn_xent(self, attn, frame_tgt, dim, denom):
+        lp = torch.log_softmax(attn, dim=dim - 1)
+        term = -lp * frame_tgt
+        if self.sweight is not None:
+            term = term * self.sweight                      # column i scaled by sweight[i] (loss.py:218-219)
+        return term.sum() / denom
+
+    def cross_attn_loss(self, match, attn, dim=None):
+        """loss.py:209-222."""
+        assert dim >= 1
+        aind, sind = match
+        dev = attn.device
+        tgt = self.onehot_seg_label[:, sind.to(dev)]
+        return self._attn_xent(attn[0, :, aind.to(dev)], tgt, dim, self.onehot_seg_label.sum())
+
+    def cross_attn_loss_tdu(self, match, attn, tdu, dim=None):
+        """loss.py:224-244."""
+        assert dim >= 1
+        aind, sind = match
+        dev = attn.device
+        z = _zoom(tdu, self.onehot_seg_label)
+        return self._attn_xent(attn[0, :, aind.to(dev)], z[:, sind.to(dev)], dim, z.sum())
+
+    def frame_loss(self, frame_clogit, is_logit=True):
+        """loss.py:246-258."""
+        lp = torch.log_softmax(frame_clogit, dim=-1) if is_logit else frame_clogit
+        w = self.cweight[:frame_clogit.shape[-1]]
+        return (-lp * self.onehot_class_label * w).sum() / self.onehot_class_label.sum()
+
+    def frame_loss_tdu(self, seg_clogit, tdu, is_logit=True):
+        """loss.py:260-277."""
+        x = seg_clogit.squeeze(1)
+        lp = torch.log_softmax(x, dim=-1) if is_logit else x
+        z = _zoom(tdu, self.onehot_class_label)
+        w = self.cweight[:lp.shape[-1]]
+        return (-lp * z * w).sum() / z.sum()
+
+
+def infonce_contrastive_loss(projected_embeddings, text_embeddings, labels, temperature=0.07):
+    """loss.py:280-341: (frame->text CE + per-class text->frame log-softmax) / 2."""
+    T, B, D = projected_embeddings.shape
+    emb = projected_embeddings.reshape(-1, D)
+    lab = labels.reshape(-1)
+    if lab.shape[0] != emb.shape[0]:
+        lab = lab.repeat(B)
+    n = text_embeddings.shape[0]
+    sim = emb @ text_embeddings.t() / temperature
+    v2t = F.cross_entropy(sim, lab)
+    tgt = F.one_hot(lab, num_classes=n).float()
+    lp_t = F.log_softmax(sim.t(), dim=1)
+    counts = torch.clamp(tgt.sum(0), min=1.0)
+    t2v = (-(lp_t * tgt.t()).sum(1) / counts).mean()
+    return (v2t + t2v) / 2.0

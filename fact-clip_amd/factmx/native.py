@@ -1,0 +1,138 @@
+"""ctypes binding of libfactmx.so (the C ABI declared in include/factmx.h).
+
+The product path has no CPU or eager-PyTorch fallback: importing an op that
+needs the library raises ``FactmxNativeError`` when the .so is missing or was
+built for another ABI, and every non-zero status from a call raises with the
+library's ``fx_last_error()`` text.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FACTMX_LIB", os.path.join(_HERE, "_lib", "libfactmx.so"))
+ABI_VERSION = 1
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+L = ctypes.c_longlong
+F = ctypes.c_float
+D = ctypes.c_double
+
+
+class FactmxNativeError(RuntimeError):
+    pass
+
+
+class Operand(ctypes.Structure):
+    _fields_ = [("ptr", P), ("ld", L), ("ptr1", P), ("ld1", L), ("k_split", I), ("rows0", P), ("rows1", P),
+                ("pos", P), ("ld_pos", L), ("pos_cols", I), ("trans", I), ("conv_taps", I), ("conv_cin", I),
+                ("conv_dil", I), ("conv_dir", I), ("seq_len", I), ("batch_stride", L)]
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [("M", I), ("N", I), ("K", I), ("batch", I), ("a", Operand), ("b", Operand), ("c", P), ("ldc", L),
+                ("c_batch_stride", L), ("alpha", F), ("beta", F), ("bias", P), ("resid", P), ("ld_resid", L),
+                ("resid_batch_stride", L), ("gate", P), ("ld_gate", L), ("relu", I), ("c_tap_cin", I),
+                ("split_k", I), ("workspace", P)]
+
+
+class MstcnParams(ctypes.Structure):
+    _fields_ = [("cin", I), ("F", I), ("cout", I), ("num_layers", I), ("layernorm", I), ("in_map", I),
+                ("dil0", I), ("dil_factor", I), ("w_in", P), ("b_in", P), ("w_dil", P), ("b_dil", P), ("w_pw", P), ("b_pw", P),
+                ("ln_w", P), ("ln_b", P), ("w_out", P), ("b_out", P)]
+
+
+class MstcnGrads(ctypes.Structure):
+    _fields_ = [("w_in", P), ("b_in", P), ("w_dil", P), ("b_dil", P), ("w_pw", P), ("b_pw", P),
+                ("ln_w", P), ("ln_b", P), ("w_out", P), ("b_out", P)]
+
+
+# name -> (restype, argtypes); every fx_* symbol declared in include/factmx.h
+SIGNATURES = {
+    "fx_version": (I, []),
+    "fx_last_error": (ctypes.c_char_p, []),
+    "fx_gemm": (I, [ctypes.POINTER(GemmDesc), P]),
+    "fx_gemm_workspace_floats": (L, [ctypes.POINTER(GemmDesc)]),
+    "fx_linear_fwd": (I, [P, L, P, L, I, I, I, P, L, P, P, L, I, I, P]),
+    "fx_linear_bwd_workspace_floats": (L, [I, I, I]),
+    "fx_linear_bwd": (I, [P, L, P, L, P, L, P, L, I, I, I, P, L, P, L, P, I, P, P]),
+    "fx_x2y_saved_floats": (L, [I, I, I, I, I]),
+    "fx_x2y_workspace_floats": (L, [I, I, I, I, I, I]),
+    "fx_x2y_fwd": (I, [P, L, I, I, P, L, I, P, L, I, I, P, L, I, P, P, P, P, P, P, P, P, I, I, P, L, P, P, P, P, P]),
+    "fx_x2y_bwd": (I, [P, L, I, I, I, P, L, I, I, I, P, P, P, P, I, I, P, P, P, L, P, P, P, P, P, P, P, P, P, P,
+                       P, P, P, P, I, I, P, P]),
+    "fx_mstcn_saved_floats": (L, [ctypes.POINTER(MstcnParams), I]),
+    "fx_mstcn_workspace_floats": (L, [ctypes.POINTER(MstcnParams), I]),
+    "fx_mstcn_fwd": (I, [ctypes.POINTER(MstcnParams), P, L, I, I, P, L, P, P, P]),
+    "fx_mstcn_bwd": (I, [ctypes.POINTER(MstcnParams), ctypes.POINTER(MstcnGrads), P, L, I, I, P, L, P, L, P, P, P]),
+    "fx_layernorm_fwd": (I, [P, L, P, L, P, P, F, I, I, I, P, L, P, L, P, P]),
+    "fx_layernorm_bwd_workspace_floats": (L, [I, I]),
+    "fx_layernorm_bwd": (I, [P, L, P, L, P, L, P, P, I, I, I, P, L, P, P, P, P]),
+    "fx_softmax_rows": (I, [P, L, I, I, F, P, L, P]),
+    "fx_softmax_rows_bwd": (I, [P, L, P, L, P, L, I, I, F, P, L, P]),
+    "fx_process_feature_fwd": (I, [P, L, I, I, I, P, L, P]),
+    "fx_process_feature_bwd": (I, [P, L, P, L, P, L, I, I, I, P, L, P]),
+    "fx_l2norm_fwd": (I, [P, L, I, I, P, L, P, P]),
+    "fx_l2norm_bwd": (I, [P, L, P, P, L, I, I, P, L, P]),
+    "fx_relu_bwd": (I, [P, L, P, L, I, I, P, L, P]),
+    "fx_add": (I, [P, L, P, L, I, I, P, L, I, P]),
+    "fx_mha_core_workspace_floats": (L, [I, I, I, I]),
+    "fx_mha_core_fwd": (I, [P, L, P, L, P, L, I, I, I, I, P, P, L, P, P]),
+    "fx_mha_core_bwd": (I, [P, L, P, L, P, L, P, P, L, I, I, I, I, P, L, P, L, P, L, P, P]),
+    "fx_segments_from_probs": (I, [P, L, I, I, I, P, P, P, P, P, P]),
+    "fx_seg_mean_fwd": (I, [P, L, P, P, I, I, P, L, P]),
+    "fx_seg_mean_bwd": (I, [P, L, P, P, P, I, I, P, L, I, P]),
+    "fx_seg_sum_rows": (I, [P, L, P, P, I, I, P, L, I, P]),
+    "fx_prof_enable": (I, [I, I]),
+    "fx_prof_collect": (I, [I, ctypes.POINTER(D), ctypes.POINTER(D), ctypes.POINTER(D), ctypes.POINTER(I)]),
+    "fx_prof_disable": (None, []),
+}
+
+_lib = None
+
+
+def load(path=None):
+    """Load and type the library once.  Raises FactmxNativeError if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        raise FactmxNativeError(
+            f"libfactmx.so not found at {path}: build it with `make -C fact-clip_amd/csrc` "
+            "(or __graft_entry__.build()); factmx has no CPU/eager fallback")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    v = lib.fx_version()
+    if v != ABI_VERSION:
+        raise FactmxNativeError(f"libfactmx ABI {v} != expected {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def check(status, what):
+    if status != 0:
+        msg = load().fx_last_error().decode(errors="replace")
+        raise FactmxNativeError(f"{what} failed ({status}): {msg}")
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t):
+    """Raw device pointer of a tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()
+
+
+def ld(t):
+    """Row stride of a 2-D row-major (possibly column-sliced) tensor."""
+    if t is None:
+        return 0
+    assert t.dim() == 2 and (t.stride(1) == 1 or t.shape[1] == 1), f"need unit column stride, got {t.stride()}"
+    return t.stride(0)

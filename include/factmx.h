@@ -1,0 +1,292 @@
+/*
+ * factmx — MI355X-native FACT / FACT_CLIP forward+backward, C ABI.
+ *
+ * The reference (lucas-t-t/FACT-CLIP) has no FFI: its hot path is a tree of
+ * nn.Modules calling ATen ops.  This header is the drop-in boundary UNDER that
+ * Python surface: every entry point replaces one reference op site (cited as
+ * file:line relative to the reference root) and is bound from Python by
+ * ctypes (fact-clip_amd/factmx/native.py; binding stub in INTEGRATION.md).
+ *
+ * Conventions
+ *   - All tensors are caller-owned device memory (fp32), row-major
+ *     "(rows, channels)" = the reference's (N, B=1, C) with the unit batch
+ *     axis dropped.  Leading dimensions (ld*) are in elements.
+ *   - `stream` is a hipStream_t (PyTorch's current stream).  No entry point
+ *     allocates, synchronises the device or keeps global mutable state; all
+ *     scratch comes from a caller workspace sized by the *_workspace_* query.
+ *   - Return 0 (FX_OK) or a negative FX_ERR_*; fx_last_error() (thread-local)
+ *     explains the last failure.
+ */
+#ifndef FACTMX_H
+#define FACTMX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FX_ABI_VERSION 1
+
+enum {
+  FX_OK = 0,
+  FX_ERR_SHAPE = -1,     /* bad shape / argument */
+  FX_ERR_HIP = -2,       /* HIP runtime error */
+  FX_ERR_UNSUPPORTED = -3
+};
+
+int fx_version(void);
+const char* fx_last_error(void);
+
+/* ------------------------------------------------------------------------
+ * Generic f32 GEMM on MFMA (v_mfma_f32_32x32x2_f32, exact f32 products):
+ *   C[b] = epilogue( alpha * op(A[b]) (MxK) * op(B[b]) (KxN) )
+ * Operands are described by a gather descriptor so the same kernel covers
+ * Linear / Conv1d(k=1) (basic.py:139,177,182; blocks.py:154,158,402,414),
+ * the implicit dilated Conv1d(k=3) (basic.py:138), concatenated inputs
+ * (basic.py:381-385 Y_W(cat[Y, attn_feat]); blocks.py:445 sf_merge(cat)),
+ * row gathers (basic.py:642 feature_seg2frame) and all their gradients.
+ *
+ * An operand is a logical (R x K) matrix (R = M for A, R = N for B):
+ *   trans == 0 : element (r,k) = src[r*ld + k]        (K contiguous)
+ *   trans == 1 : element (r,k) = src[k*ld + r]        (R contiguous)
+ * trans==0 extras: k >= k_split reads the second source ptr1 (column
+ *   k-k_split, leading dim ld1); rows0/rows1 gather source rows; pos adds
+ *   pos[r*ld_pos + k] for k < pos_cols (positional encoding add,
+ *   basic.py:313-320).
+ * conv_taps == 3 (dilated conv, zero padding per video of seq_len rows):
+ *   trans==0: k = tap*conv_cin + c, element = src[(r + s)*ld + c]
+ *   trans==1: r = tap*conv_cin + c, element = src[(k + s)*ld + c]
+ *   with s = (tap-1) * conv_dil * conv_dir, zero when the shifted row leaves
+ *   its video.
+ * ---------------------------------------------------------------------- */
+typedef struct fx_operand {
+  const float* ptr;
+  long long ld;
+  const float* ptr1;
+  long long ld1;
+  int k_split;
+  const int32_t* rows0;
+  const int32_t* rows1;
+  const float* pos;
+  long long ld_pos;
+  int pos_cols;
+  int trans;
+  int conv_taps;
+  int conv_cin;
+  int conv_dil;
+  int conv_dir;
+  int seq_len;
+  long long batch_stride;
+} fx_operand;
+
+typedef struct fx_gemm_desc {
+  int M, N, K, batch;
+  fx_operand a, b;
+  float* c;
+  long long ldc;
+  long long c_batch_stride;
+  float alpha;
+  float beta;                 /* C = ... + beta*C_old */
+  const float* bias;          /* + bias[n] */
+  const float* resid;         /* + resid[m*ld_resid + n] */
+  long long ld_resid;
+  long long resid_batch_stride;
+  const float* gate;          /* * (gate[m*ld_gate+n] > 0)   (ReLU backward) */
+  long long ld_gate;
+  int relu;                   /* 1: ReLU on the output; 2: ReLU before the residual add */
+  int c_tap_cin;              /* != 0: column n = tap*c_tap_cin + c stored at c*3 + tap */
+  int split_k;                /* >1: K split over workgroups, partials in workspace */
+  float* workspace;
+} fx_gemm_desc;
+
+int fx_gemm(const fx_gemm_desc* desc, void* stream);
+long long fx_gemm_workspace_floats(const fx_gemm_desc* desc);
+
+/* ------------------------------------------------------------------------
+ * nn.Linear / Conv1d(k=1) on (M, K) rows.  Replaces basic.py:139,177,182,
+ * 341-345,405-407,468-470,534-538; blocks.py:154,158,402,414.
+ *   fwd: y (ldy) = act((x [+pos on the first pos_cols]) . w^T + b),
+ *        w is (N, K) with row stride ldw; pos nullable (add_positional_encoding
+ *        fused into the operand load, basic.py:313-320).
+ *   bwd: dx (lddx) [+]= dy . w ;  dw (lddw) [+]= dy^T . x ;  db [+]= colsum(dy).
+ *        Any of dx/dw/db may be NULL.  accumulate != 0 adds into dx/dw/db.
+ *        relu_out (nullable): the forward output, gates dy by (relu_out>0).
+ * ---------------------------------------------------------------------- */
+int fx_linear_fwd(const float* x, long long ldx, const float* pos, long long ldpos, int pos_cols,
+                  int M, int K, const float* w, long long ldw, const float* b, float* y,
+                  long long ldy, int N, int relu, void* stream);
+long long fx_linear_bwd_workspace_floats(int M, int K, int N);
+int fx_linear_bwd(const float* dy, long long lddy, const float* x, long long ldx, const float* w,
+                  long long ldw, const float* relu_out, long long ld_relu, int M, int K, int N,
+                  float* dx, long long lddx, float* dw, long long lddw, float* db, int accumulate,
+                  float* workspace, void* stream);
+
+/* ------------------------------------------------------------------------
+ * X2Y_map, whole layer (basic.py:349-389, kq_pos=True as built by
+ * Block.create_cross_attention, blocks.py:234-240):
+ *   xk = X_K(X + Xpos), xv = X_V(X), yq = Y_Q(Y + Ypos)          (Hd wide)
+ *   logit (Ny, Nx) = yq . xk^T / sqrt(Hd);  attn = softmax over Nx
+ *   out (Ny, outdim) = Y_W(cat[Y, attn . xv])  (concat folded into the GEMM)
+ * logit and attn are outputs (the losses read them, blocks.py:363-366).
+ * Positional tensors cover the first *pos_cols channels (nullable).
+ * bwd: dout, optional direct dlogit / dattn (Ny, Nx) -> dX, dXpos, dY, dYpos
+ *   (nullable) and every weight/bias gradient (written, not accumulated).
+ * ---------------------------------------------------------------------- */
+long long fx_x2y_saved_floats(int Nx, int xdim, int Ny, int ydim, int Hd);
+long long fx_x2y_workspace_floats(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim);
+int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpos, long long ldxp,
+               int xpos_cols, const float* Y, long long ldy, int Ny, int ydim, const float* Ypos,
+               long long ldyp, int ypos_cols, const float* wk, const float* bk, const float* wv,
+               const float* bv, const float* wq, const float* bq, const float* wy, const float* by,
+               int Hd, int outdim, float* out, long long ldo, float* logit, float* attn,
+               float* saved, float* workspace, void* stream);
+int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, const float* Y,
+               long long ldy, int Ny, int ydim, int ypos_cols, const float* wk, const float* wv,
+               const float* wq, const float* wy, int Hd, int outdim, const float* attn,
+               const float* saved, const float* dout, long long lddo, const float* dlogit,
+               const float* dattn, float* dX, float* dXpos, float* dY, float* dYpos, float* dwk,
+               float* dbk, float* dwv, float* dbv, float* dwq, float* dbq, float* dwy, float* dby,
+               int has_xpos, int has_ypos, float* workspace, void* stream);
+
+/* ------------------------------------------------------------------------
+ * MS-TCN frame branch, whole stack in one call.
+ * Replaces MSTCN.forward (basic.py:200-220) with DilatedResidualLayer.forward
+ * (basic.py:154-171) unrolled over num_layers, dilation 2^i, eval-mode dropout.
+ *   x (T*nvid, cin) -> y (T*nvid, cout);   hidden width F.
+ *   w_in/b_in: Conv1d(cin->F, k=1) weights (nullable when in_map == 0, cin == F)
+ *   w_dil[i] (F,F,3), b_dil[i], w_pw[i] (F,F,1), b_pw[i]; ln_w/ln_b[i] (nullable)
+ *   w_out (cout,F,1), b_out.
+ *   saved (caller-owned, fx_mstcn_saved_floats): activations kept for backward.
+ * ---------------------------------------------------------------------- */
+typedef struct fx_mstcn_params {
+  int cin, F, cout, num_layers, layernorm, in_map;
+  int dil0, dil_factor;       /* layer i dilation = dil0 * dil_factor^i (0 -> 1 and 2) */
+  const float* w_in; const float* b_in;
+  const float* const* w_dil; const float* const* b_dil;
+  const float* const* w_pw; const float* const* b_pw;
+  const float* const* ln_w; const float* const* ln_b;
+  const float* w_out; const float* b_out;
+} fx_mstcn_params;
+
+typedef struct fx_mstcn_grads {
+  float* w_in; float* b_in;
+  float* const* w_dil; float* const* b_dil;
+  float* const* w_pw; float* const* b_pw;
+  float* const* ln_w; float* const* ln_b;
+  float* w_out; float* b_out;
+} fx_mstcn_grads;
+
+long long fx_mstcn_saved_floats(const fx_mstcn_params* p, int rows);
+long long fx_mstcn_workspace_floats(const fx_mstcn_params* p, int rows);
+int fx_mstcn_fwd(const fx_mstcn_params* p, const float* x, long long ldx, int T, int nvid,
+                 float* y, long long ldy, float* saved, float* workspace, void* stream);
+int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float* x, long long ldx,
+                 int T, int nvid, const float* dy, long long lddy, float* dx, long long lddx,
+                 const float* saved, float* workspace, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Row-wise LayerNorm with fused residual (post-norm residual blocks,
+ * basic.py:444-450, 504-522, 552-553; blocks.py:155; basic.py:144,166-169):
+ *   y = LN(x + r) * w + b  (r nullable); optionally y = relu(y).
+ *   xhat (normalised input, rows x cols) and rstd (rows) are saved for backward.
+ * bwd: given dy (and the relu output if relu), returns dx (= d(x+r)),
+ *   dw, db accumulated (+=) into the given buffers when non-NULL.
+ * ---------------------------------------------------------------------- */
+int fx_layernorm_fwd(const float* x, long long ldx, const float* r, long long ldr, const float* w,
+                     const float* b, float eps, int rows, int cols, int relu, float* y, long long ldy,
+                     float* xhat, long long ldxh, float* rstd, void* stream);
+long long fx_layernorm_bwd_workspace_floats(int rows, int cols);
+int fx_layernorm_bwd(const float* dy, long long lddy, const float* y, long long ldy, const float* xhat,
+                     long long ldxh, const float* w, const float* rstd, int rows, int cols, int relu,
+                     float* dx, long long lddx, float* dw, float* db, float* workspace, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Row softmax family.
+ * fx_softmax_rows: probs[r, :] = softmax(scale * logits[r, :]) over `cols`;
+ *   used for attention (basic.py:376 X2Y softmax; MultiheadAttention).
+ * fx_softmax_rows_bwd: dlogit = scale * p * (dp - sum(dp*p)) (+ dlogit_extra).
+ * fx_process_feature_fwd: Block.process_feature (blocks.py:195-202):
+ *   out[:, :cols-n] = x[:, :cols-n]; out[:, cols-n:] = softmax(x[:, cols-n:])
+ * fx_process_feature_bwd: dx = [dout_feat, softmax_bwd(dout_prob) + dclogit]
+ * ---------------------------------------------------------------------- */
+int fx_softmax_rows(const float* logits, long long ldl, int rows, int cols, float scale,
+                    float* probs, long long ldp, void* stream);
+int fx_softmax_rows_bwd(const float* probs, long long ldp, const float* dprobs, long long lddp,
+                        const float* dlogit_extra, long long lde, int rows, int cols, float scale,
+                        float* dlogit, long long ldd, void* stream);
+int fx_process_feature_fwd(const float* x, long long ldx, int rows, int cols, int n, float* out,
+                           long long ldo, void* stream);
+int fx_process_feature_bwd(const float* out, long long ldo, const float* dout, long long lddo,
+                           const float* dclogit, long long lddc, int rows, int cols, int n, float* dx,
+                           long long lddx, void* stream);
+
+/* ------------------------------------------------------------------------
+ * F.normalize(dim=-1, eps=1e-12) (blocks.py:174) and its backward.
+ * ---------------------------------------------------------------------- */
+int fx_l2norm_fwd(const float* x, long long ldx, int rows, int cols, float* y, long long ldy,
+                  float* norm, void* stream);
+int fx_l2norm_bwd(const float* y, long long ldy, const float* norm, const float* dy, long long lddy,
+                  int rows, int cols, float* dx, long long lddx, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Multi-head attention core (nn.MultiheadAttention math as called at
+ * basic.py:442, 500, 513): per head h, P_h = softmax(Q_h K_h^T / sqrt(hd)),
+ * O_h = P_h V_h.  q (Lq, E) ldq, k/v (Lk, E) ldk/ldv, o (Lq, E) ldo.
+ * probs (nhead, Lq, Lk) saved for backward.  bwd gives dq, dk, dv
+ * (accumulate flags per output).
+ * ---------------------------------------------------------------------- */
+long long fx_mha_core_workspace_floats(int Lq, int Lk, int E, int nhead);
+int fx_mha_core_fwd(const float* q, long long ldq, const float* k, long long ldk, const float* v,
+                    long long ldv, int Lq, int Lk, int E, int nhead, float* probs, float* o,
+                    long long ldo, float* workspace, void* stream);
+int fx_mha_core_bwd(const float* q, long long ldq, const float* k, long long ldk, const float* v,
+                    long long ldv, const float* probs, const float* dout, long long lddo, int Lq,
+                    int Lk, int E, int nhead, float* dq, long long lddq, float* dk, long long lddk,
+                    float* dv, long long lddv, float* workspace, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Temporal down/up-sampling (UpdateBlockTDU.temporal_downsample,
+ * blocks.py:417-437; TemporalDownsampleUpsample, basic.py:595-651;
+ * parse_label, utils/utils.py:25-48).
+ * fx_segments_from_probs: pred[t] = argmax_c x[t, col0 + c] (first max),
+ *   boundaries where pred changes, seg_id[t], seg_start[s], seg_end[s]
+ *   (inclusive) and *num_seg (device int) — bit-exact run-length encoding.
+ * fx_seg_mean_fwd: seg[s] = mean over frames of segment s (index_add / len)
+ * fx_seg_mean_bwd: dframe[t] (+)= dseg[seg_id[t]] / len[seg_id[t]]
+ * fx_seg_sum_rows: dseg[s] (+)= sum_{t in s} dframe[t]  (gather backward)
+ * ---------------------------------------------------------------------- */
+int fx_segments_from_probs(const float* x, long long ldx, int col0, int ncls, int T,
+                           int32_t* pred, int32_t* seg_id, int32_t* seg_start, int32_t* seg_end,
+                           int32_t* num_seg, void* stream);
+int fx_seg_mean_fwd(const float* x, long long ldx, const int32_t* seg_start, const int32_t* seg_end,
+                    int S, int cols, float* y, long long ldy, void* stream);
+int fx_seg_mean_bwd(const float* dy, long long lddy, const int32_t* seg_id, const int32_t* seg_start,
+                    const int32_t* seg_end, int T, int cols, float* dx, long long lddx, int accumulate,
+                    void* stream);
+int fx_seg_sum_rows(const float* dx, long long lddx, const int32_t* seg_start, const int32_t* seg_end,
+                    int S, int cols, float* dy, long long lddy, int accumulate, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Elementwise helpers: dz = dy * (y > 0) (ReLU backward, basic.py:158,
+ * blocks.py:156,414,433) and out (+)= a + b (residual merges).
+ * ---------------------------------------------------------------------- */
+int fx_relu_bwd(const float* dy, long long lddy, const float* y, long long ldy, int rows, int cols,
+                float* dz, long long lddz, void* stream);
+int fx_add(const float* a, long long lda, const float* b, long long ldb, int rows, int cols,
+           float* out, long long ldo, int accumulate, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Profiling hooks: HIP-event timing of every launch of one kernel class
+ * (bench.py roofline).  kind: 0 = dilated-conv implicit GEMM forward.
+ * ---------------------------------------------------------------------- */
+int fx_prof_enable(int kind, int max_events);
+int fx_prof_collect(int kind, double* total_ms, double* total_flops, double* total_bytes,
+                    int* count);
+void fx_prof_disable(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FACTMX_H */
