@@ -41,6 +41,10 @@ int launch_seg_reduce(const float* x, long long ldx, const int32_t* st, const in
                       float* y, long long ldy, int accumulate, hipStream_t s);
 int launch_seg_mean_bwd(const float* dy, long long lddy, const int32_t* sid, const int32_t* st, const int32_t* en,
                         int T, int cols, float* dx, long long lddx, int accumulate, hipStream_t s);
+int launch_gru_fwd(const float* gi, long long ldgi, int S, int Hh, const float* const whh[2], const float* const bhh[2],
+                   float* out, long long ldo, float* saved, float* ws, hipStream_t s);
+int launch_gru_bwd(const float* dout, long long lddo, int S, int Hh, const float* const whh[2], const float* saved,
+                   float* dgi, long long lddgi, float* dgh, hipStream_t s);
 
 // ---- error state ------------------------------------------------------------
 static thread_local std::string g_last_error;
@@ -769,6 +773,65 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
       FX_CHECK_HIP(hipMemcpy2DAsync(dYpos, ypos_cols * sizeof(float), dYq, ydim * sizeof(float),
                                     ypos_cols * sizeof(float), Ny, hipMemcpyDeviceToDevice, s));
     if (dY) FX_TRY(add2(dYq, ydim, dcat, cw, Ny, ydim, dY, ydim, 0, s));
+  }
+  return FX_OK;
+}
+
+// ---------------------------------------------------------------- bidirectional GRU
+long long fx_gru_saved_floats(int S, int Hh) { return 10LL * S * Hh; }
+
+long long fx_gru_workspace_floats(int S, int In, int Hh) {
+  const long long H3 = 3LL * Hh;
+  long long fwd = 2 * H3 * Hh + S * 2 * H3;
+  long long sp = std::max(split_ws(3 * Hh, In, S), split_ws(3 * Hh, Hh, S));
+  sp = std::max(sp, split_ws(S, In, 3 * Hh));
+  long long bwd = S * 2 * H3 + 2 * S * H3 + sp + colsum_workspace_floats(S, 3 * Hh);
+  return std::max(fwd, bwd);
+}
+
+int fx_gru_bidir_fwd(const float* x, long long ldx, int S, int In, int Hh, const float* w_ih_f, const float* w_hh_f,
+                     const float* b_ih_f, const float* b_hh_f, const float* w_ih_r, const float* w_hh_r,
+                     const float* b_ih_r, const float* b_hh_r, float* out, long long ldo, float* saved,
+                     float* workspace, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int H3 = 3 * Hh;
+  float* gi = workspace + 2LL * H3 * Hh;
+  // input projections of every step, both directions: gi[:, d*3Hh:(d+1)*3Hh] = x W_ih_d^T + b_ih_d
+  FX_TRY(linear_fwd(x, ldx, S, In, w_ih_f, b_ih_f, gi, 2 * H3, H3, 0, s));
+  FX_TRY(linear_fwd(x, ldx, S, In, w_ih_r, b_ih_r, gi + H3, 2 * H3, H3, 0, s));
+  const float* whh[2] = {w_hh_f, w_hh_r};
+  const float* bhh[2] = {b_hh_f, b_hh_r};
+  return launch_gru_fwd(gi, 2 * H3, S, Hh, whh, bhh, out, ldo, saved, workspace, s);
+}
+
+int fx_gru_bidir_bwd(const float* x, long long ldx, int S, int In, int Hh, const float* w_ih_f, const float* w_hh_f,
+                     const float* w_ih_r, const float* w_hh_r, const float* saved, const float* dout, long long lddo,
+                     float* dx, long long lddx, float* dw_ih_f, float* dw_hh_f, float* db_ih_f, float* db_hh_f,
+                     float* dw_ih_r, float* dw_hh_r, float* db_ih_r, float* db_hh_r, float* workspace, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int H3 = 3 * Hh;
+  float* dgi = workspace;                          // (S, 6Hh)
+  float* dgh = dgi + (long long)S * 2 * H3;        // 2 x (S, 3Hh)
+  float* spl = dgh + 2LL * S * H3;
+  long long sp = std::max(split_ws(3 * Hh, In, S), split_ws(3 * Hh, Hh, S));
+  sp = std::max(sp, split_ws(S, In, 3 * Hh));
+  float* csw = spl + sp;
+  const float* whh[2] = {w_hh_f, w_hh_r};
+  FX_TRY(launch_gru_bwd(dout, lddo, S, Hh, whh, saved, dgi, 2 * H3, dgh, s));
+  const float* wih[2] = {w_ih_f, w_ih_r};
+  float* dwih[2] = {dw_ih_f, dw_ih_r};
+  float* dwhh[2] = {dw_hh_f, dw_hh_r};
+  float* dbih[2] = {db_ih_f, db_ih_r};
+  float* dbhh[2] = {db_hh_f, db_hh_r};
+  for (int d = 0; d < 2; ++d) {
+    const float* gi_d = dgi + d * H3;
+    const float* gh_d = dgh + (long long)d * S * H3;
+    const float* hp_d = saved + (long long)d * S * Hh;
+    if (dwih[d]) FX_TRY(linear_dw(gi_d, 2 * H3, x, ldx, S, In, H3, dwih[d], 0, spl, s));
+    if (dbih[d]) FX_TRY(launch_colsum(gi_d, 2 * H3, S, H3, dbih[d], 0, csw, s));
+    if (dwhh[d]) FX_TRY(linear_dw(gh_d, H3, hp_d, Hh, S, Hh, H3, dwhh[d], 0, spl, s));
+    if (dbhh[d]) FX_TRY(launch_colsum(gh_d, H3, S, H3, dbhh[d], 0, csw, s));
+    if (dx) FX_TRY(linear_dx(gi_d, 2 * H3, wih[d], S, In, H3, dx, lddx, d, nullptr, 0, spl, s));
   }
   return FX_OK;
 }

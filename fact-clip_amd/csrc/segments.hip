@@ -77,18 +77,39 @@ __global__ __launch_bounds__(SCAN_THREADS) void boundary_scan_kernel(const int32
 }
 
 // y[s, c] = (sum_{t=start..end} x[t, c]) * (mean ? 1/len : 1)  (+ y if accumulate)
-__global__ __launch_bounds__(256) void seg_reduce_kernel(const float* x, long long ldx, const int32_t* st,
-                                                         const int32_t* en, int S, int cols, int mean, float* y,
-                                                         long long ldy, int accumulate) {
+// One workgroup per (segment, 64 channels): 16 waves stride over the segment's frames
+// (4 independent loads in flight per lane), then a fixed-order LDS combine (deterministic).
+constexpr int SEG_WAVES = 16;
+__global__ __launch_bounds__(64 * SEG_WAVES) void seg_reduce_kernel(const float* x, long long ldx, const int32_t* st,
+                                                                    const int32_t* en, int S, int cols, int mean,
+                                                                    float* y, long long ldy, int accumulate) {
+  __shared__ float part[SEG_WAVES][64];
   const int s = blockIdx.x;
-  const int c = blockIdx.y * 256 + threadIdx.x;
-  if (s >= S || c >= cols) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + lane;
   const int a = st[s], b = en[s];
-  float acc = 0.f;
-  for (int t = a; t <= b; ++t) acc += x[(long long)t * ldx + c];
-  if (mean) acc = acc / (float)(b - a + 1);
-  float* yp = y + (long long)s * ldy + c;
-  *yp = accumulate ? *yp + acc : acc;
+  float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+  if (c < cols) {
+    const float* xp = x + c;
+    int t = a + wv;
+    for (; t + 3 * SEG_WAVES <= b; t += 4 * SEG_WAVES) {
+      acc0 += xp[(long long)t * ldx];
+      acc1 += xp[(long long)(t + SEG_WAVES) * ldx];
+      acc2 += xp[(long long)(t + 2 * SEG_WAVES) * ldx];
+      acc3 += xp[(long long)(t + 3 * SEG_WAVES) * ldx];
+    }
+    for (; t <= b; t += SEG_WAVES) acc0 += xp[(long long)t * ldx];
+  }
+  part[wv][lane] = (acc0 + acc1) + (acc2 + acc3);
+  __syncthreads();
+  if (wv == 0 && c < cols) {
+    float tot = 0.f;
+#pragma unroll
+    for (int w = 0; w < SEG_WAVES; ++w) tot += part[w][lane];
+    if (mean) tot = tot / (float)(b - a + 1);
+    float* yp = y + (long long)s * ldy + c;
+    *yp = accumulate ? *yp + tot : tot;
+  }
 }
 
 // dx[t, c] (+)= dy[seg_id[t], c] / len
@@ -119,8 +140,8 @@ int launch_segments(const float* x, long long ldx, int col0, int ncls, int T, in
 int launch_seg_reduce(const float* x, long long ldx, const int32_t* st, const int32_t* en, int S, int cols, int mean,
                       float* y, long long ldy, int accumulate, hipStream_t s) {
   if (S == 0 || cols == 0) return FX_OK;
-  hipLaunchKernelGGL(seg_reduce_kernel, dim3(S, cdiv(cols, 256)), dim3(256), 0, s, x, ldx, st, en, S, cols, mean, y,
-                     ldy, accumulate);
+  hipLaunchKernelGGL(seg_reduce_kernel, dim3(S, cdiv(cols, 64)), dim3(64 * SEG_WAVES), 0, s, x, ldx, st, en, S, cols,
+                     mean, y, ldy, accumulate);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }

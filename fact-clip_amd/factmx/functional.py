@@ -537,6 +537,59 @@ def conv3(x, w, b, dil, T):
 
 
 # ---------------------------------------------------------------------------
+# bidirectional GRU over segments
+# ---------------------------------------------------------------------------
+
+class GRUFn(torch.autograd.Function):
+    """One bidirectional ``nn.GRU`` layer (blocks.py:401,432) on (S, In) rows -> (S, 2Hh)."""
+
+    @staticmethod
+    def forward(ctx, x, w_ih, w_hh, b_ih, b_hh, w_ih_r, w_hh_r, b_ih_r, b_hh_r):
+        lib = nx.load()
+        S, In = x.shape
+        Hh = w_hh.shape[1]
+        dev = x.device
+        out = _empty(S, 2 * Hh, device=dev)
+        saved = _ws(lib.fx_gru_saved_floats(S, Hh), dev)
+        ws = _ws(lib.fx_gru_workspace_floats(S, In, Hh), dev)
+        _check(lib.fx_gru_bidir_fwd(nx.ptr(x), nx.ld(x), S, In, Hh, nx.ptr(w_ih), nx.ptr(w_hh), nx.ptr(b_ih),
+                                    nx.ptr(b_hh), nx.ptr(w_ih_r), nx.ptr(w_hh_r), nx.ptr(b_ih_r), nx.ptr(b_hh_r),
+                                    nx.ptr(out), 2 * Hh, nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_gru_bidir_fwd")
+        ctx.save_for_backward(x, w_ih, w_hh, w_ih_r, w_hh_r, saved)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = nx.load()
+        x, w_ih, w_hh, w_ih_r, w_hh_r, saved = ctx.saved_tensors
+        dout = dout.contiguous()
+        S, In = x.shape
+        Hh = w_hh.shape[1]
+        dev = x.device
+        nd = ctx.needs_input_grad
+        dx = _empty(S, In, device=dev) if nd[0] else None
+        g = [_empty(*t.shape, device=dev) for t in (w_ih, w_hh, w_ih[:, 0], w_hh[:, 0],
+                                                    w_ih_r, w_hh_r, w_ih_r[:, 0], w_hh_r[:, 0])]
+        ws = _ws(lib.fx_gru_workspace_floats(S, In, Hh), dev)
+        _check(lib.fx_gru_bidir_bwd(nx.ptr(x), nx.ld(x), S, In, Hh, nx.ptr(w_ih), nx.ptr(w_hh), nx.ptr(w_ih_r),
+                                    nx.ptr(w_hh_r), nx.ptr(saved), nx.ptr(dout), 2 * Hh, nx.ptr(dx), nx.ld(dx),
+                                    *[nx.ptr(t) for t in g], nx.ptr(ws), nx.stream()), "fx_gru_bidir_bwd")
+        # argument order of GRUFn.forward: w_ih, w_hh, b_ih, b_hh, (same)_r
+        return (dx, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7])
+
+
+def gru(mod, x):
+    """Run an ``nn.GRU(bidirectional=True)`` module's parameters layer by layer through GRUFn."""
+    assert mod.bidirectional and not mod.batch_first
+    h = _2d(x)
+    for layer in range(mod.num_layers):
+        p = [getattr(mod, f"{n}_l{layer}{s}") for s in ("", "_reverse")
+             for n in ("weight_ih", "weight_hh", "bias_ih", "bias_hh")]
+        h = GRUFn.apply(h, *p)
+    return h
+
+
+# ---------------------------------------------------------------------------
 # Temporal down/up-sampling
 # ---------------------------------------------------------------------------
 

@@ -209,8 +209,7 @@ class UpdateBlockTDU(Block):
         f2 = fxf._2d(frame_feature)
         tdu = basic.TemporalDownsampleUpsample.from_probs(f2, f2.shape[1] - self.nclass, self.nclass)
         seg = tdu.feature_frame2seg(frame_feature)
-        seg, _ = self.seg_update(seg)
-        seg = torch.relu(seg)
+        seg = torch.relu(fxf.gru(self.seg_update, seg))
         seg = fxf.linear(seg, self.seg_combine.weight, self.seg_combine.bias).unsqueeze(1)
         seg, seg_clogit = self.process_feature(seg, self.nclass)
         return tdu, seg, seg_clogit

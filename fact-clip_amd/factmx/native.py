@@ -81,6 +81,10 @@ SIGNATURES = {
     "fx_mha_core_workspace_floats": (L, [I, I, I, I]),
     "fx_mha_core_fwd": (I, [P, L, P, L, P, L, I, I, I, I, P, P, L, P, P]),
     "fx_mha_core_bwd": (I, [P, L, P, L, P, L, P, P, L, I, I, I, I, P, L, P, L, P, L, P, P]),
+    "fx_gru_saved_floats": (L, [I, I]),
+    "fx_gru_workspace_floats": (L, [I, I, I]),
+    "fx_gru_bidir_fwd": (I, [P, L, I, I, I, P, P, P, P, P, P, P, P, P, L, P, P, P]),
+    "fx_gru_bidir_bwd": (I, [P, L, I, I, I, P, P, P, P, P, P, L, P, L, P, P, P, P, P, P, P, P, P, P]),
     "fx_segments_from_probs": (I, [P, L, I, I, I, P, P, P, P, P, P]),
     "fx_seg_mean_fwd": (I, [P, L, P, P, I, I, P, L, P]),
     "fx_seg_mean_bwd": (I, [P, L, P, P, P, I, I, P, L, I, P]),

@@ -269,6 +269,27 @@ int fx_seg_sum_rows(const float* dx, long long lddx, const int32_t* seg_start, c
                     int S, int cols, float* dy, long long lddy, int accumulate, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Bidirectional single-layer GRU over the S TDU segments
+ * (UpdateBlockTDU.seg_update = nn.GRU(H, H/2, 1, bidirectional=True),
+ * blocks.py:401,432; PyTorch gate order r, z, n; h0 = 0).
+ *   x (S, In) -> out (S, 2*Hh) = [forward h_t, backward h_t]; Hh <= 256.
+ *   saved (fx_gru_saved_floats): per-step h_{t-1} and gates for backward.
+ * bwd: dout (S, 2Hh) -> dx (nullable) and every weight/bias gradient
+ *   (written, not accumulated; each pointer nullable).
+ * ---------------------------------------------------------------------- */
+long long fx_gru_saved_floats(int S, int Hh);
+long long fx_gru_workspace_floats(int S, int In, int Hh);
+int fx_gru_bidir_fwd(const float* x, long long ldx, int S, int In, int Hh, const float* w_ih_f,
+                     const float* w_hh_f, const float* b_ih_f, const float* b_hh_f, const float* w_ih_r,
+                     const float* w_hh_r, const float* b_ih_r, const float* b_hh_r, float* out,
+                     long long ldo, float* saved, float* workspace, void* stream);
+int fx_gru_bidir_bwd(const float* x, long long ldx, int S, int In, int Hh, const float* w_ih_f,
+                     const float* w_hh_f, const float* w_ih_r, const float* w_hh_r, const float* saved,
+                     const float* dout, long long lddo, float* dx, long long lddx, float* dw_ih_f,
+                     float* dw_hh_f, float* db_ih_f, float* db_hh_f, float* dw_ih_r, float* dw_hh_r,
+                     float* db_ih_r, float* db_hh_r, float* workspace, void* stream);
+
+/* ------------------------------------------------------------------------
  * Elementwise helpers: dz = dy * (y > 0) (ReLU backward, basic.py:158,
  * blocks.py:156,414,433) and out (+)= a + b (residual merges).
  * ---------------------------------------------------------------------- */

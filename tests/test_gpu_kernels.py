@@ -160,6 +160,26 @@ def test_mha(Lq, Lk, E, nh):
         _close(p.grad, P[n].grad, rtol=1e-4, atol=1e-4, what=f"mha d{n}")
 
 
+@pytest.mark.parametrize("S,In,Hh", [(1, 512, 256), (40, 512, 256), (300, 64, 32), (7, 48, 24)])
+def test_gru_bidirectional(S, In, Hh):
+    mod = torch.nn.GRU(In, Hh, 1, bidirectional=True).double()
+    x = _r(S, In, seed=28)
+    g = _r(S, 2 * Hh, seed=29)
+    modd = torch.nn.GRU(In, Hh, 1, bidirectional=True).to(DEV)
+    modd.load_state_dict({k: v.float() for k, v in mod.state_dict().items()})
+    xd = x.float().to(DEV).requires_grad_(True)
+    y = fxf.gru(modd, xd)
+    (y * g.float().to(DEV)).sum().backward()
+    xr = x.clone().requires_grad_(True)
+    P = dict(mod.named_parameters())
+    yr = fo.gru(P, "", xr, 1)
+    (yr * g).sum().backward()
+    _close(y, yr, what="gru y")
+    _close(xd.grad, xr.grad, rtol=1e-4, atol=1e-4, what="gru dx")
+    for n, p in modd.named_parameters():
+        _close(p.grad, P[n].grad, rtol=1e-4, atol=1e-4, what=f"gru d{n}")
+
+
 def test_segments_bit_exact():
     rng = np.random.default_rng(0)
     for T, C in ((1, 5), (7, 3), (4096, 75), (5000, 2)):
