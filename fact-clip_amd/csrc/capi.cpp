@@ -182,15 +182,29 @@ int linear_dx(const float* dy, long long lddy, const float* w, int M, int K, int
   return launch_gemm(d, s);
 }
 
-// dw (+)= dy^T . x ; dy (M,N), x (M,K) -> dw (N,K) with row stride lddw
-int linear_dw(const float* dy, long long lddy, const float* x, long long ldx, int M, int K, int N, float* dw,
-              int accumulate, float* ws, hipStream_t s, long long lddw = -1) {
-  fx_gemm_desc d = gemm_desc(N, K, M, op_cols(dy, lddy), op_cols(x, ldx), dw, lddw < 0 ? K : lddw);
+// dw (+)= dy^T . x  and  db (+)= colsum(dy)  in ONE GEMM: x gets a virtual all-ones column K
+// whose output column (the bias gradient) is routed to db.  dy (M,N), x (M,K) -> dw (N,K), ld lddw.
+int linear_dwdb(const float* dy, long long lddy, const float* x, long long ldx, int M, int K, int N, float* dw,
+                float* db, int accumulate, float* ws, hipStream_t s, long long lddw = -1) {
+  if (!dw && !db) return FX_OK;
+  FX_REQUIRE(dw, "linear_dwdb: bias-only gradient needs dw");
+  fx_operand b = op_cols(x, ldx);
+  const int Kc = K + (db ? 1 : 0);
+  if (db) b.ones_col = K + 1;
+  fx_gemm_desc d = gemm_desc(N, Kc, M, op_cols(dy, lddy), b, dw, lddw < 0 ? K : lddw);
+  d.c_last_col = db;
   d.beta = accumulate ? 1.f : 0.f;
-  d.split_k = pick_split(N, K, M);
+  d.split_k = pick_split(N, Kc, M);
   d.workspace = ws;
   return launch_gemm(d, s);
 }
+
+int linear_dw(const float* dy, long long lddy, const float* x, long long ldx, int M, int K, int N, float* dw,
+              int accumulate, float* ws, hipStream_t s, long long lddw = -1) {
+  return linear_dwdb(dy, lddy, x, ldx, M, K, N, dw, nullptr, accumulate, ws, s, lddw);
+}
+
+long long dwdb_ws(int M, int K, int N) { return split_ws(N, K + 1, M); }
 
 // ---- MS-TCN layout of saved activations / workspace --------------------------------
 struct MstcnLayout {
@@ -219,10 +233,10 @@ MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
   L.buf2 = L.buf1 + L.rowsF;
   L.split = L.buf2 + L.rowsF;
   long long sp = 0;
-  sp = std::max(sp, split_ws(p->F, 3 * p->F, rows));          // conv dW
-  sp = std::max(sp, split_ws(p->F, p->F, rows));              // pointwise dW
-  sp = std::max(sp, split_ws(p->cout, p->F, rows));           // out dW
-  if (p->in_map) sp = std::max(sp, split_ws(p->F, p->cin, rows));  // in dW
+  sp = std::max(sp, split_ws(p->F, 3 * p->F + 1, rows));      // conv dW (+ bias column)
+  sp = std::max(sp, dwdb_ws(rows, p->F, p->F));               // pointwise dW
+  sp = std::max(sp, dwdb_ws(rows, p->F, p->cout));            // out dW
+  if (p->in_map) sp = std::max(sp, dwdb_ws(rows, p->cin, p->F));  // in dW
   sp = std::max(sp, split_ws(rows, p->F, p->cout));           // dH_L
   if (p->in_map) sp = std::max(sp, split_ws(rows, p->cin, p->F));
   sp = std::max(sp, layernorm_bwd_ws_floats(rows, p->F));
@@ -288,19 +302,20 @@ int fx_linear_fwd(const float* x, long long ldx, const float* pos, long long ldp
 }
 
 long long fx_linear_bwd_workspace_floats(int M, int K, int N) {
-  return (long long)M * N + split_ws(M, K, N) + split_ws(N, K, M) + colsum_workspace_floats(M, N);
+  return (long long)M * N + split_ws(M, K, N) + dwdb_ws(M, K, N) + colsum_workspace_floats(M, N);
 }
 
 int fx_linear_bwd(const float* dy, long long lddy, const float* x, long long ldx, const float* w, long long ldw,
                   const float* relu_out, long long ld_relu, int M, int K, int N, float* dx, long long lddx,
-                  float* dw, long long lddw, float* db, int accumulate, float* workspace, void* stream) {
+                  float* dw, long long lddw, float* db, int accumulate_dx, int accumulate_w, float* workspace,
+                  void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  FX_REQUIRE(workspace || (!relu_out && split_ws(M, K, N) == 0 && split_ws(N, K, M) == 0 && !db),
+  FX_REQUIRE(workspace || (!relu_out && split_ws(M, K, N) == 0 && dwdb_ws(M, K, N) == 0 && !(db && !dw)),
              "fx_linear_bwd: workspace required");
   float* wz = workspace;
   float* wsx = wz + (long long)M * N;
   float* wsw = wsx + split_ws(M, K, N);
-  float* wsc = wsw + split_ws(N, K, M);
+  float* wsc = wsw + dwdb_ws(M, K, N);
   const float* g = dy;
   long long ldg = lddy;
   if (relu_out) {
@@ -308,9 +323,9 @@ int fx_linear_bwd(const float* dy, long long lddy, const float* x, long long ldx
     g = wz;
     ldg = N;
   }
-  if (dx) FX_TRY(linear_dx(g, ldg, w, M, K, N, dx, lddx, accumulate, nullptr, 0, wsx, s, ldw));
-  if (dw) FX_TRY(linear_dw(g, ldg, x, ldx, M, K, N, dw, accumulate, wsw, s, lddw));
-  if (db) FX_TRY(launch_colsum(g, ldg, M, N, db, accumulate, wsc, s));
+  if (dx) FX_TRY(linear_dx(g, ldg, w, M, K, N, dx, lddx, accumulate_dx, nullptr, 0, wsx, s, ldw));
+  if (dw) FX_TRY(linear_dwdb(g, ldg, x, ldx, M, K, N, dw, db, accumulate_w, wsw, s, lddw));
+  else if (db) FX_TRY(launch_colsum(g, ldg, M, N, db, accumulate_w, wsc, s));
   return FX_OK;
 }
 
@@ -371,14 +386,14 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   float* ws = workspace;
   FX_TRY(pack_conv_weights(p, ws, L, s));
   float* spl = ws + L.split;
-  float* csw = ws + L.colsum;
   float* dH = ws + L.buf0;   // gradient w.r.t. the current layer output
   float* dU = ws + L.buf1;   // gradient at the residual sum (pre-LN)
   float* dZ = ws + L.buf2;   // gradient at the conv output (pre-ReLU)
+  // weight/bias gradients ACCUMULATE (+=) into g->* (caller zeroes them once per step);
+  // every bias gradient rides in its weight-gradient GEMM (virtual ones column).
   // output map
   const float* hL = saved + L.h + p->num_layers * L.rowsF;
-  FX_TRY(linear_dw(dy, lddy, hL, F, rows, F, p->cout, g->w_out, 0, spl, s));
-  FX_TRY(launch_colsum(dy, lddy, rows, p->cout, g->b_out, 0, csw, s));
+  FX_TRY(linear_dwdb(dy, lddy, hL, F, rows, F, p->cout, g->w_out, g->b_out, 1, spl, s));
   FX_TRY(linear_dx(dy, lddy, p->w_out, rows, F, p->cout, dH, F, 0, nullptr, 0, spl, s));
   for (int i = p->num_layers - 1; i >= 0; --i) {
     const float* hi = saved + L.h + i * L.rowsF;
@@ -391,19 +406,20 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
       gU = dU;
     }
     // pointwise: dW_pw = dU^T z, db_pw = colsum(dU), dZ = (dU . W_pw) * (z > 0)
-    FX_TRY(linear_dw(gU, F, zi, F, rows, F, F, g->w_pw[i], 0, spl, s));
-    FX_TRY(launch_colsum(gU, F, rows, F, g->b_pw[i], 0, csw, s));
+    FX_TRY(linear_dwdb(gU, F, zi, F, rows, F, F, g->w_pw[i], g->b_pw[i], 1, spl, s));
     FX_TRY(linear_dx(gU, F, p->w_pw[i], rows, F, F, dZ, F, 0, zi, F, spl, s));
-    // conv: dW (tap-major columns stored straight into (F,F,3)), db, dH_i = dU + conv^T(dZ)
+    // conv: dW (tap-major columns stored straight into (F,F,3)) + db (ones column), dH_i = dU + conv^T(dZ)
     {
-      fx_gemm_desc d = gemm_desc(F, 3 * F, rows, op_cols(dZ, F), conv_operand(hi, F, F, layer_dilation(p, i), 1, T, true),
-                                 g->w_dil[i], 3 * F);
+      fx_operand b = conv_operand(hi, F, F, layer_dilation(p, i), 1, T, true);
+      b.ones_col = 3 * F + 1;
+      fx_gemm_desc d = gemm_desc(F, 3 * F + 1, rows, op_cols(dZ, F), b, g->w_dil[i], 3 * F);
       d.c_tap_cin = F;
-      d.split_k = pick_split(F, 3 * F, rows);
+      d.c_last_col = g->b_dil[i];
+      d.beta = 1.f;
+      d.split_k = pick_split(F, 3 * F + 1, rows);
       d.workspace = spl;
       FX_TRY(launch_gemm(d, s));
     }
-    FX_TRY(launch_colsum(dZ, F, rows, F, g->b_dil[i], 0, csw, s));
     {
       float* dHn = (gU == dH) ? dU : dH;  // write into the buffer not holding gU
       fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dZ, F, F, layer_dilation(p, i), -1, T, false),
@@ -415,8 +431,7 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
     }
   }
   if (p->in_map) {
-    if (g->w_in) FX_TRY(linear_dw(dH, F, x, ldx, rows, p->cin, F, g->w_in, 0, spl, s));
-    if (g->b_in) FX_TRY(launch_colsum(dH, F, rows, F, g->b_in, 0, csw, s));
+    if (g->w_in) FX_TRY(linear_dwdb(dH, F, x, ldx, rows, p->cin, F, g->w_in, g->b_in, 1, spl, s));
     if (dx) FX_TRY(linear_dx(dH, F, p->w_in, rows, p->cin, F, dx, lddx, 0, nullptr, 0, spl, s));
   } else if (dx) {
     FX_CHECK_HIP(hipMemcpy2DAsync(dx, lddx * sizeof(float), dH, F * sizeof(float), F * sizeof(float), rows,
@@ -603,10 +618,10 @@ long long x2y_split_ws(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim) {
   sp = std::max(sp, split_ws(Ny, Hd, Nx));             // feat, dyq
   sp = std::max(sp, split_ws(Nx, Hd, Ny));             // dxv, dxk
   sp = std::max(sp, split_ws(Ny, ydim + Hd, outdim));  // dcat
-  sp = std::max(sp, split_ws(outdim, ydim, Ny));       // dW_y pieces
-  sp = std::max(sp, split_ws(outdim, Hd, Ny));
-  sp = std::max(sp, split_ws(Hd, xdim, Nx));           // dW_k / dW_v
-  sp = std::max(sp, split_ws(Hd, ydim, Ny));           // dW_q
+  sp = std::max(sp, dwdb_ws(Ny, ydim, outdim));        // dW_y pieces (+ bias column)
+  sp = std::max(sp, dwdb_ws(Ny, Hd, outdim));
+  sp = std::max(sp, dwdb_ws(Nx, xdim, Hd));            // dW_k / dW_v
+  sp = std::max(sp, dwdb_ws(Ny, ydim, Hd));            // dW_q
   sp = std::max(sp, split_ws(Nx, xdim, Hd));           // dX
   sp = std::max(sp, split_ws(Ny, ydim, Hd));           // dY
   return sp;
@@ -711,9 +726,9 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
   const float scale = 1.0f / std::sqrt((float)Hd);
   // Y_W: dcat = dout . Wy, dWy = dout^T [Y, feat], dby
   FX_TRY(linear_dx(dout, lddo, wy, Ny, cw, outdim, dcat, cw, 0, nullptr, 0, spl, s));
-  FX_TRY(linear_dw(dout, lddo, Y, ldy, Ny, ydim, outdim, dwy, 0, spl, s, cw));
-  FX_TRY(linear_dw(dout, lddo, feat, Hd, Ny, Hd, outdim, dwy + ydim, 0, spl, s, cw));
-  FX_TRY(launch_colsum(dout, lddo, Ny, outdim, dby, 0, csw, s));
+  (void)csw;
+  FX_TRY(linear_dwdb(dout, lddo, Y, ldy, Ny, ydim, outdim, dwy, dby, 1, spl, s, cw));
+  FX_TRY(linear_dw(dout, lddo, feat, Hd, Ny, Hd, outdim, dwy + ydim, 1, spl, s, cw));
   const float* dfeat = dcat + ydim;
   // dP = dfeat . xv^T (+ dattn) ; dxv = attn^T . dfeat
   {
@@ -747,12 +762,9 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
     FX_TRY(launch_gemm(d, s));
   }
   // projections
-  FX_TRY(linear_dw(dxk, Hd, xin, ldxin, Nx, xdim, Hd, dwk, 0, spl, s));
-  FX_TRY(launch_colsum(dxk, Hd, Nx, Hd, dbk, 0, csw, s));
-  FX_TRY(linear_dw(dxv, Hd, X, ldx, Nx, xdim, Hd, dwv, 0, spl, s));
-  FX_TRY(launch_colsum(dxv, Hd, Nx, Hd, dbv, 0, csw, s));
-  FX_TRY(linear_dw(dyq, Hd, yin, ldyin, Ny, ydim, Hd, dwq, 0, spl, s));
-  FX_TRY(launch_colsum(dyq, Hd, Ny, Hd, dbq, 0, csw, s));
+  FX_TRY(linear_dwdb(dxk, Hd, xin, ldxin, Nx, xdim, Hd, dwk, dbk, 1, spl, s));
+  FX_TRY(linear_dwdb(dxv, Hd, X, ldx, Nx, xdim, Hd, dwv, dbv, 1, spl, s));
+  FX_TRY(linear_dwdb(dyq, Hd, yin, ldyin, Ny, ydim, Hd, dwq, dbq, 1, spl, s));
   if (dX || dXpos) {
     FX_TRY(linear_dx(dxk, Hd, wk, Nx, xdim, Hd, dXk, xdim, 0, nullptr, 0, spl, s));
     if (dXpos)
@@ -780,11 +792,15 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
 // ---------------------------------------------------------------- bidirectional GRU
 long long fx_gru_saved_floats(int S, int Hh) { return 10LL * S * Hh; }
 
+static long long gru_split_ws(int S, int In, int Hh) {
+  long long sp = std::max(dwdb_ws(S, In, 3 * Hh), dwdb_ws(S, Hh, 3 * Hh));
+  return std::max(sp, split_ws(S, In, 3 * Hh));
+}
+
 long long fx_gru_workspace_floats(int S, int In, int Hh) {
   const long long H3 = 3LL * Hh;
   long long fwd = 2 * H3 * Hh + S * 2 * H3;
-  long long sp = std::max(split_ws(3 * Hh, In, S), split_ws(3 * Hh, Hh, S));
-  sp = std::max(sp, split_ws(S, In, 3 * Hh));
+  long long sp = gru_split_ws(S, In, Hh);
   long long bwd = S * 2 * H3 + 2 * S * H3 + sp + colsum_workspace_floats(S, 3 * Hh);
   return std::max(fwd, bwd);
 }
@@ -813,9 +829,7 @@ int fx_gru_bidir_bwd(const float* x, long long ldx, int S, int In, int Hh, const
   float* dgi = workspace;                          // (S, 6Hh)
   float* dgh = dgi + (long long)S * 2 * H3;        // 2 x (S, 3Hh)
   float* spl = dgh + 2LL * S * H3;
-  long long sp = std::max(split_ws(3 * Hh, In, S), split_ws(3 * Hh, Hh, S));
-  sp = std::max(sp, split_ws(S, In, 3 * Hh));
-  float* csw = spl + sp;
+  float* csw = spl + gru_split_ws(S, In, Hh);
   const float* whh[2] = {w_hh_f, w_hh_r};
   FX_TRY(launch_gru_bwd(dout, lddo, S, Hh, whh, saved, dgi, 2 * H3, dgh, s));
   const float* wih[2] = {w_ih_f, w_ih_r};
@@ -827,10 +841,10 @@ int fx_gru_bidir_bwd(const float* x, long long ldx, int S, int In, int Hh, const
     const float* gi_d = dgi + d * H3;
     const float* gh_d = dgh + (long long)d * S * H3;
     const float* hp_d = saved + (long long)d * S * Hh;
-    if (dwih[d]) FX_TRY(linear_dw(gi_d, 2 * H3, x, ldx, S, In, H3, dwih[d], 0, spl, s));
-    if (dbih[d]) FX_TRY(launch_colsum(gi_d, 2 * H3, S, H3, dbih[d], 0, csw, s));
-    if (dwhh[d]) FX_TRY(linear_dw(gh_d, H3, hp_d, Hh, S, Hh, H3, dwhh[d], 0, spl, s));
-    if (dbhh[d]) FX_TRY(launch_colsum(gh_d, H3, S, H3, dbhh[d], 0, csw, s));
+    if (dwih[d]) FX_TRY(linear_dwdb(gi_d, 2 * H3, x, ldx, S, In, H3, dwih[d], dbih[d], 1, spl, s));
+    else if (dbih[d]) FX_TRY(launch_colsum(gi_d, 2 * H3, S, H3, dbih[d], 1, csw, s));
+    if (dwhh[d]) FX_TRY(linear_dwdb(gh_d, H3, hp_d, Hh, S, Hh, H3, dwhh[d], dbhh[d], 1, spl, s));
+    else if (dbhh[d]) FX_TRY(launch_colsum(gh_d, H3, S, H3, dbhh[d], 1, csw, s));
     if (dx) FX_TRY(linear_dx(gi_d, 2 * H3, wih[d], S, In, H3, dx, lddx, d, nullptr, 0, spl, s));
   }
   return FX_OK;

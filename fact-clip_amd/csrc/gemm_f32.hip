@@ -36,6 +36,7 @@ struct GemmDev {
   long long ld_gate;
   int relu, split, kt_per_split, a_vec, b_vec, c_tap_cin;
   float* ws;
+  float* c_last;
 };
 
 __device__ __forceinline__ int conv_shift(const fx_operand& o, int tap) {
@@ -62,6 +63,7 @@ __device__ __forceinline__ float fetch_rm(const fx_operand& o, const float* p0, 
 
 // element (r,k) of a trans==1 operand
 __device__ __forceinline__ float fetch_cm(const fx_operand& o, const float* p0, int r, int k) {
+  if (o.ones_col && r == o.ones_col - 1) return 1.f;
   if (o.conv_taps) {
     const int j = r / o.conv_cin, c = r - j * o.conv_cin, s = conv_shift(o, j);
     const int t = k % o.seq_len + s;
@@ -123,7 +125,7 @@ __device__ __forceinline__ void load_cm8(const fx_operand& o, const float* p0, i
     for (int e = 0; e < 8; ++e) v[e] = 0.f;
     return;
   }
-  if (vec && r + 8 <= R) {
+  if (vec && r + 8 <= R && !(o.ones_col && r + 8 >= o.ones_col)) {
     const float* src;
     if (o.conv_taps) {
       const int j = r / o.conv_cin, c = r - j * o.conv_cin, s = conv_shift(o, j);
@@ -171,6 +173,12 @@ __device__ __forceinline__ void store_tile(float (*s)[LDSS], int tid, const floa
 // c_tap_cin != 0: output column n = tap*c_tap_cin + c is stored at c*3 + tap (Conv1d weight layout)
 __device__ __forceinline__ void epilogue_store(const GemmDev& g, int b, int m, int n, float acc) {
   float v = g.alpha * acc;
+  if (g.c_last && n == g.N - 1) {   // fused bias-gradient column
+    float* cp = g.c_last + (long long)b * g.M + m;
+    if (g.beta != 0.f) v += g.beta * (*cp);
+    *cp = v;
+    return;
+  }
   if (g.bias) v += g.bias[n];
   if (g.relu == 2) v = fmaxf(v, 0.f);
   if (g.resid) v += g.resid[(long long)b * g.resid_bs + (long long)m * g.ld_resid + n];
@@ -335,8 +343,9 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
   FX_REQUIRE(!(d.a.conv_taps && d.a.seq_len <= 0) && !(d.b.conv_taps && d.b.seq_len <= 0),
              "gemm: conv operand needs seq_len");
   FX_REQUIRE(!(d.a.conv_taps && d.K != d.a.conv_taps * d.a.conv_cin), "gemm: conv A needs K == taps*cin");
-  FX_REQUIRE(!(d.b.conv_taps && d.b.trans && d.N != d.b.conv_taps * d.b.conv_cin),
-             "gemm: conv B needs N == taps*cin");
+  FX_REQUIRE(!(d.b.conv_taps && d.b.trans && d.N != d.b.conv_taps * d.b.conv_cin + (d.b.ones_col ? 1 : 0)),
+             "gemm: conv B needs N == taps*cin (+1 with a ones column)");
+  FX_REQUIRE(!(d.a.ones_col && !d.a.trans) && !(d.b.ones_col && !d.b.trans), "gemm: ones_col needs trans==1");
   GemmDev g{};
   g.M = d.M;
   g.N = d.N;
@@ -356,6 +365,7 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
   g.ld_gate = d.ld_gate;
   g.relu = d.relu;
   g.c_tap_cin = d.c_tap_cin;
+  g.c_last = d.c_last_col;
   g.a_vec = operand_vec_ok(d.a);
   g.b_vec = operand_vec_ok(d.b);
   const int nkt = cdiv(d.K, BK);

@@ -3,9 +3,16 @@
 Every function here launches hand-written HIP kernels through ``native`` on
 PyTorch's current stream; tensors are fp32 row-major (rows, channels).  There
 is no eager/CPU fallback: a missing library raises FactmxNativeError.
+
+Gradient convention: the kernels ACCUMULATE weight and bias gradients (+=)
+straight into ``param.grad`` of leaf parameters (allocating zeros on first use,
+exactly what autograd's AccumulateGrad would do) and the backward returns
+``None`` for them.  With ``factmx.dp.FlatGradReducer`` those ``.grad`` tensors
+are views into the all-reduce buckets, so no per-parameter add, fill or copy
+kernel is launched.  Non-leaf weights get a fresh buffer that is returned to
+autograd as usual.
 """
 import ctypes
-import math
 
 import torch
 
@@ -41,6 +48,18 @@ def _check(status, what):
         nx.check(status, what)
 
 
+def grad_target(p, needed=True):
+    """(buffer the kernel accumulates into, value to return to autograd)."""
+    if p is None or not needed:
+        return None, None
+    if p.is_leaf:
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
+        return p.grad, None
+    buf = torch.zeros_like(p)
+    return buf, buf
+
+
 # ---------------------------------------------------------------------------
 # raw launch helpers (no autograd)
 # ---------------------------------------------------------------------------
@@ -56,22 +75,21 @@ def lin_fwd(x, w, b, relu=0, out=None):
     return y
 
 
-def lin_bwd(dy, x, w, need_dx=True, need_dw=True, need_db=True, relu_out=None):
+def lin_bwd(dy, x, w, need_dx=True, dw=None, db=None, relu_out=None, dx_out=None, acc_dx=False):
+    """dx = dy.w (returned / written to dx_out); dw += dy^T x and db += colsum(dy) when given."""
     lib = nx.load()
     w2 = _w2d(w)
     M, K = x.shape
     N = w2.shape[0]
     dev = dy.device
-    dx = _empty(M, K, device=dev) if need_dx else None
-    dw = _empty(N, K, device=dev) if need_dw else None
-    db = _empty(N, device=dev) if need_db else None
+    dx = dx_out if dx_out is not None else (_empty(M, K, device=dev) if need_dx else None)
+    dw2 = None if dw is None else (dw.reshape(dw.shape[0], -1) if dw.dim() == 3 else dw)
     ws = _ws(lib.fx_linear_bwd_workspace_floats(M, K, N), dev)
     _check(lib.fx_linear_bwd(nx.ptr(dy), nx.ld(dy), nx.ptr(x), nx.ld(x), nx.ptr(w2), nx.ld(w2),
                              nx.ptr(relu_out), nx.ld(relu_out), M, K, N, nx.ptr(dx), nx.ld(dx),
-                             nx.ptr(dw), nx.ld(dw), nx.ptr(db), 0, nx.ptr(ws), nx.stream()), "fx_linear_bwd")
-    if dw is not None and w.dim() == 3:
-        dw = dw.reshape(w.shape)
-    return dx, dw, db
+                             nx.ptr(dw2), nx.ld(dw2), nx.ptr(db), int(acc_dx), 1, nx.ptr(ws), nx.stream()),
+           "fx_linear_bwd")
+    return dx
 
 
 # ---------------------------------------------------------------------------
@@ -85,16 +103,18 @@ class LinearFn(torch.autograd.Function):
     def forward(ctx, x, w, b, relu):
         y = lin_fwd(x, w, b, relu)
         ctx.relu = relu
-        ctx.save_for_backward(x, w, y if relu else None)
+        ctx.has_b = b is not None
+        ctx.save_for_backward(x, w, b, y if relu else None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w, y = ctx.saved_tensors
-        dy = dy.contiguous()
-        dx, dw, db = lin_bwd(dy, x, w, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
-                             ctx.needs_input_grad[2], relu_out=y if ctx.relu else None)
-        return dx, dw, db, None
+        x, w, b, y = ctx.saved_tensors
+        nd = ctx.needs_input_grad
+        dwb, dw_ret = grad_target(w, nd[1])
+        dbb, db_ret = grad_target(b, nd[2] and ctx.has_b)
+        dx = lin_bwd(dy.contiguous(), x, w, nd[0], dwb, dbb, relu_out=y if ctx.relu else None)
+        return dx, dw_ret, db_ret, None
 
 
 def linear(x, w, b, relu=False):
@@ -120,24 +140,25 @@ class LayerNormFn(torch.autograd.Function):
                                     nx.stream()), "fx_layernorm_fwd")
         ctx.relu = relu
         ctx.has_r = r is not None
-        ctx.save_for_backward(y, xhat, rstd, w)
+        ctx.save_for_backward(y, xhat, rstd, w, b)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         lib = nx.load()
-        y, xhat, rstd, w = ctx.saved_tensors
+        y, xhat, rstd, w, b = ctx.saved_tensors
+        nd = ctx.needs_input_grad
         dy = dy.contiguous()
         rows, cols = y.shape
         dev = dy.device
         dx = _empty(rows, cols, device=dev)
-        dw = torch.zeros(cols, device=dev, dtype=_f32)
-        db = torch.zeros(cols, device=dev, dtype=_f32)
+        dwb, dw_ret = grad_target(w, nd[2])
+        dbb, db_ret = grad_target(b, nd[3])
         ws = _ws(lib.fx_layernorm_bwd_workspace_floats(rows, cols), dev)
         _check(lib.fx_layernorm_bwd(nx.ptr(dy), cols, nx.ptr(y), cols, nx.ptr(xhat), cols, nx.ptr(w), nx.ptr(rstd),
-                                    rows, cols, int(ctx.relu), nx.ptr(dx), cols, nx.ptr(dw), nx.ptr(db), nx.ptr(ws),
+                                    rows, cols, int(ctx.relu), nx.ptr(dx), cols, nx.ptr(dwb), nx.ptr(dbb), nx.ptr(ws),
                                     nx.stream()), "fx_layernorm_bwd")
-        return dx, (dx if ctx.has_r else None), dw, db, None, None
+        return dx, (dx if ctx.has_r else None), dw_ret, db_ret, None, None
 
 
 def layer_norm(x, w, b, eps=1e-5, residual=None, relu=False):
@@ -221,17 +242,20 @@ def l2_normalize(x):
 
 class MHAFn(torch.autograd.Function):
     """``nn.MultiheadAttention`` forward/backward as used by SALayer/SCALayer
-    (basic.py:442, 500, 513): in-projections, per-head softmax(QK^T/sqrt(hd))V, out_proj."""
+    (basic.py:442, 500, 513): in-projections, per-head softmax(QK^T/sqrt(hd))V, out_proj.
+    ``w_packed`` (3E, E) is the packed in_proj_weight (kdim == E) or None with wq/wk/wv given."""
 
     @staticmethod
-    def forward(ctx, q_in, k_in, v_in, wq, bq, wk, bk, wv, bv, wo, bo, nhead):
+    def forward(ctx, q_in, k_in, v_in, w_packed, wq, wk, wv, b_in, wo, bo, nhead):
         lib = nx.load()
         dev = q_in.device
         Lq, Lk = q_in.shape[0], k_in.shape[0]
-        E = wq.shape[0]
-        q = lin_fwd(q_in, wq, bq)
-        k = lin_fwd(k_in, wk, bk)
-        v = lin_fwd(v_in, wv, bv)
+        E = wo.shape[0]
+        if w_packed is not None:
+            wq, wk, wv = w_packed[:E], w_packed[E:2 * E], w_packed[2 * E:]
+        q = lin_fwd(q_in, wq, b_in[:E])
+        k = lin_fwd(k_in, wk, b_in[E:2 * E])
+        v = lin_fwd(v_in, wv, b_in[2 * E:])
         probs = _empty(nhead, Lq, Lk, device=dev)
         o = _empty(Lq, E, device=dev)
         ws = _ws(lib.fx_mha_core_workspace_floats(Lq, Lk, E, nhead), dev)
@@ -239,20 +263,23 @@ class MHAFn(torch.autograd.Function):
                                    nx.ptr(o), E, nx.ptr(ws), nx.stream()), "fx_mha_core_fwd")
         out = lin_fwd(o, wo, bo)
         ctx.nhead = nhead
-        ctx.save_for_backward(q_in, k_in, v_in, wq, wk, wv, wo, q, k, v, probs, o)
+        ctx.packed = w_packed is not None
+        ctx.save_for_backward(q_in, k_in, v_in, w_packed, wq, wk, wv, b_in, wo, bo, q, k, v, probs, o)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         lib = nx.load()
-        q_in, k_in, v_in, wq, wk, wv, wo, q, k, v, probs, o = ctx.saved_tensors
+        q_in, k_in, v_in, w_packed, wq, wk, wv, b_in, wo, bo, q, k, v, probs, o = ctx.saved_tensors
         nd = ctx.needs_input_grad
         dout = dout.contiguous()
         dev = dout.device
         Lq, Lk = q_in.shape[0], k_in.shape[0]
-        E = wq.shape[0]
+        E = wo.shape[0]
         nh = ctx.nhead
-        d_o, dwo, dbo = lin_bwd(dout, o, wo, True, nd[9], nd[10])
+        dwo, dwo_ret = grad_target(wo, nd[8])
+        dbo, dbo_ret = grad_target(bo, nd[9])
+        d_o = lin_bwd(dout, o, wo, True, dwo, dbo)
         dq = _empty(Lq, E, device=dev)
         dk = _empty(Lk, E, device=dev)
         dv = _empty(Lk, E, device=dev)
@@ -260,23 +287,30 @@ class MHAFn(torch.autograd.Function):
         _check(lib.fx_mha_core_bwd(nx.ptr(q), E, nx.ptr(k), E, nx.ptr(v), E, nx.ptr(probs), nx.ptr(d_o), E, Lq, Lk,
                                    E, nh, nx.ptr(dq), E, nx.ptr(dk), E, nx.ptr(dv), E, nx.ptr(ws), nx.stream()),
                "fx_mha_core_bwd")
-        dq_in, dwq, dbq = lin_bwd(dq, q_in, wq, nd[0], nd[3], nd[4])
-        dk_in, dwk, dbk = lin_bwd(dk, k_in, wk, nd[1], nd[5], nd[6])
-        dv_in, dwv, dbv = lin_bwd(dv, v_in, wv, nd[2], nd[7], nd[8])
-        return dq_in, dk_in, dv_in, dwq, dbq, dwk, dbk, dwv, dbv, dwo, dbo, None
+        dbin, dbin_ret = grad_target(b_in, nd[7])
+        rets = [None, None, None, None]
+        if ctx.packed:
+            dwp, rets[0] = grad_target(w_packed, nd[3])
+            tq, tk, tv = (None, None, None) if dwp is None else (dwp[:E], dwp[E:2 * E], dwp[2 * E:])
+        else:
+            tq, rets[1] = grad_target(wq, nd[4])
+            tk, rets[2] = grad_target(wk, nd[5])
+            tv, rets[3] = grad_target(wv, nd[6])
+        bq, bk, bv = (None, None, None) if dbin is None else (dbin[:E], dbin[E:2 * E], dbin[2 * E:])
+        dq_in = lin_bwd(dq, q_in, wq, nd[0], tq, bq)
+        dk_in = lin_bwd(dk, k_in, wk, nd[1], tk, bk)
+        dv_in = lin_bwd(dv, v_in, wv, nd[2], tv, bv)
+        return (dq_in, dk_in, dv_in, rets[0], rets[1], rets[2], rets[3], dbin_ret, dwo_ret, dbo_ret, None)
 
 
 def mha(mod, query, key, value):
     """Run an nn.MultiheadAttention module's parameters through MHAFn (dropout must be off)."""
-    E = mod.embed_dim
     if mod._qkv_same_embed_dim:
-        W = mod.in_proj_weight
-        wq, wk, wv = W[:E], W[E:2 * E], W[2 * E:]
+        args = (mod.in_proj_weight, None, None, None)
     else:
-        wq, wk, wv = mod.q_proj_weight, mod.k_proj_weight, mod.v_proj_weight
-    b = mod.in_proj_bias
-    return MHAFn.apply(_2d(query), _2d(key), _2d(value), wq, b[:E], wk, b[E:2 * E], wv, b[2 * E:],
-                       mod.out_proj.weight, mod.out_proj.bias, mod.num_heads)
+        args = (None, mod.q_proj_weight, mod.k_proj_weight, mod.v_proj_weight)
+    return MHAFn.apply(_2d(query), _2d(key), _2d(value), *args, mod.in_proj_bias, mod.out_proj.weight,
+                       mod.out_proj.bias, mod.num_heads)
 
 
 # ---------------------------------------------------------------------------
@@ -307,14 +341,14 @@ class X2YFn(torch.autograd.Function):
                               nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_x2y_fwd")
         ctx.dims = (Nx, xdim, Ny, ydim, Hd, outdim, xpc, ypc)
         ctx.has_pos = (Xpos is not None, Ypos is not None)
-        ctx.save_for_backward(X, Y, wk, wv, wq, wy, attn, saved)
+        ctx.save_for_backward(X, Y, wk, bk, wv, bv, wq, bq, wy, by, attn, saved)
         ctx.mark_non_differentiable(attn)
         return out, logit, attn
 
     @staticmethod
     def backward(ctx, dout, dlogit, dattn):
         lib = nx.load()
-        X, Y, wk, wv, wq, wy, attn, saved = ctx.saved_tensors
+        X, Y, wk, bk, wv, bv, wq, bq, wy, by, attn, saved = ctx.saved_tensors
         Nx, xdim, Ny, ydim, Hd, outdim, xpc, ypc = ctx.dims
         hx, hy = ctx.has_pos
         nd = ctx.needs_input_grad
@@ -326,14 +360,17 @@ class X2YFn(torch.autograd.Function):
         dY = _empty(Ny, ydim, device=dev) if nd[1] else None
         dXp = _empty(Nx, xpc, device=dev) if (hx and nd[2]) else None
         dYp = _empty(Ny, ypc, device=dev) if (hy and nd[3]) else None
-        g = [_empty(*t.shape, device=dev) for t in (wk, wk[:, 0], wv, wv[:, 0], wq, wq[:, 0], wy, wy[:, 0])]
+        tg = [grad_target(p, nd[4 + i]) for i, p in enumerate((wk, bk, wv, bv, wq, bq, wy, by))]
+        bufs = [t[0] for t in tg]
+        # the kernel needs every weight-gradient target; absent ones go to scratch
+        bufs = [b if b is not None else torch.zeros_like(p) for b, p in zip(bufs, (wk, bk, wv, bv, wq, bq, wy, by))]
         ws = _ws(lib.fx_x2y_workspace_floats(Nx, xdim, Ny, ydim, Hd, outdim), dev)
         _check(lib.fx_x2y_bwd(nx.ptr(X), nx.ld(X), Nx, xdim, xpc, nx.ptr(Y), nx.ld(Y), Ny, ydim, ypc,
                               nx.ptr(wk), nx.ptr(wv), nx.ptr(wq), nx.ptr(wy), Hd, outdim, nx.ptr(attn), nx.ptr(saved),
                               nx.ptr(dout), outdim, nx.ptr(dlogit), nx.ptr(dattn), nx.ptr(dX), nx.ptr(dXp),
-                              nx.ptr(dY), nx.ptr(dYp), *[nx.ptr(t) for t in g], int(hx), int(hy), nx.ptr(ws),
+                              nx.ptr(dY), nx.ptr(dYp), *[nx.ptr(t) for t in bufs], int(hx), int(hy), nx.ptr(ws),
                               nx.stream()), "fx_x2y_bwd")
-        return (dX, dY, dXp, dYp) + tuple(g)
+        return (dX, dY, dXp, dYp) + tuple(t[1] for t in tg)
 
 
 def x2y(mod, X, Y, Xpos, Ypos):
@@ -347,16 +384,14 @@ def x2y(mod, X, Y, Xpos, Ypos):
 # ---------------------------------------------------------------------------
 
 def _ptr_array(ts):
-    arr = (ctypes.c_void_p * max(len(ts), 1))(*[nx.ptr(t) for t in ts])
-    return arr
+    return (ctypes.c_void_p * max(len(ts), 1))(*[nx.ptr(t) for t in ts])
 
 
 class MSTCNFn(torch.autograd.Function):
     """Whole ``MSTCN.forward`` (basic.py:200-220) in one C call (eval-mode dropout)."""
 
     @staticmethod
-    def forward(ctx, x, meta, *params):
-        lib = nx.load()
+    def _unpack(meta, params):
         T, nvid, cin, F, cout, nl, ln, in_map, d0, dfac = meta
         it = iter(params)
         w_in = b_in = None
@@ -368,6 +403,13 @@ class MSTCNFn(torch.autograd.Function):
             lw += [next(it), next(it)] if ln else [None, None]
             layers.append(lw)
         w_out, b_out = next(it), next(it)
+        return w_in, b_in, layers, w_out, b_out
+
+    @staticmethod
+    def forward(ctx, x, meta, *params):
+        lib = nx.load()
+        T, nvid, cin, F, cout, nl, ln, in_map, d0, dfac = meta
+        w_in, b_in, layers, w_out, b_out = MSTCNFn._unpack(meta, params)
         keep = []
         prm = nx.MstcnParams()
         prm.cin, prm.F, prm.cout, prm.num_layers, prm.layernorm, prm.in_map = cin, F, cout, nl, int(ln), int(in_map)
@@ -388,7 +430,6 @@ class MSTCNFn(torch.autograd.Function):
         ctx.meta = meta
         ctx.prm = prm
         ctx.keep = keep
-        ctx.layers_shapes = [(lw[0].shape, lw[2].shape) for lw in layers]
         ctx.save_for_backward(x, saved, *params)
         return y
 
@@ -399,30 +440,22 @@ class MSTCNFn(torch.autograd.Function):
         T, nvid, cin, F, cout, nl, ln, in_map, d0, dfac = ctx.meta
         dev = x.device
         dy = dy.contiguous()
-        grads = [_empty(*p_.shape, device=dev) for p_ in params]
-        # LayerNorm gains/biases are accumulated by the kernel -> zero them
-        off = 2 if in_map else 0
-        per = 6 if ln else 4
-        if ln:
-            for i in range(nl):
-                grads[off + i * per + 4].zero_()
-                grads[off + i * per + 5].zero_()
-        it = iter(grads)
+        tg = [grad_target(p) for p in params]
+        bufs = [t[0] for t in tg]
+        w_in, b_in, layers, w_out, b_out = MSTCNFn._unpack(ctx.meta, bufs)
         g = nx.MstcnGrads()
-        if in_map:
-            g.w_in, g.b_in = nx.ptr(next(it)), nx.ptr(next(it))
-        lg = [[next(it) for _ in range(per)] for _ in range(nl)]
+        g.w_in, g.b_in = nx.ptr(w_in), nx.ptr(b_in)
         keep = []
         for field, k in (("w_dil", 0), ("b_dil", 1), ("w_pw", 2), ("b_pw", 3), ("ln_w", 4), ("ln_b", 5)):
-            arr = _ptr_array([(l_[k] if k < len(l_) else None) for l_ in lg])
+            arr = _ptr_array([lw[k] for lw in layers])
             keep.append(arr)
             setattr(g, field, ctypes.cast(arr, ctypes.c_void_p))
-        g.w_out, g.b_out = nx.ptr(next(it)), nx.ptr(next(it))
+        g.w_out, g.b_out = nx.ptr(w_out), nx.ptr(b_out)
         dx = _empty(*x.shape, device=dev) if ctx.needs_input_grad[0] else None
         ws = _ws(lib.fx_mstcn_workspace_floats(ctypes.byref(ctx.prm), x.shape[0]), dev)
         _check(lib.fx_mstcn_bwd(ctypes.byref(ctx.prm), ctypes.byref(g), nx.ptr(x), nx.ld(x), T, nvid, nx.ptr(dy),
                                 cout, nx.ptr(dx), nx.ld(dx), nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_mstcn_bwd")
-        return (dx, None) + tuple(grads)
+        return (dx, None) + tuple(t[1] for t in tg)
 
 
 def mstcn(mod, x, T, nvid=1):
@@ -463,7 +496,7 @@ def _rows_operand(t, trans=False):
 
 
 def gemm(M, N, K, a, b, c, ldc, bias=None, relu=0, resid=None, alpha=1.0, beta=0.0, gate=None, c_tap_cin=0,
-         split=1):
+         split=1, c_last=None):
     lib = nx.load()
     d = nx.GemmDesc()
     d.M, d.N, d.K, d.batch = M, N, K, 1
@@ -474,6 +507,7 @@ def gemm(M, N, K, a, b, c, ldc, bias=None, relu=0, resid=None, alpha=1.0, beta=0
     d.resid, d.ld_resid = nx.ptr(resid), nx.ld(resid)
     d.gate, d.ld_gate = nx.ptr(gate), nx.ld(gate)
     d.relu, d.c_tap_cin = relu, c_tap_cin
+    d.c_last_col = nx.ptr(c_last)
     d.split_k = split
     ws = None
     if split > 1:
@@ -494,42 +528,35 @@ class Conv3Fn(torch.autograd.Function):
         y = _empty(rows, cout, device=x.device)
         gemm(rows, cout, 3 * cin, _conv_operand(x, cin, dil, 1, T, False), _rows_operand(wf), y, cout, bias=b)
         ctx.dil, ctx.T = dil, T
-        ctx.save_for_backward(x, w)
+        ctx.save_for_backward(x, w, b)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
+        x, w, b = ctx.saved_tensors
+        nd = ctx.needs_input_grad
         dy = dy.contiguous()
         rows, cin = x.shape
         cout = w.shape[0]
         dev = x.device
-        dx = dw = db = None
-        if ctx.needs_input_grad[0]:
+        dx = None
+        if nd[0]:
             wb = w.permute(1, 2, 0).reshape(cin, 3 * cout).contiguous()   # [c][tap][n]
             dx = _empty(rows, cin, device=dev)
             gemm(rows, cin, 3 * cout, _conv_operand(dy, cout, ctx.dil, -1, ctx.T, False), _rows_operand(wb), dx, cin)
-        if ctx.needs_input_grad[1]:
-            dw = _empty(*w.shape, device=dev)
+        dwb, dw_ret = grad_target(w, nd[1])
+        dbb, db_ret = grad_target(b, nd[2])
+        if dwb is not None:
+            bop = _conv_operand(x, cin, ctx.dil, 1, ctx.T, True)
+            ncol = 3 * cin + (1 if dbb is not None else 0)
+            if dbb is not None:
+                bop.ones_col = ncol
             split = max(1, min(16, rows // 256))
-            gemm(cout, 3 * cin, rows, _rows_operand(dy, trans=True), _conv_operand(x, cin, ctx.dil, 1, ctx.T, True),
-                 dw, 3 * cin, c_tap_cin=cin, split=split)
-        if ctx.needs_input_grad[2]:
-            db = _colsum(dy)
-        return dx, dw, db, None, None
-
-
-def _colsum(t):
-    """Column sums (bias gradient) through fx_linear_bwd with dx/dw disabled."""
-    lib = nx.load()
-    M, N = t.shape
-    db = _empty(N, device=t.device)
-    ws = _ws(lib.fx_linear_bwd_workspace_floats(M, 1, N), t.device)
-    dummy_x = torch.empty(M, 1, device=t.device, dtype=_f32)
-    dummy_w = torch.empty(N, 1, device=t.device, dtype=_f32)
-    _check(lib.fx_linear_bwd(nx.ptr(t), nx.ld(t), nx.ptr(dummy_x), 1, nx.ptr(dummy_w), 1, None, 0, M, 1, N, None, 0,
-                             None, 0, nx.ptr(db), 0, nx.ptr(ws), nx.stream()), "colsum")
-    return db
+            gemm(cout, ncol, rows, _rows_operand(dy, trans=True), bop, dwb, 3 * cin, c_tap_cin=cin, split=split,
+                 beta=1.0, c_last=dbb)
+        elif dbb is not None:
+            dbb += dy.sum(0)
+        return dx, dw_ret, db_ret, None, None
 
 
 def conv3(x, w, b, dil, T):
@@ -555,27 +582,27 @@ class GRUFn(torch.autograd.Function):
         _check(lib.fx_gru_bidir_fwd(nx.ptr(x), nx.ld(x), S, In, Hh, nx.ptr(w_ih), nx.ptr(w_hh), nx.ptr(b_ih),
                                     nx.ptr(b_hh), nx.ptr(w_ih_r), nx.ptr(w_hh_r), nx.ptr(b_ih_r), nx.ptr(b_hh_r),
                                     nx.ptr(out), 2 * Hh, nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_gru_bidir_fwd")
-        ctx.save_for_backward(x, w_ih, w_hh, w_ih_r, w_hh_r, saved)
+        ctx.save_for_backward(x, w_ih, w_hh, b_ih, b_hh, w_ih_r, w_hh_r, b_ih_r, b_hh_r, saved)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         lib = nx.load()
-        x, w_ih, w_hh, w_ih_r, w_hh_r, saved = ctx.saved_tensors
+        x, *w, saved = ctx.saved_tensors
+        w_ih, w_hh, _, _, w_ih_r, w_hh_r, _, _ = w
         dout = dout.contiguous()
         S, In = x.shape
         Hh = w_hh.shape[1]
         dev = x.device
         nd = ctx.needs_input_grad
         dx = _empty(S, In, device=dev) if nd[0] else None
-        g = [_empty(*t.shape, device=dev) for t in (w_ih, w_hh, w_ih[:, 0], w_hh[:, 0],
-                                                    w_ih_r, w_hh_r, w_ih_r[:, 0], w_hh_r[:, 0])]
+        tg = [grad_target(p, nd[1 + i]) for i, p in enumerate(w)]
+        bufs = [t[0] for t in tg]
         ws = _ws(lib.fx_gru_workspace_floats(S, In, Hh), dev)
         _check(lib.fx_gru_bidir_bwd(nx.ptr(x), nx.ld(x), S, In, Hh, nx.ptr(w_ih), nx.ptr(w_hh), nx.ptr(w_ih_r),
                                     nx.ptr(w_hh_r), nx.ptr(saved), nx.ptr(dout), 2 * Hh, nx.ptr(dx), nx.ld(dx),
-                                    *[nx.ptr(t) for t in g], nx.ptr(ws), nx.stream()), "fx_gru_bidir_bwd")
-        # argument order of GRUFn.forward: w_ih, w_hh, b_ih, b_hh, (same)_r
-        return (dx, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7])
+                                    *[nx.ptr(t) for t in bufs], nx.ptr(ws), nx.stream()), "fx_gru_bidir_bwd")
+        return (dx,) + tuple(t[1] for t in tg)
 
 
 def gru(mod, x):
@@ -598,11 +625,9 @@ def segments_from_probs(x2d, col0, ncls):
     lib = nx.load()
     T = x2d.shape[0]
     dev = x2d.device
-    pred = torch.empty(T, device=dev, dtype=torch.int32)
-    seg_id = torch.empty(T, device=dev, dtype=torch.int32)
-    st = torch.empty(T, device=dev, dtype=torch.int32)
-    en = torch.empty(T, device=dev, dtype=torch.int32)
-    ns = torch.empty(1, device=dev, dtype=torch.int32)
+    buf = torch.empty(4 * T + 1, device=dev, dtype=torch.int32)
+    pred, seg_id, st, en = buf[:T], buf[T:2 * T], buf[2 * T:3 * T], buf[3 * T:4 * T]
+    ns = buf[4 * T:]
     _check(lib.fx_segments_from_probs(nx.ptr(x2d), nx.ld(x2d), col0, ncls, T, nx.ptr(pred), nx.ptr(seg_id),
                                       nx.ptr(st), nx.ptr(en), nx.ptr(ns), nx.stream()), "fx_segments_from_probs")
     S = int(ns.item())
@@ -660,24 +685,25 @@ class SegMergeFn(torch.autograd.Function):
         a.rows0 = nx.ptr(seg_id)
         a.ptr1, a.ld1, a.k_split = nx.ptr(frame), nx.ld(frame), Fs
         gemm(T, N, Fs + H, a, _rows_operand(w), y, N, bias=b, relu=1)
-        ctx.save_for_backward(seg, frame, st, en, w, y)
+        ctx.save_for_backward(seg, frame, st, en, w, b, y)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         lib = nx.load()
-        seg, frame, st, en, w, y = ctx.saved_tensors
+        seg, frame, st, en, w, b, y = ctx.saved_tensors
+        nd = ctx.needs_input_grad
         dy = dy.contiguous()
         T, N = y.shape
         Fs = seg.shape[1]
-        dev = dy.device
-        dz = _empty(T, N, device=dev)
+        dz = _empty(T, N, device=dy.device)
         _check(lib.fx_relu_bwd(nx.ptr(dy), N, nx.ptr(y), N, T, N, nx.ptr(dz), N, nx.stream()), "fx_relu_bwd")
         dzs = seg_sum_rows(dz, st, en)                        # gather backward folded before the GEMM
-        dseg, dws, _ = lin_bwd(dzs, seg, w[:, :Fs], True, True, False)
-        dframe, dwf, db = lin_bwd(dz, frame, w[:, Fs:], True, True, True)
-        dw = torch.cat([dws, dwf], 1)
-        return dseg, dframe, None, None, None, dw, db
+        dwb, dw_ret = grad_target(w, nd[5])
+        dbb, db_ret = grad_target(b, nd[6])
+        dseg = lin_bwd(dzs, seg, w[:, :Fs], nd[0], None if dwb is None else dwb[:, :Fs])
+        dframe = lin_bwd(dz, frame, w[:, Fs:], nd[1], None if dwb is None else dwb[:, Fs:], dbb)
+        return dseg, dframe, None, None, None, dw_ret, db_ret
 
 
 # ---------------------------------------------------------------------------
@@ -690,7 +716,3 @@ def add_(a, b):
     rows, cols = a.shape
     _check(lib.fx_add(nx.ptr(b), nx.ld(b), None, 0, rows, cols, nx.ptr(a), nx.ld(a), 1, nx.stream()), "fx_add")
     return a
-
-
-def mha_scale(hd):
-    return 1.0 / math.sqrt(hd)

@@ -28,14 +28,14 @@ class FactmxNativeError(RuntimeError):
 class Operand(ctypes.Structure):
     _fields_ = [("ptr", P), ("ld", L), ("ptr1", P), ("ld1", L), ("k_split", I), ("rows0", P), ("rows1", P),
                 ("pos", P), ("ld_pos", L), ("pos_cols", I), ("trans", I), ("conv_taps", I), ("conv_cin", I),
-                ("conv_dil", I), ("conv_dir", I), ("seq_len", I), ("batch_stride", L)]
+                ("conv_dil", I), ("conv_dir", I), ("seq_len", I), ("batch_stride", L), ("ones_col", I)]
 
 
 class GemmDesc(ctypes.Structure):
     _fields_ = [("M", I), ("N", I), ("K", I), ("batch", I), ("a", Operand), ("b", Operand), ("c", P), ("ldc", L),
                 ("c_batch_stride", L), ("alpha", F), ("beta", F), ("bias", P), ("resid", P), ("ld_resid", L),
                 ("resid_batch_stride", L), ("gate", P), ("ld_gate", L), ("relu", I), ("c_tap_cin", I),
-                ("split_k", I), ("workspace", P)]
+                ("split_k", I), ("workspace", P), ("c_last_col", P)]
 
 
 class MstcnParams(ctypes.Structure):
@@ -57,7 +57,7 @@ SIGNATURES = {
     "fx_gemm_workspace_floats": (L, [ctypes.POINTER(GemmDesc)]),
     "fx_linear_fwd": (I, [P, L, P, L, I, I, I, P, L, P, P, L, I, I, P]),
     "fx_linear_bwd_workspace_floats": (L, [I, I, I]),
-    "fx_linear_bwd": (I, [P, L, P, L, P, L, P, L, I, I, I, P, L, P, L, P, I, P, P]),
+    "fx_linear_bwd": (I, [P, L, P, L, P, L, P, L, I, I, I, P, L, P, L, P, I, I, P, P]),
     "fx_x2y_saved_floats": (L, [I, I, I, I, I]),
     "fx_x2y_workspace_floats": (L, [I, I, I, I, I, I]),
     "fx_x2y_fwd": (I, [P, L, I, I, P, L, I, P, L, I, I, P, L, I, P, P, P, P, P, P, P, P, I, I, P, L, P, P, P, P, P]),

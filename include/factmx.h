@@ -79,6 +79,7 @@ typedef struct fx_operand {
   int conv_dir;
   int seq_len;
   long long batch_stride;
+  int ones_col;               /* != 0: logical row ones_col-1 reads 1.0 (fused bias gradient) */
 } fx_operand;
 
 typedef struct fx_gemm_desc {
@@ -99,6 +100,7 @@ typedef struct fx_gemm_desc {
   int c_tap_cin;              /* != 0: column n = tap*c_tap_cin + c stored at c*3 + tap */
   int split_k;                /* >1: K split over workgroups, partials in workspace */
   float* workspace;
+  float* c_last_col;          /* != NULL: output column N-1 goes to c_last_col[m] (bias grad) */
 } fx_gemm_desc;
 
 int fx_gemm(const fx_gemm_desc* desc, void* stream);
@@ -111,8 +113,14 @@ long long fx_gemm_workspace_floats(const fx_gemm_desc* desc);
  *        w is (N, K) with row stride ldw; pos nullable (add_positional_encoding
  *        fused into the operand load, basic.py:313-320).
  *   bwd: dx (lddx) [+]= dy . w ;  dw (lddw) [+]= dy^T . x ;  db [+]= colsum(dy).
- *        Any of dx/dw/db may be NULL.  accumulate != 0 adds into dx/dw/db.
+ *        Any of dx/dw/db may be NULL.  accumulate_dx / accumulate_w select
+ *        += for dx and for dw/db.  db rides in the dw GEMM as a virtual
+ *        all-ones column of x (no separate reduction launch).
  *        relu_out (nullable): the forward output, gates dy by (relu_out>0).
+ *
+ * Gradient convention of every composite backward below: weight and bias
+ * gradients are ACCUMULATED (+=) into the caller's buffers (the framework
+ * points them at param.grad); input gradients are written.
  * ---------------------------------------------------------------------- */
 int fx_linear_fwd(const float* x, long long ldx, const float* pos, long long ldpos, int pos_cols,
                   int M, int K, const float* w, long long ldw, const float* b, float* y,
@@ -120,8 +128,8 @@ int fx_linear_fwd(const float* x, long long ldx, const float* pos, long long ldp
 long long fx_linear_bwd_workspace_floats(int M, int K, int N);
 int fx_linear_bwd(const float* dy, long long lddy, const float* x, long long ldx, const float* w,
                   long long ldw, const float* relu_out, long long ld_relu, int M, int K, int N,
-                  float* dx, long long lddx, float* dw, long long lddw, float* db, int accumulate,
-                  float* workspace, void* stream);
+                  float* dx, long long lddx, float* dw, long long lddw, float* db, int accumulate_dx,
+                  int accumulate_w, float* workspace, void* stream);
 
 /* ------------------------------------------------------------------------
  * X2Y_map, whole layer (basic.py:349-389, kq_pos=True as built by
@@ -132,7 +140,7 @@ int fx_linear_bwd(const float* dy, long long lddy, const float* x, long long ldx
  * logit and attn are outputs (the losses read them, blocks.py:363-366).
  * Positional tensors cover the first *pos_cols channels (nullable).
  * bwd: dout, optional direct dlogit / dattn (Ny, Nx) -> dX, dXpos, dY, dYpos
- *   (nullable) and every weight/bias gradient (written, not accumulated).
+ *   (nullable) and every weight/bias gradient (accumulated, all required).
  * ---------------------------------------------------------------------- */
 long long fx_x2y_saved_floats(int Nx, int xdim, int Ny, int ydim, int Hd);
 long long fx_x2y_workspace_floats(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim);
@@ -275,7 +283,7 @@ int fx_seg_sum_rows(const float* dx, long long lddx, const int32_t* seg_start, c
  *   x (S, In) -> out (S, 2*Hh) = [forward h_t, backward h_t]; Hh <= 256.
  *   saved (fx_gru_saved_floats): per-step h_{t-1} and gates for backward.
  * bwd: dout (S, 2Hh) -> dx (nullable) and every weight/bias gradient
- *   (written, not accumulated; each pointer nullable).
+ *   (accumulated +=; each pointer nullable).
  * ---------------------------------------------------------------------- */
 long long fx_gru_saved_floats(int S, int Hh);
 long long fx_gru_workspace_floats(int S, int In, int Hh);
