@@ -146,9 +146,9 @@ int add2(const float* a, long long lda, const float* b, long long ldb, int rows,
 // split-K factor for small-output / long-K products (dW over frames, token x frame)
 int pick_split(int M, int N, int K, int batch = 1) {
   const long long tiles = (long long)cdiv(M, 64) * cdiv(N, 64) * batch;
-  const int nkt = cdiv(K, 32);
-  if (tiles >= 160 || nkt < 8) return 1;
-  int sp = (int)std::min<long long>(nkt / 4, cdiv(320, tiles));
+  const int nkt = cdiv(K, 64);   // 64-deep K stages of the GEMM kernel
+  if (tiles >= 160 || nkt < 4) return 1;
+  int sp = (int)std::min<long long>(nkt / 2, cdiv(256, tiles));
   return std::max(sp, 1);
 }
 

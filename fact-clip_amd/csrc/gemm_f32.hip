@@ -1,27 +1,37 @@
 // f32 GEMM on CDNA4 matrix cores: v_mfma_f32_32x32x2_f32 (exact f32 products,
 // k-ordered fma chain; no xf32 on gfx950, so the parity path stays fp32).
 //
-// One kernel covers every dense contraction of the FACT frame/action branches:
-//   * Linear / Conv1d(k=1) forward:        A=x (rows), B=W (rows, = N x K)
-//   * implicit dilated Conv1d(k=3):        A = x gathered per tap (conv_taps=3)
-//   * dX of both (B = W read K-major, taps reversed for the conv)
-//   * dW = dY^T X (A read column-major, split-K over the frame axis)
-//   * concatenated inputs (Y_W(cat[Y, feat]), sf_merge) and row gathers
-// Tile: 64x64 output per 256-thread workgroup, 4 waves each owning a 32x32
-// accumulator (16 f32 AGPR/VGPR per lane), K staged through LDS in 32-deep
-// slices with a register prefetch of the next slice (one barrier per slice).
-// LDS images are stored [k][row] with a +1 pad: MFMA operand reads are
-// ds_read_b32 of 32 consecutive rows (conflict-free), staging writes are at
-// most 2-way (free for ds_write_b32 on gfx950).
+// One kernel template covers every dense contraction of the FACT frame/action
+// branches; the operand loader is specialised at compile time:
+//   ROWS      element (r,k) = p[r*ld + k]            Linear/Conv1d(k=1) fwd, B = W
+//   ROWS_CONV implicit dilated Conv1d(k=3): row r shifted by the tap of k, zero
+//             outside the video (fwd and, with reversed taps, dX)
+//   ROWS_GEN  concatenated inputs / row gathers / positional adds (generic)
+//   COLS      element (r,k) = p[k*ld + r]            dY^T for dW, W^T for dX
+//   COLS_CONV conv input for dW, tap from r; optional all-ones row (bias grad)
+// Tile: 64x64 output per 256-thread workgroup (4 waves x 32x32 accumulator,
+// 16 f32 per lane), K staged through LDS in 32-deep slices with a register
+// prefetch of the next slice (one barrier per slice).  All per-thread address
+// arithmetic is hoisted out of the K loop; inside it only pointer increments,
+// a tap lookup on uniform values, and two float4 loads per operand remain.
+// LDS images are [k][row] with a +1 pad: MFMA operand reads are ds_read_b32 of
+// 32 consecutive rows (conflict-free), staging writes at most 2-way.
+// Blocks are remapped so that consecutive output tiles share an XCD (L2).
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 #include "fx_common.h"
 
 namespace fx {
 namespace {
 
-constexpr int BM = 64, BN = 64, BK = 32, NTHREADS = 256, LDSS = 65;
+// BK: K depth per LDS stage (one barrier per 32 MFMAs per wave); loaders move it in
+// two BKH-deep halves (8 elements per thread each).
+constexpr int BM = 64, BN = 64, BK = 64, BKH = 32, NTHREADS = 512, LDSS = 65;
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+enum Kind { ROWS = 0, ROWS_CONV = 1, ROWS_GEN = 2, COLS = 3, COLS_CONV = 4 };
 
 struct GemmDev {
   int M, N, K;
@@ -37,13 +47,33 @@ struct GemmDev {
   int relu, split, kt_per_split, a_vec, b_vec, c_tap_cin;
   float* ws;
   float* c_last;
+  int tiles_x, tiles_y;
+  long long* stamps;
 };
+
+// Diagnostic builds (-DFX_STAMPS) record s_memtime / s_memrealtime at fixed points of
+// every block; the shipped library compiles the macro to nothing.
+#ifdef FX_STAMPS
+#define FX_STAMP(g, slot)                                                                          \
+  do {                                                                                            \
+    if ((g).stamps && (threadIdx.x & 255) == 0) {                                                 \
+      const long long _b = (long long)blockIdx.z * gridDim.x * gridDim.y + blockIdx.y * gridDim.x + \
+                           blockIdx.x;                                                            \
+      (g).stamps[(_b * 2 + (threadIdx.x >> 8)) * 10 + 2 * (slot)] = __builtin_amdgcn_s_memtime();    \
+      (g).stamps[(_b * 2 + (threadIdx.x >> 8)) * 10 + 2 * (slot) + 1] = __builtin_amdgcn_s_memrealtime(); \
+    }                                                                                             \
+  } while (0)
+#else
+#define FX_STAMP(g, slot) \
+  do {                    \
+  } while (0)
+#endif
 
 __device__ __forceinline__ int conv_shift(const fx_operand& o, int tap) {
   return (tap - (o.conv_taps - 1) / 2) * o.conv_dil * o.conv_dir;
 }
 
-// element (r,k) of a trans==0 operand; r < R, k < K guaranteed by the caller
+// ---------------------------------------------------------------- generic element fetch
 __device__ __forceinline__ float fetch_rm(const fx_operand& o, const float* p0, int r, int k) {
   if (o.conv_taps) {
     const int j = k / o.conv_cin, c = k - j * o.conv_cin, s = conv_shift(o, j);
@@ -61,7 +91,6 @@ __device__ __forceinline__ float fetch_rm(const fx_operand& o, const float* p0, 
   return v;
 }
 
-// element (r,k) of a trans==1 operand
 __device__ __forceinline__ float fetch_cm(const fx_operand& o, const float* p0, int r, int k) {
   if (o.ones_col && r == o.ones_col - 1) return 1.f;
   if (o.conv_taps) {
@@ -73,107 +102,128 @@ __device__ __forceinline__ float fetch_cm(const fx_operand& o, const float* p0, 
   return p0[(long long)k * o.ld + r];
 }
 
-// 8 consecutive k of row r (trans==0)
-__device__ __forceinline__ void load_rm8(const fx_operand& o, const float* p0, int r, int R, int k,
-                                         int K, bool vec, float* v) {
-  if (r >= R) {
+__device__ __forceinline__ void zero8(float* v) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = 0.f;
-    return;
+  for (int e = 0; e < 8; ++e) v[e] = 0.f;
+}
+
+__device__ __forceinline__ void ld8(const float* src, float* v) {
+  const float4 x0 = *reinterpret_cast<const float4*>(src);
+  const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
+  v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
+  v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+}
+
+// ---------------------------------------------------------------- loaders
+// Each thread owns 8 elements of the 64 x 32 (rows x k) tile:
+//   row-major kinds: row = tid/4, k = (tid%4)*8 .. +7
+//   col-major kinds: row = (tid%8)*8 .. +7, k = tid/8
+// The fast path is chosen per TILE with a wave-uniform condition (whole 64-row
+// tile and 32-deep slice in range, 16-B aligned, no ones row) so the prefetch
+// loads are straight-line code: divergent bounds branches would make the
+// compiler drain vmcnt between the A and B prefetches.  Per-row validity of the
+// conv gather is a select, not a branch.  Edge tiles take the generic path.
+template <int KIND>
+struct Loader {
+  const fx_operand* o;
+  const float* base;  // operand base incl. batch offset
+  int R, K;
+  bool tile_fast;     // uniform: rows of this tile all in range, operand vector-loadable
+  int r;              // row (row-major) or first row of the 8-chunk (col-major)
+  int kk;             // k offset inside the tile
+  int rmod;           // r % seq_len (ROWS_CONV)
+  int tapc, tap_s;    // COLS_CONV: channel and shift of this thread's rows
+
+  __device__ __forceinline__ void init(const fx_operand& op, const float* p0, int r0, int R_, int K_, bool v, int tid) {
+    o = &op;
+    base = p0;
+    R = R_;
+    K = K_;
+    tile_fast = v && (r0 + 64 <= R_) && !(op.ones_col && r0 + 64 >= op.ones_col);
+    if (KIND <= ROWS_GEN) {
+      r = r0 + (tid >> 2);
+      kk = (tid & 3) * 8;
+      if (KIND == ROWS_CONV) rmod = r % op.seq_len;
+    } else {
+      r = r0 + (tid & 7) * 8;
+      kk = tid >> 3;
+      if (KIND == COLS_CONV) {
+        const int j = r / op.conv_cin;
+        tapc = r - j * op.conv_cin;
+        tap_s = conv_shift(op, j);
+      }
+    }
   }
-  if (vec && k + 8 <= K) {
-    const float* src;
-    bool pos_add = false;
-    if (o.conv_taps) {
-      const int j = k / o.conv_cin, c = k - j * o.conv_cin, s = conv_shift(o, j);
-      const int t = r % o.seq_len + s;
-      if (t < 0 || t >= o.seq_len) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = 0.f;
+
+  __device__ __forceinline__ void load_generic(int k0, float* v) const {
+    if (KIND <= ROWS_GEN) {
+      const int k = k0 + kk;
+      if (r >= R) {
+        zero8(v);
         return;
       }
-      src = p0 + (long long)(r + s) * o.ld + c;
-    } else if (o.ptr1 && k >= o.k_split) {
-      const int rr = o.rows1 ? o.rows1[r] : r;
-      src = o.ptr1 + (long long)rr * o.ld1 + (k - o.k_split);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (k + e < K) ? fetch_rm(*o, base, r, k + e) : 0.f;
     } else {
-      const int rr = o.rows0 ? o.rows0[r] : r;
-      src = p0 + (long long)rr * o.ld + k;
-      pos_add = o.pos && k < o.pos_cols;
-    }
-    const float4 x0 = *reinterpret_cast<const float4*>(src);
-    const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
-    v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
-    v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
-    if (pos_add) {
-      const float* pp = o.pos + (long long)r * o.ld_pos;
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        if (k + e < o.pos_cols) v[e] += pp[k + e];
-    }
-    return;
-  }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = (k + e < K) ? fetch_rm(o, p0, r, k + e) : 0.f;
-}
-
-// 8 consecutive rows r..r+7 at one k (trans==1)
-__device__ __forceinline__ void load_cm8(const fx_operand& o, const float* p0, int r, int R, int k,
-                                         int K, bool vec, float* v) {
-  if (k >= K) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = 0.f;
-    return;
-  }
-  if (vec && r + 8 <= R && !(o.ones_col && r + 8 >= o.ones_col)) {
-    const float* src;
-    if (o.conv_taps) {
-      const int j = r / o.conv_cin, c = r - j * o.conv_cin, s = conv_shift(o, j);
-      const int t = k % o.seq_len + s;
-      if (t < 0 || t >= o.seq_len) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = 0.f;
+      const int k = k0 + kk;
+      if (k >= K) {
+        zero8(v);
         return;
       }
-      src = p0 + (long long)(k + s) * o.ld + c;
-    } else {
-      src = p0 + (long long)k * o.ld + r;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (r + e < R) ? fetch_cm(*o, base, r + e, k) : 0.f;
     }
-    const float4 x0 = *reinterpret_cast<const float4*>(src);
-    const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
-    v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
-    v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
-    return;
   }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = (r + e < R) ? fetch_cm(o, p0, r + e, k) : 0.f;
-}
 
-template <bool TR>
-__device__ __forceinline__ void load_tile(const fx_operand& o, const float* p0, int r0, int R, int k0,
-                                          int K, bool vec, int tid, float* v) {
-  if (!TR) load_rm8(o, p0, r0 + (tid >> 2), R, k0 + (tid & 3) * 8, K, vec, v);
-  else load_cm8(o, p0, r0 + (tid & 7) * 8, R, k0 + (tid >> 3), K, vec, v);
-}
-
-template <bool TR>
-__device__ __forceinline__ void store_tile(float (*s)[LDSS], int tid, const float* v) {
-  if (!TR) {
-    const int r = tid >> 2, kq = (tid & 3) * 8;
+  __device__ __forceinline__ void load(int k0, float* v) const {
+    const bool fast = tile_fast && (k0 + BKH <= K);
+    if (KIND == ROWS_GEN || !fast) {
+      load_generic(k0, v);
+      return;
+    }
+    if (KIND == ROWS) {
+      ld8(base + (long long)r * o->ld + k0 + kk, v);
+    } else if (KIND == ROWS_CONV) {
+      // the 32-deep slice lies in one tap (conv_cin % 32 == 0, checked on the host)
+      const int j = k0 / o->conv_cin;
+      const int c = k0 - j * o->conv_cin + kk;
+      const int s = conv_shift(*o, j);
+      const int t = rmod + s;
+      const bool ok = t >= 0 && t < o->seq_len;
+      ld8(base + (long long)(ok ? r + s : r) * o->ld + c, v);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) s[kq + e][r] = v[e];
-  } else {
-    const int k = tid >> 3, rq = (tid & 7) * 8;
+      for (int e = 0; e < 8; ++e) v[e] = ok ? v[e] : 0.f;
+    } else if (KIND == COLS) {
+      ld8(base + (long long)(k0 + kk) * o->ld + r, v);
+    } else {  // COLS_CONV
+      const int k = k0 + kk;
+      const int t = k % o->seq_len + tap_s;
+      const bool ok = t >= 0 && t < o->seq_len;
+      ld8(base + (long long)(ok ? k + tap_s : k) * o->ld + tapc, v);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) s[k][rq + e] = v[e];
+      for (int e = 0; e < 8; ++e) v[e] = ok ? v[e] : 0.f;
+    }
   }
-}
+
+  __device__ __forceinline__ void store(float (*s)[LDSS], int tid, const float* v) const {
+    if (KIND <= ROWS_GEN) {
+      const int rl = tid >> 2;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[kk + e][rl] = v[e];
+    } else {
+      const int rq = (tid & 7) * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[kk][rq + e] = v[e];
+    }
+  }
+};
 
 // epilogue: v = alpha*acc (+bias) [relu==2: ReLU here] (+resid) (+beta*C_old) (*gate>0) [relu==1: ReLU]
 // c_tap_cin != 0: output column n = tap*c_tap_cin + c is stored at c*3 + tap (Conv1d weight layout)
+// c_last != NULL: output column N-1 goes to c_last[m] (fused bias gradient)
 __device__ __forceinline__ void epilogue_store(const GemmDev& g, int b, int m, int n, float acc) {
   float v = g.alpha * acc;
-  if (g.c_last && n == g.N - 1) {   // fused bias-gradient column
+  if (g.c_last && n == g.N - 1) {
     float* cp = g.c_last + (long long)b * g.M + m;
     if (g.beta != 0.f) v += g.beta * (*cp);
     *cp = v;
@@ -194,65 +244,138 @@ __device__ __forceinline__ void epilogue_store(const GemmDev& g, int b, int m, i
   *cp = v;
 }
 
-template <bool ATR, bool BTR>
+template <int AK, int BKIND>
 __global__ __launch_bounds__(NTHREADS) void gemm_f32_kernel(GemmDev g) {
   __shared__ float sA[2][BK][LDSS];
   __shared__ float sB[2][BK][LDSS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1, li = lane & 31, lh = lane >> 5;
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  // 8 waves: waves 0-3 multiply k rows [0,32) of every stage, waves 4-7 rows [32,64), into
+  // separate accumulators of the same 32x32 sub-tile -> two independent MFMA chains per SIMD,
+  // so one wave's loads / selects / LDS traffic hide under the other wave's MFMAs.
+  const int kh = wave >> 2, koff = kh * BKH, ltid = tid & 255;
+  const int wq = wave & 3, wm = wq >> 1, wn = wq & 1, li = lane & 31, lh = lane >> 5;
+  // XCD-aware remap of (x, y) tiles: consecutive remapped ids share an XCD (L2)
+  int tx, ty;
+  {
+    const int nt = g.tiles_x * g.tiles_y;
+    const int id = blockIdx.y * g.tiles_x + blockIdx.x;
+    const int q = nt / 8, rr = nt % 8, x8 = id % 8, i8 = id / 8;
+    const int nid = (x8 < rr ? x8 * (q + 1) : rr * (q + 1) + (x8 - rr) * q) + i8;
+    ty = nid / g.tiles_x;
+    tx = nid - ty * g.tiles_x;
+  }
+  const int n0 = tx * BN, m0 = ty * BM;
   const int z = blockIdx.z, bidx = z / g.split, sk = z - bidx * g.split;
-  const float* pa = g.a.ptr + (long long)bidx * g.a.batch_stride;
-  const float* pb = g.b.ptr + (long long)bidx * g.b.batch_stride;
   const int nkt = (g.K + BK - 1) / BK;
   const int kt0 = sk * g.kt_per_split;
   const int kt1 = min(nkt, kt0 + g.kt_per_split);
 
+  Loader<AK> la;
+  Loader<BKIND> lb;
+  la.init(g.a, g.a.ptr + (long long)bidx * g.a.batch_stride, m0, g.M, g.K, g.a_vec, ltid);
+  lb.init(g.b, g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, g.b_vec, ltid);
+
   f32x16 acc;
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  FX_STAMP(g, 0);
 
-  float ra[8], rb[8];
+  // Each thread stages one 8-element chunk per operand per stage (its wave group's k half).
+  // Global loads run TWO stages ahead in ping-pong register sets (r*0 / r*1, static names:
+  // a runtime-indexed register array would spill to scratch), so a stage's loads have two
+  // MFMA phases to land before they are written to LDS.
+  float ra0[8], rb0[8], ra1[8], rb1[8];
   if (kt0 < kt1) {
-    load_tile<ATR>(g.a, pa, m0, g.M, kt0 * BK, g.K, g.a_vec, tid, ra);
-    load_tile<BTR>(g.b, pb, n0, g.N, kt0 * BK, g.K, g.b_vec, tid, rb);
-    store_tile<ATR>(sA[0], tid, ra);
-    store_tile<BTR>(sB[0], tid, rb);
+    la.load(kt0 * BK + koff, ra0);
+    lb.load(kt0 * BK + koff, rb0);
+    if (kt0 + 1 < kt1) {
+      la.load((kt0 + 1) * BK + koff, ra1);
+      lb.load((kt0 + 1) * BK + koff, rb1);
+    }
+    la.store(sA[0] + koff, ltid, ra0);
+    lb.store(sB[0] + koff, ltid, rb0);
   }
   __syncthreads();
-  for (int kt = kt0; kt < kt1; ++kt) {
-    const int cur = (kt - kt0) & 1;
-    const bool more = kt + 1 < kt1;
-    if (more) {
-      load_tile<ATR>(g.a, pa, m0, g.M, (kt + 1) * BK, g.K, g.a_vec, tid, ra);
-      load_tile<BTR>(g.b, pb, n0, g.N, (kt + 1) * BK, g.K, g.b_vec, tid, rb);
+  auto stage = [&](int kt, int cur, float* ra_free, float* rb_free, const float* ra_next, const float* rb_next) {
+    if (kt + 2 < kt1) {
+      la.load((kt + 2) * BK + koff, ra_free);
+      lb.load((kt + 2) * BK + koff, rb_free);
     }
+    // every fragment read of the half-stage first, so LDS latency overlaps the MFMA chain
+    float av[BKH / 2], bv[BKH / 2];
 #pragma unroll
-    for (int s = 0; s < BK / 2; ++s) {
-      const float av = sA[cur][2 * s + lh][wm * 32 + li];
-      const float bv = sB[cur][2 * s + lh][wn * 32 + li];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+    for (int s = 0; s < BKH / 2; ++s) {
+      av[s] = sA[cur][koff + 2 * s + lh][wm * 32 + li];
+      bv[s] = sB[cur][koff + 2 * s + lh][wn * 32 + li];
     }
-    if (more) {
-      store_tile<ATR>(sA[cur ^ 1], tid, ra);
-      store_tile<BTR>(sB[cur ^ 1], tid, rb);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < BKH / 2; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
+    if (kt + 1 < kt1) {
+      la.store(sA[cur ^ 1] + koff, ltid, ra_next);
+      lb.store(sB[cur ^ 1] + koff, ltid, rb_next);
     }
     __syncthreads();
+  };
+  FX_STAMP(g, 1);
+  for (int kt = kt0; kt < kt1; kt += 2) {
+    stage(kt, 0, ra0, rb0, ra1, rb1);               // set 0 held stage kt (already in LDS): refill it
+    if (kt + 1 < kt1) stage(kt + 1, 1, ra1, rb1, ra0, rb0);
+  }
+
+  FX_STAMP(g, 2);
+  // combine the two k-half accumulators through LDS (fixed order: deterministic)
+  {
+    float* red = &sA[0][0][0];
+    if (kh == 1) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[(wq * 16 + r) * 64 + lane] = acc[r];
+    }
+    __syncthreads();
+    if (kh == 1) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] += red[(wq * 16 + r) * 64 + lane];
   }
 
   // C/D layout of the 32x32 f32 accumulator: col = lane&31, row = (r&3)+8*(r>>2)+4*(lane>>5)
   const int col = n0 + wn * 32 + li;
   if (col >= g.N) return;
+  const int rbase = m0 + wm * 32 + 4 * lh;
+  if (g.split > 1) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-    if (row >= g.M) continue;
-    if (g.split > 1) {
-      g.ws[(((long long)bidx * g.split + sk) * g.M + row) * g.N + col] = acc[r];
-    } else {
-      epilogue_store(g, bidx, row, col, acc[r]);
+    for (int r = 0; r < 16; ++r) {
+      const int row = rbase + (r & 3) + 8 * (r >> 2);
+      if (row < g.M) g.ws[(((long long)bidx * g.split + sk) * g.M + row) * g.N + col] = acc[r];
+    }
+  } else if (!g.c_last && !g.c_tap_cin && !g.gate && g.beta == 0.f) {
+    // common forward epilogue: every read (bias, residual) is issued before the first store,
+    // so the 16 loads overlap instead of queueing behind stores they might alias
+    const float bv = g.bias ? g.bias[col] : 0.f;
+    float res[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = rbase + (r & 3) + 8 * (r >> 2);
+      res[r] = (g.resid && row < g.M) ? g.resid[(long long)bidx * g.resid_bs + (long long)row * g.ld_resid + col]
+                                      : 0.f;
+    }
+    float* cb = g.c + (long long)bidx * g.c_bs + col;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = rbase + (r & 3) + 8 * (r >> 2);
+      float v = g.alpha * acc[r] + bv;
+      if (g.relu == 2) v = fmaxf(v, 0.f);
+      v += res[r];
+      if (g.relu == 1) v = fmaxf(v, 0.f);
+      if (row < g.M) cb[(long long)row * g.ldc] = v;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = rbase + (r & 3) + 8 * (r >> 2);
+      if (row < g.M) epilogue_store(g, bidx, row, col, acc[r]);
     }
   }
+  FX_STAMP(g, 3);
 }
 
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmDev g) {
@@ -266,11 +389,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmDev g) {
   }
 }
 
-// bias-gradient column sums, two deterministic stages
+// bias-gradient column sums, two deterministic stages (used only where no dW GEMM carries them)
 constexpr int CS_ROWS = 128;
 __global__ __launch_bounds__(256) void colsum_stage1(const float* x, long long ld, int M, int N, float* ws) {
   const int n = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int rg = threadIdx.x >> 6;  // 4 row groups
+  const int rg = threadIdx.x >> 6;
   const int r0 = blockIdx.y * CS_ROWS;
   float s = 0.f;
   if (n < N)
@@ -298,6 +421,31 @@ bool operand_vec_ok(const fx_operand& o) {
   if (o.conv_taps && (o.conv_cin & 7)) return false;
   if (!o.trans && o.ptr1 && (!aligned16(o.ptr1) || (o.ld1 & 3) || (o.k_split & 7))) return false;
   return true;
+}
+
+int kind_of(const fx_operand& o, bool vec) {
+  if (o.trans) return o.conv_taps ? COLS_CONV : COLS;
+  if (o.conv_taps) return (vec && o.conv_cin % BKH == 0) ? ROWS_CONV : ROWS_GEN;
+  if (o.ptr1 || o.rows0 || o.rows1 || o.pos) return ROWS_GEN;
+  return ROWS;
+}
+
+template <int AK, int BKd>
+void launch_t(dim3 grid, hipStream_t s, const GemmDev& g) {
+  hipLaunchKernelGGL((gemm_f32_kernel<AK, BKd>), grid, dim3(NTHREADS), 0, s, g);
+}
+
+template <int AK>
+int launch_b(int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
+  switch (bk) {
+    case ROWS: launch_t<AK, ROWS>(grid, s, g); return FX_OK;
+    case COLS: launch_t<AK, COLS>(grid, s, g); return FX_OK;
+    case COLS_CONV: launch_t<AK, COLS_CONV>(grid, s, g); return FX_OK;
+    case ROWS_GEN: launch_t<AK, ROWS_GEN>(grid, s, g); return FX_OK;
+    default: break;
+  }
+  set_error("gemm: unsupported B operand kind");
+  return FX_ERR_UNSUPPORTED;
 }
 
 }  // namespace
@@ -346,6 +494,7 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
   FX_REQUIRE(!(d.b.conv_taps && d.b.trans && d.N != d.b.conv_taps * d.b.conv_cin + (d.b.ones_col ? 1 : 0)),
              "gemm: conv B needs N == taps*cin (+1 with a ones column)");
   FX_REQUIRE(!(d.a.ones_col && !d.a.trans) && !(d.b.ones_col && !d.b.trans), "gemm: ones_col needs trans==1");
+  FX_REQUIRE(!(d.b.conv_taps && !d.b.trans), "gemm: row-major conv B operand is not supported");
   GemmDev g{};
   g.M = d.M;
   g.N = d.N;
@@ -366,6 +515,7 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
   g.relu = d.relu;
   g.c_tap_cin = d.c_tap_cin;
   g.c_last = d.c_last_col;
+  g.stamps = d.dbg_stamps;
   g.a_vec = operand_vec_ok(d.a);
   g.b_vec = operand_vec_ok(d.b);
   const int nkt = cdiv(d.K, BK);
@@ -376,12 +526,29 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
   g.split = split;
   g.ws = d.workspace;
   if (split > 1) FX_REQUIRE(d.workspace, "gemm: split-K needs a workspace");
-  dim3 grid(cdiv(d.N, BN), cdiv(d.M, BM), d.batch * split);
-  const int ta = d.a.trans ? 1 : 0, tb = d.b.trans ? 1 : 0;
-  if (!ta && !tb) hipLaunchKernelGGL((gemm_f32_kernel<false, false>), grid, dim3(NTHREADS), 0, s, g);
-  else if (!ta && tb) hipLaunchKernelGGL((gemm_f32_kernel<false, true>), grid, dim3(NTHREADS), 0, s, g);
-  else if (ta && !tb) hipLaunchKernelGGL((gemm_f32_kernel<true, false>), grid, dim3(NTHREADS), 0, s, g);
-  else hipLaunchKernelGGL((gemm_f32_kernel<true, true>), grid, dim3(NTHREADS), 0, s, g);
+  g.tiles_x = cdiv(d.N, BN);
+  g.tiles_y = cdiv(d.M, BM);
+  dim3 grid(g.tiles_x, g.tiles_y, d.batch * split);
+  const int ak = kind_of(d.a, g.a_vec), bk = kind_of(d.b, g.b_vec);
+  // FX_GEMM_LOG=<file>: append one line per launch (diagnostic shape census, tools/gemm_census.py)
+  static FILE* glog = [] {
+    const char* p = std::getenv("FX_GEMM_LOG");
+    return p ? std::fopen(p, "a") : nullptr;
+  }();
+  if (glog)
+    std::fprintf(glog, "%d %d %d %d %d %d %d %d %d %d\n", d.M, d.N, d.K, d.batch, ak, bk, split,
+                 d.a.conv_taps, d.b.conv_taps, d.relu);
+  int st;
+  switch (ak) {
+    case ROWS: st = launch_b<ROWS>(bk, grid, s, g); break;
+    case ROWS_CONV: st = launch_b<ROWS_CONV>(bk, grid, s, g); break;
+    case ROWS_GEN: st = launch_b<ROWS_GEN>(bk, grid, s, g); break;
+    case COLS: st = launch_b<COLS>(bk, grid, s, g); break;
+    default:
+      set_error("gemm: unsupported A operand kind");
+      return FX_ERR_UNSUPPORTED;
+  }
+  if (st != FX_OK) return st;
   FX_CHECK_HIP(hipGetLastError());
   if (split > 1) {
     const long long total = (long long)d.M * d.N;

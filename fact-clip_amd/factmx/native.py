@@ -35,7 +35,7 @@ class GemmDesc(ctypes.Structure):
     _fields_ = [("M", I), ("N", I), ("K", I), ("batch", I), ("a", Operand), ("b", Operand), ("c", P), ("ldc", L),
                 ("c_batch_stride", L), ("alpha", F), ("beta", F), ("bias", P), ("resid", P), ("ld_resid", L),
                 ("resid_batch_stride", L), ("gate", P), ("ld_gate", L), ("relu", I), ("c_tap_cin", I),
-                ("split_k", I), ("workspace", P), ("c_last_col", P)]
+                ("split_k", I), ("workspace", P), ("c_last_col", P), ("dbg_stamps", P)]
 
 
 class MstcnParams(ctypes.Structure):

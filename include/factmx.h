@@ -101,6 +101,7 @@ typedef struct fx_gemm_desc {
   int split_k;                /* >1: K split over workgroups, partials in workspace */
   float* workspace;
   float* c_last_col;          /* != NULL: output column N-1 goes to c_last_col[m] (bias grad) */
+  long long* dbg_stamps;      /* diagnostic builds (-DFX_STAMPS) only: per-block timestamps */
 } fx_gemm_desc;
 
 int fx_gemm(const fx_gemm_desc* desc, void* stream);

@@ -1,9 +1,17 @@
+# Full GPU pass: parity tests, smoke, bench, kernel-trace profile.  Stops at the first
+# crash/timeout (pytest exit 1 = ordinary test failures, still safe to continue).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 500 > gpurun_out/pytest_gpu3.log 2>&1; echo "pytest exit $?"
-tail -4 gpurun_out/pytest_gpu3.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && echo smoke ok || echo smoke FAIL
-timeout -k 10 400 python bench.py --steps 5 --warmup 2 > gpurun_out/bench1.json 2> gpurun_out/bench1.err && echo bench ok || echo bench FAIL
-cat gpurun_out/bench1.json; tail -3 gpurun_out/bench1.err
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof1 -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/prof1.log 2>&1 && echo prof ok || echo prof FAIL
+TAG="${TAG:-run}"
+timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 500 > gpurun_out/pytest_gpu_$TAG.log 2>&1
+rc=$?; echo "pytest exit $rc"; tail -4 gpurun_out/pytest_gpu_$TAG.log
+[ $rc -le 1 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1
+rc=$?; echo "smoke exit $rc"; [ $rc -le 1 ] || exit $rc
+timeout -k 10 400 python bench.py --steps 10 --warmup 3 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
+rc=$?; echo "bench exit $rc"; cat gpurun_out/bench_$TAG.json; tail -3 gpurun_out/bench_$TAG.err
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1
+rc=$?; echo "prof exit $rc"; tail -1 gpurun_out/prof_$TAG.log
+exit $rc
