@@ -30,6 +30,7 @@ sys.path.insert(0, os.path.join(ROOT, "fact-clip_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+DOMINANT_KERNEL = "gemm_f32_kernel<1, 0>"   # rocprofv3 name: fx::(anonymous namespace)::gemm_f32_kernel<1, 0>
 METRIC = "frames/sec FACT_CLIP fwd+bwd, T=4096 D=2048 Nact=32, at 1/2/4/8 GPUs"
 F32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 HOLDOUT = [51, 53, 61, 67, 56]   # havid_view0_lh_pt_holdout.yaml
@@ -106,7 +107,7 @@ def traffic_from_profiles(kernel_prefix):
     try:
         with open(path) as f:
             d = json.load(f)
-        if str(d.get("kernel", "")).startswith(kernel_prefix):
+        if kernel_prefix in str(d.get("kernel", "")):
             return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -197,7 +198,7 @@ def main():
     S = [blk.tdu.num_seg for blk in net.block_list if hasattr(blk, "tdu")]
     log(f"[rank {rank}] TDU segments per U block: {S}")
 
-    max_ev = args.steps * args.videos * 4 * 10 + 64
+    max_ev = args.steps * args.videos * 4 * 10 * 2 + 64
     native.check(lib.fx_prof_enable(0, max_ev), "fx_prof_enable")
     if world > 1:
         dist.barrier()
@@ -230,8 +231,8 @@ def main():
         achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
         roofline = dict(bound="mfma", achieved=round(achieved, 2), peak=F32_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
                         frac=round(achieved / F32_MFMA_PEAK_TFLOPS, 4),
-                        traffic=traffic_from_profiles("_ZN2fx12_GLOBAL__N_115gemm_f32_kernel"),
-                        kernel="gemm_f32_kernel<false,false> (dilated-conv implicit GEMM fwd)",
+                        traffic=traffic_from_profiles(DOMINANT_KERNEL),
+                        kernel=DOMINANT_KERNEL + " (implicit dilated-conv GEMM: MS-TCN conv fwd + conv dX)",
                         launches=cnt.value, avg_launch_ms=round(avg_ms, 5),
                         flops_per_launch=flops_per_launch)
         line = dict(metric=METRIC, value=round(value, 1), unit="frames/s", n_gpus=world, steps=args.steps,

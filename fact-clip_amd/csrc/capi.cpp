@@ -426,7 +426,9 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
                                  op_rows(ws + L.wb + (long long)i * 3 * F * F, 3 * F), dHn, F);
       d.resid = gU;
       d.ld_resid = F;
+      prof_begin(0, s);
       FX_TRY(launch_gemm(d, s));
+      prof_end(0, s, 2.0 * rows * F * 3.0 * F, 4.0 * (3.0 * rows * F + 3.0 * F * F));
       if (dHn != dH) std::swap(dH, dU);  // dH now holds dH_i
     }
   }

@@ -20,6 +20,10 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
+#include <mutex>
+#include <string>
+#include <utility>
 
 #include "fx_common.h"
 
@@ -49,6 +53,7 @@ struct GemmDev {
   float* c_last;
   int tiles_x, tiles_y;
   long long* stamps;
+  unsigned* tile_cnt;   // split-K arrival counters (one per output tile), NULL -> separate reduce kernel
 };
 
 // Diagnostic builds (-DFX_STAMPS) record s_memtime / s_memrealtime at fixed points of
@@ -244,6 +249,33 @@ __device__ __forceinline__ void epilogue_store(const GemmDev& g, int b, int m, i
   *cp = v;
 }
 
+// split-K without a second launch: each block of a tile writes its partial sums to its
+// workspace slab; the last block to arrive (per-tile counter) adds the slabs in slab order
+// (deterministic) and runs the epilogue, then re-arms the counter for the next launch.
+template <int TM, int TN>
+__device__ void splitk_finish(const GemmDev& g, int bidx, int m0, int n0, int tile_id, int* s_last) {
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = atomicAdd(&g.tile_cnt[tile_id], 1u);
+    *s_last = prev == (unsigned)g.split - 1;
+    if (*s_last) g.tile_cnt[tile_id] = 0u;
+  }
+  __syncthreads();
+  if (!*s_last) return;
+  __threadfence();
+  const long long MN = (long long)g.M * g.N;
+  const float* base = g.ws + (long long)bidx * g.split * MN;
+  for (int e = threadIdx.x; e < TM * TN; e += blockDim.x) {
+    const int m = m0 + e / TN, n = n0 + e % TN;
+    if (m >= g.M || n >= g.N) continue;
+    const float* p = base + (long long)m * g.N + n;
+    float v = 0.f;
+    for (int k = 0; k < g.split; ++k) v += p[k * MN];
+    epilogue_store(g, bidx, m, n, v);
+  }
+}
+
 template <int AK, int BKIND>
 __global__ __launch_bounds__(NTHREADS) void gemm_f32_kernel(GemmDev g) {
   __shared__ float sA[2][BK][LDSS];
@@ -332,22 +364,32 @@ __global__ __launch_bounds__(NTHREADS) void gemm_f32_kernel(GemmDev g) {
       for (int r = 0; r < 16; ++r) red[(wq * 16 + r) * 64 + lane] = acc[r];
     }
     __syncthreads();
-    if (kh == 1) return;
+    if (kh == 1 && !(g.split > 1 && g.tile_cnt)) return;
+    if (kh == 0) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] += red[(wq * 16 + r) * 64 + lane];
+      for (int r = 0; r < 16; ++r) acc[r] += red[(wq * 16 + r) * 64 + lane];
+    }
   }
 
   // C/D layout of the 32x32 f32 accumulator: col = lane&31, row = (r&3)+8*(r>>2)+4*(lane>>5)
   const int col = n0 + wn * 32 + li;
-  if (col >= g.N) return;
   const int rbase = m0 + wm * 32 + 4 * lh;
   if (g.split > 1) {
+    if (kh == 0 && col < g.N) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = rbase + (r & 3) + 8 * (r >> 2);
-      if (row < g.M) g.ws[(((long long)bidx * g.split + sk) * g.M + row) * g.N + col] = acc[r];
+      for (int r = 0; r < 16; ++r) {
+        const int row = rbase + (r & 3) + 8 * (r >> 2);
+        if (row < g.M) g.ws[(((long long)bidx * g.split + sk) * g.M + row) * g.N + col] = acc[r];
+      }
     }
-  } else if (!g.c_last && !g.c_tap_cin && !g.gate && g.beta == 0.f) {
+    if (g.tile_cnt) {
+      __shared__ int s_last;
+      splitk_finish<BM, BN>(g, bidx, m0, n0, (bidx * g.tiles_y + ty) * g.tiles_x + tx, &s_last);
+    }
+    return;
+  }
+  if (col >= g.N) return;
+  if (!g.c_last && !g.c_tap_cin && !g.gate && g.beta == 0.f) {
     // common forward epilogue: every read (bias, residual) is issued before the first store,
     // so the 16 loads overlap instead of queueing behind stores they might alias
     const float bv = g.bias ? g.bias[col] : 0.f;
@@ -387,6 +429,113 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmDev g) {
     for (int sk = 0; sk < g.split; ++sk) s += g.ws[((long long)bidx * g.split + sk) * total + i];
     epilogue_store(g, bidx, (int)(i / g.N), (int)(i % g.N), s);
   }
+}
+
+// ---------------------------------------------------------------- direct kernel (small shapes)
+// Token-level (M = Nact = 32) projections, per-head attention products and their weight
+// gradients are far too small for the 64x64 LDS-tiled kernel: its per-tile cost is latency
+// (prologue loads, a 1 us MFMA phase per 64-deep stage, the epilogue), so a handful of tiles
+// walking K serially takes 10-30 us.  Here each wave owns one 32x32 output tile over a strided
+// set of 32-deep k chunks and loads its MFMA fragments straight from global memory (L2): a lane
+// takes 16 CONSECUTIVE k of a chunk (the k order inside an MFMA chain is free as long as A and B
+// agree), so row-major operands are float4 loads and column-major ones are coalesced across
+// lanes.  The waves of a block split K of the same tile and are summed through LDS in wave
+// order; optional cross-block split-K goes through workspace slabs + splitk_finish.
+constexpr int DCH = 32, DMAXW = 8;
+
+template <int KIND>
+__device__ __forceinline__ void dload(const fx_operand& o, const float* base, int r, int R, int k0, int K, bool vec,
+                                      float* v) {
+  if (KIND == ROWS) {
+    if (vec && r < R && k0 + 16 <= K) {
+      const float* p = base + (long long)r * o.ld + k0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 x = *reinterpret_cast<const float4*>(p + 4 * q);
+        v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+      }
+      return;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = (r < R && k0 + j < K) ? base[(long long)r * o.ld + k0 + j] : 0.f;
+  } else if (KIND == COLS) {
+    const bool ones = o.ones_col && r == o.ones_col - 1;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      v[j] = (r < R && k0 + j < K) ? (ones ? 1.f : base[(long long)(k0 + j) * o.ld + r]) : 0.f;
+  } else {  // ROWS_GEN
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = (r < R && k0 + j < K) ? fetch_rm(o, base, r, k0 + j) : 0.f;
+  }
+}
+
+__device__ __forceinline__ void direct_finish(const GemmDev& g, int bidx, int sk, int row, int col, float v) {
+  if (row >= g.M || col >= g.N) return;
+  if (g.split > 1)
+    g.ws[(((long long)bidx * g.split + sk) * g.M + row) * g.N + col] = v;
+  else
+    epilogue_store(g, bidx, row, col, v);
+}
+
+template <int AK, int BKd>
+__global__ __launch_bounds__(DMAXW * 64) void gemm_direct_kernel(GemmDev g) {
+  __shared__ float red[DMAXW * 16 * 64];
+  __shared__ int s_last;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  const int n0 = blockIdx.x * 32, m0 = blockIdx.y * 32;
+  const int z = blockIdx.z, bidx = z / g.split, sk = z - bidx * g.split;
+  const int nch = (g.K + DCH - 1) / DCH;
+  const int c0 = sk * g.kt_per_split, c1 = min(nch, c0 + g.kt_per_split);
+  const float* pa = g.a.ptr + (long long)bidx * g.a.batch_stride;
+  const float* pb = g.b.ptr + (long long)bidx * g.b.batch_stride;
+  const int ra = m0 + li, rb = n0 + li, ko = lh * 16;
+  const bool av = g.a_vec, bv = g.b_vec;
+
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  float a0[16], b0[16], a1[16], b1[16];
+  int c = c0 + w;
+  if (c < c1) {
+    dload<AK>(g.a, pa, ra, g.M, c * DCH + ko, g.K, av, a0);
+    dload<BKd>(g.b, pb, rb, g.N, c * DCH + ko, g.K, bv, b0);
+  }
+  for (; c < c1; c += 2 * nw) {
+    const int cn = c + nw;
+    if (cn < c1) {
+      dload<AK>(g.a, pa, ra, g.M, cn * DCH + ko, g.K, av, a1);
+      dload<BKd>(g.b, pb, rb, g.N, cn * DCH + ko, g.K, bv, b1);
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b0[s], acc, 0, 0, 0);
+    const int cnn = cn + nw;
+    if (cnn < c1) {
+      dload<AK>(g.a, pa, ra, g.M, cnn * DCH + ko, g.K, av, a0);
+      dload<BKd>(g.b, pb, rb, g.N, cnn * DCH + ko, g.K, bv, b0);
+    }
+    if (cn < c1) {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b1[s], acc, 0, 0, 0);
+    }
+  }
+
+  if (nw > 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[(w * 16 + r) * 64 + lane] = acc[r];
+    __syncthreads();
+    for (int e = tid; e < 1024; e += nw * 64) {
+      const int r = e >> 6, l = e & 63;
+      float v = 0.f;
+      for (int q = 0; q < nw; ++q) v += red[(q * 16 + r) * 64 + l];
+      direct_finish(g, bidx, sk, m0 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), n0 + (l & 31), v);
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) direct_finish(g, bidx, sk, m0 + (r & 3) + 8 * (r >> 2) + 4 * lh, n0 + li, acc[r]);
+  }
+  if (g.split > 1 && g.tile_cnt)
+    splitk_finish<32, 32>(g, bidx, m0, n0, (bidx * g.tiles_y + blockIdx.y) * g.tiles_x + blockIdx.x, &s_last);
 }
 
 // bias-gradient column sums, two deterministic stages (used only where no dW GEMM carries them)
@@ -446,6 +595,78 @@ int launch_b(int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
   }
   set_error("gemm: unsupported B operand kind");
   return FX_ERR_UNSUPPORTED;
+}
+
+int launch_tiled(int ak, int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
+  switch (ak) {
+    case ROWS: return launch_b<ROWS>(bk, grid, s, g);
+    case ROWS_CONV: return launch_b<ROWS_CONV>(bk, grid, s, g);
+    case ROWS_GEN: return launch_b<ROWS_GEN>(bk, grid, s, g);
+    case COLS: return launch_b<COLS>(bk, grid, s, g);
+    default: break;
+  }
+  set_error("gemm: unsupported A operand kind");
+  return FX_ERR_UNSUPPORTED;
+}
+
+template <int AK>
+int launch_direct_b(int bk, dim3 grid, dim3 block, hipStream_t s, const GemmDev& g) {
+  switch (bk) {
+    case ROWS: hipLaunchKernelGGL((gemm_direct_kernel<AK, ROWS>), grid, block, 0, s, g); return FX_OK;
+    case COLS: hipLaunchKernelGGL((gemm_direct_kernel<AK, COLS>), grid, block, 0, s, g); return FX_OK;
+    default: break;
+  }
+  set_error("gemm(direct): unsupported B operand kind");
+  return FX_ERR_UNSUPPORTED;
+}
+
+int launch_direct(int ak, int bk, dim3 grid, dim3 block, hipStream_t s, const GemmDev& g) {
+  switch (ak) {
+    case ROWS: return launch_direct_b<ROWS>(bk, grid, block, s, g);
+    case ROWS_GEN: return launch_direct_b<ROWS_GEN>(bk, grid, block, s, g);
+    case COLS: return launch_direct_b<COLS>(bk, grid, block, s, g);
+    default: break;
+  }
+  set_error("gemm(direct): unsupported A operand kind");
+  return FX_ERR_UNSUPPORTED;
+}
+
+// Small problems go to the direct kernel: token-level (M or N <= 32), shallow K, or fewer
+// 64x64 tiles than a quarter of the CUs.  Conv-gather operands always take the tiled kernel.
+// FX_GEMM_PATH=tiled|direct overrides the choice (diagnostic).
+bool use_direct(const fx_gemm_desc& d, int ak, int bk) {
+  static const int force = [] {
+    const char* p = std::getenv("FX_GEMM_PATH");
+    if (!p) return 0;
+    return std::string(p) == "tiled" ? 1 : std::string(p) == "direct" ? 2 : 0;
+  }();
+  const bool ok = (ak == ROWS || ak == ROWS_GEN || ak == COLS) && (bk == ROWS || bk == COLS);
+  if (!ok || force == 1) return false;
+  if (force == 2) return true;
+  const long long t64 = (long long)cdiv(d.M, 64) * cdiv(d.N, 64) * d.batch;
+  return d.M <= 32 || d.N <= 32 || d.K <= 64 || t64 < 64;
+}
+
+// Split-K arrival counters, one pool per (device, stream): zeroed once at allocation and
+// re-armed by the last block of every tile, so launches on one stream reuse them safely.
+constexpr long long kMaxTileCounters = 1 << 16;
+unsigned* tile_counters(hipStream_t s) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, unsigned*> pool;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  const auto key = std::make_pair(dev, s);
+  auto it = pool.find(key);
+  if (it != pool.end()) return it->second;
+  unsigned* p = nullptr;
+  if (hipMalloc(&p, kMaxTileCounters * sizeof(unsigned)) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(p, 0, kMaxTileCounters * sizeof(unsigned), s) != hipSuccess) {
+    (void)hipFree(p);
+    return nullptr;
+  }
+  pool[key] = p;
+  return p;
 }
 
 }  // namespace
@@ -518,39 +739,50 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
   g.stamps = d.dbg_stamps;
   g.a_vec = operand_vec_ok(d.a);
   g.b_vec = operand_vec_ok(d.b);
-  const int nkt = cdiv(d.K, BK);
-  int split = d.split_k > 1 ? d.split_k : 1;
-  if (split > nkt) split = nkt > 0 ? nkt : 1;
-  g.kt_per_split = nkt > 0 ? cdiv(nkt, split) : 0;
-  split = g.kt_per_split > 0 ? cdiv(nkt, g.kt_per_split) : 1;
-  g.split = split;
   g.ws = d.workspace;
-  if (split > 1) FX_REQUIRE(d.workspace, "gemm: split-K needs a workspace");
-  g.tiles_x = cdiv(d.N, BN);
-  g.tiles_y = cdiv(d.M, BM);
-  dim3 grid(g.tiles_x, g.tiles_y, d.batch * split);
   const int ak = kind_of(d.a, g.a_vec), bk = kind_of(d.b, g.b_vec);
+  const bool direct = use_direct(d, ak, bk);
+  const int cap = (d.split_k > 1 && d.workspace) ? d.split_k : 1;   // workspace holds `cap` slabs
+  FX_REQUIRE(!(d.split_k > 1 && !d.workspace), "gemm: split-K needs a workspace");
+  dim3 grid, block;
+  if (direct) {
+    const int nch = cdiv(d.K, DCH);
+    const long long t32 = (long long)cdiv(d.M, 32) * cdiv(d.N, 32) * d.batch;
+    const int nw = std::min(DMAXW, std::max(1, nch / 2));
+    int split = 1;
+    if (cap > 1) {
+      const long long want = std::min<long long>(nch / (2 * nw), cdiv(2048, t32 * nw));
+      split = (int)std::max<long long>(1, std::min<long long>(cap, want));
+    }
+    g.kt_per_split = nch > 0 ? cdiv(nch, split) : 0;
+    g.split = g.kt_per_split > 0 ? cdiv(nch, g.kt_per_split) : 1;
+    g.tiles_x = cdiv(d.N, 32);
+    g.tiles_y = cdiv(d.M, 32);
+    grid = dim3(g.tiles_x, g.tiles_y, d.batch * g.split);
+    block = dim3(nw * 64);
+  } else {
+    const int nkt = cdiv(d.K, BK);
+    int split = std::min(cap, std::max(nkt, 1));
+    g.kt_per_split = nkt > 0 ? cdiv(nkt, split) : 0;
+    g.split = g.kt_per_split > 0 ? cdiv(nkt, g.kt_per_split) : 1;
+    g.tiles_x = cdiv(d.N, BN);
+    g.tiles_y = cdiv(d.M, BM);
+    grid = dim3(g.tiles_x, g.tiles_y, d.batch * g.split);
+    block = dim3(NTHREADS);
+  }
+  if (g.split > 1 && (long long)g.tiles_x * g.tiles_y * d.batch <= kMaxTileCounters) g.tile_cnt = tile_counters(s);
   // FX_GEMM_LOG=<file>: append one line per launch (diagnostic shape census, tools/gemm_census.py)
   static FILE* glog = [] {
     const char* p = std::getenv("FX_GEMM_LOG");
     return p ? std::fopen(p, "a") : nullptr;
   }();
   if (glog)
-    std::fprintf(glog, "%d %d %d %d %d %d %d %d %d %d\n", d.M, d.N, d.K, d.batch, ak, bk, split,
-                 d.a.conv_taps, d.b.conv_taps, d.relu);
-  int st;
-  switch (ak) {
-    case ROWS: st = launch_b<ROWS>(bk, grid, s, g); break;
-    case ROWS_CONV: st = launch_b<ROWS_CONV>(bk, grid, s, g); break;
-    case ROWS_GEN: st = launch_b<ROWS_GEN>(bk, grid, s, g); break;
-    case COLS: st = launch_b<COLS>(bk, grid, s, g); break;
-    default:
-      set_error("gemm: unsupported A operand kind");
-      return FX_ERR_UNSUPPORTED;
-  }
+    std::fprintf(glog, "%d %d %d %d %d %d %d %d %d %d %d\n", d.M, d.N, d.K, d.batch, ak, bk, g.split,
+                 d.a.conv_taps, d.b.conv_taps, d.relu, direct ? (int)block.x / 64 : 0);
+  int st = direct ? launch_direct(ak, bk, grid, block, s, g) : launch_tiled(ak, bk, grid, s, g);
   if (st != FX_OK) return st;
   FX_CHECK_HIP(hipGetLastError());
-  if (split > 1) {
+  if (g.split > 1 && !g.tile_cnt) {
     const long long total = (long long)d.M * d.N;
     int blocks = (int)std::min<long long>(cdiv(total, 256), 2048);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks, d.batch), dim3(256), 0, s, g);

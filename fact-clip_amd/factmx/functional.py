@@ -496,10 +496,11 @@ def _rows_operand(t, trans=False):
 
 
 def gemm(M, N, K, a, b, c, ldc, bias=None, relu=0, resid=None, alpha=1.0, beta=0.0, gate=None, c_tap_cin=0,
-         split=1, c_last=None):
+         split=1, c_last=None, batch=1, c_bs=0):
     lib = nx.load()
     d = nx.GemmDesc()
-    d.M, d.N, d.K, d.batch = M, N, K, 1
+    d.M, d.N, d.K, d.batch = M, N, K, batch
+    d.c_batch_stride = c_bs
     d.a, d.b = a, b
     d.c, d.ldc = nx.ptr(c), ldc
     d.alpha, d.beta = alpha, beta
