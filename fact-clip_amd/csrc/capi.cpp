@@ -148,7 +148,8 @@ int pick_split(int M, int N, int K, int batch = 1) {
   const long long tiles = (long long)cdiv(M, 64) * cdiv(N, 64) * batch;
   const int nkt = cdiv(K, 64);   // 64-deep K stages of the GEMM kernel
   if (tiles >= 160 || nkt < 4) return 1;
-  int sp = (int)std::min<long long>(nkt / 2, cdiv(256, tiles));
+  // one 8-wave block per CU fits (VGPR-bound): keep tiles*split within the 256 CUs, no straggler round
+  int sp = (int)std::min<long long>(nkt / 2, 256 / tiles);
   return std::max(sp, 1);
 }
 

@@ -252,18 +252,29 @@ __device__ __forceinline__ void epilogue_store(const GemmDev& g, int b, int m, i
 // split-K without a second launch: each block of a tile writes its partial sums to its
 // workspace slab; the last block to arrive (per-tile counter) adds the slabs in slab order
 // (deterministic) and runs the epilogue, then re-arms the counter for the next launch.
+// Ordering follows the agent-scope hand-off recipe (cdna_hip_programming.md, projection GEMM
+// item 2): drain the slab stores, ONE release fence by lane 0 before the ticket, ONE acquire fence
+// in the reducer; correct for any placement of a tile's slices over XCDs.  `flag` lives inside the
+// kernel's existing LDS array (a separate __shared__ word can de-pipeline the k-loop).
 template <int TM, int TN>
-__device__ void splitk_finish(const GemmDev& g, int bidx, int m0, int n0, int tile_id, int* s_last) {
-  __threadfence();
+__device__ void splitk_finish(const GemmDev& g, int bidx, int m0, int n0, int tile_id, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned prev = atomicAdd(&g.tile_cnt[tile_id], 1u);
-    *s_last = prev == (unsigned)g.split - 1;
-    if (*s_last) g.tile_cnt[tile_id] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev =
+        __hip_atomic_fetch_add(&g.tile_cnt[tile_id], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == (unsigned)g.split - 1;
+    if (last) {
+      __hip_atomic_store(&g.tile_cnt[tile_id], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
   }
   __syncthreads();
-  if (!*s_last) return;
-  __threadfence();
+  if (!*flag) return;
   const long long MN = (long long)g.M * g.N;
   const float* base = g.ws + (long long)bidx * g.split * MN;
   for (int e = threadIdx.x; e < TM * TN; e += blockDim.x) {
@@ -382,10 +393,9 @@ __global__ __launch_bounds__(NTHREADS) void gemm_f32_kernel(GemmDev g) {
         if (row < g.M) g.ws[(((long long)bidx * g.split + sk) * g.M + row) * g.N + col] = acc[r];
       }
     }
-    if (g.tile_cnt) {
-      __shared__ int s_last;
-      splitk_finish<BM, BN>(g, bidx, m0, n0, (bidx * g.tiles_y + ty) * g.tiles_x + tx, &s_last);
-    }
+    if (g.tile_cnt)   // flag: last word of sA (the k-half combine above uses the first 16 KB)
+      splitk_finish<BM, BN>(g, bidx, m0, n0, (bidx * g.tiles_y + ty) * g.tiles_x + tx,
+                            reinterpret_cast<int*>(&sA[1][BK - 1][LDSS - 1]));
     return;
   }
   if (col >= g.N) return;
@@ -479,8 +489,7 @@ __device__ __forceinline__ void direct_finish(const GemmDev& g, int bidx, int sk
 
 template <int AK, int BKd>
 __global__ __launch_bounds__(DMAXW * 64) void gemm_direct_kernel(GemmDev g) {
-  __shared__ float red[DMAXW * 16 * 64];
-  __shared__ int s_last;
+  __shared__ float red[DMAXW * 16 * 64 + 1];   // wave partials + the split-K "last block" flag
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
   const int li = lane & 31, lh = lane >> 5;
   const int n0 = blockIdx.x * 32, m0 = blockIdx.y * 32;
@@ -535,7 +544,8 @@ __global__ __launch_bounds__(DMAXW * 64) void gemm_direct_kernel(GemmDev g) {
     for (int r = 0; r < 16; ++r) direct_finish(g, bidx, sk, m0 + (r & 3) + 8 * (r >> 2) + 4 * lh, n0 + li, acc[r]);
   }
   if (g.split > 1 && g.tile_cnt)
-    splitk_finish<32, 32>(g, bidx, m0, n0, (bidx * g.tiles_y + blockIdx.y) * g.tiles_x + blockIdx.x, &s_last);
+    splitk_finish<32, 32>(g, bidx, m0, n0, (bidx * g.tiles_y + blockIdx.y) * g.tiles_x + blockIdx.x,
+                          reinterpret_cast<int*>(&red[DMAXW * 16 * 64]));
 }
 
 // bias-gradient column sums, two deterministic stages (used only where no dW GEMM carries them)
@@ -631,8 +641,8 @@ int launch_direct(int ak, int bk, dim3 grid, dim3 block, hipStream_t s, const Ge
   return FX_ERR_UNSUPPORTED;
 }
 
-// Small problems go to the direct kernel: token-level (M or N <= 32), shallow K, or fewer
-// 64x64 tiles than a quarter of the CUs.  Conv-gather operands always take the tiled kernel.
+// Small problems go to the direct kernel: token-level (M or N <= 32) or shallow K.  (Few-tile
+// frame-level dW GEMMs with K = T stay tiled: measured 25 vs 32 us at 256x257x4096.)  Conv-gather operands always take the tiled kernel.
 // FX_GEMM_PATH=tiled|direct overrides the choice (diagnostic).
 bool use_direct(const fx_gemm_desc& d, int ak, int bk) {
   static const int force = [] {
@@ -643,8 +653,7 @@ bool use_direct(const fx_gemm_desc& d, int ak, int bk) {
   const bool ok = (ak == ROWS || ak == ROWS_GEN || ak == COLS) && (bk == ROWS || bk == COLS);
   if (!ok || force == 1) return false;
   if (force == 2) return true;
-  const long long t64 = (long long)cdiv(d.M, 64) * cdiv(d.N, 64) * d.batch;
-  return d.M <= 32 || d.N <= 32 || d.K <= 64 || t64 < 64;
+  return d.M <= 32 || d.N <= 32 || d.K <= 64;
 }
 
 // Split-K arrival counters, one pool per (device, stream): zeroed once at allocation and
@@ -770,7 +779,11 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
     grid = dim3(g.tiles_x, g.tiles_y, d.batch * g.split);
     block = dim3(NTHREADS);
   }
-  if (g.split > 1 && (long long)g.tiles_x * g.tiles_y * d.batch <= kMaxTileCounters) g.tile_cnt = tile_counters(s);
+  // in-launch reduction only while the last block's serial slab read stays small (<= 32 KB per
+  // tile); bigger ones pay less as a separate reduce launch (conv dW split 5: 78 vs 56 us)
+  const long long slab_bytes = (long long)g.split * (direct ? 32 * 32 : BM * BN) * 4;
+  if (g.split > 1 && slab_bytes <= 32768 && (long long)g.tiles_x * g.tiles_y * d.batch <= kMaxTileCounters)
+    g.tile_cnt = tile_counters(s);
   // FX_GEMM_LOG=<file>: append one line per launch (diagnostic shape census, tools/gemm_census.py)
   static FILE* glog = [] {
     const char* p = std::getenv("FX_GEMM_LOG");
