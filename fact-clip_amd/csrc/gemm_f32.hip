@@ -9,13 +9,18 @@
 //   ROWS_GEN  concatenated inputs / row gathers / positional adds (generic)
 //   COLS      element (r,k) = p[k*ld + r]            dY^T for dW, W^T for dX
 //   COLS_CONV conv input for dW, tap from r; optional all-ones row (bias grad)
-// Tile: 64x64 output per 256-thread workgroup (4 waves x 32x32 accumulator,
-// 16 f32 per lane), K staged through LDS in 32-deep slices with a register
-// prefetch of the next slice (one barrier per slice).  All per-thread address
-// arithmetic is hoisted out of the K loop; inside it only pointer increments,
-// a tap lookup on uniform values, and two float4 loads per operand remain.
-// LDS images are [k][row] with a +1 pad: MFMA operand reads are ds_read_b32 of
-// 32 consecutive rows (conflict-free), staging writes at most 2-way.
+//
+// Tiled kernel: 64x64 output tile per 256-thread workgroup, one wave per SIMD, each wave a
+// 32x32 sub-tile over the block's whole K range (32 MFMAs = 2048 matrix-core cycles per
+// 64-deep stage between barriers).  K is staged through a 3-slot LDS ring: stage s+2 is
+// written while stage s is multiplied, so the fragments of stage s+1 are already visible
+// when a wave reaches the end of stage s and one barrier per stage suffices.  Global loads
+// run one more stage ahead in two register sets.  Inside a stage each lane works on 32
+// CONSECUTIVE k (lane half h takes k in [32h, 32h+32)): A and B agree on that order, which is
+// all an MFMA chain needs, and it lets row-major images be read as ds_read_b128 (4 MFMAs of
+// operand per read) and written as ds_write_b128 straight from the float4 global loads.
+//   row-major kinds -> LDS image [row][k], stride 68 (16-B rows; b128 reads conflict-free)
+//   col-major kinds -> LDS image [k][row], stride 65 (b32 reads conflict-free over 64 lanes)
 // Blocks are remapped so that consecutive output tiles share an XCD (L2).
 #include <algorithm>
 #include <cstdio>
@@ -30,9 +35,11 @@
 namespace fx {
 namespace {
 
-// BK: K depth per LDS stage (one barrier per 32 MFMAs per wave); loaders move it in
-// two BKH-deep halves (8 elements per thread each).
-constexpr int BM = 64, BN = 64, BK = 64, BKH = 32, NTHREADS = 512, LDSS = 65;
+constexpr int BM = 64, BN = 64, BK = 64, NTHREADS = 256;
+constexpr int RS = 68;              // [row][k] image stride
+constexpr int CS = 65;              // [k][row] image stride
+constexpr int IMG = BM * RS;        // floats per operand image (>= BK * CS)
+constexpr int NSLOT = 3;            // LDS ring depth
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 enum Kind { ROWS = 0, ROWS_CONV = 1, ROWS_GEN = 2, COLS = 3, COLS_CONV = 4 };
@@ -61,11 +68,11 @@ struct GemmDev {
 #ifdef FX_STAMPS
 #define FX_STAMP(g, slot)                                                                          \
   do {                                                                                            \
-    if ((g).stamps && (threadIdx.x & 255) == 0) {                                                 \
+    if ((g).stamps && threadIdx.x == 0) {                                                         \
       const long long _b = (long long)blockIdx.z * gridDim.x * gridDim.y + blockIdx.y * gridDim.x + \
                            blockIdx.x;                                                            \
-      (g).stamps[(_b * 2 + (threadIdx.x >> 8)) * 10 + 2 * (slot)] = __builtin_amdgcn_s_memtime();    \
-      (g).stamps[(_b * 2 + (threadIdx.x >> 8)) * 10 + 2 * (slot) + 1] = __builtin_amdgcn_s_memrealtime(); \
+      (g).stamps[(_b * 2) * 10 + 2 * (slot)] = __builtin_amdgcn_s_memtime();                       \
+      (g).stamps[(_b * 2) * 10 + 2 * (slot) + 1] = __builtin_amdgcn_s_memrealtime();               \
     }                                                                                             \
   } while (0)
 #else
@@ -107,119 +114,168 @@ __device__ __forceinline__ float fetch_cm(const fx_operand& o, const float* p0, 
   return p0[(long long)k * o.ld + r];
 }
 
-__device__ __forceinline__ void zero8(float* v) {
-#pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = 0.f;
-}
+__device__ __forceinline__ float4 zero4() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
-__device__ __forceinline__ void ld8(const float* src, float* v) {
-  const float4 x0 = *reinterpret_cast<const float4*>(src);
-  const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
-  v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
-  v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
-}
+__device__ __forceinline__ float4 ldg4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
 // ---------------------------------------------------------------- loaders
-// Each thread owns 8 elements of the 64 x 32 (rows x k) tile:
-//   row-major kinds: row = tid/4, k = (tid%4)*8 .. +7
-//   col-major kinds: row = (tid%8)*8 .. +7, k = tid/8
-// The fast path is chosen per TILE with a wave-uniform condition (whole 64-row
-// tile and 32-deep slice in range, 16-B aligned, no ones row) so the prefetch
-// loads are straight-line code: divergent bounds branches would make the
-// compiler drain vmcnt between the A and B prefetches.  Per-row validity of the
-// conv gather is a select, not a branch.  Edge tiles take the generic path.
-template <int KIND>
+// A stage is the 64 x 64 (rows x k) tile of one operand; each of the 256 threads moves 4
+// float4 of it per stage:
+//   row-major kinds: rows (tid>>4) + 16j, k = (tid&15)*4 .. +3           (j = 0..3)
+//   col-major kinds: k    (tid>>4) + 16j, rows (tid&15)*4 .. +3
+// so 16 consecutive threads read one 256-B line.
+// FAST (chosen per launch on the host: 16-B aligned operands, K % 64 == 0, no gathers): the
+// loads are unconditional straight-line code -- rows past the edge are read from a clamped
+// in-range address and replaced by a select (0, or 1 for the virtual ones row) -- so the
+// pipelined loop has no bounds branches for the compiler to drain vmcnt at.  !FAST fetches
+// element by element with full bounds checks (edge shapes, gathers, concatenations).
+template <int KIND, bool FAST>
 struct Loader {
-  const fx_operand* o;
-  const float* base;  // operand base incl. batch offset
-  int R, K;
-  bool tile_fast;     // uniform: rows of this tile all in range, operand vector-loadable
-  int r;              // row (row-major) or first row of the 8-chunk (col-major)
-  int kk;             // k offset inside the tile
-  int rmod;           // r % seq_len (ROWS_CONV)
-  int tapc, tap_s;    // COLS_CONV: channel and shift of this thread's rows
+  static constexpr bool kRowImg = KIND <= ROWS_GEN;
+  fx_operand o;        // by value: the address of a kernel argument would force it to scratch
+  const float* base;   // operand base incl. batch offset
+  int R, K, r0;
+  int ta, tb;          // tid>>4, (tid&15)*4
+  int rowc[4];         // row-major: clamped row of j
+  int rmod[4];         // ROWS_CONV: row % seq_len of j
+  unsigned rok;        // row-major: bit j = row j in range
+  int rc;              // col-major: clamped first row of the 4
+  unsigned emask, omask;   // col-major: bit e = row rc+e in storage / is the ones row
+  int tapc, tap_s;     // COLS_CONV: channel / shift of this thread's 4 rows (one tap: cin % 4 == 0)
 
-  __device__ __forceinline__ void init(const fx_operand& op, const float* p0, int r0, int R_, int K_, bool v, int tid) {
-    o = &op;
+  __device__ __forceinline__ void init(const fx_operand& op, const float* p0, int r0_, int R_, int K_, int tid) {
+    o = op;
     base = p0;
     R = R_;
     K = K_;
-    tile_fast = v && (r0 + 64 <= R_) && !(op.ones_col && r0 + 64 >= op.ones_col);
-    if (KIND <= ROWS_GEN) {
-      r = r0 + (tid >> 2);
-      kk = (tid & 3) * 8;
-      if (KIND == ROWS_CONV) rmod = r % op.seq_len;
+    r0 = r0_;
+    ta = tid >> 4;
+    tb = (tid & 15) * 4;
+    if (!FAST) return;
+    if (kRowImg) {
+      rok = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = r0 + ta + 16 * j;
+        rok |= (r < R ? 1u : 0u) << j;
+        rowc[j] = min(r, R - 1);
+        if (KIND == ROWS_CONV) rmod[j] = rowc[j] % op.seq_len;
+      }
     } else {
-      r = r0 + (tid & 7) * 8;
-      kk = tid >> 3;
+      // rows that exist in storage: all but a trailing virtual ones row
+      const int stored = op.ones_col ? op.ones_col - 1 : R;
+      const int r = r0 + tb;
+      emask = omask = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        emask |= (r + e < stored ? 1u : 0u) << e;
+        omask |= (op.ones_col && r + e == op.ones_col - 1 ? 1u : 0u) << e;
+      }
+      rc = min(r, ((stored - 1) / 4) * 4);
       if (KIND == COLS_CONV) {
-        const int j = r / op.conv_cin;
-        tapc = r - j * op.conv_cin;
+        const int j = rc / op.conv_cin;
+        tapc = rc - j * op.conv_cin;
         tap_s = conv_shift(op, j);
       }
     }
   }
 
-  __device__ __forceinline__ void load_generic(int k0, float* v) const {
-    if (KIND <= ROWS_GEN) {
-      const int k = k0 + kk;
-      if (r >= R) {
-        zero8(v);
-        return;
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = (k + e < K) ? fetch_rm(*o, base, r, k + e) : 0.f;
-    } else {
-      const int k = k0 + kk;
-      if (k >= K) {
-        zero8(v);
-        return;
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = (r + e < R) ? fetch_cm(*o, base, r + e, k) : 0.f;
-    }
-  }
-
-  __device__ __forceinline__ void load(int k0, float* v) const {
-    const bool fast = tile_fast && (k0 + BKH <= K);
-    if (KIND == ROWS_GEN || !fast) {
+  // Loads are raw and unconditional; every validity select is applied when the registers are
+  // written to LDS (store), a full stage later -- a select right after the load would make the
+  // compiler wait for the load there and serialise the prefetch.
+  // vm: per-stage validity bits (row-major: bit j = row j valid; COLS_CONV: bit j = time in range)
+  __device__ __forceinline__ void load(int k0, float4* v, unsigned& vm) const {
+    if (!FAST) {
       load_generic(k0, v);
+      vm = 0xFu;
       return;
     }
     if (KIND == ROWS) {
-      ld8(base + (long long)r * o->ld + k0 + kk, v);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = ldg4(base + (long long)rowc[j] * o.ld + k0 + tb);
+      vm = rok;
     } else if (KIND == ROWS_CONV) {
-      // the 32-deep slice lies in one tap (conv_cin % 32 == 0, checked on the host)
-      const int j = k0 / o->conv_cin;
-      const int c = k0 - j * o->conv_cin + kk;
-      const int s = conv_shift(*o, j);
-      const int t = rmod + s;
-      const bool ok = t >= 0 && t < o->seq_len;
-      ld8(base + (long long)(ok ? r + s : r) * o->ld + c, v);
+      // the 64-deep stage lies in one tap (conv_cin % 64 == 0, checked on the host)
+      const int tap = k0 / o.conv_cin;
+      const int c = k0 - tap * o.conv_cin + tb;
+      const int s = conv_shift(o, tap);
+      vm = 0;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = ok ? v[e] : 0.f;
+      for (int j = 0; j < 4; ++j) {
+        const int t = rmod[j] + s;
+        const bool ok = ((rok >> j) & 1u) && t >= 0 && t < o.seq_len;
+        vm |= (ok ? 1u : 0u) << j;
+        v[j] = ldg4(base + (long long)(ok ? rowc[j] + s : rowc[j]) * o.ld + c);
+      }
     } else if (KIND == COLS) {
-      ld8(base + (long long)(k0 + kk) * o->ld + r, v);
-    } else {  // COLS_CONV
-      const int k = k0 + kk;
-      const int t = k % o->seq_len + tap_s;
-      const bool ok = t >= 0 && t < o->seq_len;
-      ld8(base + (long long)(ok ? k + tap_s : k) * o->ld + tapc, v);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = ok ? v[e] : 0.f;
+      for (int j = 0; j < 4; ++j) v[j] = ldg4(base + (long long)(k0 + ta + 16 * j) * o.ld + rc);
+      vm = 0xFu;
+    } else if (KIND == COLS_CONV) {
+      vm = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = k0 + ta + 16 * j, t = k % o.seq_len + tap_s;
+        const bool ok = t >= 0 && t < o.seq_len;
+        vm |= (ok ? 1u : 0u) << j;
+        v[j] = ldg4(base + (long long)(ok ? k + tap_s : k) * o.ld + tapc);
+      }
     }
   }
 
-  __device__ __forceinline__ void store(float (*s)[LDSS], int tid, const float* v) const {
-    if (KIND <= ROWS_GEN) {
-      const int rl = tid >> 2;
+  __device__ __forceinline__ void load_generic(int k0, float4* v) const {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s[kk + e][rl] = v[e];
-    } else {
-      const int rq = (tid & 7) * 8;
+    for (int j = 0; j < 4; ++j) {
+      float e[4];
+      if (kRowImg) {
+        const int r = r0 + ta + 16 * j;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s[kk][rq + e] = v[e];
+        for (int q = 0; q < 4; ++q) {
+          const int k = k0 + tb + q;
+          e[q] = (r < R && k < K) ? fetch_rm(o, base, r, k) : 0.f;
+        }
+      } else {
+        const int k = k0 + ta + 16 * j;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = r0 + tb + q;
+          e[q] = (r < R && k < K) ? fetch_cm(o, base, r, k) : 0.f;
+        }
+      }
+      v[j] = make_float4(e[0], e[1], e[2], e[3]);
     }
+  }
+
+  __device__ __forceinline__ void store(float* img, const float4* v, unsigned vm) const {
+    if (kRowImg) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 x = (!FAST || ((vm >> j) & 1u)) ? v[j] : zero4();
+        *reinterpret_cast<float4*>(img + (ta + 16 * j) * RS + tb) = x;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float e[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+        if (FAST) {
+          const bool tok = KIND != COLS_CONV || ((vm >> j) & 1u);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float one = ((omask >> q) & 1u) ? 1.f : 0.f;
+            e[q] = (tok && ((emask >> q) & 1u)) ? e[q] : one;
+          }
+        }
+        float* d = img + (ta + 16 * j) * CS + tb;
+        d[0] = e[0]; d[1] = e[1]; d[2] = e[2]; d[3] = e[3];
+      }
+    }
+  }
+
+  // MFMA operand of steps 4q..4q+3 for lane (i = row in the wave's 32-row half at wr, h = k half)
+  __device__ __forceinline__ static float4 frag(const float* img, int wr, int i, int h, int q) {
+    if (kRowImg) return *reinterpret_cast<const float4*>(img + (wr + i) * RS + h * 32 + 4 * q);
+    const float* p = img + (h * 32 + 4 * q) * CS + wr + i;
+    return make_float4(p[0], p[CS], p[2 * CS], p[3 * CS]);
   }
 };
 
@@ -287,16 +343,94 @@ __device__ void splitk_finish(const GemmDev& g, int bidx, int m0, int n0, int ti
   }
 }
 
-template <int AK, int BKIND>
+// One pipelined stage for this wave, as ONE basic block (no branches, so the compiler counts
+// outstanding loads exactly), in a fixed order pinned by sched_barrier: first the global loads of
+// a later stage into set `rn` (they get two MFMA phases to land), then the 32 MFMAs of the
+// current slot with each fragment read issued two groups (8 MFMAs, 512 cycles) ahead of its use,
+// and the LDS writes of set `rs` (loaded one stage ago) spread over the middle groups.  Two
+// accumulators (even / odd fragment groups) keep two independent chains in the matrix core.
+template <bool FAST, int AK, int BKd>
+__device__ __forceinline__ void stage_body(const Loader<AK, FAST>& la, const Loader<BKd, FAST>& lb, const float* cur,
+                                           float* wslot, int kload, const float4* rs_a, const float4* rs_b,
+                                           unsigned ms_a, unsigned ms_b, float4* rn_a, float4* rn_b, unsigned& mn_a,
+                                           unsigned& mn_b, int wm, int wn, int li, int lh, f32x16& acc0,
+                                           f32x16& acc1) {
+  using LA = Loader<AK, FAST>;
+  using LB = Loader<BKd, FAST>;
+  la.load(kload, rn_a, mn_a);
+  lb.load(kload, rn_b, mn_b);
+  __builtin_amdgcn_sched_barrier(0);
+  float4 fa[8], fb[8];
+  fa[0] = LA::frag(cur, wm * 32, li, lh, 0);
+  fb[0] = LB::frag(cur + IMG, wn * 32, li, lh, 0);
+  fa[1] = LA::frag(cur, wm * 32, li, lh, 1);
+  fb[1] = LB::frag(cur + IMG, wn * 32, li, lh, 1);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    f32x16& acc = (q & 1) ? acc1 : acc0;
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, fb[q].x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, fb[q].y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, fb[q].z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, fb[q].w, acc, 0, 0, 0);
+    if (q + 2 < 8) {
+      fa[q + 2] = LA::frag(cur, wm * 32, li, lh, q + 2);
+      fb[q + 2] = LB::frag(cur + IMG, wn * 32, li, lh, q + 2);
+    }
+    if (q == 2) la.store(wslot, rs_a, ms_a);
+    if (q == 4) lb.store(wslot + IMG, rs_b, ms_b);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// The pipelined K loop over stages [kt0, kt1): a 3-slot LDS ring, loads two stages ahead of
+// their LDS write.  Out-of-range prefetches are clamped to the last stage (loaded, never used)
+// and stores past the end go to a slot nobody reads again, so every iteration is straight-line.
+#define FX_INLINE __attribute__((always_inline))
+template <bool FAST, int AK, int BKd>
+__device__ __forceinline__ void kloop(const Loader<AK, FAST>& la, const Loader<BKd, FAST>& lb, float* lds, int kt0,
+                                      int kt1, int wm, int wn, int li, int lh, f32x16& acc0, f32x16& acc1) {
+  const int n = kt1 - kt0;
+  if (n <= 0) return;
+  const int klast = (kt1 - 1) * BK;
+  float4 ra0[4], rb0[4], ra1[4], rb1[4];
+  unsigned ma0, mb0, ma1, mb1;
+  // prologue: stages 0 and 1 into slots 0 and 1, stage 2 in flight in set 0
+  la.load(kt0 * BK, ra0, ma0);
+  lb.load(kt0 * BK, rb0, mb0);
+  la.load(min((kt0 + 1) * BK, klast), ra1, ma1);
+  lb.load(min((kt0 + 1) * BK, klast), rb1, mb1);
+  la.store(lds, ra0, ma0);
+  lb.store(lds + IMG, rb0, mb0);
+  la.store(lds + 2 * IMG, ra1, ma1);
+  lb.store(lds + 3 * IMG, rb1, mb1);
+  la.load(min((kt0 + 2) * BK, klast), ra0, ma0);
+  lb.load(min((kt0 + 2) * BK, klast), rb0, mb0);
+  __syncthreads();
+  // iteration i multiplies slot i%3, writes stage i+2 (held in set i&1) into slot (i+2)%3,
+  // and issues the loads of stage i+3 into set (i+1)&1
+  int slot = 0;
+  auto iter = [&](int i, const float4* rs_a, const float4* rs_b, unsigned ms_a, unsigned ms_b, float4* rn_a,
+                  float4* rn_b, unsigned& mn_a, unsigned& mn_b) FX_INLINE {
+    const int ws = slot == 0 ? 2 : slot - 1;   // (slot + 2) % 3
+    stage_body<FAST, AK, BKd>(la, lb, lds + slot * 2 * IMG, lds + ws * 2 * IMG, min((kt0 + i + 3) * BK, klast), rs_a,
+                              rs_b, ms_a, ms_b, rn_a, rn_b, mn_a, mn_b, wm, wn, li, lh, acc0, acc1);
+    __syncthreads();
+    slot = slot == 2 ? 0 : slot + 1;
+  };
+  int i = 0;
+  for (; i + 1 < n; i += 2) {
+    iter(i, ra0, rb0, ma0, mb0, ra1, rb1, ma1, mb1);
+    iter(i + 1, ra1, rb1, ma1, mb1, ra0, rb0, ma0, mb0);
+  }
+  if (i < n) iter(i, ra0, rb0, ma0, mb0, ra1, rb1, ma1, mb1);
+}
+
+template <int AK, int BKIND, bool FAST>
 __global__ __launch_bounds__(NTHREADS) void gemm_f32_kernel(GemmDev g) {
-  __shared__ float sA[2][BK][LDSS];
-  __shared__ float sB[2][BK][LDSS];
+  __shared__ float lds[NSLOT * 2 * IMG];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // 8 waves: waves 0-3 multiply k rows [0,32) of every stage, waves 4-7 rows [32,64), into
-  // separate accumulators of the same 32x32 sub-tile -> two independent MFMA chains per SIMD,
-  // so one wave's loads / selects / LDS traffic hide under the other wave's MFMAs.
-  const int kh = wave >> 2, koff = kh * BKH, ltid = tid & 255;
-  const int wq = wave & 3, wm = wq >> 1, wn = wq & 1, li = lane & 31, lh = lane >> 5;
+  const int wm = wave >> 1, wn = wave & 1, li = lane & 31, lh = lane >> 5;
   // XCD-aware remap of (x, y) tiles: consecutive remapped ids share an XCD (L2)
   int tx, ty;
   {
@@ -313,89 +447,36 @@ __global__ __launch_bounds__(NTHREADS) void gemm_f32_kernel(GemmDev g) {
   const int kt0 = sk * g.kt_per_split;
   const int kt1 = min(nkt, kt0 + g.kt_per_split);
 
-  Loader<AK> la;
-  Loader<BKIND> lb;
-  la.init(g.a, g.a.ptr + (long long)bidx * g.a.batch_stride, m0, g.M, g.K, g.a_vec, ltid);
-  lb.init(g.b, g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, g.b_vec, ltid);
+  Loader<AK, FAST> la;
+  Loader<BKIND, FAST> lb;
+  la.init(g.a, g.a.ptr + (long long)bidx * g.a.batch_stride, m0, g.M, g.K, tid);
+  lb.init(g.b, g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid);
 
-  f32x16 acc;
+  f32x16 acc0, acc1;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  for (int i = 0; i < 16; ++i) {
+    acc0[i] = 0.f;
+    acc1[i] = 0.f;
+  }
   FX_STAMP(g, 0);
-
-  // Each thread stages one 8-element chunk per operand per stage (its wave group's k half).
-  // Global loads run TWO stages ahead in ping-pong register sets (r*0 / r*1, static names:
-  // a runtime-indexed register array would spill to scratch), so a stage's loads have two
-  // MFMA phases to land before they are written to LDS.
-  float ra0[8], rb0[8], ra1[8], rb1[8];
-  if (kt0 < kt1) {
-    la.load(kt0 * BK + koff, ra0);
-    lb.load(kt0 * BK + koff, rb0);
-    if (kt0 + 1 < kt1) {
-      la.load((kt0 + 1) * BK + koff, ra1);
-      lb.load((kt0 + 1) * BK + koff, rb1);
-    }
-    la.store(sA[0] + koff, ltid, ra0);
-    lb.store(sB[0] + koff, ltid, rb0);
-  }
-  __syncthreads();
-  auto stage = [&](int kt, int cur, float* ra_free, float* rb_free, const float* ra_next, const float* rb_next) {
-    if (kt + 2 < kt1) {
-      la.load((kt + 2) * BK + koff, ra_free);
-      lb.load((kt + 2) * BK + koff, rb_free);
-    }
-    // every fragment read of the half-stage first, so LDS latency overlaps the MFMA chain
-    float av[BKH / 2], bv[BKH / 2];
-#pragma unroll
-    for (int s = 0; s < BKH / 2; ++s) {
-      av[s] = sA[cur][koff + 2 * s + lh][wm * 32 + li];
-      bv[s] = sB[cur][koff + 2 * s + lh][wn * 32 + li];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int s = 0; s < BKH / 2; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
-    if (kt + 1 < kt1) {
-      la.store(sA[cur ^ 1] + koff, ltid, ra_next);
-      lb.store(sB[cur ^ 1] + koff, ltid, rb_next);
-    }
-    __syncthreads();
-  };
-  FX_STAMP(g, 1);
-  for (int kt = kt0; kt < kt1; kt += 2) {
-    stage(kt, 0, ra0, rb0, ra1, rb1);               // set 0 held stage kt (already in LDS): refill it
-    if (kt + 1 < kt1) stage(kt + 1, 1, ra1, rb1, ra0, rb0);
-  }
-
+  kloop<FAST, AK, BKIND>(la, lb, lds, kt0, kt1, wm, wn, li, lh, acc0, acc1);
   FX_STAMP(g, 2);
-  // combine the two k-half accumulators through LDS (fixed order: deterministic)
-  {
-    float* red = &sA[0][0][0];
-    if (kh == 1) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) red[(wq * 16 + r) * 64 + lane] = acc[r];
-    }
-    __syncthreads();
-    if (kh == 1 && !(g.split > 1 && g.tile_cnt)) return;
-    if (kh == 0) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] += red[(wq * 16 + r) * 64 + lane];
-    }
-  }
+  f32x16 acc = acc0 + acc1;
 
   // C/D layout of the 32x32 f32 accumulator: col = lane&31, row = (r&3)+8*(r>>2)+4*(lane>>5)
   const int col = n0 + wn * 32 + li;
   const int rbase = m0 + wm * 32 + 4 * lh;
   if (g.split > 1) {
-    if (kh == 0 && col < g.N) {
+    if (col < g.N) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = rbase + (r & 3) + 8 * (r >> 2);
         if (row < g.M) g.ws[(((long long)bidx * g.split + sk) * g.M + row) * g.N + col] = acc[r];
       }
     }
-    if (g.tile_cnt)   // flag: last word of sA (the k-half combine above uses the first 16 KB)
+    if (g.tile_cnt)   // flag: the last word of the LDS ring (free after the k loop's final barrier)
       splitk_finish<BM, BN>(g, bidx, m0, n0, (bidx * g.tiles_y + ty) * g.tiles_x + tx,
-                            reinterpret_cast<int*>(&sA[1][BK - 1][LDSS - 1]));
+                            reinterpret_cast<int*>(&lds[NSLOT * 2 * IMG - 1]));
     return;
   }
   if (col >= g.N) return;
@@ -584,35 +665,40 @@ bool operand_vec_ok(const fx_operand& o) {
 
 int kind_of(const fx_operand& o, bool vec) {
   if (o.trans) return o.conv_taps ? COLS_CONV : COLS;
-  if (o.conv_taps) return (vec && o.conv_cin % BKH == 0) ? ROWS_CONV : ROWS_GEN;
+  if (o.conv_taps) return (vec && o.conv_cin % BK == 0) ? ROWS_CONV : ROWS_GEN;   // a stage stays in one tap
   if (o.ptr1 || o.rows0 || o.rows1 || o.pos) return ROWS_GEN;
   return ROWS;
 }
 
 template <int AK, int BKd>
-void launch_t(dim3 grid, hipStream_t s, const GemmDev& g) {
-  hipLaunchKernelGGL((gemm_f32_kernel<AK, BKd>), grid, dim3(NTHREADS), 0, s, g);
+void launch_t(dim3 grid, hipStream_t s, const GemmDev& g, bool fast) {
+  if (fast)
+    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKd, true>), grid, dim3(NTHREADS), 0, s, g);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKd, false>), grid, dim3(NTHREADS), 0, s, g);
 }
 
 template <int AK>
-int launch_b(int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
+int launch_b(int bk, dim3 grid, hipStream_t s, const GemmDev& g, bool fast) {
   switch (bk) {
-    case ROWS: launch_t<AK, ROWS>(grid, s, g); return FX_OK;
-    case COLS: launch_t<AK, COLS>(grid, s, g); return FX_OK;
-    case COLS_CONV: launch_t<AK, COLS_CONV>(grid, s, g); return FX_OK;
-    case ROWS_GEN: launch_t<AK, ROWS_GEN>(grid, s, g); return FX_OK;
+    case ROWS: launch_t<AK, ROWS>(grid, s, g, fast); return FX_OK;
+    case COLS: launch_t<AK, COLS>(grid, s, g, fast); return FX_OK;
+    case COLS_CONV: launch_t<AK, COLS_CONV>(grid, s, g, fast); return FX_OK;
+    case ROWS_GEN: launch_t<AK, ROWS_GEN>(grid, s, g, false); return FX_OK;
     default: break;
   }
   set_error("gemm: unsupported B operand kind");
   return FX_ERR_UNSUPPORTED;
 }
 
+// FAST loop: both operands 16-B vector-loadable, K a multiple of the 64-deep stage, no gathers
 int launch_tiled(int ak, int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
+  const bool fast = g.a_vec && g.b_vec && (g.K % BK) == 0 && ak != ROWS_GEN && bk != ROWS_GEN;
   switch (ak) {
-    case ROWS: return launch_b<ROWS>(bk, grid, s, g);
-    case ROWS_CONV: return launch_b<ROWS_CONV>(bk, grid, s, g);
-    case ROWS_GEN: return launch_b<ROWS_GEN>(bk, grid, s, g);
-    case COLS: return launch_b<COLS>(bk, grid, s, g);
+    case ROWS: return launch_b<ROWS>(bk, grid, s, g, fast);
+    case ROWS_CONV: return launch_b<ROWS_CONV>(bk, grid, s, g, fast);
+    case ROWS_GEN: return launch_b<ROWS_GEN>(bk, grid, s, g, false);
+    case COLS: return launch_b<COLS>(bk, grid, s, g, fast);
     default: break;
   }
   set_error("gemm: unsupported A operand kind");

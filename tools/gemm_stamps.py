@@ -41,14 +41,13 @@ def run(M, N, K, a, b, c, ldc, **kw):
 def report(name, s):
     mt = s[:, 0, :, 0].astype(np.float64)
     rt = s[:, 0, :, 1].astype(np.float64)
-    pro = mt[:, 1] - mt[:, 0]
-    loop = mt[:, 2] - mt[:, 1]
+    loop = mt[:, 2] - mt[:, 0]     # prologue + k loop (slot 1 is not stamped)
     epi = mt[:, 3] - mt[:, 2]
     span = (rt[:, 3].max() - rt[:, 0].min()) * 10.0   # 100 MHz -> ns
     start_spread = (rt[:, 0].max() - rt[:, 0].min()) * 10.0
     clk = (mt[:, 3] - mt[:, 0]) / ((rt[:, 3] - rt[:, 0]) * 10.0)   # cycles per ns
     print(f"{name}: blocks {len(mt)} span {span/1e3:.2f} us, start spread {start_spread/1e3:.2f} us, clock {np.median(clk):.2f} GHz")
-    for lab, v in (("prologue", pro), ("k-loop", loop), ("epilogue", epi)):
+    for lab, v in (("k-loop", loop), ("epilogue", epi)):
         print(f"   {lab:9s} cycles median {np.median(v):9.0f}  min {v.min():9.0f}  max {v.max():9.0f}")
 
 
