@@ -171,13 +171,15 @@ def main():
 
     from factmx import native
     from factmx.dp import FlatGradReducer
+    from factmx.optim import FusedAdam
     lib = native.load()
 
     cfg = make_cfg()
     net, _ = build_model(cfg, D_IN, NCLS, dev, seed=0)
     net.train()
     reducer = FlatGradReducer(net.parameters())
-    opt = torch.optim.Adam(net.parameters(), lr=cfg.lr)
+    # clip_grad_norm_(cfg.clip_grad_norm) + Adam(lr) of scripts/train.py:265-267, fused on the flat buffers
+    opt = FusedAdam(net.parameters(), lr=cfg.lr, max_grad_norm=cfg.clip_grad_norm, grad_flat=reducer.flat)
     seqs, labels = [], []
     for v in range(args.videos):
         f, l_ = make_video(args.T, D_IN, NCLS, cfg, seed=1 + rank * args.videos + v)
@@ -189,8 +191,7 @@ def main():
         loss, _ = net(seqs, labels, compute_loss=True)
         loss.backward()
         reducer.all_reduce_mean()
-        torch.nn.utils.clip_grad_norm_(net.parameters(), cfg.clip_grad_norm)
-        opt.step()
+        opt.step()                      # clip_grad_norm_ + Adam
         return loss
 
     for _ in range(args.warmup):

@@ -27,7 +27,8 @@ int launch_softmax_rows(const float* x, long long ldx, int rows, int cols, float
 int launch_softmax_rows_bwd(const float* p, long long ldp, const float* dp, long long lddp, const float* extra,
                             long long lde, int rows, int cols, float scale, float* dl, long long ldd,
                             hipStream_t s);
-int launch_pf_fwd(const float* x, long long ldx, int rows, int cols, int n, float* out, long long ldo,
+int launch_pf_fwd(const float* x, long long ldx, int rows, int cols, int n, float* out, long long ldo, float* clogit,
+                  long long ldc,
                   hipStream_t s);
 int launch_pf_bwd(const float* out, long long ldo, const float* dout, long long lddo, const float* dcl,
                   long long lddc, int rows, int cols, int n, float* dx, long long lddx, hipStream_t s);
@@ -473,8 +474,8 @@ int fx_softmax_rows_bwd(const float* probs, long long ldp, const float* dprobs, 
 }
 
 int fx_process_feature_fwd(const float* x, long long ldx, int rows, int cols, int n, float* out, long long ldo,
-                           void* stream) {
-  return launch_pf_fwd(x, ldx, rows, cols, n, out, ldo, (hipStream_t)stream);
+                           float* clogit, long long ldc, void* stream) {
+  return launch_pf_fwd(x, ldx, rows, cols, n, out, ldo, clogit, ldc, (hipStream_t)stream);
 }
 
 int fx_process_feature_bwd(const float* out, long long ldo, const float* dout, long long lddo, const float* dclogit,

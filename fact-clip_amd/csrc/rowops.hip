@@ -258,7 +258,7 @@ __global__ __launch_bounds__(256) void softmax_bwd_wave_kernel(const float* p, l
 
 // ---------------------------------------------------------------- process_feature
 __global__ __launch_bounds__(256) void pf_fwd_kernel(const float* x, long long ldx, int rows, int cols, int n,
-                                                     float* out, long long ldo) {
+                                                     float* out, long long ldo, float* clogit, long long ldc) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -273,6 +273,8 @@ __global__ __launch_bounds__(256) void pf_fwd_kernel(const float* x, long long l
   for (int c = lane; c < n; c += 64) s += __expf(xr[f + c] - m);
   const float inv = 1.f / wave_sum(s);
   for (int c = lane; c < n; c += 64) orow[f + c] = __expf(xr[f + c] - m) * inv;
+  if (clogit)
+    for (int c = lane; c < n; c += 64) clogit[(long long)row * ldc + c] = xr[f + c];
 }
 
 __global__ __launch_bounds__(256) void pf_bwd_kernel(const float* out, long long ldo, const float* dout,
@@ -391,10 +393,10 @@ int launch_softmax_rows_bwd(const float* p, long long ldp, const float* dp, long
 }
 
 int launch_pf_fwd(const float* x, long long ldx, int rows, int cols, int n, float* out, long long ldo,
-                  hipStream_t s) {
+                  float* clogit, long long ldc, hipStream_t s) {
   FX_REQUIRE(n > 0 && n <= cols, "process_feature: need 0 < n <= cols");
   if (rows == 0) return FX_OK;
-  hipLaunchKernelGGL(pf_fwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, rows, cols, n, out, ldo);
+  hipLaunchKernelGGL(pf_fwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, rows, cols, n, out, ldo, clogit, ldc);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }

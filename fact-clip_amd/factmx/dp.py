@@ -32,8 +32,12 @@ class FlatGradReducer:
         self.buckets = [self.flat[i:i + per] for i in range(0, total, per)]
 
     def zero_grad(self):
-        """Zero in place (keeps the .grad views; never set grads to None)."""
+        """Zero in place (keeps the .grad views; never set grads to None).  The views are
+        re-verified every 64th call only (a Python loop over 400+ tensors is host time)."""
         self.flat.zero_()
+        self._calls = getattr(self, "_calls", -1) + 1
+        if self._calls % 64:
+            return
         for p in self.params:
             if p.grad is None or p.grad.data_ptr() < self.flat.data_ptr() or \
                     p.grad.data_ptr() >= self.flat.data_ptr() + self.flat.numel() * self.flat.element_size():
@@ -45,6 +49,12 @@ class FlatGradReducer:
             return
         world = dist.get_world_size(self.group)
         if world == 1:
+            return
+        if dist.get_backend(self.group) == "nccl":
+            # RCCL averages in the collective itself (no extra scale launch)
+            works = [dist.all_reduce(b, op=dist.ReduceOp.AVG, group=self.group, async_op=True) for b in self.buckets]
+            for w in works:
+                w.wait()
             return
         works = [dist.all_reduce(b, op=dist.ReduceOp.SUM, group=self.group, async_op=True) for b in self.buckets]
         for w in works:

@@ -33,7 +33,7 @@ def _2d(t):
     """(N, 1, C) or (N, C) -> (N, C) view with unit column stride."""
     if t.dim() == 3:
         assert t.shape[1] == 1, t.shape
-        t = t[:, 0, :]
+        t = t.squeeze(1)          # a view: its backward is a view too (t[:, 0] would zero-fill + copy)
     if t.stride(-1) != 1:
         t = t.contiguous()
     return t
@@ -170,36 +170,41 @@ def layer_norm(x, w, b, eps=1e-5, residual=None, relu=False):
 # ---------------------------------------------------------------------------
 
 class ProcessFeatureFn(torch.autograd.Function):
-    """``Block.process_feature`` (blocks.py:195-202): out = [x[:, :-n], softmax(x[:, -n:])]."""
+    """``Block.process_feature`` (blocks.py:195-202): out = [x[:, :-n], softmax(x[:, -n:])] and the
+    class logits x[:, -n:] as a second output, so their gradient (from the losses) enters the
+    backward kernel directly instead of through a zero-filled slice gradient plus an add."""
 
     @staticmethod
     def forward(ctx, x, n):
         lib = nx.load()
         rows, cols = x.shape
         out = _empty(rows, cols, device=x.device)
-        _check(lib.fx_process_feature_fwd(nx.ptr(x), nx.ld(x), rows, cols, n, nx.ptr(out), cols, nx.stream()),
-               "fx_process_feature_fwd")
+        clogit = _empty(rows, n, device=x.device)
+        _check(lib.fx_process_feature_fwd(nx.ptr(x), nx.ld(x), rows, cols, n, nx.ptr(out), cols, nx.ptr(clogit), n,
+                                          nx.stream()), "fx_process_feature_fwd")
         ctx.n = n
         ctx.save_for_backward(out)
-        return out
+        return out, clogit
 
     @staticmethod
-    def backward(ctx, dout):
+    def backward(ctx, dout, dclogit):
         lib = nx.load()
         (out,) = ctx.saved_tensors
-        dout = dout.contiguous()
         rows, cols = out.shape
+        if dout is None:
+            dout = torch.zeros_like(out)
+        dout = dout.contiguous()
+        dclogit = None if dclogit is None else dclogit.contiguous()
         dx = _empty(rows, cols, device=out.device)
-        _check(lib.fx_process_feature_bwd(nx.ptr(out), cols, nx.ptr(dout), cols, None, 0, rows, cols, ctx.n,
-                                          nx.ptr(dx), cols, nx.stream()), "fx_process_feature_bwd")
+        _check(lib.fx_process_feature_bwd(nx.ptr(out), cols, nx.ptr(dout), cols, nx.ptr(dclogit), ctx.n, rows, cols,
+                                          ctx.n, nx.ptr(dx), cols, nx.stream()), "fx_process_feature_bwd")
         return dx, None
 
 
 def process_feature(x, n):
-    """Returns (feature-with-probs, clogit view) exactly like the reference."""
-    x2 = _2d(x)
-    out = ProcessFeatureFn.apply(x2, n)
-    return out, x2[:, -n:]
+    """Returns (feature-with-probs, class logits) like the reference (its clogit is a view of the
+    input; here it is a copy with the same values written by the same kernel)."""
+    return ProcessFeatureFn.apply(_2d(x), n)
 
 
 # ---------------------------------------------------------------------------

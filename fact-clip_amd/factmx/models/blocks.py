@@ -174,8 +174,8 @@ class UpdateBlock(Block):
         self.action_feature = action_feature[:, :, :-(self.nclass + 1)]
         self.f2a_attn = self.f2a_layer.attn[0]
         self.a2f_attn = self.a2f_layer.attn[0]
-        self.f2a_attn_logit = self.f2a_layer.attn_logit[0].unsqueeze(0)
-        self.a2f_attn_logit = self.a2f_layer.attn_logit[0].unsqueeze(0)
+        self.f2a_attn_logit = self.f2a_layer.attn_logit.squeeze(0).unsqueeze(0)
+        self.a2f_attn_logit = self.a2f_layer.attn_logit.squeeze(0).unsqueeze(0)
         return frame_feature, action_feature
 
     def compute_loss(self, criterion, match=None):
@@ -235,9 +235,9 @@ class UpdateBlockTDU(Block):
         self.tdu = tdu
         self.action_clogit = action_clogit
         self.action_feature = action_feature[:, :, :-(self.nclass + 1)]
-        self.f2a_attn_logit = self.f2a_layer.attn_logit[0].unsqueeze(0)
+        self.f2a_attn_logit = self.f2a_layer.attn_logit.squeeze(0).unsqueeze(0)
         self.f2a_attn = tdu.attn_seg2frame(self.f2a_layer.attn[0].transpose(2, 1)).transpose(2, 1)
-        self.a2f_attn_logit = self.a2f_layer.attn_logit[0].unsqueeze(0)
+        self.a2f_attn_logit = self.a2f_layer.attn_logit.squeeze(0).unsqueeze(0)
         self.a2f_attn = tdu.attn_seg2frame(self.a2f_layer.attn[0])
         return frame_feature, action_feature
 
@@ -414,7 +414,10 @@ class FACT_CLIP(_FACTBase):
         return ((1 - w) * ab + w * clip_prob).argmax(1)
 
     def forward(self, seq_list, label_list, compute_loss=False):
-        save_list, losses = [], []
+        """blocks.py:889-917.  The per-video loss floats of ``save['loss']`` are read back in one
+        device->host copy after the last video (the reference calls .item() three times per
+        video, each a full device drain); values and keys are the same."""
+        save_list, losses, pending = [], [], []
         for seq, label in zip(seq_list, label_list):
             trans = torch_class_label_to_segment_label(label)[0]
             self._forward_one_video(seq.unsqueeze(1), trans)
@@ -423,12 +426,19 @@ class FACT_CLIP(_FACTBase):
             if compute_loss:
                 lo = self._loss_one_video(label)
                 losses.append(lo)
-                ld = {"loss": lo.item()}
+                keys, vals = ["loss"], [lo.detach()]
                 if hasattr(self, "fact_loss"):
-                    ld["fact_loss"] = self.fact_loss.item()
+                    keys.append("fact_loss")
+                    vals.append(self.fact_loss.detach().reshape(()))
                 if hasattr(self, "contrastive_loss"):
-                    ld["contrastive_loss"] = self.contrastive_loss.item()
-                save["loss"] = ld
+                    keys.append("contrastive_loss")
+                    vals.append(self.contrastive_loss.detach().reshape(()))
+                pending.append((save, keys, vals))
         if compute_loss:
+            flat = torch.stack([v.float() for _, _, vals in pending for v in vals]).tolist()
+            i = 0
+            for save, keys, vals in pending:
+                save["loss"] = dict(zip(keys, flat[i:i + len(keys)]))
+                i += len(keys)
             return sum(losses) / len(losses), save_list
         return save_list

@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FACTMX_LIB", os.path.join(_HERE, "_lib", "libfactmx.so"))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -72,7 +72,7 @@ SIGNATURES = {
     "fx_layernorm_bwd": (I, [P, L, P, L, P, L, P, P, I, I, I, P, L, P, P, P, P]),
     "fx_softmax_rows": (I, [P, L, I, I, F, P, L, P]),
     "fx_softmax_rows_bwd": (I, [P, L, P, L, P, L, I, I, F, P, L, P]),
-    "fx_process_feature_fwd": (I, [P, L, I, I, I, P, L, P]),
+    "fx_process_feature_fwd": (I, [P, L, I, I, I, P, L, P, L, P]),
     "fx_process_feature_bwd": (I, [P, L, P, L, P, L, I, I, I, P, L, P]),
     "fx_l2norm_fwd": (I, [P, L, I, I, P, L, P, P]),
     "fx_l2norm_bwd": (I, [P, L, P, P, L, I, I, P, L, P]),
@@ -89,6 +89,10 @@ SIGNATURES = {
     "fx_seg_mean_fwd": (I, [P, L, P, P, I, I, P, L, P]),
     "fx_seg_mean_bwd": (I, [P, L, P, P, P, I, I, P, L, I, P]),
     "fx_seg_sum_rows": (I, [P, L, P, P, I, I, P, L, I, P]),
+    "fx_grad_norm_workspace_floats": (L, []),
+    "fx_grad_norm": (I, [P, L, P, P, P]),
+    "fx_clip_grad_scale": (I, [P, L, P, F, P]),
+    "fx_adam_step": (I, [P, P, P, P, L, L, F, F, F, F, F, F, P, P, P]),
     "fx_prof_enable": (I, [I, I]),
     "fx_prof_collect": (I, [I, ctypes.POINTER(D), ctypes.POINTER(D), ctypes.POINTER(D), ctypes.POINTER(I)]),
     "fx_prof_disable": (None, []),

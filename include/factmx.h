@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FX_ABI_VERSION 1
+#define FX_ABI_VERSION 2
 
 enum {
   FX_OK = 0,
@@ -217,7 +217,9 @@ int fx_layernorm_bwd(const float* dy, long long lddy, const float* y, long long 
  *   used for attention (basic.py:376 X2Y softmax; MultiheadAttention).
  * fx_softmax_rows_bwd: dlogit = scale * p * (dp - sum(dp*p)) (+ dlogit_extra).
  * fx_process_feature_fwd: Block.process_feature (blocks.py:195-202):
- *   out[:, :cols-n] = x[:, :cols-n]; out[:, cols-n:] = softmax(x[:, cols-n:])
+ *   out[:, :cols-n] = x[:, :cols-n]; out[:, cols-n:] = softmax(x[:, cols-n:]);
+ *   clogit (nullable, rows x n, ldc) = x[:, cols-n:] (the class logits the
+ *   losses read, as a separate tensor so their gradient enters dclogit)
  * fx_process_feature_bwd: dx = [dout_feat, softmax_bwd(dout_prob) + dclogit]
  * ---------------------------------------------------------------------- */
 int fx_softmax_rows(const float* logits, long long ldl, int rows, int cols, float scale,
@@ -226,7 +228,7 @@ int fx_softmax_rows_bwd(const float* probs, long long ldp, const float* dprobs, 
                         const float* dlogit_extra, long long lde, int rows, int cols, float scale,
                         float* dlogit, long long ldd, void* stream);
 int fx_process_feature_fwd(const float* x, long long ldx, int rows, int cols, int n, float* out,
-                           long long ldo, void* stream);
+                           long long ldo, float* clogit, long long ldc, void* stream);
 int fx_process_feature_bwd(const float* out, long long ldo, const float* dout, long long lddo,
                            const float* dclogit, long long lddc, int rows, int cols, int n, float* dx,
                            long long lddx, void* stream);
@@ -306,6 +308,25 @@ int fx_relu_bwd(const float* dy, long long lddy, const float* y, long long ldy, 
                 float* dz, long long lddz, void* stream);
 int fx_add(const float* a, long long lda, const float* b, long long ldb, int rows, int cols,
            float* out, long long ldo, int accumulate, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Train-step tail on flat fp32 buffers (scripts/train.py:265-267:
+ * torch.nn.utils.clip_grad_norm_(params, max_norm) + torch.optim.Adam.step()).
+ * fx_grad_norm: workspace (fx_grad_norm_workspace_floats) <- deterministic
+ *   partial sums of g^2; norm_out (nullable, 1 float) <- ||g||_2.
+ * fx_clip_grad_scale: g *= min(max_norm / (||g|| + 1e-6), 1) from a workspace
+ *   filled by fx_grad_norm (clip_grad_norm_ alone).
+ * fx_adam_step: optional clipping (max_norm > 0: norm computed in-launch into
+ *   workspace, g scaled and written back as clip_grad_norm_ leaves it), then
+ *   torch.optim.Adam (amsgrad off, L2 weight_decay, bias corrections for the
+ *   1-based `step`).  p, g, m, v: n floats, 16-byte aligned.
+ * ---------------------------------------------------------------------- */
+long long fx_grad_norm_workspace_floats(void);
+int fx_grad_norm(const float* g, long long n, float* workspace, float* norm_out, void* stream);
+int fx_clip_grad_scale(float* g, long long n, const float* workspace, float max_norm, void* stream);
+int fx_adam_step(float* p, float* g, float* m, float* v, long long n, long long step, float lr,
+                 float beta1, float beta2, float eps, float weight_decay, float max_norm,
+                 float* workspace, float* norm_out, void* stream);
 
 /* ------------------------------------------------------------------------
  * Profiling hooks: HIP-event timing of every launch of one kernel class
