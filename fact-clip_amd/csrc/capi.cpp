@@ -10,42 +10,9 @@
 #include <vector>
 
 #include "fx_common.h"
+#include "ops.h"
 
 namespace fx {
-
-// ---- kernels implemented in the other translation units -------------------
-long long colsum_workspace_floats(int M, int N);
-int launch_layernorm_fwd(const float* x, long long ldx, const float* r, long long ldr, const float* w,
-                         const float* b, float eps, int rows, int cols, int relu, float* y, long long ldy,
-                         float* mean, float* rstd, float* xhat, long long ldxh, hipStream_t s);
-long long layernorm_bwd_ws_floats(int rows, int cols);
-int launch_layernorm_bwd(const float* dy, long long lddy, const float* y, long long ldy, const float* xhat,
-                         long long ldxh, const float* w, const float* rstd, int rows, int cols, int relu,
-                         float* dx, long long lddx, float* dw, float* db, float* ws, hipStream_t s);
-int launch_softmax_rows(const float* x, long long ldx, int rows, int cols, float scale, float* p, long long ldp,
-                        hipStream_t s);
-int launch_softmax_rows_bwd(const float* p, long long ldp, const float* dp, long long lddp, const float* extra,
-                            long long lde, int rows, int cols, float scale, float* dl, long long ldd,
-                            hipStream_t s);
-int launch_pf_fwd(const float* x, long long ldx, int rows, int cols, int n, float* out, long long ldo, float* clogit,
-                  long long ldc,
-                  hipStream_t s);
-int launch_pf_bwd(const float* out, long long ldo, const float* dout, long long lddo, const float* dcl,
-                  long long lddc, int rows, int cols, int n, float* dx, long long lddx, hipStream_t s);
-int launch_l2n_fwd(const float* x, long long ldx, int rows, int cols, float* y, long long ldy, float* nrm,
-                   hipStream_t s);
-int launch_l2n_bwd(const float* y, long long ldy, const float* nrm, const float* dy, long long lddy, int rows,
-                   int cols, float* dx, long long lddx, hipStream_t s);
-int launch_segments(const float* x, long long ldx, int col0, int ncls, int T, int32_t* pred, int32_t* seg_id,
-                    int32_t* seg_start, int32_t* seg_end, int32_t* num_seg, hipStream_t s);
-int launch_seg_reduce(const float* x, long long ldx, const int32_t* st, const int32_t* en, int S, int cols, int mean,
-                      float* y, long long ldy, int accumulate, hipStream_t s);
-int launch_seg_mean_bwd(const float* dy, long long lddy, const int32_t* sid, const int32_t* st, const int32_t* en,
-                        int T, int cols, float* dx, long long lddx, int accumulate, hipStream_t s);
-int launch_gru_fwd(const float* gi, long long ldgi, int S, int Hh, const float* const whh[2], const float* const bhh[2],
-                   float* out, long long ldo, float* saved, float* ws, hipStream_t s);
-int launch_gru_bwd(const float* dout, long long lddo, int S, int Hh, const float* const whh[2], const float* saved,
-                   float* dgi, long long lddgi, float* dgh, hipStream_t s);
 
 // ---- error state ------------------------------------------------------------
 static thread_local std::string g_last_error;
@@ -124,6 +91,8 @@ __global__ void pack_conv_kernel(PackArgs p) {
   }
 }
 
+}  // namespace
+
 int ew_grid(long long total) { return (int)std::min<long long>(std::max<long long>(cdiv(total, 256), 1), 4096); }
 
 int relu_bwd(const float* dy, long long lddy, const float* y, long long ldy, int rows, int cols, float* dz,
@@ -145,7 +114,7 @@ int add2(const float* a, long long lda, const float* b, long long ldb, int rows,
 }
 
 // split-K factor for small-output / long-K products (dW over frames, token x frame)
-int pick_split(int M, int N, int K, int batch = 1) {
+int pick_split(int M, int N, int K, int batch) {
   const long long tiles = (long long)cdiv(M, 64) * cdiv(N, 64) * batch;
   const int nkt = cdiv(K, 64);   // 64-deep K stages of the GEMM kernel
   if (tiles >= 160 || nkt < 4) return 1;
@@ -154,15 +123,14 @@ int pick_split(int M, int N, int K, int batch = 1) {
   return std::max(sp, 1);
 }
 
-long long split_ws(int M, int N, int K, int batch = 1) {
+long long split_ws(int M, int N, int K, int batch) {
   const int sp = pick_split(M, N, K, batch);
   return sp > 1 ? (long long)sp * M * N * batch : 0;
 }
 
 // y = (x [+pos on the first pos_cols columns]) . w^T (+b) (+relu);  w (N,K) with row stride ldw
 int linear_fwd(const float* x, long long ldx, int M, int K, const float* w, const float* b, float* y, long long ldy,
-               int N, int relu, hipStream_t s, long long ldw = -1, const float* pos = nullptr,
-               long long ldpos = 0, int pos_cols = 0) {
+               int N, int relu, hipStream_t s, long long ldw, const float* pos, long long ldpos, int pos_cols) {
   fx_gemm_desc d = gemm_desc(M, N, K, op_rows(x, ldx), op_rows(w, ldw < 0 ? K : ldw), y, ldy);
   d.a.pos = pos;
   d.a.ld_pos = ldpos;
@@ -174,7 +142,7 @@ int linear_fwd(const float* x, long long ldx, int M, int K, const float* w, cons
 
 // dx (+)= dy . w  [* (gate > 0)];  w (N,K)
 int linear_dx(const float* dy, long long lddy, const float* w, int M, int K, int N, float* dx, long long lddx,
-              int accumulate, const float* gate, long long ld_gate, float* ws, hipStream_t s, long long ldw = -1) {
+              int accumulate, const float* gate, long long ld_gate, float* ws, hipStream_t s, long long ldw) {
   fx_gemm_desc d = gemm_desc(M, K, N, op_rows(dy, lddy), op_cols(w, ldw < 0 ? K : ldw), dx, lddx);
   d.beta = accumulate ? 1.f : 0.f;
   d.gate = gate;
@@ -187,7 +155,7 @@ int linear_dx(const float* dy, long long lddy, const float* w, int M, int K, int
 // dw (+)= dy^T . x  and  db (+)= colsum(dy)  in ONE GEMM: x gets a virtual all-ones column K
 // whose output column (the bias gradient) is routed to db.  dy (M,N), x (M,K) -> dw (N,K), ld lddw.
 int linear_dwdb(const float* dy, long long lddy, const float* x, long long ldx, int M, int K, int N, float* dw,
-                float* db, int accumulate, float* ws, hipStream_t s, long long lddw = -1) {
+                float* db, int accumulate, float* ws, hipStream_t s, long long lddw) {
   if (!dw && !db) return FX_OK;
   FX_REQUIRE(dw, "linear_dwdb: bias-only gradient needs dw");
   fx_operand b = op_cols(x, ldx);
@@ -202,11 +170,13 @@ int linear_dwdb(const float* dy, long long lddy, const float* x, long long ldx, 
 }
 
 int linear_dw(const float* dy, long long lddy, const float* x, long long ldx, int M, int K, int N, float* dw,
-              int accumulate, float* ws, hipStream_t s, long long lddw = -1) {
+              int accumulate, float* ws, hipStream_t s, long long lddw) {
   return linear_dwdb(dy, lddy, x, ldx, M, K, N, dw, nullptr, accumulate, ws, s, lddw);
 }
 
 long long dwdb_ws(int M, int K, int N) { return split_ws(N, K + 1, M); }
+
+namespace {
 
 // ---- MS-TCN layout of saved activations / workspace --------------------------------
 struct MstcnLayout {

@@ -1,0 +1,480 @@
+// Action-token decoders, whole stack per call: SCADecoder (basic.py:525-557, SCALayer
+// basic.py:454-523) and SADecoder (basic.py:561-593, SALayer basic.py:391-452).
+//
+// The reference runs each layer as ~15 ATen ops from Python (plus positional-encoding clones,
+// autograd grad accumulations and MultiheadAttention's own reshapes).  Here one C call runs the
+// whole decoder forward (or backward) on the caller's stream:
+//   * the cross-attention key/value projections of ALL layers read the same frame memory, so
+//     they are ONE GEMM  KV = memory . [Wk_0..Wk_{L-1} | Wv_0..Wv_{L-1}]^T  (T x 2AL) instead of
+//     2L frame-level GEMMs; backward likewise folds into one dMemory GEMM (K = 2AL) and one
+//     weight-gradient GEMM (the frame-level work of the decoder is three large GEMMs);
+//   * the self-attention core over the Q tokens is one fused launch per direction
+//     (attn_small.hip); the cross-attention core over T frames uses the MHA core GEMMs;
+//   * residual adds ride in GEMM epilogues, bias gradients in the weight-gradient GEMMs.
+// Post-norm, ReLU FFN, eval-mode dropout; SALayer/SCALayer value has no positional term
+// (sa_value_w_pos = ca_value_w_pos = vpos = False, as the reference builds them).
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "fx_common.h"
+#include "ops.h"
+
+namespace fx {
+namespace {
+
+constexpr int MAXL = 16;
+
+struct PackKV {
+  const float* src[2 * MAXL];   // k_w[0..L-1], v_w[0..L-1]   (A x Hm each)
+  const float* bsrc[2 * MAXL];  // in_proj_bias + A, + 2A       (A each)
+  float* dst;                   // (2AL x Hm)
+  float* bdst;                  // (2AL)
+  int A, Hm, L;
+};
+
+// pack the per-layer cross-attention K/V weights and biases into one row-major (2AL x Hm) operand
+__global__ void pack_kv_kernel(PackKV p) {
+  const int blk = blockIdx.y;  // 0..2L-1
+  const long long n = (long long)p.A * p.Hm;
+  const float* src = p.src[blk];
+  float* dst = p.dst + (long long)blk * n;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < p.A; i += blockDim.x) p.bdst[blk * p.A + i] = p.bsrc[blk][i];
+}
+
+struct UnpackKV {
+  float* dst[2 * MAXL];   // dk_w[l], dv_w[l]  (accumulate)
+  float* bdst[2 * MAXL];  // d in_proj_bias + A, + 2A  (accumulate)
+  const float* src;
+  const float* bsrc;
+  int A, Hm, L;
+};
+
+__global__ void unpack_kv_acc_kernel(UnpackKV p) {
+  const int blk = blockIdx.y;
+  const long long n = (long long)p.A * p.Hm;
+  const float* src = p.src + (long long)blk * n;
+  float* dst = p.dst[blk];
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    dst[i] += src[i];
+  if (blockIdx.x == 0 && p.bdst[blk])
+    for (int i = threadIdx.x; i < p.A; i += blockDim.x) p.bdst[blk][i] += p.bsrc[blk * p.A + i];
+}
+
+// o1 = a + b (nullable b -> a);  o2 += b  (pos-path gradient accumulation)
+__global__ void add_acc_kernel(const float* a, const float* b, float* o1, float* o2, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float bv = b[i];
+    o1[i] = a[i] + bv;
+    if (o2) o2[i] += bv;
+  }
+}
+
+int add_acc(const float* a, const float* b, float* o1, float* o2, long long n, hipStream_t s) {
+  if (n == 0) return FX_OK;
+  hipLaunchKernelGGL(add_acc_kernel, dim3(ew_grid(n)), dim3(256), 0, s, a, b, o1, o2, n);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+// y = x . w^T + b + resid   (w (N, K) row stride ldw)
+int linear_fwd_res(const float* x, long long ldx, int M, int K, const float* w, long long ldw, const float* b,
+                   const float* resid, long long ldr, float* y, long long ldy, int N, hipStream_t s) {
+  fx_gemm_desc d = gemm_desc(M, N, K, op_rows(x, ldx), op_rows(w, ldw), y, ldy);
+  d.bias = b;
+  d.resid = resid;
+  d.ld_resid = ldr;
+  return launch_gemm(d, s);
+}
+
+// dx = dy . w + resid   (w (N, K) row stride ldw)
+int linear_dx_res(const float* dy, long long lddy, const float* w, long long ldw, int M, int K, int N,
+                  const float* resid, long long ldr, float* dx, long long lddx, float* ws, hipStream_t s) {
+  fx_gemm_desc d = gemm_desc(M, K, N, op_rows(dy, lddy), op_cols(w, ldw), dx, lddx);
+  d.resid = resid;
+  d.ld_resid = ldr;
+  d.split_k = pick_split(M, K, N);
+  d.workspace = ws;
+  return launch_gemm(d, s);
+}
+
+struct DecLayout {
+  // per-layer saved offsets (relative to layer base) and the layer stride
+  long long xq, qkv, psa, osa, xh1, rs1, t1, t1q, qc, pca, oca, xh2, rs2, t2, f1, xh3, rs3, t3, per_layer;
+  long long layers, fxh, frs, fo, kv, mpos, total_saved;
+  // workspace (fwd)
+  long long wkv, bkv, wsp, total_ws_fwd;
+  // workspace (bwd)
+  long long dkv, dwkv, dbkv, dT, dS, dU, dF, dQKV, dO, dq, G, P, lnws, core, split, total_ws_bwd;
+};
+
+long long dec_split_ws(const fx_decoder_params* p, int R, int T) {
+  const int A = p->A, FF = p->FF;
+  long long sp = 0;
+  sp = std::max(sp, dwdb_ws(R, A, 3 * A));
+  sp = std::max(sp, dwdb_ws(R, A, A));
+  sp = std::max(sp, dwdb_ws(R, A, FF));
+  sp = std::max(sp, dwdb_ws(R, FF, A));
+  sp = std::max(sp, split_ws(R, A, 3 * A));
+  sp = std::max(sp, split_ws(R, A, FF));
+  sp = std::max(sp, split_ws(R, FF, A));
+  sp = std::max(sp, dwdb_ws(R, A, p->out_dim));
+  sp = std::max(sp, split_ws(R, A, p->out_dim));
+  if (p->cross) {
+    const long long AL2 = 2LL * A * p->num_layers;
+    sp = std::max(sp, split_ws(T, (int)AL2, p->Hm));
+    sp = std::max(sp, dwdb_ws(T, p->Hm, (int)AL2));
+    sp = std::max(sp, split_ws(T, p->Hm, (int)AL2));
+  }
+  return sp;
+}
+
+DecLayout dec_layout(const fx_decoder_params* p, int R, int T, int has_qpos, int has_mpos) {
+  DecLayout L{};
+  const long long A = p->A, FF = p->FF, h = p->nhead, RA = (long long)R * A;
+  long long o = 0;
+  L.xq = o; o += has_qpos ? RA : 0;
+  L.qkv = o; o += 3 * RA;
+  L.psa = o; o += h * R * R;
+  L.osa = o; o += RA;
+  L.xh1 = o; o += RA;
+  L.rs1 = o; o += R;
+  L.t1 = o; o += RA;
+  if (p->cross) {
+    L.t1q = o; o += has_qpos ? RA : 0;
+    L.qc = o; o += RA;
+    L.pca = o; o += h * R * T;
+    L.oca = o; o += RA;
+    L.xh2 = o; o += RA;
+    L.rs2 = o; o += R;
+    L.t2 = o; o += RA;
+  }
+  L.f1 = o; o += (long long)R * FF;
+  L.xh3 = o; o += RA;
+  L.rs3 = o; o += R;
+  L.t3 = o; o += RA;
+  L.per_layer = o;
+  L.layers = 0;
+  o = L.layers + L.per_layer * p->num_layers;
+  L.fxh = o; o += p->final_norm ? RA : 0;
+  L.frs = o; o += p->final_norm ? R : 0;
+  L.fo = o; o += p->final_norm ? RA : 0;
+  const long long AL2 = 2 * A * p->num_layers;
+  L.kv = o; o += p->cross ? (long long)T * AL2 : 0;
+  L.mpos = o; o += (p->cross && has_mpos) ? (long long)T * p->Hm : 0;
+  L.total_saved = o;
+  const long long sp = dec_split_ws(p, R, T);
+  // forward workspace
+  o = 0;
+  L.wkv = o; o += p->cross ? AL2 * p->Hm : 0;
+  L.bkv = o; o += p->cross ? AL2 : 0;
+  L.wsp = o; o += std::max(sp, p->cross ? fx_mha_core_workspace_floats(R, T, (int)A, (int)h) : 0LL) + RA;
+  L.total_ws_fwd = o;
+  // backward workspace
+  o = 0;
+  L.dkv = o; o += p->cross ? (long long)T * AL2 : 0;
+  L.dwkv = o; o += p->cross ? AL2 * p->Hm : 0;
+  L.dbkv = o; o += p->cross ? AL2 : 0;
+  L.dT = o; o += RA;
+  L.dS = o; o += RA;
+  L.dU = o; o += RA;
+  L.dF = o; o += (long long)R * FF;
+  L.dQKV = o; o += 3 * RA;
+  L.dO = o; o += RA;
+  L.dq = o; o += RA;
+  L.G = o; o += RA;
+  L.P = o; o += RA;
+  L.lnws = o; o += layernorm_bwd_ws_floats(R, (int)A);
+  L.core = o; o += p->cross ? fx_mha_core_workspace_floats(R, T, (int)A, (int)h) : 0;
+  L.split = o; o += sp;
+  L.total_ws_bwd = o;
+  (void)FF;
+  return L;
+}
+
+int dec_check(const fx_decoder_params* p, int R, int T) {
+  FX_REQUIRE(p && p->num_layers >= 1 && p->num_layers <= MAXL, "decoder: 1..16 layers");
+  FX_REQUIRE(p->nhead > 0 && p->A % p->nhead == 0, "decoder: A must be divisible by nhead");
+  FX_REQUIRE(R >= 1 && R <= 64, "decoder: 1..64 tokens (fused self-attention core)");
+  FX_REQUIRE(p->A / p->nhead <= 64, "decoder: head dim must be <= 64");
+  FX_REQUIRE(p->A <= 1024, "decoder: A <= 1024 (LayerNorm row kernel)");
+  FX_REQUIRE(!p->cross || (T >= 1 && p->Hm > 0), "decoder: cross attention needs memory rows");
+  return FX_OK;
+}
+
+}  // namespace
+}  // namespace fx
+
+using namespace fx;
+
+extern "C" {
+
+long long fx_decoder_saved_floats(const fx_decoder_params* p, int R, int T, int has_qpos, int has_mpos) {
+  return dec_layout(p, R, T, has_qpos, has_mpos).total_saved;
+}
+
+long long fx_decoder_workspace_floats(const fx_decoder_params* p, int R, int T, int has_qpos, int has_mpos) {
+  const DecLayout L = dec_layout(p, R, T, has_qpos, has_mpos);
+  return std::max(L.total_ws_fwd, L.total_ws_bwd);
+}
+
+int fx_decoder_fwd(const fx_decoder_params* p, const float* tgt, long long ldt, int R, const float* qpos,
+                   long long ldqp, const float* mem, long long ldm, int T, const float* mpos, long long ldmp,
+                   float* out, long long ldo, float* saved, float* workspace, void* stream) {
+  FX_TRY(dec_check(p, R, T));
+  hipStream_t s = (hipStream_t)stream;
+  const int A = p->A, FF = p->FF, h = p->nhead, hd = A / h, NL = p->num_layers;
+  const long long RA = (long long)R * A;
+  const float eps = p->eps > 0.f ? p->eps : 1e-5f;
+  const float scale = 1.0f / std::sqrt((float)hd);
+  const DecLayout L = dec_layout(p, R, T, qpos != nullptr, mpos != nullptr);
+  FX_REQUIRE(!qpos || ldqp == A, "decoder: query_pos must be dense (R, A)");
+  float* spl = workspace + L.wsp;
+  const int AL2 = 2 * A * NL;
+  float* kv = saved + L.kv;
+  if (p->cross) {
+    // K/V projections of every layer in one frame-level GEMM (keys see mem + pos, values mem)
+    PackKV pk{};
+    for (int l = 0; l < NL; ++l) {
+      pk.src[l] = p->ca_k_w[l];
+      pk.src[NL + l] = p->ca_v_w[l];
+      pk.bsrc[l] = p->ca_in_b[l] + A;
+      pk.bsrc[NL + l] = p->ca_in_b[l] + 2 * A;
+    }
+    pk.dst = workspace + L.wkv;
+    pk.bdst = workspace + L.bkv;
+    pk.A = A;
+    pk.Hm = p->Hm;
+    pk.L = NL;
+    hipLaunchKernelGGL(pack_kv_kernel, dim3(std::min(cdiv((long long)A * p->Hm, 256), 256), 2 * NL), dim3(256), 0, s,
+                       pk);
+    FX_CHECK_HIP(hipGetLastError());
+    if (!mpos) {
+      FX_TRY(linear_fwd(mem, ldm, T, p->Hm, workspace + L.wkv, workspace + L.bkv, kv, AL2, AL2, 0, s));
+    } else {
+      const int AL = A * NL;
+      FX_TRY(linear_fwd(mem, ldm, T, p->Hm, workspace + L.wkv, workspace + L.bkv, kv, AL2, AL, 0, s, -1, mpos, ldmp,
+                        p->Hm));
+      FX_TRY(linear_fwd(mem, ldm, T, p->Hm, workspace + L.wkv + (long long)AL * p->Hm, workspace + L.bkv + AL,
+                        kv + AL, AL2, AL, 0, s));
+      // keep mem + pos for the key weight gradient
+      FX_CHECK_HIP(hipMemcpy2DAsync(saved + L.mpos, p->Hm * sizeof(float), mem, ldm * sizeof(float),
+                                    p->Hm * sizeof(float), T, hipMemcpyDeviceToDevice, s));
+      FX_TRY(add2(mpos, ldmp, nullptr, 0, T, p->Hm, saved + L.mpos, p->Hm, 1, s));
+    }
+  }
+  const float* x = tgt;
+  long long ldx = ldt;
+  for (int l = 0; l < NL; ++l) {
+    float* b = saved + L.layers + l * L.per_layer;
+    // --- self-attention over the tokens: q = k = x + qpos, v = x  (basic.py:495-503 / 438-444)
+    const float* xq = x;
+    long long ldxq = ldx;
+    if (qpos) {
+      FX_TRY(add2(x, ldx, qpos, A, R, A, b + L.xq, A, 0, s));
+      xq = b + L.xq;
+      ldxq = A;
+    }
+    float* qkv = b + L.qkv;   // (R, 3A): [q | k | v]
+    if (!qpos) {
+      FX_TRY(linear_fwd(x, ldx, R, A, p->sa_in_w[l], p->sa_in_b[l], qkv, 3 * A, 3 * A, 0, s));
+    } else {
+      FX_TRY(linear_fwd(xq, ldxq, R, A, p->sa_in_w[l], p->sa_in_b[l], qkv, 3 * A, 2 * A, 0, s));
+      FX_TRY(linear_fwd(x, ldx, R, A, p->sa_in_w[l] + 2LL * A * A, p->sa_in_b[l] + 2 * A, qkv + 2 * A, 3 * A, A, 0,
+                        s));
+    }
+    FX_TRY(launch_mha_small_fwd(qkv, 3 * A, qkv + A, 3 * A, qkv + 2 * A, 3 * A, R, R, hd, h, scale, b + L.psa,
+                                b + L.osa, A, s));
+    // t1 = LN(x + out_proj(o))
+    float* u = spl + (std::max(L.total_ws_fwd - L.wsp, RA) - RA);   // last RA floats of the scratch
+    FX_TRY(linear_fwd_res(b + L.osa, A, R, A, p->sa_out_w[l], A, p->sa_out_b[l], x, ldx, u, A, A, s));
+    FX_TRY(launch_layernorm_fwd(u, A, nullptr, 0, p->ln_sa_w[l], p->ln_sa_b[l], eps, R, A, 0, b + L.t1, A, nullptr,
+                                b + L.rs1, b + L.xh1, A, s));
+    const float* t2 = b + L.t1;
+    if (p->cross) {
+      // --- cross-attention onto the frames: q = t1 + qpos, k = mem + pos, v = mem (basic.py:504-515)
+      const float* tq = b + L.t1;
+      if (qpos) {
+        FX_TRY(add2(b + L.t1, A, qpos, A, R, A, b + L.t1q, A, 0, s));
+        tq = b + L.t1q;
+      }
+      FX_TRY(linear_fwd(tq, A, R, A, p->ca_q_w[l], p->ca_in_b[l], b + L.qc, A, A, 0, s));
+      FX_TRY(fx_mha_core_fwd(b + L.qc, A, kv + (long long)l * A, AL2, kv + (long long)(NL + l) * A, AL2, R, T, A, h,
+                             b + L.pca, b + L.oca, A, spl, s));
+      FX_TRY(linear_fwd_res(b + L.oca, A, R, A, p->ca_out_w[l], A, p->ca_out_b[l], b + L.t1, A, u, A, A, s));
+      FX_TRY(launch_layernorm_fwd(u, A, nullptr, 0, p->ln_ca_w[l], p->ln_ca_b[l], eps, R, A, 0, b + L.t2, A,
+                                  nullptr, b + L.rs2, b + L.xh2, A, s));
+      t2 = b + L.t2;
+    }
+    // --- FFN: t3 = LN(t2 + W2 relu(W1 t2 + b1) + b2)   (basic.py:516-522 / 446-450)
+    FX_TRY(linear_fwd(t2, A, R, A, p->ff1_w[l], p->ff1_b[l], b + L.f1, FF, FF, 1, s));
+    FX_TRY(linear_fwd_res(b + L.f1, FF, R, FF, p->ff2_w[l], FF, p->ff2_b[l], t2, A, u, A, A, s));
+    FX_TRY(launch_layernorm_fwd(u, A, nullptr, 0, p->ln_ff_w[l], p->ln_ff_b[l], eps, R, A, 0, b + L.t3, A, nullptr,
+                                b + L.rs3, b + L.xh3, A, s));
+    x = b + L.t3;
+    ldx = A;
+  }
+  if (p->final_norm) {
+    FX_TRY(launch_layernorm_fwd(x, ldx, nullptr, 0, p->fn_w, p->fn_b, eps, R, A, 0, saved + L.fo, A, nullptr,
+                                saved + L.frs, saved + L.fxh, A, s));
+    x = saved + L.fo;
+    ldx = A;
+  }
+  return linear_fwd(x, ldx, R, A, p->out_w, p->out_b, out, ldo, p->out_dim, 0, s);
+}
+
+int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const float* tgt, long long ldt, int R,
+                   const float* qpos, const float* mem, long long ldm, int T, const float* mpos, long long ldmp,
+                   const float* dout, long long lddo, float* dtgt, long long lddt, float* dqpos, float* dmem,
+                   long long lddm, float* dmpos, long long lddmp, const float* saved, float* workspace,
+                   void* stream) {
+  FX_TRY(dec_check(p, R, T));
+  hipStream_t s = (hipStream_t)stream;
+  const int A = p->A, FF = p->FF, h = p->nhead, hd = A / h, NL = p->num_layers;
+  const long long RA = (long long)R * A;
+  const float scale = 1.0f / std::sqrt((float)hd);
+  const DecLayout L = dec_layout(p, R, T, qpos != nullptr, mpos != nullptr);
+  const int AL2 = 2 * A * NL;
+  float* ws = workspace;
+  float* spl = ws + L.split;
+  float* lnws = ws + L.lnws;
+  float* dT = ws + L.dT;     // gradient w.r.t. the current layer output
+  float* dS = ws + L.dS;
+  float* dU = ws + L.dU;
+  float* dF = ws + L.dF;
+  float* dQKV = ws + L.dQKV;
+  float* dO = ws + L.dO;
+  float* dq = ws + L.dq;
+  float* G = ws + L.G;       // sum of the query-position gradients over layers
+  float* P = ws + L.P;
+  float* dkv = ws + L.dkv;
+  if (qpos) FX_CHECK_HIP(hipMemsetAsync(G, 0, RA * sizeof(float), s));
+  // out_linear and the final LayerNorm
+  const float* xl = saved + L.layers + (NL - 1) * L.per_layer + L.t3;   // last layer output
+  const float* fin = p->final_norm ? saved + L.fo : xl;
+  FX_TRY(linear_dwdb(dout, lddo, fin, A, R, A, p->out_dim, g->out_w, g->out_b, 1, spl, s));
+  FX_TRY(linear_dx(dout, lddo, p->out_w, R, A, p->out_dim, p->final_norm ? dS : dT, A, 0, nullptr, 0, spl, s));
+  if (p->final_norm)
+    FX_TRY(launch_layernorm_bwd(dS, A, nullptr, 0, saved + L.fxh, A, p->fn_w, saved + L.frs, R, A, 0, dT, A, g->fn_w,
+                                g->fn_b, lnws, s));
+  for (int l = NL - 1; l >= 0; --l) {
+    const float* b = saved + L.layers + l * L.per_layer;
+    const float* x = l == 0 ? tgt : saved + L.layers + (l - 1) * L.per_layer + L.t3;
+    const long long ldx = l == 0 ? ldt : A;
+    const float* xq = qpos ? b + L.xq : x;
+    const long long ldxq = qpos ? A : ldx;
+    const float* t2 = p->cross ? b + L.t2 : b + L.t1;
+    // --- FFN + its LayerNorm:  dU = LN_bwd(dT) ; dF = (dU W2) * (f1 > 0) ; dT2 = dU + dF W1
+    FX_TRY(launch_layernorm_bwd(dT, A, nullptr, 0, b + L.xh3, A, p->ln_ff_w[l], b + L.rs3, R, A, 0, dU, A,
+                                g->ln_ff_w[l], g->ln_ff_b[l], lnws, s));
+    FX_TRY(linear_dwdb(dU, A, b + L.f1, FF, R, FF, A, g->ff2_w[l], g->ff2_b[l], 1, spl, s));
+    FX_TRY(linear_dx(dU, A, p->ff2_w[l], R, FF, A, dF, FF, 0, b + L.f1, FF, spl, s));
+    FX_TRY(linear_dwdb(dF, FF, t2, A, R, A, FF, g->ff1_w[l], g->ff1_b[l], 1, spl, s));
+    FX_TRY(linear_dx_res(dF, FF, p->ff1_w[l], A, R, A, FF, dU, A, dT, A, spl, s));   // dT <- dT2
+    if (p->cross) {
+      // --- cross-attention + LN2
+      FX_TRY(launch_layernorm_bwd(dT, A, nullptr, 0, b + L.xh2, A, p->ln_ca_w[l], b + L.rs2, R, A, 0, dU, A,
+                                  g->ln_ca_w[l], g->ln_ca_b[l], lnws, s));
+      FX_TRY(linear_dwdb(dU, A, b + L.oca, A, R, A, A, g->ca_out_w[l], g->ca_out_b[l], 1, spl, s));
+      FX_TRY(linear_dx(dU, A, p->ca_out_w[l], R, A, A, dO, A, 0, nullptr, 0, spl, s));
+      const float* kv = saved + L.kv;
+      FX_TRY(fx_mha_core_bwd(b + L.qc, A, kv + (long long)l * A, AL2, kv + (long long)(NL + l) * A, AL2, b + L.pca,
+                             dO, A, R, T, A, h, dq, A, dkv + (long long)l * A, AL2, dkv + (long long)(NL + l) * A,
+                             AL2, ws + L.core, s));
+      const float* tq = qpos ? b + L.t1q : b + L.t1;
+      FX_TRY(linear_dwdb(dq, A, tq, A, R, A, A, g->ca_q_w[l], g->ca_in_b[l], 1, spl, s));
+      if (qpos) {
+        FX_TRY(linear_dx(dq, A, p->ca_q_w[l], R, A, A, P, A, 0, nullptr, 0, spl, s));
+        FX_TRY(add_acc(dU, P, dT, G, RA, s));                                     // dT1 = dU + P ; G += P
+      } else {
+        FX_TRY(linear_dx_res(dq, A, p->ca_q_w[l], A, R, A, A, dU, A, dT, A, spl, s));
+      }
+    }
+    // --- self-attention + LN1
+    FX_TRY(launch_layernorm_bwd(dT, A, nullptr, 0, b + L.xh1, A, p->ln_sa_w[l], b + L.rs1, R, A, 0, dU, A,
+                                g->ln_sa_w[l], g->ln_sa_b[l], lnws, s));
+    FX_TRY(linear_dwdb(dU, A, b + L.osa, A, R, A, A, g->sa_out_w[l], g->sa_out_b[l], 1, spl, s));
+    FX_TRY(linear_dx(dU, A, p->sa_out_w[l], R, A, A, dO, A, 0, nullptr, 0, spl, s));
+    const float* qkv = b + L.qkv;
+    FX_TRY(launch_mha_small_bwd(qkv, 3 * A, qkv + A, 3 * A, qkv + 2 * A, 3 * A, b + L.psa, dO, A, R, R, hd, h, scale,
+                                dQKV, 3 * A, dQKV + A, 3 * A, dQKV + 2 * A, 3 * A, s));
+    float* dX = l == 0 ? nullptr : dT;   // the next (earlier) layer's output gradient, in place
+    if (!qpos) {
+      FX_TRY(linear_dwdb(dQKV, 3 * A, x, ldx, R, A, 3 * A, g->sa_in_w[l], g->sa_in_b[l], 1, spl, s));
+      if (l > 0 || dtgt)
+        FX_TRY(linear_dx_res(dQKV, 3 * A, p->sa_in_w[l], A, R, A, 3 * A, dU, A, l > 0 ? dX : dtgt,
+                             l > 0 ? A : lddt, spl, s));
+    } else {
+      FX_TRY(linear_dwdb(dQKV, 3 * A, xq, ldxq, R, A, 2 * A, g->sa_in_w[l], g->sa_in_b[l], 1, spl, s));
+      FX_TRY(linear_dwdb(dQKV + 2 * A, 3 * A, x, ldx, R, A, A, g->sa_in_w[l] + 2LL * A * A, g->sa_in_b[l] + 2 * A, 1,
+                         spl, s));
+      // P = dq W_q + dk W_k  (the position path);  dX = dU + dv W_v + P ; G += P
+      FX_TRY(linear_dx(dQKV, 3 * A, p->sa_in_w[l], R, A, 2 * A, P, A, 0, nullptr, 0, spl, s));
+      if (l > 0 || dtgt) {
+        FX_TRY(linear_dx_res(dQKV + 2 * A, 3 * A, p->sa_in_w[l] + 2LL * A * A, A, R, A, A, dU, A, dS, A, spl, s));
+        if (l > 0) {
+          FX_TRY(add_acc(dS, P, dX, G, RA, s));
+        } else {
+          FX_TRY(add_acc(dS, P, dS, G, RA, s));
+          FX_CHECK_HIP(hipMemcpy2DAsync(dtgt, lddt * sizeof(float), dS, A * sizeof(float), A * sizeof(float), R,
+                                        hipMemcpyDeviceToDevice, s));
+        }
+      } else {
+        FX_TRY(add2(P, A, nullptr, 0, R, A, G, A, 1, s));
+      }
+    }
+  }
+  if (qpos && dqpos) FX_CHECK_HIP(hipMemcpyAsync(dqpos, G, RA * sizeof(float), hipMemcpyDeviceToDevice, s));
+  if (p->cross) {
+    // frame memory: dmem = dKV . Wkv ; dWkv = dKV^T [mem+pos | mem] ; dbkv = colsum(dKV)
+    PackKV pk{};
+    for (int l = 0; l < NL; ++l) {
+      pk.src[l] = p->ca_k_w[l];
+      pk.src[NL + l] = p->ca_v_w[l];
+      pk.bsrc[l] = p->ca_in_b[l] + A;
+      pk.bsrc[NL + l] = p->ca_in_b[l] + 2 * A;
+    }
+    float* wkv = ws + L.dwkv;   // packed weights first (for dmem), then reused for their gradient
+    pk.dst = wkv;
+    pk.bdst = ws + L.dbkv;
+    pk.A = A;
+    pk.Hm = p->Hm;
+    pk.L = NL;
+    const int AL = A * NL;
+    if (dmem || dmpos) {
+      hipLaunchKernelGGL(pack_kv_kernel, dim3(std::min(cdiv((long long)A * p->Hm, 256), 256), 2 * NL), dim3(256), 0,
+                         s, pk);
+      FX_CHECK_HIP(hipGetLastError());
+      if (dmem) FX_TRY(linear_dx(dkv, AL2, wkv, T, p->Hm, AL2, dmem, lddm, 0, nullptr, 0, spl, s));
+      if (dmpos) FX_TRY(linear_dx(dkv, AL2, wkv, T, p->Hm, AL, dmpos, lddmp, 0, nullptr, 0, spl, s));
+    }
+    if (!mpos) {
+      FX_TRY(linear_dwdb(dkv, AL2, mem, ldm, T, p->Hm, AL2, wkv, ws + L.dbkv, 0, spl, s));
+    } else {
+      FX_TRY(linear_dwdb(dkv, AL2, saved + L.mpos, p->Hm, T, p->Hm, AL, wkv, ws + L.dbkv, 0, spl, s));
+      FX_TRY(linear_dwdb(dkv + AL, AL2, mem, ldm, T, p->Hm, AL, wkv + (long long)AL * p->Hm, ws + L.dbkv + AL, 0, spl,
+                         s));
+    }
+    UnpackKV uk{};
+    for (int l = 0; l < NL; ++l) {
+      uk.dst[l] = g->ca_k_w[l];
+      uk.dst[NL + l] = g->ca_v_w[l];
+      uk.bdst[l] = g->ca_in_b[l] ? g->ca_in_b[l] + A : nullptr;
+      uk.bdst[NL + l] = g->ca_in_b[l] ? g->ca_in_b[l] + 2 * A : nullptr;
+    }
+    uk.src = wkv;
+    uk.bsrc = ws + L.dbkv;
+    uk.A = A;
+    uk.Hm = p->Hm;
+    uk.L = NL;
+    hipLaunchKernelGGL(unpack_kv_acc_kernel, dim3(std::min(cdiv((long long)A * p->Hm, 256), 256), 2 * NL), dim3(256),
+                       0, s, uk);
+    FX_CHECK_HIP(hipGetLastError());
+  }
+  return FX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,75 @@
+// Internal (non-ABI) declarations shared by the factmx translation units.
+#pragma once
+#include "fx_common.h"
+
+namespace fx {
+
+// ---- kernels (rowops.hip, segments.hip, gru.hip, gemm_f32.hip, attn_small.hip) ----
+long long colsum_workspace_floats(int M, int N);
+int launch_layernorm_fwd(const float* x, long long ldx, const float* r, long long ldr, const float* w,
+                         const float* b, float eps, int rows, int cols, int relu, float* y, long long ldy,
+                         float* mean, float* rstd, float* xhat, long long ldxh, hipStream_t s);
+long long layernorm_bwd_ws_floats(int rows, int cols);
+int launch_layernorm_bwd(const float* dy, long long lddy, const float* y, long long ldy, const float* xhat,
+                         long long ldxh, const float* w, const float* rstd, int rows, int cols, int relu,
+                         float* dx, long long lddx, float* dw, float* db, float* ws, hipStream_t s);
+int launch_softmax_rows(const float* x, long long ldx, int rows, int cols, float scale, float* p, long long ldp,
+                        hipStream_t s);
+int launch_softmax_rows_bwd(const float* p, long long ldp, const float* dp, long long lddp, const float* extra,
+                            long long lde, int rows, int cols, float scale, float* dl, long long ldd,
+                            hipStream_t s);
+int launch_pf_fwd(const float* x, long long ldx, int rows, int cols, int n, float* out, long long ldo, float* clogit,
+                  long long ldc,
+                  hipStream_t s);
+int launch_pf_bwd(const float* out, long long ldo, const float* dout, long long lddo, const float* dcl,
+                  long long lddc, int rows, int cols, int n, float* dx, long long lddx, hipStream_t s);
+int launch_l2n_fwd(const float* x, long long ldx, int rows, int cols, float* y, long long ldy, float* nrm,
+                   hipStream_t s);
+int launch_l2n_bwd(const float* y, long long ldy, const float* nrm, const float* dy, long long lddy, int rows,
+                   int cols, float* dx, long long lddx, hipStream_t s);
+int launch_segments(const float* x, long long ldx, int col0, int ncls, int T, int32_t* pred, int32_t* seg_id,
+                    int32_t* seg_start, int32_t* seg_end, int32_t* num_seg, hipStream_t s);
+int launch_seg_reduce(const float* x, long long ldx, const int32_t* st, const int32_t* en, int S, int cols, int mean,
+                      float* y, long long ldy, int accumulate, hipStream_t s);
+int launch_seg_mean_bwd(const float* dy, long long lddy, const int32_t* sid, const int32_t* st, const int32_t* en,
+                        int T, int cols, float* dx, long long lddx, int accumulate, hipStream_t s);
+int launch_gru_fwd(const float* gi, long long ldgi, int S, int Hh, const float* const whh[2], const float* const bhh[2],
+                   float* out, long long ldo, float* saved, float* ws, hipStream_t s);
+int launch_gru_bwd(const float* dout, long long lddo, int S, int Hh, const float* const whh[2], const float* saved,
+                   float* dgi, long long lddgi, float* dgh, hipStream_t s);
+
+// ---- composite helpers (capi.cpp) --------------------------------------------
+int ew_grid(long long total);
+int relu_bwd(const float* dy, long long lddy, const float* y, long long ldy, int rows, int cols, float* dz,
+             long long lddz, hipStream_t s);
+int add2(const float* a, long long lda, const float* b, long long ldb, int rows, int cols, float* o, long long ldo,
+         int accumulate, hipStream_t s);
+// split-K factor / workspace floats for a (M x N, depth K) product
+int pick_split(int M, int N, int K, int batch = 1);
+long long split_ws(int M, int N, int K, int batch = 1);
+// y = (x [+pos on the first pos_cols columns]) . w^T (+b) (+relu);  w (N,K) with row stride ldw
+int linear_fwd(const float* x, long long ldx, int M, int K, const float* w, const float* b, float* y, long long ldy,
+               int N, int relu, hipStream_t s, long long ldw = -1, const float* pos = nullptr, long long ldpos = 0,
+               int pos_cols = 0);
+// dx (+)= dy . w  [* (gate > 0)];  w (N,K)
+int linear_dx(const float* dy, long long lddy, const float* w, int M, int K, int N, float* dx, long long lddx,
+              int accumulate, const float* gate, long long ld_gate, float* ws, hipStream_t s, long long ldw = -1);
+// dw (+)= dy^T . x and db (+)= colsum(dy) in one GEMM (virtual ones column)
+int linear_dwdb(const float* dy, long long lddy, const float* x, long long ldx, int M, int K, int N, float* dw,
+                float* db, int accumulate, float* ws, hipStream_t s, long long lddw = -1);
+int linear_dw(const float* dy, long long lddy, const float* x, long long ldx, int M, int K, int N, float* dw,
+              int accumulate, float* ws, hipStream_t s, long long lddw = -1);
+long long dwdb_ws(int M, int K, int N);
+
+// ---- fused small multi-head attention (attn_small.hip): Lq, Lk, head_dim <= 64 ----
+// probs (nhead, Lq, Lk) saved; o (Lq, nhead*hd) with row stride ldo.
+int launch_mha_small_fwd(const float* q, long long ldq, const float* k, long long ldk, const float* v,
+                         long long ldv, int Lq, int Lk, int hd, int nhead, float scale, float* probs, float* o,
+                         long long ldo, hipStream_t s);
+// dq, dk, dv written (nullable) with their row strides
+int launch_mha_small_bwd(const float* q, long long ldq, const float* k, long long ldk, const float* v,
+                         long long ldv, const float* probs, const float* dout, long long lddo, int Lq, int Lk, int hd,
+                         int nhead, float scale, float* dq, long long lddq, float* dk, long long lddk, float* dv,
+                         long long lddv, hipStream_t s);
+
+}  // namespace fx

@@ -129,6 +129,67 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* dy, long long 
   }
 }
 
+// token-sized LayerNorm backward (rows <= 64): ONE 1024-thread block, 16 waves over the rows, the
+// weight/bias gradient column sums reduced in LDS and accumulated (+=) in the same launch
+__global__ __launch_bounds__(1024) void ln_bwd_small_kernel(const float* dy, long long lddy, const float* y,
+                                                            long long ldy, const float* xhat, long long ldxh,
+                                                            const float* w, const float* rstd, int rows, int cols,
+                                                            int relu, float* dx, long long lddx, float* dw,
+                                                            float* db) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __shared__ float red[16][2][64];
+  for (int c0 = 0; c0 < cols; c0 += 64) {
+    const int c = c0 + lane;
+    float pw = 0.f, pb = 0.f;
+    for (int row = wv; row < rows; row += 16) {
+      if (c < cols) {
+        float d = dy[(long long)row * lddy + c];
+        if (relu && !(y[(long long)row * ldy + c] > 0.f)) d = 0.f;
+        pw += d * xhat[(long long)row * ldxh + c];
+        pb += d;
+      }
+    }
+    red[wv][0][lane] = pw;
+    red[wv][1][lane] = pb;
+    __syncthreads();
+    if (wv == 0 && c < cols) {
+      float a = 0.f, b = 0.f;
+      for (int k = 0; k < 16; ++k) {
+        a += red[k][0][lane];
+        b += red[k][1][lane];
+      }
+      if (dw) dw[c] += a;
+      if (db) db[c] += b;
+    }
+    __syncthreads();
+  }
+  for (int row = wv; row < rows; row += 16) {
+    float g[MAXPL], h[MAXPL];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXPL; ++i) {
+      const int c = i * 64 + lane;
+      g[i] = h[i] = 0.f;
+      if (c < cols) {
+        float d = dy[(long long)row * lddy + c];
+        if (relu && !(y[(long long)row * ldy + c] > 0.f)) d = 0.f;
+        h[i] = xhat[(long long)row * ldxh + c];
+        g[i] = d * w[c];
+        s1 += g[i];
+        s2 += g[i] * h[i];
+      }
+    }
+    s1 = wave_sum(s1) / cols;
+    s2 = wave_sum(s2) / cols;
+    const float rs = rstd[row];
+#pragma unroll
+    for (int i = 0; i < MAXPL; ++i) {
+      const int c = i * 64 + lane;
+      if (c < cols) dx[(long long)row * lddx + c] = rs * (g[i] - s1 - h[i] * s2);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void ln_bwd_reduce(const float* ws, int nblk, int cols, float* dw, float* db) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= cols) return;
@@ -357,6 +418,13 @@ int launch_layernorm_bwd(const float* dy, long long lddy, const float* y, long l
                          float* dx, long long lddx, float* dw, float* db, float* ws, hipStream_t s) {
   FX_REQUIRE(cols > 0 && cols <= 64 * MAXPL, "layernorm: cols must be in (0, 1024]");
   if (rows == 0) return FX_OK;
+  if (rows <= 64) {
+    // dx is written after every dy row was read for the column sums: dx may alias dy
+    hipLaunchKernelGGL(ln_bwd_small_kernel, dim3(1), dim3(1024), 0, s, dy, lddy, y, ldy, xhat, ldxh, w, rstd, rows,
+                       cols, relu, dx, lddx, dw, db);
+    FX_CHECK_HIP(hipGetLastError());
+    return FX_OK;
+  }
   const int nblk = std::min(cdiv(rows, 4), 256);
   const bool want = dw || db;
   FX_REQUIRE(!want || ws, "layernorm bwd: workspace required for dw/db");

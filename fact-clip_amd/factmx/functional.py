@@ -722,3 +722,168 @@ def add_(a, b):
     rows, cols = a.shape
     _check(lib.fx_add(nx.ptr(b), nx.ld(b), None, 0, rows, cols, nx.ptr(a), nx.ld(a), 1, nx.stream()), "fx_add")
     return a
+
+
+# ---------------------------------------------------------------------------
+# Action-token decoders (SCADecoder / SADecoder), whole stack per call
+# ---------------------------------------------------------------------------
+
+def _decoder_slots(mod):
+    """Map an SCADecoder / SADecoder onto fx_decoder_params: returns (meta, params, slots) where
+    ``params`` are the unique parameter tensors (autograd inputs) and ``slots[field]`` lists, per
+    layer (or once for the global fields), (param index, element offset)."""
+    layers = list(mod.layers)
+    cross = hasattr(layers[0], "self_attn")
+    params, index = [], {}
+
+    def slot(t, off=0):
+        if t is None:
+            return None
+        k = id(t)
+        if k not in index:
+            index[k] = len(params)
+            params.append(t)
+        return (index[k], off)
+
+    slots = {f: [] for f in nx.DECODER_LAYER_FIELDS}
+    for lyr in layers:
+        sa = lyr.self_attn if cross else lyr.multihead_attn
+        if not sa._qkv_same_embed_dim:
+            raise NotImplementedError("self-attention with kdim != embed_dim")
+        A = sa.embed_dim
+        slots["sa_in_w"].append(slot(sa.in_proj_weight))
+        slots["sa_in_b"].append(slot(sa.in_proj_bias))
+        slots["sa_out_w"].append(slot(sa.out_proj.weight))
+        slots["sa_out_b"].append(slot(sa.out_proj.bias))
+        if cross:
+            ca = lyr.multihead_attn
+            if ca._qkv_same_embed_dim:
+                w = ca.in_proj_weight
+                qw, kw, vw = slot(w, 0), slot(w, A * A), slot(w, 2 * A * A)
+            else:
+                qw, kw, vw = slot(ca.q_proj_weight), slot(ca.k_proj_weight), slot(ca.v_proj_weight)
+            slots["ca_q_w"].append(qw)
+            slots["ca_k_w"].append(kw)
+            slots["ca_v_w"].append(vw)
+            slots["ca_in_b"].append(slot(ca.in_proj_bias))
+            slots["ca_out_w"].append(slot(ca.out_proj.weight))
+            slots["ca_out_b"].append(slot(ca.out_proj.bias))
+            slots["ln_ca_w"].append(slot(lyr.norm2.weight))
+            slots["ln_ca_b"].append(slot(lyr.norm2.bias))
+            ln_ff = lyr.norm3
+        else:
+            for f in ("ca_q_w", "ca_k_w", "ca_v_w", "ca_in_b", "ca_out_w", "ca_out_b", "ln_ca_w", "ln_ca_b"):
+                slots[f].append(None)
+            ln_ff = lyr.norm2
+        slots["ff1_w"].append(slot(lyr.linear1.weight))
+        slots["ff1_b"].append(slot(lyr.linear1.bias))
+        slots["ff2_w"].append(slot(lyr.linear2.weight))
+        slots["ff2_b"].append(slot(lyr.linear2.bias))
+        slots["ln_sa_w"].append(slot(lyr.norm1.weight))
+        slots["ln_sa_b"].append(slot(lyr.norm1.bias))
+        slots["ln_ff_w"].append(slot(ln_ff.weight))
+        slots["ln_ff_b"].append(slot(ln_ff.bias))
+    norm = mod.norm
+    gl = {"fn_w": slot(norm.weight) if norm is not None else None,
+          "fn_b": slot(norm.bias) if norm is not None else None,
+          "out_w": slot(mod.out_linear.weight), "out_b": slot(mod.out_linear.bias)}
+    lyr0 = layers[0]
+    sa0 = lyr0.self_attn if cross else lyr0.multihead_attn
+    eps = lyr0.norm1.eps
+    meta = dict(A=sa0.embed_dim, FF=lyr0.linear1.out_features, nhead=sa0.num_heads, num_layers=len(layers),
+                cross=int(cross), Hm=(lyr0.multihead_attn.kdim if cross else 0), out_dim=mod.out_linear.out_features,
+                final_norm=int(norm is not None), eps=float(eps))
+    return meta, params, slots, gl
+
+
+def _fill_decoder_struct(st, slots, gl, tensors, keep):
+    """Point every field of a DecoderParams / DecoderGrads at ``tensors[idx] + off``."""
+    def addr(s):
+        if s is None or tensors[s[0]] is None:
+            return None
+        return tensors[s[0]].data_ptr() + 4 * s[1]
+    for f, lst in slots.items():
+        arr = (ctypes.c_void_p * max(len(lst), 1))(*[addr(s) for s in lst])
+        keep.append(arr)
+        setattr(st, f, ctypes.cast(arr, ctypes.c_void_p))
+    for f, s in gl.items():
+        setattr(st, f, addr(s))
+
+
+class DecoderFn(torch.autograd.Function):
+    """SCADecoder.forward (basic.py:542-557) / SADecoder.forward (basic.py:578-593) in one C call
+    per direction (fx_decoder_fwd / fx_decoder_bwd)."""
+
+    @staticmethod
+    def forward(ctx, tgt, qpos, mem, mpos, spec, *params):
+        lib = nx.load()
+        meta, slots, gl, cache = spec
+        prm = cache.get("prm")
+        key = tuple(p.data_ptr() for p in params)
+        if prm is None or cache.get("key") != key:
+            prm = nx.DecoderParams(**meta)
+            keep = []
+            _fill_decoder_struct(prm, slots, gl, params, keep)
+            cache.update(prm=prm, key=key, keep=keep)
+        R = tgt.shape[0]
+        T = mem.shape[0] if mem is not None else 0
+        hq, hm = int(qpos is not None), int(mpos is not None)
+        dev = tgt.device
+        out = _empty(R, meta["out_dim"], device=dev)
+        saved = _ws(lib.fx_decoder_saved_floats(ctypes.byref(prm), R, T, hq, hm), dev)
+        ws = _ws(lib.fx_decoder_workspace_floats(ctypes.byref(prm), R, T, hq, hm), dev)
+        _check(lib.fx_decoder_fwd(ctypes.byref(prm), nx.ptr(tgt), nx.ld(tgt), R, nx.ptr(qpos), nx.ld(qpos),
+                                  nx.ptr(mem), nx.ld(mem), T, nx.ptr(mpos), nx.ld(mpos), nx.ptr(out), nx.ld(out),
+                                  nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_decoder_fwd")
+        ctx.spec = spec
+        ctx.flags = (hq, hm, T)
+        ctx.save_for_backward(tgt, qpos, mem, mpos, saved, *params)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = nx.load()
+        tgt, qpos, mem, mpos, saved, *params = ctx.saved_tensors
+        meta, slots, gl, cache = ctx.spec
+        hq, hm, T = ctx.flags
+        nd = ctx.needs_input_grad
+        dev = dout.device
+        dout = dout.contiguous()
+        R = tgt.shape[0]
+        tg = [grad_target(p, nd[5 + i]) for i, p in enumerate(params)]
+        bufs = [t[0] for t in tg]
+        gkey = tuple(0 if b is None else b.data_ptr() for b in bufs)
+        g = cache.get("grads")
+        if g is None or cache.get("gkey") != gkey:
+            g = nx.DecoderGrads()
+            keep = []
+            _fill_decoder_struct(g, slots, gl, bufs, keep)
+            cache.update(grads=g, gkey=gkey, gkeep=keep)
+        prm = cache["prm"]
+        A = meta["A"]
+        dtgt = _empty(R, A, device=dev) if nd[0] else None
+        dqpos = _empty(R, A, device=dev) if (hq and nd[1]) else None
+        dmem = _empty(*mem.shape, device=dev) if (mem is not None and nd[2]) else None
+        dmpos = _empty(*mpos.shape, device=dev) if (hm and nd[3]) else None
+        ws = _ws(lib.fx_decoder_workspace_floats(ctypes.byref(prm), R, T, hq, hm), dev)
+        _check(lib.fx_decoder_bwd(ctypes.byref(prm), ctypes.byref(g), nx.ptr(tgt), nx.ld(tgt), R, nx.ptr(qpos),
+                                  nx.ptr(mem), nx.ld(mem), T, nx.ptr(mpos), nx.ld(mpos), nx.ptr(dout), nx.ld(dout),
+                                  nx.ptr(dtgt), nx.ld(dtgt), nx.ptr(dqpos), nx.ptr(dmem), nx.ld(dmem), nx.ptr(dmpos),
+                                  nx.ld(dmpos), nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_decoder_bwd")
+        return (dtgt, dqpos, dmem, dmpos, None) + tuple(t[1] for t in tg)
+
+
+def decoder(mod, tgt, memory=None, pos=None, query_pos=None):
+    """Run an SCADecoder (memory given) or SADecoder through DecoderFn; returns (R, out_dim)."""
+    spec = getattr(mod, "_fx_spec", None)
+    if spec is None:
+        meta, params, slots, gl = _decoder_slots(mod)
+        spec = (meta, slots, gl, {})
+        mod._fx_spec = spec
+        mod._fx_params = params
+    params = mod._fx_params
+    t2 = _2d(tgt)
+    qp = None if query_pos is None else _2d(query_pos).contiguous()
+    mem = None if memory is None else _2d(memory)
+    mp = None if pos is None else _2d(pos)
+    return DecoderFn.apply(t2, qp, mem, mp, spec, *params)

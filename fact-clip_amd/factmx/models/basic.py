@@ -365,6 +365,25 @@ class SCALayer(nn.Module):
         return _as3d(fxf.layer_norm(t2, self.norm3.weight, self.norm3.bias, self.norm3.eps, residual=t))
 
 
+def _fused_decoder_ok(dec):
+    """The whole-decoder kernel path (fx_decoder_*) runs eval-mode dropout and the default layer
+    options; training with non-zero dropout, sa/ca value positions or pre-norm takes the per-layer
+    path (still HIP kernels)."""
+    if len(dec.layers) == 0 or len(dec.layers) > 16:
+        return False
+    for lyr in dec.layers:
+        drops = [m.p for m in lyr.modules() if isinstance(m, nn.Dropout)]
+        attn = [lyr.multihead_attn.dropout] + ([lyr.self_attn.dropout] if hasattr(lyr, "self_attn") else [])
+        if dec.training and any(p > 0 for p in drops + attn):
+            return False
+        if getattr(lyr, "sa_value_w_pos", False) or getattr(lyr, "ca_value_w_pos", False) or \
+                getattr(lyr, "use_vpos", False) or getattr(lyr, "normalize_before", False):
+            return False
+        if hasattr(lyr, "self_attn") is False and lyr.kv_dim != lyr.q_dim:
+            return False
+    return True
+
+
 class SCADecoder(nn.Module):
     """basic.py:525-557."""
 
@@ -382,6 +401,8 @@ class SCADecoder(nn.Module):
 
     def forward(self, tgt, memory, pos: Optional[Tensor] = None, query_pos: Optional[Tensor] = None):
         out = _as3d(fxf.linear(tgt, self.in_linear.weight, self.in_linear.bias)) if self.in_map else tgt
+        if _fused_decoder_ok(self):
+            return _as3d(fxf.decoder(self, out, memory, pos=pos, query_pos=query_pos))
         for layer in self.layers:
             out = layer(out, memory, pos=pos, query_pos=query_pos)
         if self.norm is not None:
@@ -406,6 +427,8 @@ class SADecoder(nn.Module):
 
     def forward(self, tgt, pos: Optional[Tensor] = None):
         out = _as3d(fxf.linear(tgt, self.in_linear.weight, self.in_linear.bias)) if self.in_map else tgt
+        if _fused_decoder_ok(self):
+            return _as3d(fxf.decoder(self, out, None, pos=None, query_pos=pos))
         for layer in self.layers:
             out = layer(out, out, out, query_pos=pos, key_pos=pos, value_pos=pos)
         if self.norm is not None:

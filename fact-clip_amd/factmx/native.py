@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FACTMX_LIB", os.path.join(_HERE, "_lib", "libfactmx.so"))
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -49,6 +49,22 @@ class MstcnGrads(ctypes.Structure):
                 ("ln_w", P), ("ln_b", P), ("w_out", P), ("b_out", P)]
 
 
+_DEC_PTRS = ["sa_in_w", "sa_in_b", "sa_out_w", "sa_out_b", "ca_q_w", "ca_k_w", "ca_v_w", "ca_in_b", "ca_out_w",
+             "ca_out_b", "ff1_w", "ff1_b", "ff2_w", "ff2_b", "ln_sa_w", "ln_sa_b", "ln_ca_w", "ln_ca_b", "ln_ff_w",
+             "ln_ff_b"]
+DECODER_LAYER_FIELDS = _DEC_PTRS
+DECODER_GLOBAL_FIELDS = ["fn_w", "fn_b", "out_w", "out_b"]
+
+
+class DecoderParams(ctypes.Structure):
+    _fields_ = ([("A", I), ("FF", I), ("nhead", I), ("num_layers", I), ("cross", I), ("Hm", I), ("out_dim", I),
+                 ("final_norm", I), ("eps", F)] + [(n, P) for n in _DEC_PTRS] + [(n, P) for n in DECODER_GLOBAL_FIELDS])
+
+
+class DecoderGrads(ctypes.Structure):
+    _fields_ = [(n, P) for n in _DEC_PTRS] + [(n, P) for n in DECODER_GLOBAL_FIELDS]
+
+
 # name -> (restype, argtypes); every fx_* symbol declared in include/factmx.h
 SIGNATURES = {
     "fx_version": (I, []),
@@ -63,6 +79,11 @@ SIGNATURES = {
     "fx_x2y_fwd": (I, [P, L, I, I, P, L, I, P, L, I, I, P, L, I, P, P, P, P, P, P, P, P, I, I, P, L, P, P, P, P, P]),
     "fx_x2y_bwd": (I, [P, L, I, I, I, P, L, I, I, I, P, P, P, P, I, I, P, P, P, L, P, P, P, P, P, P, P, P, P, P,
                        P, P, P, P, I, I, P, P]),
+    "fx_decoder_saved_floats": (L, [ctypes.POINTER(DecoderParams), I, I, I, I]),
+    "fx_decoder_workspace_floats": (L, [ctypes.POINTER(DecoderParams), I, I, I, I]),
+    "fx_decoder_fwd": (I, [ctypes.POINTER(DecoderParams), P, L, I, P, L, P, L, I, P, L, P, L, P, P, P]),
+    "fx_decoder_bwd": (I, [ctypes.POINTER(DecoderParams), ctypes.POINTER(DecoderGrads), P, L, I, P, P, L, I, P, L,
+                           P, L, P, L, P, P, L, P, L, P, P, P]),
     "fx_mstcn_saved_floats": (L, [ctypes.POINTER(MstcnParams), I]),
     "fx_mstcn_workspace_floats": (L, [ctypes.POINTER(MstcnParams), I]),
     "fx_mstcn_fwd": (I, [ctypes.POINTER(MstcnParams), P, L, I, I, P, L, P, P, P]),

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FX_ABI_VERSION 2
+#define FX_ABI_VERSION 3
 
 enum {
   FX_OK = 0,
@@ -158,6 +158,67 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
                const float* dattn, float* dX, float* dXpos, float* dY, float* dYpos, float* dwk,
                float* dbk, float* dwv, float* dbv, float* dwq, float* dbq, float* dwy, float* dby,
                int has_xpos, int has_ypos, float* workspace, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Action-token decoder, whole stack in one call (eval-mode dropout, post-norm, ReLU FFN):
+ *   cross = 1: SCADecoder (basic.py:525-557) of SCALayer (basic.py:454-523):
+ *     per layer  t1 = LN_sa(x + SA(x+qpos, x+qpos, x))
+ *                t2 = LN_ca(t1 + CA(t1+qpos, mem+mpos, mem))
+ *                x' = LN_ff(t2 + W2 relu(W1 t2 + b1) + b2)
+ *     then the optional final LayerNorm (SCADecoder.norm) and out_linear.
+ *   cross = 0: SADecoder (basic.py:561-593) of SALayer (basic.py:391-452): the same
+ *     without the CA stage (SALayer.norm1 -> ln_sa, norm2 -> ln_ff).
+ * SA/CA = nn.MultiheadAttention math with nhead heads (head dim A/nhead <= 64); the
+ * self-attention in-projection is the packed (3A, A) in_proj_weight, the cross one
+ * separate q (A,A), k (A,Hm), v (A,Hm) weights with the packed (3A) in_proj_bias.
+ * Shapes: tgt (R, A) ld, qpos (R, A) dense or NULL, mem (T, Hm) ld, mpos (T, Hm) or
+ * NULL, out (R, out_dim).  R <= 64 tokens.  saved/workspace sized by the queries.
+ * bwd: every weight gradient ACCUMULATES (+=) into g; dtgt, dqpos (dense (R,A)),
+ * dmem, dmpos are written (each nullable).
+ * ---------------------------------------------------------------------- */
+typedef struct fx_decoder_params {
+  int A, FF, nhead, num_layers, cross, Hm, out_dim, final_norm;
+  float eps;
+  const float* const* sa_in_w; const float* const* sa_in_b;
+  const float* const* sa_out_w; const float* const* sa_out_b;
+  const float* const* ca_q_w; const float* const* ca_k_w; const float* const* ca_v_w;
+  const float* const* ca_in_b;
+  const float* const* ca_out_w; const float* const* ca_out_b;
+  const float* const* ff1_w; const float* const* ff1_b;
+  const float* const* ff2_w; const float* const* ff2_b;
+  const float* const* ln_sa_w; const float* const* ln_sa_b;
+  const float* const* ln_ca_w; const float* const* ln_ca_b;
+  const float* const* ln_ff_w; const float* const* ln_ff_b;
+  const float* fn_w; const float* fn_b;
+  const float* out_w; const float* out_b;
+} fx_decoder_params;
+
+typedef struct fx_decoder_grads {
+  float* const* sa_in_w; float* const* sa_in_b;
+  float* const* sa_out_w; float* const* sa_out_b;
+  float* const* ca_q_w; float* const* ca_k_w; float* const* ca_v_w;
+  float* const* ca_in_b;
+  float* const* ca_out_w; float* const* ca_out_b;
+  float* const* ff1_w; float* const* ff1_b;
+  float* const* ff2_w; float* const* ff2_b;
+  float* const* ln_sa_w; float* const* ln_sa_b;
+  float* const* ln_ca_w; float* const* ln_ca_b;
+  float* const* ln_ff_w; float* const* ln_ff_b;
+  float* fn_w; float* fn_b;
+  float* out_w; float* out_b;
+} fx_decoder_grads;
+
+long long fx_decoder_saved_floats(const fx_decoder_params* p, int R, int T, int has_qpos, int has_mpos);
+long long fx_decoder_workspace_floats(const fx_decoder_params* p, int R, int T, int has_qpos, int has_mpos);
+int fx_decoder_fwd(const fx_decoder_params* p, const float* tgt, long long ldt, int R, const float* qpos,
+                   long long ldqp, const float* mem, long long ldm, int T, const float* mpos,
+                   long long ldmp, float* out, long long ldo, float* saved, float* workspace,
+                   void* stream);
+int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const float* tgt,
+                   long long ldt, int R, const float* qpos, const float* mem, long long ldm, int T,
+                   const float* mpos, long long ldmp, const float* dout, long long lddo, float* dtgt,
+                   long long lddt, float* dqpos, float* dmem, long long lddm, float* dmpos,
+                   long long lddmp, const float* saved, float* workspace, void* stream);
 
 /* ------------------------------------------------------------------------
  * MS-TCN frame branch, whole stack in one call.
