@@ -771,11 +771,12 @@ static long long gru_split_ws(int S, int In, int Hh) {
   return std::max(sp, split_ws(S, In, 3 * Hh));
 }
 
+// fwd: [sync area][gi (S, 6Hh)];  bwd: [dgi (S, 6Hh)][dgh 2 x (S, 3Hh)][split-K][colsum][sync area]
 long long fx_gru_workspace_floats(int S, int In, int Hh) {
   const long long H3 = 3LL * Hh;
-  long long fwd = 2 * H3 * Hh + S * 2 * H3;
+  long long fwd = gru_sync_floats(Hh) + S * 2 * H3;
   long long sp = gru_split_ws(S, In, Hh);
-  long long bwd = S * 2 * H3 + 2 * S * H3 + sp + colsum_workspace_floats(S, 3 * Hh);
+  long long bwd = S * 2 * H3 + 2 * S * H3 + sp + colsum_workspace_floats(S, 3 * Hh) + gru_sync_floats(Hh);
   return std::max(fwd, bwd);
 }
 
@@ -785,7 +786,7 @@ int fx_gru_bidir_fwd(const float* x, long long ldx, int S, int In, int Hh, const
                      float* workspace, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int H3 = 3 * Hh;
-  float* gi = workspace + 2LL * H3 * Hh;
+  float* gi = workspace + gru_sync_floats(Hh);
   // input projections of every step, both directions: gi[:, d*3Hh:(d+1)*3Hh] = x W_ih_d^T + b_ih_d
   FX_TRY(linear_fwd(x, ldx, S, In, w_ih_f, b_ih_f, gi, 2 * H3, H3, 0, s));
   FX_TRY(linear_fwd(x, ldx, S, In, w_ih_r, b_ih_r, gi + H3, 2 * H3, H3, 0, s));
@@ -804,8 +805,9 @@ int fx_gru_bidir_bwd(const float* x, long long ldx, int S, int In, int Hh, const
   float* dgh = dgi + (long long)S * 2 * H3;        // 2 x (S, 3Hh)
   float* spl = dgh + 2LL * S * H3;
   float* csw = spl + gru_split_ws(S, In, Hh);
+  float* sync_ws = csw + colsum_workspace_floats(S, 3 * Hh);
   const float* whh[2] = {w_hh_f, w_hh_r};
-  FX_TRY(launch_gru_bwd(dout, lddo, S, Hh, whh, saved, dgi, 2 * H3, dgh, s));
+  FX_TRY(launch_gru_bwd(dout, lddo, S, Hh, whh, saved, dgi, 2 * H3, dgh, sync_ws, s));
   const float* wih[2] = {w_ih_f, w_ih_r};
   float* dwih[2] = {dw_ih_f, dw_ih_r};
   float* dwhh[2] = {dw_hh_f, dw_hh_r};

@@ -17,61 +17,138 @@
 namespace fx {
 namespace {
 
-constexpr int GRU_THREADS = 1024;
+// ---------------------------------------------------------------------------------------------
+// The recurrence is sequential in S and W_hh (3Hh x Hh fp32 = 786 KB at Hh = 256) is too large to
+// re-stream through ONE CU every step (that version spent 11 us / 35 us per fwd / bwd step).  Here
+// each direction is spread over NW = 16 workgroups that keep their slice of W_hh in REGISTERS for
+// the whole sequence; per step they exchange only the new hidden state (fwd, Hh floats) or the
+// gate gradients (bwd, 3Hh floats) through epoch-tagged 8-byte granules (the data is the flag:
+// agent-scope relaxed atomic stores/loads, cdna_hip_programming.md Guideline 16 recipe R2),
+// double-buffered by step parity so a workgroup one step ahead never overwrites a slot another is
+// still reading.  All 2*NW workgroups are co-resident (32 of 256 CUs); every spin is bounded and
+// sets a timeout word, so the grid always drains.
+constexpr int NW = 16;          // workgroups per direction
+constexpr int GT = 256;         // threads per workgroup
+constexpr int MAXU = 16;        // hidden units per workgroup (Hh <= 256)
+constexpr int KCH = 64;         // fwd: k-chunk per thread (4 chunks cover Hh <= 256)
+constexpr int RCH = 48;         // bwd: gate rows per thread (16 chunks cover 3Hh <= 768)
+constexpr unsigned SPIN_MAX = 1u << 20;   // ~1 s of polling: a lost peer ends the kernel, never hangs it
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+
+__device__ __forceinline__ void put_granule(unsigned long long* g, unsigned epoch, float v) {
+  __hip_atomic_store((gu64*)g, ((unsigned long long)epoch << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one wave gathers n granules of `epoch` into LDS dst (bounded spin; on timeout flags *tmo)
+__device__ __forceinline__ bool gather_granules(unsigned long long* g, int n, unsigned epoch, float* dst,
+                                                unsigned* tmo, int lane) {
+  for (int base = 0; base < n; base += 64 * 4) {
+    unsigned long long x[4];
+    bool done[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) done[q] = base + q * 64 + lane >= n;
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (!done[q]) {
+          x[q] = __hip_atomic_load((gu64*)(g + base + q * 64 + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((unsigned)(x[q] >> 32) == epoch) {
+            dst[base + q * 64 + lane] = __uint_as_float((unsigned)x[q]);
+            done[q] = true;
+          } else {
+            ok = false;
+          }
+        }
+      }
+      if (__all(ok)) break;
+      if (spins > SPIN_MAX) {
+        if (lane == 0) __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+    }
+  }
+  return true;
+}
 
 struct GruDirArgs {
   const float* gi;     // (S, 3Hh) for this direction, ld = ldgi
   long long ldgi;
-  const float* whT;    // (Hh, 3Hh): W_hh transposed, [k][row]
+  const float* whh;    // (3Hh, Hh) natural layout [row][k]
   const float* bhh;    // (3Hh)
   float* out;          // (S, ldo) h_t written at column offset
   long long ldo;
   float* hprev;        // (S, Hh) h_{t-1} per step
   float* gates;        // (S, 4Hh): r, z, n, gh_n
+  unsigned long long* gran;   // 2 slots x Hh granules
   int S, Hh, reverse;
 };
 
 struct GruArgs {
   GruDirArgs d[2];
+  unsigned* tmo;
 };
 
-__global__ __launch_bounds__(GRU_THREADS) void gru_fwd_kernel(GruArgs args) {
-  const GruDirArgs a = args.d[blockIdx.x];
-  extern __shared__ float sm[];
-  float* h = sm;                 // Hh
-  float* gh = sm + a.Hh;         // 3Hh
-  const int tid = threadIdx.x, H3 = 3 * a.Hh;
-  for (int j = tid; j < a.Hh; j += GRU_THREADS) h[j] = 0.f;
+__global__ __launch_bounds__(GT) void gru_fwd_kernel(GruArgs args) {
+  const int dir = blockIdx.x / NW, j = blockIdx.x - dir * NW;
+  const GruDirArgs& a = args.d[dir];
+  const int Hh = a.Hh, tid = threadIdx.x, lane = tid & 63;
+  const int U = (Hh + NW - 1) / NW, u0 = j * U;
+  __shared__ float h[256];
+  __shared__ float gh[3 * MAXU];
+  __shared__ int dead;
+  if (tid == 0) dead = 0;
+  // this thread's slice of W_hh: row o of the workgroup's 3U rows, k-chunk c
+  const int o = tid >> 2, c = tid & 3;
+  const int g = o / U, ui = o - g * U, unit = u0 + ui;
+  const bool act = o < 3 * U && unit < Hh;
+  const int row = g * Hh + unit;
+  float w[KCH];
+#pragma unroll
+  for (int i = 0; i < KCH; ++i) {
+    const int k = c * KCH + i;
+    w[i] = (act && k < Hh) ? a.whh[(long long)row * Hh + k] : 0.f;
+  }
+  const float bias = act ? a.bhh[row] : 0.f;
+  for (int k = tid; k < 256; k += GT) h[k] = 0.f;
   __syncthreads();
   for (int s = 0; s < a.S; ++s) {
     const int t = a.reverse ? a.S - 1 - s : s;
-    for (int row = tid; row < H3; row += GRU_THREADS) {
-      float acc = a.bhh[row];
-      const float* w = a.whT + row;
-#pragma unroll 8
-      for (int k = 0; k < a.Hh; ++k) acc = fmaf(w[(long long)k * H3], h[k], acc);
-      gh[row] = acc;
-    }
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < KCH; ++i) acc = fmaf(w[i], h[c * KCH + i], acc);
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    if (act && c == 0) gh[o] = acc + bias;
     __syncthreads();
-    for (int j = tid; j < a.Hh; j += GRU_THREADS) {
-      const float* g = a.gi + (long long)t * a.ldgi;
-      const float r = sigm(g[j] + gh[j]);
-      const float z = sigm(g[a.Hh + j] + gh[a.Hh + j]);
-      const float n = tanhf(g[2 * a.Hh + j] + r * gh[2 * a.Hh + j]);
-      const float hp = h[j];
+    if (tid < U && u0 + tid < Hh) {
+      const int u = u0 + tid;
+      const float* gg = a.gi + (long long)t * a.ldgi;
+      const float r = sigm(gg[u] + gh[tid]);
+      const float z = sigm(gg[Hh + u] + gh[U + tid]);
+      const float n = tanhf(gg[2 * Hh + u] + r * gh[2 * U + tid]);
+      const float hp = h[u];
       const float hn = (1.f - z) * n + z * hp;
-      a.out[(long long)t * a.ldo + j] = hn;
-      a.hprev[(long long)t * a.Hh + j] = hp;
-      float* gs = a.gates + (long long)t * 4 * a.Hh;
-      gs[j] = r;
-      gs[a.Hh + j] = z;
-      gs[2 * a.Hh + j] = n;
-      gs[3 * a.Hh + j] = gh[2 * a.Hh + j];
-      h[j] = hn;
+      a.out[(long long)t * a.ldo + u] = hn;
+      a.hprev[(long long)t * Hh + u] = hp;
+      float* gs = a.gates + (long long)t * 4 * Hh;
+      gs[u] = r;
+      gs[Hh + u] = z;
+      gs[2 * Hh + u] = n;
+      gs[3 * Hh + u] = gh[2 * U + tid];
+      put_granule(a.gran + (long long)(s & 1) * Hh + u, (unsigned)(s + 1), hn);
     }
+    __syncthreads();   // every wave is done with the old h
+    if (s + 1 < a.S && tid < 64 &&
+        !gather_granules(a.gran + (long long)(s & 1) * Hh, Hh, (unsigned)(s + 1), h, args.tmo, lane))
+      dead = 1;
     __syncthreads();
+    if (dead) break;
   }
 }
 
@@ -84,107 +161,125 @@ struct GruBwdDirArgs {
   float* dgi;          // (S, 3Hh) ld lddgi
   long long lddgi;
   float* dgh;          // (S, 3Hh)
+  unsigned long long* gran;   // 2 slots x 3Hh granules
   int S, Hh, reverse;
 };
 
 struct GruBwdArgs {
   GruBwdDirArgs d[2];
+  unsigned* tmo;
 };
 
-__global__ __launch_bounds__(GRU_THREADS) void gru_bwd_kernel(GruBwdArgs args) {
-  const GruBwdDirArgs a = args.d[blockIdx.x];
-  extern __shared__ float sm[];
-  const int Hh = a.Hh, H3 = 3 * Hh;
-  float* dh = sm;              // Hh: recurrent gradient into h_{t}
-  float* g3 = sm + Hh;         // 3Hh: dgh of the current step
-  float* part = g3 + H3;       // 4 x Hh partial sums of W^T dgh
-  const int tid = threadIdx.x;
-  for (int j = tid; j < Hh; j += GRU_THREADS) dh[j] = 0.f;
+__global__ __launch_bounds__(GT) void gru_bwd_kernel(GruBwdArgs args) {
+  const int dir = blockIdx.x / NW, j = blockIdx.x - dir * NW;
+  const GruBwdDirArgs& a = args.d[dir];
+  const int Hh = a.Hh, H3 = 3 * Hh, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int U = (Hh + NW - 1) / NW, u0 = j * U;
+  __shared__ float dg[768];
+  __shared__ float dh[MAXU], dhd[MAXU];
+  __shared__ float part[4][MAXU];
+  __shared__ int dead;
+  if (tid == 0) dead = 0;
+  // this thread's slice of W_hh^T: unit i of the workgroup, gate rows [c*RCH, c*RCH + RCH)
+  const int i = tid & 15, c = tid >> 4;
+  const bool act = i < U && u0 + i < Hh;
+  float w[RCH];
+#pragma unroll
+  for (int r = 0; r < RCH; ++r) {
+    const int row = c * RCH + r;
+    w[r] = (act && row < H3) ? a.whh[(long long)row * Hh + u0 + i] : 0.f;
+  }
+  if (tid < MAXU) dh[tid] = 0.f;
   __syncthreads();
   for (int s = 0; s < a.S; ++s) {
     const int t = a.reverse ? s : a.S - 1 - s;   // reverse of the forward visiting order
-    const float* gs = a.gates + (long long)t * 4 * Hh;
-    for (int j = tid; j < Hh; j += GRU_THREADS) {
-      const float r = gs[j], z = gs[Hh + j], n = gs[2 * Hh + j], ghn = gs[3 * Hh + j];
-      const float hp = a.hprev[(long long)t * Hh + j];
-      const float d = a.dout[(long long)t * a.lddo + j] + dh[j];
+    unsigned long long* slot = a.gran + (long long)(s & 1) * H3;
+    if (tid < U && u0 + tid < Hh) {
+      const int u = u0 + tid;
+      const float* gs = a.gates + (long long)t * 4 * Hh;
+      const float r = gs[u], z = gs[Hh + u], n = gs[2 * Hh + u], ghn = gs[3 * Hh + u];
+      const float hp = a.hprev[(long long)t * Hh + u];
+      const float d = a.dout[(long long)t * a.lddo + u] + dh[tid];
       const float dnp = d * (1.f - z) * (1.f - n * n);
       const float dzp = d * (hp - n) * z * (1.f - z);
       const float drp = dnp * ghn * r * (1.f - r);
       float* gi = a.dgi + (long long)t * a.lddgi;
-      gi[j] = drp;
-      gi[Hh + j] = dzp;
-      gi[2 * Hh + j] = dnp;
+      gi[u] = drp;
+      gi[Hh + u] = dzp;
+      gi[2 * Hh + u] = dnp;
       float* gg = a.dgh + (long long)t * H3;
-      gg[j] = drp;
-      gg[Hh + j] = dzp;
-      gg[2 * Hh + j] = dnp * r;
-      g3[j] = drp;
-      g3[Hh + j] = dzp;
-      g3[2 * Hh + j] = dnp * r;
-      dh[j] = d * z;   // direct path; W^T dgh added below
+      gg[u] = drp;
+      gg[Hh + u] = dzp;
+      gg[2 * Hh + u] = dnp * r;
+      put_granule(slot + u, (unsigned)(s + 1), drp);
+      put_granule(slot + Hh + u, (unsigned)(s + 1), dzp);
+      put_granule(slot + 2 * Hh + u, (unsigned)(s + 1), dnp * r);
+      dhd[tid] = d * z;   // direct path; W^T dgh added below
     }
+    if (s + 1 == a.S) break;   // the last step's recurrent gradient feeds nothing
+    if (tid < 64 && !gather_granules(slot, H3, (unsigned)(s + 1), dg, args.tmo, lane)) dead = 1;
     __syncthreads();
-    // dh_rec[k] += sum_row W[row][k] * g3[row]; rows split over 4 thread groups
-    {
-      const int q = tid / Hh, k = tid - q * Hh;   // Hh <= 256 -> 4 groups of Hh threads
-      if (q < 4 && k < Hh) {
-        const int r0 = q * ((H3 + 3) / 4), r1 = min(H3, r0 + (H3 + 3) / 4);
-        float acc = 0.f;
-        for (int row = r0; row < r1; ++row) acc = fmaf(a.whh[(long long)row * Hh + k], g3[row], acc);
-        part[q * Hh + k] = acc;
-      }
+    if (dead) break;
+    float acc = 0.f;
+#pragma unroll
+    for (int r = 0; r < RCH; ++r) {
+      const int row = c * RCH + r;
+      acc = fmaf(w[r], row < H3 ? dg[row] : 0.f, acc);
     }
+    acc += __shfl_xor(acc, 16, 64);
+    acc += __shfl_xor(acc, 32, 64);
+    if (lane < 16) part[wv][lane] = acc;
     __syncthreads();
-    for (int j = tid; j < Hh; j += GRU_THREADS) dh[j] += (part[j] + part[Hh + j]) + (part[2 * Hh + j] + part[3 * Hh + j]);
+    if (tid < U) dh[tid] = dhd[tid] + (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
     __syncthreads();
-  }
-}
-
-__global__ void transpose_kernel(const float* in, int rows, int cols, float* out) {
-  // out[c][r] = in[r][c]
-  const long long total = (long long)rows * cols;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const long long r = i / cols, c = i % cols;
-    out[c * rows + r] = in[i];
   }
 }
 
 }  // namespace
 
+// floats of the per-call sync area: timeout word (padded to 16 B) + 2 dirs x 2 slots x 3Hh granules
+long long gru_sync_floats(int Hh) { return 4 + 2LL * 2 * 2 * 3 * Hh; }
+
 int launch_gru_fwd(const float* gi, long long ldgi, int S, int Hh, const float* const whh[2], const float* const bhh[2],
                    float* out, long long ldo, float* saved, float* ws, hipStream_t s) {
-  FX_REQUIRE(Hh > 0 && Hh <= 256, "gru: hidden size per direction must be <= 256");
+  FX_REQUIRE(Hh > 0 && Hh <= NW * MAXU, "gru: hidden size per direction must be <= 256");
   if (S == 0) return FX_OK;
-  const int H3 = 3 * Hh;
+  // ws: [timeout word (4 floats)] [2 dirs x 2 slots x Hh granules]; zeroed every call
+  unsigned* tmo = reinterpret_cast<unsigned*>(ws);
+  unsigned long long* gran = reinterpret_cast<unsigned long long*>(ws + 4);
+  FX_CHECK_HIP(hipMemsetAsync(ws, 0, sizeof(float) * gru_sync_floats(Hh), s));
   GruArgs args{};
+  args.tmo = tmo;
   for (int d = 0; d < 2; ++d) {
-    float* whT = ws + (long long)d * H3 * Hh;
-    hipLaunchKernelGGL(transpose_kernel, dim3(256), dim3(256), 0, s, whh[d], H3, Hh, whT);
     GruDirArgs& a = args.d[d];
-    a.gi = gi + d * H3;
+    a.gi = gi + d * 3 * Hh;
     a.ldgi = ldgi;
-    a.whT = whT;
+    a.whh = whh[d];
     a.bhh = bhh[d];
     a.out = out + d * Hh;
     a.ldo = ldo;
     a.hprev = saved + (long long)d * S * Hh;
     a.gates = saved + 2LL * S * Hh + (long long)d * S * 4 * Hh;
+    a.gran = gran + (long long)d * 2 * Hh;
     a.S = S;
     a.Hh = Hh;
     a.reverse = d;
   }
-  const size_t lds = sizeof(float) * 4 * Hh;
-  hipLaunchKernelGGL(gru_fwd_kernel, dim3(2), dim3(GRU_THREADS), lds, s, args);
+  hipLaunchKernelGGL(gru_fwd_kernel, dim3(2 * NW), dim3(GT), 0, s, args);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }
 
 int launch_gru_bwd(const float* dout, long long lddo, int S, int Hh, const float* const whh[2], const float* saved,
-                   float* dgi, long long lddgi, float* dgh, hipStream_t s) {
+                   float* dgi, long long lddgi, float* dgh, float* sync_ws, hipStream_t s) {
+  FX_REQUIRE(Hh > 0 && Hh <= NW * MAXU, "gru: hidden size per direction must be <= 256");
   if (S == 0) return FX_OK;
   const int H3 = 3 * Hh;
+  unsigned* tmo = reinterpret_cast<unsigned*>(sync_ws);
+  unsigned long long* gran = reinterpret_cast<unsigned long long*>(sync_ws + 4);
+  FX_CHECK_HIP(hipMemsetAsync(sync_ws, 0, sizeof(float) * gru_sync_floats(Hh), s));
   GruBwdArgs args{};
+  args.tmo = tmo;
   for (int d = 0; d < 2; ++d) {
     GruBwdDirArgs& a = args.d[d];
     a.dout = dout + d * Hh;
@@ -195,12 +290,12 @@ int launch_gru_bwd(const float* dout, long long lddo, int S, int Hh, const float
     a.dgi = dgi + d * H3;
     a.lddgi = lddgi;
     a.dgh = dgh + (long long)d * S * H3;
+    a.gran = gran + (long long)d * 2 * H3;
     a.S = S;
     a.Hh = Hh;
     a.reverse = d;
   }
-  const size_t lds = sizeof(float) * (Hh + 3 * Hh + 4 * Hh);
-  hipLaunchKernelGGL(gru_bwd_kernel, dim3(2), dim3(GRU_THREADS), lds, s, args);
+  hipLaunchKernelGGL(gru_bwd_kernel, dim3(2 * NW), dim3(GT), 0, s, args);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }

@@ -136,33 +136,13 @@ __global__ __launch_bounds__(1024) void ln_bwd_small_kernel(const float* dy, lon
                                                             const float* w, const float* rstd, int rows, int cols,
                                                             int relu, float* dx, long long lddx, float* dw,
                                                             float* db) {
+  // one pass: each wave loads its rows once (registers), writes dx and keeps per-column partial
+  // sums; the 16 waves' partials are then reduced in LDS 64 columns at a time
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   __shared__ float red[16][2][64];
-  for (int c0 = 0; c0 < cols; c0 += 64) {
-    const int c = c0 + lane;
-    float pw = 0.f, pb = 0.f;
-    for (int row = wv; row < rows; row += 16) {
-      if (c < cols) {
-        float d = dy[(long long)row * lddy + c];
-        if (relu && !(y[(long long)row * ldy + c] > 0.f)) d = 0.f;
-        pw += d * xhat[(long long)row * ldxh + c];
-        pb += d;
-      }
-    }
-    red[wv][0][lane] = pw;
-    red[wv][1][lane] = pb;
-    __syncthreads();
-    if (wv == 0 && c < cols) {
-      float a = 0.f, b = 0.f;
-      for (int k = 0; k < 16; ++k) {
-        a += red[k][0][lane];
-        b += red[k][1][lane];
-      }
-      if (dw) dw[c] += a;
-      if (db) db[c] += b;
-    }
-    __syncthreads();
-  }
+  float pw[MAXPL], pb[MAXPL];
+#pragma unroll
+  for (int i = 0; i < MAXPL; ++i) pw[i] = pb[i] = 0.f;
   for (int row = wv; row < rows; row += 16) {
     float g[MAXPL], h[MAXPL];
     float s1 = 0.f, s2 = 0.f;
@@ -174,6 +154,8 @@ __global__ __launch_bounds__(1024) void ln_bwd_small_kernel(const float* dy, lon
         float d = dy[(long long)row * lddy + c];
         if (relu && !(y[(long long)row * ldy + c] > 0.f)) d = 0.f;
         h[i] = xhat[(long long)row * ldxh + c];
+        pw[i] += d * h[i];
+        pb[i] += d;
         g[i] = d * w[c];
         s1 += g[i];
         s2 += g[i] * h[i];
@@ -187,6 +169,25 @@ __global__ __launch_bounds__(1024) void ln_bwd_small_kernel(const float* dy, lon
       const int c = i * 64 + lane;
       if (c < cols) dx[(long long)row * lddx + c] = rs * (g[i] - s1 - h[i] * s2);
     }
+  }
+  if (!dw && !db) return;
+#pragma unroll
+  for (int i = 0; i < MAXPL; ++i) {
+    if (i * 64 >= cols) break;
+    red[wv][0][lane] = pw[i];
+    red[wv][1][lane] = pb[i];
+    __syncthreads();
+    const int c = i * 64 + lane;
+    if (wv == 0 && c < cols) {
+      float a = 0.f, b = 0.f;
+      for (int k = 0; k < 16; ++k) {
+        a += red[k][0][lane];
+        b += red[k][1][lane];
+      }
+      if (dw) dw[c] += a;
+      if (db) db[c] += b;
+    }
+    __syncthreads();
   }
 }
 
@@ -419,7 +420,6 @@ int launch_layernorm_bwd(const float* dy, long long lddy, const float* y, long l
   FX_REQUIRE(cols > 0 && cols <= 64 * MAXPL, "layernorm: cols must be in (0, 1024]");
   if (rows == 0) return FX_OK;
   if (rows <= 64) {
-    // dx is written after every dy row was read for the column sums: dx may alias dy
     hipLaunchKernelGGL(ln_bwd_small_kernel, dim3(1), dim3(1024), 0, s, dy, lddy, y, ldy, xhat, ldxh, w, rstd, rows,
                        cols, relu, dx, lddx, dw, db);
     FX_CHECK_HIP(hipGetLastError());

@@ -90,23 +90,24 @@ class Block(nn.Module):
 
     @staticmethod
     def _abranch_prob(action_clogit, a2f_attn):
-        """Per-frame class distribution of the most-attended non-null token (blocks.py:246-258)."""
+        """Per-frame class distribution of the most-attended non-null token (blocks.py:246-258),
+        without a host sync: null tokens are masked to -inf before the argmax (first maximum, as
+        the reference's argmax over the non-null subset).  Returns (prob (T, C), any_token)
+        where ``any_token`` is a device bool: False is the reference's ``len(action_loc) == 0``."""
         acl = action_clogit.squeeze(1)
         a2f = a2f_attn.squeeze(0)
         null_cid = acl.shape[-1] - 1
-        loc = torch.nonzero(acl.argmax(1) != null_cid)[:, 0]
-        if loc.numel() == 0:
-            return None
+        is_tok = acl.argmax(1) != null_cid
+        masked = torch.where(is_tok[None, :], a2f, torch.full((), float("-inf"), device=a2f.device, dtype=a2f.dtype))
         qtk_prob = torch.softmax(acl[:, :-1], dim=1)
-        return qtk_prob[loc[a2f[:, loc].argmax(-1)]]
+        return qtk_prob[masked.argmax(-1)], is_tok.any()
 
     @staticmethod
     def _eval(action_clogit, a2f_attn, frame_clogit, weight):
         fprob = torch.softmax(frame_clogit.squeeze(1), dim=-1)
-        ab = Block._abranch_prob(action_clogit, a2f_attn)
-        if ab is None:
-            return fprob.argmax(1)
-        return ((1 - weight) * ab + weight * fprob).argmax(1)
+        ab, any_tok = Block._abranch_prob(action_clogit, a2f_attn)
+        mixed = ((1 - weight) * ab + weight * fprob).argmax(1)
+        return torch.where(any_tok, mixed, fprob.argmax(1))
 
     @staticmethod
     def _eval_w_transcript(transcript, a2f_attn, frame_clogit, weight):
@@ -304,9 +305,9 @@ class _FACTBase(nn.Module):
             block_output.append([frame_feature, action_feature])
         return block_output
 
-    def _fact_loss(self, label):
+    def _fact_loss(self, label, label_host=None):
         mc: MatchCriterion = self.mcriterion
-        mc.set_label(label)
+        mc.set_label(label, label_host=label_host)
         last = self.block_list[-1]
         match = mc.match(basic.logit2prob(last.action_clogit, dim=-1), last.a2f_attn)
         self.loss_list = [blk.compute_loss(mc, match) for blk in self.block_list]
@@ -328,23 +329,11 @@ class FACT(_FACTBase):
     def _forward_one_video(self, seq, transcript=None):
         return self._run_blocks(seq, transcript)
 
-    def _loss_one_video(self, label):
-        return self._fact_loss(label)
+    def _loss_one_video(self, label, label_host=None):
+        return self._fact_loss(label, label_host)
 
     def forward(self, seq_list, label_list, compute_loss=False):
-        save_list, losses = [], []
-        for seq, label in zip(seq_list, label_list):
-            trans = torch_class_label_to_segment_label(label)[0]
-            self._forward_one_video(seq.unsqueeze(1), trans)
-            save = {"pred": utils.to_numpy(self.block_list[-1].eval(trans))}
-            save_list.append(save)
-            if compute_loss:
-                lo = self._loss_one_video(label)
-                losses.append(lo)
-                save["loss"] = {"loss": lo.item()}
-        if compute_loss:
-            return sum(losses) / len(losses), save_list
-        return save_list
+        return _forward_videos(self, seq_list, label_list, compute_loss)
 
 
 class FACT_CLIP(_FACTBase):
@@ -372,8 +361,8 @@ class FACT_CLIP(_FACTBase):
         self.projected_frame_embeddings = self.frame_projection(frame_feature[:, :, :feat_dim])
         return out
 
-    def _loss_one_video(self, label):
-        fact_loss = self._fact_loss(label)
+    def _loss_one_video(self, label, label_host=None):
+        fact_loss = self._fact_loss(label, label_host)
         if self.text_embeddings is None or not hasattr(self, "projected_frame_embeddings"):
             return fact_loss
         mc = self.mcriterion
@@ -383,15 +372,28 @@ class FACT_CLIP(_FACTBase):
         hold = list(getattr(self.cfg, "holdout_classes", []) or [])
         if hold:
             n = text.shape[0]
-            seen = torch.tensor([i for i in range(n) if i not in set(hold)], device=text.device)
+            key = (n, tuple(hold), str(text.device))
+            if getattr(self, "_holdout_key", None) != key:
+                seen_h = [i for i in range(n) if i not in set(hold)]
+                remap_h = torch.full((n,), -1, dtype=torch.long)
+                remap_h[seen_h] = torch.arange(len(seen_h))
+                self._holdout_key = key
+                self._holdout_tabs = (torch.tensor(seen_h, device=text.device), remap_h.to(text.device),
+                                      remap_h.numpy())
+            seen, remap, remap_np = self._holdout_tabs
             text = text[seen]
-            remap = torch.full((n,), -1, device=text.device, dtype=torch.long)
-            remap[seen] = torch.arange(len(seen), device=text.device)
             labels = remap[labels]
-            valid = labels != -1
-            if not bool(valid.all()):
-                if int(valid.sum()) == 0:
+            lab_np = getattr(mc, "_label_np", None)
+            if lab_np is not None:
+                valid_np = remap_np[lab_np] != -1
+                n_valid, all_valid = int(valid_np.sum()), bool(valid_np.all())
+            else:                                     # no host copy: decide on the device (a sync)
+                valid_d = labels != -1
+                n_valid, all_valid = int(valid_d.sum()), bool(valid_d.all())
+            if not all_valid:
+                if n_valid == 0:
                     return fact_loss
+                valid = labels != -1
                 labels = labels[valid]
                 emb = emb.reshape(-1, emb.shape[-1])[valid].unsqueeze(1)
         con = loss_mod.infonce_contrastive_loss(emb, text, labels, temperature=self.cfg.CLIP.temp)
@@ -407,38 +409,58 @@ class FACT_CLIP(_FACTBase):
         emb = self.projected_frame_embeddings.squeeze(1)
         clip_prob = torch.softmax(emb @ self.text_embeddings.t() / self.cfg.CLIP.temp, dim=-1)
         last = self.block_list[-1]
-        ab = Block._abranch_prob(last.action_clogit, last.a2f_attn)
-        if ab is None:
-            return clip_prob.argmax(1)
+        ab, any_tok = Block._abranch_prob(last.action_clogit, last.a2f_attn)
         w = self.cfg.FACT.mwt
-        return ((1 - w) * ab + w * clip_prob).argmax(1)
+        return torch.where(any_tok, ((1 - w) * ab + w * clip_prob).argmax(1), clip_prob.argmax(1))
 
     def forward(self, seq_list, label_list, compute_loss=False):
-        """blocks.py:889-917.  The per-video loss floats of ``save['loss']`` are read back in one
-        device->host copy after the last video (the reference calls .item() three times per
-        video, each a full device drain); values and keys are the same."""
-        save_list, losses, pending = [], [], []
-        for seq, label in zip(seq_list, label_list):
-            trans = torch_class_label_to_segment_label(label)[0]
-            self._forward_one_video(seq.unsqueeze(1), trans)
-            save = {"pred": utils.to_numpy(self.eval_with_clip(trans))}
-            save_list.append(save)
-            if compute_loss:
-                lo = self._loss_one_video(label)
-                losses.append(lo)
-                keys, vals = ["loss"], [lo.detach()]
-                if hasattr(self, "fact_loss"):
-                    keys.append("fact_loss")
-                    vals.append(self.fact_loss.detach().reshape(()))
-                if hasattr(self, "contrastive_loss"):
-                    keys.append("contrastive_loss")
-                    vals.append(self.contrastive_loss.detach().reshape(()))
-                pending.append((save, keys, vals))
+        return _forward_videos(self, seq_list, label_list, compute_loss)
+
+
+def _forward_videos(net, seq_list, label_list, compute_loss):
+    """FACT.forward / FACT_CLIP.forward (blocks.py:118-135, 889-917) with the reference's results and
+    fewer device drains: the transcript is only built where it is used (FACT.trans), each label is
+    copied to the host asynchronously at the start of its video (read at the loss, after the TDU
+    segmentation already synchronised), the per-frame predictions and the loss floats come back in
+    one device->host copy after the last video."""
+    clip = isinstance(net, FACT_CLIP)
+    save_list, losses, pending, preds = [], [], [], []
+    for seq, label in zip(seq_list, label_list):
+        if label.is_cuda:
+            label_host = label.to("cpu", non_blocking=True)
+            ready = torch.cuda.Event()
+            ready.record()
+        else:
+            label_host, ready = label, None
+        trans = torch_class_label_to_segment_label(label)[0] if net.cfg.FACT.trans else None
+        net._forward_one_video(seq.unsqueeze(1), trans)
+        preds.append(net.eval_with_clip(trans) if clip else net.block_list[-1].eval(trans))
+        save = {}
+        save_list.append(save)
         if compute_loss:
-            flat = torch.stack([v.float() for _, _, vals in pending for v in vals]).tolist()
-            i = 0
-            for save, keys, vals in pending:
-                save["loss"] = dict(zip(keys, flat[i:i + len(keys)]))
-                i += len(keys)
-            return sum(losses) / len(losses), save_list
-        return save_list
+            lo = net._loss_one_video(label, label_host=(label_host, ready))
+            losses.append(lo)
+            keys, vals = ["loss"], [lo.detach()]
+            if clip and hasattr(net, "fact_loss"):
+                keys.append("fact_loss")
+                vals.append(net.fact_loss.detach().reshape(()))
+            if clip and hasattr(net, "contrastive_loss"):
+                keys.append("contrastive_loss")
+                vals.append(net.contrastive_loss.detach().reshape(()))
+            pending.append((save, keys, vals))
+    # one readback for every video's predictions (+ loss floats)
+    flat = [p.reshape(-1).to(torch.int64) for p in preds]
+    nums = [v.float().reshape(1) for _, _, vals in pending for v in vals]
+    host = torch.cat(flat).cpu().numpy() if flat else None
+    off = 0
+    for save, p in zip(save_list, preds):
+        save["pred"] = host[off:off + p.numel()].copy()
+        off += p.numel()
+    if compute_loss:
+        vals = torch.cat(nums).tolist()
+        i = 0
+        for save, keys, _ in pending:
+            save["loss"] = dict(zip(keys, vals[i:i + len(keys)]))
+            i += len(keys)
+        return sum(losses) / len(losses), save_list
+    return save_list

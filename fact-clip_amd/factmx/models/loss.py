@@ -22,6 +22,13 @@ def smooth_loss(logit, is_logit=True):
     return torch.clamp(step * step, min=0, max=16).mean()
 
 
+def _to_dev(t, dev):
+    """Host -> device without a device drain: pinned staging + non-blocking copy."""
+    if t.device == dev or dev.type == "cpu":
+        return t.to(dev)
+    return t.pin_memory().to(dev, non_blocking=True)
+
+
 def _onehot(idx, n):
     return F.one_hot(idx.to(torch.int64), n).to(torch.float32)
 
@@ -47,23 +54,45 @@ class MatchCriterion:
         self.bg_ids = list(bg_ids) if bg_ids is not None else []
         self._class_weight = class_weight
 
-    def set_label(self, label):
+    def set_label(self, label, label_host=None):
+        """loss.py:58-84.  ``label_host`` = (cpu tensor, cuda event) from an asynchronous copy
+        started earlier (FACT*.forward): the run-length transcript is then built on the host
+        without draining the device; without it the device path below is used."""
         self.class_label = label
-        self.transcript, self.seg_label = torch_class_label_to_segment_label(label)
-        self.onehot_class_label = _onehot(label, self.nclasses)
-        self.onehot_seg_label = _onehot(self.seg_label, len(self.transcript))
         dev = label.device
+        lab_np = None
+        if label_host is not None:
+            lh, ev = label_host
+            if ev is not None:
+                ev.synchronize()
+            lab_np = lh.numpy()
+        elif not label.is_cuda:
+            lab_np = label.numpy()
+        self._label_np = lab_np
+        if lab_np is not None:
+            change = np.ones(len(lab_np), dtype=bool)
+            change[1:] = lab_np[1:] != lab_np[:-1]
+            self._transcript_np = lab_np[change].astype(np.int64)
+            self.transcript = _to_dev(torch.from_numpy(self._transcript_np), dev)
+            self.seg_label = _to_dev(torch.from_numpy((np.cumsum(change) - 1).astype(lab_np.dtype)), dev)
+        else:
+            self.transcript, self.seg_label = torch_class_label_to_segment_label(label)
+            self._transcript_np = None
+        S = int(self.transcript.shape[0])
+        self.onehot_class_label = _onehot(label, self.nclasses)
+        self.onehot_seg_label = _onehot(self.seg_label, S)
         cw = torch.ones(self.nclasses + 1, device=dev)
         cw[-1] = self.cfg.Loss.nullw
-        sw = torch.ones(len(self.transcript), dtype=torch.float32, device=dev)
+        sw = torch.ones(S, dtype=torch.float32, device=dev)
         if self._class_weight is not None:
             cw[:self.nclasses] = torch.as_tensor(self._class_weight[:self.nclasses], dtype=torch.float32, device=dev)
             sw = torch.as_tensor(self._class_weight, dtype=torch.float32, device=dev)[self.transcript]
         else:
             for i in self.bg_ids:
                 cw[i] = self.cfg.Loss.bgw
-                sw[self.transcript == i] = self.cfg.Loss.bgw
+                sw = torch.where(self.transcript == i, torch.full_like(sw, self.cfg.Loss.bgw), sw)
         self.cweight, self.sweight = cw, sw
+        self._match_cache = None
 
     def _label_to_onehot(self, label, nclass):
         return _onehot(label, nclass)
@@ -99,11 +128,22 @@ class MatchCriterion:
             ai, si = self._one_to_many_match(cost)
         else:
             raise ValueError(mcfg.match)
-        return torch.as_tensor(np.asarray(ai), dtype=torch.int64), torch.as_tensor(np.asarray(si), dtype=torch.int64)
+        ai = torch.as_tensor(np.asarray(ai), dtype=torch.int64)
+        si = torch.as_tensor(np.asarray(si), dtype=torch.int64)
+        self._match_cache = (ai, si, _to_dev(ai, clogit.device), _to_dev(si, clogit.device))
+        return ai, si
+
+    def _dev_match(self, match, dev):
+        """Device copies of the match indices (made once per match, not once per loss term)."""
+        aind, sind = match
+        mc = getattr(self, "_match_cache", None)
+        if mc is not None and aind is mc[0] and sind is mc[1] and mc[2].device == dev:
+            return mc[2], mc[3]
+        return _to_dev(aind, dev), _to_dev(sind, dev)
 
     def _one_to_many_match(self, cost):
         """loss.py:155-193."""
-        tr = self.transcript.cpu().numpy()
+        tr = self._transcript_np if getattr(self, "_transcript_np", None) is not None else self.transcript.cpu().numpy()
         actions = np.unique(tr)
         per_action = np.stack([cost[:, tr == a].sum(1) for a in actions], axis=1)
         aid, cid = linear_sum_assignment(per_action)
@@ -123,11 +163,11 @@ class MatchCriterion:
 
     def action_token_loss(self, match, action_clogit, is_logit=True):
         """loss.py:195-207."""
-        aind, sind = match
         A, C = action_clogit.shape[0], action_clogit.shape[-1]
         dev = action_clogit.device
+        aind, sind = self._dev_match(match, dev)
         tgt = torch.full((A,), C - 1, dtype=torch.int64, device=dev)
-        tgt[aind.to(dev)] = self.transcript[sind.to(dev)]
+        tgt[aind] = self.transcript[sind]
         x = action_clogit.squeeze(1)
         if is_logit:
             return _weighted_xent(x, tgt, self.cweight)
@@ -143,18 +183,16 @@ class MatchCriterion:
     def cross_attn_loss(self, match, attn, dim=None):
         """loss.py:209-222."""
         assert dim >= 1
-        aind, sind = match
-        dev = attn.device
-        tgt = self.onehot_seg_label[:, sind.to(dev)]
-        return self._attn_xent(attn[0, :, aind.to(dev)], tgt, dim, self.onehot_seg_label.sum())
+        aind, sind = self._dev_match(match, attn.device)
+        tgt = self.onehot_seg_label[:, sind]
+        return self._attn_xent(attn[0, :, aind], tgt, dim, self.onehot_seg_label.sum())
 
     def cross_attn_loss_tdu(self, match, attn, tdu, dim=None):
         """loss.py:224-244."""
         assert dim >= 1
-        aind, sind = match
-        dev = attn.device
+        aind, sind = self._dev_match(match, attn.device)
         z = _zoom(tdu, self.onehot_seg_label)
-        return self._attn_xent(attn[0, :, aind.to(dev)], z[:, sind.to(dev)], dim, z.sum())
+        return self._attn_xent(attn[0, :, aind], z[:, sind], dim, z.sum())
 
     def frame_loss(self, frame_clogit, is_logit=True):
         """loss.py:246-258."""

@@ -50,10 +50,10 @@ static double time_us(F fn, int iters = 200) {
 }
 
 static void gemm_case(const char* name, int M, int N, int K, fx_operand a, fx_operand b, float* c, long long ldc,
-                      int split = 1, float* ws = nullptr) {
+                      int split = 1, float* ws = nullptr, float beta = 0.f, float* c_last = nullptr) {
   fx_gemm_desc d{};
   d.M = M; d.N = N; d.K = K; d.batch = 1; d.a = a; d.b = b; d.c = c; d.ldc = ldc; d.alpha = 1.f;
-  d.split_k = split; d.workspace = ws;
+  d.split_k = split; d.workspace = ws; d.beta = beta; d.c_last_col = c_last;
   int st = fx_gemm(&d, nullptr);
   if (st) { printf("%s: error %s\n", name, fx_last_error()); return; }
   double us = time_us([&] { fx_gemm(&d, nullptr); });
@@ -76,6 +76,26 @@ int main() {
   gemm_case("tok dy.W    (rows,cols)", 32, 256, 256, rows(big, 256), cols(w, 256), c, 256);
   gemm_case("tok dW dy^T.x (cols,cols)", 256, 256, 32, cols(big, 256), cols(w, 256), c, 256);
   gemm_case("tok dW dy^T.x (cols,cols)", 512, 256, 32, cols(big, 512), cols(w, 256), c, 256);
+  {
+    fx_operand bo = cols(w, 256);
+    bo.ones_col = 257;
+    gemm_case("tok dW+db beta1 (cols,cols+1)", 256, 257, 32, cols(big, 256), bo, c, 256, 1, nullptr, 1.f, c + 300000);
+  }
+  {
+    float* xh = dalloc(64 * 1024, 1.f);
+    float* rs = dalloc(1024, 1.f);
+    float* lw = dalloc(1024, 1.f);
+    float* dw = dalloc(1024, 0.f);
+    float* lws = dalloc(1 << 20, 0.f);
+    double us = time_us([&] { fx_layernorm_bwd(big, 256, nullptr, 0, xh, 256, lw, rs, 32, 256, 0, c, 256, dw, dw + 256,
+                                               lws, nullptr); });
+    printf("%-34s rows=32 cols=256           %8.2f us\n", "layernorm bwd (token)", us);
+    us = time_us([&] { fx_layernorm_fwd(big, 256, nullptr, 0, lw, lw, 1e-5f, 32, 256, 0, c, 256, xh, 256, rs, nullptr); });
+    printf("%-34s rows=32 cols=256           %8.2f us\n", "layernorm fwd (token)", us);
+    us = time_us([&] { fx_layernorm_bwd(big, 256, nullptr, 0, xh, 256, lw, rs, 4096, 256, 0, c, 256, dw, dw + 256,
+                                        lws, nullptr); });
+    printf("%-34s rows=4096 cols=256         %8.2f us\n", "layernorm bwd (frames)", us);
+  }
   // frame-level
   gemm_case("frame 1x1   (rows,rows)", 4096, 256, 256, rows(big, 256), rows(w, 256), c, 256);
   gemm_case("frame 1x1   (rows,rows)", 8192, 256, 256, rows(big, 256), rows(w, 256), c, 256);
