@@ -41,7 +41,12 @@ __global__ __launch_bounds__(NT) void mha_small_fwd_kernel(const float* q, long 
                                                            int Lk, int hd, float scale, float* probs, float* o,
                                                            long long ldo) {
   __shared__ float Qs[SM][SP], Ks[SM][SP], Vs[SM][SP], Ps[SM][SP];
-  const int h = blockIdx.x;
+  const int h = blockIdx.x, vid = blockIdx.y;   // head, video (rows vid*Lq.. of q/o, vid*Lk.. of k/v)
+  q += (long long)vid * Lq * ldq;
+  k += (long long)vid * Lk * ldk;
+  v += (long long)vid * Lk * ldv;
+  o += (long long)vid * Lq * ldo;
+  probs += (long long)vid * gridDim.x * Lq * Lk;
   load_tile(Qs, q + h * hd, ldq, Lq, hd);
   load_tile(Ks, k + h * hd, ldk, Lk, hd);
   load_tile(Vs, v + h * hd, ldv, Lk, hd);
@@ -81,7 +86,15 @@ __global__ __launch_bounds__(NT) void mha_small_bwd_kernel(const float* q, long 
                                                            long long lddq, float* dk, long long lddk, float* dv,
                                                            long long lddv) {
   __shared__ float Qs[SM][SP], Ks[SM][SP], Vs[SM][SP], Ps[SM][SP], Ds[SM][SP], Gs[SM][SP];
-  const int h = blockIdx.x;
+  const int h = blockIdx.x, vid = blockIdx.y;
+  q += (long long)vid * Lq * ldq;
+  k += (long long)vid * Lk * ldk;
+  v += (long long)vid * Lk * ldv;
+  probs += (long long)vid * gridDim.x * Lq * Lk;
+  dout += (long long)vid * Lq * lddo;
+  if (dq) dq += (long long)vid * Lq * lddq;
+  if (dk) dk += (long long)vid * Lk * lddk;
+  if (dv) dv += (long long)vid * Lk * lddv;
   load_tile(Qs, q + h * hd, ldq, Lq, hd);
   load_tile(Ks, k + h * hd, ldk, Lk, hd);
   load_tile(Vs, v + h * hd, ldv, Lk, hd);
@@ -133,10 +146,11 @@ __global__ __launch_bounds__(NT) void mha_small_bwd_kernel(const float* q, long 
 
 int launch_mha_small_fwd(const float* q, long long ldq, const float* k, long long ldk, const float* v, long long ldv,
                          int Lq, int Lk, int hd, int nhead, float scale, float* probs, float* o, long long ldo,
-                         hipStream_t s) {
+                         hipStream_t s, int nvid) {
   FX_REQUIRE(Lq > 0 && Lk > 0 && hd > 0 && Lq <= SM && Lk <= SM && hd <= SM && nhead > 0,
              "mha_small: Lq, Lk, head_dim must be in [1, 64]");
-  hipLaunchKernelGGL(mha_small_fwd_kernel, dim3(nhead), dim3(NT), 0, s, q, ldq, k, ldk, v, ldv, Lq, Lk, hd, scale,
+  FX_REQUIRE(nvid >= 1, "mha_small: nvid >= 1");
+  hipLaunchKernelGGL(mha_small_fwd_kernel, dim3(nhead, nvid), dim3(NT), 0, s, q, ldq, k, ldk, v, ldv, Lq, Lk, hd, scale,
                      probs, o, ldo);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
@@ -145,10 +159,11 @@ int launch_mha_small_fwd(const float* q, long long ldq, const float* k, long lon
 int launch_mha_small_bwd(const float* q, long long ldq, const float* k, long long ldk, const float* v, long long ldv,
                          const float* probs, const float* dout, long long lddo, int Lq, int Lk, int hd, int nhead,
                          float scale, float* dq, long long lddq, float* dk, long long lddk, float* dv, long long lddv,
-                         hipStream_t s) {
+                         hipStream_t s, int nvid) {
   FX_REQUIRE(Lq > 0 && Lk > 0 && hd > 0 && Lq <= SM && Lk <= SM && hd <= SM && nhead > 0,
              "mha_small: Lq, Lk, head_dim must be in [1, 64]");
-  hipLaunchKernelGGL(mha_small_bwd_kernel, dim3(nhead), dim3(NT), 0, s, q, ldq, k, ldk, v, ldv, probs, dout, lddo,
+  FX_REQUIRE(nvid >= 1, "mha_small: nvid >= 1");
+  hipLaunchKernelGGL(mha_small_bwd_kernel, dim3(nhead, nvid), dim3(NT), 0, s, q, ldq, k, ldk, v, ldv, probs, dout, lddo,
                      Lq, Lk, hd, scale, dq, lddq, dk, lddk, dv, lddv);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;

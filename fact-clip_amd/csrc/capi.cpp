@@ -569,8 +569,12 @@ int fx_mha_core_bwd(const float* q, long long ldq, const float* k, long long ldk
 }
 
 // ---------------------------------------------------------------- X2Y_map
-// Single-head cross attention of basic.py:349-389 (kq_pos=True).
+// Single-head cross attention of basic.py:349-389 (kq_pos=True), nvid videos stacked by rows:
+// video v owns X rows [x_off[v], x_off[v+1]) and Y rows [y_off[v], y_off[v+1]) (host prefix arrays,
+// NULL for one video); projections run over all rows at once, the attention core per video.
+// logit / attn hold each video's (ny_v x nx_v) block, packed in video order.
 // saved: xin (Nx*xdim, X+Xpos when Xpos), yin (Ny*ydim), xk, xv (Nx*Hd), yq, feat (Ny*Hd)
+}  // extern "C"
 namespace {
 struct X2YLayout {
   long long xin, yin, xk, xv, yq, feat, total;
@@ -586,7 +590,28 @@ X2YLayout x2y_layout(int Nx, int xdim, int Ny, int ydim, int Hd) {
   L.total = L.feat + (long long)Ny * Hd;
   return L;
 }
-long long x2y_split_ws(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim) {
+struct VidRows {
+  int n;
+  std::vector<int> x, y;        // prefix offsets (n + 1)
+  std::vector<long long> a;     // attention block offsets (n + 1)
+};
+VidRows vid_rows(int Nx, int Ny, int nvid, const int* x_off, const int* y_off) {
+  VidRows v;
+  v.n = std::max(nvid, 1);
+  if (v.n == 1 || !x_off || !y_off) {
+    v.n = 1;
+    v.x = {0, Nx};
+    v.y = {0, Ny};
+  } else {
+    v.x.assign(x_off, x_off + v.n + 1);
+    v.y.assign(y_off, y_off + v.n + 1);
+  }
+  v.a.assign(v.n + 1, 0);
+  for (int i = 0; i < v.n; ++i)
+    v.a[i + 1] = v.a[i] + (long long)(v.y[i + 1] - v.y[i]) * (v.x[i + 1] - v.x[i]);
+  return v;
+}
+long long x2y_split_ws1(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim) {
   long long sp = 0;
   sp = std::max(sp, split_ws(Ny, Nx, Hd));             // logits
   sp = std::max(sp, split_ws(Ny, Hd, Nx));             // feat, dyq
@@ -600,25 +625,35 @@ long long x2y_split_ws(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim) {
   sp = std::max(sp, split_ws(Ny, ydim, Hd));           // dY
   return sp;
 }
+long long x2y_split_ws(const VidRows& v, int xdim, int ydim, int Hd, int outdim) {
+  long long sp = x2y_split_ws1(v.x[v.n], xdim, v.y[v.n], ydim, Hd, outdim);
+  for (int i = 0; i < v.n; ++i)
+    sp = std::max(sp, x2y_split_ws1(v.x[i + 1] - v.x[i], xdim, v.y[i + 1] - v.y[i], ydim, Hd, outdim));
+  return sp;
+}
 }  // namespace
+extern "C" {
 
 long long fx_x2y_saved_floats(int Nx, int xdim, int Ny, int ydim, int Hd) {
   return x2y_layout(Nx, xdim, Ny, ydim, Hd).total;
 }
 
-long long fx_x2y_workspace_floats(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim) {
-  long long w = (long long)Ny * (ydim + Hd) + (long long)Ny * Nx + 2LL * Nx * Hd + (long long)Ny * Hd +
+long long fx_x2y_workspace_floats(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim, int nvid,
+                                  const int* x_off, const int* y_off) {
+  const VidRows v = vid_rows(Nx, Ny, nvid, x_off, y_off);
+  long long w = (long long)Ny * (ydim + Hd) + v.a[v.n] + 2LL * Nx * Hd + (long long)Ny * Hd +
                 (long long)Nx * xdim + (long long)Ny * ydim;
-  return w + x2y_split_ws(Nx, xdim, Ny, ydim, Hd, outdim) +
-         colsum_workspace_floats(std::max(Nx, Ny), std::max(Hd, outdim));
+  return w + x2y_split_ws(v, xdim, ydim, Hd, outdim) + colsum_workspace_floats(std::max(Nx, Ny), std::max(Hd, outdim));
 }
 
 int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpos, long long ldxp, int xpos_cols,
                const float* Y, long long ldy, int Ny, int ydim, const float* Ypos, long long ldyp, int ypos_cols,
                const float* wk, const float* bk, const float* wv, const float* bv, const float* wq, const float* bq,
-               const float* wy, const float* by, int Hd, int outdim, float* out, long long ldo, float* logit,
-               float* attn, float* saved, float* workspace, void* stream) {
+               const float* wy, const float* by, int Hd, int outdim, int nvid, const int* x_off, const int* y_off,
+               float* out, long long ldo, float* logit, float* attn, float* saved, float* workspace, void* stream) {
   hipStream_t s = (hipStream_t)stream;
+  const VidRows V = vid_rows(Nx, Ny, nvid, x_off, y_off);
+  FX_REQUIRE(V.x[V.n] == Nx && V.y[V.n] == Ny, "x2y: offsets must end at Nx / Ny");
   const X2YLayout L = x2y_layout(Nx, xdim, Ny, ydim, Hd);
   float* xk = saved + L.xk;
   float* xv = saved + L.xv;
@@ -647,19 +682,27 @@ int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpo
   FX_TRY(linear_fwd(X, ldx, Nx, xdim, wv, bv, xv, Hd, Hd, 0, s));
   FX_TRY(linear_fwd(yin, ldyin, Ny, ydim, wq, bq, yq, Hd, Hd, 0, s));
   const float scale = 1.0f / std::sqrt((float)Hd);
-  {
-    fx_gemm_desc d = gemm_desc(Ny, Nx, Hd, op_rows(yq, Hd), op_rows(xk, Hd), logit, Nx);
-    d.alpha = scale;
-    d.split_k = pick_split(Ny, Nx, Hd);
-    d.workspace = workspace;
-    FX_TRY(launch_gemm(d, s));
-  }
-  FX_TRY(launch_softmax_rows(logit, Nx, Ny, Nx, 1.f, attn, Nx, s));
-  {
-    fx_gemm_desc d = gemm_desc(Ny, Hd, Nx, op_rows(attn, Nx), op_cols(xv, Hd), feat, Hd);
-    d.split_k = pick_split(Ny, Hd, Nx);
-    d.workspace = workspace;
-    FX_TRY(launch_gemm(d, s));
+  for (int v = 0; v < V.n; ++v) {
+    const int nx = V.x[v + 1] - V.x[v], ny = V.y[v + 1] - V.y[v];
+    if (nx == 0 || ny == 0) continue;
+    float* lg = logit + V.a[v];
+    float* at = attn + V.a[v];
+    {
+      fx_gemm_desc d = gemm_desc(ny, nx, Hd, op_rows(yq + (long long)V.y[v] * Hd, Hd),
+                                 op_rows(xk + (long long)V.x[v] * Hd, Hd), lg, nx);
+      d.alpha = scale;
+      d.split_k = pick_split(ny, nx, Hd);
+      d.workspace = workspace;
+      FX_TRY(launch_gemm(d, s));
+    }
+    FX_TRY(launch_softmax_rows(lg, nx, ny, nx, 1.f, at, nx, s));
+    {
+      fx_gemm_desc d = gemm_desc(ny, Hd, nx, op_rows(at, nx), op_cols(xv + (long long)V.x[v] * Hd, Hd),
+                                 feat + (long long)V.y[v] * Hd, Hd);
+      d.split_k = pick_split(ny, Hd, nx);
+      d.workspace = workspace;
+      FX_TRY(launch_gemm(d, s));
+    }
   }
   // Y_W(cat[Y, feat]) with the concatenation folded into the A-operand loader
   fx_operand a = op_rows(Y, ldy);
@@ -673,11 +716,13 @@ int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpo
 
 int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, const float* Y, long long ldy, int Ny,
                int ydim, int ypos_cols, const float* wk, const float* wv, const float* wq, const float* wy, int Hd,
-               int outdim, const float* attn, const float* saved, const float* dout, long long lddo,
-               const float* dlogit, const float* dattn, float* dX, float* dXpos, float* dY, float* dYpos, float* dwk,
-               float* dbk, float* dwv, float* dbv, float* dwq, float* dbq, float* dwy, float* dby, int has_xpos,
-               int has_ypos, float* workspace, void* stream) {
+               int outdim, int nvid, const int* x_off, const int* y_off, const float* attn, const float* saved,
+               const float* dout, long long lddo, const float* dlogit, const float* dattn, float* dX, float* dXpos,
+               float* dY, float* dYpos, float* dwk, float* dbk, float* dwv, float* dbv, float* dwq, float* dbq,
+               float* dwy, float* dby, int has_xpos, int has_ypos, float* workspace, void* stream) {
   hipStream_t s = (hipStream_t)stream;
+  const VidRows V = vid_rows(Nx, Ny, nvid, x_off, y_off);
+  FX_REQUIRE(V.x[V.n] == Nx && V.y[V.n] == Ny, "x2y: offsets must end at Nx / Ny");
   const X2YLayout L = x2y_layout(Nx, xdim, Ny, ydim, Hd);
   const float* xk = saved + L.xk;
   const float* xv = saved + L.xv;
@@ -690,50 +735,55 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
   const int cw = ydim + Hd;
   float* dcat = workspace;
   float* dL = dcat + (long long)Ny * cw;
-  float* dxv = dL + (long long)Ny * Nx;
+  float* dxv = dL + V.a[V.n];
   float* dxk = dxv + (long long)Nx * Hd;
   float* dyq = dxk + (long long)Nx * Hd;
   float* dXk = dyq + (long long)Ny * Hd;
   float* dYq = dXk + (long long)Nx * xdim;
   float* spl = dYq + (long long)Ny * ydim;
-  float* csw = spl + x2y_split_ws(Nx, xdim, Ny, ydim, Hd, outdim);
   const float scale = 1.0f / std::sqrt((float)Hd);
   // Y_W: dcat = dout . Wy, dWy = dout^T [Y, feat], dby
   FX_TRY(linear_dx(dout, lddo, wy, Ny, cw, outdim, dcat, cw, 0, nullptr, 0, spl, s));
-  (void)csw;
   FX_TRY(linear_dwdb(dout, lddo, Y, ldy, Ny, ydim, outdim, dwy, dby, 1, spl, s, cw));
   FX_TRY(linear_dw(dout, lddo, feat, Hd, Ny, Hd, outdim, dwy + ydim, 1, spl, s, cw));
-  const float* dfeat = dcat + ydim;
-  // dP = dfeat . xv^T (+ dattn) ; dxv = attn^T . dfeat
-  {
-    fx_gemm_desc d = gemm_desc(Ny, Nx, Hd, op_rows(dfeat, cw), op_rows(xv, Hd), dL, Nx);
-    d.resid = dattn;
-    d.ld_resid = Nx;
-    d.split_k = pick_split(Ny, Nx, Hd);
-    d.workspace = spl;
-    FX_TRY(launch_gemm(d, s));
-  }
-  {
-    fx_gemm_desc d = gemm_desc(Nx, Hd, Ny, op_cols(attn, Nx), op_cols(dfeat, cw), dxv, Hd);
-    d.split_k = pick_split(Nx, Hd, Ny);
-    d.workspace = spl;
-    FX_TRY(launch_gemm(d, s));
-  }
-  // dlogit = softmax_bwd(attn, dP) + dlogit_direct   (in place)
-  FX_TRY(launch_softmax_rows_bwd(attn, Nx, dL, Nx, dlogit, Nx, Ny, Nx, 1.f, dL, Nx, s));
-  {
-    fx_gemm_desc d = gemm_desc(Ny, Hd, Nx, op_rows(dL, Nx), op_cols(xk, Hd), dyq, Hd);
-    d.alpha = scale;
-    d.split_k = pick_split(Ny, Hd, Nx);
-    d.workspace = spl;
-    FX_TRY(launch_gemm(d, s));
-  }
-  {
-    fx_gemm_desc d = gemm_desc(Nx, Hd, Ny, op_cols(dL, Nx), op_cols(yq, Hd), dxk, Hd);
-    d.alpha = scale;
-    d.split_k = pick_split(Nx, Hd, Ny);
-    d.workspace = spl;
-    FX_TRY(launch_gemm(d, s));
+  for (int v = 0; v < V.n; ++v) {
+    const int nx = V.x[v + 1] - V.x[v], ny = V.y[v + 1] - V.y[v];
+    if (nx == 0 || ny == 0) continue;
+    const float* dfeat = dcat + (long long)V.y[v] * cw + ydim;
+    const float* at = attn + V.a[v];
+    float* dl = dL + V.a[v];
+    const long long xr = (long long)V.x[v] * Hd, yr = (long long)V.y[v] * Hd;
+    // dP = dfeat . xv^T (+ dattn) ; dxv = attn^T . dfeat
+    {
+      fx_gemm_desc d = gemm_desc(ny, nx, Hd, op_rows(dfeat, cw), op_rows(xv + xr, Hd), dl, nx);
+      d.resid = dattn ? dattn + V.a[v] : nullptr;
+      d.ld_resid = nx;
+      d.split_k = pick_split(ny, nx, Hd);
+      d.workspace = spl;
+      FX_TRY(launch_gemm(d, s));
+    }
+    {
+      fx_gemm_desc d = gemm_desc(nx, Hd, ny, op_cols(at, nx), op_cols(dfeat, cw), dxv + xr, Hd);
+      d.split_k = pick_split(nx, Hd, ny);
+      d.workspace = spl;
+      FX_TRY(launch_gemm(d, s));
+    }
+    // dlogit = softmax_bwd(attn, dP) + dlogit_direct   (in place)
+    FX_TRY(launch_softmax_rows_bwd(at, nx, dl, nx, dlogit ? dlogit + V.a[v] : nullptr, nx, ny, nx, 1.f, dl, nx, s));
+    {
+      fx_gemm_desc d = gemm_desc(ny, Hd, nx, op_rows(dl, nx), op_cols(xk + xr, Hd), dyq + yr, Hd);
+      d.alpha = scale;
+      d.split_k = pick_split(ny, Hd, nx);
+      d.workspace = spl;
+      FX_TRY(launch_gemm(d, s));
+    }
+    {
+      fx_gemm_desc d = gemm_desc(nx, Hd, ny, op_cols(dl, nx), op_cols(yq + yr, Hd), dxk + xr, Hd);
+      d.alpha = scale;
+      d.split_k = pick_split(nx, Hd, ny);
+      d.workspace = spl;
+      FX_TRY(launch_gemm(d, s));
+    }
   }
   // projections
   FX_TRY(linear_dwdb(dxk, Hd, xin, ldxin, Nx, xdim, Hd, dwk, dbk, 1, spl, s));
@@ -772,42 +822,54 @@ static long long gru_split_ws(int S, int In, int Hh) {
 }
 
 // fwd: [sync area][gi (S, 6Hh)];  bwd: [dgi (S, 6Hh)][dgh 2 x (S, 3Hh)][split-K][colsum][sync area]
-long long fx_gru_workspace_floats(int S, int In, int Hh) {
+long long fx_gru_workspace_floats(int S, int nseq, int In, int Hh) {
   const long long H3 = 3LL * Hh;
-  long long fwd = gru_sync_floats(Hh) + S * 2 * H3;
+  long long fwd = gru_sync_floats(Hh, nseq) + S * 2 * H3;
   long long sp = gru_split_ws(S, In, Hh);
-  long long bwd = S * 2 * H3 + 2 * S * H3 + sp + colsum_workspace_floats(S, 3 * Hh) + gru_sync_floats(Hh);
+  long long bwd = S * 2 * H3 + 2 * S * H3 + sp + colsum_workspace_floats(S, 3 * Hh) + gru_sync_floats(Hh, nseq);
   return std::max(fwd, bwd);
 }
 
-int fx_gru_bidir_fwd(const float* x, long long ldx, int S, int In, int Hh, const float* w_ih_f, const float* w_hh_f,
-                     const float* b_ih_f, const float* b_hh_f, const float* w_ih_r, const float* w_hh_r,
-                     const float* b_ih_r, const float* b_hh_r, float* out, long long ldo, float* saved,
-                     float* workspace, void* stream) {
+static std::vector<int> seq_offsets(int S, int nseq, const int* seq_off) {
+  if (nseq <= 1 || !seq_off) return {0, S};
+  return std::vector<int>(seq_off, seq_off + nseq + 1);
+}
+
+int fx_gru_bidir_fwd(const float* x, long long ldx, int S, int nseq, const int* seq_off, int In, int Hh,
+                     const float* w_ih_f, const float* w_hh_f, const float* b_ih_f, const float* b_hh_f,
+                     const float* w_ih_r, const float* w_hh_r, const float* b_ih_r, const float* b_hh_r, float* out,
+                     long long ldo, float* saved, float* workspace, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int H3 = 3 * Hh;
-  float* gi = workspace + gru_sync_floats(Hh);
+  const std::vector<int> off = seq_offsets(S, nseq, seq_off);
+  const int nq = (int)off.size() - 1;
+  FX_REQUIRE(off.back() == S && off.front() == 0, "gru: sequence offsets must span [0, S]");
+  float* gi = workspace + gru_sync_floats(Hh, nq);
   // input projections of every step, both directions: gi[:, d*3Hh:(d+1)*3Hh] = x W_ih_d^T + b_ih_d
   FX_TRY(linear_fwd(x, ldx, S, In, w_ih_f, b_ih_f, gi, 2 * H3, H3, 0, s));
   FX_TRY(linear_fwd(x, ldx, S, In, w_ih_r, b_ih_r, gi + H3, 2 * H3, H3, 0, s));
   const float* whh[2] = {w_hh_f, w_hh_r};
   const float* bhh[2] = {b_hh_f, b_hh_r};
-  return launch_gru_fwd(gi, 2 * H3, S, Hh, whh, bhh, out, ldo, saved, workspace, s);
+  return launch_gru_fwd(gi, 2 * H3, nq, off.data(), Hh, whh, bhh, out, ldo, saved, workspace, s);
 }
 
-int fx_gru_bidir_bwd(const float* x, long long ldx, int S, int In, int Hh, const float* w_ih_f, const float* w_hh_f,
-                     const float* w_ih_r, const float* w_hh_r, const float* saved, const float* dout, long long lddo,
-                     float* dx, long long lddx, float* dw_ih_f, float* dw_hh_f, float* db_ih_f, float* db_hh_f,
-                     float* dw_ih_r, float* dw_hh_r, float* db_ih_r, float* db_hh_r, float* workspace, void* stream) {
+int fx_gru_bidir_bwd(const float* x, long long ldx, int S, int nseq, const int* seq_off, int In, int Hh,
+                     const float* w_ih_f, const float* w_hh_f, const float* w_ih_r, const float* w_hh_r,
+                     const float* saved, const float* dout, long long lddo, float* dx, long long lddx, float* dw_ih_f,
+                     float* dw_hh_f, float* db_ih_f, float* db_hh_f, float* dw_ih_r, float* dw_hh_r, float* db_ih_r,
+                     float* db_hh_r, float* workspace, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int H3 = 3 * Hh;
+  const std::vector<int> off = seq_offsets(S, nseq, seq_off);
+  const int nq = (int)off.size() - 1;
+  FX_REQUIRE(off.back() == S && off.front() == 0, "gru: sequence offsets must span [0, S]");
   float* dgi = workspace;                          // (S, 6Hh)
   float* dgh = dgi + (long long)S * 2 * H3;        // 2 x (S, 3Hh)
   float* spl = dgh + 2LL * S * H3;
   float* csw = spl + gru_split_ws(S, In, Hh);
   float* sync_ws = csw + colsum_workspace_floats(S, 3 * Hh);
   const float* whh[2] = {w_hh_f, w_hh_r};
-  FX_TRY(launch_gru_bwd(dout, lddo, S, Hh, whh, saved, dgi, 2 * H3, dgh, sync_ws, s));
+  FX_TRY(launch_gru_bwd(dout, lddo, nq, off.data(), Hh, whh, saved, dgi, 2 * H3, dgh, sync_ws, s));
   const float* wih[2] = {w_ih_f, w_ih_r};
   float* dwih[2] = {dw_ih_f, dw_ih_r};
   float* dwhh[2] = {dw_hh_f, dw_hh_r};
@@ -827,9 +889,17 @@ int fx_gru_bidir_bwd(const float* x, long long ldx, int S, int In, int Hh, const
 }
 
 // ---------------------------------------------------------------- segments
-int fx_segments_from_probs(const float* x, long long ldx, int col0, int ncls, int T, int32_t* pred, int32_t* seg_id,
-                           int32_t* seg_start, int32_t* seg_end, int32_t* num_seg, void* stream) {
-  return launch_segments(x, ldx, col0, ncls, T, pred, seg_id, seg_start, seg_end, num_seg, (hipStream_t)stream);
+int fx_segments_from_probs(const float* x, long long ldx, int col0, int ncls, int T, int nvid, int32_t* pred,
+                           int32_t* seg_id, int32_t* seg_start, int32_t* seg_end, int32_t* num_seg, void* stream) {
+  return launch_segments(x, ldx, col0, ncls, T, nvid, pred, seg_id, seg_start, seg_end, num_seg, (hipStream_t)stream);
+}
+
+int fx_segments_globalize(int nvid, int T, const int32_t* num_seg_host, const int32_t* seg_id,
+                          const int32_t* seg_start, const int32_t* seg_end, int32_t* gseg_id, int32_t* gstart,
+                          int32_t* gend, void* stream) {
+  FX_REQUIRE(nvid >= 1 && T > 0 && num_seg_host, "segments_globalize: bad arguments");
+  return launch_seg_globalize(nvid, T, num_seg_host, seg_id, seg_start, seg_end, gseg_id, gstart, gend,
+                              (hipStream_t)stream);
 }
 
 int fx_seg_mean_fwd(const float* x, long long ldx, const int32_t* seg_start, const int32_t* seg_end, int S, int cols,

@@ -132,13 +132,14 @@ long long dec_split_ws(const fx_decoder_params* p, int R, int T) {
   return sp;
 }
 
-DecLayout dec_layout(const fx_decoder_params* p, int R, int T, int has_qpos, int has_mpos) {
+DecLayout dec_layout(const fx_decoder_params* p, int R, int T, int has_qpos, int has_mpos, int nvid) {
   DecLayout L{};
   const long long A = p->A, FF = p->FF, h = p->nhead, RA = (long long)R * A;
+  const long long Qv = R / nvid, Tv = T / nvid;   // tokens / frames per video
   long long o = 0;
   L.xq = o; o += has_qpos ? RA : 0;
   L.qkv = o; o += 3 * RA;
-  L.psa = o; o += h * R * R;
+  L.psa = o; o += nvid * h * Qv * Qv;
   L.osa = o; o += RA;
   L.xh1 = o; o += RA;
   L.rs1 = o; o += R;
@@ -146,7 +147,7 @@ DecLayout dec_layout(const fx_decoder_params* p, int R, int T, int has_qpos, int
   if (p->cross) {
     L.t1q = o; o += has_qpos ? RA : 0;
     L.qc = o; o += RA;
-    L.pca = o; o += h * R * T;
+    L.pca = o; o += nvid * h * Qv * Tv;
     L.oca = o; o += RA;
     L.xh2 = o; o += RA;
     L.rs2 = o; o += R;
@@ -171,7 +172,7 @@ DecLayout dec_layout(const fx_decoder_params* p, int R, int T, int has_qpos, int
   o = 0;
   L.wkv = o; o += p->cross ? AL2 * p->Hm : 0;
   L.bkv = o; o += p->cross ? AL2 : 0;
-  L.wsp = o; o += std::max(sp, p->cross ? fx_mha_core_workspace_floats(R, T, (int)A, (int)h) : 0LL) + RA;
+  L.wsp = o; o += std::max(sp, p->cross ? fx_mha_core_workspace_floats((int)Qv, (int)Tv, (int)A, (int)h) : 0LL) + RA;
   L.total_ws_fwd = o;
   // backward workspace
   o = 0;
@@ -188,17 +189,21 @@ DecLayout dec_layout(const fx_decoder_params* p, int R, int T, int has_qpos, int
   L.G = o; o += RA;
   L.P = o; o += RA;
   L.lnws = o; o += layernorm_bwd_ws_floats(R, (int)A);
-  L.core = o; o += p->cross ? fx_mha_core_workspace_floats(R, T, (int)A, (int)h) : 0;
+  L.core = o; o += p->cross ? fx_mha_core_workspace_floats((int)Qv, (int)Tv, (int)A, (int)h) : 0;
   L.split = o; o += sp;
   L.total_ws_bwd = o;
   (void)FF;
   return L;
 }
 
-int dec_check(const fx_decoder_params* p, int R, int T) {
+int dec_check(const fx_decoder_params* p, int R, int T, int nvid) {
   FX_REQUIRE(p && p->num_layers >= 1 && p->num_layers <= MAXL, "decoder: 1..16 layers");
+  FX_REQUIRE(nvid >= 1 && R % nvid == 0 && (!p->cross || T % nvid == 0),
+             "decoder: token and memory rows must split evenly over the videos");
+  R /= nvid;
+  T /= nvid;
   FX_REQUIRE(p->nhead > 0 && p->A % p->nhead == 0, "decoder: A must be divisible by nhead");
-  FX_REQUIRE(R >= 1 && R <= 64, "decoder: 1..64 tokens (fused self-attention core)");
+  FX_REQUIRE(R >= 1 && R <= 64, "decoder: 1..64 tokens per video (fused self-attention core)");
   FX_REQUIRE(p->A / p->nhead <= 64, "decoder: head dim must be <= 64");
   FX_REQUIRE(p->A <= 1024, "decoder: A <= 1024 (LayerNorm row kernel)");
   FX_REQUIRE(!p->cross || (T >= 1 && p->Hm > 0), "decoder: cross attention needs memory rows");
@@ -212,25 +217,27 @@ using namespace fx;
 
 extern "C" {
 
-long long fx_decoder_saved_floats(const fx_decoder_params* p, int R, int T, int has_qpos, int has_mpos) {
-  return dec_layout(p, R, T, has_qpos, has_mpos).total_saved;
+long long fx_decoder_saved_floats(const fx_decoder_params* p, int R, int T, int nvid, int has_qpos, int has_mpos) {
+  return dec_layout(p, R, T, has_qpos, has_mpos, std::max(nvid, 1)).total_saved;
 }
 
-long long fx_decoder_workspace_floats(const fx_decoder_params* p, int R, int T, int has_qpos, int has_mpos) {
-  const DecLayout L = dec_layout(p, R, T, has_qpos, has_mpos);
+long long fx_decoder_workspace_floats(const fx_decoder_params* p, int R, int T, int nvid, int has_qpos,
+                                      int has_mpos) {
+  const DecLayout L = dec_layout(p, R, T, has_qpos, has_mpos, std::max(nvid, 1));
   return std::max(L.total_ws_fwd, L.total_ws_bwd);
 }
 
 int fx_decoder_fwd(const fx_decoder_params* p, const float* tgt, long long ldt, int R, const float* qpos,
-                   long long ldqp, const float* mem, long long ldm, int T, const float* mpos, long long ldmp,
+                   long long ldqp, const float* mem, long long ldm, int T, int nvid, const float* mpos, long long ldmp,
                    float* out, long long ldo, float* saved, float* workspace, void* stream) {
-  FX_TRY(dec_check(p, R, T));
+  FX_TRY(dec_check(p, R, T, nvid));
+  const int Qv = R / nvid, Tv = T / nvid;
   hipStream_t s = (hipStream_t)stream;
   const int A = p->A, FF = p->FF, h = p->nhead, hd = A / h, NL = p->num_layers;
   const long long RA = (long long)R * A;
   const float eps = p->eps > 0.f ? p->eps : 1e-5f;
   const float scale = 1.0f / std::sqrt((float)hd);
-  const DecLayout L = dec_layout(p, R, T, qpos != nullptr, mpos != nullptr);
+  const DecLayout L = dec_layout(p, R, T, qpos != nullptr, mpos != nullptr, nvid);
   FX_REQUIRE(!qpos || ldqp == A, "decoder: query_pos must be dense (R, A)");
   float* spl = workspace + L.wsp;
   const int AL2 = 2 * A * NL;
@@ -286,8 +293,8 @@ int fx_decoder_fwd(const fx_decoder_params* p, const float* tgt, long long ldt, 
       FX_TRY(linear_fwd(x, ldx, R, A, p->sa_in_w[l] + 2LL * A * A, p->sa_in_b[l] + 2 * A, qkv + 2 * A, 3 * A, A, 0,
                         s));
     }
-    FX_TRY(launch_mha_small_fwd(qkv, 3 * A, qkv + A, 3 * A, qkv + 2 * A, 3 * A, R, R, hd, h, scale, b + L.psa,
-                                b + L.osa, A, s));
+    FX_TRY(launch_mha_small_fwd(qkv, 3 * A, qkv + A, 3 * A, qkv + 2 * A, 3 * A, Qv, Qv, hd, h, scale, b + L.psa,
+                                b + L.osa, A, s, nvid));
     // t1 = LN(x + out_proj(o))
     float* u = spl + (std::max(L.total_ws_fwd - L.wsp, RA) - RA);   // last RA floats of the scratch
     FX_TRY(linear_fwd_res(b + L.osa, A, R, A, p->sa_out_w[l], A, p->sa_out_b[l], x, ldx, u, A, A, s));
@@ -302,8 +309,12 @@ int fx_decoder_fwd(const fx_decoder_params* p, const float* tgt, long long ldt, 
         tq = b + L.t1q;
       }
       FX_TRY(linear_fwd(tq, A, R, A, p->ca_q_w[l], p->ca_in_b[l], b + L.qc, A, A, 0, s));
-      FX_TRY(fx_mha_core_fwd(b + L.qc, A, kv + (long long)l * A, AL2, kv + (long long)(NL + l) * A, AL2, R, T, A, h,
-                             b + L.pca, b + L.oca, A, spl, s));
+      for (int v = 0; v < nvid; ++v) {   // each video's tokens attend to its own frames
+        const long long kr = (long long)v * Tv * AL2;
+        FX_TRY(fx_mha_core_fwd(b + L.qc + (long long)v * Qv * A, A, kv + kr + (long long)l * A, AL2,
+                               kv + kr + (long long)(NL + l) * A, AL2, Qv, Tv, A, h,
+                               b + L.pca + (long long)v * h * Qv * Tv, b + L.oca + (long long)v * Qv * A, A, spl, s));
+      }
       FX_TRY(linear_fwd_res(b + L.oca, A, R, A, p->ca_out_w[l], A, p->ca_out_b[l], b + L.t1, A, u, A, A, s));
       FX_TRY(launch_layernorm_fwd(u, A, nullptr, 0, p->ln_ca_w[l], p->ln_ca_b[l], eps, R, A, 0, b + L.t2, A,
                                   nullptr, b + L.rs2, b + L.xh2, A, s));
@@ -327,16 +338,17 @@ int fx_decoder_fwd(const fx_decoder_params* p, const float* tgt, long long ldt, 
 }
 
 int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const float* tgt, long long ldt, int R,
-                   const float* qpos, const float* mem, long long ldm, int T, const float* mpos, long long ldmp,
-                   const float* dout, long long lddo, float* dtgt, long long lddt, float* dqpos, float* dmem,
-                   long long lddm, float* dmpos, long long lddmp, const float* saved, float* workspace,
+                   const float* qpos, const float* mem, long long ldm, int T, int nvid, const float* mpos,
+                   long long ldmp, const float* dout, long long lddo, float* dtgt, long long lddt, float* dqpos,
+                   float* dmem, long long lddm, float* dmpos, long long lddmp, const float* saved, float* workspace,
                    void* stream) {
-  FX_TRY(dec_check(p, R, T));
+  FX_TRY(dec_check(p, R, T, nvid));
+  const int Qv = R / nvid, Tv = T / nvid;
   hipStream_t s = (hipStream_t)stream;
   const int A = p->A, FF = p->FF, h = p->nhead, hd = A / h, NL = p->num_layers;
   const long long RA = (long long)R * A;
   const float scale = 1.0f / std::sqrt((float)hd);
-  const DecLayout L = dec_layout(p, R, T, qpos != nullptr, mpos != nullptr);
+  const DecLayout L = dec_layout(p, R, T, qpos != nullptr, mpos != nullptr, nvid);
   const int AL2 = 2 * A * NL;
   float* ws = workspace;
   float* spl = ws + L.split;
@@ -381,9 +393,13 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
       FX_TRY(linear_dwdb(dU, A, b + L.oca, A, R, A, A, g->ca_out_w[l], g->ca_out_b[l], 1, spl, s));
       FX_TRY(linear_dx(dU, A, p->ca_out_w[l], R, A, A, dO, A, 0, nullptr, 0, spl, s));
       const float* kv = saved + L.kv;
-      FX_TRY(fx_mha_core_bwd(b + L.qc, A, kv + (long long)l * A, AL2, kv + (long long)(NL + l) * A, AL2, b + L.pca,
-                             dO, A, R, T, A, h, dq, A, dkv + (long long)l * A, AL2, dkv + (long long)(NL + l) * A,
-                             AL2, ws + L.core, s));
+      for (int v = 0; v < nvid; ++v) {
+        const long long kr = (long long)v * Tv * AL2, qr = (long long)v * Qv * A;
+        FX_TRY(fx_mha_core_bwd(b + L.qc + qr, A, kv + kr + (long long)l * A, AL2, kv + kr + (long long)(NL + l) * A,
+                               AL2, b + L.pca + (long long)v * h * Qv * Tv, dO + qr, A, Qv, Tv, A, h, dq + qr, A,
+                               dkv + kr + (long long)l * A, AL2, dkv + kr + (long long)(NL + l) * A, AL2, ws + L.core,
+                               s));
+      }
       const float* tq = qpos ? b + L.t1q : b + L.t1;
       FX_TRY(linear_dwdb(dq, A, tq, A, R, A, A, g->ca_q_w[l], g->ca_in_b[l], 1, spl, s));
       if (qpos) {
@@ -399,8 +415,8 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
     FX_TRY(linear_dwdb(dU, A, b + L.osa, A, R, A, A, g->sa_out_w[l], g->sa_out_b[l], 1, spl, s));
     FX_TRY(linear_dx(dU, A, p->sa_out_w[l], R, A, A, dO, A, 0, nullptr, 0, spl, s));
     const float* qkv = b + L.qkv;
-    FX_TRY(launch_mha_small_bwd(qkv, 3 * A, qkv + A, 3 * A, qkv + 2 * A, 3 * A, b + L.psa, dO, A, R, R, hd, h, scale,
-                                dQKV, 3 * A, dQKV + A, 3 * A, dQKV + 2 * A, 3 * A, s));
+    FX_TRY(launch_mha_small_bwd(qkv, 3 * A, qkv + A, 3 * A, qkv + 2 * A, 3 * A, b + L.psa, dO, A, Qv, Qv, hd, h, scale,
+                                dQKV, 3 * A, dQKV + A, 3 * A, dQKV + 2 * A, 3 * A, s, nvid));
     float* dX = l == 0 ? nullptr : dT;   // the next (earlier) layer's output gradient, in place
     if (!qpos) {
       FX_TRY(linear_dwdb(dQKV, 3 * A, x, ldx, R, A, 3 * A, g->sa_in_w[l], g->sa_in_b[l], 1, spl, s));

@@ -12,6 +12,8 @@
 //         dgi  = [dr_p, dz_p, dn_p];  dgh = [dr_p, dz_p, dn_p * r]
 //         dh_rec = dh z + W_hh^T dgh  (thread = hidden unit k, W_hh stored [row][k]: coalesced)
 // Weight/bias/input gradients are GEMMs over the saved per-step tables.
+#include <algorithm>
+
 #include "fx_common.h"
 
 namespace fx {
@@ -76,6 +78,8 @@ __device__ __forceinline__ bool gather_granules(unsigned long long* g, int n, un
   return true;
 }
 
+constexpr int MAXSEQ = 32;      // sequences per launch (more are launched in chunks)
+
 struct GruDirArgs {
   const float* gi;     // (S, 3Hh) for this direction, ld = ldgi
   long long ldgi;
@@ -85,19 +89,25 @@ struct GruDirArgs {
   long long ldo;
   float* hprev;        // (S, Hh) h_{t-1} per step
   float* gates;        // (S, 4Hh): r, z, n, gh_n
-  unsigned long long* gran;   // 2 slots x Hh granules
-  int S, Hh, reverse;
+  int Hh, reverse;
 };
 
+// sequence sq of the launch owns rows [off[sq], off[sq+1]) of every table; its direction d uses the
+// granule slots gran + ((sq * 2 + d) * 2 + slot) * G
 struct GruArgs {
   GruDirArgs d[2];
+  unsigned long long* gran;
   unsigned* tmo;
+  int off[MAXSEQ + 1];
 };
 
 __global__ __launch_bounds__(GT) void gru_fwd_kernel(GruArgs args) {
-  const int dir = blockIdx.x / NW, j = blockIdx.x - dir * NW;
+  const int sq = blockIdx.x / (2 * NW), rem = blockIdx.x - sq * 2 * NW;
+  const int dir = rem / NW, j = rem - dir * NW;
   const GruDirArgs& a = args.d[dir];
   const int Hh = a.Hh, tid = threadIdx.x, lane = tid & 63;
+  const int r0 = args.off[sq], S = args.off[sq + 1] - r0;
+  unsigned long long* gran = args.gran + (long long)(sq * 2 + dir) * 2 * Hh;
   const int U = (Hh + NW - 1) / NW, u0 = j * U;
   __shared__ float h[256];
   __shared__ float gh[3 * MAXU];
@@ -117,8 +127,8 @@ __global__ __launch_bounds__(GT) void gru_fwd_kernel(GruArgs args) {
   const float bias = act ? a.bhh[row] : 0.f;
   for (int k = tid; k < 256; k += GT) h[k] = 0.f;
   __syncthreads();
-  for (int s = 0; s < a.S; ++s) {
-    const int t = a.reverse ? a.S - 1 - s : s;
+  for (int s = 0; s < S; ++s) {
+    const int t = r0 + (a.reverse ? S - 1 - s : s);
     float acc = 0.f;
 #pragma unroll
     for (int i = 0; i < KCH; ++i) acc = fmaf(w[i], h[c * KCH + i], acc);
@@ -141,11 +151,11 @@ __global__ __launch_bounds__(GT) void gru_fwd_kernel(GruArgs args) {
       gs[Hh + u] = z;
       gs[2 * Hh + u] = n;
       gs[3 * Hh + u] = gh[2 * U + tid];
-      put_granule(a.gran + (long long)(s & 1) * Hh + u, (unsigned)(s + 1), hn);
+      put_granule(gran + (long long)(s & 1) * Hh + u, (unsigned)(s + 1), hn);
     }
     __syncthreads();   // every wave is done with the old h
-    if (s + 1 < a.S && tid < 64 &&
-        !gather_granules(a.gran + (long long)(s & 1) * Hh, Hh, (unsigned)(s + 1), h, args.tmo, lane))
+    if (s + 1 < S && tid < 64 &&
+        !gather_granules(gran + (long long)(s & 1) * Hh, Hh, (unsigned)(s + 1), h, args.tmo, lane))
       dead = 1;
     __syncthreads();
     if (dead) break;
@@ -161,19 +171,23 @@ struct GruBwdDirArgs {
   float* dgi;          // (S, 3Hh) ld lddgi
   long long lddgi;
   float* dgh;          // (S, 3Hh)
-  unsigned long long* gran;   // 2 slots x 3Hh granules
-  int S, Hh, reverse;
+  int Hh, reverse;
 };
 
 struct GruBwdArgs {
   GruBwdDirArgs d[2];
+  unsigned long long* gran;
   unsigned* tmo;
+  int off[MAXSEQ + 1];
 };
 
 __global__ __launch_bounds__(GT) void gru_bwd_kernel(GruBwdArgs args) {
-  const int dir = blockIdx.x / NW, j = blockIdx.x - dir * NW;
+  const int sq = blockIdx.x / (2 * NW), rem = blockIdx.x - sq * 2 * NW;
+  const int dir = rem / NW, j = rem - dir * NW;
   const GruBwdDirArgs& a = args.d[dir];
   const int Hh = a.Hh, H3 = 3 * Hh, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int r0 = args.off[sq], S = args.off[sq + 1] - r0;
+  unsigned long long* gran = args.gran + (long long)(sq * 2 + dir) * 2 * H3;
   const int U = (Hh + NW - 1) / NW, u0 = j * U;
   __shared__ float dg[768];
   __shared__ float dh[MAXU], dhd[MAXU];
@@ -191,9 +205,9 @@ __global__ __launch_bounds__(GT) void gru_bwd_kernel(GruBwdArgs args) {
   }
   if (tid < MAXU) dh[tid] = 0.f;
   __syncthreads();
-  for (int s = 0; s < a.S; ++s) {
-    const int t = a.reverse ? s : a.S - 1 - s;   // reverse of the forward visiting order
-    unsigned long long* slot = a.gran + (long long)(s & 1) * H3;
+  for (int s = 0; s < S; ++s) {
+    const int t = r0 + (a.reverse ? s : S - 1 - s);   // reverse of the forward visiting order
+    unsigned long long* slot = gran + (long long)(s & 1) * H3;
     if (tid < U && u0 + tid < Hh) {
       const int u = u0 + tid;
       const float* gs = a.gates + (long long)t * 4 * Hh;
@@ -216,7 +230,7 @@ __global__ __launch_bounds__(GT) void gru_bwd_kernel(GruBwdArgs args) {
       put_granule(slot + 2 * Hh + u, (unsigned)(s + 1), dnp * r);
       dhd[tid] = d * z;   // direct path; W^T dgh added below
     }
-    if (s + 1 == a.S) break;   // the last step's recurrent gradient feeds nothing
+    if (s + 1 == S) break;   // the last step's recurrent gradient feeds nothing
     if (tid < 64 && !gather_granules(slot, H3, (unsigned)(s + 1), dg, args.tmo, lane)) dead = 1;
     __syncthreads();
     if (dead) break;
@@ -237,66 +251,74 @@ __global__ __launch_bounds__(GT) void gru_bwd_kernel(GruBwdArgs args) {
 
 }  // namespace
 
-// floats of the per-call sync area: timeout word (padded to 16 B) + 2 dirs x 2 slots x 3Hh granules
-long long gru_sync_floats(int Hh) { return 4 + 2LL * 2 * 2 * 3 * Hh; }
+// floats of the per-call sync area for nseq sequences: timeout word (padded to 16 B) +
+// per sequence 2 dirs x 2 slots x 3Hh granules (8 B each)
+long long gru_sync_floats(int Hh, int nseq) { return 4 + (long long)std::max(nseq, 1) * 2 * 2 * 3 * Hh * 2; }
 
-int launch_gru_fwd(const float* gi, long long ldgi, int S, int Hh, const float* const whh[2], const float* const bhh[2],
-                   float* out, long long ldo, float* saved, float* ws, hipStream_t s) {
+int launch_gru_fwd(const float* gi, long long ldgi, int nseq, const int* seq_off, int Hh, const float* const whh[2],
+                   const float* const bhh[2], float* out, long long ldo, float* saved, float* ws, hipStream_t s) {
   FX_REQUIRE(Hh > 0 && Hh <= NW * MAXU, "gru: hidden size per direction must be <= 256");
-  if (S == 0) return FX_OK;
-  // ws: [timeout word (4 floats)] [2 dirs x 2 slots x Hh granules]; zeroed every call
+  const int Stot = seq_off[nseq];
+  if (Stot == 0) return FX_OK;
   unsigned* tmo = reinterpret_cast<unsigned*>(ws);
   unsigned long long* gran = reinterpret_cast<unsigned long long*>(ws + 4);
-  FX_CHECK_HIP(hipMemsetAsync(ws, 0, sizeof(float) * gru_sync_floats(Hh), s));
-  GruArgs args{};
-  args.tmo = tmo;
-  for (int d = 0; d < 2; ++d) {
-    GruDirArgs& a = args.d[d];
-    a.gi = gi + d * 3 * Hh;
-    a.ldgi = ldgi;
-    a.whh = whh[d];
-    a.bhh = bhh[d];
-    a.out = out + d * Hh;
-    a.ldo = ldo;
-    a.hprev = saved + (long long)d * S * Hh;
-    a.gates = saved + 2LL * S * Hh + (long long)d * S * 4 * Hh;
-    a.gran = gran + (long long)d * 2 * Hh;
-    a.S = S;
-    a.Hh = Hh;
-    a.reverse = d;
+  FX_CHECK_HIP(hipMemsetAsync(ws, 0, sizeof(float) * gru_sync_floats(Hh, nseq), s));
+  for (int c0 = 0; c0 < nseq; c0 += MAXSEQ) {
+    const int nc = std::min(MAXSEQ, nseq - c0);
+    GruArgs args{};
+    args.tmo = tmo;
+    args.gran = gran + (long long)c0 * 2 * 2 * 3 * Hh;
+    for (int q = 0; q <= nc; ++q) args.off[q] = seq_off[c0 + q];
+    for (int d = 0; d < 2; ++d) {
+      GruDirArgs& a = args.d[d];
+      a.gi = gi + d * 3 * Hh;
+      a.ldgi = ldgi;
+      a.whh = whh[d];
+      a.bhh = bhh[d];
+      a.out = out + d * Hh;
+      a.ldo = ldo;
+      a.hprev = saved + (long long)d * Stot * Hh;
+      a.gates = saved + 2LL * Stot * Hh + (long long)d * Stot * 4 * Hh;
+      a.Hh = Hh;
+      a.reverse = d;
+    }
+    hipLaunchKernelGGL(gru_fwd_kernel, dim3(nc * 2 * NW), dim3(GT), 0, s, args);
+    FX_CHECK_HIP(hipGetLastError());
   }
-  hipLaunchKernelGGL(gru_fwd_kernel, dim3(2 * NW), dim3(GT), 0, s, args);
-  FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }
 
-int launch_gru_bwd(const float* dout, long long lddo, int S, int Hh, const float* const whh[2], const float* saved,
-                   float* dgi, long long lddgi, float* dgh, float* sync_ws, hipStream_t s) {
+int launch_gru_bwd(const float* dout, long long lddo, int nseq, const int* seq_off, int Hh, const float* const whh[2],
+                   const float* saved, float* dgi, long long lddgi, float* dgh, float* sync_ws, hipStream_t s) {
   FX_REQUIRE(Hh > 0 && Hh <= NW * MAXU, "gru: hidden size per direction must be <= 256");
-  if (S == 0) return FX_OK;
+  const int Stot = seq_off[nseq];
+  if (Stot == 0) return FX_OK;
   const int H3 = 3 * Hh;
   unsigned* tmo = reinterpret_cast<unsigned*>(sync_ws);
   unsigned long long* gran = reinterpret_cast<unsigned long long*>(sync_ws + 4);
-  FX_CHECK_HIP(hipMemsetAsync(sync_ws, 0, sizeof(float) * gru_sync_floats(Hh), s));
-  GruBwdArgs args{};
-  args.tmo = tmo;
-  for (int d = 0; d < 2; ++d) {
-    GruBwdDirArgs& a = args.d[d];
-    a.dout = dout + d * Hh;
-    a.lddo = lddo;
-    a.whh = whh[d];
-    a.hprev = saved + (long long)d * S * Hh;
-    a.gates = saved + 2LL * S * Hh + (long long)d * S * 4 * Hh;
-    a.dgi = dgi + d * H3;
-    a.lddgi = lddgi;
-    a.dgh = dgh + (long long)d * S * H3;
-    a.gran = gran + (long long)d * 2 * H3;
-    a.S = S;
-    a.Hh = Hh;
-    a.reverse = d;
+  FX_CHECK_HIP(hipMemsetAsync(sync_ws, 0, sizeof(float) * gru_sync_floats(Hh, nseq), s));
+  for (int c0 = 0; c0 < nseq; c0 += MAXSEQ) {
+    const int nc = std::min(MAXSEQ, nseq - c0);
+    GruBwdArgs args{};
+    args.tmo = tmo;
+    args.gran = gran + (long long)c0 * 2 * 2 * H3;
+    for (int q = 0; q <= nc; ++q) args.off[q] = seq_off[c0 + q];
+    for (int d = 0; d < 2; ++d) {
+      GruBwdDirArgs& a = args.d[d];
+      a.dout = dout + d * Hh;
+      a.lddo = lddo;
+      a.whh = whh[d];
+      a.hprev = saved + (long long)d * Stot * Hh;
+      a.gates = saved + 2LL * Stot * Hh + (long long)d * Stot * 4 * Hh;
+      a.dgi = dgi + d * H3;
+      a.lddgi = lddgi;
+      a.dgh = dgh + (long long)d * Stot * H3;
+      a.Hh = Hh;
+      a.reverse = d;
+    }
+    hipLaunchKernelGGL(gru_bwd_kernel, dim3(nc * 2 * NW), dim3(GT), 0, s, args);
+    FX_CHECK_HIP(hipGetLastError());
   }
-  hipLaunchKernelGGL(gru_bwd_kernel, dim3(2 * NW), dim3(GT), 0, s, args);
-  FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }
 

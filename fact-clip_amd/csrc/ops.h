@@ -27,17 +27,20 @@ int launch_l2n_fwd(const float* x, long long ldx, int rows, int cols, float* y, 
                    hipStream_t s);
 int launch_l2n_bwd(const float* y, long long ldy, const float* nrm, const float* dy, long long lddy, int rows,
                    int cols, float* dx, long long lddx, hipStream_t s);
-int launch_segments(const float* x, long long ldx, int col0, int ncls, int T, int32_t* pred, int32_t* seg_id,
-                    int32_t* seg_start, int32_t* seg_end, int32_t* num_seg, hipStream_t s);
+int launch_segments(const float* x, long long ldx, int col0, int ncls, int T, int nvid, int32_t* pred,
+                    int32_t* seg_id, int32_t* seg_start, int32_t* seg_end, int32_t* num_seg, hipStream_t s);
+int launch_seg_globalize(int nvid, int T, const int32_t* num_seg_host, const int32_t* seg_id, const int32_t* st,
+                         const int32_t* en, int32_t* gseg_id, int32_t* gst, int32_t* gen, hipStream_t s);
 int launch_seg_reduce(const float* x, long long ldx, const int32_t* st, const int32_t* en, int S, int cols, int mean,
                       float* y, long long ldy, int accumulate, hipStream_t s);
 int launch_seg_mean_bwd(const float* dy, long long lddy, const int32_t* sid, const int32_t* st, const int32_t* en,
                         int T, int cols, float* dx, long long lddx, int accumulate, hipStream_t s);
-int launch_gru_fwd(const float* gi, long long ldgi, int S, int Hh, const float* const whh[2], const float* const bhh[2],
-                   float* out, long long ldo, float* saved, float* ws, hipStream_t s);
-long long gru_sync_floats(int Hh);
-int launch_gru_bwd(const float* dout, long long lddo, int S, int Hh, const float* const whh[2], const float* saved,
-                   float* dgi, long long lddgi, float* dgh, float* sync_ws, hipStream_t s);
+// nseq independent sequences stacked by rows: sequence q owns rows [seq_off[q], seq_off[q+1]) (host)
+int launch_gru_fwd(const float* gi, long long ldgi, int nseq, const int* seq_off, int Hh, const float* const whh[2],
+                   const float* const bhh[2], float* out, long long ldo, float* saved, float* ws, hipStream_t s);
+long long gru_sync_floats(int Hh, int nseq);
+int launch_gru_bwd(const float* dout, long long lddo, int nseq, const int* seq_off, int Hh, const float* const whh[2],
+                   const float* saved, float* dgi, long long lddgi, float* dgh, float* sync_ws, hipStream_t s);
 
 // ---- composite helpers (capi.cpp) --------------------------------------------
 int ew_grid(long long total);
@@ -63,14 +66,15 @@ int linear_dw(const float* dy, long long lddy, const float* x, long long ldx, in
 long long dwdb_ws(int M, int K, int N);
 
 // ---- fused small multi-head attention (attn_small.hip): Lq, Lk, head_dim <= 64 ----
-// probs (nhead, Lq, Lk) saved; o (Lq, nhead*hd) with row stride ldo.
+// nvid independent problems stacked by rows (video v: q/o rows v*Lq.., k/v rows v*Lk..);
+// probs (nvid, nhead, Lq, Lk) saved; o (Lq, nhead*hd) with row stride ldo.
 int launch_mha_small_fwd(const float* q, long long ldq, const float* k, long long ldk, const float* v,
                          long long ldv, int Lq, int Lk, int hd, int nhead, float scale, float* probs, float* o,
-                         long long ldo, hipStream_t s);
+                         long long ldo, hipStream_t s, int nvid = 1);
 // dq, dk, dv written (nullable) with their row strides
 int launch_mha_small_bwd(const float* q, long long ldq, const float* k, long long ldk, const float* v,
                          long long ldv, const float* probs, const float* dout, long long lddo, int Lq, int Lk, int hd,
                          int nhead, float scale, float* dq, long long lddq, float* dk, long long lddk, float* dv,
-                         long long lddv, hipStream_t s);
+                         long long lddv, hipStream_t s, int nvid = 1);
 
 }  // namespace fx

@@ -7,6 +7,8 @@
 // 1024-thread workgroup does the boundary scan and writes seg_id / starts /
 // ends / S; the host reads S once (the reference also synchronises here).
 // Segment pooling is a deterministic, frame-ordered sum per segment.
+#include <algorithm>
+
 #include "fx_common.h"
 
 namespace fx {
@@ -45,6 +47,13 @@ constexpr int SCAN_THREADS = 1024;
 __global__ __launch_bounds__(SCAN_THREADS) void boundary_scan_kernel(const int32_t* pred, int T, int32_t* seg_id,
                                                                      int32_t* seg_start, int32_t* seg_end,
                                                                      int32_t* num_seg) {
+  // one block per video: rows [v*T, (v+1)*T), video-local segment numbering and frame indices
+  const long long vo = (long long)blockIdx.x * T;
+  pred += vo;
+  seg_id += vo;
+  seg_start += vo;
+  seg_end += vo;
+  num_seg += blockIdx.x;
   __shared__ int32_t sums[SCAN_THREADS];
   const int tid = threadIdx.x;
   const int per = (T + SCAN_THREADS - 1) / SCAN_THREADS;
@@ -125,13 +134,67 @@ __global__ __launch_bounds__(256) void seg_mean_bwd_kernel(const float* dy, long
   *p = accumulate ? *p + v : v;
 }
 
+constexpr int MAXV = 32;
+struct GlobalizeArgs {
+  const int32_t* seg_id;  // (nvid*T) video-local ids
+  int32_t* gseg_id;       // (nvid*T) global ids
+  const int32_t* st;      // (nvid*T) local tables
+  const int32_t* en;
+  int32_t* gst;           // (sum S) global frame rows
+  int32_t* gen;
+  int T, nv;
+  int soff[MAXV + 1];     // segment prefix offsets of this chunk's videos
+  int v0;                 // first video of the chunk
+};
+
+__global__ __launch_bounds__(256) void seg_globalize_kernel(GlobalizeArgs a) {
+  const int v = blockIdx.y;
+  const int vg = a.v0 + v;
+  const int S = a.soff[v + 1] - a.soff[v];
+  const long long base = (long long)vg * a.T;
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < a.T; t += gridDim.x * 256) {
+    a.gseg_id[base + t] = a.seg_id[base + t] + a.soff[v];
+    if (t < S) {
+      a.gst[a.soff[v] + t] = a.st[base + t] + (int)base;
+      a.gen[a.soff[v] + t] = a.en[base + t] + (int)base;
+    }
+  }
+}
+
 }  // namespace
 
-int launch_segments(const float* x, long long ldx, int col0, int ncls, int T, int32_t* pred, int32_t* seg_id,
-                    int32_t* seg_start, int32_t* seg_end, int32_t* num_seg, hipStream_t s) {
+int launch_seg_globalize(int nvid, int T, const int32_t* num_seg_host, const int32_t* seg_id, const int32_t* st,
+                         const int32_t* en, int32_t* gseg_id, int32_t* gst, int32_t* gen, hipStream_t s) {
+  int off = 0;
+  for (int c0 = 0; c0 < nvid; c0 += MAXV) {
+    GlobalizeArgs a{};
+    a.seg_id = seg_id;
+    a.gseg_id = gseg_id;
+    a.st = st;
+    a.en = en;
+    a.gst = gst;
+    a.gen = gen;
+    a.T = T;
+    a.nv = std::min(MAXV, nvid - c0);
+    a.v0 = c0;
+    for (int v = 0; v < a.nv; ++v) {
+      a.soff[v] = off;
+      off += num_seg_host[c0 + v];
+    }
+    a.soff[a.nv] = off;
+    hipLaunchKernelGGL(seg_globalize_kernel, dim3(std::max(1, std::min(cdiv(T, 256), 64)), a.nv), dim3(256), 0, s, a);
+    FX_CHECK_HIP(hipGetLastError());
+  }
+  return FX_OK;
+}
+
+int launch_segments(const float* x, long long ldx, int col0, int ncls, int T, int nvid, int32_t* pred,
+                    int32_t* seg_id, int32_t* seg_start, int32_t* seg_end, int32_t* num_seg, hipStream_t s) {
   FX_REQUIRE(T > 0 && ncls > 0, "segments: need T > 0 and ncls > 0");
-  hipLaunchKernelGGL(argmax_rows_kernel, dim3(cdiv(T, 4)), dim3(256), 0, s, x, ldx, col0, ncls, T, pred);
-  hipLaunchKernelGGL(boundary_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, s, pred, T, seg_id, seg_start, seg_end,
+  FX_REQUIRE(nvid >= 1, "segments: nvid >= 1");
+  hipLaunchKernelGGL(argmax_rows_kernel, dim3(cdiv((long long)T * nvid, 4)), dim3(256), 0, s, x, ldx, col0, ncls, T * nvid,
+                     pred);
+  hipLaunchKernelGGL(boundary_scan_kernel, dim3(nvid), dim3(SCAN_THREADS), 0, s, pred, T, seg_id, seg_start, seg_end,
                      num_seg);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;

@@ -323,31 +323,43 @@ def mha(mod, query, key, value):
 # ---------------------------------------------------------------------------
 
 class X2YFn(torch.autograd.Function):
-    """``X2Y_map.forward`` (basic.py:349-389): returns (Y_out, attn_logit, attn)."""
+    """``X2Y_map.forward`` (basic.py:349-389): returns (Y_out, attn_logit, attn).  ``rows`` = None
+    (one video) or (x_off, y_off) host prefix lists of nvid stacked videos; logit / attn then pack
+    each video's (ny_v, nx_v) block in video order."""
 
     @staticmethod
-    def forward(ctx, X, Y, Xpos, Ypos, wk, bk, wv, bv, wq, bq, wy, by):
+    def forward(ctx, X, Y, Xpos, Ypos, rows, wk, bk, wv, bv, wq, bq, wy, by):
         lib = nx.load()
         dev = X.device
         Nx, xdim = X.shape
         Ny, ydim = Y.shape
         Hd, outdim = wk.shape[0], wy.shape[0]
+        if rows is None:
+            nvid, xo, yo, na = 1, None, None, Ny * Nx
+        else:
+            xl, yl = rows
+            nvid = len(xl) - 1
+            xo, yo = nx.int_array(xl), nx.int_array(yl)
+            na = sum((yl[v + 1] - yl[v]) * (xl[v + 1] - xl[v]) for v in range(nvid))
         out = _empty(Ny, outdim, device=dev)
-        logit = _empty(Ny, Nx, device=dev)
-        attn = _empty(Ny, Nx, device=dev)
+        logit = _empty(na, device=dev)
+        attn = _empty(na, device=dev)
         saved = _ws(lib.fx_x2y_saved_floats(Nx, xdim, Ny, ydim, Hd), dev)
-        ws = _ws(lib.fx_x2y_workspace_floats(Nx, xdim, Ny, ydim, Hd, outdim), dev)
+        ws = _ws(lib.fx_x2y_workspace_floats(Nx, xdim, Ny, ydim, Hd, outdim, nvid, xo, yo), dev)
         xpc = 0 if Xpos is None else Xpos.shape[1]
         ypc = 0 if Ypos is None else Ypos.shape[1]
         _check(lib.fx_x2y_fwd(nx.ptr(X), nx.ld(X), Nx, xdim, nx.ptr(Xpos), nx.ld(Xpos), xpc,
                               nx.ptr(Y), nx.ld(Y), Ny, ydim, nx.ptr(Ypos), nx.ld(Ypos), ypc,
                               nx.ptr(wk), nx.ptr(bk), nx.ptr(wv), nx.ptr(bv), nx.ptr(wq), nx.ptr(bq),
-                              nx.ptr(wy), nx.ptr(by), Hd, outdim, nx.ptr(out), outdim, nx.ptr(logit), nx.ptr(attn),
-                              nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_x2y_fwd")
+                              nx.ptr(wy), nx.ptr(by), Hd, outdim, nvid, xo, yo, nx.ptr(out), outdim, nx.ptr(logit),
+                              nx.ptr(attn), nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_x2y_fwd")
         ctx.dims = (Nx, xdim, Ny, ydim, Hd, outdim, xpc, ypc)
+        ctx.rows = rows
         ctx.has_pos = (Xpos is not None, Ypos is not None)
         ctx.save_for_backward(X, Y, wk, bk, wv, bv, wq, bq, wy, by, attn, saved)
         ctx.mark_non_differentiable(attn)
+        if rows is None:
+            return out, logit.view(Ny, Nx), attn.view(Ny, Nx)
         return out, logit, attn
 
     @staticmethod
@@ -358,6 +370,12 @@ class X2YFn(torch.autograd.Function):
         hx, hy = ctx.has_pos
         nd = ctx.needs_input_grad
         dev = X.device
+        rows = ctx.rows
+        if rows is None:
+            nvid, xo, yo = 1, None, None
+        else:
+            nvid = len(rows[0]) - 1
+            xo, yo = nx.int_array(rows[0]), nx.int_array(rows[1])
         dout = torch.zeros(Ny, outdim, device=dev) if dout is None else dout.contiguous()
         dlogit = None if dlogit is None else dlogit.contiguous()
         dattn = None if dattn is None else dattn.contiguous()
@@ -365,23 +383,23 @@ class X2YFn(torch.autograd.Function):
         dY = _empty(Ny, ydim, device=dev) if nd[1] else None
         dXp = _empty(Nx, xpc, device=dev) if (hx and nd[2]) else None
         dYp = _empty(Ny, ypc, device=dev) if (hy and nd[3]) else None
-        tg = [grad_target(p, nd[4 + i]) for i, p in enumerate((wk, bk, wv, bv, wq, bq, wy, by))]
+        tg = [grad_target(p, nd[5 + i]) for i, p in enumerate((wk, bk, wv, bv, wq, bq, wy, by))]
         bufs = [t[0] for t in tg]
         # the kernel needs every weight-gradient target; absent ones go to scratch
         bufs = [b if b is not None else torch.zeros_like(p) for b, p in zip(bufs, (wk, bk, wv, bv, wq, bq, wy, by))]
-        ws = _ws(lib.fx_x2y_workspace_floats(Nx, xdim, Ny, ydim, Hd, outdim), dev)
+        ws = _ws(lib.fx_x2y_workspace_floats(Nx, xdim, Ny, ydim, Hd, outdim, nvid, xo, yo), dev)
         _check(lib.fx_x2y_bwd(nx.ptr(X), nx.ld(X), Nx, xdim, xpc, nx.ptr(Y), nx.ld(Y), Ny, ydim, ypc,
-                              nx.ptr(wk), nx.ptr(wv), nx.ptr(wq), nx.ptr(wy), Hd, outdim, nx.ptr(attn), nx.ptr(saved),
-                              nx.ptr(dout), outdim, nx.ptr(dlogit), nx.ptr(dattn), nx.ptr(dX), nx.ptr(dXp),
-                              nx.ptr(dY), nx.ptr(dYp), *[nx.ptr(t) for t in bufs], int(hx), int(hy), nx.ptr(ws),
-                              nx.stream()), "fx_x2y_bwd")
-        return (dX, dY, dXp, dYp) + tuple(t[1] for t in tg)
+                              nx.ptr(wk), nx.ptr(wv), nx.ptr(wq), nx.ptr(wy), Hd, outdim, nvid, xo, yo, nx.ptr(attn),
+                              nx.ptr(saved), nx.ptr(dout), outdim, nx.ptr(dlogit), nx.ptr(dattn), nx.ptr(dX),
+                              nx.ptr(dXp), nx.ptr(dY), nx.ptr(dYp), *[nx.ptr(t) for t in bufs], int(hx), int(hy),
+                              nx.ptr(ws), nx.stream()), "fx_x2y_bwd")
+        return (dX, dY, dXp, dYp, None) + tuple(t[1] for t in tg)
 
 
-def x2y(mod, X, Y, Xpos, Ypos):
+def x2y(mod, X, Y, Xpos, Ypos, rows=None):
     return X2YFn.apply(_2d(X), _2d(Y), None if Xpos is None else _2d(Xpos), None if Ypos is None else _2d(Ypos),
-                       mod.X_K.weight, mod.X_K.bias, mod.X_V.weight, mod.X_V.bias, mod.Y_Q.weight, mod.Y_Q.bias,
-                       mod.Y_W.weight, mod.Y_W.bias)
+                       rows, mod.X_K.weight, mod.X_K.bias, mod.X_V.weight, mod.X_V.bias, mod.Y_Q.weight,
+                       mod.Y_Q.bias, mod.Y_W.weight, mod.Y_W.bias)
 
 
 # ---------------------------------------------------------------------------
@@ -574,20 +592,25 @@ def conv3(x, w, b, dil, T):
 # ---------------------------------------------------------------------------
 
 class GRUFn(torch.autograd.Function):
-    """One bidirectional ``nn.GRU`` layer (blocks.py:401,432) on (S, In) rows -> (S, 2Hh)."""
+    """One bidirectional ``nn.GRU`` layer (blocks.py:401,432) on (S, In) rows -> (S, 2Hh).
+    ``seq_off`` = None (one sequence) or the host prefix list of several sequences stacked by
+    rows (one per video), run concurrently by the kernel."""
 
     @staticmethod
-    def forward(ctx, x, w_ih, w_hh, b_ih, b_hh, w_ih_r, w_hh_r, b_ih_r, b_hh_r):
+    def forward(ctx, x, seq_off, w_ih, w_hh, b_ih, b_hh, w_ih_r, w_hh_r, b_ih_r, b_hh_r):
         lib = nx.load()
         S, In = x.shape
         Hh = w_hh.shape[1]
         dev = x.device
+        nq = 1 if seq_off is None else len(seq_off) - 1
+        so = None if seq_off is None else nx.int_array(seq_off)
         out = _empty(S, 2 * Hh, device=dev)
         saved = _ws(lib.fx_gru_saved_floats(S, Hh), dev)
-        ws = _ws(lib.fx_gru_workspace_floats(S, In, Hh), dev)
-        _check(lib.fx_gru_bidir_fwd(nx.ptr(x), nx.ld(x), S, In, Hh, nx.ptr(w_ih), nx.ptr(w_hh), nx.ptr(b_ih),
+        ws = _ws(lib.fx_gru_workspace_floats(S, nq, In, Hh), dev)
+        _check(lib.fx_gru_bidir_fwd(nx.ptr(x), nx.ld(x), S, nq, so, In, Hh, nx.ptr(w_ih), nx.ptr(w_hh), nx.ptr(b_ih),
                                     nx.ptr(b_hh), nx.ptr(w_ih_r), nx.ptr(w_hh_r), nx.ptr(b_ih_r), nx.ptr(b_hh_r),
                                     nx.ptr(out), 2 * Hh, nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_gru_bidir_fwd")
+        ctx.seq_off = seq_off
         ctx.save_for_backward(x, w_ih, w_hh, b_ih, b_hh, w_ih_r, w_hh_r, b_ih_r, b_hh_r, saved)
         return out
 
@@ -601,24 +624,27 @@ class GRUFn(torch.autograd.Function):
         Hh = w_hh.shape[1]
         dev = x.device
         nd = ctx.needs_input_grad
+        seq_off = ctx.seq_off
+        nq = 1 if seq_off is None else len(seq_off) - 1
+        so = None if seq_off is None else nx.int_array(seq_off)
         dx = _empty(S, In, device=dev) if nd[0] else None
-        tg = [grad_target(p, nd[1 + i]) for i, p in enumerate(w)]
+        tg = [grad_target(p, nd[2 + i]) for i, p in enumerate(w)]
         bufs = [t[0] for t in tg]
-        ws = _ws(lib.fx_gru_workspace_floats(S, In, Hh), dev)
-        _check(lib.fx_gru_bidir_bwd(nx.ptr(x), nx.ld(x), S, In, Hh, nx.ptr(w_ih), nx.ptr(w_hh), nx.ptr(w_ih_r),
+        ws = _ws(lib.fx_gru_workspace_floats(S, nq, In, Hh), dev)
+        _check(lib.fx_gru_bidir_bwd(nx.ptr(x), nx.ld(x), S, nq, so, In, Hh, nx.ptr(w_ih), nx.ptr(w_hh), nx.ptr(w_ih_r),
                                     nx.ptr(w_hh_r), nx.ptr(saved), nx.ptr(dout), 2 * Hh, nx.ptr(dx), nx.ld(dx),
                                     *[nx.ptr(t) for t in bufs], nx.ptr(ws), nx.stream()), "fx_gru_bidir_bwd")
-        return (dx,) + tuple(t[1] for t in tg)
+        return (dx, None) + tuple(t[1] for t in tg)
 
 
-def gru(mod, x):
+def gru(mod, x, seq_off=None):
     """Run an ``nn.GRU(bidirectional=True)`` module's parameters layer by layer through GRUFn."""
     assert mod.bidirectional and not mod.batch_first
     h = _2d(x)
     for layer in range(mod.num_layers):
         p = [getattr(mod, f"{n}_l{layer}{s}") for s in ("", "_reverse")
              for n in ("weight_ih", "weight_hh", "bias_ih", "bias_hh")]
-        h = GRUFn.apply(h, *p)
+        h = GRUFn.apply(h, seq_off, *p)
     return h
 
 
@@ -634,10 +660,32 @@ def segments_from_probs(x2d, col0, ncls):
     buf = torch.empty(4 * T + 1, device=dev, dtype=torch.int32)
     pred, seg_id, st, en = buf[:T], buf[T:2 * T], buf[2 * T:3 * T], buf[3 * T:4 * T]
     ns = buf[4 * T:]
-    _check(lib.fx_segments_from_probs(nx.ptr(x2d), nx.ld(x2d), col0, ncls, T, nx.ptr(pred), nx.ptr(seg_id),
+    _check(lib.fx_segments_from_probs(nx.ptr(x2d), nx.ld(x2d), col0, ncls, T, 1, nx.ptr(pred), nx.ptr(seg_id),
                                       nx.ptr(st), nx.ptr(en), nx.ptr(ns), nx.stream()), "fx_segments_from_probs")
     S = int(ns.item())
     return S, seg_id, st[:S], en[:S]
+
+
+def segments_from_probs_batched(x2d, col0, ncls, T, nvid):
+    """``segments_from_probs`` for nvid videos of T rows stacked in x2d, with ONE host read of all
+    segment counts.  Returns (S list, per-video local (seg_id, start, end) views, global
+    (seg_id, start, end) over the stacked frame rows / concatenated segments)."""
+    lib = nx.load()
+    dev = x2d.device
+    n = nvid * T
+    buf = torch.empty(4 * n + nvid, device=dev, dtype=torch.int32)
+    pred, seg_id, st, en = buf[:n], buf[n:2 * n], buf[2 * n:3 * n], buf[3 * n:4 * n]
+    ns = buf[4 * n:]
+    _check(lib.fx_segments_from_probs(nx.ptr(x2d), nx.ld(x2d), col0, ncls, T, nvid, nx.ptr(pred), nx.ptr(seg_id),
+                                      nx.ptr(st), nx.ptr(en), nx.ptr(ns), nx.stream()), "fx_segments_from_probs")
+    S = [int(v) for v in ns.tolist()]
+    tot = sum(S)
+    g = torch.empty(n + 2 * tot, device=dev, dtype=torch.int32)
+    gid, gst, gen = g[:n], g[n:n + tot], g[n + tot:]
+    _check(lib.fx_segments_globalize(nvid, T, nx.int_array(S), nx.ptr(seg_id), nx.ptr(st), nx.ptr(en), nx.ptr(gid),
+                                     nx.ptr(gst), nx.ptr(gen), nx.stream()), "fx_segments_globalize")
+    local = [(seg_id[v * T:(v + 1) * T], st[v * T:v * T + S[v]], en[v * T:v * T + S[v]]) for v in range(nvid)]
+    return S, local, (gid, gst, gen)
 
 
 class SegMeanFn(torch.autograd.Function):
@@ -815,7 +863,7 @@ class DecoderFn(torch.autograd.Function):
     per direction (fx_decoder_fwd / fx_decoder_bwd)."""
 
     @staticmethod
-    def forward(ctx, tgt, qpos, mem, mpos, spec, *params):
+    def forward(ctx, tgt, qpos, mem, mpos, spec, nvid, *params):
         lib = nx.load()
         meta, slots, gl, cache = spec
         prm = cache.get("prm")
@@ -830,13 +878,13 @@ class DecoderFn(torch.autograd.Function):
         hq, hm = int(qpos is not None), int(mpos is not None)
         dev = tgt.device
         out = _empty(R, meta["out_dim"], device=dev)
-        saved = _ws(lib.fx_decoder_saved_floats(ctypes.byref(prm), R, T, hq, hm), dev)
-        ws = _ws(lib.fx_decoder_workspace_floats(ctypes.byref(prm), R, T, hq, hm), dev)
+        saved = _ws(lib.fx_decoder_saved_floats(ctypes.byref(prm), R, T, nvid, hq, hm), dev)
+        ws = _ws(lib.fx_decoder_workspace_floats(ctypes.byref(prm), R, T, nvid, hq, hm), dev)
         _check(lib.fx_decoder_fwd(ctypes.byref(prm), nx.ptr(tgt), nx.ld(tgt), R, nx.ptr(qpos), nx.ld(qpos),
-                                  nx.ptr(mem), nx.ld(mem), T, nx.ptr(mpos), nx.ld(mpos), nx.ptr(out), nx.ld(out),
-                                  nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_decoder_fwd")
+                                  nx.ptr(mem), nx.ld(mem), T, nvid, nx.ptr(mpos), nx.ld(mpos), nx.ptr(out),
+                                  nx.ld(out), nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_decoder_fwd")
         ctx.spec = spec
-        ctx.flags = (hq, hm, T)
+        ctx.flags = (hq, hm, T, nvid)
         ctx.save_for_backward(tgt, qpos, mem, mpos, saved, *params)
         return out
 
@@ -845,12 +893,12 @@ class DecoderFn(torch.autograd.Function):
         lib = nx.load()
         tgt, qpos, mem, mpos, saved, *params = ctx.saved_tensors
         meta, slots, gl, cache = ctx.spec
-        hq, hm, T = ctx.flags
+        hq, hm, T, nvid = ctx.flags
         nd = ctx.needs_input_grad
         dev = dout.device
         dout = dout.contiguous()
         R = tgt.shape[0]
-        tg = [grad_target(p, nd[5 + i]) for i, p in enumerate(params)]
+        tg = [grad_target(p, nd[6 + i]) for i, p in enumerate(params)]
         bufs = [t[0] for t in tg]
         gkey = tuple(0 if b is None else b.data_ptr() for b in bufs)
         g = cache.get("grads")
@@ -865,16 +913,18 @@ class DecoderFn(torch.autograd.Function):
         dqpos = _empty(R, A, device=dev) if (hq and nd[1]) else None
         dmem = _empty(*mem.shape, device=dev) if (mem is not None and nd[2]) else None
         dmpos = _empty(*mpos.shape, device=dev) if (hm and nd[3]) else None
-        ws = _ws(lib.fx_decoder_workspace_floats(ctypes.byref(prm), R, T, hq, hm), dev)
+        ws = _ws(lib.fx_decoder_workspace_floats(ctypes.byref(prm), R, T, nvid, hq, hm), dev)
         _check(lib.fx_decoder_bwd(ctypes.byref(prm), ctypes.byref(g), nx.ptr(tgt), nx.ld(tgt), R, nx.ptr(qpos),
-                                  nx.ptr(mem), nx.ld(mem), T, nx.ptr(mpos), nx.ld(mpos), nx.ptr(dout), nx.ld(dout),
+                                  nx.ptr(mem), nx.ld(mem), T, nvid, nx.ptr(mpos), nx.ld(mpos), nx.ptr(dout),
+                                  nx.ld(dout),
                                   nx.ptr(dtgt), nx.ld(dtgt), nx.ptr(dqpos), nx.ptr(dmem), nx.ld(dmem), nx.ptr(dmpos),
                                   nx.ld(dmpos), nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_decoder_bwd")
-        return (dtgt, dqpos, dmem, dmpos, None) + tuple(t[1] for t in tg)
+        return (dtgt, dqpos, dmem, dmpos, None, None) + tuple(t[1] for t in tg)
 
 
-def decoder(mod, tgt, memory=None, pos=None, query_pos=None):
-    """Run an SCADecoder (memory given) or SADecoder through DecoderFn; returns (R, out_dim)."""
+def decoder(mod, tgt, memory=None, pos=None, query_pos=None, nvid=1):
+    """Run an SCADecoder (memory given) or SADecoder through DecoderFn; returns (R, out_dim).
+    ``nvid`` videos stacked by rows (tokens and memory frames split evenly)."""
     spec = getattr(mod, "_fx_spec", None)
     if spec is None:
         meta, params, slots, gl = _decoder_slots(mod)
@@ -886,4 +936,4 @@ def decoder(mod, tgt, memory=None, pos=None, query_pos=None):
     qp = None if query_pos is None else _2d(query_pos).contiguous()
     mem = None if memory is None else _2d(memory)
     mp = None if pos is None else _2d(pos)
-    return DecoderFn.apply(t2, qp, mem, mp, spec, *params)
+    return DecoderFn.apply(t2, qp, mem, mp, spec, int(nvid), *params)

@@ -143,6 +143,18 @@ class InputBlock(Block):
         self.action_feature = action_feature[:, :, :-(self.nclass + 1)]
         return frame_feature, action_feature
 
+    def forward_batch(self, f2, a2, fpos, apos, vb):
+        """``forward`` over vb.nvid stacked videos (frames (nvid*T, C), tokens (nvid*Q, A));
+        per-video side-channel attributes go to ``self._vrec``."""
+        f = fxf.mstcn(self.frame_branch, f2, T=vb.T, nvid=vb.nvid)
+        f_out, f_cl = fxf.process_feature(f, self.nclass)
+        a = fxf.decoder(self.action_branch, a2, f_out, pos=fpos, query_pos=apos, nvid=vb.nvid)
+        a_out, a_cl = fxf.process_feature(a, self.nclass + 1)
+        n = self.nclass + 1
+        self._vrec = [dict(frame_clogit=f_cl[vb.fr(v)].unsqueeze(1), action_clogit=a_cl[vb.tk(v)].unsqueeze(1),
+                           action_feature=a_out[vb.tk(v), :-n].unsqueeze(1)) for v in range(vb.nvid)]
+        return f_out, a_out
+
     def compute_loss(self, criterion, match=None):
         fl = criterion.frame_loss(self.frame_clogit.squeeze(1))
         atk = criterion.action_token_loss(match, self.action_clogit)
@@ -178,6 +190,27 @@ class UpdateBlock(Block):
         self.f2a_attn_logit = self.f2a_layer.attn_logit.squeeze(0).unsqueeze(0)
         self.a2f_attn_logit = self.a2f_layer.attn_logit.squeeze(0).unsqueeze(0)
         return frame_feature, action_feature
+
+    def forward_batch(self, f2, a2, fpos, apos, vb):
+        f2a, a2f = self.f2a_layer, self.a2f_layer
+        a, f2a_lg, f2a_at = fxf.x2y(f2a, f2, a2, fpos if f2a.kq_pos else None, apos if f2a.kq_pos else None,
+                                    rows=(vb.f_off, vb.a_off))
+        a = fxf.decoder(self.action_branch, a, None, query_pos=apos, nvid=vb.nvid)
+        a_out, a_cl = fxf.process_feature(a, self.nclass + 1)
+        f, a2f_lg, a2f_at = fxf.x2y(a2f, a_out, f2, apos if a2f.kq_pos else None, fpos if a2f.kq_pos else None,
+                                    rows=(vb.a_off, vb.f_off))
+        f = fxf.mstcn(self.frame_branch, f, T=vb.T, nvid=vb.nvid)
+        f_out, f_cl = fxf.process_feature(f, self.nclass)
+        n, Q, T = self.nclass + 1, vb.Q, vb.T
+        recs = []
+        for v in range(vb.nvid):
+            blk = slice(v * Q * T, (v + 1) * Q * T)
+            recs.append(dict(frame_clogit=f_cl[vb.fr(v)].unsqueeze(1), action_clogit=a_cl[vb.tk(v)].unsqueeze(1),
+                             action_feature=a_out[vb.tk(v), :-n].unsqueeze(1),
+                             f2a_attn=f2a_at[blk].view(1, Q, T), a2f_attn=a2f_at[blk].view(1, T, Q),
+                             f2a_attn_logit=f2a_lg[blk].view(1, Q, T), a2f_attn_logit=a2f_lg[blk].view(1, T, Q)))
+        self._vrec = recs
+        return f_out, a_out
 
     def compute_loss(self, criterion, match=None):
         fl = criterion.frame_loss(self.frame_clogit.squeeze(1))
@@ -242,6 +275,51 @@ class UpdateBlockTDU(Block):
         self.a2f_attn = tdu.attn_seg2frame(self.a2f_layer.attn[0])
         return frame_feature, action_feature
 
+    def forward_batch(self, f2, a2, fpos, apos, vb):
+        # temporal downsample: one segmentation launch + ONE host read of every video's S
+        S, local, (gid, gst, gen) = fxf.segments_from_probs_batched(f2, f2.shape[1] - self.nclass, self.nclass,
+                                                                     vb.T, vb.nvid)
+        s_off = [0]
+        for n_ in S:
+            s_off.append(s_off[-1] + n_)
+        tdus = [basic.TemporalDownsampleUpsample(*local[v]) for v in range(vb.nvid)]
+        seg = fxf.SegMeanFn.apply(f2, gid, gst, gen)
+        seg = torch.relu(fxf.gru(self.seg_update, seg, seq_off=s_off))
+        seg = fxf.linear(seg, self.seg_combine.weight, self.seg_combine.bias)
+        seg_out, seg_cl = fxf.process_feature(seg, self.nclass)
+        seg_pos = None
+        if fpos is not None:
+            seg_pos = fpos[torch.div(gst + gen, 2, rounding_mode="floor").to(torch.int64)]
+        f2a, a2f = self.f2a_layer, self.a2f_layer
+        a, f2a_lg, f2a_at = fxf.x2y(f2a, seg_out, a2, seg_pos if f2a.kq_pos else None, apos if f2a.kq_pos else None,
+                                    rows=(s_off, vb.a_off))
+        a = fxf.decoder(self.action_branch, a, None, query_pos=apos, nvid=vb.nvid)
+        a_out, a_cl = fxf.process_feature(a, self.nclass + 1)
+        sg, a2f_lg, a2f_at = fxf.x2y(a2f, a_out, seg_out, apos if a2f.kq_pos else None,
+                                     seg_pos if a2f.kq_pos else None, rows=(vb.a_off, s_off))
+        lin = self.sf_merge[0]
+        f = fxf.SegMergeFn.apply(sg, f2, gid, gst, gen, lin.weight, lin.bias)
+        f = fxf.mstcn(self.frame_branch, f, T=vb.T, nvid=vb.nvid)
+        f_out, f_cl = fxf.process_feature(f, self.nclass)
+        n, Q = self.nclass + 1, vb.Q
+        recs, a0 = [], 0
+        for v in range(vb.nvid):
+            Sv, tdu = S[v], tdus[v]
+            blk = slice(a0, a0 + Q * Sv)
+            a0 += Q * Sv
+            f2a_at_v = f2a_at[blk].view(1, 1, Q, Sv)
+            a2f_at_v = a2f_at[blk].view(1, 1, Sv, Q)
+            recs.append(dict(frame_clogit=f_cl[vb.fr(v)].unsqueeze(1),
+                             seg_clogit=seg_cl[s_off[v]:s_off[v + 1]].unsqueeze(1), tdu=tdu,
+                             action_clogit=a_cl[vb.tk(v)].unsqueeze(1),
+                             action_feature=a_out[vb.tk(v), :-n].unsqueeze(1),
+                             f2a_attn_logit=f2a_lg[blk].view(1, Q, Sv),
+                             f2a_attn=tdu.attn_seg2frame(f2a_at_v[0].transpose(2, 1)).transpose(2, 1),
+                             a2f_attn_logit=a2f_lg[blk].view(1, Sv, Q),
+                             a2f_attn=tdu.attn_seg2frame(a2f_at_v[0])))
+        self._vrec = recs
+        return f_out, a_out
+
     def compute_loss(self, criterion, match=None):
         fl = criterion.frame_loss(self.frame_clogit.squeeze(1))
         sl = criterion.frame_loss_tdu(self.seg_clogit, self.tdu)
@@ -304,6 +382,40 @@ class _FACTBase(nn.Module):
             frame_feature, action_feature = block(frame_feature, action_feature, frame_pe, action_pe)
             block_output.append([frame_feature, action_feature])
         return block_output
+
+    def _forward_batch(self, seq_list):
+        """All videos through the blocks in lockstep (see _forward_videos); returns restore(v), which
+        points every side-channel attribute at video v's views."""
+        nvid, T = len(seq_list), seq_list[0].shape[0]
+        Q = self.cfg.FACT.ntoken
+        vb = _VideoBatch(nvid, T, Q)
+        frames = []
+        for seq in seq_list:
+            x = seq.unsqueeze(1)
+            if self.cfg.FACT.cmr and self.training:
+                x = self.channel_masking_dropout(x.permute([1, 2, 0])).permute([2, 0, 1])
+            if self.cfg.TM.use and self.training:
+                x = time_mask(x, self.cfg.TM.t, self.cfg.TM.m, self.cfg.TM.p, replace_with_zero=True)
+            frames.append(x.squeeze(1))
+        f2 = torch.cat(frames, 0)
+        fpe = _frame_pos(self.frame_pe, seq_list[0].unsqueeze(1))
+        fpos = None if fpe is None else fpe.squeeze(1).repeat(nvid, 1)
+        apos = self.action_query.squeeze(1).repeat(nvid, 1)
+        a2 = torch.zeros_like(apos)
+        for blk in self.block_list:
+            f2, a2 = blk.forward_batch(f2, a2, fpos, apos, vb)
+        proj = None
+        if isinstance(self, FACT_CLIP):
+            feat_dim = f2.shape[-1] - self.num_classes
+            proj = self.frame_projection(f2[:, :feat_dim])
+
+        def restore(v):
+            for blk in self.block_list:
+                for k, val in blk._vrec[v].items():
+                    setattr(blk, k, val)
+            if proj is not None:
+                self.projected_frame_embeddings = proj[vb.fr(v)].unsqueeze(1)
+        return restore
 
     def _fact_loss(self, label, label_host=None):
         mc: MatchCriterion = self.mcriterion
@@ -417,28 +529,67 @@ class FACT_CLIP(_FACTBase):
         return _forward_videos(self, seq_list, label_list, compute_loss)
 
 
+class _VideoBatch:
+    """Row layout of nvid equal-length videos stacked for one batched pass: frames of video v are
+    rows [v*T, (v+1)*T), its action tokens rows [v*Q, (v+1)*Q)."""
+
+    def __init__(self, nvid, T, Q):
+        self.nvid, self.T, self.Q = nvid, T, Q
+        self.f_off = [v * T for v in range(nvid + 1)]
+        self.a_off = [v * Q for v in range(nvid + 1)]
+
+    def fr(self, v):
+        return slice(v * self.T, (v + 1) * self.T)
+
+    def tk(self, v):
+        return slice(v * self.Q, (v + 1) * self.Q)
+
+
+def _batchable(net, seq_list):
+    """The lockstep path needs equal-length videos, the fused decoders and no transcript input."""
+    if len(seq_list) < 2 or net.cfg.FACT.trans:
+        return False
+    T = seq_list[0].shape[0]
+    if any(s.shape[0] != T or not s.is_cuda for s in seq_list):
+        return False
+    for blk in net.block_list:
+        if not basic._fused_decoder_ok(blk.action_branch) or not hasattr(blk, "forward_batch"):
+            return False
+        if isinstance(blk.frame_branch, basic.MSTCN2):
+            return False
+    return True
+
+
+def _label_to_host(label):
+    if label.is_cuda:
+        label_host = label.to("cpu", non_blocking=True)
+        ready = torch.cuda.Event()
+        ready.record()
+        return label_host, ready
+    return label, None
+
+
 def _forward_videos(net, seq_list, label_list, compute_loss):
-    """FACT.forward / FACT_CLIP.forward (blocks.py:118-135, 889-917) with the reference's results and
-    fewer device drains: the transcript is only built where it is used (FACT.trans), each label is
-    copied to the host asynchronously at the start of its video (read at the loss, after the TDU
-    segmentation already synchronised), the per-frame predictions and the loss floats come back in
-    one device->host copy after the last video."""
+    """FACT.forward / FACT_CLIP.forward (blocks.py:118-135, 889-917): per-video predictions and the
+    mean of the per-video losses, with the reference's side-channel attributes holding the last
+    video's values afterwards.
+
+    Equal-length videos run in LOCKSTEP (``forward_batch``): every block processes all videos in one
+    pass (frame GEMMs over nvid*T rows, token GEMMs over nvid*Q rows, attention kept within each
+    video, one segmentation read-back per TDU block for all videos); the losses then run per video
+    on that video's views.  Otherwise videos run one by one as in the reference.  Either way: the
+    transcript is only built where it is used (FACT.trans), labels reach the host by an async copy
+    started before the forward, predictions and loss floats come back in one read-back."""
     clip = isinstance(net, FACT_CLIP)
+    hosts = [_label_to_host(l_) for l_ in label_list]
     save_list, losses, pending, preds = [], [], [], []
-    for seq, label in zip(seq_list, label_list):
-        if label.is_cuda:
-            label_host = label.to("cpu", non_blocking=True)
-            ready = torch.cuda.Event()
-            ready.record()
-        else:
-            label_host, ready = label, None
-        trans = torch_class_label_to_segment_label(label)[0] if net.cfg.FACT.trans else None
-        net._forward_one_video(seq.unsqueeze(1), trans)
+
+    def finish_video(v, trans):
         preds.append(net.eval_with_clip(trans) if clip else net.block_list[-1].eval(trans))
         save = {}
         save_list.append(save)
         if compute_loss:
-            lo = net._loss_one_video(label, label_host=(label_host, ready))
+            lo = net._loss_one_video(label_list[v], label_host=hosts[v])
             losses.append(lo)
             keys, vals = ["loss"], [lo.detach()]
             if clip and hasattr(net, "fact_loss"):
@@ -448,16 +599,25 @@ def _forward_videos(net, seq_list, label_list, compute_loss):
                 keys.append("contrastive_loss")
                 vals.append(net.contrastive_loss.detach().reshape(()))
             pending.append((save, keys, vals))
-    # one readback for every video's predictions (+ loss floats)
-    flat = [p.reshape(-1).to(torch.int64) for p in preds]
-    nums = [v.float().reshape(1) for _, _, vals in pending for v in vals]
-    host = torch.cat(flat).cpu().numpy() if flat else None
+
+    if _batchable(net, seq_list):
+        restore = net._forward_batch(seq_list)
+        for v in range(len(seq_list)):
+            restore(v)
+            finish_video(v, None)
+    else:
+        for v, (seq, label) in enumerate(zip(seq_list, label_list)):
+            trans = torch_class_label_to_segment_label(label)[0] if net.cfg.FACT.trans else None
+            net._forward_one_video(seq.unsqueeze(1), trans)
+            finish_video(v, trans)
+    # one read-back for every video's predictions (+ loss floats)
+    host = torch.cat([p.reshape(-1).to(torch.int64) for p in preds]).cpu().numpy()
     off = 0
     for save, p in zip(save_list, preds):
         save["pred"] = host[off:off + p.numel()].copy()
         off += p.numel()
     if compute_loss:
-        vals = torch.cat(nums).tolist()
+        vals = torch.cat([v.float().reshape(1) for _, _, vs in pending for v in vs]).tolist()
         i = 0
         for save, keys, _ in pending:
             save["loss"] = dict(zip(keys, vals[i:i + len(keys)]))

@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FACTMX_LIB", os.path.join(_HERE, "_lib", "libfactmx.so"))
-ABI_VERSION = 3
+ABI_VERSION = 5
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -75,14 +75,15 @@ SIGNATURES = {
     "fx_linear_bwd_workspace_floats": (L, [I, I, I]),
     "fx_linear_bwd": (I, [P, L, P, L, P, L, P, L, I, I, I, P, L, P, L, P, I, I, P, P]),
     "fx_x2y_saved_floats": (L, [I, I, I, I, I]),
-    "fx_x2y_workspace_floats": (L, [I, I, I, I, I, I]),
-    "fx_x2y_fwd": (I, [P, L, I, I, P, L, I, P, L, I, I, P, L, I, P, P, P, P, P, P, P, P, I, I, P, L, P, P, P, P, P]),
-    "fx_x2y_bwd": (I, [P, L, I, I, I, P, L, I, I, I, P, P, P, P, I, I, P, P, P, L, P, P, P, P, P, P, P, P, P, P,
-                       P, P, P, P, I, I, P, P]),
-    "fx_decoder_saved_floats": (L, [ctypes.POINTER(DecoderParams), I, I, I, I]),
-    "fx_decoder_workspace_floats": (L, [ctypes.POINTER(DecoderParams), I, I, I, I]),
-    "fx_decoder_fwd": (I, [ctypes.POINTER(DecoderParams), P, L, I, P, L, P, L, I, P, L, P, L, P, P, P]),
-    "fx_decoder_bwd": (I, [ctypes.POINTER(DecoderParams), ctypes.POINTER(DecoderGrads), P, L, I, P, P, L, I, P, L,
+    "fx_x2y_workspace_floats": (L, [I, I, I, I, I, I, I, P, P]),
+    "fx_x2y_fwd": (I, [P, L, I, I, P, L, I, P, L, I, I, P, L, I, P, P, P, P, P, P, P, P, I, I, I, P, P, P, L, P, P,
+                       P, P, P]),
+    "fx_x2y_bwd": (I, [P, L, I, I, I, P, L, I, I, I, P, P, P, P, I, I, I, P, P, P, P, P, L, P, P, P, P, P, P, P, P,
+                       P, P, P, P, P, P, I, I, P, P]),
+    "fx_decoder_saved_floats": (L, [ctypes.POINTER(DecoderParams), I, I, I, I, I]),
+    "fx_decoder_workspace_floats": (L, [ctypes.POINTER(DecoderParams), I, I, I, I, I]),
+    "fx_decoder_fwd": (I, [ctypes.POINTER(DecoderParams), P, L, I, P, L, P, L, I, I, P, L, P, L, P, P, P]),
+    "fx_decoder_bwd": (I, [ctypes.POINTER(DecoderParams), ctypes.POINTER(DecoderGrads), P, L, I, P, P, L, I, I, P, L,
                            P, L, P, L, P, P, L, P, L, P, P, P]),
     "fx_mstcn_saved_floats": (L, [ctypes.POINTER(MstcnParams), I]),
     "fx_mstcn_workspace_floats": (L, [ctypes.POINTER(MstcnParams), I]),
@@ -103,10 +104,11 @@ SIGNATURES = {
     "fx_mha_core_fwd": (I, [P, L, P, L, P, L, I, I, I, I, P, P, L, P, P]),
     "fx_mha_core_bwd": (I, [P, L, P, L, P, L, P, P, L, I, I, I, I, P, L, P, L, P, L, P, P]),
     "fx_gru_saved_floats": (L, [I, I]),
-    "fx_gru_workspace_floats": (L, [I, I, I]),
-    "fx_gru_bidir_fwd": (I, [P, L, I, I, I, P, P, P, P, P, P, P, P, P, L, P, P, P]),
-    "fx_gru_bidir_bwd": (I, [P, L, I, I, I, P, P, P, P, P, P, L, P, L, P, P, P, P, P, P, P, P, P, P]),
-    "fx_segments_from_probs": (I, [P, L, I, I, I, P, P, P, P, P, P]),
+    "fx_gru_workspace_floats": (L, [I, I, I, I]),
+    "fx_gru_bidir_fwd": (I, [P, L, I, I, P, I, I, P, P, P, P, P, P, P, P, P, L, P, P, P]),
+    "fx_gru_bidir_bwd": (I, [P, L, I, I, P, I, I, P, P, P, P, P, P, L, P, L, P, P, P, P, P, P, P, P, P, P]),
+    "fx_segments_from_probs": (I, [P, L, I, I, I, I, P, P, P, P, P, P]),
+    "fx_segments_globalize": (I, [I, I, P, P, P, P, P, P, P, P]),
     "fx_seg_mean_fwd": (I, [P, L, P, P, I, I, P, L, P]),
     "fx_seg_mean_bwd": (I, [P, L, P, P, P, I, I, P, L, I, P]),
     "fx_seg_sum_rows": (I, [P, L, P, P, I, I, P, L, I, P]),
@@ -142,6 +144,13 @@ def load(path=None):
         raise FactmxNativeError(f"libfactmx ABI {v} != expected {ABI_VERSION}")
     _lib = lib
     return lib
+
+
+def int_array(vals):
+    """Host int32 array for the C ABI's prefix-offset arguments (None -> NULL)."""
+    if vals is None:
+        return None
+    return (ctypes.c_int * len(vals))(*[int(v) for v in vals])
 
 
 def check(status, what):

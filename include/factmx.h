@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FX_ABI_VERSION 3
+#define FX_ABI_VERSION 5
 
 enum {
   FX_OK = 0,
@@ -139,25 +139,30 @@ int fx_linear_bwd(const float* dy, long long lddy, const float* x, long long ldx
  *   logit (Ny, Nx) = yq . xk^T / sqrt(Hd);  attn = softmax over Nx
  *   out (Ny, outdim) = Y_W(cat[Y, attn . xv])  (concat folded into the GEMM)
  * logit and attn are outputs (the losses read them, blocks.py:363-366).
+ * nvid videos stacked by rows: x_off / y_off are HOST prefix arrays (nvid+1 ints,
+ * NULL when nvid == 1) of each video's X / Y rows; attention stays within a video
+ * and logit / attn pack the per-video (ny_v, nx_v) blocks in video order.
  * Positional tensors cover the first *pos_cols channels (nullable).
  * bwd: dout, optional direct dlogit / dattn (Ny, Nx) -> dX, dXpos, dY, dYpos
  *   (nullable) and every weight/bias gradient (accumulated, all required).
  * ---------------------------------------------------------------------- */
 long long fx_x2y_saved_floats(int Nx, int xdim, int Ny, int ydim, int Hd);
-long long fx_x2y_workspace_floats(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim);
+long long fx_x2y_workspace_floats(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim, int nvid,
+                                  const int* x_off, const int* y_off);
 int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpos, long long ldxp,
                int xpos_cols, const float* Y, long long ldy, int Ny, int ydim, const float* Ypos,
                long long ldyp, int ypos_cols, const float* wk, const float* bk, const float* wv,
                const float* bv, const float* wq, const float* bq, const float* wy, const float* by,
-               int Hd, int outdim, float* out, long long ldo, float* logit, float* attn,
-               float* saved, float* workspace, void* stream);
+               int Hd, int outdim, int nvid, const int* x_off, const int* y_off, float* out,
+               long long ldo, float* logit, float* attn, float* saved, float* workspace, void* stream);
 int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, const float* Y,
                long long ldy, int Ny, int ydim, int ypos_cols, const float* wk, const float* wv,
-               const float* wq, const float* wy, int Hd, int outdim, const float* attn,
-               const float* saved, const float* dout, long long lddo, const float* dlogit,
-               const float* dattn, float* dX, float* dXpos, float* dY, float* dYpos, float* dwk,
-               float* dbk, float* dwv, float* dbv, float* dwq, float* dbq, float* dwy, float* dby,
-               int has_xpos, int has_ypos, float* workspace, void* stream);
+               const float* wq, const float* wy, int Hd, int outdim, int nvid, const int* x_off,
+               const int* y_off, const float* attn, const float* saved, const float* dout,
+               long long lddo, const float* dlogit, const float* dattn, float* dX, float* dXpos,
+               float* dY, float* dYpos, float* dwk, float* dbk, float* dwv, float* dbv, float* dwq,
+               float* dbq, float* dwy, float* dby, int has_xpos, int has_ypos, float* workspace,
+               void* stream);
 
 /* ------------------------------------------------------------------------
  * Action-token decoder, whole stack in one call (eval-mode dropout, post-norm, ReLU FFN):
@@ -172,7 +177,9 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
  * self-attention in-projection is the packed (3A, A) in_proj_weight, the cross one
  * separate q (A,A), k (A,Hm), v (A,Hm) weights with the packed (3A) in_proj_bias.
  * Shapes: tgt (R, A) ld, qpos (R, A) dense or NULL, mem (T, Hm) ld, mpos (T, Hm) or
- * NULL, out (R, out_dim).  R <= 64 tokens.  saved/workspace sized by the queries.
+ * NULL, out (R, out_dim).  nvid videos stacked by rows: video v owns token rows
+ * [v*R/nvid, (v+1)*R/nvid) and memory rows [v*T/nvid, (v+1)*T/nvid); attention never
+ * crosses videos, every projection runs over all rows at once.  R/nvid <= 64.
  * bwd: every weight gradient ACCUMULATES (+=) into g; dtgt, dqpos (dense (R,A)),
  * dmem, dmpos are written (each nullable).
  * ---------------------------------------------------------------------- */
@@ -208,15 +215,17 @@ typedef struct fx_decoder_grads {
   float* out_w; float* out_b;
 } fx_decoder_grads;
 
-long long fx_decoder_saved_floats(const fx_decoder_params* p, int R, int T, int has_qpos, int has_mpos);
-long long fx_decoder_workspace_floats(const fx_decoder_params* p, int R, int T, int has_qpos, int has_mpos);
+long long fx_decoder_saved_floats(const fx_decoder_params* p, int R, int T, int nvid, int has_qpos,
+                                  int has_mpos);
+long long fx_decoder_workspace_floats(const fx_decoder_params* p, int R, int T, int nvid, int has_qpos,
+                                      int has_mpos);
 int fx_decoder_fwd(const fx_decoder_params* p, const float* tgt, long long ldt, int R, const float* qpos,
-                   long long ldqp, const float* mem, long long ldm, int T, const float* mpos,
+                   long long ldqp, const float* mem, long long ldm, int T, int nvid, const float* mpos,
                    long long ldmp, float* out, long long ldo, float* saved, float* workspace,
                    void* stream);
 int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const float* tgt,
                    long long ldt, int R, const float* qpos, const float* mem, long long ldm, int T,
-                   const float* mpos, long long ldmp, const float* dout, long long lddo, float* dtgt,
+                   int nvid, const float* mpos, long long ldmp, const float* dout, long long lddo, float* dtgt,
                    long long lddt, float* dqpos, float* dmem, long long lddm, float* dmpos,
                    long long lddmp, const float* saved, float* workspace, void* stream);
 
@@ -325,13 +334,21 @@ int fx_mha_core_bwd(const float* q, long long ldq, const float* k, long long ldk
  * fx_segments_from_probs: pred[t] = argmax_c x[t, col0 + c] (first max),
  *   boundaries where pred changes, seg_id[t], seg_start[s], seg_end[s]
  *   (inclusive) and *num_seg (device int) — bit-exact run-length encoding.
+ *   nvid videos of T rows each: video v's tables live at [v*T, (v+1)*T) with
+ *   video-local numbering, num_seg[v] its count.
+ * fx_segments_globalize: after the host read num_seg: gseg_id = seg_id + the
+ *   segment offset of its video; gstart/gend (sum S) = the videos' segment bounds as
+ *   global frame rows, in video order.
  * fx_seg_mean_fwd: seg[s] = mean over frames of segment s (index_add / len)
  * fx_seg_mean_bwd: dframe[t] (+)= dseg[seg_id[t]] / len[seg_id[t]]
  * fx_seg_sum_rows: dseg[s] (+)= sum_{t in s} dframe[t]  (gather backward)
  * ---------------------------------------------------------------------- */
-int fx_segments_from_probs(const float* x, long long ldx, int col0, int ncls, int T,
+int fx_segments_from_probs(const float* x, long long ldx, int col0, int ncls, int T, int nvid,
                            int32_t* pred, int32_t* seg_id, int32_t* seg_start, int32_t* seg_end,
                            int32_t* num_seg, void* stream);
+int fx_segments_globalize(int nvid, int T, const int32_t* num_seg_host, const int32_t* seg_id,
+                          const int32_t* seg_start, const int32_t* seg_end, int32_t* gseg_id,
+                          int32_t* gstart, int32_t* gend, void* stream);
 int fx_seg_mean_fwd(const float* x, long long ldx, const int32_t* seg_start, const int32_t* seg_end,
                     int S, int cols, float* y, long long ldy, void* stream);
 int fx_seg_mean_bwd(const float* dy, long long lddy, const int32_t* seg_id, const int32_t* seg_start,
@@ -345,21 +362,25 @@ int fx_seg_sum_rows(const float* dx, long long lddx, const int32_t* seg_start, c
  * (UpdateBlockTDU.seg_update = nn.GRU(H, H/2, 1, bidirectional=True),
  * blocks.py:401,432; PyTorch gate order r, z, n; h0 = 0).
  *   x (S, In) -> out (S, 2*Hh) = [forward h_t, backward h_t]; Hh <= 256.
+ *   nseq independent sequences stacked by rows (one per video): sequence q owns rows
+ *   [seq_off[q], seq_off[q+1]) (host prefix array, NULL when nseq == 1); they run concurrently.
  *   saved (fx_gru_saved_floats): per-step h_{t-1} and gates for backward.
  * bwd: dout (S, 2Hh) -> dx (nullable) and every weight/bias gradient
  *   (accumulated +=; each pointer nullable).
  * ---------------------------------------------------------------------- */
 long long fx_gru_saved_floats(int S, int Hh);
-long long fx_gru_workspace_floats(int S, int In, int Hh);
-int fx_gru_bidir_fwd(const float* x, long long ldx, int S, int In, int Hh, const float* w_ih_f,
-                     const float* w_hh_f, const float* b_ih_f, const float* b_hh_f, const float* w_ih_r,
-                     const float* w_hh_r, const float* b_ih_r, const float* b_hh_r, float* out,
-                     long long ldo, float* saved, float* workspace, void* stream);
-int fx_gru_bidir_bwd(const float* x, long long ldx, int S, int In, int Hh, const float* w_ih_f,
-                     const float* w_hh_f, const float* w_ih_r, const float* w_hh_r, const float* saved,
-                     const float* dout, long long lddo, float* dx, long long lddx, float* dw_ih_f,
-                     float* dw_hh_f, float* db_ih_f, float* db_hh_f, float* dw_ih_r, float* dw_hh_r,
-                     float* db_ih_r, float* db_hh_r, float* workspace, void* stream);
+long long fx_gru_workspace_floats(int S, int nseq, int In, int Hh);
+int fx_gru_bidir_fwd(const float* x, long long ldx, int S, int nseq, const int* seq_off, int In,
+                     int Hh, const float* w_ih_f, const float* w_hh_f, const float* b_ih_f,
+                     const float* b_hh_f, const float* w_ih_r, const float* w_hh_r, const float* b_ih_r,
+                     const float* b_hh_r, float* out, long long ldo, float* saved, float* workspace,
+                     void* stream);
+int fx_gru_bidir_bwd(const float* x, long long ldx, int S, int nseq, const int* seq_off, int In,
+                     int Hh, const float* w_ih_f, const float* w_hh_f, const float* w_ih_r,
+                     const float* w_hh_r, const float* saved, const float* dout, long long lddo,
+                     float* dx, long long lddx, float* dw_ih_f, float* dw_hh_f, float* db_ih_f,
+                     float* db_hh_f, float* dw_ih_r, float* dw_hh_r, float* db_ih_r, float* db_hh_r,
+                     float* workspace, void* stream);
 
 /* ------------------------------------------------------------------------
  * Elementwise helpers: dz = dy * (y > 0) (ReLU backward, basic.py:158,
