@@ -42,7 +42,9 @@ constexpr int IMG = BM * RS;        // floats per operand image (>= BK * CS)
 constexpr int NSLOT = 3;            // LDS ring depth
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-enum Kind { ROWS = 0, ROWS_CONV = 1, ROWS_GEN = 2, COLS = 3, COLS_CONV = 4 };
+// ROWS_CAT: [src0[rows0[r]] | src1[rows1[r]]] split at k_split (a multiple of the 64-deep stage),
+//           either gather optional -- the FAST form of the concatenation / gather operands
+enum Kind { ROWS = 0, ROWS_CONV = 1, ROWS_GEN = 2, COLS = 3, COLS_CONV = 4, ROWS_CAT = 5 };
 
 struct GemmDev {
   int M, N, K;
@@ -131,12 +133,13 @@ __device__ __forceinline__ float4 ldg4(const float* p) { return *reinterpret_cas
 // element by element with full bounds checks (edge shapes, gathers, concatenations).
 template <int KIND, bool FAST>
 struct Loader {
-  static constexpr bool kRowImg = KIND <= ROWS_GEN;
+  static constexpr bool kRowImg = KIND <= ROWS_GEN || KIND == ROWS_CAT;
   fx_operand o;        // by value: the address of a kernel argument would force it to scratch
   const float* base;   // operand base incl. batch offset
   int R, K, r0;
   int ta, tb;          // tid>>4, (tid&15)*4
-  int rowc[4];         // row-major: clamped row of j
+  int rowc[4];         // row-major: clamped row of j (ROWS_CAT: gathered row of the first source)
+  int rowc1[4];        // ROWS_CAT: gathered row of the second source
   int rmod[4];         // ROWS_CONV: row % seq_len of j
   unsigned rok;        // row-major: bit j = row j in range
   int rc;              // col-major: clamped first row of the 4
@@ -160,6 +163,11 @@ struct Loader {
         rok |= (r < R ? 1u : 0u) << j;
         rowc[j] = min(r, R - 1);
         if (KIND == ROWS_CONV) rmod[j] = rowc[j] % op.seq_len;
+        if (KIND == ROWS_CAT) {
+          const int rr = rowc[j];
+          rowc1[j] = op.rows1 ? op.rows1[rr] : rr;
+          rowc[j] = op.rows0 ? op.rows0[rr] : rr;
+        }
       }
     } else {
       // rows that exist in storage: all but a trailing virtual ones row
@@ -207,6 +215,15 @@ struct Loader {
         vm |= (ok ? 1u : 0u) << j;
         v[j] = ldg4(base + (long long)(ok ? rowc[j] + s : rowc[j]) * o.ld + c);
       }
+    } else if (KIND == ROWS_CAT) {
+      // the whole stage reads one source (k_split % 64 == 0): a uniform select of base / stride
+      const bool second = o.ptr1 && k0 >= o.k_split;
+      const float* src = second ? o.ptr1 : base;
+      const long long ld = second ? o.ld1 : o.ld;
+      const int kk = (second ? k0 - o.k_split : k0) + tb;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = ldg4(src + (long long)(second ? rowc1[j] : rowc[j]) * ld + kk);
+      vm = rok;
     } else if (KIND == COLS) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = ldg4(base + (long long)(k0 + ta + 16 * j) * o.ld + rc);
@@ -666,7 +683,8 @@ bool operand_vec_ok(const fx_operand& o) {
 int kind_of(const fx_operand& o, bool vec) {
   if (o.trans) return o.conv_taps ? COLS_CONV : COLS;
   if (o.conv_taps) return (vec && o.conv_cin % BK == 0) ? ROWS_CONV : ROWS_GEN;   // a stage stays in one tap
-  if (o.ptr1 || o.rows0 || o.rows1 || o.pos) return ROWS_GEN;
+  if (o.pos) return ROWS_GEN;
+  if (o.ptr1 || o.rows0 || o.rows1) return (vec && (!o.ptr1 || o.k_split % BK == 0)) ? ROWS_CAT : ROWS_GEN;
   return ROWS;
 }
 
@@ -684,7 +702,8 @@ int launch_b(int bk, dim3 grid, hipStream_t s, const GemmDev& g, bool fast) {
     case ROWS: launch_t<AK, ROWS>(grid, s, g, fast); return FX_OK;
     case COLS: launch_t<AK, COLS>(grid, s, g, fast); return FX_OK;
     case COLS_CONV: launch_t<AK, COLS_CONV>(grid, s, g, fast); return FX_OK;
-    case ROWS_GEN: launch_t<AK, ROWS_GEN>(grid, s, g, false); return FX_OK;
+    case ROWS_GEN:
+    case ROWS_CAT: launch_t<AK, ROWS_GEN>(grid, s, g, false); return FX_OK;
     default: break;
   }
   set_error("gemm: unsupported B operand kind");
@@ -698,6 +717,7 @@ int launch_tiled(int ak, int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
     case ROWS: return launch_b<ROWS>(bk, grid, s, g, fast);
     case ROWS_CONV: return launch_b<ROWS_CONV>(bk, grid, s, g, fast);
     case ROWS_GEN: return launch_b<ROWS_GEN>(bk, grid, s, g, false);
+    case ROWS_CAT: return launch_b<ROWS_CAT>(bk, grid, s, g, fast);
     case COLS: return launch_b<COLS>(bk, grid, s, g, fast);
     default: break;
   }
@@ -719,7 +739,8 @@ int launch_direct_b(int bk, dim3 grid, dim3 block, hipStream_t s, const GemmDev&
 int launch_direct(int ak, int bk, dim3 grid, dim3 block, hipStream_t s, const GemmDev& g) {
   switch (ak) {
     case ROWS: return launch_direct_b<ROWS>(bk, grid, block, s, g);
-    case ROWS_GEN: return launch_direct_b<ROWS_GEN>(bk, grid, block, s, g);
+    case ROWS_GEN:
+    case ROWS_CAT: return launch_direct_b<ROWS_GEN>(bk, grid, block, s, g);
     case COLS: return launch_direct_b<COLS>(bk, grid, block, s, g);
     default: break;
   }
@@ -736,7 +757,7 @@ bool use_direct(const fx_gemm_desc& d, int ak, int bk) {
     if (!p) return 0;
     return std::string(p) == "tiled" ? 1 : std::string(p) == "direct" ? 2 : 0;
   }();
-  const bool ok = (ak == ROWS || ak == ROWS_GEN || ak == COLS) && (bk == ROWS || bk == COLS);
+  const bool ok = (ak == ROWS || ak == ROWS_GEN || ak == ROWS_CAT || ak == COLS) && (bk == ROWS || bk == COLS);
   if (!ok || force == 1) return false;
   if (force == 2) return true;
   return d.M <= 32 || d.N <= 32 || d.K <= 64;

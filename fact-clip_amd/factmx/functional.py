@@ -121,6 +121,56 @@ def linear(x, w, b, relu=False):
     return LinearFn.apply(_2d(x), w, b, int(relu))
 
 
+class LinearPadKFn(torch.autograd.Function):
+    """nn.Linear for an in-feature count K that is not a multiple of the GEMM's 64-deep stage, on an
+    input that is a column slice of a wider row-major tensor (FeatureProjection's x[:, :H-C],
+    blocks.py:168-170): the GEMMs run over Kp = ceil64(K) against a zero-padded copy of W, so every
+    operand is 16-B vector-loadable (the extra input columns meet zero weights).  Same values as
+    the unpadded product (the padded terms are exact zeros)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, Kp):
+        M, K = x.shape
+        N = w.shape[0]
+        wp = torch.nn.functional.pad(w.detach(), (0, Kp - K))
+        y = _empty(M, N, device=x.device)
+        gemm(M, N, Kp, _rows_operand(x), _rows_operand(wp), y, N, bias=b)
+        ctx.save_for_backward(x, w, b, wp)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b, wp = ctx.saved_tensors
+        nd = ctx.needs_input_grad
+        dy = dy.contiguous()
+        M, K = x.shape
+        N = w.shape[0]
+        dx = None
+        if nd[0]:
+            dx = _empty(M, K, device=dy.device)
+            o = nx.Operand()
+            o.ptr, o.ld, o.trans, o.conv_dir = nx.ptr(wp), wp.shape[1], 1, 1
+            gemm(M, K, N, _rows_operand(dy), o, dx, K)
+        dwb, dw_ret = grad_target(w, nd[1])
+        dbb, db_ret = grad_target(b, nd[2])
+        if dwb is not None or dbb is not None:
+            lin_bwd(dy, x, w, False, dwb, dbb)
+        return dx, dw_ret, db_ret, None
+
+
+def linear_any_k(x, w, b):
+    """linear() that pads K to the 64-deep GEMM stage when x has the room to be read that wide."""
+    x2 = _2d(x)
+    M, K = x2.shape
+    Kp = (K + 63) // 64 * 64
+    if K % 64 == 0 or x2.stride(1) != 1 or x2.stride(0) < Kp or x2.stride(0) % 4 or x2.data_ptr() % 16:
+        return LinearFn.apply(x2, w, b, 0)
+    last = x2.storage_offset() + (M - 1) * x2.stride(0) + Kp
+    if last > x2.untyped_storage().nbytes() // x2.element_size():
+        return LinearFn.apply(x2, w, b, 0)
+    return LinearPadKFn.apply(x2, w, b, Kp)
+
+
 # ---------------------------------------------------------------------------
 # LayerNorm (+ fused residual, + fused ReLU)
 # ---------------------------------------------------------------------------

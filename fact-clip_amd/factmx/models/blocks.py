@@ -38,7 +38,7 @@ class FeatureProjection(nn.Module):
     def forward(self, feature):
         lin0, ln, _, drop, lin1 = self.projection
         shp = feature.shape
-        h = fxf.linear(feature, lin0.weight, lin0.bias)
+        h = fxf.linear_any_k(feature, lin0.weight, lin0.bias)
         h = fxf.layer_norm(h, ln.weight, ln.bias, ln.eps, relu=True)
         h = basic._dropout(h, drop.p, self.training)
         h = fxf.linear(h, lin1.weight, lin1.bias)

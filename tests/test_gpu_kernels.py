@@ -203,3 +203,25 @@ def test_library_reports_errors():
     lib = nx.load()
     st = lib.fx_layernorm_fwd(None, 0, None, 0, None, None, 1e-5, 4, 4096, 0, None, 0, None, 0, None, None)
     assert st != 0 and b"cols" in lib.fx_last_error()
+
+
+@pytest.mark.parametrize("M,K,N", [(300, 437, 512), (4096, 437, 512), (64, 70, 33)])
+def test_linear_padded_k_on_wider_input(M, K, N):
+    """LinearPadKFn (K not a multiple of 64, input a column slice of a wider tensor) vs float64."""
+    Kw = (K + 63) // 64 * 64 + 64
+    xw = _r(M, Kw, seed=40)
+    w = _r(N, K, seed=41, scale=K ** -0.5)
+    b = _r(N, seed=42)
+    g = _r(M, N, seed=43)
+    xwd = xw.float().to(DEV).requires_grad_(True)
+    wd, bd = w.float().to(DEV).requires_grad_(True), b.float().to(DEV).requires_grad_(True)
+    y = fxf.linear_any_k(xwd[:, :K], wd, bd)
+    (y * g.float().to(DEV)).sum().backward()
+    xr = xw.clone().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = xr[:, :K] @ wr.t() + br
+    (yr * g).sum().backward()
+    _close(y, yr, what="y")
+    _close(xwd.grad, xr.grad, rtol=1e-4, atol=1e-4, what="dx")
+    _close(wd.grad, wr.grad, rtol=1e-4, atol=1e-4, what="dw")
+    _close(bd.grad, br.grad, rtol=1e-4, atol=1e-4, what="db")
