@@ -129,50 +129,67 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* dy, long long 
   }
 }
 
-// token-sized LayerNorm backward (rows <= 64): ONE 1024-thread block, 16 waves over the rows, the
-// weight/bias gradient column sums reduced in LDS and accumulated (+=) in the same launch
+// token-sized LayerNorm backward (rows <= 64, cols <= 256): ONE 1024-thread block; each of the 16
+// waves owns rows w, w+16, w+32, w+48 and issues the loads of all of them up front (one memory
+// round trip instead of one per row), writes dx, and keeps per-column partial sums of the weight /
+// bias gradients that are reduced in LDS and accumulated (+=) in the same launch.
+constexpr int SMALL_RPW = 4;   // rows per wave
+constexpr int SMALL_CPL = 4;   // columns per lane (cols <= 256)
 __global__ __launch_bounds__(1024) void ln_bwd_small_kernel(const float* dy, long long lddy, const float* y,
                                                             long long ldy, const float* xhat, long long ldxh,
                                                             const float* w, const float* rstd, int rows, int cols,
                                                             int relu, float* dx, long long lddx, float* dw,
                                                             float* db) {
-  // one pass: each wave loads its rows once (registers), writes dx and keeps per-column partial
-  // sums; the 16 waves' partials are then reduced in LDS 64 columns at a time
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   __shared__ float red[16][2][64];
-  float pw[MAXPL], pb[MAXPL];
+  float d[SMALL_RPW][SMALL_CPL], h[SMALL_RPW][SMALL_CPL], wc[SMALL_CPL];
 #pragma unroll
-  for (int i = 0; i < MAXPL; ++i) pw[i] = pb[i] = 0.f;
-  for (int row = wv; row < rows; row += 16) {
-    float g[MAXPL], h[MAXPL];
-    float s1 = 0.f, s2 = 0.f;
+  for (int i = 0; i < SMALL_CPL; ++i) {
+    const int c = i * 64 + lane;
+    wc[i] = c < cols ? w[c] : 0.f;
+  }
 #pragma unroll
-    for (int i = 0; i < MAXPL; ++i) {
+  for (int q = 0; q < SMALL_RPW; ++q) {
+    const int row = wv + 16 * q;
+#pragma unroll
+    for (int i = 0; i < SMALL_CPL; ++i) {
       const int c = i * 64 + lane;
-      g[i] = h[i] = 0.f;
-      if (c < cols) {
-        float d = dy[(long long)row * lddy + c];
-        if (relu && !(y[(long long)row * ldy + c] > 0.f)) d = 0.f;
-        h[i] = xhat[(long long)row * ldxh + c];
-        pw[i] += d * h[i];
-        pb[i] += d;
-        g[i] = d * w[c];
-        s1 += g[i];
-        s2 += g[i] * h[i];
-      }
+      const bool ok = row < rows && c < cols;
+      float g = ok ? dy[(long long)row * lddy + c] : 0.f;
+      if (relu && ok && !(y[(long long)row * ldy + c] > 0.f)) g = 0.f;
+      d[q][i] = g;
+      h[q][i] = ok ? xhat[(long long)row * ldxh + c] : 0.f;
+    }
+  }
+  float pw[SMALL_CPL], pb[SMALL_CPL];
+#pragma unroll
+  for (int i = 0; i < SMALL_CPL; ++i) pw[i] = pb[i] = 0.f;
+#pragma unroll
+  for (int q = 0; q < SMALL_RPW; ++q) {
+    const int row = wv + 16 * q;
+    float s1 = 0.f, s2 = 0.f, g[SMALL_CPL];
+#pragma unroll
+    for (int i = 0; i < SMALL_CPL; ++i) {
+      pw[i] += d[q][i] * h[q][i];
+      pb[i] += d[q][i];
+      g[i] = d[q][i] * wc[i];
+      s1 += g[i];
+      s2 += g[i] * h[q][i];
     }
     s1 = wave_sum(s1) / cols;
     s2 = wave_sum(s2) / cols;
-    const float rs = rstd[row];
+    if (row < rows) {
+      const float rs = rstd[row];
 #pragma unroll
-    for (int i = 0; i < MAXPL; ++i) {
-      const int c = i * 64 + lane;
-      if (c < cols) dx[(long long)row * lddx + c] = rs * (g[i] - s1 - h[i] * s2);
+      for (int i = 0; i < SMALL_CPL; ++i) {
+        const int c = i * 64 + lane;
+        if (c < cols) dx[(long long)row * lddx + c] = rs * (g[i] - s1 - h[q][i] * s2);
+      }
     }
   }
   if (!dw && !db) return;
 #pragma unroll
-  for (int i = 0; i < MAXPL; ++i) {
+  for (int i = 0; i < SMALL_CPL; ++i) {
     if (i * 64 >= cols) break;
     red[wv][0][lane] = pw[i];
     red[wv][1][lane] = pb[i];
@@ -419,7 +436,7 @@ int launch_layernorm_bwd(const float* dy, long long lddy, const float* y, long l
                          float* dx, long long lddx, float* dw, float* db, float* ws, hipStream_t s) {
   FX_REQUIRE(cols > 0 && cols <= 64 * MAXPL, "layernorm: cols must be in (0, 1024]");
   if (rows == 0) return FX_OK;
-  if (rows <= 64) {
+  if (rows <= 16 * SMALL_RPW && cols <= 64 * SMALL_CPL) {
     hipLaunchKernelGGL(ln_bwd_small_kernel, dim3(1), dim3(1024), 0, s, dy, lddy, y, ldy, xhat, ldxh, w, rstd, rows,
                        cols, relu, dx, lddx, dw, db);
     FX_CHECK_HIP(hipGetLastError());

@@ -987,3 +987,87 @@ def decoder(mod, tgt, memory=None, pos=None, query_pos=None, nvid=1):
     mem = None if memory is None else _2d(memory)
     mp = None if pos is None else _2d(pos)
     return DecoderFn.apply(t2, qp, mem, mp, spec, int(nvid), *params)
+
+
+# ---------------------------------------------------------------------------
+# Fused loss terms (fx_class_loss_*, fx_attn_loss_*)
+# ---------------------------------------------------------------------------
+
+_loss_ws_cache = {}
+
+
+def _loss_ws(dev):
+    t = _loss_ws_cache.get(dev)
+    if t is None:
+        t = torch.empty(nx.load().fx_loss_workspace_floats(), device=dev)
+        _loss_ws_cache[dev] = t
+    return t
+
+
+class ClassLossFn(torch.autograd.Function):
+    """c_ce * sum_r CE(x_r; target_r, w) + c_sm * sum smooth terms of x (loss.py:8-18, 246-277) as one
+    scalar; hard int64 labels y or soft target rows z (R, C)."""
+
+    @staticmethod
+    def forward(ctx, x, y, z, w, c_ce, c_sm):
+        lib = nx.load()
+        R, C = x.shape
+        dev = x.device
+        lse = _empty(R, device=dev)
+        out = _empty(1, device=dev)
+        _check(lib.fx_class_loss_fwd(nx.ptr(x), x.stride(0), x.stride(1), R, C, nx.ptr(y), nx.ptr(z), nx.ptr(w),
+                                     float(c_ce), float(c_sm), nx.ptr(lse), nx.ptr(out), nx.ptr(_loss_ws(dev)),
+                                     nx.stream()), "fx_class_loss_fwd")
+        ctx.c = (float(c_ce), float(c_sm))
+        ctx.save_for_backward(x, y, z, w, lse)
+        return out.reshape(())
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = nx.load()
+        x, y, z, w, lse = ctx.saved_tensors
+        R, C = x.shape
+        g = g.reshape(1).contiguous()
+        dx = _empty(R, C, device=x.device)
+        _check(lib.fx_class_loss_bwd(nx.ptr(x), x.stride(0), x.stride(1), R, C, nx.ptr(y), nx.ptr(z), nx.ptr(w),
+                                     nx.ptr(lse), ctx.c[0], ctx.c[1], nx.ptr(g), nx.ptr(dx), nx.stream()),
+               "fx_class_loss_bwd")
+        return dx, None, None, None, None, None
+
+
+class AttnLossFn(torch.autograd.Function):
+    """c_xe * cross-attention CE over the matched columns (loss.py:209-244) + c_sm * smooth terms of
+    the attention logits, as one scalar.  ``L`` (R, Q) may be any strided view."""
+
+    @staticmethod
+    def forward(ctx, L, z, a_idx, s_idx, sweight, axis, c_xe, c_sm):
+        lib = nx.load()
+        R, Q = L.shape
+        dev = L.device
+        K, S = len(a_idx), z.shape[1]
+        ai, si, sw = nx.int_array(a_idx), nx.int_array(s_idx), nx.float_array(sweight)
+        lse_sel = _empty(max(R if axis == 1 else K, 1), device=dev)
+        lse_full = _empty(R, device=dev) if c_sm else None
+        colz = _empty(max(K, 1), device=dev) if axis == 0 else None
+        out = _empty(1, device=dev)
+        _check(lib.fx_attn_loss_fwd(nx.ptr(L), L.stride(0), L.stride(1), R, Q, K, ai, si, sw, nx.ptr(z), S, axis,
+                                    float(c_xe), float(c_sm), nx.ptr(lse_sel), nx.ptr(lse_full), nx.ptr(colz),
+                                    nx.ptr(out), nx.ptr(_loss_ws(dev)), nx.stream()), "fx_attn_loss_fwd")
+        ctx.args = (list(a_idx), list(s_idx), list(sweight), axis, float(c_xe), float(c_sm))
+        ctx.save_for_backward(L, z, lse_sel, lse_full, colz)
+        return out.reshape(())
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = nx.load()
+        L, z, lse_sel, lse_full, colz = ctx.saved_tensors
+        a_idx, s_idx, sweight, axis, c_xe, c_sm = ctx.args
+        R, Q = L.shape
+        g = g.reshape(1).contiguous()
+        # gradient in the input view's memory order (a transposed view gets a transposed buffer)
+        dL = _empty(Q, R, device=L.device).t() if (L.stride(0) == 1 and Q > 1) else _empty(R, Q, device=L.device)
+        _check(lib.fx_attn_loss_bwd(nx.ptr(L), L.stride(0), L.stride(1), R, Q, len(a_idx), nx.int_array(a_idx),
+                                    nx.int_array(s_idx), nx.float_array(sweight), nx.ptr(z), z.shape[1], axis,
+                                    nx.ptr(lse_sel), nx.ptr(lse_full), nx.ptr(colz), c_xe, c_sm, nx.ptr(g),
+                                    nx.ptr(dL), dL.stride(0), dL.stride(1), nx.stream()), "fx_attn_loss_bwd")
+        return dL, None, None, None, None, None, None, None

@@ -156,10 +156,10 @@ class InputBlock(Block):
         return f_out, a_out
 
     def compute_loss(self, criterion, match=None):
-        fl = criterion.frame_loss(self.frame_clogit.squeeze(1))
+        """blocks.py:313-320: frame CE + token CE + sw * smooth(frame logits); the frame CE and its
+        smooth term are one fused kernel pair."""
         atk = criterion.action_token_loss(match, self.action_clogit)
-        sm = loss_mod.smooth_loss(self.frame_clogit.transpose(0, 1))
-        return fl + atk + self.cfg.Loss.sw * sm
+        return criterion.frame_terms(self.frame_clogit, 1.0, self.cfg.Loss.sw) + atk
 
 
 class UpdateBlock(Block):
@@ -213,14 +213,14 @@ class UpdateBlock(Block):
         return f_out, a_out
 
     def compute_loss(self, criterion, match=None):
-        fl = criterion.frame_loss(self.frame_clogit.squeeze(1))
+        """blocks.py:369-382: token CE + f2a / a2f cross-attention CE + frame CE + sw * (smooth of both
+        attention logits and the frame logits), as three fused terms + the token CE."""
+        sw = self.cfg.Loss.sw
         atk = criterion.action_token_loss(match, self.action_clogit)
         f2a_t = self.f2a_attn_logit.transpose(1, 2)
-        f2a = criterion.cross_attn_loss(match, f2a_t, dim=1)
-        a2f = criterion.cross_attn_loss(match, self.a2f_attn_logit, dim=2)
-        sm = (loss_mod.smooth_loss(self.a2f_attn_logit) + loss_mod.smooth_loss(f2a_t)
-              + loss_mod.smooth_loss(self.frame_clogit.transpose(0, 1)))
-        return atk + f2a + a2f + fl + self.cfg.Loss.sw * sm
+        f2a = criterion.attn_terms(match, f2a_t, axis=0, xe_coef=1.0, sm_coef=sw)
+        a2f = criterion.attn_terms(match, self.a2f_attn_logit, axis=1, xe_coef=1.0, sm_coef=sw)
+        return atk + f2a + a2f + criterion.frame_terms(self.frame_clogit, 1.0, sw)
 
 
 class UpdateBlockTDU(Block):
@@ -321,13 +321,13 @@ class UpdateBlockTDU(Block):
         return f_out, a_out
 
     def compute_loss(self, criterion, match=None):
-        fl = criterion.frame_loss(self.frame_clogit.squeeze(1))
-        sl = criterion.frame_loss_tdu(self.seg_clogit, self.tdu)
+        """blocks.py:487-497: (frame CE + segment CE) / 2 + token CE + segment-level f2a / a2f
+        cross-attention CE + sw * smooth(frame logits), as four fused terms + the token CE."""
         atk = criterion.action_token_loss(match, self.action_clogit)
-        f2a = criterion.cross_attn_loss_tdu(match, self.f2a_attn_logit.transpose(1, 2), self.tdu, dim=1)
-        a2f = criterion.cross_attn_loss_tdu(match, self.a2f_attn_logit, self.tdu, dim=2)
-        sm = loss_mod.smooth_loss(self.frame_clogit.transpose(0, 1))
-        return (fl + sl) / 2 + atk + f2a + a2f + self.cfg.Loss.sw * sm
+        f2a = criterion.attn_terms(match, self.f2a_attn_logit.transpose(1, 2), axis=0, tdu=self.tdu)
+        a2f = criterion.attn_terms(match, self.a2f_attn_logit, axis=1, tdu=self.tdu)
+        return (criterion.frame_terms(self.frame_clogit, 0.5, self.cfg.Loss.sw)
+                + criterion.seg_terms(self.seg_clogit, self.tdu, 0.5) + atk + f2a + a2f)
 
 
 def _build_blocks(cfg, in_dim, n_classes):

@@ -11,6 +11,7 @@ import torch
 import torch.nn.functional as F
 from scipy.optimize import linear_sum_assignment
 
+from .. import functional as fxf
 from . import basic
 from .basic import torch_class_label_to_segment_label, logit2prob  # noqa: F401  (re-exported like loss.py:20,38)
 
@@ -79,6 +80,15 @@ class MatchCriterion:
             self.transcript, self.seg_label = torch_class_label_to_segment_label(label)
             self._transcript_np = None
         S = int(self.transcript.shape[0])
+        self._sweight_np = None
+        if self._transcript_np is not None:
+            if self._class_weight is not None:
+                self._sweight_np = np.asarray(self._class_weight, dtype=np.float32)[self._transcript_np]
+            else:
+                swn = np.ones(S, dtype=np.float32)
+                for i in self.bg_ids:
+                    swn[self._transcript_np == i] = self.cfg.Loss.bgw
+                self._sweight_np = swn
         self.onehot_class_label = _onehot(label, self.nclasses)
         self.onehot_seg_label = _onehot(self.seg_label, S)
         cw = torch.ones(self.nclasses + 1, device=dev)
@@ -193,6 +203,50 @@ class MatchCriterion:
         aind, sind = self._dev_match(match, attn.device)
         z = _zoom(tdu, self.onehot_seg_label)
         return self._attn_xent(attn[0, :, aind], z[:, sind], dim, z.sum())
+
+    # ---------------- fused forms (one HIP launch pair per term group; same values) ----------------
+    def frame_terms(self, frame_clogit, ce_coef=1.0, sm_coef=0.0):
+        """ce_coef * frame_loss(frame_clogit) + sm_coef * smooth_loss(frame_clogit^T)
+        (loss.py:246-258 and 8-18 on the same logits) as one fused term."""
+        x = frame_clogit.squeeze(1) if frame_clogit.dim() == 3 else frame_clogit
+        if not x.is_cuda:
+            return ce_coef * self.frame_loss(x) + sm_coef * smooth_loss(x.unsqueeze(0))
+        R, C = x.shape
+        c_sm = (sm_coef / ((R - 1) * C) if R > 1 else float("inf")) if sm_coef else 0.0
+        return fxf.ClassLossFn.apply(x, self.class_label.to(torch.int64).contiguous(), None, self.cweight[:C],
+                                     ce_coef / float(R), c_sm)
+
+    def seg_terms(self, seg_clogit, tdu, ce_coef=1.0):
+        """ce_coef * frame_loss_tdu(seg_clogit, tdu) (loss.py:260-277) as one fused term."""
+        x = seg_clogit.squeeze(1) if seg_clogit.dim() == 3 else seg_clogit
+        if not x.is_cuda:
+            return ce_coef * self.frame_loss_tdu(seg_clogit, tdu)
+        z = _zoom(tdu, self.onehot_class_label).contiguous()
+        return fxf.ClassLossFn.apply(x, None, z, self.cweight[:x.shape[1]], ce_coef / float(x.shape[0]), 0.0)
+
+    def attn_terms(self, match, attn, axis, tdu=None, xe_coef=1.0, sm_coef=0.0):
+        """xe_coef * cross_attn_loss(_tdu)(match, attn) + sm_coef * smooth_loss(attn) (loss.py:209-244,
+        8-18) as one fused term.  ``attn`` is the (1, R, Q) logit view the reference passes;
+        ``axis`` = dim - 1 of the reference call."""
+        L = attn[0]
+        aind, sind = match
+        K = int(aind.numel())
+        swn = getattr(self, "_sweight_np", None)
+        if (not L.is_cuda) or swn is None or K > 64:
+            z = None if tdu is None else _zoom(tdu, self.onehot_seg_label)
+            xe = (self.cross_attn_loss(match, attn, dim=axis + 1) if tdu is None else
+                  self.cross_attn_loss_tdu(match, attn, tdu, dim=axis + 1))
+            return xe_coef * xe + (sm_coef * smooth_loss(attn) if sm_coef else 0.0)
+        if len(swn) not in (K, 1):
+            raise RuntimeError(f"cross_attn_loss: {K} matched columns vs {len(swn)} segment weights")
+        sw = [float(swn[i if len(swn) == K else 0]) for i in range(K)]
+        if tdu is None:
+            z, denom = self.onehot_seg_label, float(L.shape[0])
+        else:
+            z, denom = _zoom(tdu, self.onehot_seg_label), float(tdu.num_seg)
+        R, Q = L.shape
+        c_sm = (sm_coef / ((R - 1) * Q) if R > 1 else float("inf")) if sm_coef else 0.0
+        return fxf.AttnLossFn.apply(L, z.contiguous(), aind.tolist(), sind.tolist(), sw, axis, xe_coef / denom, c_sm)
 
     def frame_loss(self, frame_clogit, is_logit=True):
         """loss.py:246-258."""

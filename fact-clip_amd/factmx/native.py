@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FACTMX_LIB", os.path.join(_HERE, "_lib", "libfactmx.so"))
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -116,6 +116,11 @@ SIGNATURES = {
     "fx_grad_norm": (I, [P, L, P, P, P]),
     "fx_clip_grad_scale": (I, [P, L, P, F, P]),
     "fx_adam_step": (I, [P, P, P, P, L, L, F, F, F, F, F, F, P, P, P]),
+    "fx_loss_workspace_floats": (L, []),
+    "fx_class_loss_fwd": (I, [P, L, L, I, I, P, P, P, F, F, P, P, P, P]),
+    "fx_class_loss_bwd": (I, [P, L, L, I, I, P, P, P, P, F, F, P, P, P]),
+    "fx_attn_loss_fwd": (I, [P, L, L, I, I, I, P, P, P, P, I, I, F, F, P, P, P, P, P, P]),
+    "fx_attn_loss_bwd": (I, [P, L, L, I, I, I, P, P, P, P, I, I, P, P, P, F, F, P, P, L, L, P]),
     "fx_prof_enable": (I, [I, I]),
     "fx_prof_collect": (I, [I, ctypes.POINTER(D), ctypes.POINTER(D), ctypes.POINTER(D), ctypes.POINTER(I)]),
     "fx_prof_disable": (None, []),
@@ -144,6 +149,13 @@ def load(path=None):
         raise FactmxNativeError(f"libfactmx ABI {v} != expected {ABI_VERSION}")
     _lib = lib
     return lib
+
+
+def float_array(vals):
+    """Host float32 array for the C ABI (None -> NULL)."""
+    if vals is None:
+        return None
+    return (ctypes.c_float * max(len(vals), 1))(*[float(v) for v in vals])
 
 
 def int_array(vals):

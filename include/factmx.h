@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FX_ABI_VERSION 5
+#define FX_ABI_VERSION 6
 
 enum {
   FX_OK = 0,
@@ -409,6 +409,40 @@ int fx_clip_grad_scale(float* g, long long n, const float* workspace, float max_
 int fx_adam_step(float* p, float* g, float* m, float* v, long long n, long long step, float lr,
                  float beta1, float beta2, float eps, float weight_decay, float max_norm,
                  float* workspace, float* norm_out, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Fused loss terms (fact_clip/models/loss.py); each returns ONE scalar
+ *   out = c_ce * sum(CE terms) + c_sm * sum(smooth terms)
+ * (the caller folds 1/denominator, 1/count and the term's weight into c_*; c_sm == 0 skips
+ * the smooth term).  workspace: fx_loss_workspace_floats().  Backward reads the upstream
+ * scalar gradient from device memory (gout) and writes the whole logit gradient.
+ * fx_class_loss_*: frame_loss (loss.py:246-258) / frame_loss_tdu (260-277) with hard labels
+ *   y (int64, R) or soft targets z (R, C); smooth_loss (loss.py:8-18) on the same logits
+ *   (log_softmax over C, difference over rows).  x (R, C) element (r,c) at x[r*sr + c*sc];
+ *   lse (R) saved by the forward; dx written dense (R, C).
+ * fx_attn_loss_*: cross_attn_loss (loss.py:209-222) / cross_attn_loss_tdu (224-244): the K
+ *   matched token columns a_idx (host, K <= 64) against target columns z[:, s_idx] (z dense
+ *   (R, S)), per-column weights sweight (host), log_softmax over the selected columns of each
+ *   row (axis 1) or over the rows of each selected column (axis 0); optional smooth_loss over
+ *   all Q columns.  lse_sel ((R) for axis 1, (K) for axis 0), lse_full (R), colz (K) saved;
+ *   dL written with strides (dsr, dsc).
+ * ---------------------------------------------------------------------- */
+long long fx_loss_workspace_floats(void);
+int fx_class_loss_fwd(const float* x, long long sr, long long sc, int R, int C, const long long* y,
+                      const float* z, const float* w, float c_ce, float c_sm, float* lse, float* out,
+                      float* workspace, void* stream);
+int fx_class_loss_bwd(const float* x, long long sr, long long sc, int R, int C, const long long* y,
+                      const float* z, const float* w, const float* lse, float c_ce, float c_sm,
+                      const float* gout, float* dx, void* stream);
+int fx_attn_loss_fwd(const float* L, long long sr, long long sc, int R, int Q, int K,
+                     const int* a_idx, const int* s_idx, const float* sweight, const float* z, int S,
+                     int axis, float c_xe, float c_sm, float* lse_sel, float* lse_full, float* colz,
+                     float* out, float* workspace, void* stream);
+int fx_attn_loss_bwd(const float* L, long long sr, long long sc, int R, int Q, int K,
+                     const int* a_idx, const int* s_idx, const float* sweight, const float* z, int S,
+                     int axis, const float* lse_sel, const float* lse_full, const float* colz,
+                     float c_xe, float c_sm, const float* gout, float* dL, long long dsr,
+                     long long dsc, void* stream);
 
 /* ------------------------------------------------------------------------
  * Profiling hooks: HIP-event timing of every launch of one kernel class
