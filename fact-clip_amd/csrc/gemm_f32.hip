@@ -528,6 +528,186 @@ __global__ __launch_bounds__(NTHREADS) void gemm_f32_kernel(GemmDev g) {
   FX_STAMP(g, 3);
 }
 
+// ---------------------------------------------------------------- wide tile (128 x 64)
+// The 64x64 tile moves 32 KB per 64-deep stage for 0.5 MFLOP: at the f32 MFMA rate that is ~32 B/clk
+// per CU, i.e. the XCD L2 bandwidth, so that kernel is L2-bound near 40 % of peak.  Here a block
+// owns 128 rows x 64 cols: two 64x64 A stages (the same loaders, rows m0 and m0+64) and one B stage
+// per step, 48 KB for 1 MFLOP (1.5x the intensity).  Wave w computes rows 64*(w>>1) .. +63 (two
+// 32x32 sub-tiles sharing one B fragment) of columns 32*(w&1) .. +31: per stage 64 MFMAs (4096
+// matrix-core cycles) per wave.  LDS: 3-slot ring of [A0 | A1 | B] images = 153 KB, one block
+// per CU, one wave per SIMD.  FAST operands only (chosen on the host).
+constexpr int WBM = 128;
+template <int AK, int BKd>
+__device__ __forceinline__ void wide_stage(const Loader<AK, true>& la0, const Loader<AK, true>& la1,
+                                           const Loader<BKd, true>& lb, const float* cur, float* wslot, int kload,
+                                           const float4* rs0, const float4* rs1, const float4* rsb, unsigned ms0,
+                                           unsigned ms1, unsigned msb, float4* rn0, float4* rn1, float4* rnb,
+                                           unsigned& mn0, unsigned& mn1, unsigned& mnb, int wm, int wn, int li,
+                                           int lh, f32x16& acc0, f32x16& acc1) {
+  using LA = Loader<AK, true>;
+  using LB = Loader<BKd, true>;
+  la0.load(kload, rn0, mn0);
+  la1.load(kload, rn1, mn1);
+  lb.load(kload, rnb, mnb);
+  __builtin_amdgcn_sched_barrier(0);
+  const float* ia = cur + wm * IMG;
+  const float* ib = cur + 2 * IMG;
+  float4 f0[8], f1[8], fb[8];
+  f0[0] = LA::frag(ia, 0, li, lh, 0);
+  f1[0] = LA::frag(ia, 32, li, lh, 0);
+  fb[0] = LB::frag(ib, wn * 32, li, lh, 0);
+  f0[1] = LA::frag(ia, 0, li, lh, 1);
+  f1[1] = LA::frag(ia, 32, li, lh, 1);
+  fb[1] = LB::frag(ib, wn * 32, li, lh, 1);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(f0[q].x, fb[q].x, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(f1[q].x, fb[q].x, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(f0[q].y, fb[q].y, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(f1[q].y, fb[q].y, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(f0[q].z, fb[q].z, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(f1[q].z, fb[q].z, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(f0[q].w, fb[q].w, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(f1[q].w, fb[q].w, acc1, 0, 0, 0);
+    if (q + 2 < 8) {
+      f0[q + 2] = LA::frag(ia, 0, li, lh, q + 2);
+      f1[q + 2] = LA::frag(ia, 32, li, lh, q + 2);
+      fb[q + 2] = LB::frag(ib, wn * 32, li, lh, q + 2);
+    }
+    if (q == 1) la0.store(wslot, rs0, ms0);
+    if (q == 3) la1.store(wslot + IMG, rs1, ms1);
+    if (q == 5) lb.store(wslot + 2 * IMG, rsb, msb);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int AK, int BKd>
+__device__ __forceinline__ void wide_kloop(const Loader<AK, true>& la0, const Loader<AK, true>& la1,
+                                           const Loader<BKd, true>& lb, float* lds, int kt0, int kt1, int wm, int wn,
+                                           int li, int lh, f32x16& acc0, f32x16& acc1) {
+  const int n = kt1 - kt0;
+  if (n <= 0) return;
+  const int klast = (kt1 - 1) * BK;
+  constexpr int SLOT = 3 * IMG;
+  float4 a0x[4], a1x[4], bx[4], a0y[4], a1y[4], by[4];
+  unsigned m0x, m1x, mbx, m0y, m1y, mby;
+  la0.load(kt0 * BK, a0x, m0x);
+  la1.load(kt0 * BK, a1x, m1x);
+  lb.load(kt0 * BK, bx, mbx);
+  la0.load(min((kt0 + 1) * BK, klast), a0y, m0y);
+  la1.load(min((kt0 + 1) * BK, klast), a1y, m1y);
+  lb.load(min((kt0 + 1) * BK, klast), by, mby);
+  la0.store(lds, a0x, m0x);
+  la1.store(lds + IMG, a1x, m1x);
+  lb.store(lds + 2 * IMG, bx, mbx);
+  la0.store(lds + SLOT, a0y, m0y);
+  la1.store(lds + SLOT + IMG, a1y, m1y);
+  lb.store(lds + SLOT + 2 * IMG, by, mby);
+  la0.load(min((kt0 + 2) * BK, klast), a0x, m0x);
+  la1.load(min((kt0 + 2) * BK, klast), a1x, m1x);
+  lb.load(min((kt0 + 2) * BK, klast), bx, mbx);
+  __syncthreads();
+  int slot = 0;
+  auto iter = [&](int i, const float4* s0, const float4* s1, const float4* sb, unsigned q0, unsigned q1, unsigned qb,
+                  float4* n0, float4* n1, float4* nb, unsigned& p0, unsigned& p1, unsigned& pb) FX_INLINE {
+    const int ws = slot == 0 ? 2 : slot - 1;
+    wide_stage<AK, BKd>(la0, la1, lb, lds + slot * SLOT, lds + ws * SLOT, min((kt0 + i + 3) * BK, klast), s0, s1, sb,
+                        q0, q1, qb, n0, n1, nb, p0, p1, pb, wm, wn, li, lh, acc0, acc1);
+    __syncthreads();
+    slot = slot == 2 ? 0 : slot + 1;
+  };
+  int i = 0;
+  for (; i + 1 < n; i += 2) {
+    iter(i, a0x, a1x, bx, m0x, m1x, mbx, a0y, a1y, by, m0y, m1y, mby);
+    iter(i + 1, a0y, a1y, by, m0y, m1y, mby, a0x, a1x, bx, m0x, m1x, mbx);
+  }
+  if (i < n) iter(i, a0x, a1x, bx, m0x, m1x, mbx, a0y, a1y, by, m0y, m1y, mby);
+}
+
+__device__ __forceinline__ void tile_epilogue(const GemmDev& g, int bidx, int rbase, int col, const f32x16& acc) {
+  if (col >= g.N) return;
+  if (!g.c_last && !g.c_tap_cin && !g.gate && g.beta == 0.f) {
+    const float bv = g.bias ? g.bias[col] : 0.f;
+    float res[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = rbase + (r & 3) + 8 * (r >> 2);
+      res[r] = (g.resid && row < g.M) ? g.resid[(long long)bidx * g.resid_bs + (long long)row * g.ld_resid + col]
+                                      : 0.f;
+    }
+    float* cb = g.c + (long long)bidx * g.c_bs + col;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = rbase + (r & 3) + 8 * (r >> 2);
+      float v = g.alpha * acc[r] + bv;
+      if (g.relu == 2) v = fmaxf(v, 0.f);
+      v += res[r];
+      if (g.relu == 1) v = fmaxf(v, 0.f);
+      if (row < g.M) cb[(long long)row * g.ldc] = v;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = rbase + (r & 3) + 8 * (r >> 2);
+      if (row < g.M) epilogue_store(g, bidx, row, col, acc[r]);
+    }
+  }
+}
+
+template <int AK, int BKIND>
+__global__ __launch_bounds__(NTHREADS) void gemm_f32_wide_kernel(GemmDev g) {
+  __shared__ float lds[NSLOT * 3 * IMG];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, li = lane & 31, lh = lane >> 5;
+  int tx, ty;
+  {
+    const int nt = g.tiles_x * g.tiles_y;
+    const int id = blockIdx.y * g.tiles_x + blockIdx.x;
+    const int q = nt / 8, rr = nt % 8, x8 = id % 8, i8 = id / 8;
+    const int nid = (x8 < rr ? x8 * (q + 1) : rr * (q + 1) + (x8 - rr) * q) + i8;
+    ty = nid / g.tiles_x;
+    tx = nid - ty * g.tiles_x;
+  }
+  const int n0 = tx * BN, m0 = ty * WBM;
+  const int z = blockIdx.z, bidx = z / g.split, sk = z - bidx * g.split;
+  const int nkt = (g.K + BK - 1) / BK;
+  const int kt0 = sk * g.kt_per_split;
+  const int kt1 = min(nkt, kt0 + g.kt_per_split);
+  Loader<AK, true> la0, la1;
+  Loader<BKIND, true> lb;
+  const float* pa = g.a.ptr + (long long)bidx * g.a.batch_stride;
+  la0.init(g.a, pa, m0, g.M, g.K, tid);
+  la1.init(g.a, pa, m0 + BM, g.M, g.K, tid);
+  lb.init(g.b, g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid);
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    acc0[i] = 0.f;
+    acc1[i] = 0.f;
+  }
+  wide_kloop<AK, BKIND>(la0, la1, lb, lds, kt0, kt1, wm, wn, li, lh, acc0, acc1);
+  const int col = n0 + wn * 32 + li;
+  const int rb0 = m0 + wm * 64 + 4 * lh, rb1 = rb0 + 32;
+  if (g.split > 1) {
+    if (col < g.N) {
+      float* slab = g.ws + ((long long)bidx * g.split + sk) * g.M * (long long)g.N;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row0 = rb0 + (r & 3) + 8 * (r >> 2), row1 = row0 + 32;
+        if (row0 < g.M) slab[(long long)row0 * g.N + col] = acc0[r];
+        if (row1 < g.M) slab[(long long)row1 * g.N + col] = acc1[r];
+      }
+    }
+    if (g.tile_cnt)
+      splitk_finish<WBM, BN>(g, bidx, m0, n0, (bidx * g.tiles_y + ty) * g.tiles_x + tx,
+                             reinterpret_cast<int*>(&lds[NSLOT * 3 * IMG - 1]));
+    return;
+  }
+  tile_epilogue(g, bidx, rb0, col, acc0);
+  tile_epilogue(g, bidx, rb1, col, acc1);
+}
+
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmDev g) {
   const long long total = (long long)g.M * g.N;
   const int bidx = blockIdx.y;
@@ -564,13 +744,23 @@ __device__ __forceinline__ void dload(const fx_operand& o, const float* base, in
       }
       return;
     }
+    // edge chunk: clamped, unconditional loads (all 16 in flight at once), zeroed by select
+    const int rc = min(r, R - 1);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = (r < R && k0 + j < K) ? base[(long long)r * o.ld + k0 + j] : 0.f;
+    for (int j = 0; j < 16; ++j) {
+      const float x = base[(long long)rc * o.ld + min(k0 + j, K - 1)];
+      v[j] = (r < R && k0 + j < K) ? x : 0.f;
+    }
   } else if (KIND == COLS) {
+    // clamped, unconditional loads so the compiler issues all 16 before the first wait (the ones
+    // column is a virtual operand column: its row index is clamped too and the value replaced)
     const bool ones = o.ones_col && r == o.ones_col - 1;
+    const int rc = max(min(r, o.ones_col ? o.ones_col - 2 : R - 1), 0);
 #pragma unroll
-    for (int j = 0; j < 16; ++j)
-      v[j] = (r < R && k0 + j < K) ? (ones ? 1.f : base[(long long)(k0 + j) * o.ld + r]) : 0.f;
+    for (int j = 0; j < 16; ++j) {
+      const float x = base[(long long)min(k0 + j, K - 1) * o.ld + rc];
+      v[j] = (r < R && k0 + j < K) ? (ones ? 1.f : x) : 0.f;
+    }
   } else {  // ROWS_GEN
 #pragma unroll
     for (int j = 0; j < 16; ++j) v[j] = (r < R && k0 + j < K) ? fetch_rm(o, base, r, k0 + j) : 0.f;
@@ -697,6 +887,32 @@ void launch_t(dim3 grid, hipStream_t s, const GemmDev& g, bool fast) {
 }
 
 template <int AK>
+int launch_wide_b(int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
+  switch (bk) {
+    case ROWS: hipLaunchKernelGGL((gemm_f32_wide_kernel<AK, ROWS>), grid, dim3(NTHREADS), 0, s, g); return FX_OK;
+    case COLS: hipLaunchKernelGGL((gemm_f32_wide_kernel<AK, COLS>), grid, dim3(NTHREADS), 0, s, g); return FX_OK;
+    case COLS_CONV:
+      hipLaunchKernelGGL((gemm_f32_wide_kernel<AK, COLS_CONV>), grid, dim3(NTHREADS), 0, s, g);
+      return FX_OK;
+    default: break;
+  }
+  set_error("gemm(wide): unsupported B operand kind");
+  return FX_ERR_UNSUPPORTED;
+}
+
+int launch_wide(int ak, int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
+  switch (ak) {
+    case ROWS: return launch_wide_b<ROWS>(bk, grid, s, g);
+    case ROWS_CONV: return launch_wide_b<ROWS_CONV>(bk, grid, s, g);
+    case ROWS_CAT: return launch_wide_b<ROWS_CAT>(bk, grid, s, g);
+    case COLS: return launch_wide_b<COLS>(bk, grid, s, g);
+    default: break;
+  }
+  set_error("gemm(wide): unsupported A operand kind");
+  return FX_ERR_UNSUPPORTED;
+}
+
+template <int AK>
 int launch_b(int bk, dim3 grid, hipStream_t s, const GemmDev& g, bool fast) {
   switch (bk) {
     case ROWS: launch_t<AK, ROWS>(grid, s, g, fast); return FX_OK;
@@ -748,8 +964,9 @@ int launch_direct(int ak, int bk, dim3 grid, dim3 block, hipStream_t s, const Ge
   return FX_ERR_UNSUPPORTED;
 }
 
-// Small problems go to the direct kernel: token-level (M or N <= 32) or shallow K.  (Few-tile
-// frame-level dW GEMMs with K = T stay tiled: measured 25 vs 32 us at 256x257x4096.)  Conv-gather operands always take the tiled kernel.
+// Small problems go to the direct kernel: token-level (M or N <= 64: the Nact tokens of one or two
+// lockstep videos) or shallow K.  (Few-tile frame-level dW GEMMs with K = T stay tiled: measured
+// 25 vs 32 us at 256x257x4096.)  Conv-gather operands always take the tiled kernel.
 // FX_GEMM_PATH=tiled|direct overrides the choice (diagnostic).
 bool use_direct(const fx_gemm_desc& d, int ak, int bk) {
   static const int force = [] {
@@ -760,7 +977,22 @@ bool use_direct(const fx_gemm_desc& d, int ak, int bk) {
   const bool ok = (ak == ROWS || ak == ROWS_GEN || ak == ROWS_CAT || ak == COLS) && (bk == ROWS || bk == COLS);
   if (!ok || force == 1) return false;
   if (force == 2) return true;
-  return d.M <= 32 || d.N <= 32 || d.K <= 64;
+  return d.M <= 64 || d.N <= 64 || d.K <= 64;
+}
+
+// 128x64 tiles where the launch still has ~3/4 of a block per CU: FAST operands only.
+// FX_GEMM_WIDE=0|1 forces the choice among eligible launches (diagnostic).
+bool use_wide(const GemmDev& g, int ak, int bk, int batch) {
+  static const int force = [] {
+    const char* p = std::getenv("FX_GEMM_WIDE");
+    return p ? (p[0] == '1' ? 1 : 0) : -1;
+  }();
+  const bool fast = g.a_vec && g.b_vec && (g.K % BK) == 0;
+  const bool ok = fast && (ak == ROWS || ak == ROWS_CONV || ak == ROWS_CAT || ak == COLS) &&
+                  (bk == ROWS || bk == COLS || bk == COLS_CONV);
+  if (!ok || force == 0) return false;
+  if (force == 1) return true;
+  return (long long)cdiv(g.M, WBM) * g.tiles_x * batch * g.split >= 192;
 }
 
 // Split-K arrival counters, one pool per (device, stream): zeroed once at allocation and
@@ -858,6 +1090,7 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
   g.ws = d.workspace;
   const int ak = kind_of(d.a, g.a_vec), bk = kind_of(d.b, g.b_vec);
   const bool direct = use_direct(d, ak, bk);
+  bool wide = false;
   const int cap = (d.split_k > 1 && d.workspace) ? d.split_k : 1;   // workspace holds `cap` slabs
   FX_REQUIRE(!(d.split_k > 1 && !d.workspace), "gemm: split-K needs a workspace");
   dim3 grid, block;
@@ -882,13 +1115,14 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
     g.kt_per_split = nkt > 0 ? cdiv(nkt, split) : 0;
     g.split = g.kt_per_split > 0 ? cdiv(nkt, g.kt_per_split) : 1;
     g.tiles_x = cdiv(d.N, BN);
-    g.tiles_y = cdiv(d.M, BM);
+    wide = use_wide(g, ak, bk, d.batch);
+    g.tiles_y = cdiv(d.M, wide ? WBM : BM);
     grid = dim3(g.tiles_x, g.tiles_y, d.batch * g.split);
     block = dim3(NTHREADS);
   }
   // in-launch reduction only while the last block's serial slab read stays small (<= 32 KB per
   // tile); bigger ones pay less as a separate reduce launch (conv dW split 5: 78 vs 56 us)
-  const long long slab_bytes = (long long)g.split * (direct ? 32 * 32 : BM * BN) * 4;
+  const long long slab_bytes = (long long)g.split * (direct ? 32 * 32 : (wide ? WBM : BM) * BN) * 4;
   if (g.split > 1 && slab_bytes <= 32768 && (long long)g.tiles_x * g.tiles_y * d.batch <= kMaxTileCounters)
     g.tile_cnt = tile_counters(s);
   // FX_GEMM_LOG=<file>: append one line per launch (diagnostic shape census, tools/gemm_census.py)
@@ -898,8 +1132,9 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
   }();
   if (glog)
     std::fprintf(glog, "%d %d %d %d %d %d %d %d %d %d %d\n", d.M, d.N, d.K, d.batch, ak, bk, g.split,
-                 d.a.conv_taps, d.b.conv_taps, d.relu, direct ? (int)block.x / 64 : 0);
-  int st = direct ? launch_direct(ak, bk, grid, block, s, g) : launch_tiled(ak, bk, grid, s, g);
+                 d.a.conv_taps, d.b.conv_taps, d.relu, direct ? (int)block.x / 64 : (wide ? -1 : 0));
+  int st = direct ? launch_direct(ak, bk, grid, block, s, g)
+                  : (wide ? launch_wide(ak, bk, grid, s, g) : launch_tiled(ak, bk, grid, s, g));
   if (st != FX_OK) return st;
   FX_CHECK_HIP(hipGetLastError());
   if (g.split > 1 && !g.tile_cnt) {

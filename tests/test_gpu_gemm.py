@@ -86,8 +86,11 @@ def test_gemm_fused_bias_column(M, K, split):
     b.ones_col = N1 + 1
     fxf.gemm(M, N1 + 1, K, _operand(dyd, True), b, dwd, N1, beta=1.0, split=split, c_last=dbd)
     torch.cuda.synchronize()
-    torch.testing.assert_close(dwd.double().cpu(), dw + dy.t() @ x, rtol=1e-5, atol=1e-4)
-    torch.testing.assert_close(dbd.double().cpu(), db + dy.sum(0), rtol=1e-5, atol=1e-4)
+    # fp32 accumulation over K terms of unit-variance products: rounding grows ~sqrt(K) (the 128x64
+    # tile runs one serial MFMA chain per split instead of two k-halves, so ~1.4x the 64x64 error).
+    atol = max(1e-4, 5e-6 * K ** 0.5)
+    torch.testing.assert_close(dwd.double().cpu(), dw + dy.t() @ x, rtol=1e-5, atol=atol)
+    torch.testing.assert_close(dbd.double().cpu(), db + dy.sum(0), rtol=1e-5, atol=atol)
 
 
 def test_split_k_repeat_is_deterministic():

@@ -1,0 +1,6 @@
+# GEMM shape census: FX_GEMM_LOG shape log + kernel trace of a 1-step bench (diagnostic)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
+rm -rf gpurun_out/census gpurun_out/gemm_log.txt
+FX_GEMM_LOG=gpurun_out/gemm_log.txt timeout -k 10 200 rocprofv3 --kernel-trace -d gpurun_out/census -o c \
+  --output-format csv -- python bench.py --steps 1 --warmup 2 --no-cpu-baseline > gpurun_out/census.log 2>&1

@@ -6,13 +6,13 @@ import collections
 import csv
 import sys
 
-KIND = ["rows", "rconv", "rgen", "cols", "cconv"]
+KIND = ["rows", "rconv", "rgen", "cols", "cconv", "rcat"]
 
 
 def main(log_path, trace_path):
     shapes = [tuple(int(v) for v in ln.split()) for ln in open(log_path) if ln.strip()]
     rows = sorted(csv.DictReader(open(trace_path)), key=lambda r: int(r["Start_Timestamp"]))
-    g = [r for r in rows if "gemm_f32_kernel" in r["Kernel_Name"] or "gemm_direct_kernel" in r["Kernel_Name"]]
+    g = [r for r in rows if "gemm_f32_kernel" in r["Kernel_Name"] or "gemm_f32_wide" in r["Kernel_Name"] or "gemm_direct_kernel" in r["Kernel_Name"]]
     red = [r for r in rows if "splitk_reduce" in r["Kernel_Name"]]
     n = min(len(g), len(shapes))
     g, shapes = g[-n:], shapes[-n:]
