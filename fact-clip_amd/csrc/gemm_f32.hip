@@ -145,6 +145,11 @@ struct Loader {
   int rc;              // col-major: clamped first row of the 4
   unsigned emask, omask;   // col-major: bit e = row rc+e in storage / is the ones row
   int tapc, tap_s;     // COLS_CONV: channel / shift of this thread's 4 rows (one tap: cin % 4 == 0)
+  // FAST: per-thread addresses made once, so a stage's load is a uniform offset plus one add per
+  // row (the per-row 64-bit multiply-adds otherwise sit in every stage, ahead of its MFMAs)
+  const float* prow[4];    // row kinds: row j at k = tb (ROWS_CAT: first source)
+  const float* prow1[4];   // ROWS_CAT: row j of the second source at k = tb
+  const float* pcol;       // COLS: k = ta, first of the thread's 4 rows
 
   __device__ __forceinline__ void init(const fx_operand& op, const float* p0, int r0_, int R_, int K_, int tid) {
     o = op;
@@ -168,6 +173,8 @@ struct Loader {
           rowc1[j] = op.rows1 ? op.rows1[rr] : rr;
           rowc[j] = op.rows0 ? op.rows0[rr] : rr;
         }
+        prow[j] = p0 + (long long)rowc[j] * op.ld + tb;
+        if (KIND == ROWS_CAT) prow1[j] = op.ptr1 ? op.ptr1 + (long long)rowc1[j] * op.ld1 + tb : prow[j];
       }
     } else {
       // rows that exist in storage: all but a trailing virtual ones row
@@ -180,6 +187,7 @@ struct Loader {
         omask |= (op.ones_col && r + e == op.ones_col - 1 ? 1u : 0u) << e;
       }
       rc = min(r, ((stored - 1) / 4) * 4);
+      pcol = p0 + (long long)ta * op.ld + rc;
       if (KIND == COLS_CONV) {
         const int j = rc / op.conv_cin;
         tapc = rc - j * op.conv_cin;
@@ -200,33 +208,33 @@ struct Loader {
     }
     if (KIND == ROWS) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = ldg4(base + (long long)rowc[j] * o.ld + k0 + tb);
+      for (int j = 0; j < 4; ++j) v[j] = ldg4(prow[j] + k0);
       vm = rok;
     } else if (KIND == ROWS_CONV) {
-      // the 64-deep stage lies in one tap (conv_cin % 64 == 0, checked on the host)
+      // the 64-deep stage lies in one tap (conv_cin % 64 == 0, checked on the host): a uniform
+      // channel offset and a uniform row shift, taken per row only where the shifted frame exists
       const int tap = k0 / o.conv_cin;
-      const int c = k0 - tap * o.conv_cin + tb;
+      const int c = k0 - tap * o.conv_cin;
       const int s = conv_shift(o, tap);
+      const long long soff = (long long)s * o.ld;
       vm = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int t = rmod[j] + s;
         const bool ok = ((rok >> j) & 1u) && t >= 0 && t < o.seq_len;
         vm |= (ok ? 1u : 0u) << j;
-        v[j] = ldg4(base + (long long)(ok ? rowc[j] + s : rowc[j]) * o.ld + c);
+        v[j] = ldg4(prow[j] + c + (ok ? soff : 0ll));
       }
     } else if (KIND == ROWS_CAT) {
-      // the whole stage reads one source (k_split % 64 == 0): a uniform select of base / stride
+      // the whole stage reads one source (k_split % 64 == 0): a uniform choice of row addresses
       const bool second = o.ptr1 && k0 >= o.k_split;
-      const float* src = second ? o.ptr1 : base;
-      const long long ld = second ? o.ld1 : o.ld;
-      const int kk = (second ? k0 - o.k_split : k0) + tb;
+      const int kk = second ? k0 - o.k_split : k0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = ldg4(src + (long long)(second ? rowc1[j] : rowc[j]) * ld + kk);
+      for (int j = 0; j < 4; ++j) v[j] = ldg4((second ? prow1[j] : prow[j]) + kk);
       vm = rok;
     } else if (KIND == COLS) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = ldg4(base + (long long)(k0 + ta + 16 * j) * o.ld + rc);
+      for (int j = 0; j < 4; ++j) v[j] = ldg4(pcol + (long long)(k0 + 16 * j) * o.ld);
       vm = 0xFu;
     } else if (KIND == COLS_CONV) {
       vm = 0;
@@ -299,24 +307,30 @@ struct Loader {
 // epilogue: v = alpha*acc (+bias) [relu==2: ReLU here] (+resid) (+beta*C_old) (*gate>0) [relu==1: ReLU]
 // c_tap_cin != 0: output column n = tap*c_tap_cin + c is stored at c*3 + tap (Conv1d weight layout)
 // c_last != NULL: output column N-1 goes to c_last[m] (fused bias gradient)
-__device__ __forceinline__ void epilogue_store(const GemmDev& g, int b, int m, int n, float acc) {
+__device__ __forceinline__ float* epilogue_ptr(const GemmDev& g, int b, int m, int n) {
+  if (g.c_last && n == g.N - 1) return g.c_last + (long long)b * g.M + m;
+  long long col = n;
+  if (g.c_tap_cin) {
+    const int j = n / g.c_tap_cin;
+    col = (long long)(n - j * g.c_tap_cin) * 3 + j;
+  }
+  return g.c + (long long)b * g.c_bs + (long long)m * g.ldc + col;
+}
+
+// `pre`: the caller has already loaded the old C value into `cold` (beta != 0), else it is read here
+__device__ __forceinline__ void epilogue_store(const GemmDev& g, int b, int m, int n, float acc, bool pre = false,
+                                               float cold = 0.f) {
   float v = g.alpha * acc;
+  float* cp = epilogue_ptr(g, b, m, n);
   if (g.c_last && n == g.N - 1) {
-    float* cp = g.c_last + (long long)b * g.M + m;
-    if (g.beta != 0.f) v += g.beta * (*cp);
+    if (g.beta != 0.f) v += g.beta * (pre ? cold : *cp);
     *cp = v;
     return;
   }
   if (g.bias) v += g.bias[n];
   if (g.relu == 2) v = fmaxf(v, 0.f);
   if (g.resid) v += g.resid[(long long)b * g.resid_bs + (long long)m * g.ld_resid + n];
-  long long col = n;
-  if (g.c_tap_cin) {
-    const int j = n / g.c_tap_cin;
-    col = (long long)(n - j * g.c_tap_cin) * 3 + j;
-  }
-  float* cp = g.c + (long long)b * g.c_bs + (long long)m * g.ldc + col;
-  if (g.beta != 0.f) v += g.beta * (*cp);
+  if (g.beta != 0.f) v += g.beta * (pre ? cold : *cp);
   if (g.gate && !(g.gate[(long long)m * g.ld_gate + n] > 0.f)) v = 0.f;
   if (g.relu == 1) v = fmaxf(v, 0.f);
   *cp = v;
@@ -359,7 +373,6 @@ __device__ void splitk_finish(const GemmDev& g, int bidx, int m0, int n0, int ti
     epilogue_store(g, bidx, m, n, v);
   }
 }
-
 // One pipelined stage for this wave, as ONE basic block (no branches, so the compiler counts
 // outstanding loads exactly), in a fixed order pinned by sched_barrier: first the global loads of
 // a later stage into set `rn` (they get two MFMA phases to land), then the 32 MFMAs of the
@@ -374,9 +387,6 @@ __device__ __forceinline__ void stage_body(const Loader<AK, FAST>& la, const Loa
                                            f32x16& acc1) {
   using LA = Loader<AK, FAST>;
   using LB = Loader<BKd, FAST>;
-  la.load(kload, rn_a, mn_a);
-  lb.load(kload, rn_b, mn_b);
-  __builtin_amdgcn_sched_barrier(0);
   float4 fa[8], fb[8];
   fa[0] = LA::frag(cur, wm * 32, li, lh, 0);
   fb[0] = LB::frag(cur + IMG, wn * 32, li, lh, 0);
@@ -394,6 +404,9 @@ __device__ __forceinline__ void stage_body(const Loader<AK, FAST>& la, const Loa
       fa[q + 2] = LA::frag(cur, wm * 32, li, lh, q + 2);
       fb[q + 2] = LB::frag(cur + IMG, wn * 32, li, lh, q + 2);
     }
+    // the next loads' address work runs beside the first MFMA groups, not ahead of them
+    if (q == 0) la.load(kload, rn_a, mn_a);
+    if (q == 1) lb.load(kload, rn_b, mn_b);
     if (q == 2) la.store(wslot, rs_a, ms_a);
     if (q == 4) lb.store(wslot + IMG, rs_b, ms_b);
     __builtin_amdgcn_sched_barrier(0);
@@ -518,6 +531,16 @@ __global__ __launch_bounds__(NTHREADS) void gemm_f32_kernel(GemmDev g) {
       if (g.relu == 1) v = fmaxf(v, 0.f);
       if (row < g.M) cb[(long long)row * g.ldc] = v;
     }
+  } else if (g.beta != 0.f) {
+    // accumulating (dW into param.grad): load the 16 old values before the first store
+    float cold[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) cold[r] = *epilogue_ptr(g, bidx, min(rbase + (r & 3) + 8 * (r >> 2), g.M - 1), col);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = rbase + (r & 3) + 8 * (r >> 2);
+      if (row < g.M) epilogue_store(g, bidx, row, col, acc[r], true, cold[r]);
+    }
   } else {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -546,10 +569,6 @@ __device__ __forceinline__ void wide_stage(const Loader<AK, true>& la0, const Lo
                                            int lh, f32x16& acc0, f32x16& acc1) {
   using LA = Loader<AK, true>;
   using LB = Loader<BKd, true>;
-  la0.load(kload, rn0, mn0);
-  la1.load(kload, rn1, mn1);
-  lb.load(kload, rnb, mnb);
-  __builtin_amdgcn_sched_barrier(0);
   const float* ia = cur + wm * IMG;
   const float* ib = cur + 2 * IMG;
   float4 f0[8], f1[8], fb[8];
@@ -575,6 +594,10 @@ __device__ __forceinline__ void wide_stage(const Loader<AK, true>& la0, const Lo
       f1[q + 2] = LA::frag(ia, 32, li, lh, q + 2);
       fb[q + 2] = LB::frag(ib, wn * 32, li, lh, q + 2);
     }
+    // the next loads' address work runs beside the first MFMA groups, not ahead of them
+    if (q == 0) la0.load(kload, rn0, mn0);
+    if (q == 1) la1.load(kload, rn1, mn1);
+    if (q == 2) lb.load(kload, rnb, mnb);
     if (q == 1) la0.store(wslot, rs0, ms0);
     if (q == 3) la1.store(wslot + IMG, rs1, ms1);
     if (q == 5) lb.store(wslot + 2 * IMG, rsb, msb);
@@ -646,7 +669,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmDev& g, int bidx, int rb
       if (g.relu == 1) v = fmaxf(v, 0.f);
       if (row < g.M) cb[(long long)row * g.ldc] = v;
     }
-  } else {
+  } else {   // (a preloaded-C variant here costs the 128x64 kernel 416 B of scratch)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = rbase + (r & 3) + 8 * (r >> 2);
@@ -827,6 +850,21 @@ __global__ __launch_bounds__(DMAXW * 64) void gemm_direct_kernel(GemmDev g) {
       for (int q = 0; q < nw; ++q) v += red[(q * 16 + r) * 64 + l];
       direct_finish(g, bidx, sk, m0 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), n0 + (l & 31), v);
     }
+  } else if (g.split > 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) direct_finish(g, bidx, sk, m0 + (r & 3) + 8 * (r >> 2) + 4 * lh, n0 + li, acc[r]);
+  } else if (g.beta != 0.f) {
+    // accumulate into C (e.g. K = 64 dW GEMMs into param.grad): all 16 old values are loaded
+    // before the first store; element by element each store would hold back the next load
+    float cold[16];
+    const int col = min(n0 + li, g.N - 1);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) cold[r] = *epilogue_ptr(g, bidx, min(m0 + (r & 3) + 8 * (r >> 2) + 4 * lh, g.M - 1), col);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      if (row < g.M && n0 + li < g.N) epilogue_store(g, bidx, row, n0 + li, acc[r], true, cold[r]);
+    }
   } else {
 #pragma unroll
     for (int r = 0; r < 16; ++r) direct_finish(g, bidx, sk, m0 + (r & 3) + 8 * (r >> 2) + 4 * lh, n0 + li, acc[r]);
@@ -974,10 +1012,20 @@ bool use_direct(const fx_gemm_desc& d, int ak, int bk) {
     if (!p) return 0;
     return std::string(p) == "tiled" ? 1 : std::string(p) == "direct" ? 2 : 0;
   }();
-  const bool ok = (ak == ROWS || ak == ROWS_GEN || ak == ROWS_CAT || ak == COLS) && (bk == ROWS || bk == COLS);
+  // the direct kernel addresses ROWS / COLS operands with 32-bit byte offsets (dload)
+  auto fits = [&](const fx_operand& o, int kind, int R) {
+    const double k = (double)d.K + 2 * DMAXW * DCH + 64, ld = (double)o.ld;
+    const double bytes = kind == ROWS ? ((double)R * ld + k) * 4 : kind == COLS ? (k * ld + R) * 4 : 0;
+    return bytes < 4294967296.0;
+  };
+  const bool ok = d.K > 0 && (ak == ROWS || ak == ROWS_GEN || ak == ROWS_CAT || ak == COLS) && (bk == ROWS || bk == COLS) &&
+                  fits(d.a, ak, d.M) && fits(d.b, bk, d.N);
   if (!ok || force == 1) return false;
   if (force == 2) return true;
-  return d.M <= 64 || d.N <= 64 || d.K <= 64;
+  // gathered A rows (ROWS_GEN / ROWS_CAT) load element by element in the direct kernel: only the
+  // 32-row case pays off there (64 x 256 x 1024 concat: 54 us direct vs 29 us tiled)
+  const int lim = (ak == ROWS_GEN || ak == ROWS_CAT) ? 32 : 64;
+  return d.M <= lim || d.N <= lim || d.K <= 64;
 }
 
 // 128x64 tiles where the launch still has ~3/4 of a block per CU: FAST operands only.
