@@ -30,7 +30,7 @@ sys.path.insert(0, os.path.join(ROOT, "fact-clip_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-DOMINANT_KERNEL = "gemm_f32_wide_kernel<1, 0>"   # rocprofv3 name: fx::(anonymous namespace)::gemm_f32_wide_kernel<1, 0>
+DOMINANT_KERNEL = "gemm_f32_wide8_kernel<1, 0>"   # rocprofv3 name: fx::(anonymous namespace)::gemm_f32_wide8_kernel<1, 0>
 METRIC = "frames/sec FACT_CLIP fwd+bwd, T=4096 D=2048 Nact=32, at 1/2/4/8 GPUs"
 F32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 HOLDOUT = [51, 53, 61, 67, 56]   # havid_view0_lh_pt_holdout.yaml

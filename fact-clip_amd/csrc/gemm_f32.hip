@@ -121,18 +121,19 @@ __device__ __forceinline__ float4 zero4() { return make_float4(0.f, 0.f, 0.f, 0.
 __device__ __forceinline__ float4 ldg4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
 // ---------------------------------------------------------------- loaders
-// A stage is the 64 x 64 (rows x k) tile of one operand; each of the 256 threads moves 4
-// float4 of it per stage:
-//   row-major kinds: rows (tid>>4) + 16j, k = (tid&15)*4 .. +3           (j = 0..3)
-//   col-major kinds: k    (tid>>4) + 16j, rows (tid&15)*4 .. +3
+// A stage is the 64 x 64 (rows x k) tile of one operand; each of the 1024 / NJ threads moves NJ
+// float4 of it per stage (NJ = 4: 256-thread blocks, NJ = 2: 512-thread blocks):
+//   row-major kinds: rows (tid>>4) + (64/NJ) j, k = (tid&15)*4 .. +3      (j < NJ)
+//   col-major kinds: k    (tid>>4) + (64/NJ) j, rows (tid&15)*4 .. +3
 // so 16 consecutive threads read one 256-B line.
 // FAST (chosen per launch on the host: 16-B aligned operands, K % 64 == 0, no gathers): the
 // loads are unconditional straight-line code -- rows past the edge are read from a clamped
 // in-range address and replaced by a select (0, or 1 for the virtual ones row) -- so the
 // pipelined loop has no bounds branches for the compiler to drain vmcnt at.  !FAST fetches
 // element by element with full bounds checks (edge shapes, gathers, concatenations).
-template <int KIND, bool FAST>
+template <int KIND, bool FAST, int NJ = 4>
 struct Loader {
+  static constexpr int RSTEP = 64 / NJ;   // row (or k) step between a thread's NJ vectors
   static constexpr bool kRowImg = KIND <= ROWS_GEN || KIND == ROWS_CAT;
   fx_operand o;        // by value: the address of a kernel argument would force it to scratch
   const float* base;   // operand base incl. batch offset
@@ -163,8 +164,8 @@ struct Loader {
     if (kRowImg) {
       rok = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int r = r0 + ta + 16 * j;
+      for (int j = 0; j < NJ; ++j) {
+        const int r = r0 + ta + RSTEP * j;
         rok |= (r < R ? 1u : 0u) << j;
         rowc[j] = min(r, R - 1);
         if (KIND == ROWS_CONV) rmod[j] = rowc[j] % op.seq_len;
@@ -208,7 +209,7 @@ struct Loader {
     }
     if (KIND == ROWS) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = ldg4(prow[j] + k0);
+      for (int j = 0; j < NJ; ++j) v[j] = ldg4(prow[j] + k0);
       vm = rok;
     } else if (KIND == ROWS_CONV) {
       // the 64-deep stage lies in one tap (conv_cin % 64 == 0, checked on the host): a uniform
@@ -219,7 +220,7 @@ struct Loader {
       const long long soff = (long long)s * o.ld;
       vm = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         const int t = rmod[j] + s;
         const bool ok = ((rok >> j) & 1u) && t >= 0 && t < o.seq_len;
         vm |= (ok ? 1u : 0u) << j;
@@ -230,17 +231,17 @@ struct Loader {
       const bool second = o.ptr1 && k0 >= o.k_split;
       const int kk = second ? k0 - o.k_split : k0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = ldg4((second ? prow1[j] : prow[j]) + kk);
+      for (int j = 0; j < NJ; ++j) v[j] = ldg4((second ? prow1[j] : prow[j]) + kk);
       vm = rok;
     } else if (KIND == COLS) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = ldg4(pcol + (long long)(k0 + 16 * j) * o.ld);
+      for (int j = 0; j < NJ; ++j) v[j] = ldg4(pcol + (long long)(k0 + RSTEP * j) * o.ld);
       vm = 0xFu;
     } else if (KIND == COLS_CONV) {
       vm = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = k0 + ta + 16 * j, t = k % o.seq_len + tap_s;
+      for (int j = 0; j < NJ; ++j) {
+        const int k = k0 + ta + RSTEP * j, t = k % o.seq_len + tap_s;
         const bool ok = t >= 0 && t < o.seq_len;
         vm |= (ok ? 1u : 0u) << j;
         v[j] = ldg4(base + (long long)(ok ? k + tap_s : k) * o.ld + tapc);
@@ -250,17 +251,17 @@ struct Loader {
 
   __device__ __forceinline__ void load_generic(int k0, float4* v) const {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       float e[4];
       if (kRowImg) {
-        const int r = r0 + ta + 16 * j;
+        const int r = r0 + ta + RSTEP * j;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int k = k0 + tb + q;
           e[q] = (r < R && k < K) ? fetch_rm(o, base, r, k) : 0.f;
         }
       } else {
-        const int k = k0 + ta + 16 * j;
+        const int k = k0 + ta + RSTEP * j;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int r = r0 + tb + q;
@@ -274,13 +275,13 @@ struct Loader {
   __device__ __forceinline__ void store(float* img, const float4* v, unsigned vm) const {
     if (kRowImg) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         const float4 x = (!FAST || ((vm >> j) & 1u)) ? v[j] : zero4();
-        *reinterpret_cast<float4*>(img + (ta + 16 * j) * RS + tb) = x;
+        *reinterpret_cast<float4*>(img + (ta + RSTEP * j) * RS + tb) = x;
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         float e[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
         if (FAST) {
           const bool tok = KIND != COLS_CONV || ((vm >> j) & 1u);
@@ -290,7 +291,7 @@ struct Loader {
             e[q] = (tok && ((emask >> q) & 1u)) ? e[q] : one;
           }
         }
-        float* d = img + (ta + 16 * j) * CS + tb;
+        float* d = img + (ta + RSTEP * j) * CS + tb;
         d[0] = e[0]; d[1] = e[1]; d[2] = e[2]; d[3] = e[3];
       }
     }
@@ -407,8 +408,8 @@ __device__ __forceinline__ void stage_body(const Loader<AK, FAST>& la, const Loa
     // the next loads' address work runs beside the first MFMA groups, not ahead of them
     if (q == 0) la.load(kload, rn_a, mn_a);
     if (q == 1) lb.load(kload, rn_b, mn_b);
-    if (q == 2) la.store(wslot, rs_a, ms_a);
-    if (q == 4) lb.store(wslot + IMG, rs_b, ms_b);
+    if (q == 6) la.store(wslot, rs_a, ms_a);   // late: the loads get ~1.7 stages to land
+    if (q == 7) lb.store(wslot + IMG, rs_b, ms_b);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -598,9 +599,11 @@ __device__ __forceinline__ void wide_stage(const Loader<AK, true>& la0, const Lo
     if (q == 0) la0.load(kload, rn0, mn0);
     if (q == 1) la1.load(kload, rn1, mn1);
     if (q == 2) lb.load(kload, rnb, mnb);
-    if (q == 1) la0.store(wslot, rs0, ms0);
-    if (q == 3) la1.store(wslot + IMG, rs1, ms1);
-    if (q == 5) lb.store(wslot + 2 * IMG, rsb, msb);
+    // the stored set was loaded a whole stage ago; storing it late in this stage gives those loads
+    // ~1.7 stages to land (PMC: waits on them were a quarter of the wave cycles when stored early)
+    if (q == 5) la0.store(wslot, rs0, ms0);
+    if (q == 6) la1.store(wslot + IMG, rs1, ms1);
+    if (q == 7) lb.store(wslot + 2 * IMG, rsb, msb);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -729,6 +732,148 @@ __global__ __launch_bounds__(NTHREADS) void gemm_f32_wide_kernel(GemmDev g) {
   }
   tile_epilogue(g, bidx, rb0, col, acc0);
   tile_epilogue(g, bidx, rb1, col, acc1);
+}
+
+// ---------------------------------------------------------------- wide tile, two waves per SIMD
+// The same 128 x 64 tile and LDS ring with 8 waves (512 threads): wave w owns ONE 32x32 sub-tile
+// (rows 32 (w>>1) of the 128, columns 32 (w&1)), 32 MFMAs per stage over two accumulators, and
+// each thread stages 2 float4 per operand image (Loader NJ = 2).  PMC on the 4-wave kernel: the
+// matrix pipe was busy 51 % of the wave cycles, the rest waits (barrier / loads, 24 %) and issue
+// of the address / select / LDS work (26 %) that one wave cannot hide behind its own MFMAs; with
+// a partner wave on the SIMD, one wave's MFMAs run while the other issues or waits.
+constexpr int W8T = 512;
+template <int AK, int BKd>
+__device__ __forceinline__ void wide8_stage(const Loader<AK, true, 2>& la0, const Loader<AK, true, 2>& la1,
+                                            const Loader<BKd, true, 2>& lb, const float* cur, float* wslot,
+                                            int kload, const float4* rs0, const float4* rs1, const float4* rsb,
+                                            unsigned ms0, unsigned ms1, unsigned msb, float4* rn0, float4* rn1,
+                                            float4* rnb, unsigned& mn0, unsigned& mn1, unsigned& mnb, int ai, int wr,
+                                            int wn, int li, int lh, f32x16& acc0, f32x16& acc1) {
+  using LA = Loader<AK, true, 2>;
+  using LB = Loader<BKd, true, 2>;
+  const float* ia = cur + ai * IMG;
+  const float* ib = cur + 2 * IMG;
+  float4 fa[8], fb[8];
+  fa[0] = LA::frag(ia, wr, li, lh, 0);
+  fb[0] = LB::frag(ib, wn * 32, li, lh, 0);
+  fa[1] = LA::frag(ia, wr, li, lh, 1);
+  fb[1] = LB::frag(ib, wn * 32, li, lh, 1);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    f32x16& acc = (q & 1) ? acc1 : acc0;
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, fb[q].x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, fb[q].y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, fb[q].z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, fb[q].w, acc, 0, 0, 0);
+    if (q + 2 < 8) {
+      fa[q + 2] = LA::frag(ia, wr, li, lh, q + 2);
+      fb[q + 2] = LB::frag(ib, wn * 32, li, lh, q + 2);
+    }
+    if (q == 0) la0.load(kload, rn0, mn0);
+    if (q == 1) la1.load(kload, rn1, mn1);
+    if (q == 2) lb.load(kload, rnb, mnb);
+    if (q == 5) la0.store(wslot, rs0, ms0);
+    if (q == 6) la1.store(wslot + IMG, rs1, ms1);
+    if (q == 7) lb.store(wslot + 2 * IMG, rsb, msb);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int AK, int BKd>
+__device__ __forceinline__ void wide8_kloop(const Loader<AK, true, 2>& la0, const Loader<AK, true, 2>& la1,
+                                            const Loader<BKd, true, 2>& lb, float* lds, int kt0, int kt1, int ai,
+                                            int wr, int wn, int li, int lh, f32x16& acc0, f32x16& acc1) {
+  const int n = kt1 - kt0;
+  if (n <= 0) return;
+  const int klast = (kt1 - 1) * BK;
+  constexpr int SLOT = 3 * IMG;
+  float4 a0x[2], a1x[2], bx[2], a0y[2], a1y[2], by[2];
+  unsigned m0x, m1x, mbx, m0y, m1y, mby;
+  la0.load(kt0 * BK, a0x, m0x);
+  la1.load(kt0 * BK, a1x, m1x);
+  lb.load(kt0 * BK, bx, mbx);
+  la0.load(min((kt0 + 1) * BK, klast), a0y, m0y);
+  la1.load(min((kt0 + 1) * BK, klast), a1y, m1y);
+  lb.load(min((kt0 + 1) * BK, klast), by, mby);
+  la0.store(lds, a0x, m0x);
+  la1.store(lds + IMG, a1x, m1x);
+  lb.store(lds + 2 * IMG, bx, mbx);
+  la0.store(lds + SLOT, a0y, m0y);
+  la1.store(lds + SLOT + IMG, a1y, m1y);
+  lb.store(lds + SLOT + 2 * IMG, by, mby);
+  la0.load(min((kt0 + 2) * BK, klast), a0x, m0x);
+  la1.load(min((kt0 + 2) * BK, klast), a1x, m1x);
+  lb.load(min((kt0 + 2) * BK, klast), bx, mbx);
+  __syncthreads();
+  int slot = 0;
+  auto iter = [&](int i, const float4* s0, const float4* s1, const float4* sb, unsigned q0, unsigned q1, unsigned qb,
+                  float4* n0, float4* n1, float4* nb, unsigned& p0, unsigned& p1, unsigned& pb) FX_INLINE {
+    const int ws = slot == 0 ? 2 : slot - 1;
+    wide8_stage<AK, BKd>(la0, la1, lb, lds + slot * SLOT, lds + ws * SLOT, min((kt0 + i + 3) * BK, klast), s0, s1,
+                         sb, q0, q1, qb, n0, n1, nb, p0, p1, pb, ai, wr, wn, li, lh, acc0, acc1);
+    __syncthreads();
+    slot = slot == 2 ? 0 : slot + 1;
+  };
+  int i = 0;
+  for (; i + 1 < n; i += 2) {
+    iter(i, a0x, a1x, bx, m0x, m1x, mbx, a0y, a1y, by, m0y, m1y, mby);
+    iter(i + 1, a0y, a1y, by, m0y, m1y, mby, a0x, a1x, bx, m0x, m1x, mbx);
+  }
+  if (i < n) iter(i, a0x, a1x, bx, m0x, m1x, mbx, a0y, a1y, by, m0y, m1y, mby);
+}
+
+template <int AK, int BKIND>
+__global__ __launch_bounds__(W8T) void gemm_f32_wide8_kernel(GemmDev g) {
+  __shared__ float lds[NSLOT * 3 * IMG];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, li = lane & 31, lh = lane >> 5;
+  const int ai = wm >> 1, wr = (wm & 1) * 32;   // A image (rows m0 / m0 + 64) and row offset in it
+  int tx, ty;
+  {
+    const int nt = g.tiles_x * g.tiles_y;
+    const int id = blockIdx.y * g.tiles_x + blockIdx.x;
+    const int q = nt / 8, rr = nt % 8, x8 = id % 8, i8 = id / 8;
+    const int nid = (x8 < rr ? x8 * (q + 1) : rr * (q + 1) + (x8 - rr) * q) + i8;
+    ty = nid / g.tiles_x;
+    tx = nid - ty * g.tiles_x;
+  }
+  const int n0 = tx * BN, m0 = ty * WBM;
+  const int z = blockIdx.z, bidx = z / g.split, sk = z - bidx * g.split;
+  const int nkt = (g.K + BK - 1) / BK;
+  const int kt0 = sk * g.kt_per_split;
+  const int kt1 = min(nkt, kt0 + g.kt_per_split);
+  Loader<AK, true, 2> la0, la1;
+  Loader<BKIND, true, 2> lb;
+  const float* pa = g.a.ptr + (long long)bidx * g.a.batch_stride;
+  la0.init(g.a, pa, m0, g.M, g.K, tid);
+  la1.init(g.a, pa, m0 + BM, g.M, g.K, tid);
+  lb.init(g.b, g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid);
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    acc0[i] = 0.f;
+    acc1[i] = 0.f;
+  }
+  wide8_kloop<AK, BKIND>(la0, la1, lb, lds, kt0, kt1, ai, wr, wn, li, lh, acc0, acc1);
+  const f32x16 acc = acc0 + acc1;
+  const int col = n0 + wn * 32 + li;
+  const int rbase = m0 + wm * 32 + 4 * lh;
+  if (g.split > 1) {
+    if (col < g.N) {
+      float* slab = g.ws + ((long long)bidx * g.split + sk) * g.M * (long long)g.N;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rbase + (r & 3) + 8 * (r >> 2);
+        if (row < g.M) slab[(long long)row * g.N + col] = acc[r];
+      }
+    }
+    if (g.tile_cnt)
+      splitk_finish<WBM, BN>(g, bidx, m0, n0, (bidx * g.tiles_y + ty) * g.tiles_x + tx,
+                             reinterpret_cast<int*>(&lds[NSLOT * 3 * IMG - 1]));
+    return;
+  }
+  tile_epilogue(g, bidx, rbase, col, acc);
 }
 
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmDev g) {
@@ -938,6 +1083,32 @@ int launch_wide_b(int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
   return FX_ERR_UNSUPPORTED;
 }
 
+template <int AK>
+int launch_wide8_b(int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
+  switch (bk) {
+    case ROWS: hipLaunchKernelGGL((gemm_f32_wide8_kernel<AK, ROWS>), grid, dim3(W8T), 0, s, g); return FX_OK;
+    case COLS: hipLaunchKernelGGL((gemm_f32_wide8_kernel<AK, COLS>), grid, dim3(W8T), 0, s, g); return FX_OK;
+    case COLS_CONV:
+      hipLaunchKernelGGL((gemm_f32_wide8_kernel<AK, COLS_CONV>), grid, dim3(W8T), 0, s, g);
+      return FX_OK;
+    default: break;
+  }
+  set_error("gemm(wide8): unsupported B operand kind");
+  return FX_ERR_UNSUPPORTED;
+}
+
+int launch_wide8(int ak, int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
+  switch (ak) {
+    case ROWS: return launch_wide8_b<ROWS>(bk, grid, s, g);
+    case ROWS_CONV: return launch_wide8_b<ROWS_CONV>(bk, grid, s, g);
+    case ROWS_CAT: return launch_wide8_b<ROWS_CAT>(bk, grid, s, g);
+    case COLS: return launch_wide8_b<COLS>(bk, grid, s, g);
+    default: break;
+  }
+  set_error("gemm(wide8): unsupported A operand kind");
+  return FX_ERR_UNSUPPORTED;
+}
+
 int launch_wide(int ak, int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
   switch (ak) {
     case ROWS: return launch_wide_b<ROWS>(bk, grid, s, g);
@@ -1030,6 +1201,15 @@ bool use_direct(const fx_gemm_desc& d, int ak, int bk) {
 
 // 128x64 tiles where the launch still has ~3/4 of a block per CU: FAST operands only.
 // FX_GEMM_WIDE=0|1 forces the choice among eligible launches (diagnostic).
+// 128x64 tiles with 8 waves (two per SIMD) instead of 4; FX_GEMM_W8=0|1 overrides (diagnostic)
+bool wide8() {
+  static const bool on = [] {
+    const char* p = std::getenv("FX_GEMM_W8");
+    return p ? p[0] == '1' : true;
+  }();
+  return on;
+}
+
 bool use_wide(const GemmDev& g, int ak, int bk, int batch) {
   static const int force = [] {
     const char* p = std::getenv("FX_GEMM_WIDE");
@@ -1182,7 +1362,8 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
     std::fprintf(glog, "%d %d %d %d %d %d %d %d %d %d %d\n", d.M, d.N, d.K, d.batch, ak, bk, g.split,
                  d.a.conv_taps, d.b.conv_taps, d.relu, direct ? (int)block.x / 64 : (wide ? -1 : 0));
   int st = direct ? launch_direct(ak, bk, grid, block, s, g)
-                  : (wide ? launch_wide(ak, bk, grid, s, g) : launch_tiled(ak, bk, grid, s, g));
+                  : (wide ? (wide8() ? launch_wide8(ak, bk, grid, s, g) : launch_wide(ak, bk, grid, s, g))
+                          : launch_tiled(ak, bk, grid, s, g));
   if (st != FX_OK) return st;
   FX_CHECK_HIP(hipGetLastError());
   if (g.split > 1 && !g.tile_cnt) {
