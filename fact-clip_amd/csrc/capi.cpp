@@ -115,10 +115,13 @@ int add2(const float* a, long long lda, const float* b, long long ldb, int rows,
 
 // split-K factor for small-output / long-K products (dW over frames, token x frame)
 int pick_split(int M, int N, int K, int batch) {
-  const long long tiles = (long long)cdiv(M, 64) * cdiv(N, 64) * batch;
   const int nkt = cdiv(K, 64);   // 64-deep K stages of the GEMM kernel
-  if (tiles >= 160 || nkt < 4) return 1;
-  // one 8-wave block per CU fits (VGPR-bound): keep tiles*split within the 256 CUs, no straggler round
+  if (nkt < 4) return 1;
+  // whole 64-deep stages and >= 128 rows: the launch can take the 128x64 tile (8 waves), so count
+  // those tiles; one block per CU: keep tiles*split within the 256 CUs, no straggler round
+  const bool wide = M >= 128 && K % 64 == 0;
+  const long long tiles = (long long)cdiv(M, wide ? 128 : 64) * cdiv(N, 64) * batch;
+  if (tiles >= 160) return 1;
   int sp = (int)std::min<long long>(nkt / 2, 256 / tiles);
   return std::max(sp, 1);
 }
