@@ -234,6 +234,7 @@ class ProcessFeatureFn(torch.autograd.Function):
                                           nx.stream()), "fx_process_feature_fwd")
         ctx.n = n
         ctx.save_for_backward(out)
+        ctx.set_materialize_grads(False)   # an output without a gradient stays None (no zero fill)
         return out, clogit
 
     @staticmethod
@@ -408,6 +409,7 @@ class X2YFn(torch.autograd.Function):
         ctx.has_pos = (Xpos is not None, Ypos is not None)
         ctx.save_for_backward(X, Y, wk, bk, wv, bv, wq, bq, wy, by, attn, saved)
         ctx.mark_non_differentiable(attn)
+        ctx.set_materialize_grads(False)   # unused logit / attn gradients arrive as None (no zero fill)
         if rows is None:
             return out, logit.view(Ny, Nx), attn.view(Ny, Nx)
         return out, logit, attn
