@@ -63,6 +63,7 @@ struct GemmDev {
   int tiles_x, tiles_y;
   long long* stamps;
   unsigned* tile_cnt;   // split-K arrival counters (one per output tile), NULL -> separate reduce kernel
+  int w8_stagger;       // wide8: waves 4-7 run the staggered stage schedule
 };
 
 // Diagnostic builds (-DFX_STAMPS) record s_memtime / s_memrealtime at fixed points of
@@ -742,7 +743,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_f32_wide_kernel(GemmDev g) {
 // of the address / select / LDS work (26 %) that one wave cannot hide behind its own MFMAs; with
 // a partner wave on the SIMD, one wave's MFMAs run while the other issues or waits.
 constexpr int W8T = 512;
-template <int AK, int BKd>
+template <int AK, int BKd, int PH>
 __device__ __forceinline__ void wide8_stage(const Loader<AK, true, 2>& la0, const Loader<AK, true, 2>& la1,
                                             const Loader<BKd, true, 2>& lb, const float* cur, float* wslot,
                                             int kload, const float4* rs0, const float4* rs1, const float4* rsb,
@@ -770,17 +771,20 @@ __device__ __forceinline__ void wide8_stage(const Loader<AK, true, 2>& la0, cons
       fa[q + 2] = LA::frag(ia, wr, li, lh, q + 2);
       fb[q + 2] = LB::frag(ib, wn * 32, li, lh, q + 2);
     }
-    if (q == 0) la0.load(kload, rn0, mn0);
-    if (q == 1) la1.load(kload, rn1, mn1);
-    if (q == 2) lb.load(kload, rnb, mnb);
-    if (q == 5) la0.store(wslot, rs0, ms0);
-    if (q == 6) la1.store(wslot + IMG, rs1, ms1);
-    if (q == 7) lb.store(wslot + 2 * IMG, rsb, msb);
+    // staggered halves: waves 0-3 (PH 0) load early and store late in the stage, their SIMD
+    // partners 4-7 (PH 1) the other way round, so one wave of each SIMD issues plain MFMA groups
+    // while the other does its load / LDS-store work
+    if (q == (PH ? 4 : 0)) la0.load(kload, rn0, mn0);
+    if (q == (PH ? 5 : 1)) la1.load(kload, rn1, mn1);
+    if (q == (PH ? 6 : 2)) lb.load(kload, rnb, mnb);
+    if (q == (PH ? 1 : 5)) la0.store(wslot, rs0, ms0);
+    if (q == (PH ? 2 : 6)) la1.store(wslot + IMG, rs1, ms1);
+    if (q == (PH ? 3 : 7)) lb.store(wslot + 2 * IMG, rsb, msb);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
 
-template <int AK, int BKd>
+template <int AK, int BKd, int PH>
 __device__ __forceinline__ void wide8_kloop(const Loader<AK, true, 2>& la0, const Loader<AK, true, 2>& la1,
                                             const Loader<BKd, true, 2>& lb, float* lds, int kt0, int kt1, int ai,
                                             int wr, int wn, int li, int lh, f32x16& acc0, f32x16& acc1) {
@@ -810,9 +814,9 @@ __device__ __forceinline__ void wide8_kloop(const Loader<AK, true, 2>& la0, cons
   auto iter = [&](int i, const float4* s0, const float4* s1, const float4* sb, unsigned q0, unsigned q1, unsigned qb,
                   float4* n0, float4* n1, float4* nb, unsigned& p0, unsigned& p1, unsigned& pb) FX_INLINE {
     const int ws = slot == 0 ? 2 : slot - 1;
-    wide8_stage<AK, BKd>(la0, la1, lb, lds + slot * SLOT, lds + ws * SLOT, min((kt0 + i + 3) * BK, klast), s0, s1,
+    wide8_stage<AK, BKd, PH>(la0, la1, lb, lds + slot * SLOT, lds + ws * SLOT, min((kt0 + i + 3) * BK, klast), s0, s1,
                          sb, q0, q1, qb, n0, n1, nb, p0, p1, pb, ai, wr, wn, li, lh, acc0, acc1);
-    __syncthreads();
+    __syncthreads();   // (a barrier after the next stage's first MFMA group instead measured 3 % slower)
     slot = slot == 2 ? 0 : slot + 1;
   };
   int i = 0;
@@ -855,7 +859,10 @@ __global__ __launch_bounds__(W8T) void gemm_f32_wide8_kernel(GemmDev g) {
     acc0[i] = 0.f;
     acc1[i] = 0.f;
   }
-  wide8_kloop<AK, BKIND>(la0, la1, lb, lds, kt0, kt1, ai, wr, wn, li, lh, acc0, acc1);
+  if (g.w8_stagger && wave >= 4)
+    wide8_kloop<AK, BKIND, 1>(la0, la1, lb, lds, kt0, kt1, ai, wr, wn, li, lh, acc0, acc1);
+  else
+    wide8_kloop<AK, BKIND, 0>(la0, la1, lb, lds, kt0, kt1, ai, wr, wn, li, lh, acc0, acc1);
   const f32x16 acc = acc0 + acc1;
   const int col = n0 + wn * 32 + li;
   const int rbase = m0 + wm * 32 + 4 * lh;
@@ -1316,6 +1323,11 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
   g.a_vec = operand_vec_ok(d.a);
   g.b_vec = operand_vec_ok(d.b);
   g.ws = d.workspace;
+  static const int stagger = [] {
+    const char* p = std::getenv("FX_GEMM_STAGGER");   // diagnostic A/B: 0 = both halves alike
+    return p ? (p[0] == '1' ? 1 : 0) : 1;
+  }();
+  g.w8_stagger = stagger;
   const int ak = kind_of(d.a, g.a_vec), bk = kind_of(d.b, g.b_vec);
   const bool direct = use_direct(d, ak, bk);
   bool wide = false;
