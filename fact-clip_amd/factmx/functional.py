@@ -593,6 +593,27 @@ def gemm(M, N, K, a, b, c, ldc, bias=None, relu=0, resid=None, alpha=1.0, beta=0
     return ws
 
 
+def matmul_nt(x, w, alpha=1.0):
+    """alpha * x . w^T for row-major x (M, K), w (N, K) without autograd (eval / matching paths):
+    one fx_gemm launch instead of a hipBLASLt call and its host-side setup."""
+    x, w = x.contiguous(), w.contiguous()
+    M, K = x.shape
+    N = w.shape[0]
+    y = _empty(M, N, device=x.device)
+    gemm(M, N, K, _rows_operand(x), _rows_operand(w), y, N, alpha=alpha)
+    return y
+
+
+def matmul_tn(a, b):
+    """a^T . b for row-major a (K, M), b (K, N), no autograd: (M, N) via column-major operands."""
+    a, b = a.contiguous(), b.contiguous()
+    K, M = a.shape
+    N = b.shape[1]
+    y = _empty(M, N, device=a.device)
+    gemm(M, N, K, _rows_operand(a, trans=True), _rows_operand(b, trans=True), y, N)
+    return y
+
+
 class Conv3Fn(torch.autograd.Function):
     """Conv1d(k=3, dilation d, padding d) on (T*nvid, C) rows as an implicit GEMM (basic.py:138, 237-245)."""
 

@@ -519,7 +519,12 @@ class FACT_CLIP(_FACTBase):
         if self.text_embeddings is None or not hasattr(self, "projected_frame_embeddings"):
             return self.block_list[-1].eval(transcript)
         emb = self.projected_frame_embeddings.squeeze(1)
-        clip_prob = torch.softmax(emb @ self.text_embeddings.t() / self.cfg.CLIP.temp, dim=-1)
+        if emb.is_cuda:
+            with torch.no_grad():
+                logits = fxf.matmul_nt(emb.detach(), self.text_embeddings, alpha=1.0 / self.cfg.CLIP.temp)
+        else:
+            logits = emb @ self.text_embeddings.t() / self.cfg.CLIP.temp
+        clip_prob = torch.softmax(logits, dim=-1)
         last = self.block_list[-1]
         ab, any_tok = Block._abranch_prob(last.action_clogit, last.a2f_attn)
         w = self.cfg.FACT.mwt

@@ -111,7 +111,10 @@ class MatchCriterion:
     def a2f_soft_iou(cls, a2f_attn, onehot_seg_label):
         """loss.py:91-106 on the device: overlap / sum_t min(attn + onehot, 1)."""
         a = a2f_attn[0]                                      # (T, A)
-        overlap = a.t() @ onehot_seg_label                   # (A, S)
+        if a.is_cuda:
+            overlap = fxf.matmul_tn(a, onehot_seg_label)     # (A, S), one fx_gemm
+        else:
+            overlap = a.t() @ onehot_seg_label
         union = torch.minimum(a[:, :, None] + onehot_seg_label[:, None, :], torch.ones((), device=a.device)).sum(0)
         return torch.nan_to_num(overlap / union, nan=0.0)
 
@@ -271,7 +274,10 @@ def infonce_contrastive_loss(projected_embeddings, text_embeddings, labels, temp
     if lab.shape[0] != emb.shape[0]:
         lab = lab.repeat(B)
     n = text_embeddings.shape[0]
-    sim = emb @ text_embeddings.t() / temperature
+    if emb.is_cuda:
+        sim = fxf.linear(emb, text_embeddings.detach(), None) * (1.0 / temperature)
+    else:
+        sim = emb @ text_embeddings.t() / temperature
     v2t = F.cross_entropy(sim, lab)
     tgt = F.one_hot(lab, num_classes=n).float()
     lp_t = F.log_softmax(sim.t(), dim=1)
