@@ -114,9 +114,10 @@ def traffic_from_profiles(kernel_prefix):
     return None
 
 
-def cpu_baseline(T, videos_timed=2):
+def cpu_baseline(T, min_seconds=10.0, min_steps=2):
     """The CPU oracle (fp32 PyTorch restatement pinned to the reference) timed on host cores:
-    one video per step, full T, forward+loss+backward+Adam; also counts algorithmic FLOPs."""
+    one video per step, full T, forward+loss+backward+Adam, repeated until >= min_seconds of
+    CPU work (bounded sample, ~10 s); also counts algorithmic FLOPs."""
     from torch.utils.flop_counter import FlopCounterMode
     from oracle import fact_oracle as fo
     cfg = make_cfg()
@@ -141,8 +142,10 @@ def cpu_baseline(T, videos_timed=2):
         step()
     flops = fc.get_total_flops()
     t0 = time.perf_counter()
-    for _ in range(videos_timed):
+    videos_timed = 0
+    while videos_timed < min_steps or time.perf_counter() - t0 < min_seconds:
         step()
+        videos_timed += 1
     dt = time.perf_counter() - t0
     return dict(value=round(videos_timed * T / dt, 1), unit="frames/s", cores=torch.get_num_threads(), kind="port",
                 sample=f"{videos_timed} steps x 1 video (T={T}, seg10) fwd+loss+bwd+Adam, oracle fp32 "
