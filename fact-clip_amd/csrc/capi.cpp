@@ -167,7 +167,9 @@ int linear_dwdb(const float* dy, long long lddy, const float* x, long long ldx, 
   fx_gemm_desc d = gemm_desc(N, Kc, M, op_cols(dy, lddy), b, dw, lddw < 0 ? K : lddw);
   d.c_last_col = db;
   d.beta = accumulate ? 1.f : 0.f;
-  d.split_k = pick_split(N, Kc, M);
+  // split sized for the K+1 columns dwdb_ws() reserves, with or without the bias column: counting
+  // only K columns can pick a larger split (fewer tiles) than the reservation holds
+  d.split_k = pick_split(N, K + 1, M);
   d.workspace = ws;
   return launch_gemm(d, s);
 }

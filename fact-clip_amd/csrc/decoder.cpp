@@ -115,6 +115,7 @@ long long dec_split_ws(const fx_decoder_params* p, int R, int T) {
   const int A = p->A, FF = p->FF;
   long long sp = 0;
   sp = std::max(sp, dwdb_ws(R, A, 3 * A));
+  sp = std::max(sp, dwdb_ws(R, A, 2 * A));   // q/k rows of the packed in-proj (value rows apart)
   sp = std::max(sp, dwdb_ws(R, A, A));
   sp = std::max(sp, dwdb_ws(R, A, FF));
   sp = std::max(sp, dwdb_ws(R, FF, A));
@@ -128,6 +129,9 @@ long long dec_split_ws(const fx_decoder_params* p, int R, int T) {
     sp = std::max(sp, split_ws(T, (int)AL2, p->Hm));
     sp = std::max(sp, dwdb_ws(T, p->Hm, (int)AL2));
     sp = std::max(sp, split_ws(T, p->Hm, (int)AL2));
+    // key rows only (the memory-pos gradient and its dW piece): half the tiles, up to twice the split
+    sp = std::max(sp, dwdb_ws(T, p->Hm, (int)(AL2 / 2)));
+    sp = std::max(sp, split_ws(T, p->Hm, (int)(AL2 / 2)));
   }
   return sp;
 }
