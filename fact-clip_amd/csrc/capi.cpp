@@ -300,8 +300,14 @@ int fx_linear_bwd(const float* dy, long long lddy, const float* x, long long ldx
     g = wz;
     ldg = N;
   }
-  if (dx) FX_TRY(linear_dx(g, ldg, w, M, K, N, dx, lddx, accumulate_dx, nullptr, 0, wsx, s, ldw));
-  if (dw) FX_TRY(linear_dwdb(g, ldg, x, ldx, M, K, N, dw, db, accumulate_w, wsw, s, lddw));
+  if (dx) {
+    WsBound wb(wsx, split_ws(M, K, N));
+    FX_TRY(linear_dx(g, ldg, w, M, K, N, dx, lddx, accumulate_dx, nullptr, 0, wsx, s, ldw));
+  }
+  if (dw) {
+    WsBound wb(wsw, dwdb_ws(M, K, N));
+    FX_TRY(linear_dwdb(g, ldg, x, ldx, M, K, N, dw, db, accumulate_w, wsw, s, lddw));
+  }
   else if (db) FX_TRY(launch_colsum(g, ldg, M, N, db, accumulate_w, wsc, s));
   return FX_OK;
 }
@@ -363,6 +369,7 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   float* ws = workspace;
   FX_TRY(pack_conv_weights(p, ws, L, s));
   float* spl = ws + L.split;
+  WsBound wb(spl, L.colsum - L.split);
   float* dH = ws + L.buf0;   // gradient w.r.t. the current layer output
   float* dU = ws + L.buf1;   // gradient at the residual sum (pre-LN)
   float* dZ = ws + L.buf2;   // gradient at the conv output (pre-ReLU)
@@ -496,6 +503,7 @@ int fx_mha_core_fwd(const float* q, long long ldq, const float* k, long long ldk
   FX_REQUIRE(nhead > 0 && E % nhead == 0, "mha: E must be divisible by nhead");
   const int hd = E / nhead;
   const float scale = 1.0f / std::sqrt((float)hd);
+  WsBound wb(workspace, workspace ? fx_mha_core_workspace_floats(Lq, Lk, E, nhead) : 0);
   // S_h = (Q_h K_h^T) * scale  -> probs buffer, then row softmax in place
   fx_gemm_desc d = gemm_desc(Lq, Lk, hd, op_rows(q, ldq), op_rows(k, ldk), probs, Lk);
   d.batch = nhead;
@@ -526,6 +534,7 @@ int fx_mha_core_bwd(const float* q, long long ldq, const float* k, long long ldk
   const float scale = 1.0f / std::sqrt((float)hd);
   float* dS = workspace;
   float* spl = workspace + (long long)nhead * Lq * Lk;
+  WsBound wb(spl, fx_mha_core_workspace_floats(Lq, Lk, E, nhead) - (long long)nhead * Lq * Lk);
   // dP_h = dO_h V_h^T
   fx_gemm_desc d = gemm_desc(Lq, Lk, hd, op_rows(dout, lddo), op_rows(v, ldv), dS, Lk);
   d.batch = nhead;
@@ -660,6 +669,7 @@ int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpo
   const VidRows V = vid_rows(Nx, Ny, nvid, x_off, y_off);
   FX_REQUIRE(V.x[V.n] == Nx && V.y[V.n] == Ny, "x2y: offsets must end at Nx / Ny");
   const X2YLayout L = x2y_layout(Nx, xdim, Ny, ydim, Hd);
+  WsBound wb(workspace, x2y_split_ws(V, xdim, ydim, Hd, outdim));
   float* xk = saved + L.xk;
   float* xv = saved + L.xv;
   float* yq = saved + L.yq;
@@ -746,6 +756,7 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
   float* dXk = dyq + (long long)Ny * Hd;
   float* dYq = dXk + (long long)Nx * xdim;
   float* spl = dYq + (long long)Ny * ydim;
+  WsBound wb(spl, x2y_split_ws(V, xdim, ydim, Hd, outdim));
   const float scale = 1.0f / std::sqrt((float)Hd);
   // Y_W: dcat = dout . Wy, dWy = dout^T [Y, feat], dby
   FX_TRY(linear_dx(dout, lddo, wy, Ny, cw, outdim, dcat, cw, 0, nullptr, 0, spl, s));
@@ -872,6 +883,7 @@ int fx_gru_bidir_bwd(const float* x, long long ldx, int S, int nseq, const int* 
   float* dgh = dgi + (long long)S * 2 * H3;        // 2 x (S, 3Hh)
   float* spl = dgh + 2LL * S * H3;
   float* csw = spl + gru_split_ws(S, In, Hh);
+  WsBound wb(spl, gru_split_ws(S, In, Hh));
   float* sync_ws = csw + colsum_workspace_floats(S, 3 * Hh);
   const float* whh[2] = {w_hh_f, w_hh_r};
   FX_TRY(launch_gru_bwd(dout, lddo, nq, off.data(), Hh, whh, saved, dgi, 2 * H3, dgh, sync_ws, s));

@@ -244,6 +244,7 @@ int fx_decoder_fwd(const fx_decoder_params* p, const float* tgt, long long ldt, 
   const DecLayout L = dec_layout(p, R, T, qpos != nullptr, mpos != nullptr, nvid);
   FX_REQUIRE(!qpos || ldqp == A, "decoder: query_pos must be dense (R, A)");
   float* spl = workspace + L.wsp;
+  WsBound wb(spl, L.total_ws_fwd - L.wsp);
   const int AL2 = 2 * A * NL;
   float* kv = saved + L.kv;
   if (p->cross) {
@@ -356,6 +357,7 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
   const int AL2 = 2 * A * NL;
   float* ws = workspace;
   float* spl = ws + L.split;
+  WsBound wb(spl, L.total_ws_bwd - L.split);
   float* lnws = ws + L.lnws;
   float* dT = ws + L.dT;     // gradient w.r.t. the current layer output
   float* dS = ws + L.dS;

@@ -41,6 +41,16 @@ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 // GEMM (internal C++ view of fx_gemm_desc; see include/factmx.h)
 // ------------------------------------------------------------------------
 int launch_gemm(const fx_gemm_desc& d, hipStream_t s);
+
+// Bound on the split-K slabs of the GEMMs issued while one of these is alive (thread-local, nests):
+// launch_gemm refuses a split whose slabs would leave [base, base + floats) -- a too-small
+// workspace reservation then fails loudly instead of overrunning the caller's buffer.
+struct WsBound {
+  WsBound(const float* base, long long floats);
+  ~WsBound();
+  const float* prev_lo;
+  const float* prev_hi;
+};
 // workspace floats needed by a split-K descriptor
 long long gemm_workspace_floats(const fx_gemm_desc& d);
 

@@ -1254,6 +1254,18 @@ unsigned* tile_counters(hipStream_t s) {
 
 }  // namespace
 
+thread_local const float* t_ws_lo = nullptr;
+thread_local const float* t_ws_hi = nullptr;
+
+WsBound::WsBound(const float* base, long long floats) : prev_lo(t_ws_lo), prev_hi(t_ws_hi) {
+  t_ws_lo = base;
+  t_ws_hi = base ? base + std::max(floats, 0LL) : nullptr;
+}
+WsBound::~WsBound() {
+  t_ws_lo = prev_lo;
+  t_ws_hi = prev_hi;
+}
+
 fx_operand op_rows(const float* p, long long ld) {
   fx_operand o{};
   o.ptr = p;
@@ -1360,6 +1372,9 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
     grid = dim3(g.tiles_x, g.tiles_y, d.batch * g.split);
     block = dim3(NTHREADS);
   }
+  FX_REQUIRE(g.split <= 1 || !t_ws_hi ||
+                 (g.ws >= t_ws_lo && g.ws + (long long)g.split * d.M * d.N * d.batch <= t_ws_hi),
+             "gemm: split-K slabs would overrun the entry point's workspace reservation");
   // in-launch reduction only while the last block's serial slab read stays small (<= 32 KB per
   // tile); bigger ones pay less as a separate reduce launch (conv dW split 5: 78 vs 56 us)
   const long long slab_bytes = (long long)g.split * (direct ? 32 * 32 : (wide ? WBM : BM) * BN) * 4;
