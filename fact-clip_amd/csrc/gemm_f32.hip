@@ -1203,7 +1203,9 @@ bool use_direct(const fx_gemm_desc& d, int ak, int bk) {
   // gathered A rows (ROWS_GEN / ROWS_CAT) load element by element in the direct kernel: only the
   // 32-row case pays off there (64 x 256 x 1024 concat: 54 us direct vs 29 us tiled)
   const int lim = (ak == ROWS_GEN || ak == ROWS_CAT) ? 32 : 64;
-  return d.M <= lim || d.N <= lim || d.K <= 64;
+  // a shallow K that is not a whole number of 64-deep stages would take the generic tiled kernel
+  // (InfoNCE dF: 4096 x 512 x 70, 80 us there); one pass of the direct kernel per tile is ~10x faster
+  return d.M <= lim || d.N <= lim || d.K <= 64 || (d.K <= 128 && d.K % 64 != 0);
 }
 
 // 128x64 tiles where the launch still has ~3/4 of a block per CU: FAST operands only.
