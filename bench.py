@@ -235,7 +235,7 @@ def main():
         achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
         roofline = dict(bound="mfma", achieved=round(achieved, 2), peak=F32_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
                         frac=round(achieved / F32_MFMA_PEAK_TFLOPS, 4),
-                        traffic=traffic_from_profiles(DOMINANT_KERNEL),
+                        traffic=(traffic_from_profiles(DOMINANT_KERNEL) if args.T == T_DEFAULT and args.videos == 2 else None),
                         kernel=DOMINANT_KERNEL + " (implicit dilated-conv GEMM: MS-TCN conv fwd + conv dX)",
                         launches=cnt.value, avg_launch_ms=round(avg_ms, 5),
                         flops_per_launch=flops_per_launch)
