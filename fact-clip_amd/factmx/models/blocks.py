@@ -151,8 +151,9 @@ class InputBlock(Block):
         a = fxf.decoder(self.action_branch, a2, f_out, pos=fpos, query_pos=apos, nvid=vb.nvid)
         a_out, a_cl = fxf.process_feature(a, self.nclass + 1)
         n = self.nclass + 1
-        self._vrec = [dict(frame_clogit=f_cl[vb.fr(v)].unsqueeze(1), action_clogit=a_cl[vb.tk(v)].unsqueeze(1),
-                           action_feature=a_out[vb.tk(v), :-n].unsqueeze(1)) for v in range(vb.nvid)]
+        fc, ac, ao = vb.frames(f_cl), vb.tokens(a_cl), vb.tokens(a_out)
+        self._vrec = [dict(frame_clogit=fc[v].unsqueeze(1), action_clogit=ac[v].unsqueeze(1),
+                           action_feature=ao[v][:, :-n].unsqueeze(1)) for v in range(vb.nvid)]
         return f_out, a_out
 
     def compute_loss(self, criterion, match=None):
@@ -203,12 +204,13 @@ class UpdateBlock(Block):
         f_out, f_cl = fxf.process_feature(f, self.nclass)
         n, Q, T = self.nclass + 1, vb.Q, vb.T
         recs = []
+        fc, ac, ao = vb.frames(f_cl), vb.tokens(a_cl), vb.tokens(a_out)
+        fat, aat, flg, alg = (torch.split(t, Q * T) for t in (f2a_at, a2f_at, f2a_lg, a2f_lg))
         for v in range(vb.nvid):
-            blk = slice(v * Q * T, (v + 1) * Q * T)
-            recs.append(dict(frame_clogit=f_cl[vb.fr(v)].unsqueeze(1), action_clogit=a_cl[vb.tk(v)].unsqueeze(1),
-                             action_feature=a_out[vb.tk(v), :-n].unsqueeze(1),
-                             f2a_attn=f2a_at[blk].view(1, Q, T), a2f_attn=a2f_at[blk].view(1, T, Q),
-                             f2a_attn_logit=f2a_lg[blk].view(1, Q, T), a2f_attn_logit=a2f_lg[blk].view(1, T, Q)))
+            recs.append(dict(frame_clogit=fc[v].unsqueeze(1), action_clogit=ac[v].unsqueeze(1),
+                             action_feature=ao[v][:, :-n].unsqueeze(1),
+                             f2a_attn=fat[v].view(1, Q, T), a2f_attn=aat[v].view(1, T, Q),
+                             f2a_attn_logit=flg[v].view(1, Q, T), a2f_attn_logit=alg[v].view(1, T, Q)))
         self._vrec = recs
         return f_out, a_out
 
@@ -302,20 +304,22 @@ class UpdateBlockTDU(Block):
         f = fxf.mstcn(self.frame_branch, f, T=vb.T, nvid=vb.nvid)
         f_out, f_cl = fxf.process_feature(f, self.nclass)
         n, Q = self.nclass + 1, vb.Q
-        recs, a0 = [], 0
+        recs = []
+        fc, ac, ao = vb.frames(f_cl), vb.tokens(a_cl), vb.tokens(a_out)
+        sc = torch.split(seg_cl, [s_off[v + 1] - s_off[v] for v in range(vb.nvid)])
+        qs = [Q * S[v] for v in range(vb.nvid)]
+        fat, aat, flg, alg = (torch.split(t, qs) for t in (f2a_at, a2f_at, f2a_lg, a2f_lg))
         for v in range(vb.nvid):
             Sv, tdu = S[v], tdus[v]
-            blk = slice(a0, a0 + Q * Sv)
-            a0 += Q * Sv
-            f2a_at_v = f2a_at[blk].view(1, 1, Q, Sv)
-            a2f_at_v = a2f_at[blk].view(1, 1, Sv, Q)
-            recs.append(dict(frame_clogit=f_cl[vb.fr(v)].unsqueeze(1),
-                             seg_clogit=seg_cl[s_off[v]:s_off[v + 1]].unsqueeze(1), tdu=tdu,
-                             action_clogit=a_cl[vb.tk(v)].unsqueeze(1),
-                             action_feature=a_out[vb.tk(v), :-n].unsqueeze(1),
-                             f2a_attn_logit=f2a_lg[blk].view(1, Q, Sv),
+            f2a_at_v = fat[v].view(1, 1, Q, Sv)
+            a2f_at_v = aat[v].view(1, 1, Sv, Q)
+            recs.append(dict(frame_clogit=fc[v].unsqueeze(1),
+                             seg_clogit=sc[v].unsqueeze(1), tdu=tdu,
+                             action_clogit=ac[v].unsqueeze(1),
+                             action_feature=ao[v][:, :-n].unsqueeze(1),
+                             f2a_attn_logit=flg[v].view(1, Q, Sv),
                              f2a_attn=tdu.attn_seg2frame(f2a_at_v[0].transpose(2, 1)).transpose(2, 1),
-                             a2f_attn_logit=a2f_lg[blk].view(1, Sv, Q),
+                             a2f_attn_logit=alg[v].view(1, Sv, Q),
                              a2f_attn=tdu.attn_seg2frame(a2f_at_v[0])))
         self._vrec = recs
         return f_out, a_out
@@ -409,12 +413,14 @@ class _FACTBase(nn.Module):
             feat_dim = f2.shape[-1] - self.num_classes
             proj = self.frame_projection(f2[:, :feat_dim])
 
+        proj_v = None if proj is None else vb.frames(proj)
+
         def restore(v):
             for blk in self.block_list:
                 for k, val in blk._vrec[v].items():
                     setattr(blk, k, val)
-            if proj is not None:
-                self.projected_frame_embeddings = proj[vb.fr(v)].unsqueeze(1)
+            if proj_v is not None:
+                self.projected_frame_embeddings = proj_v[v].unsqueeze(1)
         return restore
 
     def _fact_loss(self, label, label_host=None):
@@ -548,6 +554,15 @@ class _VideoBatch:
 
     def tk(self, v):
         return slice(v * self.Q, (v + 1) * self.Q)
+
+    # Per-video chunks through ONE split node per tensor: its backward concatenates the chunks'
+    # gradients once, where per-video slicing costs a zero-filled full-size tensor, a copy and an
+    # accumulating add per video (for every side-channel tensor a loss reads).
+    def frames(self, t):
+        return torch.split(t, self.T, dim=0)
+
+    def tokens(self, t):
+        return torch.split(t, self.Q, dim=0)
 
 
 def _batchable(net, seq_list):
