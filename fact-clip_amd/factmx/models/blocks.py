@@ -222,7 +222,7 @@ class UpdateBlock(Block):
         f2a_t = self.f2a_attn_logit.transpose(1, 2)
         f2a = criterion.attn_terms(match, f2a_t, axis=0, xe_coef=1.0, sm_coef=sw)
         a2f = criterion.attn_terms(match, self.a2f_attn_logit, axis=1, xe_coef=1.0, sm_coef=sw)
-        return atk + f2a + a2f + criterion.frame_terms(self.frame_clogit, 1.0, sw)
+        return _sum_terms([atk, f2a, a2f, criterion.frame_terms(self.frame_clogit, 1.0, sw)])
 
 
 class UpdateBlockTDU(Block):
@@ -330,8 +330,8 @@ class UpdateBlockTDU(Block):
         atk = criterion.action_token_loss(match, self.action_clogit)
         f2a = criterion.attn_terms(match, self.f2a_attn_logit.transpose(1, 2), axis=0, tdu=self.tdu)
         a2f = criterion.attn_terms(match, self.a2f_attn_logit, axis=1, tdu=self.tdu)
-        return (criterion.frame_terms(self.frame_clogit, 0.5, self.cfg.Loss.sw)
-                + criterion.seg_terms(self.seg_clogit, self.tdu, 0.5) + atk + f2a + a2f)
+        return _sum_terms([criterion.frame_terms(self.frame_clogit, 0.5, self.cfg.Loss.sw),
+                           criterion.seg_terms(self.seg_clogit, self.tdu, 0.5), atk, f2a, a2f])
 
 
 def _build_blocks(cfg, in_dim, n_classes):
@@ -429,7 +429,7 @@ class _FACTBase(nn.Module):
         last = self.block_list[-1]
         match = mc.match(basic.logit2prob(last.action_clogit, dim=-1), last.a2f_attn)
         self.loss_list = [blk.compute_loss(mc, match) for blk in self.block_list]
-        return sum(self.loss_list) / len(self.loss_list)
+        return _sum_terms(self.loss_list) / len(self.loss_list)
 
     def save_model(self, fname):
         torch.save(self.state_dict(), fname)
@@ -538,6 +538,17 @@ class FACT_CLIP(_FACTBase):
 
     def forward(self, seq_list, label_list, compute_loss=False):
         return _forward_videos(self, seq_list, label_list, compute_loss)
+
+
+def _sum_terms(terms):
+    """Sum of scalar loss terms in one reduction launch (a chain of `+` costs one 1-element kernel
+    per term); Python floats (terms a config switched off) are added on the host side."""
+    ts = [t for t in terms if torch.is_tensor(t)]
+    const = sum(float(t) for t in terms if not torch.is_tensor(t))
+    if not ts:
+        return const
+    total = ts[0] if len(ts) == 1 else torch.stack([t.reshape(()) for t in ts]).sum()
+    return total + const if const else total
 
 
 class _VideoBatch:
