@@ -1,5 +1,5 @@
 #!/usr/bin/env python
-"""Benchmark: FACT_CLIP forward+loss+backward(+grad all-reduce)+clip+Adam frames/s on MI355X.
+"""Benchmark: FACT_CLIP forward + loss + backward (+ gradient all-reduce) frames/s on MI355X.
 
 Workload (BASELINE.json metric, SURVEY.md section 8d "primary"): FACT_CLIP with
 the HAViD view0_lh_pt_holdout dims and FACT.ntoken 32 (H=512, A=F=256, FF=512,
@@ -7,19 +7,25 @@ the HAViD view0_lh_pt_holdout dims and FACT.ntoken 32 (H=512, A=F=256, FF=512,
 synthetic "seg10" videos (10 ground-truth segments, piecewise-constant
 features), random-init weights (torch.manual_seed), fp32 parity arithmetic,
 dropout / channel masking / time mask off (as in the reference CPU baseline).
-One step = the reference train step (scripts/train.py:262-268) over
-``--videos`` videos per rank: zero_grad, forward + loss, backward, gradient
-all-reduce (N>1), clip_grad_norm_(10), Adam(lr 1e-4).
+
+One timed step = zero_grad + forward + loss + backward over
+``--videos`` videos per rank (+ the gradient all-reduce for N>1), with the weights
+FIXED, so the data-dependent TDU segment counts S stay those of the initial weights
+(bench asserts they equal the CPU oracle's).  The reference train step's
+clip_grad_norm_(10) + Adam(lr 1e-4) (scripts/train.py:265-268) is timed separately
+afterwards and reported as the extra key ``train_step_with_adam`` (its updates move
+the weights and therefore S; the S it ends with is reported there).
 
   python bench.py [--gpus N --steps K --warmup W]
+  python bench.py --config breakfast         # BASELINE configs[0]: vanilla FACT, T=512
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Rank 0 prints one JSON line.  ``value`` = all frames processed by all ranks /
 max-over-ranks wall time of the K timed steps.
 """
 import argparse
+import ctypes
 import json
-import math
 import os
 import sys
 import time
@@ -32,9 +38,12 @@ import torch  # noqa: E402
 
 DOMINANT_KERNEL = "gemm_f32_wide8_kernel<1, 0>"   # rocprofv3 name: fx::(anonymous namespace)::gemm_f32_wide8_kernel<1, 0>
 METRIC = "frames/sec FACT_CLIP fwd+bwd, T=4096 D=2048 Nact=32, at 1/2/4/8 GPUs"
+METRIC_BREAKFAST = "frames/sec FACT fwd+bwd, Breakfast dims T=512 D=2048 Nact=60 (BASELINE configs[0])"
 F32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 HOLDOUT = [51, 53, 61, 67, 56]   # havid_view0_lh_pt_holdout.yaml
 D_IN, NCLS, NTOKEN, T_DEFAULT = 2048, 75, 32, 4096
+BF_NCLS, BF_NTOKEN, BF_T = 48, 60, 512   # breakfast.yaml (FACT.ntoken 60, 48 classes)
 
 
 def log(*a):
@@ -67,11 +76,37 @@ def make_cfg(ntoken=NTOKEN):
     return cfg
 
 
+def make_cfg_breakfast():
+    """fact_clip/configs/breakfast.yaml (vanilla FACT: MS-TCN++ frame branch 'm2', hid/a/f dim 512,
+    ntoken 60, 48 classes) with cmr / time mask off, as the CPU reference baseline runs."""
+    from factmx.configs import get_cfg_defaults
+    cfg = get_cfg_defaults()
+    cfg.Bi.update(dict(hid_dim=512, dropout=0.0, a="sca", a_nhead=8, a_ffdim=512, a_layers=6, a_dim=512,
+                       f="m2", f_layers=10, f_ln=False, f_dim=512, f_ngp=1))
+    for blk in (cfg.Bu, cfg.BU):
+        blk.update(dict(a="sa", a_dim=None, a_ffdim=None, a_layers=1, a_nhead=8, dropout=None, f=None,
+                        f_dim=None, f_layers=10, f_ln=None, f_ngp=None, hid_dim=None))
+    cfg.BU.s_layers = 1
+    cfg.FACT.update(dict(block="iuUU", cmr=0.0, fpos=False, mwt=0.1, ntoken=BF_NTOKEN, trans=False))
+    cfg.Loss.update(dict(a2fc=1.0, bgw=1.0, match="o2o", pc=0.2, sw=5.0))
+    cfg.Loss.nullw = BF_NTOKEN / ((BF_NTOKEN - 10) * BF_NCLS)
+    cfg.TM.use = False
+    cfg.holdout_mode = False
+    cfg.holdout_classes = []
+    cfg.use_clip = False
+    cfg.batch_size = 4
+    cfg.lr = 1e-4
+    cfg.optimizer = "Adam"
+    cfg.clip_grad_norm = 10.0
+    return cfg
+
+
 def make_video(T, D, C, cfg, seed, nseg=10):
     """seg10 synthetic video: 10 segments with sorted random cut points,
     one randn(D) prototype per segment, labels seen[(7i+3) % |seen|]."""
     g = torch.Generator().manual_seed(seed)
-    seen = [c for c in range(C) if c not in set(cfg.holdout_classes)]
+    hold = set(getattr(cfg, "holdout_classes", []) or [])
+    seen = [c for c in range(C) if c not in hold]
     cuts = torch.sort(torch.randperm(T - 1, generator=g)[: nseg - 1] + 1).values.tolist()
     bounds = [0] + cuts + [T]
     protos = torch.randn(nseg, D, generator=g)
@@ -89,14 +124,26 @@ def text_embeddings(C):
     return t / t.norm(dim=1, keepdim=True)
 
 
-def build_model(cfg, D, C, device, seed=0):
-    from factmx.models.blocks import FACT_CLIP
+def build_model(cfg, D, C, device, seed=0, clip=True):
+    from factmx.models.blocks import FACT, FACT_CLIP
     from factmx.models.loss import MatchCriterion
     text = text_embeddings(C)
     torch.manual_seed(seed)
-    net = FACT_CLIP(cfg, D, C, text_embeddings=text.clone())
+    net = FACT_CLIP(cfg, D, C, text_embeddings=text.clone()) if clip else FACT(cfg, D, C)
     net.mcriterion = MatchCriterion(cfg, C, [])
     return net.to(device), text
+
+
+def workload(name):
+    """(cfg, D, C, T default, videos per rank, FACT_CLIP?, metric) of a named bench workload."""
+    if name == "breakfast":
+        return make_cfg_breakfast(), D_IN, BF_NCLS, BF_T, 4, False, METRIC_BREAKFAST
+    return make_cfg(), D_IN, NCLS, T_DEFAULT, 2, True, METRIC
+
+
+def video_segments(net):
+    """Per-video TDU segment counts of the last forward: [[S of each U block] for each video]."""
+    return [list(s) for s in getattr(net, "video_segments", [])]
 
 
 def traffic_from_profiles(kernel_prefix):
@@ -114,42 +161,47 @@ def traffic_from_profiles(kernel_prefix):
     return None
 
 
-def cpu_baseline(T, min_seconds=10.0, min_steps=2):
-    """The CPU oracle (fp32 PyTorch restatement pinned to the reference) timed on host cores:
-    one video per step, full T, forward+loss+backward+Adam, repeated until >= min_seconds of
-    CPU work (bounded sample, ~10 s); also counts algorithmic FLOPs."""
+def cpu_baseline(wl, T, videos_seeds, min_seconds=10.0, min_steps=2):
+    """The CPU oracle (fp32 PyTorch restatement pinned to the reference) timed on host cores: one
+    video per step, full T, forward + prediction + loss + backward with FIXED weights (the same
+    unit as the GPU step), repeated until >= min_seconds of CPU work (a bounded sample).  Also
+    returns the algorithmic FLOPs of one video step and the oracle's TDU segment counts of every
+    bench video at the initial weights."""
     from torch.utils.flop_counter import FlopCounterMode
     from oracle import fact_oracle as fo
-    cfg = make_cfg()
-    net, text = build_model(cfg, D_IN, NCLS, "cpu", seed=0)
-    spec = fo.resolve_spec(cfg, D_IN, NCLS, clip=True)
+    cfg, D, C, _, _, clip, _ = workload(wl)
+    net, text = build_model(cfg, D, C, "cpu", seed=0, clip=clip)
+    spec = fo.resolve_spec(cfg, D, C, clip=clip)
     P = {n: p.detach().clone().float().requires_grad_(True) for n, p in net.named_parameters()}
-    opt = torch.optim.Adam(list(P.values()), lr=1e-4)
-    feats, label = make_video(T, D_IN, NCLS, cfg, seed=1)
-    seq = torch.from_numpy(feats)
+    txt = text if clip else None
+    vids = [make_video(T, D, C, cfg, seed=s) for s in videos_seeds]
 
-    def step():
+    def step(v=0):
         for p in P.values():
             p.grad = None
-        out = fo.forward(spec, P, seq)
-        fo.predict(spec, out, text)
-        total, _, _, _ = fo.video_loss(spec, out, label, text)
+        out = fo.forward(spec, P, torch.from_numpy(vids[v][0]))
+        fo.predict(spec, out, txt)
+        total, _, _, _ = fo.video_loss(spec, out, vids[v][1], txt)
         total.backward()
-        torch.nn.utils.clip_grad_norm_(list(P.values()), 10.0)
-        opt.step()
+        return out
 
+    S = []
+    with torch.no_grad():
+        for f, _ in vids:
+            out = fo.forward(spec, P, torch.from_numpy(f))
+            S.append([len(r["tdu"].starts) for r in out["blocks"] if r["type"] == "U"])
     with FlopCounterMode(display=False) as fc:
         step()
     flops = fc.get_total_flops()
     t0 = time.perf_counter()
-    videos_timed = 0
-    while videos_timed < min_steps or time.perf_counter() - t0 < min_seconds:
-        step()
-        videos_timed += 1
+    n = 0
+    while n < min_steps or time.perf_counter() - t0 < min_seconds:
+        step(n % len(vids))
+        n += 1
     dt = time.perf_counter() - t0
-    return dict(value=round(videos_timed * T / dt, 1), unit="frames/s", cores=torch.get_num_threads(), kind="port",
-                sample=f"{videos_timed} steps x 1 video (T={T}, seg10) fwd+loss+bwd+Adam, oracle fp32 "
-                       f"(1 untimed warm-up step, {dt:.1f} s timed)"), flops
+    return dict(value=round(n * T / dt, 1), unit="frames/s", cores=torch.get_num_threads(), kind="port",
+                sample=f"{n} steps x 1 video (T={T}, seg10, the bench videos in turn) fwd+loss+bwd, fixed weights, "
+                       f"oracle fp32 (1 untimed warm-up step, {dt:.1f} s timed)"), flops, S
 
 
 def main():
@@ -157,10 +209,18 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--videos", type=int, default=2, help="videos per rank per step (HAViD batch_size)")
-    ap.add_argument("--T", type=int, default=T_DEFAULT)
+    ap.add_argument("--config", choices=["havid", "breakfast"], default="havid",
+                    help="havid: FACT_CLIP T=4096 (the BASELINE metric); breakfast: vanilla FACT T=512")
+    ap.add_argument("--videos", type=int, default=None, help="videos per rank per step (yaml batch_size)")
+    ap.add_argument("--T", type=int, default=None)
+    ap.add_argument("--adam-steps", type=int, default=None,
+                    help="extra timed steps with clip_grad_norm_ + Adam after the fixed-weight steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    cfg, D, C, T_def, vids_def, clip, metric = workload(args.config)
+    T = args.T or T_def
+    nv = args.videos or vids_def
+    adam_steps = args.steps if args.adam_steps is None else args.adam_steps
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -173,36 +233,33 @@ def main():
     dev = torch.device("cuda", local)
 
     from factmx import native
-    from factmx.dp import FlatGradReducer
+    from factmx.dp import DataParallel
     from factmx.optim import FusedAdam
     lib = native.load()
 
-    cfg = make_cfg()
-    net, _ = build_model(cfg, D_IN, NCLS, dev, seed=0)
+    net, _ = build_model(cfg, D, C, dev, seed=0, clip=clip)
     net.train()
-    reducer = FlatGradReducer(net.parameters())
-    # clip_grad_norm_(cfg.clip_grad_norm) + Adam(lr) of scripts/train.py:265-267, fused on the flat buffers
-    opt = FusedAdam(net.parameters(), lr=cfg.lr, max_grad_norm=cfg.clip_grad_norm, grad_flat=reducer.flat)
+    dp = DataParallel(net)      # flat gradient buckets (+ rank-0 weight broadcast, overlapped all-reduce)
+    seeds = [1 + rank * nv + v for v in range(nv)]
     seqs, labels = [], []
-    for v in range(args.videos):
-        f, l_ = make_video(args.T, D_IN, NCLS, cfg, seed=1 + rank * args.videos + v)
+    for s in seeds:
+        f, l_ = make_video(T, D, C, cfg, seed=s)
         seqs.append(torch.from_numpy(f).to(dev))
         labels.append(torch.from_numpy(l_).to(dev))
 
     def step():
-        reducer.zero_grad()
+        dp.zero_grad()
         loss, _ = net(seqs, labels, compute_loss=True)
         loss.backward()
-        reducer.all_reduce_mean()
-        opt.step()                      # clip_grad_norm_ + Adam
+        dp.finish_gradients()           # bucket all-reduces (mean) for N>1
         return loss
 
     for _ in range(args.warmup):
         step()
-    S = [blk.tdu.num_seg for blk in net.block_list if hasattr(blk, "tdu")]
-    log(f"[rank {rank}] TDU segments per U block: {S}")
+    S = video_segments(net)
+    log(f"[rank {rank}] TDU segments per video (per U block): {S}")
 
-    max_ev = args.steps * args.videos * 4 * 10 * 2 + 64
+    max_ev = args.steps * nv * 4 * 10 * 2 + 64
     native.check(lib.fx_prof_enable(0, max_ev), "fx_prof_enable")
     if world > 1:
         dist.barrier()
@@ -214,45 +271,75 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ms = native.D()
-    fl = native.D()
-    by = native.D()
-    cnt = native.I()
-    import ctypes
+    ms, fl, by, cnt = native.D(), native.D(), native.D(), native.I()
     native.check(lib.fx_prof_collect(0, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(by), ctypes.byref(cnt)),
                  "fx_prof_collect")
     lib.fx_prof_disable()
+    S_after = video_segments(net)
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
 
-    frames = world * args.videos * args.T * args.steps
+    # the reference train step (clip_grad_norm_ + Adam), timed after the fixed-weight steps
+    adam = None
+    if adam_steps > 0:
+        opt = FusedAdam(net.parameters(), lr=cfg.lr, max_grad_norm=cfg.clip_grad_norm, grad_flat=dp.flat)
+        step()
+        opt.step()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ta = time.perf_counter()
+        for _ in range(adam_steps):
+            step()
+            opt.step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        ea = time.perf_counter() - ta
+        if world > 1:
+            t = torch.tensor([ea], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ea = t.item()
+        adam = dict(value=round(world * nv * T * adam_steps / ea, 1), unit="frames/s", steps=adam_steps,
+                    ms_per_step=round(1e3 * ea / adam_steps, 3), tdu_segments_after=video_segments(net),
+                    note="zero_grad + fwd + loss + bwd (+all-reduce) + clip_grad_norm_(10) + Adam(lr 1e-4); the "
+                         "updates move the weights, so S drifts from the fixed-weight value")
+
+    frames = world * nv * T * args.steps
     value = frames / elapsed
     if rank == 0:
         avg_ms = ms.value / max(cnt.value, 1)
         flops_per_launch = fl.value / max(cnt.value, 1)
         achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
+        default_shape = args.config == "havid" and T == T_DEFAULT and nv == 2
         roofline = dict(bound="mfma", achieved=round(achieved, 2), peak=F32_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
                         frac=round(achieved / F32_MFMA_PEAK_TFLOPS, 4),
-                        traffic=(traffic_from_profiles(DOMINANT_KERNEL) if args.T == T_DEFAULT and args.videos == 2 else None),
-                        kernel=DOMINANT_KERNEL + " (implicit dilated-conv GEMM: MS-TCN conv fwd + conv dX)",
+                        traffic=(traffic_from_profiles(DOMINANT_KERNEL) if default_shape else None),
+                        kernel=("gemm_f32_wide8_kernel (implicit dilated-conv GEMM: conv fwd + conv dX)"),
                         launches=cnt.value, avg_launch_ms=round(avg_ms, 5),
                         flops_per_launch=flops_per_launch)
-        line = dict(metric=METRIC, value=round(value, 1), unit="frames/s", n_gpus=world, steps=args.steps,
+        line = dict(metric=metric, value=round(value, 1), unit="frames/s", n_gpus=world, steps=args.steps,
                     warmup=args.warmup, ms_per_step=round(1e3 * elapsed / args.steps, 3), higher_is_better=True,
                     scaling="weak", vs_baseline=None, dtype="fp32", data="synthetic",
-                    config=dict(workload=f"FACT_CLIP HAViD-holdout dims, seg10 synthetic, T={args.T}",
-                                model="FACT_CLIP", T=args.T, D=D_IN, Nact=NTOKEN, C=NCLS,
-                                videos_per_rank=args.videos, global_batch=world * args.videos, seq_len=args.T,
-                                parallelism=f"dp{world}", tdu_segments=S),
-                    roofline=roofline)
+                    config=dict(workload=(f"FACT_CLIP HAViD-holdout dims, seg10 synthetic, T={T}" if clip else
+                                          f"FACT (vanilla) Breakfast dims, seg10 synthetic, T={T}"),
+                                model="FACT_CLIP" if clip else "FACT", T=T, D=D, Nact=cfg.FACT.ntoken, C=C,
+                                videos_per_rank=nv, global_batch=world * nv, seq_len=T,
+                                parallelism=f"dp{world}", weights="fixed (no optimizer update in the timed steps)",
+                                tdu_segments=S, tdu_segments_after_timing=S_after),
+                    roofline=roofline, train_step_with_adam=adam)
         if world == 1 and not args.no_cpu_baseline:
-            cb, step_flops = cpu_baseline(args.T)
+            cb, step_flops, S_oracle = cpu_baseline(args.config, T, seeds)
             line["cpu_baseline"] = cb
+            line["tdu_segments_oracle"] = S_oracle
+            line["tdu_segments_match_oracle"] = S_oracle == S
             step_time = elapsed / args.steps
-            line["step_mfma_frac"] = round(step_flops * args.videos / step_time / 1e12 / F32_MFMA_PEAK_TFLOPS, 5)
+            line["step_mfma_frac"] = round(step_flops * nv / step_time / 1e12 / F32_MFMA_PEAK_TFLOPS, 5)
             line["step_gflop_per_video"] = round(step_flops / 1e9, 2)
+            if S_oracle != S:
+                log(f"WARNING: GPU TDU segments {S} differ from the oracle's {S_oracle}")
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)

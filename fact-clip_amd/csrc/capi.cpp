@@ -266,7 +266,13 @@ const char* fx_last_error(void) { return g_last_error.c_str(); }
 
 int fx_gemm(const fx_gemm_desc* desc, void* stream) {
   FX_REQUIRE(desc, "fx_gemm: null descriptor");
-  return launch_gemm(*desc, (hipStream_t)stream);
+  // implicit dilated-conv GEMMs (A = shifted-tap operand: conv forward / conv dX, e.g. MSTCN2) are
+  // the same kernel class the bench times inside fx_mstcn_*
+  const bool conv = desc->a.conv_taps && !desc->a.trans;
+  if (conv) prof_begin(0, (hipStream_t)stream);
+  const int st = launch_gemm(*desc, (hipStream_t)stream);
+  if (conv) prof_end(0, (hipStream_t)stream, 2.0 * desc->M * desc->N * desc->K * desc->batch, 0.0);
+  return st;
 }
 
 long long fx_gemm_workspace_floats(const fx_gemm_desc* desc) { return desc ? gemm_workspace_floats(*desc) : 0; }

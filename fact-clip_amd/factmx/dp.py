@@ -5,29 +5,68 @@ loop over B=1 videos whose losses are averaged (blocks.py:913-915).  Sharding
 the videos over ranks and averaging gradients is therefore exactly equivalent
 for equal per-rank counts.
 
-``FlatGradReducer`` makes every parameter's ``.grad`` a view into a few large
-contiguous buckets, so backward accumulates straight into the communication
-buffers and the exchange is a handful of large all-reduces (xGMI rings are
-per-link bandwidth bound: few, big messages).  Buckets are launched
-asynchronously as soon as backward finishes; clip-grad-norm then runs on the
-identical reduced gradients on every rank with no extra collective.
+``DataParallel`` makes every parameter's ``.grad`` a view into ONE flat fp32
+buffer (the HIP kernels accumulate weight gradients straight into those views),
+laid out in parameter order, so the parameters of each FACT block are one
+contiguous slice.  Those slices are the all-reduce buckets: the model marks the
+input of every block during the forward (``mark_block_input``); when autograd
+has produced the gradient of block k's input, every kernel of block k's backward
+has been enqueued, so its bucket's all-reduce is launched right there
+(asynchronously, on the collective stream, ordered after those kernels) and runs
+over xGMI while blocks k-1 .. 0 compute their backward.  ``finish_gradients``
+launches what is left (block 0, the action queries and the CLIP projection head,
+whose gradients are only final at the end) and makes the compute stream wait
+for all of them -- no host synchronisation.  Buckets are few and large (xGMI
+rings are per-link bandwidth bound).  Rank 0's weights are broadcast once at
+construction, so every rank starts from identical parameters whatever its seed.
+
+``FlatGradReducer`` is the same flat buffer without per-block buckets (one or
+more equal buckets reduced after backward), for models without a block list.
 """
 import torch
 import torch.distributed as dist
+
+
+def _dist_world(group=None):
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1
+    return dist.get_world_size(group)
+
+
+def _flat_grads(params):
+    dev = params[0].device
+    total = sum(p.numel() for p in params)
+    flat = torch.zeros(total, device=dev, dtype=params[0].dtype)
+    off = 0
+    for p in params:
+        n = p.numel()
+        p.grad = flat[off:off + n].view_as(p)
+        off += n
+    return flat
+
+
+def _check_views(params, flat):
+    lo = flat.data_ptr()
+    hi = lo + flat.numel() * flat.element_size()
+    for p in params:
+        if p.grad is None or not (lo <= p.grad.data_ptr() < hi):
+            raise RuntimeError("parameter .grad was detached from the flat buffer (use zero_grad here, "
+                               "not optimizer.zero_grad(set_to_none=True))")
+
+
+def _all_reduce_mean_async(t, group):
+    """Launch an all-reduce (mean) of t; returns (work, needs_div)."""
+    if dist.get_backend(group) == "nccl":      # RCCL averages inside the collective
+        return dist.all_reduce(t, op=dist.ReduceOp.AVG, group=group, async_op=True), False
+    return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True), True
 
 
 class FlatGradReducer:
     def __init__(self, params, bucket_mb=64, group=None):
         self.params = [p for p in params if p.requires_grad]
         self.group = group
-        dev = self.params[0].device
-        total = sum(p.numel() for p in self.params)
-        self.flat = torch.zeros(total, device=dev, dtype=self.params[0].dtype)
-        off = 0
-        for p in self.params:
-            n = p.numel()
-            p.grad = self.flat[off:off + n].view_as(p)
-            off += n
+        self.flat = _flat_grads(self.params)
+        total = self.flat.numel()
         per = max(1, int(bucket_mb * (1 << 20) // self.flat.element_size()))
         self.buckets = [self.flat[i:i + per] for i in range(0, total, per)]
 
@@ -36,27 +75,132 @@ class FlatGradReducer:
         re-verified every 64th call only (a Python loop over 400+ tensors is host time)."""
         self.flat.zero_()
         self._calls = getattr(self, "_calls", -1) + 1
-        if self._calls % 64:
-            return
-        for p in self.params:
-            if p.grad is None or p.grad.data_ptr() < self.flat.data_ptr() or \
-                    p.grad.data_ptr() >= self.flat.data_ptr() + self.flat.numel() * self.flat.element_size():
-                raise RuntimeError("parameter .grad was detached from the flat buffer (use zero_grad here, "
-                                   "not optimizer.zero_grad(set_to_none=True))")
+        if self._calls % 64 == 0:
+            _check_views(self.params, self.flat)
 
     def all_reduce_mean(self):
-        if not (dist.is_available() and dist.is_initialized()):
-            return
-        world = dist.get_world_size(self.group)
+        world = _dist_world(self.group)
         if world == 1:
             return
-        if dist.get_backend(self.group) == "nccl":
-            # RCCL averages in the collective itself (no extra scale launch)
-            works = [dist.all_reduce(b, op=dist.ReduceOp.AVG, group=self.group, async_op=True) for b in self.buckets]
-            for w in works:
-                w.wait()
-            return
-        works = [dist.all_reduce(b, op=dist.ReduceOp.SUM, group=self.group, async_op=True) for b in self.buckets]
-        for w in works:
+        works = [_all_reduce_mean_async(b, self.group) for b in self.buckets]
+        for w, _ in works:
             w.wait()
-        self.flat.div_(world)
+        if works and works[0][1]:
+            self.flat.div_(world)
+
+
+def mark_block_input(net, k, x):
+    """Called by the model's forward with the input tensor of block k: registers the hook that
+    launches block k's gradient bucket once autograd has produced x's gradient."""
+    dp = getattr(net, "_fx_dp", None)
+    if dp is None or not torch.is_grad_enabled() or not torch.is_tensor(x) or not x.requires_grad:
+        return
+    dp._arm(k, x)
+
+
+class DataParallel:
+    """Whole-video data parallelism for FACT / FACT_CLIP (or any module with a ``block_list``).
+
+    dp = DataParallel(net)                 # broadcast rank 0's weights, flat grad buckets
+    dp.zero_grad(); loss = net(...)[0]; loss.backward(); dp.finish_gradients()
+    optimizer over dp.flat (factmx.optim.FusedAdam(..., grad_flat=dp.flat))
+    """
+
+    def __init__(self, net, group=None, broadcast=True, bucket_mb=256):
+        self.net = net
+        self.group = group
+        self.world = _dist_world(group)
+        named = [(n, p) for n, p in net.named_parameters() if p.requires_grad]
+        self.params = [p for _, p in named]
+        if broadcast and self.world > 1:
+            self._broadcast_from_rank0()
+        self.flat = _flat_grads(self.params)
+        # contiguous parameter range of every block (parameter order = registration order)
+        nblk = len(getattr(net, "block_list", []))
+        ranges = {}
+        off = 0
+        for n, p in named:
+            parts = n.split(".")
+            if parts[0] == "block_list" and len(parts) > 1 and parts[1].isdigit():
+                k = int(parts[1])
+                lo, hi = ranges.get(k, (off, off))
+                if hi != off:
+                    raise RuntimeError(f"block {k} parameters are not contiguous in parameter order")
+                ranges[k] = (lo, off + p.numel())
+            off += p.numel()
+        per = max(1, int(bucket_mb * (1 << 20) // 4))
+        self.block_buckets = {k: [self.flat[i:min(i + per, hi)] for i in range(lo, hi, per)]
+                              for k, (lo, hi) in ranges.items()}
+        # everything outside the blocks (action queries, CLIP projection head): the tail buckets
+        rest, cur = [], 0
+        for lo, hi in sorted(ranges.values()) + [(self.flat.numel(), self.flat.numel())]:
+            rest += [self.flat[a:min(a + per, lo)] for a in range(cur, lo, per)]
+            cur = hi
+        self.rest_buckets = rest
+        self.nblk = nblk
+        self._pending = []
+        self._launched = set()
+        self.hook_launched = []
+        self._armed = {}
+        self._calls = -1
+        if self.world > 1:
+            net._fx_dp = self
+
+    @torch.no_grad()
+    def _broadcast_from_rank0(self):
+        flat = torch.cat([p.detach().reshape(-1) for p in self.params])
+        dist.broadcast(flat, 0, group=self.group)
+        off = 0
+        for p in self.params:
+            p.copy_(flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+        for b in self.net.buffers():
+            if b.is_floating_point():
+                dist.broadcast(b, 0, group=self.group)
+
+    def zero_grad(self):
+        self.flat.zero_()
+        self._pending = []
+        self._launched = set()
+        self.hook_launched = []
+        self._armed = {}
+        self._calls += 1
+        if self._calls % 64 == 0:
+            _check_views(self.params, self.flat)
+
+    def _arm(self, k, x):
+        # one arm per video that ran block k (the per-video path runs the blocks once per video):
+        # the bucket launches when the LAST of them has its input gradient
+        if k in self.block_buckets:
+            self._armed[k] = self._armed.get(k, 0) + 1
+            x.register_hook(lambda g, k=k: self._fired(k))
+
+    def _fired(self, k):
+        self._armed[k] -= 1
+        if self._armed[k] == 0:
+            self._launch_block(k, True)
+
+    def _launch_block(self, k, from_hook=False):
+        if self.world == 1 or k in self._launched:
+            return
+        self._launched.add(k)
+        if from_hook:
+            self.hook_launched.append(k)
+        for b in self.block_buckets.get(k, []):
+            self._pending.append(_all_reduce_mean_async(b, self.group))
+
+    def finish_gradients(self):
+        """Launch the buckets no hook has launched and make the current stream wait for all of them."""
+        if self.world == 1:
+            return
+        for k in sorted(self.block_buckets, reverse=True):
+            self._launch_block(k)
+        for b in self.rest_buckets:
+            self._pending.append(_all_reduce_mean_async(b, self.group))
+        need_div = False
+        for w, div in self._pending:
+            w.wait()
+            need_div = need_div or div
+        self._pending = []
+        if need_div:
+            self.flat.div_(self.world)

@@ -12,6 +12,7 @@ import torch.nn as nn
 
 from .. import functional as fxf
 from ..configs.utils import update_from
+from ..dp import mark_block_input
 from ..utils import utils
 from . import basic
 from . import loss as loss_mod
@@ -382,7 +383,8 @@ class _FACTBase(nn.Module):
             action_feature = self.action_embed(transcript).unsqueeze(1) + action_pe
             action_pe = torch.zeros_like(action_pe)
         block_output = []
-        for block in self.block_list:
+        for k, block in enumerate(self.block_list):
+            mark_block_input(self, k, frame_feature)
             frame_feature, action_feature = block(frame_feature, action_feature, frame_pe, action_pe)
             block_output.append([frame_feature, action_feature])
         return block_output
@@ -406,7 +408,8 @@ class _FACTBase(nn.Module):
         fpos = None if fpe is None else fpe.squeeze(1).repeat(nvid, 1)
         apos = self.action_query.squeeze(1).repeat(nvid, 1)
         a2 = torch.zeros_like(apos)
-        for blk in self.block_list:
+        for k, blk in enumerate(self.block_list):
+            mark_block_input(self, k, f2)       # DP: block k's gradient bucket launches once f2 has its grad
             f2, a2 = blk.forward_batch(f2, a2, fpos, apos, vb)
         proj = None
         if isinstance(self, FACT_CLIP):
@@ -631,15 +634,18 @@ def _forward_videos(net, seq_list, label_list, compute_loss):
                 vals.append(net.contrastive_loss.detach().reshape(()))
             pending.append((save, keys, vals))
 
+    net.video_segments = []     # per video: the TDU segment count of every U block (host ints, no sync)
     if _batchable(net, seq_list):
         restore = net._forward_batch(seq_list)
         for v in range(len(seq_list)):
             restore(v)
+            net.video_segments.append([blk.tdu.num_seg for blk in net.block_list if hasattr(blk, "tdu")])
             finish_video(v, None)
     else:
         for v, (seq, label) in enumerate(zip(seq_list, label_list)):
             trans = torch_class_label_to_segment_label(label)[0] if net.cfg.FACT.trans else None
             net._forward_one_video(seq.unsqueeze(1), trans)
+            net.video_segments.append([blk.tdu.num_seg for blk in net.block_list if hasattr(blk, "tdu")])
             finish_video(v, trans)
     # one read-back for every video's predictions (+ loss floats)
     host = torch.cat([p.reshape(-1).to(torch.int64) for p in preds]).cpu().numpy()

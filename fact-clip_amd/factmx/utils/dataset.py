@@ -98,19 +98,33 @@ class Dataset:
 class DataLoader:
     """dataset.py:80-131: batches of ``batch_size`` videos; the last batch wraps around to the
     start of the (shuffled) order; reshuffles (np.random) at the end of every epoch. Yields
-    (video names, [float32 (T, D) tensors], [int64 (T,) tensors], [evaluation label lists])."""
+    (video names, [float32 (T, D) tensors], [int64 (T,) tensors], [evaluation label lists]).
 
-    def __init__(self, dataset, batch_size, shuffle=False):
+    Data parallel (factmx.dp): with ``world_size`` > 1 every rank walks the SAME global batch
+    sequence (the shuffle comes from a RandomState seeded with ``seed``, identical on every rank,
+    instead of the global np.random stream) and yields only its own share of each global batch,
+    videos ``rank, rank + world_size, ...`` of it -- so the ranks' per-video losses together are
+    exactly the reference's batch (blocks.py:913-915 averages them), and the DP all-reduce of the
+    mean gradients equals the single-process gradient.  ``batch_size`` is the global batch and
+    must be a multiple of ``world_size``."""
+
+    def __init__(self, dataset, batch_size, shuffle=False, rank=0, world_size=1, seed=0):
+        if world_size < 1 or not 0 <= rank < world_size:
+            raise ValueError(f"rank {rank} / world_size {world_size}")
+        if batch_size % world_size:
+            raise ValueError(f"global batch {batch_size} is not a multiple of world_size {world_size}")
         self.num_video = len(dataset)
         self.dataset = dataset
         self.videos = list(dataset.get_vnames())
         self.shuffle = shuffle
         self.batch_size = batch_size
+        self.rank, self.world_size = rank, world_size
+        self._rng = np.random.RandomState(seed) if world_size > 1 else np.random
         self.num_batch = int(np.ceil(self.num_video / self.batch_size))
         self.selector = list(range(self.num_video))
         self.index = 0
         if self.shuffle:
-            np.random.shuffle(self.selector)
+            self._rng.shuffle(self.selector)
 
     def __len__(self):
         return self.num_batch
@@ -118,17 +132,21 @@ class DataLoader:
     def __iter__(self):
         return self
 
-    def __next__(self):
+    def global_batch(self):
+        """Video names of the next global batch (all ranks), advancing the iterator."""
         if self.index >= self.num_video:
             if self.shuffle:
-                np.random.shuffle(self.selector)
+                self._rng.shuffle(self.selector)
             self.index = 0
             raise StopIteration
         idx = self.selector[self.index:self.index + self.batch_size]
         if len(idx) < self.batch_size:
             idx = idx + self.selector[:self.batch_size - len(idx)]
-        videos = [self.videos[i] for i in idx]
         self.index += self.batch_size
+        return [self.videos[i] for i in idx]
+
+    def __next__(self):
+        videos = self.global_batch()[self.rank::self.world_size]
         seqs, train_labels, eval_labels = [], [], []
         for v in videos:
             seq, tl, el = self.dataset[v]

@@ -1,8 +1,11 @@
-"""Data parallelism over whole videos (factmx.dp.FlatGradReducer), world_size 2 on gloo/CPU.
+"""Data parallelism over whole videos (factmx.dp), world_size 2 on gloo/CPU.
 
 The reference averages per-video losses over its batch (blocks.py:913-915), so
 sharding videos over ranks and all-reducing the mean of the gradients must equal
-the single-process gradient of the batch-mean loss.
+the single-process gradient of the batch-mean loss.  DataParallel additionally
+broadcasts rank 0's weights, launches each block's bucket from a backward hook
+(overlapping the rest of backward) and the rank-sharded DataLoader hands every
+rank its share of the same global batch.
 """
 import os
 import socket
@@ -12,7 +15,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from factmx.dp import FlatGradReducer
+from factmx.dp import DataParallel, FlatGradReducer, mark_block_input
 
 
 def _free_port():
@@ -83,3 +86,92 @@ def test_single_process_reduce_is_noop():
     red.flat.fill_(3.0)
     red.all_reduce_mean()
     assert torch.all(red.flat == 3.0)
+
+
+class _ToyBlocks(torch.nn.Module):
+    """block_list + a parameter shared by every block (like FACT's action queries)."""
+
+    def __init__(self, seed=0):
+        super().__init__()
+        torch.manual_seed(seed)
+        self.q = torch.nn.Parameter(torch.randn(12) * 0.1)
+        self.block_list = torch.nn.ModuleList([torch.nn.Linear(12, 12), torch.nn.Linear(12, 12),
+                                               torch.nn.Linear(12, 5)])
+
+    def forward(self, x):
+        h = x
+        for k, b in enumerate(self.block_list):
+            mark_block_input(self, k, h)
+            h = torch.tanh(b(h + (self.q if h.shape[-1] == 12 else 0)))
+        return h
+
+
+def _dp_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        net = _ToyBlocks(seed=rank)          # rank 1 starts from other weights: the broadcast fixes that
+        dp = DataParallel(net, bucket_mb=0.0002)
+        vids = _videos()
+        mine = vids[rank::world]
+        for step in range(2):
+            dp.zero_grad()
+            loss = sum(net(x).pow(2).mean() for x in mine) / len(mine)   # per-video forwards
+            loss.backward()
+            early = list(dp.hook_launched)
+            dp.finish_gradients()
+        if rank == 0:
+            torch.save({"grads": {n: p.grad.clone() for n, p in net.named_parameters()},
+                        "early": torch.tensor(early)}, out_path)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_hooks_broadcast_and_mean(tmp_path):
+    out = str(tmp_path / "dp.pt")
+    mp.spawn(_dp_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    # blocks 2 and 1 launched from backward hooks, in backward order; block 0 (input needs no grad)
+    # and the shared parameter at finish_gradients
+    assert got["early"].tolist() == [2, 1]
+    net = _ToyBlocks(seed=0)
+    vids = _videos()
+    loss = sum(net(x).pow(2).mean() for x in vids) / len(vids)
+    loss.backward()
+    for n, p in net.named_parameters():
+        torch.testing.assert_close(got["grads"][n], p.grad, rtol=1e-5, atol=1e-7)
+
+
+class _NamesDataset:
+    def __init__(self, n):
+        self.names = [f"v{i}" for i in range(n)]
+
+    def get_vnames(self):
+        return self.names
+
+    def __len__(self):
+        return len(self.names)
+
+    def __getitem__(self, v):
+        i = int(v[1:])
+        return torch.full((3, 2), float(i)).numpy(), [i] * 3, [i] * 3
+
+
+def test_rank_sharded_loader_partitions_the_global_batch():
+    from factmx.utils.dataset import DataLoader
+    ds = _NamesDataset(10)
+    loaders = [DataLoader(ds, 4, shuffle=True, rank=r, world_size=2, seed=7) for r in range(2)]
+    ref = DataLoader(ds, 4, shuffle=True, rank=0, world_size=2, seed=7)
+    for _ in range(2):                       # two epochs (reshuffle in between)
+        for _ in range(len(ref)):
+            parts = [next(ld) for ld in loaders]
+            glob = ref.global_batch()
+            assert parts[0][0] == glob[0::2] and parts[1][0] == glob[1::2]
+            assert sorted(parts[0][0] + parts[1][0]) == sorted(glob)
+        for ld in loaders:
+            with pytest.raises(StopIteration):
+                next(ld)
+        with pytest.raises(StopIteration):
+            ref.global_batch()
+    with pytest.raises(ValueError):
+        DataLoader(ds, 3, rank=0, world_size=2)

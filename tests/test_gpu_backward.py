@@ -1,0 +1,133 @@
+"""Forward + loss + BACKWARD parity of the HIP path against the fp64 CPU oracle at the
+benchmark and BASELINE.json config shapes (GPU).
+
+* north star (BASELINE metric / configs[2]): FACT_CLIP, HAViD holdout dims, T=4096, the bench's
+  two seg10 videos (seeds 1, 2) in one lockstep batch -- exactly the step bench.py times (split-K
+  dW over 8192 stacked rows, 128x64 wide tiles, lockstep split nodes).  TDU segment counts equal
+  the oracle's at these weights ([103, 27] and [89, 75]); batch loss within 1e-4 relative; every
+  parameter gradient within 2e-3 (sampled entries, norm and sum).  The same batch run as two
+  single-video steps gives the same mean gradient (the data-parallel equivalence on the real model:
+  DP over whole videos averages exactly these per-video gradients).
+* configs[1]: FACT_CLIP at HAViD dims with T=2048 (fp32; the bf16 perf mode reports its own S).
+* configs[0]: vanilla FACT at Breakfast dims (MS-TCN++ 'm2' frame branch, hid/a/f dim 512,
+  ntoken 60, C=48), T=512.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import GruKinks, compare_grads, oracle_batch
+from oracle import fact_oracle as fo
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _gpu_step(net, vids):
+    seqs = [torch.from_numpy(f).to(DEV) for f, _ in vids]
+    labs = [torch.from_numpy(l_).to(DEV) for _, l_ in vids]
+    for p in net.parameters():
+        p.grad = None
+    loss, saves = net(seqs, labs, compute_loss=True)
+    loss.backward()
+    torch.cuda.synchronize()
+    return loss.item(), saves
+
+
+def _segments(net):
+    import bench
+    return bench.video_segments(net)
+
+
+def _check_forward(net, spec, outs, saves, text, last_only_attrs=True):
+    """Per-video predictions identical; the side-channel attributes (the last video's) give logits
+    within 1e-3 and TDU boundaries identical."""
+    for v, out in enumerate(outs):
+        pred = fo.predict(spec, out, None if text is None else text.double().cpu())
+        np.testing.assert_array_equal(saves[v]["pred"], pred.numpy(), err_msg=f"video {v}")
+    rec_last = outs[-1]
+    for i, (blk, rec) in enumerate(zip(net.block_list, rec_last["blocks"])):
+        if rec["type"] == "U":
+            np.testing.assert_array_equal(blk.tdu.start32.cpu().numpy(), rec["tdu"].starts, err_msg=f"block {i}")
+            np.testing.assert_array_equal(blk.tdu.end32.cpu().numpy(), rec["tdu"].ends, err_msg=f"block {i}")
+        err = (blk.frame_clogit[:, 0].double().cpu() - rec["frame_clogit"]).abs().max().item()
+        assert err < 1e-3, f"block {i}: per-frame logits differ by {err}"
+
+
+def test_north_star_lockstep_backward_vs_oracle(monkeypatch):
+    import bench
+    from factmx.models import blocks as blocks_mod
+    cfg = bench.make_cfg()
+    T, D, C = 4096, 2048, 75
+    net, text = bench.build_model(cfg, D, C, device=DEV, seed=0)
+    net.train()
+    vids = [bench.make_video(T, D, C, cfg, seed=s) for s in (1, 2)]
+    assert blocks_mod._batchable(net, [torch.zeros(T, 1, device=DEV)] * 2)
+    kinks = GruKinks(monkeypatch)
+    loss, saves = _gpu_step(net, vids)
+    S = _segments(net)
+    grads = {n: p.grad.detach().clone() for n, p in net.named_parameters()}
+    spec = fo.resolve_spec(cfg, D, C, clip=True)
+    ref_loss, ref_grads, outs = oracle_batch(spec, net, vids, text)
+    S_ref = [[len(r["tdu"].starts) for r in o["blocks"] if r["type"] == "U"] for o in outs]
+    assert S == S_ref, (S, S_ref)
+    _check_forward(net, spec, outs, saves, text)
+    assert abs(loss - ref_loss) <= 1e-4 * abs(ref_loss), (loss, ref_loss)
+    compare_grads(net, ref_grads, rtol=2e-3, relaxed=kinks.flipped_prefixes(len(vids)), what="lockstep T=4096: ")
+    # data-parallel equivalence on the real model: the mean of the single-video gradients equals
+    # the batch gradient (a GRU output at the ReLU kink may round to the other side between the
+    # stacked and the single-video GEMMs: those blocks' GRU gradients are compared normwise)
+    lock_gru = [(y, off) for y, off in kinks.gpu]
+    acc = {n: torch.zeros_like(g) for n, g in grads.items()}
+    for v in vids:
+        _gpu_step(net, [v])
+        for n, p in net.named_parameters():
+            acc[n] += p.grad / len(vids)
+    single = [y for y, _ in kinks.gpu[len(lock_gru):]]          # video-major, one per U block
+    ublocks = [i for i, b in enumerate(net.block_list) if hasattr(b, "seg_update")]
+    flips = set()
+    for v in range(len(vids)):
+        for j, (y, off) in enumerate(lock_gru):
+            if ((y[off[v]:off[v + 1]] > 0) != (single[v * len(lock_gru) + j] > 0)).any():
+                flips.add(f"block_list.{ublocks[j]}.seg_update.")
+    for n, g in grads.items():
+        if any(n.startswith(f) for f in flips):
+            err = ((acc[n] - g).norm() / g.norm()).item()
+            assert err <= 2e-2, (n, "normwise", err)
+        else:
+            err = (acc[n] - g).abs().max().item()
+            assert err <= 1e-3 * g.abs().max().item() + 1e-7, (n, err)
+
+
+def test_fact_clip_T2048_vs_oracle(monkeypatch):
+    import bench
+    cfg = bench.make_cfg()
+    T, D, C = 2048, 2048, 75
+    net, text = bench.build_model(cfg, D, C, device=DEV, seed=0)
+    net.train()
+    vids = [bench.make_video(T, D, C, cfg, seed=s) for s in (3, 4)]
+    kinks = GruKinks(monkeypatch)
+    loss, saves = _gpu_step(net, vids)
+    S = _segments(net)
+    spec = fo.resolve_spec(cfg, D, C, clip=True)
+    ref_loss, ref_grads, outs = oracle_batch(spec, net, vids, text)
+    assert S == [[len(r["tdu"].starts) for r in o["blocks"] if r["type"] == "U"] for o in outs]
+    _check_forward(net, spec, outs, saves, text)
+    assert abs(loss - ref_loss) <= 1e-4 * abs(ref_loss), (loss, ref_loss)
+    compare_grads(net, ref_grads, rtol=2e-3, relaxed=kinks.flipped_prefixes(len(vids)), what="T=2048: ")
+
+
+def test_breakfast_vanilla_fact_vs_oracle(monkeypatch):
+    import bench
+    cfg = bench.make_cfg_breakfast()
+    T, D, C = bench.BF_T, 2048, bench.BF_NCLS
+    net, _ = bench.build_model(cfg, D, C, device=DEV, seed=0, clip=False)
+    net.train()
+    vids = [bench.make_video(T, D, C, cfg, seed=s) for s in (1, 2)]
+    kinks = GruKinks(monkeypatch)
+    loss, saves = _gpu_step(net, vids)
+    spec = fo.resolve_spec(cfg, D, C, clip=False)
+    ref_loss, ref_grads, outs = oracle_batch(spec, net, vids, None)
+    _check_forward(net, spec, outs, saves, None)
+    assert abs(loss - ref_loss) <= 1e-4 * abs(ref_loss), (loss, ref_loss)
+    compare_grads(net, ref_grads, rtol=2e-3, relaxed=kinks.flipped_prefixes(len(vids)), what="breakfast: ")

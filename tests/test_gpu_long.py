@@ -1,17 +1,18 @@
-"""Long-video and many-segment cases of the HIP FACT_CLIP path vs the CPU oracle (GPU).
+"""Long-video and many-segment cases of the HIP FACT_CLIP path vs the fp64 CPU oracle (GPU).
 
 * T=16384 seg10 — the synthetic stand-in for BASELINE.json configs[4] (Epic-Kitchens
   long video; the "dilated temporal window" is the MS-TCN dilation 2^i): per-frame logits
   within 1e-3 of the float64 oracle, TDU segment boundaries and per-frame predictions
-  identical, total loss within 1e-4 relative; backward produces finite gradients for
-  every parameter.
+  identical, total loss within 1e-4 relative, every parameter gradient within 2e-3
+  (sampled entries, norm and sum).
 * T=4096 i.i.d. features — the SURVEY §8(d) stress input (thousands of TDU segments,
-  GRU-bound): same checks on the forward and the loss.
+  GRU-bound: S = [3404, 1501]): the same checks.
 """
 import numpy as np
 import pytest
 import torch
 
+from helpers import GruKinks, compare_grads, oracle_batch
 from oracle import fact_oracle as fo
 
 pytestmark = pytest.mark.gpu
@@ -26,7 +27,7 @@ def _iid_video(T, D, C, cfg, seed):
 
 
 @pytest.mark.parametrize("kind,T", [("seg10", 16384), ("iid", 4096)])
-def test_long_and_many_segments_vs_oracle(kind, T):
+def test_long_and_many_segments_vs_oracle(kind, T, monkeypatch):
     import bench
     cfg = bench.make_cfg()
     D, C = 2048, 75
@@ -36,28 +37,29 @@ def test_long_and_many_segments_vs_oracle(kind, T):
     else:
         feats, label = _iid_video(T, D, C, cfg, seed=1)
     net.train()
+    kinks = GruKinks(monkeypatch)
     seq = torch.from_numpy(feats).to(DEV)
     lab = torch.from_numpy(label).to(DEV)
     loss, saves = net([seq], [lab], compute_loss=True)
     loss.backward()
-    for n, p in net.named_parameters():
-        assert p.grad is not None and torch.isfinite(p.grad).all(), n
+    torch.cuda.synchronize()
 
     spec = fo.resolve_spec(cfg, D, C, clip=True)
-    P = {n: p.detach().double().cpu() for n, p in net.named_parameters()}
+    ref_loss, ref_grads, (out,) = oracle_batch(spec, net, [(feats, label)], text)
     with torch.no_grad():
-        out = fo.forward(spec, P, torch.from_numpy(feats).double())
         pred = fo.predict(spec, out, text.double().cpu())
-        total, _, _, _ = fo.video_loss(spec, out, label, text.double().cpu())
     nseg = []
     for i, (blk, rec) in enumerate(zip(net.block_list, out["blocks"])):
         if rec["type"] == "U":
             np.testing.assert_array_equal(blk.tdu.start32.cpu().numpy(), rec["tdu"].starts, err_msg=f"block {i}")
             np.testing.assert_array_equal(blk.tdu.end32.cpu().numpy(), rec["tdu"].ends, err_msg=f"block {i}")
             nseg.append(len(rec["tdu"].starts))
-        err = (blk.frame_clogit[:, 0].double().cpu() - rec["frame_clogit"]).abs().max().item()
+        err = (blk.frame_clogit[:, 0].double().cpu() - rec["frame_clogit"].detach()).abs().max().item()
         assert err < 1e-3, f"block {i}: per-frame logits differ by {err}"
     np.testing.assert_array_equal(saves[0]["pred"], pred.numpy())
-    rel = abs(loss.item() - float(total)) / abs(float(total))
-    assert rel < 1e-4, f"loss {loss.item()} vs oracle {float(total)}"
+    rel = abs(loss.item() - ref_loss) / abs(ref_loss)
+    assert rel < 1e-4, f"loss {loss.item()} vs oracle {ref_loss}"
+    # absolute floor 1e-2 x RMS at 4096 frames, growing with sqrt(T) (fp32 sums over T rows)
+    compare_grads(net, ref_grads, rtol=2e-3, atol_rms=1e-2 * (T / 4096) ** 0.5, relaxed=kinks.flipped_prefixes(1),
+                  what=f"{kind} T={T}: ")
     print(f"{kind} T={T}: TDU segments {nseg}, loss {loss.item():.6f}")
