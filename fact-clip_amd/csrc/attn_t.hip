@@ -1,0 +1,618 @@
+// Multi-head attention of a few queries over T frames, fused (SCALayer cross-attention,
+// basic.py:508-516: nn.MultiheadAttention with Q = Nact action tokens, K/V = T frames, 8 heads).
+//
+// The reference runs it as ATen bmm -> softmax -> (dropout) -> bmm and keeps the (h, Q, T)
+// probabilities for backward; round 1 here was the same three GEMM/softmax launches (+ a split-K
+// reduce) per video.  Here ONE launch covers every video and head, flash-decoding style:
+//   grid = (T-chunk c, head h, video v); a workgroup stages q_h (Q x hd), K_c and V_c (Tc x hd) in
+//   LDS, computes S = q K_c^T (MFMA 32x32x2 f32), its row max m_c / sum l_c, and O_c = exp(S - m_c) V_c;
+//   the partials go to a workspace and the LAST workgroup of each (video, head) to arrive (arrival
+//   counter, agent-scope release/acquire) merges them in chunk order -- deterministic -- into
+//   o = sum_c e^(m_c - M) O_c / L and lse = M + log L.  Only lse (Q floats per head) is kept for
+//   backward, not the probabilities.
+// Backward recomputes P = exp(S - lse) per chunk: dV_c = P^T dO, dP = dO V_c^T, dS = P (dP - D)
+// with D = rowsum(dO o), dK_c = scale dS^T q (K/V rows of a chunk belong to ONE workgroup: written,
+// not accumulated), and dq = scale sum_c dS_c K_c through the same ordered last-arriver merge.
+// HBM bytes per frame and layer: K and V rows read once (2 hd h x 4 B per frame forward; backward
+// also writes dK, dV).
+#include <algorithm>
+#include <cmath>
+#include <mutex>
+
+#include "fx_common.h"
+#include "ops.h"
+
+namespace fx {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int AT = 256;   // threads per workgroup (4 waves)
+
+// Diagnostic builds (-DFX_STAMPS, libfactmx_stamps.so) stamp s_memtime at fixed points of every
+// workgroup into a buffer set by fx_dbg_tattn_stamps(); the shipped library compiles them away.
+#ifdef FX_STAMPS
+__device__ long long* g_tattn_stamps;
+#define TSTAMP(slot)                                                                                       \
+  do {                                                                                                   \
+    if (g_tattn_stamps && threadIdx.x == 0) {                                                            \
+      const long long _b = ((long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;      \
+      g_tattn_stamps[_b * 8 + (slot)] = __builtin_amdgcn_s_memtime();                                    \
+    }                                                                                                    \
+  } while (0)
+#else
+#define TSTAMP(slot) \
+  do {               \
+  } while (0)
+#endif
+
+// acc (32x32) += A (32 x K) . B (K x 32), operands in LDS.
+//   A element (r, k) = ATR ? a[k*lda + r] : a[r*lda + k]
+//   B element (k, c) = BTR ? b[c*ldb + k] : b[k*ldb + c]
+// K even; lane half hh takes k in [hh*K/2, hh*K/2 + K/2) -- any k order works as long as A and B agree.
+// Strides are odd (row length + 1) so the 32 lanes of a half hit 32 different banks.
+template <bool ATR, bool BTR>
+__device__ __forceinline__ void mm32(const float* a, int lda, const float* b, int ldb, int K, f32x16& acc, int lane) {
+  // K % 8 == 0 (every caller).  Software-pipelined: the LDS reads of the next 4 k-steps are issued
+  // before the MFMAs of the current 4.
+  const int li = lane & 31, kh = (lane >> 5) * (K >> 1);
+  float av[4], bv[4];
+  auto ld4 = [&](int j0, float* x, float* y) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = kh + j0 + j;
+      x[j] = ATR ? a[k * lda + li] : a[li * lda + k];
+      y[j] = BTR ? b[li * ldb + k] : b[k * ldb + li];
+    }
+  };
+  ld4(0, av, bv);
+  for (int j0 = 0; j0 < (K >> 1); j0 += 4) {
+    float an[4], bn[4];
+    if (j0 + 4 < (K >> 1)) ld4(j0 + 4, an, bn);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], bv[j], acc, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      av[j] = an[j];
+      bv[j] = bn[j];
+    }
+  }
+}
+
+// The same product with A row-major (k contiguous per row) read as ds_read_b128: a lane half's k range is
+// contiguous, so one 16-B read feeds 4 MFMAs.  B: BTR -> also contiguous k (b128); else b[k*ldb + c] (b32).
+// lda (and ldb for BTR) = row length + 4: 16-B aligned rows, conflict-free b128 lane groups.
+template <bool BTR>
+__device__ __forceinline__ void mm32v(const float* a, int lda, const float* b, int ldb, int K, f32x16& acc, int lane) {
+  const int li = lane & 31, kh = (lane >> 5) * (K >> 1);
+  const float* pa = a + li * lda + kh;
+  const float* pb = BTR ? b + li * ldb + kh : b + kh * ldb + li;
+  auto ldb4 = [&](int j0) {
+    if (BTR) return *reinterpret_cast<const float4*>(pb + j0);
+    return make_float4(pb[j0 * ldb], pb[(j0 + 1) * ldb], pb[(j0 + 2) * ldb], pb[(j0 + 3) * ldb]);
+  };
+  float4 av = *reinterpret_cast<const float4*>(pa), bv = ldb4(0);
+  for (int j0 = 0; j0 < (K >> 1); j0 += 4) {
+    float4 an = av, bn = bv;
+    if (j0 + 4 < (K >> 1)) {
+      an = *reinterpret_cast<const float4*>(pa + j0 + 4);
+      bn = ldb4(j0 + 4);
+    }
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv.w, acc, 0, 0, 0);
+    av = an;
+    bv = bn;
+  }
+}
+
+__device__ __forceinline__ void zero16(f32x16& a) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) a[i] = 0.f;
+}
+
+// accumulator element r of a lane: row (r&3) + 8 (r>>2) + 4 (lane>>5), column lane&31
+__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+struct TAttnArgs {
+  const float* q; long long ldq;
+  const float* k; long long ldk;
+  const float* v; long long ldv;
+  const float* o; long long ldo;        // bwd: forward output
+  const float* dout; long long lddo;    // bwd
+  float* out; long long ld_out;         // fwd: o;  bwd: dq
+  float* dk; long long lddk;            // bwd
+  float* dv; long long lddv;            // bwd
+  float* lse;                           // (nvid, h, Qv): fwd writes, bwd reads
+  float* ws;                            // partials
+  int Qv, Tv, hd, nh, Qp, Hp, Tc, nsplit;
+  float scale;
+  int vec;                              // 16-B loads of every q / k / v / o / dout row slice
+};
+
+// Strips of row-major sources staged into LDS images (row stride ld, zero outside the `nvalid` rows and
+// `hd` columns).  Every load of a workgroup's strips is issued before the first LDS store (a store
+// behind its own load would serialise the strips on the memory latency): float4 loads when every row
+// slice is 16-B aligned, up to NV float4 per thread and strip.
+template <int NV>
+struct Strip {
+  float4 v[NV];
+  __device__ __forceinline__ void load(int rows, int cols, const float* src, long long lds_, int nvalid, int hd,
+                                       int tid) {
+    const int c4 = cols >> 2, total = rows * c4;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int e = tid + i * AT;
+      const int r = e / c4, c = (e - r * c4) * 4;
+      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < total && r < nvalid && c < hd) x = *reinterpret_cast<const float4*>(src + (long long)r * lds_ + c);
+      v[i] = x;
+    }
+  }
+  __device__ __forceinline__ void store(float* img, int ld, int rows, int cols, int tid) const {
+    const int c4 = cols >> 2, total = rows * c4;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int e = tid + i * AT;
+      if (e < total) {
+        const int r = e / c4, c = (e - r * c4) * 4;
+        float* d = img + r * ld + c;
+        d[0] = v[i].x;
+        d[1] = v[i].y;
+        d[2] = v[i].z;
+        d[3] = v[i].w;
+      }
+    }
+  }
+};
+constexpr int NVQ = 4;    // q / o / dout strips: <= 64 x 64 floats
+constexpr int NVK = 8;    // K / V chunks: <= 8192 floats (the host keeps Tc * Hp within it)
+
+// element-wise fallback for unaligned / odd-width slices
+__device__ __forceinline__ void stage_scalar(float* img, int ld, int rows, int cols, const float* src, long long lds_,
+                                             int nvalid, int hd, int tid) {
+  for (int e = tid; e < rows * cols; e += AT) {
+    const int r = e / cols, c = e - r * cols;
+    img[r * ld + c] = (r < nvalid && c < hd) ? src[(long long)r * lds_ + c] : 0.f;
+  }
+}
+
+// ------------------------------------------------------------------------------------------ forward
+// grid (chunk, head, video).  nsplit == 1: o and lse directly; else the chunk's partial
+// O_c = e^(S - m_c) V_c (Qp x Hp) and its row stats (m_c, l_c) go to the workspace for tattn_merge.
+__global__ __launch_bounds__(AT) void tattn_fwd_kernel(TAttnArgs a) {
+  extern __shared__ float sm[];
+  const int c = blockIdx.x, h = blockIdx.y, vid = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int Qp = a.Qp, Hp = a.Hp, Tc = a.Tc, hd = a.hd;
+  const int lq = Hp + 4, lk = Hp + 4, ls = Tc + 4;   // 16-B aligned rows (b128 operand reads)
+  float* qs = sm;                       // [Qp][lq]
+  float* ks = qs + Qp * lq;             // [Tc][lk]
+  float* vs = ks + Tc * lk;             // [Tc][lk]
+  float* ss = vs + Tc * lk;             // [Qp][ls]
+  float* red = ss + Qp * ls;            // [4][1024] wave partials
+  float* rowm = red + 4 * 1024;         // [Qp]
+  float* rowl = rowm + Qp;              // [Qp]
+  const int t0 = c * Tc, nk = min(Tc, a.Tv - t0);
+  const long long qrow = (long long)vid * a.Qv, krow = (long long)vid * a.Tv + t0;
+  const float* qsrc = a.q + qrow * a.ldq + h * hd;
+  const float* ksrc = a.k + krow * a.ldk + h * hd;
+  const float* vsrc = a.v + krow * a.ldv + h * hd;
+  TSTAMP(0);
+  if (a.vec) {
+    Strip<NVQ> sq;
+    Strip<NVK> sk, sv;
+    sq.load(Qp, Hp, qsrc, a.ldq, a.Qv, hd, tid);
+    sk.load(Tc, Hp, ksrc, a.ldk, nk, hd, tid);
+    sv.load(Tc, Hp, vsrc, a.ldv, nk, hd, tid);
+    sq.store(qs, lq, Qp, Hp, tid);
+    sk.store(ks, lk, Tc, Hp, tid);
+    sv.store(vs, lk, Tc, Hp, tid);
+  } else {
+    stage_scalar(qs, lq, Qp, Hp, qsrc, a.ldq, a.Qv, hd, tid);
+    stage_scalar(ks, lk, Tc, Hp, ksrc, a.ldk, nk, hd, tid);
+    stage_scalar(vs, lk, Tc, Hp, vsrc, a.ldv, nk, hd, tid);
+  }
+  __syncthreads();
+  TSTAMP(1);
+  // S^T tiles (keys x queries) = scale K q^T kept in registers: wave w takes tiles w and w + 4 of the
+  // (key tile, query tile) grid -- both in query tile w % nrt -- and a lane holds 16 keys of ONE query
+  // column, so the softmax statistics are in-register reductions, one exchange with the other lane
+  // half and one pass through LDS across the waves.  Keys past the video: -inf.
+  const int nrt = Qp / 32, nct = Tc / 32;
+  const int qtw = wave % nrt;
+  const int myq = qtw * 32 + (lane & 31);
+  f32x16 st[2];
+  bool has[2];
+  float lm = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int t = wave + 4 * u;
+    has[u] = t < nrt * nct;
+    zero16(st[u]);
+    if (has[u]) {
+      const int kt = t / nrt;
+      mm32v<true>(ks + kt * 32 * lk, lk, qs + qtw * 32 * lq, lq, Hp, st[u], lane);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kt * 32 + acc_row(r, lane);
+        st[u][r] = key < nk ? st[u][r] * a.scale : -INFINITY;
+        lm = fmaxf(lm, st[u][r]);
+      }
+    }
+  }
+  TSTAMP(2);
+  float* wmax = red;              // [4][Qp]: per-wave maxima (-inf where the wave has no keys of a query)
+  float* wsum = red + 4 * Qp;     // [4][Qp]: per-wave sums
+  lm = fmaxf(lm, __shfl_xor(lm, 32, 64));
+  if (lane < Qp) wmax[wave * Qp + lane] = (has[0] && (lane >> 5) == qtw) ? lm : -INFINITY;
+  __syncthreads();
+  float M = -INFINITY;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) M = fmaxf(M, wmax[w * Qp + myq]);
+  float ls_ = 0.f;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (!has[u]) continue;
+    const int kt = (wave + 4 * u) / nrt;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = __expf(st[u][r] - M);
+      ls_ += p;
+      ss[myq * ls + kt * 32 + acc_row(r, lane)] = p;     // P image [query][key] for P V
+    }
+  }
+  ls_ += __shfl_xor(ls_, 32, 64);
+  if (lane < Qp) wsum[wave * Qp + lane] = (has[0] && (lane >> 5) == qtw) ? ls_ : 0.f;
+  __syncthreads();
+  if (wave < nrt && lane < 32) {
+    float L = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) L += wsum[w * Qp + myq];
+    rowm[myq] = M;
+    rowl[myq] = L;
+  }
+  __syncthreads();
+  TSTAMP(3);
+  // O_c = P V: nt output tiles, each split over wpt waves along the chunk
+  const int nht = Hp / 32, nt = nrt * nht, wpt = 4 / nt;
+  const int tile = wave / wpt, part = wave - tile * wpt;
+  const int dlen = Tc / wpt, d0 = part * dlen;
+  const int rt = tile / nht, ht = tile - rt * nht;
+  f32x16 acc;
+  zero16(acc);
+  mm32v<false>(ss + rt * 32 * ls + d0, ls, vs + d0 * lk + ht * 32, lk, dlen, acc, lane);
+  if (wpt > 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[wave * 1024 + r * 64 + lane] = acc[r];
+    __syncthreads();
+    if (part == 0)
+      for (int q = 1; q < wpt; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] += red[(wave + q) * 1024 + r * 64 + lane];
+  }
+  const long long pid = ((long long)vid * a.nh + h) * a.nsplit + c;   // partial index
+  if (part == 0) {
+    const int col = ht * 32 + (lane & 31);
+    if (a.nsplit == 1) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rt * 32 + acc_row(r, lane);
+        if (row < a.Qv && col < hd) a.out[(qrow + row) * a.ld_out + h * hd + col] = acc[r] / rowl[row];
+      }
+    } else {
+      float* po = a.ws + pid * Qp * Hp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) po[(rt * 32 + acc_row(r, lane)) * Hp + col] = acc[r];
+    }
+  }
+  if (a.nsplit == 1) {
+    for (int r = tid; r < a.Qv; r += AT) a.lse[((long long)vid * a.nh + h) * a.Qv + r] = rowm[r] + __logf(rowl[r]);
+    return;
+  }
+  float* pm = a.ws + (long long)gridDim.z * a.nh * a.nsplit * Qp * Hp;   // m partials, then l partials
+  float* pl = pm + (long long)gridDim.z * a.nh * a.nsplit * Qp;
+  for (int r = tid; r < Qp; r += AT) {
+    pm[pid * Qp + r] = rowm[r];
+    pl[pid * Qp + r] = rowl[r];
+  }
+  TSTAMP(4);
+}
+
+// Ordered merge of the nsplit partials of one (video, head) per workgroup, chunk order fixed
+// (deterministic).  Forward (stats != 0): w_s(r) = e^(m_s - M) / L, o = sum_s w_s O_s, lse = M + log L;
+// backward: dq = scale * sum_s dq_s.  A thread owns 4 consecutive columns of a row with 16 splits'
+// float4 loads in flight.
+__global__ __launch_bounds__(AT) void tattn_merge_kernel(TAttnArgs a, int stats, float mul) {
+  extern __shared__ float sm[];
+  const int h = blockIdx.x, vid = blockIdx.y, tid = threadIdx.x;
+  const int Qp = a.Qp, Hp = a.Hp, hd = a.hd, ns = a.nsplit;
+  const long long pbase = ((long long)vid * a.nh + h) * ns;
+  const float* part = a.ws + pbase * Qp * Hp;
+  float* w = sm;                         // [ns][Qp] weights
+  float* wl = sm + ns * Qp;              // [ns][Qp] l partials
+  if (stats) {
+    const float* pm = a.ws + (long long)gridDim.y * a.nh * ns * Qp * Hp + pbase * Qp;
+    const float* pl = pm + (long long)gridDim.y * a.nh * ns * Qp;
+    for (int e = tid; e < ns * Qp; e += AT) {
+      w[e] = pm[e];
+      wl[e] = pl[e];
+    }
+    __syncthreads();
+    for (int r = tid; r < Qp; r += AT) {
+      float M = -INFINITY;
+      for (int sp = 0; sp < ns; ++sp) M = fmaxf(M, w[sp * Qp + r]);
+      float L = 0.f;
+      for (int sp = 0; sp < ns; ++sp) L += __expf(w[sp * Qp + r] - M) * wl[sp * Qp + r];
+      const float inv = 1.f / L;
+      for (int sp = 0; sp < ns; ++sp) w[sp * Qp + r] = __expf(w[sp * Qp + r] - M) * inv;
+      if (r < a.Qv) a.lse[((long long)vid * a.nh + h) * a.Qv + r] = M + __logf(L);
+    }
+    __syncthreads();
+  }
+  float* out = a.out + (long long)vid * a.Qv * a.ld_out + h * hd;
+  const int c4 = Hp >> 2;
+  for (int e = tid; e < a.Qv * c4; e += AT) {
+    const int r = e / c4, col = (e - r * c4) * 4;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s0 = 0; s0 < ns; s0 += 16) {
+      float4 x[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        x[j] = *reinterpret_cast<const float4*>(part + ((long long)min(s0 + j, ns - 1) * Qp + r) * Hp + col);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if (s0 + j < ns) {
+          const float ww = stats ? w[(s0 + j) * Qp + r] : 1.f;
+          acc.x += ww * x[j].x;
+          acc.y += ww * x[j].y;
+          acc.z += ww * x[j].z;
+          acc.w += ww * x[j].w;
+        }
+      }
+    }
+    float* o = out + (long long)r * a.ld_out + col;
+    const float v[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (col + j < hd) o[j] = v[j] * mul;
+  }
+}
+
+// ------------------------------------------------------------------------------------------ backward
+__global__ __launch_bounds__(AT) void tattn_bwd_kernel(TAttnArgs a) {
+  extern __shared__ float sm[];
+  const int c = blockIdx.x, h = blockIdx.y, vid = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int Qp = a.Qp, Hp = a.Hp, Tc = a.Tc, hd = a.hd;
+  const int lq = Hp + 4, ls = Tc + 4;   // 16-B aligned rows (b128 operand reads)
+  float* qs = sm;                       // [Qp][lq]
+  float* dos = qs + Qp * lq;            // [Qp][lq]
+  float* ks = dos + Qp * lq;            // [Tc][lq]
+  float* vs = ks + Tc * lq;             // [Tc][lq]
+  float* ps = vs + Tc * lq;             // [Qp][ls]  P   (o until P is written)
+  float* ds = ps + Qp * ls;             // [Qp][ls]  dS
+  float* red = ds + Qp * ls;            // [4][1024]
+  float* rl = red + 4 * 1024;           // [Qp] lse
+  float* rd = rl + Qp;                  // [Qp] D
+  const int t0 = c * Tc, nk = min(Tc, a.Tv - t0);
+  const long long qrow = (long long)vid * a.Qv, krow = (long long)vid * a.Tv + t0;
+  const float* qsrc = a.q + qrow * a.ldq + h * hd;
+  const float* dsrc = a.dout + qrow * a.lddo + h * hd;
+  const float* osrc = a.o + qrow * a.ldo + h * hd;
+  const float* ksrc = a.k + krow * a.ldk + h * hd;
+  const float* vsrc = a.v + krow * a.ldv + h * hd;
+  if (tid < Qp) rl[tid] = tid < a.Qv ? a.lse[((long long)vid * a.nh + h) * a.Qv + tid] : 0.f;
+  if (a.vec) {
+    Strip<NVQ> sq, sd, so;
+    Strip<NVK> sk, sv;
+    sq.load(Qp, Hp, qsrc, a.ldq, a.Qv, hd, tid);
+    sd.load(Qp, Hp, dsrc, a.lddo, a.Qv, hd, tid);
+    so.load(Qp, Hp, osrc, a.ldo, a.Qv, hd, tid);
+    sk.load(Tc, Hp, ksrc, a.ldk, nk, hd, tid);
+    sv.load(Tc, Hp, vsrc, a.ldv, nk, hd, tid);
+    sq.store(qs, lq, Qp, Hp, tid);
+    sd.store(dos, lq, Qp, Hp, tid);
+    so.store(ps, lq, Qp, Hp, tid);
+    sk.store(ks, lq, Tc, Hp, tid);
+    sv.store(vs, lq, Tc, Hp, tid);
+  } else {
+    stage_scalar(qs, lq, Qp, Hp, qsrc, a.ldq, a.Qv, hd, tid);
+    stage_scalar(dos, lq, Qp, Hp, dsrc, a.lddo, a.Qv, hd, tid);
+    stage_scalar(ps, lq, Qp, Hp, osrc, a.ldo, a.Qv, hd, tid);
+    stage_scalar(ks, lq, Tc, Hp, ksrc, a.ldk, nk, hd, tid);
+    stage_scalar(vs, lq, Tc, Hp, vsrc, a.ldv, nk, hd, tid);
+  }
+  __syncthreads();
+  // D_i = sum_d dO_id o_id
+  if (tid < Qp) {
+    float d = 0.f;
+    for (int j = 0; j < Hp; ++j) d += dos[tid * lq + j] * ps[tid * lq + j];
+    rd[tid] = d;
+  }
+  __syncthreads();
+  const int nrt = Qp / 32, nct = Tc / 32, nht = Hp / 32;
+  // P = exp(scale q K^T - lse) and dS = P (dO V^T - D), tile by tile
+  for (int t = wave; t < nrt * nct; t += 4) {
+    const int rt = t / nct, ct = t - rt * nct;
+    f32x16 s, dp;
+    zero16(s);
+    zero16(dp);
+    mm32v<true>(qs + rt * 32 * lq, lq, ks + ct * 32 * lq, lq, Hp, s, lane);
+    mm32v<true>(dos + rt * 32 * lq, lq, vs + ct * 32 * lq, lq, Hp, dp, lane);
+    const int col = ct * 32 + (lane & 31);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = rt * 32 + acc_row(r, lane);
+      const float p = (col < nk && row < a.Qv) ? __expf(s[r] * a.scale - rl[row]) : 0.f;
+      ps[row * ls + col] = p;
+      ds[row * ls + col] = p * (dp[r] - rd[row]);
+    }
+  }
+  __syncthreads();
+  // dV_c = P^T dO and dK_c = scale dS^T q  (Tc x Hp each), written straight to their rows
+  for (int t = wave; t < 2 * nct * nht; t += 4) {
+    const int which = t / (nct * nht), u = t - which * nct * nht;
+    const int kt = u / nht, ht = u - kt * nht;
+    f32x16 acc;
+    zero16(acc);
+    if (which == 0)
+      mm32<true, false>(ps + kt * 32, ls, dos + ht * 32, lq, Qp, acc, lane);
+    else
+      mm32<true, false>(ds + kt * 32, ls, qs + ht * 32, lq, Qp, acc, lane);
+    const int col = ht * 32 + (lane & 31);
+    float* dst = which == 0 ? a.dv : a.dk;
+    const long long ld = which == 0 ? a.lddv : a.lddk;
+    const float mul = which == 0 ? 1.f : a.scale;
+    if (col < hd) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kt * 32 + acc_row(r, lane);
+        if (key < nk) dst[(krow + key) * ld + h * hd + col] = acc[r] * mul;
+      }
+    }
+  }
+  // dq partial = dS K_c  (Qp x Hp), tiles split along the chunk like the forward's O
+  const int nt = nrt * nht, wpt = 4 / nt;
+  const int tile = wave / wpt, part = wave - tile * wpt;
+  const int dlen = Tc / wpt, d0 = part * dlen;
+  const int rt = tile / nht, ht = tile - rt * nht;
+  f32x16 acc;
+  zero16(acc);
+  mm32v<false>(ds + rt * 32 * ls + d0, ls, ks + d0 * lq + ht * 32, lq, dlen, acc, lane);
+  if (wpt > 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[wave * 1024 + r * 64 + lane] = acc[r];
+    __syncthreads();
+    if (part == 0)
+      for (int q = 1; q < wpt; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] += red[(wave + q) * 1024 + r * 64 + lane];
+  }
+  if (part == 0) {
+    const int col = ht * 32 + (lane & 31);
+    if (a.nsplit == 1) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rt * 32 + acc_row(r, lane);
+        if (row < a.Qv && col < hd) a.out[(qrow + row) * a.ld_out + h * hd + col] = acc[r] * a.scale;
+      }
+    } else {
+      float* po = a.ws + (((long long)vid * a.nh + h) * a.nsplit + c) * Qp * Hp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) po[(rt * 32 + acc_row(r, lane)) * Hp + col] = acc[r];
+    }
+  }
+}
+
+struct TAttnGeom {
+  int Qp, Hp, Tc, nsplit;
+  size_t lds;
+};
+
+// chunk: the largest power of two in [32, 256] whose LDS images fit (Tc * Hp <= NVK float4 per thread),
+// halved while the launch has fewer than ~256 workgroups
+TAttnGeom tattn_geom(int nvid, int Qv, int Tv, int hd, int nh, bool bwd) {
+  TAttnGeom g{};
+  g.Qp = std::max(32, (Qv + 31) / 32 * 32);
+  g.Hp = std::max(32, (hd + 31) / 32 * 32);
+  auto lds_b = [&](int Tc) {
+    const size_t q = bwd ? 2 : 1, p = bwd ? 2 : 1;
+    return sizeof(float) * (q * g.Qp * (g.Hp + 4) + 2 * (size_t)Tc * (g.Hp + 4) + p * g.Qp * (Tc + 4) + 4 * 1024 +
+                            2 * g.Qp + 4);
+  };
+  int Tc = 256;
+  // (forward: at most 8 score tiles, two per wave, in registers)
+  while (Tc > 32 && (lds_b(Tc) > 150 * 1024 || Tc * g.Hp > NVK * 4 * AT || Tc * g.Qp > 8 * 1024)) Tc >>= 1;
+  while (Tc > 32 && (long long)nvid * nh * ((Tv + Tc - 1) / Tc) < 256) Tc >>= 1;
+  g.Tc = Tc;
+  g.nsplit = std::max(1, (Tv + Tc - 1) / Tc);
+  g.lds = lds_b(Tc);
+  return g;
+}
+
+}  // namespace
+
+#ifdef FX_STAMPS
+extern "C" int fx_dbg_tattn_stamps(long long* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_tattn_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -2;
+}
+#endif
+
+long long tattn_ws_floats(int nvid, int Qv, int Tv, int hd, int nh) {
+  long long w = 0;
+  for (int bwd = 0; bwd < 2; ++bwd) {
+    const TAttnGeom g = tattn_geom(nvid, Qv, Tv, hd, nh, bwd);
+    const long long np = (long long)nvid * nh * g.nsplit;
+    w = std::max(w, np * g.Qp * g.Hp + 2 * np * g.Qp);
+  }
+  return w;
+}
+
+static size_t merge_lds(const TAttnGeom& g) { return sizeof(float) * 2 * (size_t)g.nsplit * g.Qp; }
+
+static bool a16(const void* p, long long ld) { return p == nullptr || (((uintptr_t)p & 15) == 0 && (ld & 3) == 0); }
+
+static int tattn_check(int nvid, int Qv, int Tv, int hd, int nh) {
+  static std::once_flag once;
+  std::call_once(once, [] {   // dynamic LDS above the 64 KB default (gfx950: 160 KB per workgroup)
+    (void)hipFuncSetAttribute((const void*)tattn_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)tattn_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)tattn_merge_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  });
+  FX_REQUIRE(nvid >= 1 && Qv >= 1 && Qv <= 64 && hd >= 1 && hd <= 64 && nh >= 1 && Tv >= 1,
+             "attention over T: 1..64 queries and head dim <= 64 per video, T >= 1");
+  FX_REQUIRE((long long)nvid * nh <= kArrivalCounters, "attention over T: too many (video, head) pairs");
+  return FX_OK;
+}
+
+int launch_tattn_fwd(const float* q, long long ldq, const float* k, long long ldk, const float* v, long long ldv,
+                     int nvid, int Qv, int Tv, int hd, int nh, float scale, float* o, long long ldo, float* lse,
+                     float* ws, hipStream_t s) {
+  FX_TRY(tattn_check(nvid, Qv, Tv, hd, nh));
+  const TAttnGeom g = tattn_geom(nvid, Qv, Tv, hd, nh, false);
+  FX_REQUIRE(ws || g.nsplit == 1, "attention over T: workspace required");
+  FX_REQUIRE(g.lds <= 160 * 1024, "attention over T: LDS images too large");
+  FX_REQUIRE(merge_lds(g) <= 160 * 1024, "attention over T: too many frames per video for the in-LDS merge");
+  TAttnArgs a{};
+  a.q = q; a.ldq = ldq; a.k = k; a.ldk = ldk; a.v = v; a.ldv = ldv;
+  a.out = o; a.ld_out = ldo; a.lse = lse; a.ws = ws;
+  a.Qv = Qv; a.Tv = Tv; a.hd = hd; a.nh = nh; a.Qp = g.Qp; a.Hp = g.Hp; a.Tc = g.Tc; a.nsplit = g.nsplit;
+  a.scale = scale;
+  a.vec = (hd % 4 == 0) && a16(q, ldq) && a16(k, ldk) && a16(v, ldv);
+  hipLaunchKernelGGL(tattn_fwd_kernel, dim3(g.nsplit, nh, nvid), dim3(AT), g.lds, s, a);
+  FX_CHECK_HIP(hipGetLastError());
+  if (g.nsplit > 1) {
+    hipLaunchKernelGGL(tattn_merge_kernel, dim3(nh, nvid), dim3(AT), merge_lds(g), s, a, 1, 1.f);
+    FX_CHECK_HIP(hipGetLastError());
+  }
+  return FX_OK;
+}
+
+int launch_tattn_bwd(const float* q, long long ldq, const float* k, long long ldk, const float* v, long long ldv,
+                     const float* o, long long ldo, const float* dout, long long lddo, const float* lse, int nvid,
+                     int Qv, int Tv, int hd, int nh, float scale, float* dq, long long lddq, float* dk, long long lddk,
+                     float* dv, long long lddv, float* ws, hipStream_t s) {
+  FX_TRY(tattn_check(nvid, Qv, Tv, hd, nh));
+  const TAttnGeom g = tattn_geom(nvid, Qv, Tv, hd, nh, true);
+  FX_REQUIRE(ws || g.nsplit == 1, "attention over T: workspace required");
+  FX_REQUIRE(g.lds <= 160 * 1024, "attention over T: LDS images too large");
+  FX_REQUIRE(dq && dk && dv, "attention over T backward: dq, dk, dv required");
+  TAttnArgs a{};
+  a.q = q; a.ldq = ldq; a.k = k; a.ldk = ldk; a.v = v; a.ldv = ldv;
+  a.o = o; a.ldo = ldo; a.dout = dout; a.lddo = lddo;
+  a.out = dq; a.ld_out = lddq; a.dk = dk; a.lddk = lddk; a.dv = dv; a.lddv = lddv;
+  a.lse = const_cast<float*>(lse); a.ws = ws;
+  a.Qv = Qv; a.Tv = Tv; a.hd = hd; a.nh = nh; a.Qp = g.Qp; a.Hp = g.Hp; a.Tc = g.Tc; a.nsplit = g.nsplit;
+  a.scale = scale;
+  a.vec = (hd % 4 == 0) && a16(q, ldq) && a16(k, ldk) && a16(v, ldv) && a16(o, ldo) && a16(dout, lddo);
+  hipLaunchKernelGGL(tattn_bwd_kernel, dim3(g.nsplit, nh, nvid), dim3(AT), g.lds, s, a);
+  FX_CHECK_HIP(hipGetLastError());
+  if (g.nsplit > 1) {
+    hipLaunchKernelGGL(tattn_merge_kernel, dim3(nh, nvid), dim3(AT), 0, s, a, 0, scale);
+    FX_CHECK_HIP(hipGetLastError());
+  }
+  return FX_OK;
+}
+
+}  // namespace fx

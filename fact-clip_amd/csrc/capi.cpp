@@ -588,6 +588,26 @@ int fx_mha_core_bwd(const float* q, long long ldq, const float* k, long long ldk
   return FX_OK;
 }
 
+// ---------------------------------------------------------------- MHA over T (fused)
+long long fx_mha_t_workspace_floats(int nvid, int Lq, int T, int hd, int nhead) {
+  return tattn_ws_floats(nvid, Lq, T, hd, nhead);
+}
+
+int fx_mha_t_fwd(const float* q, long long ldq, const float* k, long long ldk, const float* v, long long ldv, int nvid,
+                 int Lq, int T, int hd, int nhead, float scale, float* o, long long ldo, float* lse, float* workspace,
+                 void* stream) {
+  return launch_tattn_fwd(q, ldq, k, ldk, v, ldv, nvid, Lq, T, hd, nhead, scale, o, ldo, lse, workspace,
+                          (hipStream_t)stream);
+}
+
+int fx_mha_t_bwd(const float* q, long long ldq, const float* k, long long ldk, const float* v, long long ldv,
+                 const float* o, long long ldo, const float* dout, long long lddo, const float* lse, int nvid, int Lq,
+                 int T, int hd, int nhead, float scale, float* dq, long long lddq, float* dk, long long lddk, float* dv,
+                 long long lddv, float* workspace, void* stream) {
+  return launch_tattn_bwd(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, nvid, Lq, T, hd, nhead, scale, dq, lddq, dk,
+                          lddk, dv, lddv, workspace, (hipStream_t)stream);
+}
+
 // ---------------------------------------------------------------- X2Y_map
 // Single-head cross attention of basic.py:349-389 (kq_pos=True), nvid videos stacked by rows:
 // video v owns X rows [x_off[v], x_off[v+1]) and Y rows [y_off[v], y_off[v+1]) (host prefix arrays,

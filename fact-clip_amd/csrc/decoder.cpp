@@ -151,7 +151,7 @@ DecLayout dec_layout(const fx_decoder_params* p, int R, int T, int has_qpos, int
   if (p->cross) {
     L.t1q = o; o += has_qpos ? RA : 0;
     L.qc = o; o += RA;
-    L.pca = o; o += nvid * h * Qv * Tv;
+    L.pca = o; o += nvid * h * Qv;            // cross-attention log-sum-exp per (video, head, token)
     L.oca = o; o += RA;
     L.xh2 = o; o += RA;
     L.rs2 = o; o += R;
@@ -176,7 +176,7 @@ DecLayout dec_layout(const fx_decoder_params* p, int R, int T, int has_qpos, int
   o = 0;
   L.wkv = o; o += p->cross ? AL2 * p->Hm : 0;
   L.bkv = o; o += p->cross ? AL2 : 0;
-  L.wsp = o; o += std::max(sp, p->cross ? fx_mha_core_workspace_floats((int)Qv, (int)Tv, (int)A, (int)h) : 0LL) + RA;
+  L.wsp = o; o += std::max(sp, p->cross ? tattn_ws_floats(nvid, (int)Qv, (int)Tv, (int)(A / h), (int)h) : 0LL) + RA;
   L.total_ws_fwd = o;
   // backward workspace
   o = 0;
@@ -193,7 +193,7 @@ DecLayout dec_layout(const fx_decoder_params* p, int R, int T, int has_qpos, int
   L.G = o; o += RA;
   L.P = o; o += RA;
   L.lnws = o; o += layernorm_bwd_ws_floats(R, (int)A);
-  L.core = o; o += p->cross ? fx_mha_core_workspace_floats((int)Qv, (int)Tv, (int)A, (int)h) : 0;
+  L.core = o; o += p->cross ? tattn_ws_floats(nvid, (int)Qv, (int)Tv, (int)(A / h), (int)h) : 0;
   L.split = o; o += sp;
   L.total_ws_bwd = o;
   (void)FF;
@@ -314,12 +314,9 @@ int fx_decoder_fwd(const fx_decoder_params* p, const float* tgt, long long ldt, 
         tq = b + L.t1q;
       }
       FX_TRY(linear_fwd(tq, A, R, A, p->ca_q_w[l], p->ca_in_b[l], b + L.qc, A, A, 0, s));
-      for (int v = 0; v < nvid; ++v) {   // each video's tokens attend to its own frames
-        const long long kr = (long long)v * Tv * AL2;
-        FX_TRY(fx_mha_core_fwd(b + L.qc + (long long)v * Qv * A, A, kv + kr + (long long)l * A, AL2,
-                               kv + kr + (long long)(NL + l) * A, AL2, Qv, Tv, A, h,
-                               b + L.pca + (long long)v * h * Qv * Tv, b + L.oca + (long long)v * Qv * A, A, spl, s));
-      }
+      // every video's tokens over its own frames, all heads, one fused launch (attn_t.hip)
+      FX_TRY(launch_tattn_fwd(b + L.qc, A, kv + (long long)l * A, AL2, kv + (long long)(NL + l) * A, AL2, nvid, Qv, Tv,
+                              hd, h, scale, b + L.oca, A, b + L.pca, spl, s));
       FX_TRY(linear_fwd_res(b + L.oca, A, R, A, p->ca_out_w[l], A, p->ca_out_b[l], b + L.t1, A, u, A, A, s));
       FX_TRY(launch_layernorm_fwd(u, A, nullptr, 0, p->ln_ca_w[l], p->ln_ca_b[l], eps, R, A, 0, b + L.t2, A,
                                   nullptr, b + L.rs2, b + L.xh2, A, s));
@@ -399,13 +396,9 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
       FX_TRY(linear_dwdb(dU, A, b + L.oca, A, R, A, A, g->ca_out_w[l], g->ca_out_b[l], 1, spl, s));
       FX_TRY(linear_dx(dU, A, p->ca_out_w[l], R, A, A, dO, A, 0, nullptr, 0, spl, s));
       const float* kv = saved + L.kv;
-      for (int v = 0; v < nvid; ++v) {
-        const long long kr = (long long)v * Tv * AL2, qr = (long long)v * Qv * A;
-        FX_TRY(fx_mha_core_bwd(b + L.qc + qr, A, kv + kr + (long long)l * A, AL2, kv + kr + (long long)(NL + l) * A,
-                               AL2, b + L.pca + (long long)v * h * Qv * Tv, dO + qr, A, Qv, Tv, A, h, dq + qr, A,
-                               dkv + kr + (long long)l * A, AL2, dkv + kr + (long long)(NL + l) * A, AL2, ws + L.core,
-                               s));
-      }
+      FX_TRY(launch_tattn_bwd(b + L.qc, A, kv + (long long)l * A, AL2, kv + (long long)(NL + l) * A, AL2, b + L.oca, A,
+                              dO, A, b + L.pca, nvid, Qv, Tv, hd, h, scale, dq, A, dkv + (long long)l * A, AL2,
+                              dkv + (long long)(NL + l) * A, AL2, ws + L.core, s));
       const float* tq = qpos ? b + L.t1q : b + L.t1;
       FX_TRY(linear_dwdb(dq, A, tq, A, R, A, A, g->ca_q_w[l], g->ca_in_b[l], 1, spl, s));
       if (qpos) {

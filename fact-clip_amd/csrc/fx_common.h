@@ -63,6 +63,12 @@ fx_gemm_desc gemm_desc(int M, int N, int K, fx_operand a, fx_operand b, float* c
 int launch_colsum(const float* x, long long ld, int M, int N, float* out, int accumulate,
                   float* ws, hipStream_t s);
 
+// Arrival counters for in-launch "last block merges" reductions (split-K GEMMs, split-T attention):
+// one zeroed pool of kArrivalCounters words per (device, stream); the last arriver of every
+// counter re-arms it to 0, so launches on one stream can reuse the pool.
+constexpr long long kArrivalCounters = 1 << 16;
+unsigned* arrival_counters(hipStream_t s);
+
 // event-based timing hooks around launches of one kernel class (bench roofline)
 void prof_begin(int kind, hipStream_t s);
 void prof_end(int kind, hipStream_t s, double flops, double bytes);

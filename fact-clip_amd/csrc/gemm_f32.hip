@@ -1234,7 +1234,7 @@ bool use_wide(const GemmDev& g, int ak, int bk, int batch) {
 
 // Split-K arrival counters, one pool per (device, stream): zeroed once at allocation and
 // re-armed by the last block of every tile, so launches on one stream reuse them safely.
-constexpr long long kMaxTileCounters = 1 << 16;
+constexpr long long kMaxTileCounters = kArrivalCounters;
 unsigned* tile_counters(hipStream_t s) {
   static std::mutex mu;
   static std::map<std::pair<int, hipStream_t>, unsigned*> pool;
@@ -1255,6 +1255,8 @@ unsigned* tile_counters(hipStream_t s) {
 }
 
 }  // namespace
+
+unsigned* arrival_counters(hipStream_t s) { return tile_counters(s); }
 
 thread_local const float* t_ws_lo = nullptr;
 thread_local const float* t_ws_hi = nullptr;

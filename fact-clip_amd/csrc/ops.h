@@ -77,4 +77,16 @@ int launch_mha_small_bwd(const float* q, long long ldq, const float* k, long lon
                          int nhead, float scale, float* dq, long long lddq, float* dk, long long lddk, float* dv,
                          long long lddv, hipStream_t s, int nvid = 1);
 
+// ---- fused multi-head attention of <= 64 queries over T frames (attn_t.hip) ----------------
+// nvid videos stacked by rows (queries v*Qv.., keys/values v*Tv..); head h = columns [h*hd, h*hd+hd)
+// of q/k/v/o.  fwd writes o and lse (nvid, nhead, Qv); bwd writes dq, dk, dv (dk/dv rows: one per key).
+long long tattn_ws_floats(int nvid, int Qv, int Tv, int hd, int nhead);
+int launch_tattn_fwd(const float* q, long long ldq, const float* k, long long ldk, const float* v, long long ldv,
+                     int nvid, int Qv, int Tv, int hd, int nhead, float scale, float* o, long long ldo, float* lse,
+                     float* ws, hipStream_t s);
+int launch_tattn_bwd(const float* q, long long ldq, const float* k, long long ldk, const float* v, long long ldv,
+                     const float* o, long long ldo, const float* dout, long long lddo, const float* lse, int nvid,
+                     int Qv, int Tv, int hd, int nhead, float scale, float* dq, long long lddq, float* dk,
+                     long long lddk, float* dv, long long lddv, float* ws, hipStream_t s);
+
 }  // namespace fx

@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FACTMX_LIB", os.path.join(_HERE, "_lib", "libfactmx.so"))
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -100,6 +100,9 @@ SIGNATURES = {
     "fx_l2norm_bwd": (I, [P, L, P, P, L, I, I, P, L, P]),
     "fx_relu_bwd": (I, [P, L, P, L, I, I, P, L, P]),
     "fx_add": (I, [P, L, P, L, I, I, P, L, I, P]),
+    "fx_mha_t_workspace_floats": (L, [I, I, I, I, I]),
+    "fx_mha_t_fwd": (I, [P, L, P, L, P, L, I, I, I, I, I, F, P, L, P, P, P]),
+    "fx_mha_t_bwd": (I, [P, L, P, L, P, L, P, L, P, L, P, I, I, I, I, I, F, P, L, P, L, P, L, P, P]),
     "fx_mha_core_workspace_floats": (L, [I, I, I, I]),
     "fx_mha_core_fwd": (I, [P, L, P, L, P, L, I, I, I, I, P, P, L, P, P]),
     "fx_mha_core_bwd": (I, [P, L, P, L, P, L, P, P, L, I, I, I, I, P, L, P, L, P, L, P, P]),

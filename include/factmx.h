@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FX_ABI_VERSION 6
+#define FX_ABI_VERSION 7
 
 enum {
   FX_OK = 0,
@@ -326,6 +326,25 @@ int fx_mha_core_bwd(const float* q, long long ldq, const float* k, long long ldk
                     long long ldv, const float* probs, const float* dout, long long lddo, int Lq,
                     int Lk, int E, int nhead, float* dq, long long lddq, float* dk, long long lddk,
                     float* dv, long long lddv, float* workspace, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Multi-head attention of a few queries over T frames, ONE fused launch for every video and
+ * head (SCALayer cross-attention core, basic.py:508-516; nn.MultiheadAttention math with
+ * Lq <= 64 queries and head dim hd <= 64): split-T partial softmax + P.V per workgroup, ordered
+ * last-arriver merge; only lse is kept for backward (no (h, Lq, T) probabilities).
+ *   nvid videos stacked by rows: queries v*Lq.., keys / values v*T..; head h = columns
+ *   [h*hd, (h+1)*hd) of q, k, v, o.  fwd: o, lse (nvid, nhead, Lq).
+ *   bwd: dq, dk, dv written (dk/dv may alias interleaved column ranges of one buffer).
+ * ---------------------------------------------------------------------- */
+long long fx_mha_t_workspace_floats(int nvid, int Lq, int T, int hd, int nhead);
+int fx_mha_t_fwd(const float* q, long long ldq, const float* k, long long ldk, const float* v,
+                 long long ldv, int nvid, int Lq, int T, int hd, int nhead, float scale, float* o,
+                 long long ldo, float* lse, float* workspace, void* stream);
+int fx_mha_t_bwd(const float* q, long long ldq, const float* k, long long ldk, const float* v,
+                 long long ldv, const float* o, long long ldo, const float* dout, long long lddo,
+                 const float* lse, int nvid, int Lq, int T, int hd, int nhead, float scale, float* dq,
+                 long long lddq, float* dk, long long lddk, float* dv, long long lddv,
+                 float* workspace, void* stream);
 
 /* ------------------------------------------------------------------------
  * Temporal down/up-sampling (UpdateBlockTDU.temporal_downsample,
