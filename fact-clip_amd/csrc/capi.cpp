@@ -264,6 +264,17 @@ extern "C" {
 int fx_version(void) { return FX_ABI_VERSION; }
 const char* fx_last_error(void) { return g_last_error.c_str(); }
 
+long long fx_struct_size(int which) {
+  switch (which) {
+    case 0: return (long long)sizeof(fx_gemm_desc);
+    case 1: return (long long)sizeof(fx_decoder_params);
+    case 2: return (long long)sizeof(fx_mstcn_params);
+    case 3: return (long long)sizeof(fx_loss_term);
+    case 4: return (long long)sizeof(fx_video_attn);
+    default: return -1;
+  }
+}
+
 int fx_gemm(const fx_gemm_desc* desc, void* stream) {
   FX_REQUIRE(desc, "fx_gemm: null descriptor");
   // implicit dilated-conv GEMMs (A = shifted-tap operand: conv forward / conv dX, e.g. MSTCN2) are

@@ -1,0 +1,680 @@
+// The loss phase of FACT / FACT_CLIP for a whole batch of videos in a handful of launches
+// (fact_clip/models/loss.py, blocks.py:677-786 _loss_one_video, blocks.py:788-887 eval_with_clip).
+//
+// The reference builds the loss of every video from ~150 ATen ops (one-hot matrices, index_add
+// "zooms" of them onto the TDU segments, F.cross_entropy, the InfoNCE log-softmaxes, numpy soft-IoU
+// for the matching) with a Python loop around them; round 1 here still had ~300 small launches with
+// host work between them.  Here:
+//   fx_match_cost     one launch: every video's Hungarian cost -pc P[:, transcript] - a2fc softIoU.
+//                     The soft IoU needs no one-hot matrix: ground-truth segments are frame intervals,
+//                     overlap[a,s] = sum of a's attention over segment s and union = len_s + colsum_a -
+//                     overlap[a,s] (attention <= 1, so min(attn + 1, 1) = 1 inside the segment).
+//   fx_loss_terms_fwd every CE / smooth / cross-attention / InfoNCE term of every block of every video
+//                     from ONE device-resident term table: one launch for the class terms, one for the
+//                     attention terms, one per InfoNCE group (+ its similarity GEMM), one fixed-order
+//                     finish and one combine into the batch loss and the per-video values.  Soft targets
+//                     (the TDU "zoom" of the one-hot labels, loss.py:226-231, 266-269) are frame-interval
+//                     overlaps between TDU segments and ground-truth segments, computed in the kernels.
+//   fx_loss_terms_bwd the gradient of every term's logits in the same two launches (+ InfoNCE).
+//   fx_eval_pred      one launch: every video's per-frame prediction (eval_with_clip / Block._eval).
+#include <algorithm>
+#include <cmath>
+
+#include "fx_common.h"
+#include "ops.h"
+
+namespace fx {
+namespace {
+
+constexpr int VT = 256;        // threads per block (4 waves, one row at a time per wave)
+constexpr int VNB = 64;        // row blocks per term
+
+__device__ __forceinline__ float vsum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float vmax(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ float at(const fx_loss_term& t, int r, int c) {
+  return t.x[(long long)r * t.sr + (long long)c * t.sc];
+}
+
+__device__ __forceinline__ float row_lse_t(const fx_loss_term& t, int r, int n, int lane) {
+  float m = -INFINITY;
+  for (int c = lane; c < n; c += 64) m = fmaxf(m, at(t, r, c));
+  m = vmax(m);
+  float s = 0.f;
+  for (int c = lane; c < n; c += 64) s += __expf(at(t, r, c) - m);
+  return m + __logf(vsum(s));
+}
+
+// row r's frame interval
+__device__ __forceinline__ void row_iv(const fx_loss_term& t, int r, int& a, int& b) {
+  if (t.rs) {
+    a = t.rs[r];
+    b = t.re[r];
+  } else {
+    a = b = r;
+  }
+}
+
+__device__ __forceinline__ float overlap(int a0, int a1, int b0, int b1) {
+  const int lo = max(a0, b0), hi = min(a1, b1);
+  return hi >= lo ? (float)(hi - lo + 1) : 0.f;
+}
+
+// first ground-truth segment whose end >= f (segments sorted, contiguous)
+__device__ __forceinline__ int first_gt(const fx_loss_term& t, int f) {
+  int lo = 0, hi = t.G;
+  while (lo < hi) {
+    const int m = (lo + hi) >> 1;
+    if (t.ge[m] < f) lo = m + 1;
+    else hi = m;
+  }
+  return lo;
+}
+
+// gradient of the smooth term w.r.t. log_softmax(x)[r, c] (through the clamp), unscaled
+__device__ __forceinline__ float smooth_g(const fx_loss_term& t, int r, int c, float l0, float lm, float lp1, int R) {
+  float g = 0.f;
+  const float lpc = at(t, r, c) - l0;
+  if (r > 0) {
+    const float d = lpc - (at(t, r - 1, c) - lm);
+    if (d * d <= 16.f) g += 2.f * d;
+  }
+  if (r + 1 < R) {
+    const float d = (at(t, r + 1, c) - lp1) - lpc;
+    if (d * d <= 16.f) g -= 2.f * d;
+  }
+  return g;
+}
+
+// ------------------------------------------------------------------ class terms (frame / seg / token CE + smooth)
+__device__ void class_fwd(const fx_loss_term& t, int lane, int gw, int nw, float& ce, float& sm) {
+  for (int r = gw; r < t.R; r += nw) {
+    const float l0 = row_lse_t(t, r, t.C, lane);
+    if (lane == 0) t.lse[r] = l0;
+    if (t.y) {
+      if (lane == 0) {
+        const int c = t.y[r];
+        if (c >= 0) ce += t.w[c] * (l0 - at(t, r, c));
+      }
+    } else if (t.G > 0) {
+      // soft target: class distribution of the row's frame interval over the ground-truth segments
+      int f0, f1;
+      row_iv(t, r, f0, f1);
+      const float inv = 1.f / (float)(f1 - f0 + 1);
+      float acc = 0.f;
+      for (int j = first_gt(t, f0) + lane; j < t.G && t.gs[j] <= f1; j += 64) {
+        const int c = t.gl[j];
+        acc += overlap(f0, f1, t.gs[j], t.ge[j]) * inv * t.w[c] * (l0 - at(t, r, c));
+      }
+      ce += acc;
+    }
+    if (t.c_sm != 0.f && r + 1 < t.R) {
+      const float l1 = row_lse_t(t, r + 1, t.C, lane);
+      float s = 0.f;
+      for (int c = lane; c < t.C; c += 64) {
+        const float d = (at(t, r + 1, c) - l1) - (at(t, r, c) - l0);
+        s += fminf(d * d, 16.f);
+      }
+      sm += s;
+    }
+  }
+}
+
+__device__ void class_bwd(const fx_loss_term& t, float* tzrow, int lane, int gw, int nw, float gout) {
+  const float g_ce = gout * t.c_ce, g_sm = gout * t.c_sm;
+  const bool smooth = t.c_sm != 0.f;
+  for (int r = gw; r < t.R; r += nw) {
+    const float l0 = t.lse[r];
+    const float lm = (smooth && r > 0) ? t.lse[r - 1] : 0.f;
+    const float lp1 = (smooth && r + 1 < t.R) ? t.lse[r + 1] : 0.f;
+    // target weights of the row: tz[c] (LDS row of this wave) and their sum zw
+    for (int c = lane; c < t.C; c += 64) tzrow[c] = 0.f;
+    float zw = 0.f;
+    if (t.y) {
+      const int yc = t.y[r];
+      if (yc >= 0) {
+        zw = t.w[yc];
+        if (lane == 0) tzrow[yc] = zw;
+      }
+    } else if (t.G > 0) {
+      int f0, f1;
+      row_iv(t, r, f0, f1);
+      const float inv = 1.f / (float)(f1 - f0 + 1);
+      if (lane == 0)   // few segments per row: one lane, fixed order
+        for (int j = first_gt(t, f0); j < t.G && t.gs[j] <= f1; ++j) {
+          const int c = t.gl[j];
+          const float v = overlap(f0, f1, t.gs[j], t.ge[j]) * inv * t.w[c];
+          tzrow[c] += v;
+          zw += v;
+        }
+      zw = __shfl(zw, 0, 64);
+    }
+    __builtin_amdgcn_wave_barrier();
+    float gsum = 0.f;
+    if (smooth)
+      for (int c = lane; c < t.C; c += 64) gsum += smooth_g(t, r, c, l0, lm, lp1, t.R) * g_sm;
+    gsum = vsum(gsum);
+    for (int c = lane; c < t.C; c += 64) {
+      const float p = __expf(at(t, r, c) - l0);
+      const float g = smooth ? smooth_g(t, r, c, l0, lm, lp1, t.R) * g_sm : 0.f;
+      t.dx[(long long)r * t.dsr + (long long)c * t.dsc] = (g - p * gsum) + g_ce * (zw * p - tzrow[c]);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// ------------------------------------------------------------------ attention terms (cross_attn_loss(_tdu) + smooth)
+__device__ __forceinline__ float attn_target(const fx_loss_term& t, int r, int i) {
+  int f0, f1;
+  row_iv(t, r, f0, f1);
+  return overlap(f0, f1, t.kgs[i], t.kge[i]) / (float)(f1 - f0 + 1);
+}
+
+__device__ void attn_fwd(const fx_loss_term& t, int lane, int gw, int nw, float& xe, float& sm) {
+  if (t.axis == 1) {
+    for (int r = gw; r < t.R; r += nw) {
+      const float v = lane < t.K ? at(t, r, t.ka[lane]) : -INFINITY;
+      const float m = vmax(v);
+      const float l = m + __logf(vsum(lane < t.K ? __expf(v - m) : 0.f));
+      if (lane == 0) t.lse[r] = l;
+      xe += lane < t.K ? -(v - l) * attn_target(t, r, lane) * t.ksw[lane] : 0.f;
+    }
+  } else {
+    for (int i = gw; i < t.K; i += nw) {
+      const int q = t.ka[i];
+      float m = -INFINITY;
+      for (int r = lane; r < t.R; r += 64) m = fmaxf(m, at(t, r, q));
+      m = vmax(m);
+      float s = 0.f, zs = 0.f, zl = 0.f;
+      for (int r = lane; r < t.R; r += 64) {
+        const float x = at(t, r, q);
+        const float zz = attn_target(t, r, i);
+        s += __expf(x - m);
+        zs += zz;
+        zl += zz * x;
+      }
+      const float l = m + __logf(vsum(s));
+      zs = vsum(zs);
+      zl = vsum(zl);
+      if (lane == 0) {
+        t.lse2[t.R + i] = l;              // per-column lse after the R row slots
+        t.colz[i] = zs * t.ksw[i];
+        xe += -(zl - zs * l) * t.ksw[i];
+      }
+    }
+  }
+  if (t.c_sm != 0.f) {
+    for (int r = gw; r < t.R; r += nw) {
+      const float l0 = row_lse_t(t, r, t.C, lane);
+      if (lane == 0) t.lse2[r] = l0;
+      if (r + 1 < t.R) {
+        const float l1 = row_lse_t(t, r + 1, t.C, lane);
+        float s = 0.f;
+        for (int c = lane; c < t.C; c += 64) {
+          const float d = (at(t, r + 1, c) - l1) - (at(t, r, c) - l0);
+          s += fminf(d * d, 16.f);
+        }
+        sm += s;
+      }
+    }
+  }
+}
+
+__device__ void attn_bwd(const fx_loss_term& t, int lane, int gw, int nw, float gout) {
+  const float g_xe = gout * t.c_ce, g_sm = gout * t.c_sm;
+  const bool smooth = t.c_sm != 0.f;
+  for (int r = gw; r < t.R; r += nw) {
+    const float l0 = smooth ? t.lse2[r] : 0.f;
+    const float lm = (smooth && r > 0) ? t.lse2[r - 1] : 0.f;
+    const float lp1 = (smooth && r + 1 < t.R) ? t.lse2[r + 1] : 0.f;
+    float gsum = 0.f;
+    if (smooth)
+      for (int c = lane; c < t.C; c += 64) gsum += smooth_g(t, r, c, l0, lm, lp1, t.R) * g_sm;
+    gsum = vsum(gsum);
+    float zrow = 0.f;
+    if (t.axis == 1) zrow = vsum(lane < t.K ? attn_target(t, r, lane) * t.ksw[lane] : 0.f);
+    for (int c = lane; c < t.C; c += 64) {
+      float g = 0.f;
+      if (smooth) g = smooth_g(t, r, c, l0, lm, lp1, t.R) * g_sm - __expf(at(t, r, c) - l0) * gsum;
+      for (int i = 0; i < t.K; ++i) {
+        if (t.ka[i] != c) continue;
+        const float x = at(t, r, c);
+        const float zz = attn_target(t, r, i) * t.ksw[i];
+        if (t.axis == 1) g += g_xe * (__expf(x - t.lse[r]) * zrow - zz);
+        else g += g_xe * (__expf(x - t.lse2[t.R + i]) * t.colz[i] - zz);
+      }
+      t.dx[(long long)r * t.dsr + (long long)c * t.dsc] = g;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ term kernels (grid: row blocks x terms)
+__global__ __launch_bounds__(VT) void terms_fwd_kernel(const fx_loss_term* terms, float* part, int kind) {
+  __shared__ float red[2][VT / 64];
+  const fx_loss_term& t = terms[blockIdx.y];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int gw = blockIdx.x * (VT / 64) + wv, nw = gridDim.x * (VT / 64);
+  float a = 0.f, b = 0.f;
+  if (t.kind == kind) {
+    if (kind == FX_TERM_CLASS) class_fwd(t, lane, gw, nw, a, b);
+    else attn_fwd(t, lane, gw, nw, a, b);
+  }
+  a = vsum(a);
+  b = vsum(b);
+  if (lane == 0) {
+    red[0][wv] = a;
+    red[1][wv] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && t.kind == kind) {
+    float s0 = 0.f, s1 = 0.f;
+    for (int i = 0; i < VT / 64; ++i) {
+      s0 += red[0][i];
+      s1 += red[1][i];
+    }
+    part[(t.slot * (long long)gridDim.x + blockIdx.x) * 2] = s0;
+    part[(t.slot * (long long)gridDim.x + blockIdx.x) * 2 + 1] = s1;
+  }
+}
+
+__global__ __launch_bounds__(VT) void terms_bwd_kernel(const fx_loss_term* terms, const float* gterm, int kind) {
+  extern __shared__ float tz[];   // [4 waves][maxC] target rows of the class terms
+  const fx_loss_term& t = terms[blockIdx.y];
+  if (t.kind != kind) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int gw = blockIdx.x * (VT / 64) + wv, nw = gridDim.x * (VT / 64);
+  if (kind == FX_TERM_CLASS) class_bwd(t, tz + wv * t.C, lane, gw, nw, gterm[blockIdx.y]);
+  else attn_bwd(t, lane, gw, nw, gterm[blockIdx.y]);
+}
+
+// gterm[i] = sum_o gout[o] coef[o, i]   (upstream gradient of each term)
+__global__ __launch_bounds__(64) void combine_bwd_kernel(const float* gout, const float* coef, int nterms, int nout,
+                                                         float* gterm) {
+  for (int i = blockIdx.x * 64 + threadIdx.x; i < nterms; i += gridDim.x * 64) {
+    float s = 0.f;
+    for (int o = 0; o < nout; ++o) s += gout[o] * coef[(long long)o * nterms + i];
+    gterm[i] = s;
+  }
+}
+
+// term value = c_ce * sum(part0) + c_sm * sum(part1), blocks in fixed order (one wave per term)
+__global__ __launch_bounds__(64) void terms_finish_kernel(const fx_loss_term* terms, int nterms, const float* part,
+                                                          int nb, float* vals) {
+  const int i = blockIdx.x;
+  const fx_loss_term& t = terms[i];
+  if (t.kind == FX_TERM_INFONCE) return;
+  const int lane = threadIdx.x;
+  float a = 0.f, b = 0.f;
+  for (int k = lane; k < nb; k += 64) {
+    a += part[((long long)t.slot * nb + k) * 2];
+    b += part[((long long)t.slot * nb + k) * 2 + 1];
+  }
+  a = vsum(a);
+  b = vsum(b);
+  if (lane == 0) vals[i] = t.c_sm != 0.f ? t.c_ce * a + t.c_sm * b : t.c_ce * a;
+}
+
+// ------------------------------------------------------------------ InfoNCE (loss.py:280-341)
+// x = sim (R frames x C classes, = emb . text^T / temp), y = class per frame (-1: masked frame).
+// value = c_ce * ( mean over valid frames of CE(sim_t, y_t)  +  mean over C classes of
+//          -sum_{t: y_t = c} log_softmax_over_t(sim[:, c])[t] / max(count_c, 1) ),   c_ce = 1/2
+// scratch: lse (R) row lse, lse2 (C) column lse, colz (C) counts; kval[0] = number of valid frames
+constexpr int IT = 1024;
+__global__ __launch_bounds__(IT) void infonce_fwd_kernel(const fx_loss_term* terms, float* vals) {
+  __shared__ float red[IT / 64][3];
+  const fx_loss_term& t = terms[blockIdx.x];
+  if (t.kind != FX_TERM_INFONCE) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = IT / 64;
+  float v2t = 0.f, nval = 0.f, t2v = 0.f;
+  for (int r = wv; r < t.R; r += nwv) {
+    const int y = t.y[r];
+    const float l = row_lse_t(t, r, t.C, lane);
+    if (lane == 0) {
+      t.lse[r] = l;
+      if (y >= 0) {
+        v2t += l - at(t, r, y);
+        nval += 1.f;
+      }
+    }
+  }
+  for (int c = wv; c < t.C; c += nwv) {
+    float m = -INFINITY;
+    for (int r = lane; r < t.R; r += 64)
+      if (t.y[r] >= 0) m = fmaxf(m, at(t, r, c));
+    m = vmax(m);
+    float s = 0.f, cnt = 0.f, sx = 0.f;
+    for (int r = lane; r < t.R; r += 64) {
+      const int y = t.y[r];
+      if (y < 0) continue;
+      const float x = at(t, r, c);
+      s += __expf(x - m);
+      if (y == c) {
+        cnt += 1.f;
+        sx += x;
+      }
+    }
+    s = vsum(s);
+    cnt = vsum(cnt);
+    sx = vsum(sx);
+    const float l = m + __logf(s);
+    if (lane == 0) {
+      t.lse2[c] = l;
+      t.colz[c] = cnt;
+      t2v += -(sx - cnt * l) / fmaxf(cnt, 1.f);
+    }
+  }
+  if (lane == 0) {
+    red[wv][0] = v2t;
+    red[wv][1] = nval;
+    red[wv][2] = t2v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0.f, n = 0.f, b = 0.f;
+    for (int i = 0; i < nwv; ++i) {
+      a += red[i][0];
+      n += red[i][1];
+      b += red[i][2];
+    }
+    t.colz[t.C] = n;
+    vals[blockIdx.x] = n > 0.f ? t.c_ce * (a / n + b / (float)t.C) : 0.f;
+  }
+}
+
+// dsim[t, c] = g c_ce ( (p_row - [c == y_t]) / n_valid + (has_c p_col[t, c] - [c == y_t] / count_c) / C ) for
+// valid frames, 0 for masked ones; written into dx (R x C), then the caller's GEMM takes it to demb
+__global__ __launch_bounds__(VT) void infonce_bwd_kernel(const fx_loss_term* terms, const float* gterm) {
+  const fx_loss_term& t = terms[blockIdx.y];
+  if (t.kind != FX_TERM_INFONCE) return;
+  const float n = t.colz[t.C];
+  const float g = gterm[blockIdx.y] * t.c_ce;
+  const float inv_n = n > 0.f ? 1.f / n : 0.f, inv_c = 1.f / (float)t.C;
+  const long long total = (long long)t.R * t.C;
+  for (long long e = (long long)blockIdx.x * VT + threadIdx.x; e < total; e += (long long)gridDim.x * VT) {
+    const int r = (int)(e / t.C), c = (int)(e - (long long)r * t.C);
+    const int y = t.y[r];
+    float v = 0.f;
+    if (y >= 0 && n > 0.f) {
+      const float x = at(t, r, c);
+      const float cnt = t.colz[c];
+      const float pr = __expf(x - t.lse[r]);
+      const float pc = cnt > 0.f ? __expf(x - t.lse2[c]) : 0.f;
+      const float d = c == y ? 1.f : 0.f;
+      v = g * ((pr - d) * inv_n + (pc - (cnt > 0.f ? d / cnt : 0.f)) * inv_c);
+    }
+    t.dx[(long long)r * t.dsr + (long long)c * t.dsc] = v;
+  }
+}
+
+// out[o] = sum_i coef[o * nterms + i] vals[i]   (fixed order)
+__global__ __launch_bounds__(64) void combine_kernel(const float* vals, const float* coef, int nterms, int nout,
+                                                     float* out) {
+  const int o = blockIdx.x, lane = threadIdx.x;
+  float s = 0.f;
+  for (int i = lane; i < nterms; i += 64) s += coef[(long long)o * nterms + i] * vals[i];
+  s = vsum(s);
+  if (lane == 0 && o < nout) out[o] = s;
+}
+
+// ------------------------------------------------------------------ matching cost (loss.py:108-153, 91-106)
+// frame t's attention to token a: frame-level att[t*lda + a] or segment-level att[seg_id[t]*lda + a]
+__device__ __forceinline__ float frame_attn(const fx_video_attn& v, int t, int a) {
+  const int row = v.seg_id ? v.seg_id[t] : t;
+  return v.attn[(long long)row * v.lda + a];
+}
+
+__global__ __launch_bounds__(VT) void match_cost_kernel(const fx_video_attn* vids, float pc, float a2fc, int Gmax,
+                                                        float* cost) {
+  extern __shared__ float sm[];   // [C1] prob row, then [Gmax] overlaps
+  const int a = blockIdx.x, vi = blockIdx.y;
+  const fx_video_attn& v = vids[vi];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float* prob = sm;
+  float* ov = sm + v.C1;
+  if (a >= v.Q) return;
+  if (wv == 0) {
+    const float* row = v.clogit + (long long)a * v.ldc;
+    float m = -INFINITY;
+    for (int c = lane; c < v.C1; c += 64) m = fmaxf(m, row[c]);
+    m = vmax(m);
+    float s = 0.f;
+    for (int c = lane; c < v.C1; c += 64) s += __expf(row[c] - m);
+    s = vsum(s);
+    for (int c = lane; c < v.C1; c += 64) prob[c] = __expf(row[c] - m) / s;
+  }
+  for (int sg = wv; sg < v.G; sg += VT / 64) {
+    float acc = 0.f;
+    for (int t = v.gs[sg] + lane; t <= v.ge[sg]; t += 64) acc += frame_attn(v, t, a);
+    acc = vsum(acc);
+    if (lane == 0) ov[sg] = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float col = 0.f;
+    for (int sg = 0; sg < v.G; ++sg) col += ov[sg];
+    ov[v.G] = col;
+  }
+  __syncthreads();
+  const float col = ov[v.G];
+  for (int sg = threadIdx.x; sg < Gmax; sg += VT) {
+    float c = 0.f;
+    if (sg < v.G) {
+      const float len = (float)(v.ge[sg] - v.gs[sg] + 1);
+      const float den = col - ov[sg] + len;
+      const float iou = den != 0.f ? ov[sg] / den : 0.f;
+      c = -pc * prob[v.gl[sg]] - a2fc * iou;
+    }
+    cost[((long long)vi * v.Q + a) * Gmax + sg] = c;
+  }
+}
+
+// ------------------------------------------------------------------ per-frame prediction (blocks.py:243-261, 854-887)
+// fprob = softmax(flogit[t]) (frame classifier or CLIP similarity); if any token predicts a non-null
+// class: pred = argmax((1 - w) qtk_prob[best token of t] + w fprob), best token = first argmax of t's
+// attention over the non-null tokens; else pred = argmax(fprob).  (first maximum everywhere, as torch)
+__global__ __launch_bounds__(VT) void eval_pred_kernel(const fx_video_attn* vids, float w, int32_t* pred) {
+  extern __shared__ float sm[];   // [Q][C] token class probs, [Q] is_token flags
+  const fx_video_attn& v = vids[blockIdx.y];
+  const int C = v.C1 - 1, Q = v.Q;
+  float* qp = sm;
+  float* ist = sm + Q * C;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int a = wv; a < Q; a += VT / 64) {
+    const float* row = v.clogit + (long long)a * v.ldc;
+    // argmax over all C1 logits (first max) and softmax over the first C
+    float bm = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int c = lane; c < v.C1; c += 64) {
+      const float x = row[c];
+      if (x > bm) {
+        bm = x;
+        bi = c;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float om = __shfl_xor(bm, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (om > bm || (om == bm && oi < bi)) {
+        bm = om;
+        bi = oi;
+      }
+    }
+    float m = -INFINITY;
+    for (int c = lane; c < C; c += 64) m = fmaxf(m, row[c]);
+    m = vmax(m);
+    float s = 0.f;
+    for (int c = lane; c < C; c += 64) s += __expf(row[c] - m);
+    s = vsum(s);
+    for (int c = lane; c < C; c += 64) qp[a * C + c] = __expf(row[c] - m) / s;
+    if (lane == 0) ist[a] = bi != C ? 1.f : 0.f;
+  }
+  __syncthreads();
+  const int t = blockIdx.x * VT + threadIdx.x;
+  if (t >= v.T) return;
+  bool any = false;
+  int best = -1;
+  float ba = -INFINITY;
+  for (int a = 0; a < Q; ++a) {
+    if (ist[a] == 0.f) continue;
+    any = true;
+    const float x = frame_attn(v, t, a);
+    if (best < 0 || x > ba) {
+      ba = x;
+      best = a;
+    }
+  }
+  const float* fl = v.flogit + (long long)t * v.ldf;
+  float m = -INFINITY;
+  for (int c = 0; c < C; ++c) m = fmaxf(m, fl[c]);
+  float s = 0.f;
+  for (int c = 0; c < C; ++c) s += __expf(fl[c] - m);
+  const float inv = 1.f / s;
+  float bv = -INFINITY;
+  int bc = 0;
+  for (int c = 0; c < C; ++c) {
+    const float fp = __expf(fl[c] - m) * inv;
+    const float p = any ? (1.f - w) * qp[best * C + c] + w * fp : fp;
+    if (p > bv) {
+      bv = p;
+      bc = c;
+    }
+  }
+  pred[v.pred_off + t] = bc;
+}
+
+}  // namespace
+}  // namespace fx
+
+using namespace fx;
+
+extern "C" {
+
+long long fx_loss_terms_workspace_floats(int nterms) { return 2LL * VNB * std::max(nterms, 1) + std::max(nterms, 1); }
+
+int fx_loss_terms_fwd(const fx_loss_term* terms_host, const fx_loss_term* terms_dev, int nterms, const float* coef_dev,
+                      int nout, float* out, float* workspace, void* stream) {
+  FX_REQUIRE(terms_host && terms_dev && nterms > 0 && coef_dev && out && workspace, "loss_terms: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  float* part = workspace;
+  float* vals = workspace + 2LL * VNB * nterms;
+  int max_rows[3] = {0, 0, 0};
+  for (int i = 0; i < nterms; ++i) {
+    const fx_loss_term& t = terms_host[i];
+    FX_REQUIRE(t.kind >= 0 && t.kind <= 2, "loss_terms: unknown term kind");
+    FX_REQUIRE(t.R > 0 && t.C > 0 && t.x && t.lse, "loss_terms: empty term");
+    FX_REQUIRE(t.kind != FX_TERM_ATTN || (t.K >= 0 && t.K <= FX_LOSS_MAXK && t.lse2 && t.colz && t.C <= 4096),
+               "loss_terms: attention term needs K <= 64 matched columns and scratch");
+    FX_REQUIRE(t.kind != FX_TERM_CLASS || t.w, "loss_terms: class term needs weights");
+    FX_REQUIRE(t.kind != FX_TERM_INFONCE || (t.y && t.lse2 && t.colz && t.emb && t.text && t.dx && t.sc == 1 &&
+                                             t.dsc == 1 && t.D > 0),
+               "loss_terms: InfoNCE term needs labels, embeddings, text and scratch");
+    FX_REQUIRE(t.slot == i, "loss_terms: term slot must equal its index");
+    max_rows[t.kind] = std::max(max_rows[t.kind], t.kind == FX_TERM_ATTN ? std::max(t.R, t.K) : t.R);
+  }
+  const int nb = VNB;
+  FX_CHECK_HIP(hipMemsetAsync(part, 0, sizeof(float) * 2LL * nb * nterms, s));
+  for (int k = 0; k < 2; ++k) {
+    if (!max_rows[k]) continue;
+    hipLaunchKernelGGL(terms_fwd_kernel, dim3(nb, nterms), dim3(VT), 0, s, terms_dev, part, k);
+    FX_CHECK_HIP(hipGetLastError());
+  }
+  hipLaunchKernelGGL(terms_finish_kernel, dim3(nterms), dim3(64), 0, s, terms_dev, nterms, part, nb, vals);
+  FX_CHECK_HIP(hipGetLastError());
+  if (max_rows[FX_TERM_INFONCE]) {
+    for (int i = 0; i < nterms; ++i) {   // similarity GEMMs: sim = emb . text^T / temp
+      const fx_loss_term& t = terms_host[i];
+      if (t.kind != FX_TERM_INFONCE) continue;
+      fx_gemm_desc d = gemm_desc(t.R, t.C, t.D, op_rows(t.emb, t.ld_emb), op_rows(t.text, t.D),
+                                 const_cast<float*>(t.x), t.sr);
+      d.alpha = t.inv_temp;
+      FX_TRY(launch_gemm(d, s));
+    }
+    hipLaunchKernelGGL(infonce_fwd_kernel, dim3(nterms), dim3(IT), 0, s, terms_dev, vals);
+    FX_CHECK_HIP(hipGetLastError());
+  }
+  hipLaunchKernelGGL(combine_kernel, dim3(nout), dim3(64), 0, s, vals, coef_dev, nterms, nout, out);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+int fx_loss_terms_bwd(const fx_loss_term* terms_host, const fx_loss_term* terms_dev, int nterms, const float* coef,
+                      int nout, const float* gout, float* workspace, void* stream) {
+  FX_REQUIRE(terms_host && terms_dev && nterms > 0 && coef && gout && workspace, "loss_terms_bwd: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  float* gterm = workspace;
+  hipLaunchKernelGGL(combine_bwd_kernel, dim3(cdiv(nterms, 64)), dim3(64), 0, s, gout, coef, nterms, nout, gterm);
+  FX_CHECK_HIP(hipGetLastError());
+  int maxC = 1;
+  bool has[3] = {false, false, false};
+  for (int i = 0; i < nterms; ++i) {
+    const fx_loss_term& t = terms_host[i];
+    FX_REQUIRE(t.dx, "loss_terms_bwd: term without a gradient buffer");
+    has[t.kind] = true;
+    if (t.kind == FX_TERM_CLASS) maxC = std::max(maxC, t.C);
+  }
+  if (has[FX_TERM_CLASS]) {
+    hipLaunchKernelGGL(terms_bwd_kernel, dim3(VNB, nterms), dim3(VT), sizeof(float) * 4 * maxC, s, terms_dev, gterm,
+                       (int)FX_TERM_CLASS);
+    FX_CHECK_HIP(hipGetLastError());
+  }
+  if (has[FX_TERM_ATTN]) {
+    hipLaunchKernelGGL(terms_bwd_kernel, dim3(VNB, nterms), dim3(VT), 0, s, terms_dev, gterm, (int)FX_TERM_ATTN);
+    FX_CHECK_HIP(hipGetLastError());
+  }
+  if (has[FX_TERM_INFONCE]) {
+    hipLaunchKernelGGL(infonce_bwd_kernel, dim3(256, nterms), dim3(VT), 0, s, terms_dev, gterm);
+    FX_CHECK_HIP(hipGetLastError());
+    for (int i = 0; i < nterms; ++i) {   // demb = dsim . text / temp
+      const fx_loss_term& t = terms_host[i];
+      if (t.kind != FX_TERM_INFONCE) continue;
+      FX_REQUIRE(t.demb, "loss_terms_bwd: InfoNCE term without an embedding gradient buffer");
+      fx_gemm_desc d = gemm_desc(t.R, t.D, t.C, op_rows(t.dx, t.dsr), op_cols(t.text, t.D), t.demb, t.ld_demb);
+      d.alpha = t.inv_temp;
+      FX_TRY(launch_gemm(d, s));
+    }
+  }
+  return FX_OK;
+}
+
+int fx_match_cost(const fx_video_attn* vids_host, const fx_video_attn* vids_dev, int nvid, float pc, float a2fc,
+                  int Gmax, float* cost, void* stream) {
+  FX_REQUIRE(vids_host && vids_dev && nvid > 0 && Gmax > 0 && cost, "match_cost: bad arguments");
+  int Q = 0, C1 = 0;
+  for (int i = 0; i < nvid; ++i) {
+    FX_REQUIRE(vids_host[i].G <= Gmax && vids_host[i].G >= 1, "match_cost: segment count");
+    Q = std::max(Q, vids_host[i].Q);
+    C1 = std::max(C1, vids_host[i].C1);
+  }
+  hipLaunchKernelGGL(match_cost_kernel, dim3(Q, nvid), dim3(VT), sizeof(float) * (C1 + Gmax + 1), (hipStream_t)stream,
+                     vids_dev, pc, a2fc, Gmax, cost);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+int fx_eval_pred(const fx_video_attn* vids_host, const fx_video_attn* vids_dev, int nvid, float mwt, int32_t* pred,
+                 void* stream) {
+  FX_REQUIRE(vids_host && vids_dev && nvid > 0 && pred, "eval_pred: bad arguments");
+  int T = 0, QC = 0;
+  for (int i = 0; i < nvid; ++i) {
+    const fx_video_attn& v = vids_host[i];
+    FX_REQUIRE(v.flogit && v.C1 >= 2 && v.Q >= 1, "eval_pred: video without logits");
+    T = std::max(T, v.T);
+    QC = std::max(QC, v.Q * v.C1);
+  }
+  FX_REQUIRE((size_t)QC * sizeof(float) <= 60 * 1024, "eval_pred: too many token x class probabilities");
+  hipLaunchKernelGGL(eval_pred_kernel, dim3(cdiv(T, VT), nvid), dim3(VT), sizeof(float) * QC, (hipStream_t)stream,
+                     vids_dev, mwt, pred);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+}  // extern "C"

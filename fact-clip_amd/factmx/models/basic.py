@@ -460,10 +460,22 @@ class TemporalDownsampleUpsample:
         self.seg_id32 = seg_id
         self.start32, self.end32 = starts, ends
         self.num_seg = int(starts.shape[0])
-        self.seg_label = seg_id.to(torch.int64)
-        self.seg_lens = (ends - starts + 1).to(torch.int64)
+        self._seg_label = self._seg_lens = None
         self._pred = pred
         self._segs = None
+
+    @property
+    def seg_label(self):
+        """int64 frame -> segment id (made on first use: the fused loss path never needs it)."""
+        if self._seg_label is None:
+            self._seg_label = self.seg_id32.to(torch.int64)
+        return self._seg_label
+
+    @property
+    def seg_lens(self):
+        if self._seg_lens is None:
+            self._seg_lens = (self.end32 - self.start32 + 1).to(torch.int64)
+        return self._seg_lens
 
     @classmethod
     def from_probs(cls, frame2d, col0, ncls):

@@ -16,6 +16,7 @@ from ..dp import mark_block_input
 from ..utils import utils
 from . import basic
 from . import loss as loss_mod
+from . import vloss
 from .basic import time_mask, torch_class_label_to_segment_label
 from .loss import MatchCriterion
 
@@ -47,8 +48,37 @@ class FeatureProjection(nn.Module):
         return y.reshape(*shp[:-1], self.clip_dim)
 
 
+class _Lazy:
+    """A side-channel value computed on first read (frame-level gathers of segment attention that
+    only evaluation code reads)."""
+    __slots__ = ("fn",)
+
+    def __init__(self, fn):
+        self.fn = fn
+
+
+def _lazy_attr(name):
+    key = "_lz_" + name
+
+    def get(self):
+        d = self.__dict__
+        if key not in d:
+            raise AttributeError(name)
+        v = d[key]
+        if isinstance(v, _Lazy):
+            v = d[key] = v.fn()
+        return v
+
+    def put(self, v):
+        self.__dict__[key] = v
+    return property(get, put)
+
+
 class Block(nn.Module):
     """blocks.py:180-281."""
+
+    f2a_attn = _lazy_attr("f2a_attn")
+    a2f_attn = _lazy_attr("a2f_attn")
 
     def __repr__(self):
         return (f"{type(self).__name__}(\n  f:{self.frame_branch},\n  a:{self.action_branch},\n"
@@ -155,6 +185,7 @@ class InputBlock(Block):
         fc, ac, ao = vb.frames(f_cl), vb.tokens(a_cl), vb.tokens(a_out)
         self._vrec = [dict(frame_clogit=fc[v].unsqueeze(1), action_clogit=ac[v].unsqueeze(1),
                            action_feature=ao[v][:, :-n].unsqueeze(1)) for v in range(vb.nvid)]
+        self._bt = dict(f_cl=f_cl, a_cl=a_cl)
         return f_out, a_out
 
     def compute_loss(self, criterion, match=None):
@@ -213,6 +244,7 @@ class UpdateBlock(Block):
                              f2a_attn=fat[v].view(1, Q, T), a2f_attn=aat[v].view(1, T, Q),
                              f2a_attn_logit=flg[v].view(1, Q, T), a2f_attn_logit=alg[v].view(1, T, Q)))
         self._vrec = recs
+        self._bt = dict(f_cl=f_cl, a_cl=a_cl, f2a_lg=f2a_lg, a2f_lg=a2f_lg, a2f_at=a2f_at)
         return f_out, a_out
 
     def compute_loss(self, criterion, match=None):
@@ -319,10 +351,13 @@ class UpdateBlockTDU(Block):
                              action_clogit=ac[v].unsqueeze(1),
                              action_feature=ao[v][:, :-n].unsqueeze(1),
                              f2a_attn_logit=flg[v].view(1, Q, Sv),
-                             f2a_attn=tdu.attn_seg2frame(f2a_at_v[0].transpose(2, 1)).transpose(2, 1),
+                             f2a_attn=_Lazy(lambda t=tdu, a=f2a_at_v: t.attn_seg2frame(a[0].transpose(2, 1))
+                                            .transpose(2, 1)),
                              a2f_attn_logit=alg[v].view(1, Sv, Q),
-                             a2f_attn=tdu.attn_seg2frame(a2f_at_v[0])))
+                             a2f_attn=_Lazy(lambda t=tdu, a=a2f_at_v: t.attn_seg2frame(a[0]))))
         self._vrec = recs
+        self._bt = dict(f_cl=f_cl, a_cl=a_cl, f2a_lg=f2a_lg, a2f_lg=a2f_lg, a2f_at=a2f_at, seg_cl=seg_cl, S=S,
+                        s_off=s_off, local=local)
         return f_out, a_out
 
     def compute_loss(self, criterion, match=None):
@@ -416,6 +451,8 @@ class _FACTBase(nn.Module):
             feat_dim = f2.shape[-1] - self.num_classes
             proj = self.frame_projection(f2[:, :feat_dim])
 
+        self._proj = proj
+        self._vb = vb
         proj_v = None if proj is None else vb.frames(proj)
 
         def restore(v):
@@ -579,6 +616,10 @@ class _VideoBatch:
         return torch.split(t, self.Q, dim=0)
 
 
+# lockstep batches take the loss phase through models/vloss.py (False: per-video MatchCriterion ops)
+FUSED_LOSS = True
+
+
 def _batchable(net, seq_list):
     """The lockstep path needs equal-length videos, the fused decoders and no transcript input."""
     if len(seq_list) < 2 or net.cfg.FACT.trans:
@@ -637,6 +678,12 @@ def _forward_videos(net, seq_list, label_list, compute_loss):
     net.video_segments = []     # per video: the TDU segment count of every U block (host ints, no sync)
     if _batchable(net, seq_list):
         restore = net._forward_batch(seq_list)
+        if FUSED_LOSS and vloss.supported(net):
+            nvid = len(seq_list)
+            restore(nvid - 1)       # side-channel attributes: the last video's views, as in the reference
+            net.video_segments = [[blk._bt["S"][v] for blk in net.block_list if "S" in blk._bt]
+                                  for v in range(nvid)]
+            return vloss.run(net, net._vb, label_list, hosts, compute_loss)
         for v in range(len(seq_list)):
             restore(v)
             net.video_segments.append([blk.tdu.num_seg for blk in net.block_list if hasattr(blk, "tdu")])

@@ -3,8 +3,10 @@
 Label bookkeeping is vectorised on the label's device (the reference loops over
 frames in Python).  The Hungarian assignment stays on the host (scipy, as in
 the reference); its cost matrix (tokens x GT segments) is built on the device
-and copied once.  Loss arithmetic runs as device tensor ops; fusing it into
-HIP kernels is the next step on the roadmap.
+and copied once.  The per-term losses run as fused HIP kernel pairs
+(functional.ClassLossFn / AttnLossFn); a lockstep batch of videos takes the
+whole loss phase through models/vloss.py instead (a handful of launches for
+every term of every video).
 """
 import numpy as np
 import torch
@@ -157,22 +159,7 @@ class MatchCriterion:
     def _one_to_many_match(self, cost):
         """loss.py:155-193."""
         tr = self._transcript_np if getattr(self, "_transcript_np", None) is not None else self.transcript.cpu().numpy()
-        actions = np.unique(tr)
-        per_action = np.stack([cost[:, tr == a].sum(1) for a in actions], axis=1)
-        aid, cid = linear_sum_assignment(per_action)
-        rest = [a for a in range(cost.shape[0]) if a not in set(aid.tolist())]
-        rest_c = per_action[rest].argmin(1) if rest else np.zeros(0, dtype=np.int64)
-        token_cls = np.zeros(cost.shape[0])
-        token_cls[np.array(aid.tolist() + rest, dtype=np.int64)] = np.array(
-            [actions[i] for i in cid.tolist() + list(rest_c)])
-        pairs = {}
-        for a in actions:
-            segs = np.where(tr == a)[0]
-            toks = np.where(token_cls == a)[0]
-            pick = cost[toks][:, segs].argmin(0)
-            for s, k in zip(segs, pick):
-                pairs[s] = toks[k]
-        return list(pairs.values()), list(pairs.keys())
+        return one_to_many_match(cost, tr)
 
     def action_token_loss(self, match, action_clogit, is_logit=True):
         """loss.py:195-207."""
@@ -284,3 +271,24 @@ def infonce_contrastive_loss(projected_embeddings, text_embeddings, labels, temp
     counts = torch.clamp(tgt.sum(0), min=1.0)
     t2v = (-(lp_t * tgt.t()).sum(1) / counts).mean()
     return (v2t + t2v) / 2.0
+
+
+def one_to_many_match(cost, tr):
+    """MatchCriterion._one_to_many_match (loss.py:155-193) on a host cost matrix (tokens x segments)
+    and the segments' classes ``tr``."""
+    actions = np.unique(tr)
+    per_action = np.stack([cost[:, tr == a].sum(1) for a in actions], axis=1)
+    aid, cid = linear_sum_assignment(per_action)
+    rest = [a for a in range(cost.shape[0]) if a not in set(aid.tolist())]
+    rest_c = per_action[rest].argmin(1) if rest else np.zeros(0, dtype=np.int64)
+    token_cls = np.zeros(cost.shape[0])
+    token_cls[np.array(aid.tolist() + rest, dtype=np.int64)] = np.array(
+        [actions[i] for i in cid.tolist() + list(rest_c)])
+    pairs = {}
+    for a in actions:
+        segs = np.where(tr == a)[0]
+        toks = np.where(token_cls == a)[0]
+        pick = cost[toks][:, segs].argmin(0)
+        for s, k in zip(segs, pick):
+            pairs[s] = toks[k]
+    return list(pairs.values()), list(pairs.keys())

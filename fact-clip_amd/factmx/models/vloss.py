@@ -1,0 +1,417 @@
+"""The loss phase of a lockstep batch of videos in a handful of launches (blocks._forward_videos).
+
+The reference computes, per video and one after another (blocks.py:118-135 / 889-917):
+predictions (Block._eval / eval_with_clip, blocks.py:243-261, 788-887), the Hungarian matching
+(MatchCriterion.match, loss.py:108-153, soft IoU 91-106), every block's loss terms (compute_loss,
+blocks.py:313-320, 369-382, 487-497 over loss.py:195-277) and the CLIP InfoNCE term
+(loss.py:280-341, blocks.py:677-786).  Here, for all videos at once:
+
+  1. one upload of the host-side tables (ground-truth segments from the labels, class weights,
+     the per-video pointer table), then ONE launch of per-frame predictions (fx_eval_pred, after
+     the CLIP similarity GEMM) and ONE launch of every video's matching cost (fx_match_cost);
+  2. one read-back (predictions + costs), the Hungarian assignment per video on the host (scipy,
+     as the reference);
+  3. one upload of the term table (every CE / smooth / cross-attention / InfoNCE term of every
+     block of every video, soft targets described by frame intervals instead of one-hot / "zoom"
+     matrices), and fx_loss_terms_fwd: class terms, attention terms, InfoNCE, fixed-order finish
+     and one combine into [batch loss, per video (loss, fact, contrastive, per-block values)].
+     The backward (fx_loss_terms_bwd) writes the gradient of every logit tensor in four launches.
+"""
+import ctypes
+
+import numpy as np
+import torch
+from scipy.optimize import linear_sum_assignment
+
+from .. import functional as fxf
+from .. import native as nx
+from .loss import one_to_many_match
+
+
+class _Pack:
+    """Host tables and ABI structs laid out in one buffer: allocated on the device first (so the
+    structs can hold device addresses), then filled on the host and sent by ONE non-blocking copy
+    from pinned memory."""
+
+    def __init__(self):
+        self.items = []
+        self.size = 0
+
+    def _reserve(self, nbytes):
+        off = (self.size + 15) & ~15
+        self.size = off + max(int(nbytes), 4)
+        return off
+
+    def array(self, a, dtype):
+        a = np.ascontiguousarray(a, dtype=dtype).reshape(-1)
+        off = self._reserve(a.nbytes)
+        self.items.append((off, a))
+        return off
+
+    def structs(self, ctype, n):
+        arr = (ctype * n)()
+        off = self._reserve(ctypes.sizeof(arr))
+        self.items.append((off, arr))
+        return off, arr
+
+    def alloc(self, dev):
+        self.dev = torch.empty(self.size, dtype=torch.uint8, device=dev)
+        self.base = self.dev.data_ptr()
+        return self.base
+
+    def send(self):
+        host = torch.empty(self.size, dtype=torch.uint8, pin_memory=True)
+        hv = host.numpy()
+        for off, a in self.items:
+            b = np.frombuffer(a, dtype=np.uint8) if isinstance(a, ctypes.Array) else a.view(np.uint8)
+            hv[off:off + b.size] = b
+        self.dev.copy_(host, non_blocking=True)
+
+
+def gt_segments(lab):
+    """Run-length ground truth of a frame label vector: (starts, ends inclusive, classes) int32
+    (torch_class_label_to_segment_label, utils.py / loss.py:58-84)."""
+    lab = np.asarray(lab)
+    change = np.ones(len(lab), dtype=bool)
+    change[1:] = lab[1:] != lab[:-1]
+    st = np.nonzero(change)[0]
+    en = np.append(st[1:] - 1, len(lab) - 1)
+    return st.astype(np.int32), en.astype(np.int32), lab[st].astype(np.int32)
+
+
+def class_weights(mc, C1):
+    """MatchCriterion.set_label's cweight (C1) and the per-segment weight rule (loss.py:58-84)."""
+    cw = np.ones(C1, dtype=np.float32)
+    cw[-1] = mc.cfg.Loss.nullw
+    if mc._class_weight is not None:
+        cw[:C1 - 1] = np.asarray(mc._class_weight[:C1 - 1], dtype=np.float32)
+    else:
+        for i in mc.bg_ids:
+            cw[i] = mc.cfg.Loss.bgw
+    return cw
+
+
+def segment_weights(mc, transcript):
+    if mc._class_weight is not None:
+        return np.asarray(mc._class_weight, dtype=np.float32)[transcript]
+    sw = np.ones(len(transcript), dtype=np.float32)
+    for i in mc.bg_ids:
+        sw[transcript == i] = mc.cfg.Loss.bgw
+    return sw
+
+
+def supported(net):
+    """The fused phase covers FACT / FACT_CLIP without transcripts whose last block has token->frame
+    attention (every reference config: the matching reads it) and <= 64 tokens."""
+    from .blocks import UpdateBlock, UpdateBlockTDU
+    mc = getattr(net, "mcriterion", None)
+    if mc is None or net.cfg.FACT.trans or net.cfg.Loss.match not in ("o2o", "o2m", "seq"):
+        return False
+    if not isinstance(net.block_list[-1], (UpdateBlock, UpdateBlockTDU)):
+        return False
+    if net.cfg.FACT.ntoken > nx.LOSS_MAXK:
+        return False
+    return all(hasattr(b, "_bt") for b in net.block_list)
+
+
+def _ptr_rows(t, row0, ld):
+    return t.data_ptr() + 4 * row0 * ld
+
+
+class _LossFn(torch.autograd.Function):
+    """out = fx_loss_terms_fwd(term table); backward writes every input's gradient whole."""
+
+    @staticmethod
+    def forward(ctx, plan, *inputs):
+        lib = nx.load()
+        out = torch.empty(plan["nout"], device=inputs[0].device, dtype=torch.float32)
+        nx.check(lib.fx_loss_terms_fwd(ctypes.addressof(plan["terms_host"]), plan["terms_dev"], plan["nterms"],
+                                       plan["coef_dev"], plan["nout"], nx.ptr(out), nx.ptr(plan["ws"]), nx.stream()),
+                 "fx_loss_terms_fwd")
+        ctx.plan = plan
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        plan = ctx.plan
+        lib = nx.load()
+        gout = gout.contiguous()
+        nx.check(lib.fx_loss_terms_bwd(ctypes.addressof(plan["terms_host"]), plan["terms_dev"], plan["nterms"],
+                                       plan["coef_dev"], plan["nout"], nx.ptr(gout), nx.ptr(plan["ws"]), nx.stream()),
+                 "fx_loss_terms_bwd")
+        return (None,) + tuple(plan["grads"])
+
+
+def run(net, vb, label_list, hosts, compute_loss):
+    """Predictions (and with compute_loss the batch loss + per-video loss values) of the lockstep
+    batch whose block outputs forward_batch left in ``blk._bt``.  Returns what _forward_videos
+    returns: save_list, or (loss, save_list)."""
+    from .blocks import FACT_CLIP, InputBlock, UpdateBlockTDU
+    lib = nx.load()
+    cfg = net.cfg
+    blocks = list(net.block_list)
+    last = blocks[-1]._bt
+    nvid, T, Q = vb.nvid, vb.T, vb.Q
+    C = net.num_classes
+    C1 = C + 1
+    dev = last["f_cl"].device
+    mc = net.mcriterion
+    clip = isinstance(net, FACT_CLIP)
+    text = getattr(net, "text_embeddings", None) if clip else None
+    proj = getattr(net, "_proj", None) if clip else None
+    use_clip = text is not None and proj is not None
+
+    # ------------------------------------------------------------------ labels -> ground truth (host)
+    gts, labs = [], []
+    if compute_loss:
+        for v, (lh, ev) in enumerate(hosts):
+            if ev is not None:
+                ev.synchronize()
+            lab = lh.numpy() if torch.is_tensor(lh) else np.asarray(lh)
+            labs.append(lab)
+            gts.append(gt_segments(lab))
+    G = [len(g[0]) for g in gts]
+    Gmax = max(G) if G else 1
+    match_kind = cfg.Loss.match
+
+    # ------------------------------------------------------------------ stage 1: preds + costs
+    flog = fxf.matmul_nt(proj.detach(), text, alpha=1.0 / cfg.CLIP.temp) if use_clip else last["f_cl"]
+    tdu_last = "S" in last
+    pk = _Pack()
+    gt_off = [(pk.array(g[0], np.int32), pk.array(g[1], np.int32), pk.array(g[2], np.int32)) for g in gts]
+    lab_off = [pk.array(lab, np.int32) for lab in labs]
+    cw = class_weights(mc, C1)
+    cw_off = pk.array(cw, np.float32)
+    va_off, va = pk.structs(nx.VideoAttn, nvid)
+    base = pk.alloc(dev)
+    for v in range(nvid):
+        a = va[v]
+        a.Q, a.C1, a.T, a.G = Q, C1, T, (G[v] if compute_loss else 0)
+        a.clogit, a.ldc = _ptr_rows(last["a_cl"], v * Q, C1), C1
+        if tdu_last:
+            a.attn, a.lda = last["a2f_at"].data_ptr() + 4 * Q * last["s_off"][v], Q
+            a.seg_id = last["local"][v][0].data_ptr()
+        else:
+            a.attn, a.lda = last["a2f_at"].data_ptr() + 4 * Q * T * v, Q
+        a.flogit, a.ldf = _ptr_rows(flog, v * T, C), C
+        if compute_loss:
+            a.gs, a.ge, a.gl = (base + o for o in gt_off[v])
+        a.pred_off = v * T
+    pk.send()
+    need_cost = compute_loss and match_kind != "seq"
+    res = torch.empty(nvid * T + (nvid * Q * Gmax if need_cost else 0), dtype=torch.int32, device=dev)
+    nx.check(lib.fx_eval_pred(ctypes.addressof(va), base + va_off, nvid, float(cfg.FACT.mwt), nx.ptr(res),
+                              nx.stream()), "fx_eval_pred")
+    if need_cost:
+        cost_d = res[nvid * T:].view(torch.float32)
+        nx.check(lib.fx_match_cost(ctypes.addressof(va), base + va_off, nvid, float(cfg.Loss.pc), float(cfg.Loss.a2fc),
+                                   Gmax, nx.ptr(cost_d), nx.stream()), "fx_match_cost")
+    host = res.cpu().numpy()
+    save_list = [{"pred": host[v * T:(v + 1) * T].astype(np.int64)} for v in range(nvid)]
+    if not compute_loss:
+        return save_list
+    cost = host[nvid * T:].view(np.float32).reshape(nvid, Q, Gmax) if need_cost else None
+
+    # ------------------------------------------------------------------ Hungarian (host, per video)
+    matches = []
+    for v in range(nvid):
+        if match_kind == "seq":
+            assert Q >= G[v], (Q, G[v])
+            ai = si = np.arange(G[v])
+        else:
+            c = cost[v, :, :G[v]].astype(np.float64)
+            ai, si = linear_sum_assignment(c) if match_kind == "o2o" else one_to_many_match(c, gts[v][2])
+        matches.append((np.asarray(ai, dtype=np.int64), np.asarray(si, dtype=np.int64)))
+
+    # ------------------------------------------------------------------ stage 2: the term table
+    sw_coef = float(cfg.Loss.sw)
+    nb = len(blocks)
+    con_on = []
+    remap = None
+    text_seen = text
+    if use_clip:
+        hold = list(getattr(cfg, "holdout_classes", []) or [])
+        if hold:
+            n = text.shape[0]
+            key = (n, tuple(hold), text.data_ptr(), text._version)
+            if getattr(net, "_vloss_text_key", None) != key:
+                seen = [i for i in range(n) if i not in set(hold)]
+                rm = np.full(n, -1, dtype=np.int64)
+                rm[seen] = np.arange(len(seen))
+                net._vloss_text = (text[torch.tensor(seen, device=text.device)].contiguous(), rm)
+                net._vloss_text_key = key
+            text_seen, remap = net._vloss_text
+        else:
+            text_seen = text.contiguous()
+    y_con = []
+    for v in range(nvid):
+        if not use_clip:
+            con_on.append(False)
+            y_con.append(None)
+            continue
+        y = remap[labs[v]] if remap is not None else labs[v]
+        con_on.append(bool((y != -1).any()))
+        y_con.append(y)
+
+    pk2 = _Pack()
+    tgt_off, sw_list = [], []
+    for v in range(nvid):
+        ai, si = matches[v]
+        tgt = np.full(Q, C1 - 1, dtype=np.int32)
+        tgt[ai] = gts[v][2][si]
+        tgt_off.append((pk2.array(tgt, np.int32), float(cw[tgt].sum())))
+        swn = segment_weights(mc, gts[v][2])
+        K = len(ai)
+        if len(swn) not in (K, 1):
+            raise RuntimeError(f"cross_attn_loss: {K} matched columns vs {len(swn)} segment weights")
+        sw_list.append([float(swn[i if len(swn) == K else 0]) for i in range(K)])
+    ycon_off = [pk2.array(y, np.int32) if y is not None and con_on[v] else None for v, y in enumerate(y_con)]
+
+    inputs, grads, gidx = [], [], {}
+
+    def grad_of(t):
+        k = id(t)
+        if k not in gidx:
+            gidx[k] = len(inputs)
+            inputs.append(t)
+            grads.append(torch.empty_like(t))
+        return grads[gidx[k]]
+
+    specs = []       # (block index or -1 for InfoNCE, video, dict of LossTerm fields, scratch sizes)
+    scratch = [0]
+
+    def add(k, v, f, n_lse, n_lse2, n_colz):
+        offs = []
+        for n in (n_lse, n_lse2, n_colz):
+            offs.append(scratch[0])
+            scratch[0] += max(n, 1)
+        specs.append((k, v, f, offs))
+
+    for k, blk in enumerate(blocks):
+        bt = blk._bt
+        is_tdu = isinstance(blk, UpdateBlockTDU)
+        f_cl, a_cl = bt["f_cl"], bt["a_cl"]
+        gf, ga = grad_of(f_cl), grad_of(a_cl)
+        fce = 0.5 if is_tdu else 1.0
+        for v in range(nvid):
+            gs, ge, gl = gt_off[v]
+            # frame CE (+ smooth) on the block's frame logits
+            add(k, v, dict(kind=nx.TERM_CLASS, R=T, C=C, x=_ptr_rows(f_cl, v * T, C), sr=C, sc=1,
+                           dx=_ptr_rows(gf, v * T, C), dsr=C, dsc=1, y=("p1", lab_off[v]), w=("p1", cw_off),
+                           c_ce=fce / T, c_sm=(sw_coef / ((T - 1) * C) if sw_coef and T > 1 else 0.0)), T, 0, 0)
+            # token CE
+            add(k, v, dict(kind=nx.TERM_CLASS, R=Q, C=C1, x=_ptr_rows(a_cl, v * Q, C1), sr=C1, sc=1,
+                           dx=_ptr_rows(ga, v * Q, C1), dsr=C1, dsc=1, y=("p2", tgt_off[v][0]), w=("p1", cw_off),
+                           c_ce=1.0 / tgt_off[v][1], c_sm=0.0), Q, 0, 0)
+            if isinstance(blk, InputBlock):
+                continue
+            ai, si = matches[v]
+            K = len(ai)
+            kgs = gts[v][0][si]
+            kge = gts[v][1][si]
+            if is_tdu:
+                Sv, s0 = bt["S"][v], bt["s_off"][v]
+                st, en = bt["local"][v][1], bt["local"][v][2]
+                seg_cl = bt["seg_cl"]
+                gsg = grad_of(seg_cl)
+                add(k, v, dict(kind=nx.TERM_CLASS, R=Sv, C=C, x=_ptr_rows(seg_cl, s0, C), sr=C, sc=1,
+                               dx=_ptr_rows(gsg, s0, C), dsr=C, dsc=1, rs=st.data_ptr(), re=en.data_ptr(),
+                               gs=("p1", gs), ge=("p1", ge), gl=("p1", gl), G=G[v], w=("p1", cw_off),
+                               c_ce=0.5 / Sv, c_sm=0.0), Sv, 0, 0)
+                R, off, ivs, c_xe, c_sm = Sv, Q * s0, (st.data_ptr(), en.data_ptr()), 1.0 / Sv, 0.0
+            else:
+                R, off, ivs = T, Q * T * v, (None, None)
+                c_xe, c_sm = 1.0 / T, (sw_coef / ((T - 1) * Q) if sw_coef and T > 1 else 0.0)
+            f2a, a2f = bt["f2a_lg"], bt["a2f_lg"]
+            gfa, gaf = grad_of(f2a), grad_of(a2f)
+            common = dict(kind=nx.TERM_ATTN, R=R, C=Q, rs=ivs[0], re=ivs[1], K=K, ka=ai, kgs=kgs, kge=kge,
+                          ksw=sw_list[v], c_ce=c_xe, c_sm=c_sm)
+            # f2a logits (Q, R) read as (R, Q): log_softmax over rows per matched column (dim=1)
+            add(k, v, dict(common, x=f2a.data_ptr() + 4 * off, sr=1, sc=R, dx=gfa.data_ptr() + 4 * off, dsr=1,
+                           dsc=R, axis=0), R, R + K, K)
+            add(k, v, dict(common, x=a2f.data_ptr() + 4 * off, sr=Q, sc=1, dx=gaf.data_ptr() + 4 * off, dsr=Q,
+                           dsc=1, axis=1), R, R + K, K)
+    sims = None
+    if any(con_on):
+        Cs = text_seen.shape[0]
+        Dc = text_seen.shape[1]
+        sims = torch.empty(2, nvid * T, Cs, device=dev)
+        gp = grad_of(proj)
+        if not all(con_on):
+            gp.zero_()
+        for v in range(nvid):
+            if not con_on[v]:
+                continue
+            add(-1, v, dict(kind=nx.TERM_INFONCE, R=T, C=Cs, x=_ptr_rows(sims[0], v * T, Cs), sr=Cs, sc=1,
+                            dx=_ptr_rows(sims[1], v * T, Cs), dsr=Cs, dsc=1, y=("p2", ycon_off[v]),
+                            emb=_ptr_rows(proj, v * T, Dc), ld_emb=Dc, text=text_seen.data_ptr(), D=Dc,
+                            inv_temp=1.0 / float(cfg.CLIP.temp), demb=_ptr_rows(gp, v * T, Dc), ld_demb=Dc,
+                            c_ce=0.5), T, Cs, Cs + 1)
+
+    # coefficient matrix: out = [batch loss, per video (loss, fact, contrastive, block values...)]
+    nterms = len(specs)
+    per = 3 + nb
+    nout = 1 + nvid * per
+    coef = np.zeros((nout, nterms), dtype=np.float32)
+    fw, cwt = float(getattr(cfg.CLIP, "fact_loss_weight", 1.0)), float(getattr(cfg.CLIP, "contrastive_weight", 0.0))
+    for i, (k, v, _, _) in enumerate(specs):
+        o = 1 + v * per
+        if k >= 0:
+            coef[o + 3 + k, i] = 1.0
+            coef[o + 1, i] = 1.0 / nb
+            lw = fw / nb if con_on[v] else 1.0 / nb
+        else:
+            coef[o + 2, i] = 1.0
+            lw = cwt
+        coef[o, i] = lw
+        coef[0, i] = lw / nvid
+    coef_off = pk2.array(coef, np.float32)
+    t_off, terms = pk2.structs(nx.LossTerm, nterms)
+    base2 = pk2.alloc(dev)
+    scr = torch.empty(max(scratch[0], 1), device=dev, dtype=torch.float32)
+    sbase = scr.data_ptr()
+    bases = {"p1": base, "p2": base2}
+    for i, (k, v, f, offs) in enumerate(specs):
+        t = terms[i]
+        t.slot = i
+        for name, val in f.items():
+            if name in ("ka", "kgs", "kge"):
+                arr = getattr(t, name)
+                for j, x in enumerate(val):
+                    arr[j] = int(x)
+            elif name == "ksw":
+                for j, x in enumerate(val):
+                    t.ksw[j] = float(x)
+            elif isinstance(val, tuple):
+                setattr(t, name, bases[val[0]] + val[1])
+            elif val is not None:
+                setattr(t, name, val)
+        t.lse, t.lse2, t.colz = (sbase + 4 * o for o in offs)
+    pk2.send()
+    ws = torch.empty(max(lib.fx_loss_terms_workspace_floats(nterms), 1), device=dev, dtype=torch.float32)
+    plan = dict(terms_host=terms, terms_dev=base2 + t_off, nterms=nterms, coef_dev=base2 + coef_off, nout=nout,
+                ws=ws, grads=grads, keep=(pk, pk2, scr, sims, res, flog, text_seen))
+    out = _LossFn.apply(plan, *inputs)
+
+    # the reference's side channels: last video's per-block losses, fact / contrastive terms
+    # (blocks.py:905-910: a video without a contrastive term reports the attributes an earlier
+    # video -- or an earlier call -- left behind, as the reference's hasattr checks do)
+    prev = None
+    if hasattr(net, "fact_loss") and hasattr(net, "contrastive_loss"):
+        prev = (float(net.fact_loss), float(net.contrastive_loss))
+    o = 1 + (nvid - 1) * per
+    net.loss_list = [out[o + 3 + k] for k in range(nb)]
+    for v in range(nvid):
+        if con_on[v]:
+            o = 1 + v * per
+            net.fact_loss, net.contrastive_loss = out[o + 1], out[o + 2]
+    vals = out.detach().cpu().tolist()
+    for v in range(nvid):
+        o = 1 + v * per
+        d = {"loss": vals[o]}
+        if con_on[v]:
+            prev = (vals[o + 1], vals[o + 2])
+        if prev is not None:
+            d["fact_loss"], d["contrastive_loss"] = prev
+        save_list[v]["loss"] = d
+    return out[0], save_list

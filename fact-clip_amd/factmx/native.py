@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FACTMX_LIB", os.path.join(_HERE, "_lib", "libfactmx.so"))
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -65,10 +65,31 @@ class DecoderGrads(ctypes.Structure):
     _fields_ = [(n, P) for n in _DEC_PTRS] + [(n, P) for n in DECODER_GLOBAL_FIELDS]
 
 
+LOSS_MAXK = 64
+TERM_CLASS, TERM_ATTN, TERM_INFONCE = 0, 1, 2
+
+
+class LossTerm(ctypes.Structure):
+    _fields_ = [("kind", I), ("slot", I), ("R", I), ("C", I), ("x", P), ("sr", L), ("sc", L), ("dx", P), ("dsr", L),
+                ("dsc", L), ("y", P), ("rs", P), ("re", P), ("gs", P), ("ge", P), ("gl", P), ("G", I), ("axis", I),
+                ("K", I), ("D", I), ("w", P), ("c_ce", F), ("c_sm", F), ("inv_temp", F), ("pad0", F), ("lse", P),
+                ("lse2", P), ("colz", P), ("emb", P), ("ld_emb", L), ("text", P), ("demb", P), ("ld_demb", L),
+                ("ka", I * LOSS_MAXK), ("kgs", I * LOSS_MAXK), ("kge", I * LOSS_MAXK), ("ksw", F * LOSS_MAXK)]
+
+
+class VideoAttn(ctypes.Structure):
+    _fields_ = [("Q", I), ("C1", I), ("T", I), ("G", I), ("clogit", P), ("ldc", L), ("attn", P), ("lda", L),
+                ("seg_id", P), ("flogit", P), ("ldf", L), ("gs", P), ("ge", P), ("gl", P), ("pred_off", L)]
+
+
+ABI_STRUCTS = (GemmDesc, DecoderParams, MstcnParams, LossTerm, VideoAttn)   # fx_struct_size ids
+
+
 # name -> (restype, argtypes); every fx_* symbol declared in include/factmx.h
 SIGNATURES = {
     "fx_version": (I, []),
     "fx_last_error": (ctypes.c_char_p, []),
+    "fx_struct_size": (L, [I]),
     "fx_gemm": (I, [ctypes.POINTER(GemmDesc), P]),
     "fx_gemm_workspace_floats": (L, [ctypes.POINTER(GemmDesc)]),
     "fx_linear_fwd": (I, [P, L, P, L, I, I, I, P, L, P, P, L, I, I, P]),
@@ -124,6 +145,11 @@ SIGNATURES = {
     "fx_class_loss_bwd": (I, [P, L, L, I, I, P, P, P, P, F, F, P, P, P]),
     "fx_attn_loss_fwd": (I, [P, L, L, I, I, I, P, P, P, P, I, I, F, F, P, P, P, P, P, P]),
     "fx_attn_loss_bwd": (I, [P, L, L, I, I, I, P, P, P, P, I, I, P, P, P, F, F, P, P, L, L, P]),
+    "fx_loss_terms_workspace_floats": (L, [I]),
+    "fx_loss_terms_fwd": (I, [P, P, I, P, I, P, P, P]),
+    "fx_loss_terms_bwd": (I, [P, P, I, P, I, P, P, P]),
+    "fx_match_cost": (I, [P, P, I, F, F, I, P, P]),
+    "fx_eval_pred": (I, [P, P, I, F, P, P]),
     "fx_prof_enable": (I, [I, I]),
     "fx_prof_collect": (I, [I, ctypes.POINTER(D), ctypes.POINTER(D), ctypes.POINTER(D), ctypes.POINTER(I)]),
     "fx_prof_disable": (None, []),
@@ -150,6 +176,9 @@ def load(path=None):
     v = lib.fx_version()
     if v != ABI_VERSION:
         raise FactmxNativeError(f"libfactmx ABI {v} != expected {ABI_VERSION}")
+    for i, st in enumerate(ABI_STRUCTS):
+        if lib.fx_struct_size(i) != ctypes.sizeof(st):
+            raise FactmxNativeError(f"{st.__name__}: C size {lib.fx_struct_size(i)} != ctypes {ctypes.sizeof(st)}")
     _lib = lib
     return lib
 

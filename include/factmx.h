@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FX_ABI_VERSION 7
+#define FX_ABI_VERSION 8
 
 enum {
   FX_OK = 0,
@@ -38,6 +38,9 @@ enum {
 
 int fx_version(void);
 const char* fx_last_error(void);
+/* sizeof of the ABI structs (0 gemm_desc, 1 decoder_params, 2 mstcn_params, 3 loss_term,
+ * 4 video_attn) so bindings can check their layouts; -1 for an unknown id */
+long long fx_struct_size(int which);
 
 /* ------------------------------------------------------------------------
  * Generic f32 GEMM on MFMA (v_mfma_f32_32x32x2_f32, exact f32 products):
@@ -462,6 +465,84 @@ int fx_attn_loss_bwd(const float* L, long long sr, long long sc, int R, int Q, i
                      int axis, const float* lse_sel, const float* lse_full, const float* colz,
                      float c_xe, float c_sm, const float* gout, float* dL, long long dsr,
                      long long dsc, void* stream);
+
+/* ------------------------------------------------------------------------
+ * The loss phase of a batch of videos from a device-resident term table
+ * (replaces MatchCriterion's per-video loss ops, loss.py:195-277, the InfoNCE
+ * loss, loss.py:280-341, and their sum, blocks.py:677-786).  Each term is one
+ * scalar; the caller uploads the table (terms_dev, its host copy terms_host
+ * gives the shapes) and a coefficient matrix coef (nout x nterms): out[o] =
+ * sum_i coef[o, i] * term_i (batch loss, per-video losses, per-block values).
+ *   FX_TERM_CLASS   c_ce * sum_r sum_c z[r,c] w[c] (lse_r - x[r,c]) + c_sm * smooth
+ *                   hard labels y (-1 = ignored) or, y == NULL, soft targets: row r
+ *                   covers frames [rs[r], re[r]] (NULL: frame r) and z[r, gl[j]] is
+ *                   its overlap with ground-truth segment j / its length
+ *                   (frame_loss, frame_loss_tdu, action_token_loss, loss.py:195-277).
+ *   FX_TERM_ATTN    c_ce * cross-attention CE of the K matched token columns ka
+ *                   (axis 1: log_softmax over them per row, axis 0: over the rows of
+ *                   each), targets = overlap(row frames, [kgs[i], kge[i]]) / row
+ *                   length, column weights ksw; + c_sm * smooth over all C columns
+ *                   (cross_attn_loss(_tdu), loss.py:209-244).
+ *   FX_TERM_INFONCE x (R x C) <- emb . text^T * inv_temp (one GEMM), y class per
+ *                   frame (-1 = held out), c_ce * (row CE mean + per-class column
+ *                   log-softmax mean); backward writes demb.
+ * Scratch per term: lse (R), lse2 (R + K or C), colz (K or C + 1) floats.
+ * bwd: gout (nout) upstream gradient of out; every term's dx (and demb) written whole.
+ * ---------------------------------------------------------------------- */
+enum { FX_TERM_CLASS = 0, FX_TERM_ATTN = 1, FX_TERM_INFONCE = 2 };
+#define FX_LOSS_MAXK 64
+
+typedef struct fx_loss_term {
+  int kind, slot, R, C;
+  const float* x; long long sr, sc;
+  float* dx; long long dsr, dsc;
+  const int32_t* y;
+  const int32_t* rs; const int32_t* re;
+  const int32_t* gs; const int32_t* ge; const int32_t* gl;
+  int G, axis, K, D;
+  const float* w;
+  float c_ce, c_sm, inv_temp, pad0;
+  float* lse; float* lse2; float* colz;
+  const float* emb; long long ld_emb;
+  const float* text;
+  float* demb; long long ld_demb;
+  int32_t ka[FX_LOSS_MAXK]; int32_t kgs[FX_LOSS_MAXK]; int32_t kge[FX_LOSS_MAXK];
+  float ksw[FX_LOSS_MAXK];
+} fx_loss_term;
+
+long long fx_loss_terms_workspace_floats(int nterms);
+int fx_loss_terms_fwd(const fx_loss_term* terms_host, const fx_loss_term* terms_dev, int nterms,
+                      const float* coef, int nout, float* out, float* workspace, void* stream);
+int fx_loss_terms_bwd(const fx_loss_term* terms_host, const fx_loss_term* terms_dev, int nterms,
+                      const float* coef, int nout, const float* gout, float* workspace, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Per-video matching cost and prediction (one launch each for every video).
+ * A video: Q token class logits clogit (Q, C1) ldc; the last block's token->frame
+ * attention attn (T rows, or S segment rows + seg_id (T)) lda; frame logits flogit
+ * (T, C1-1) ldf (eval only); ground-truth segments gs/ge (inclusive frames) and
+ * their classes gl, G of them.
+ * fx_match_cost (MatchCriterion.match, loss.py:108-153 + a2f_soft_iou 91-106):
+ *   cost[v, a, s] = -pc * softmax(clogit[a])[gl[s]] - a2fc * overlap / union,
+ *   (nvid, Q, Gmax), s >= G_v zero-filled.
+ * fx_eval_pred (Block._eval / eval_with_clip, blocks.py:243-261, 854-887):
+ *   pred[pred_off + t] = argmax((1-mwt) softmax(clogit[best token of t])[:C] +
+ *   mwt softmax(flogit[t])), or argmax(softmax(flogit[t])) when every token is null.
+ * ---------------------------------------------------------------------- */
+typedef struct fx_video_attn {
+  int Q, C1, T, G;
+  const float* clogit; long long ldc;
+  const float* attn; long long lda;
+  const int32_t* seg_id;
+  const float* flogit; long long ldf;
+  const int32_t* gs; const int32_t* ge; const int32_t* gl;
+  long long pred_off;
+} fx_video_attn;
+
+int fx_match_cost(const fx_video_attn* vids_host, const fx_video_attn* vids_dev, int nvid, float pc,
+                  float a2fc, int Gmax, float* cost, void* stream);
+int fx_eval_pred(const fx_video_attn* vids_host, const fx_video_attn* vids_dev, int nvid, float mwt,
+                 int32_t* pred, void* stream);
 
 /* ------------------------------------------------------------------------
  * Profiling hooks: HIP-event timing of every launch of one kernel class
