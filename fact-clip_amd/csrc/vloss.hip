@@ -10,12 +10,13 @@
 //                     overlap[a,s] = sum of a's attention over segment s and union = len_s + colsum_a -
 //                     overlap[a,s] (attention <= 1, so min(attn + 1, 1) = 1 inside the segment).
 //   fx_loss_terms_fwd every CE / smooth / cross-attention / InfoNCE term of every block of every video
-//                     from ONE device-resident term table: one launch for the class terms, one for the
-//                     attention terms, one per InfoNCE group (+ its similarity GEMM), one fixed-order
-//                     finish and one combine into the batch loss and the per-video values.  Soft targets
-//                     (the TDU "zoom" of the one-hot labels, loss.py:226-231, 266-269) are frame-interval
-//                     overlaps between TDU segments and ground-truth segments, computed in the kernels.
-//   fx_loss_terms_bwd the gradient of every term's logits in the same two launches (+ InfoNCE).
+//                     from ONE device-resident term table: the InfoNCE similarity GEMMs, then ONE launch
+//                     of every term over (row blocks x terms), one fixed-order finish (InfoNCE column
+//                     log-softmax merged from per-block partials) and one combine into the batch loss and
+//                     the per-video values.  Soft targets (the TDU "zoom" of the one-hot labels,
+//                     loss.py:226-231, 266-269) are frame-interval overlaps between TDU segments and
+//                     ground-truth segments, computed in the kernels.
+//   fx_loss_terms_bwd the gradient of every term's logits: class, attention, InfoNCE launches (+ GEMM).
 //   fx_eval_pred      one launch: every video's per-frame prediction (eval_with_clip / Block._eval).
 #include <algorithm>
 #include <cmath>
@@ -27,7 +28,6 @@ namespace fx {
 namespace {
 
 constexpr int VT = 256;        // threads per block (4 waves, one row at a time per wave)
-constexpr int VNB = 64;        // row blocks per term
 
 __device__ __forceinline__ float vsum(float v) {
 #pragma unroll
@@ -95,9 +95,10 @@ __device__ __forceinline__ float smooth_g(const fx_loss_term& t, int r, int c, f
 }
 
 // ------------------------------------------------------------------ class terms (frame / seg / token CE + smooth)
-__device__ void class_fwd(const fx_loss_term& t, int lane, int gw, int nw, float& ce, float& sm) {
-  for (int r = gw; r < t.R; r += nw) {
-    const float l0 = row_lse_t(t, r, t.C, lane);
+// rows [r0, r1) of one wave: the next row's lse is carried into the following iteration
+__device__ void class_fwd(const fx_loss_term& t, int lane, int r0, int r1, float& ce, float& sm) {
+  float l0 = r0 < r1 ? row_lse_t(t, r0, t.C, lane) : 0.f;
+  for (int r = r0; r < r1; ++r) {
     if (lane == 0) t.lse[r] = l0;
     if (t.y) {
       if (lane == 0) {
@@ -116,8 +117,9 @@ __device__ void class_fwd(const fx_loss_term& t, int lane, int gw, int nw, float
       }
       ce += acc;
     }
+    float l1 = 0.f;
+    if (r + 1 < t.R && (t.c_sm != 0.f || r + 1 < r1)) l1 = row_lse_t(t, r + 1, t.C, lane);
     if (t.c_sm != 0.f && r + 1 < t.R) {
-      const float l1 = row_lse_t(t, r + 1, t.C, lane);
       float s = 0.f;
       for (int c = lane; c < t.C; c += 64) {
         const float d = (at(t, r + 1, c) - l1) - (at(t, r, c) - l0);
@@ -125,13 +127,14 @@ __device__ void class_fwd(const fx_loss_term& t, int lane, int gw, int nw, float
       }
       sm += s;
     }
+    l0 = l1;
   }
 }
 
-__device__ void class_bwd(const fx_loss_term& t, float* tzrow, int lane, int gw, int nw, float gout) {
+__device__ void class_bwd(const fx_loss_term& t, float* tzrow, int lane, int r0, int r1, float gout) {
   const float g_ce = gout * t.c_ce, g_sm = gout * t.c_sm;
   const bool smooth = t.c_sm != 0.f;
-  for (int r = gw; r < t.R; r += nw) {
+  for (int r = r0; r < r1; ++r) {
     const float l0 = t.lse[r];
     const float lm = (smooth && r > 0) ? t.lse[r - 1] : 0.f;
     const float lp1 = (smooth && r + 1 < t.R) ? t.lse[r + 1] : 0.f;
@@ -178,42 +181,40 @@ __device__ __forceinline__ float attn_target(const fx_loss_term& t, int r, int i
   return overlap(f0, f1, t.kgs[i], t.kge[i]) / (float)(f1 - f0 + 1);
 }
 
-__device__ void attn_fwd(const fx_loss_term& t, int lane, int gw, int nw, float& xe, float& sm) {
+__device__ void attn_fwd(const fx_loss_term& t, int lane, int gw, int r0, int r1, float& xe, float& sm) {
   if (t.axis == 1) {
-    for (int r = gw; r < t.R; r += nw) {
+    for (int r = r0; r < r1; ++r) {
       const float v = lane < t.K ? at(t, r, t.ka[lane]) : -INFINITY;
       const float m = vmax(v);
       const float l = m + __logf(vsum(lane < t.K ? __expf(v - m) : 0.f));
       if (lane == 0) t.lse[r] = l;
       xe += lane < t.K ? -(v - l) * attn_target(t, r, lane) * t.ksw[lane] : 0.f;
     }
-  } else {
-    for (int i = gw; i < t.K; i += nw) {
-      const int q = t.ka[i];
-      float m = -INFINITY;
-      for (int r = lane; r < t.R; r += 64) m = fmaxf(m, at(t, r, q));
-      m = vmax(m);
-      float s = 0.f, zs = 0.f, zl = 0.f;
-      for (int r = lane; r < t.R; r += 64) {
-        const float x = at(t, r, q);
-        const float zz = attn_target(t, r, i);
-        s += __expf(x - m);
-        zs += zz;
-        zl += zz * x;
-      }
-      const float l = m + __logf(vsum(s));
-      zs = vsum(zs);
-      zl = vsum(zl);
-      if (lane == 0) {
-        t.lse2[t.R + i] = l;              // per-column lse after the R row slots
-        t.colz[i] = zs * t.ksw[i];
-        xe += -(zl - zs * l) * t.ksw[i];
-      }
+  } else if (gw < t.K) {   // one wave per matched column: log_softmax over the rows
+    const int i = gw, q = t.ka[i];
+    float m = -INFINITY;
+    for (int r = lane; r < t.R; r += 64) m = fmaxf(m, at(t, r, q));
+    m = vmax(m);
+    float s = 0.f, zs = 0.f, zl = 0.f;
+    for (int r = lane; r < t.R; r += 64) {
+      const float x = at(t, r, q);
+      const float zz = attn_target(t, r, i);
+      s += __expf(x - m);
+      zs += zz;
+      zl += zz * x;
+    }
+    const float l = m + __logf(vsum(s));
+    zs = vsum(zs);
+    zl = vsum(zl);
+    if (lane == 0) {
+      t.lse2[t.R + i] = l;              // per-column lse after the R row slots
+      t.colz[i] = zs * t.ksw[i];
+      xe += -(zl - zs * l) * t.ksw[i];
     }
   }
   if (t.c_sm != 0.f) {
-    for (int r = gw; r < t.R; r += nw) {
-      const float l0 = row_lse_t(t, r, t.C, lane);
+    float l0 = r0 < r1 ? row_lse_t(t, r0, t.C, lane) : 0.f;
+    for (int r = r0; r < r1; ++r) {
       if (lane == 0) t.lse2[r] = l0;
       if (r + 1 < t.R) {
         const float l1 = row_lse_t(t, r + 1, t.C, lane);
@@ -223,15 +224,59 @@ __device__ void attn_fwd(const fx_loss_term& t, int lane, int gw, int nw, float&
           s += fminf(d * d, 16.f);
         }
         sm += s;
+        l0 = l1;
       }
     }
   }
 }
 
-__device__ void attn_bwd(const fx_loss_term& t, int lane, int gw, int nw, float gout) {
+// InfoNCE, rows [r0, r1) of one wave: row lse and CE of the valid frames
+__device__ void infonce_rows(const fx_loss_term& t, int lane, int r0, int r1, float& v2t, float& nval) {
+  for (int r = r0; r < r1; ++r) {
+    const int y = t.y[r];
+    const float l = row_lse_t(t, r, t.C, lane);
+    if (lane == 0) {
+      t.lse[r] = l;
+      if (y >= 0) {
+        v2t += l - at(t, r, y);
+        nval += 1.f;
+      }
+    }
+  }
+}
+
+// InfoNCE column partials over the block's rows [b0, b1): per column online (max, sum exp) over the
+// valid frames, their count and the sum of the frames labelled with the column's class
+__device__ void infonce_cols(const fx_loss_term& t, int b0, int b1, float* cp) {
+  for (int c = threadIdx.x; c < t.C; c += VT) {
+    float m = -INFINITY, s = 0.f, cnt = 0.f, sx = 0.f;
+    for (int r = b0; r < b1; ++r) {
+      const int y = t.y[r];
+      if (y < 0) continue;
+      const float x = at(t, r, c);
+      if (x > m) {
+        s = s * __expf(m - x) + 1.f;
+        m = x;
+      } else {
+        s += __expf(x - m);
+      }
+      if (y == c) {
+        cnt += 1.f;
+        sx += x;
+      }
+    }
+    float* o = cp + ((long long)blockIdx.x * t.C + c) * 4;
+    o[0] = m;
+    o[1] = s;
+    o[2] = cnt;
+    o[3] = sx;
+  }
+}
+
+__device__ void attn_bwd(const fx_loss_term& t, int lane, int r0, int r1, float gout) {
   const float g_xe = gout * t.c_ce, g_sm = gout * t.c_sm;
   const bool smooth = t.c_sm != 0.f;
-  for (int r = gw; r < t.R; r += nw) {
+  for (int r = r0; r < r1; ++r) {
     const float l0 = smooth ? t.lse2[r] : 0.f;
     const float lm = (smooth && r > 0) ? t.lse2[r - 1] : 0.f;
     const float lp1 = (smooth && r + 1 < t.R) ? t.lse2[r + 1] : 0.f;
@@ -257,15 +302,28 @@ __device__ void attn_bwd(const fx_loss_term& t, int lane, int gw, int nw, float 
 }
 
 // ------------------------------------------------------------------ term kernels (grid: row blocks x terms)
-__global__ __launch_bounds__(VT) void terms_fwd_kernel(const fx_loss_term* terms, float* part, int kind) {
+// block b of a term owns the contiguous rows [b * rpb, (b + 1) * rpb), each wave a quarter of them
+__device__ __forceinline__ void wave_rows(int R, int wv, int& r0, int& r1, int& b0, int& b1) {
+  const int rpw = (R + gridDim.x * (VT / 64) - 1) / (gridDim.x * (VT / 64));
+  b0 = min(R, (int)blockIdx.x * (VT / 64) * rpw);
+  b1 = min(R, b0 + (VT / 64) * rpw);
+  r0 = min(R, b0 + wv * rpw);
+  r1 = min(R, r0 + rpw);
+}
+
+__global__ __launch_bounds__(VT) void terms_fwd_kernel(const fx_loss_term* terms, float* part) {
   __shared__ float red[2][VT / 64];
   const fx_loss_term& t = terms[blockIdx.y];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int gw = blockIdx.x * (VT / 64) + wv, nw = gridDim.x * (VT / 64);
+  const int gw = blockIdx.x * (VT / 64) + wv;
+  int r0, r1, b0, b1;
+  wave_rows(t.R, wv, r0, r1, b0, b1);
   float a = 0.f, b = 0.f;
-  if (t.kind == kind) {
-    if (kind == FX_TERM_CLASS) class_fwd(t, lane, gw, nw, a, b);
-    else attn_fwd(t, lane, gw, nw, a, b);
+  if (t.kind == FX_TERM_CLASS) class_fwd(t, lane, r0, r1, a, b);
+  else if (t.kind == FX_TERM_ATTN) attn_fwd(t, lane, gw, r0, r1, a, b);
+  else {
+    infonce_rows(t, lane, r0, r1, a, b);
+    infonce_cols(t, b0, b1, t.colz + t.C + 1);
   }
   a = vsum(a);
   b = vsum(b);
@@ -274,7 +332,7 @@ __global__ __launch_bounds__(VT) void terms_fwd_kernel(const fx_loss_term* terms
     red[1][wv] = b;
   }
   __syncthreads();
-  if (threadIdx.x == 0 && t.kind == kind) {
+  if (threadIdx.x == 0) {
     float s0 = 0.f, s1 = 0.f;
     for (int i = 0; i < VT / 64; ++i) {
       s0 += red[0][i];
@@ -290,9 +348,10 @@ __global__ __launch_bounds__(VT) void terms_bwd_kernel(const fx_loss_term* terms
   const fx_loss_term& t = terms[blockIdx.y];
   if (t.kind != kind) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int gw = blockIdx.x * (VT / 64) + wv, nw = gridDim.x * (VT / 64);
-  if (kind == FX_TERM_CLASS) class_bwd(t, tz + wv * t.C, lane, gw, nw, gterm[blockIdx.y]);
-  else attn_bwd(t, lane, gw, nw, gterm[blockIdx.y]);
+  int r0, r1, b0, b1;
+  wave_rows(t.R, wv, r0, r1, b0, b1);
+  if (kind == FX_TERM_CLASS) class_bwd(t, tz + wv * t.C, lane, r0, r1, gterm[blockIdx.y]);
+  else attn_bwd(t, lane, r0, r1, gterm[blockIdx.y]);
 }
 
 // gterm[i] = sum_o gout[o] coef[o, i]   (upstream gradient of each term)
@@ -305,87 +364,57 @@ __global__ __launch_bounds__(64) void combine_bwd_kernel(const float* gout, cons
   }
 }
 
-// term value = c_ce * sum(part0) + c_sm * sum(part1), blocks in fixed order (one wave per term)
-__global__ __launch_bounds__(64) void terms_finish_kernel(const fx_loss_term* terms, int nterms, const float* part,
-                                                          int nb, float* vals) {
+// term value = c_ce * sum(part0) + c_sm * sum(part1), blocks in fixed order.  InfoNCE (loss.py:280-341):
+// x = sim (R frames x C classes), y = class per frame (-1: masked); the column partials of the row
+// blocks merge into the column lse (lse2), the class counts (colz, colz[C] = valid frames) and
+//   value = c_ce * ( v2t / n_valid + (1/C) sum_c -(sum_{y_t = c} sim[t, c] - count_c lse_c) / max(count_c, 1) )
+__global__ __launch_bounds__(VT) void terms_finish_kernel(const fx_loss_term* terms, const float* part, int nb,
+                                                          float* vals) {
+  __shared__ float red[VT / 64];
   const int i = blockIdx.x;
   const fx_loss_term& t = terms[i];
-  if (t.kind == FX_TERM_INFONCE) return;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   float a = 0.f, b = 0.f;
-  for (int k = lane; k < nb; k += 64) {
-    a += part[((long long)t.slot * nb + k) * 2];
-    b += part[((long long)t.slot * nb + k) * 2 + 1];
-  }
-  a = vsum(a);
-  b = vsum(b);
-  if (lane == 0) vals[i] = t.c_sm != 0.f ? t.c_ce * a + t.c_sm * b : t.c_ce * a;
-}
-
-// ------------------------------------------------------------------ InfoNCE (loss.py:280-341)
-// x = sim (R frames x C classes, = emb . text^T / temp), y = class per frame (-1: masked frame).
-// value = c_ce * ( mean over valid frames of CE(sim_t, y_t)  +  mean over C classes of
-//          -sum_{t: y_t = c} log_softmax_over_t(sim[:, c])[t] / max(count_c, 1) ),   c_ce = 1/2
-// scratch: lse (R) row lse, lse2 (C) column lse, colz (C) counts; kval[0] = number of valid frames
-constexpr int IT = 1024;
-__global__ __launch_bounds__(IT) void infonce_fwd_kernel(const fx_loss_term* terms, float* vals) {
-  __shared__ float red[IT / 64][3];
-  const fx_loss_term& t = terms[blockIdx.x];
-  if (t.kind != FX_TERM_INFONCE) return;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = IT / 64;
-  float v2t = 0.f, nval = 0.f, t2v = 0.f;
-  for (int r = wv; r < t.R; r += nwv) {
-    const int y = t.y[r];
-    const float l = row_lse_t(t, r, t.C, lane);
-    if (lane == 0) {
-      t.lse[r] = l;
-      if (y >= 0) {
-        v2t += l - at(t, r, y);
-        nval += 1.f;
-      }
+  if (wv == 0) {
+    for (int k = lane; k < nb; k += 64) {
+      a += part[((long long)t.slot * nb + k) * 2];
+      b += part[((long long)t.slot * nb + k) * 2 + 1];
     }
+    a = vsum(a);
+    b = vsum(b);
   }
-  for (int c = wv; c < t.C; c += nwv) {
-    float m = -INFINITY;
-    for (int r = lane; r < t.R; r += 64)
-      if (t.y[r] >= 0) m = fmaxf(m, at(t, r, c));
-    m = vmax(m);
-    float s = 0.f, cnt = 0.f, sx = 0.f;
-    for (int r = lane; r < t.R; r += 64) {
-      const int y = t.y[r];
-      if (y < 0) continue;
-      const float x = at(t, r, c);
-      s += __expf(x - m);
-      if (y == c) {
-        cnt += 1.f;
-        sx += x;
-      }
+  if (t.kind != FX_TERM_INFONCE) {
+    if (threadIdx.x == 0) vals[i] = t.c_sm != 0.f ? t.c_ce * a + t.c_sm * b : t.c_ce * a;
+    return;
+  }
+  const float* cp = t.colz + t.C + 1;
+  float t2v = 0.f;
+  for (int c = threadIdx.x; c < t.C; c += VT) {
+    float m = -INFINITY, cnt = 0.f, sx = 0.f;
+    for (int k = 0; k < nb; ++k) {
+      const float* o = cp + ((long long)k * t.C + c) * 4;
+      if (o[1] > 0.f) m = fmaxf(m, o[0]);
+      cnt += o[2];
+      sx += o[3];
     }
-    s = vsum(s);
-    cnt = vsum(cnt);
-    sx = vsum(sx);
+    float s = 0.f;
+    for (int k = 0; k < nb; ++k) {
+      const float* o = cp + ((long long)k * t.C + c) * 4;
+      if (o[1] > 0.f) s += o[1] * __expf(o[0] - m);
+    }
     const float l = m + __logf(s);
-    if (lane == 0) {
-      t.lse2[c] = l;
-      t.colz[c] = cnt;
-      t2v += -(sx - cnt * l) / fmaxf(cnt, 1.f);
-    }
+    t.lse2[c] = l;
+    t.colz[c] = cnt;
+    t2v += cnt > 0.f ? -(sx - cnt * l) / cnt : 0.f;
   }
-  if (lane == 0) {
-    red[wv][0] = v2t;
-    red[wv][1] = nval;
-    red[wv][2] = t2v;
-  }
+  t2v = vsum(t2v);
+  if (lane == 0) red[wv] = t2v;
   __syncthreads();
   if (threadIdx.x == 0) {
-    float a = 0.f, n = 0.f, b = 0.f;
-    for (int i = 0; i < nwv; ++i) {
-      a += red[i][0];
-      n += red[i][1];
-      b += red[i][2];
-    }
-    t.colz[t.C] = n;
-    vals[blockIdx.x] = n > 0.f ? t.c_ce * (a / n + b / (float)t.C) : 0.f;
+    float tt = 0.f;
+    for (int k = 0; k < VT / 64; ++k) tt += red[k];
+    t.colz[t.C] = b;
+    vals[i] = b > 0.f ? t.c_ce * (a / b + tt / (float)t.C) : 0.f;
   }
 }
 
@@ -558,49 +587,39 @@ using namespace fx;
 
 extern "C" {
 
-long long fx_loss_terms_workspace_floats(int nterms) { return 2LL * VNB * std::max(nterms, 1) + std::max(nterms, 1); }
+long long fx_loss_terms_workspace_floats(int nterms) {
+  return 2LL * FX_LOSS_NB * std::max(nterms, 1) + std::max(nterms, 1);
+}
 
 int fx_loss_terms_fwd(const fx_loss_term* terms_host, const fx_loss_term* terms_dev, int nterms, const float* coef_dev,
                       int nout, float* out, float* workspace, void* stream) {
   FX_REQUIRE(terms_host && terms_dev && nterms > 0 && coef_dev && out && workspace, "loss_terms: bad arguments");
   hipStream_t s = (hipStream_t)stream;
+  const int nb = FX_LOSS_NB;
   float* part = workspace;
-  float* vals = workspace + 2LL * VNB * nterms;
-  int max_rows[3] = {0, 0, 0};
+  float* vals = workspace + 2LL * nb * nterms;
   for (int i = 0; i < nterms; ++i) {
     const fx_loss_term& t = terms_host[i];
     FX_REQUIRE(t.kind >= 0 && t.kind <= 2, "loss_terms: unknown term kind");
     FX_REQUIRE(t.R > 0 && t.C > 0 && t.x && t.lse, "loss_terms: empty term");
-    FX_REQUIRE(t.kind != FX_TERM_ATTN || (t.K >= 0 && t.K <= FX_LOSS_MAXK && t.lse2 && t.colz && t.C <= 4096),
+    FX_REQUIRE(t.kind != FX_TERM_ATTN || (t.K >= 0 && t.K <= FX_LOSS_MAXK && t.lse2 && t.colz),
                "loss_terms: attention term needs K <= 64 matched columns and scratch");
     FX_REQUIRE(t.kind != FX_TERM_CLASS || t.w, "loss_terms: class term needs weights");
     FX_REQUIRE(t.kind != FX_TERM_INFONCE || (t.y && t.lse2 && t.colz && t.emb && t.text && t.dx && t.sc == 1 &&
                                              t.dsc == 1 && t.D > 0),
                "loss_terms: InfoNCE term needs labels, embeddings, text and scratch");
     FX_REQUIRE(t.slot == i, "loss_terms: term slot must equal its index");
-    max_rows[t.kind] = std::max(max_rows[t.kind], t.kind == FX_TERM_ATTN ? std::max(t.R, t.K) : t.R);
-  }
-  const int nb = VNB;
-  FX_CHECK_HIP(hipMemsetAsync(part, 0, sizeof(float) * 2LL * nb * nterms, s));
-  for (int k = 0; k < 2; ++k) {
-    if (!max_rows[k]) continue;
-    hipLaunchKernelGGL(terms_fwd_kernel, dim3(nb, nterms), dim3(VT), 0, s, terms_dev, part, k);
-    FX_CHECK_HIP(hipGetLastError());
-  }
-  hipLaunchKernelGGL(terms_finish_kernel, dim3(nterms), dim3(64), 0, s, terms_dev, nterms, part, nb, vals);
-  FX_CHECK_HIP(hipGetLastError());
-  if (max_rows[FX_TERM_INFONCE]) {
-    for (int i = 0; i < nterms; ++i) {   // similarity GEMMs: sim = emb . text^T / temp
-      const fx_loss_term& t = terms_host[i];
-      if (t.kind != FX_TERM_INFONCE) continue;
+    if (t.kind == FX_TERM_INFONCE) {   // similarity GEMM first: sim = emb . text^T / temp
       fx_gemm_desc d = gemm_desc(t.R, t.C, t.D, op_rows(t.emb, t.ld_emb), op_rows(t.text, t.D),
                                  const_cast<float*>(t.x), t.sr);
       d.alpha = t.inv_temp;
       FX_TRY(launch_gemm(d, s));
     }
-    hipLaunchKernelGGL(infonce_fwd_kernel, dim3(nterms), dim3(IT), 0, s, terms_dev, vals);
-    FX_CHECK_HIP(hipGetLastError());
   }
+  hipLaunchKernelGGL(terms_fwd_kernel, dim3(nb, nterms), dim3(VT), 0, s, terms_dev, part);
+  FX_CHECK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(terms_finish_kernel, dim3(nterms), dim3(VT), 0, s, terms_dev, part, nb, vals);
+  FX_CHECK_HIP(hipGetLastError());
   hipLaunchKernelGGL(combine_kernel, dim3(nout), dim3(64), 0, s, vals, coef_dev, nterms, nout, out);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
@@ -622,12 +641,12 @@ int fx_loss_terms_bwd(const fx_loss_term* terms_host, const fx_loss_term* terms_
     if (t.kind == FX_TERM_CLASS) maxC = std::max(maxC, t.C);
   }
   if (has[FX_TERM_CLASS]) {
-    hipLaunchKernelGGL(terms_bwd_kernel, dim3(VNB, nterms), dim3(VT), sizeof(float) * 4 * maxC, s, terms_dev, gterm,
+    hipLaunchKernelGGL(terms_bwd_kernel, dim3(FX_LOSS_NB, nterms), dim3(VT), sizeof(float) * 4 * maxC, s, terms_dev, gterm,
                        (int)FX_TERM_CLASS);
     FX_CHECK_HIP(hipGetLastError());
   }
   if (has[FX_TERM_ATTN]) {
-    hipLaunchKernelGGL(terms_bwd_kernel, dim3(VNB, nterms), dim3(VT), 0, s, terms_dev, gterm, (int)FX_TERM_ATTN);
+    hipLaunchKernelGGL(terms_bwd_kernel, dim3(FX_LOSS_NB, nterms), dim3(VT), 0, s, terms_dev, gterm, (int)FX_TERM_ATTN);
     FX_CHECK_HIP(hipGetLastError());
   }
   if (has[FX_TERM_INFONCE]) {

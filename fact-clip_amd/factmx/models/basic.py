@@ -110,10 +110,6 @@ def add_positional_encoding(tensor, pos):
     return tensor
 
 
-def _pos_or_none(pe_module_or_tensor):
-    return pe_module_or_tensor
-
-
 class DilatedResidualLayer(nn.Module):
     """basic.py:131-171; forward runs the one-layer fused MS-TCN kernel path."""
 

@@ -232,6 +232,8 @@ class UpdateBlock(Block):
         a_out, a_cl = fxf.process_feature(a, self.nclass + 1)
         f, a2f_lg, a2f_at = fxf.x2y(a2f, a_out, f2, apos if a2f.kq_pos else None, fpos if a2f.kq_pos else None,
                                     rows=(vb.a_off, vb.f_off))
+        if vb.on_a2f is not None and vb.last is self:
+            vb.on_a2f(vb, a_cl, a2f_at)         # the loss phase's matching starts here (vloss.EarlyMatch)
         f = fxf.mstcn(self.frame_branch, f, T=vb.T, nvid=vb.nvid)
         f_out, f_cl = fxf.process_feature(f, self.nclass)
         n, Q, T = self.nclass + 1, vb.Q, vb.T
@@ -332,6 +334,8 @@ class UpdateBlockTDU(Block):
         a_out, a_cl = fxf.process_feature(a, self.nclass + 1)
         sg, a2f_lg, a2f_at = fxf.x2y(a2f, a_out, seg_out, apos if a2f.kq_pos else None,
                                      seg_pos if a2f.kq_pos else None, rows=(vb.a_off, s_off))
+        if vb.on_a2f is not None and vb.last is self:
+            vb.on_a2f(vb, a_cl, a2f_at, (s_off, local))
         lin = self.sf_merge[0]
         f = fxf.SegMergeFn.apply(sg, f2, gid, gst, gen, lin.weight, lin.bias)
         f = fxf.mstcn(self.frame_branch, f, T=vb.T, nvid=vb.nvid)
@@ -424,12 +428,14 @@ class _FACTBase(nn.Module):
             block_output.append([frame_feature, action_feature])
         return block_output
 
-    def _forward_batch(self, seq_list):
+    def _forward_batch(self, seq_list, on_a2f=None):
         """All videos through the blocks in lockstep (see _forward_videos); returns restore(v), which
-        points every side-channel attribute at video v's views."""
+        points every side-channel attribute at video v's views.  ``on_a2f`` (vloss.EarlyMatch) runs
+        when the last block's token logits and token->frame attention exist."""
         nvid, T = len(seq_list), seq_list[0].shape[0]
         Q = self.cfg.FACT.ntoken
         vb = _VideoBatch(nvid, T, Q)
+        vb.on_a2f, vb.last = on_a2f, self.block_list[-1]
         frames = []
         for seq in seq_list:
             x = seq.unsqueeze(1)
@@ -599,6 +605,7 @@ class _VideoBatch:
         self.nvid, self.T, self.Q = nvid, T, Q
         self.f_off = [v * T for v in range(nvid + 1)]
         self.a_off = [v * Q for v in range(nvid + 1)]
+        self.on_a2f = self.last = None
 
     def fr(self, v):
         return slice(v * self.T, (v + 1) * self.T)
@@ -677,13 +684,15 @@ def _forward_videos(net, seq_list, label_list, compute_loss):
 
     net.video_segments = []     # per video: the TDU segment count of every U block (host ints, no sync)
     if _batchable(net, seq_list):
-        restore = net._forward_batch(seq_list)
-        if FUSED_LOSS and vloss.supported(net):
+        fused = FUSED_LOSS and vloss.supported(net)
+        early = vloss.EarlyMatch(net, hosts) if (fused and compute_loss) else None
+        restore = net._forward_batch(seq_list, early)
+        if fused:
             nvid = len(seq_list)
             restore(nvid - 1)       # side-channel attributes: the last video's views, as in the reference
             net.video_segments = [[blk._bt["S"][v] for blk in net.block_list if "S" in blk._bt]
                                   for v in range(nvid)]
-            return vloss.run(net, net._vb, label_list, hosts, compute_loss)
+            return vloss.run(net, net._vb, compute_loss, early)
         for v in range(len(seq_list)):
             restore(v)
             net.video_segments.append([blk.tdu.num_seg for blk in net.block_list if hasattr(blk, "tdu")])

@@ -26,10 +26,13 @@ def smooth_loss(logit, is_logit=True):
 
 
 def _to_dev(t, dev):
-    """Host -> device without a device drain: pinned staging + non-blocking copy."""
+    """Host -> device without a device drain: a non-blocking copy through torch's caching pinned
+    allocator (the staging block is reused once its copy has completed, no per-call pinning)."""
     if t.device == dev or dev.type == "cpu":
         return t.to(dev)
-    return t.pin_memory().to(dev, non_blocking=True)
+    staged = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    staged.copy_(t)
+    return staged.to(dev, non_blocking=True)
 
 
 def _onehot(idx, n):

@@ -109,9 +109,7 @@ def supported(net):
         return False
     if not isinstance(net.block_list[-1], (UpdateBlock, UpdateBlockTDU)):
         return False
-    if net.cfg.FACT.ntoken > nx.LOSS_MAXK:
-        return False
-    return all(hasattr(b, "_bt") for b in net.block_list)
+    return net.cfg.FACT.ntoken <= nx.LOSS_MAXK
 
 
 def _ptr_rows(t, row0, ld):
@@ -142,10 +140,88 @@ class _LossFn(torch.autograd.Function):
         return (None,) + tuple(plan["grads"])
 
 
-def run(net, vb, label_list, hosts, compute_loss):
+class EarlyMatch:
+    """Stage 1, called by the LAST block's forward_batch as soon as its token logits and token->frame
+    attention exist (before its frame branch and the CLIP head run): ground truth from the host
+    labels, one upload, ONE fx_match_cost launch for every video and an asynchronous read-back of
+    the costs, so the host's Hungarian overlaps the rest of the forward on the device."""
+
+    def __init__(self, net, hosts):
+        self.net, self.hosts = net, hosts
+        self.done = False
+
+    def __call__(self, vb, a_cl, a2f_at, seg=None):
+        net, cfg = self.net, self.net.cfg
+        lib = nx.load()
+        nvid, T, Q = vb.nvid, vb.T, vb.Q
+        C1 = net.num_classes + 1
+        dev = a_cl.device
+        gts, labs = [], []
+        for lh, ev in self.hosts:
+            if ev is not None:
+                ev.synchronize()
+            lab = lh.numpy() if torch.is_tensor(lh) else np.asarray(lh)
+            labs.append(lab)
+            gts.append(gt_segments(lab))
+        G = [len(g[0]) for g in gts]
+        Gmax = max(G)
+        pk = _Pack()
+        gt_off = [(pk.array(g[0], np.int32), pk.array(g[1], np.int32), pk.array(g[2], np.int32)) for g in gts]
+        lab_off = [pk.array(lab, np.int32) for lab in labs]
+        cw = class_weights(net.mcriterion, C1)
+        cw_off = pk.array(cw, np.float32)
+        va_off, va = pk.structs(nx.VideoAttn, nvid)
+        base = pk.alloc(dev)
+        for v in range(nvid):
+            a = va[v]
+            a.Q, a.C1, a.T, a.G = Q, C1, T, G[v]
+            a.clogit, a.ldc = _ptr_rows(a_cl, v * Q, C1), C1
+            if seg is not None:
+                s_off, local = seg
+                a.attn, a.lda = a2f_at.data_ptr() + 4 * Q * s_off[v], Q
+                a.seg_id = local[v][0].data_ptr()
+            else:
+                a.attn, a.lda = a2f_at.data_ptr() + 4 * Q * T * v, Q
+            a.gs, a.ge, a.gl = (base + o for o in gt_off[v])
+            a.pred_off = v * T
+        pk.send()
+        self.cost_host = None
+        if cfg.Loss.match != "seq":
+            cost = torch.empty(nvid * Q * Gmax, dtype=torch.float32, device=dev)
+            nx.check(lib.fx_match_cost(ctypes.addressof(va), base + va_off, nvid, float(cfg.Loss.pc),
+                                       float(cfg.Loss.a2fc), Gmax, nx.ptr(cost), nx.stream()), "fx_match_cost")
+            self.cost_host = torch.empty(cost.shape, dtype=torch.float32, pin_memory=True)
+            self.cost_host.copy_(cost, non_blocking=True)
+            self.cost_ready = torch.cuda.Event()
+            self.cost_ready.record()
+            self.cost_dev = cost
+        self.__dict__.update(labs=labs, gts=gts, G=G, Gmax=Gmax, gt_off=gt_off, lab_off=lab_off, cw=cw,
+                             cw_off=cw_off, pk=pk, base=base)
+        self.done = True
+
+    def matches(self, Q):
+        """Hungarian / one-to-many / sequential matching per video (loss.py:108-193) on the host."""
+        kind = self.net.cfg.Loss.match
+        cost = None
+        if self.cost_host is not None:
+            self.cost_ready.synchronize()
+            cost = self.cost_host.numpy().reshape(len(self.G), Q, self.Gmax)
+        out = []
+        for v, Gv in enumerate(self.G):
+            if kind == "seq":
+                assert Q >= Gv, (Q, Gv)
+                ai = si = np.arange(Gv)
+            else:
+                c = cost[v, :, :Gv].astype(np.float64)
+                ai, si = linear_sum_assignment(c) if kind == "o2o" else one_to_many_match(c, self.gts[v][2])
+            out.append((np.asarray(ai, dtype=np.int64), np.asarray(si, dtype=np.int64)))
+        return out
+
+
+def run(net, vb, compute_loss, early=None):
     """Predictions (and with compute_loss the batch loss + per-video loss values) of the lockstep
-    batch whose block outputs forward_batch left in ``blk._bt``.  Returns what _forward_videos
-    returns: save_list, or (loss, save_list)."""
+    batch whose block outputs forward_batch left in ``blk._bt``; ``early`` is the EarlyMatch the last
+    block already ran.  Returns what _forward_videos returns: save_list, or (loss, save_list)."""
     from .blocks import FACT_CLIP, InputBlock, UpdateBlockTDU
     lib = nx.load()
     cfg = net.cfg
@@ -160,68 +236,38 @@ def run(net, vb, label_list, hosts, compute_loss):
     text = getattr(net, "text_embeddings", None) if clip else None
     proj = getattr(net, "_proj", None) if clip else None
     use_clip = text is not None and proj is not None
-
-    # ------------------------------------------------------------------ labels -> ground truth (host)
-    gts, labs = [], []
-    if compute_loss:
-        for v, (lh, ev) in enumerate(hosts):
-            if ev is not None:
-                ev.synchronize()
-            lab = lh.numpy() if torch.is_tensor(lh) else np.asarray(lh)
-            labs.append(lab)
-            gts.append(gt_segments(lab))
-    G = [len(g[0]) for g in gts]
-    Gmax = max(G) if G else 1
-    match_kind = cfg.Loss.match
-
-    # ------------------------------------------------------------------ stage 1: preds + costs
     flog = fxf.matmul_nt(proj.detach(), text, alpha=1.0 / cfg.CLIP.temp) if use_clip else last["f_cl"]
-    tdu_last = "S" in last
-    pk = _Pack()
-    gt_off = [(pk.array(g[0], np.int32), pk.array(g[1], np.int32), pk.array(g[2], np.int32)) for g in gts]
-    lab_off = [pk.array(lab, np.int32) for lab in labs]
-    cw = class_weights(mc, C1)
-    cw_off = pk.array(cw, np.float32)
-    va_off, va = pk.structs(nx.VideoAttn, nvid)
-    base = pk.alloc(dev)
-    for v in range(nvid):
-        a = va[v]
-        a.Q, a.C1, a.T, a.G = Q, C1, T, (G[v] if compute_loss else 0)
-        a.clogit, a.ldc = _ptr_rows(last["a_cl"], v * Q, C1), C1
-        if tdu_last:
-            a.attn, a.lda = last["a2f_at"].data_ptr() + 4 * Q * last["s_off"][v], Q
-            a.seg_id = last["local"][v][0].data_ptr()
-        else:
-            a.attn, a.lda = last["a2f_at"].data_ptr() + 4 * Q * T * v, Q
-        a.flogit, a.ldf = _ptr_rows(flog, v * T, C), C
-        if compute_loss:
-            a.gs, a.ge, a.gl = (base + o for o in gt_off[v])
-        a.pred_off = v * T
-    pk.send()
-    need_cost = compute_loss and match_kind != "seq"
-    res = torch.empty(nvid * T + (nvid * Q * Gmax if need_cost else 0), dtype=torch.int32, device=dev)
-    nx.check(lib.fx_eval_pred(ctypes.addressof(va), base + va_off, nvid, float(cfg.FACT.mwt), nx.ptr(res),
-                              nx.stream()), "fx_eval_pred")
-    if need_cost:
-        cost_d = res[nvid * T:].view(torch.float32)
-        nx.check(lib.fx_match_cost(ctypes.addressof(va), base + va_off, nvid, float(cfg.Loss.pc), float(cfg.Loss.a2fc),
-                                   Gmax, nx.ptr(cost_d), nx.stream()), "fx_match_cost")
-    host = res.cpu().numpy()
-    save_list = [{"pred": host[v * T:(v + 1) * T].astype(np.int64)} for v in range(nvid)]
-    if not compute_loss:
-        return save_list
-    cost = host[nvid * T:].view(np.float32).reshape(nvid, Q, Gmax) if need_cost else None
 
-    # ------------------------------------------------------------------ Hungarian (host, per video)
-    matches = []
-    for v in range(nvid):
-        if match_kind == "seq":
-            assert Q >= G[v], (Q, G[v])
-            ai = si = np.arange(G[v])
-        else:
-            c = cost[v, :, :G[v]].astype(np.float64)
-            ai, si = linear_sum_assignment(c) if match_kind == "o2o" else one_to_many_match(c, gts[v][2])
-        matches.append((np.asarray(ai, dtype=np.int64), np.asarray(si, dtype=np.int64)))
+    def eval_structs(pk):
+        off, va = pk.structs(nx.VideoAttn, nvid)
+        for v in range(nvid):
+            a = va[v]
+            a.Q, a.C1, a.T = Q, C1, T
+            a.clogit, a.ldc = _ptr_rows(last["a_cl"], v * Q, C1), C1
+            if "S" in last:
+                a.attn, a.lda = last["a2f_at"].data_ptr() + 4 * Q * last["s_off"][v], Q
+                a.seg_id = last["local"][v][0].data_ptr()
+            else:
+                a.attn, a.lda = last["a2f_at"].data_ptr() + 4 * Q * T * v, Q
+            a.flogit, a.ldf = _ptr_rows(flog, v * T, C), C
+            a.pred_off = v * T
+        return off, va
+
+    pred = torch.empty(nvid * T, dtype=torch.int32, device=dev)
+    if not compute_loss:
+        pk = _Pack()
+        va_off, va = eval_structs(pk)
+        base = pk.alloc(dev)
+        pk.send()
+        nx.check(lib.fx_eval_pred(ctypes.addressof(va), base + va_off, nvid, float(cfg.FACT.mwt), nx.ptr(pred),
+                                  nx.stream()), "fx_eval_pred")
+        host = pred.cpu().numpy()
+        return [{"pred": host[v * T:(v + 1) * T].astype(np.int64)} for v in range(nvid)]
+
+    assert early is not None and early.done, "the last block did not run the early matching stage"
+    matches = early.matches(Q)
+    labs, gts, G, gt_off, lab_off = early.labs, early.gts, early.G, early.gt_off, early.lab_off
+    cw, cw_off, base = early.cw, early.cw_off, early.base
 
     # ------------------------------------------------------------------ stage 2: the term table
     sw_coef = float(cfg.Loss.sw)
@@ -254,6 +300,7 @@ def run(net, vb, label_list, hosts, compute_loss):
         y_con.append(y)
 
     pk2 = _Pack()
+    va_off, va = eval_structs(pk2)
     tgt_off, sw_list = [], []
     for v in range(nvid):
         ai, si = matches[v]
@@ -336,6 +383,7 @@ def run(net, vb, label_list, hosts, compute_loss):
         Cs = text_seen.shape[0]
         Dc = text_seen.shape[1]
         sims = torch.empty(2, nvid * T, Cs, device=dev)
+        ncolz = Cs + 1 + 4 * nx.LOSS_NB * Cs
         gp = grad_of(proj)
         if not all(con_on):
             gp.zero_()
@@ -346,7 +394,7 @@ def run(net, vb, label_list, hosts, compute_loss):
                             dx=_ptr_rows(sims[1], v * T, Cs), dsr=Cs, dsc=1, y=("p2", ycon_off[v]),
                             emb=_ptr_rows(proj, v * T, Dc), ld_emb=Dc, text=text_seen.data_ptr(), D=Dc,
                             inv_temp=1.0 / float(cfg.CLIP.temp), demb=_ptr_rows(gp, v * T, Dc), ld_demb=Dc,
-                            c_ce=0.5), T, Cs, Cs + 1)
+                            c_ce=0.5), T, Cs, ncolz)
 
     # coefficient matrix: out = [batch loss, per video (loss, fact, contrastive, block values...)]
     nterms = len(specs)
@@ -388,16 +436,18 @@ def run(net, vb, label_list, hosts, compute_loss):
                 setattr(t, name, val)
         t.lse, t.lse2, t.colz = (sbase + 4 * o for o in offs)
     pk2.send()
+    nx.check(lib.fx_eval_pred(ctypes.addressof(va), base2 + va_off, nvid, float(cfg.FACT.mwt), nx.ptr(pred),
+                              nx.stream()), "fx_eval_pred")
     ws = torch.empty(max(lib.fx_loss_terms_workspace_floats(nterms), 1), device=dev, dtype=torch.float32)
     plan = dict(terms_host=terms, terms_dev=base2 + t_off, nterms=nterms, coef_dev=base2 + coef_off, nout=nout,
-                ws=ws, grads=grads, keep=(pk, pk2, scr, sims, res, flog, text_seen))
+                ws=ws, grads=grads, keep=(early, pk2, scr, sims, flog, text_seen))
     out = _LossFn.apply(plan, *inputs)
 
     # the reference's side channels: last video's per-block losses, fact / contrastive terms
     # (blocks.py:905-910: a video without a contrastive term reports the attributes an earlier
     # video -- or an earlier call -- left behind, as the reference's hasattr checks do)
     prev = None
-    if hasattr(net, "fact_loss") and hasattr(net, "contrastive_loss"):
+    if not all(con_on) and hasattr(net, "fact_loss") and hasattr(net, "contrastive_loss"):
         prev = (float(net.fact_loss), float(net.contrastive_loss))
     o = 1 + (nvid - 1) * per
     net.loss_list = [out[o + 3 + k] for k in range(nb)]
@@ -405,7 +455,15 @@ def run(net, vb, label_list, hosts, compute_loss):
         if con_on[v]:
             o = 1 + v * per
             net.fact_loss, net.contrastive_loss = out[o + 1], out[o + 2]
-    vals = out.detach().cpu().tolist()
+    # one synchronisation for the predictions and every loss value
+    out_h = torch.empty(out.shape, dtype=torch.float32, pin_memory=True)
+    pred_h = torch.empty(pred.shape, dtype=torch.int32, pin_memory=True)
+    out_h.copy_(out.detach(), non_blocking=True)
+    pred_h.copy_(pred, non_blocking=True)
+    torch.cuda.current_stream().synchronize()
+    vals = out_h.tolist()
+    ph = pred_h.numpy()
+    save_list = [{"pred": ph[v * T:(v + 1) * T].astype(np.int64)} for v in range(nvid)]
     for v in range(nvid):
         o = 1 + v * per
         d = {"loss": vals[o]}

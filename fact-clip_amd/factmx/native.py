@@ -66,6 +66,7 @@ class DecoderGrads(ctypes.Structure):
 
 
 LOSS_MAXK = 64
+LOSS_NB = 128          # FX_LOSS_NB: row blocks per loss term
 TERM_CLASS, TERM_ATTN, TERM_INFONCE = 0, 1, 2
 
 

@@ -486,11 +486,13 @@ int fx_attn_loss_bwd(const float* L, long long sr, long long sc, int R, int Q, i
  *   FX_TERM_INFONCE x (R x C) <- emb . text^T * inv_temp (one GEMM), y class per
  *                   frame (-1 = held out), c_ce * (row CE mean + per-class column
  *                   log-softmax mean); backward writes demb.
- * Scratch per term: lse (R), lse2 (R + K or C), colz (K or C + 1) floats.
+ * Scratch per term: lse (R), lse2 (R + K or C), colz (K, or C + 1 + 4 * FX_LOSS_NB * C for
+ * InfoNCE: counts, valid frames, per-row-block column partials) floats.
  * bwd: gout (nout) upstream gradient of out; every term's dx (and demb) written whole.
  * ---------------------------------------------------------------------- */
 enum { FX_TERM_CLASS = 0, FX_TERM_ATTN = 1, FX_TERM_INFONCE = 2 };
 #define FX_LOSS_MAXK 64
+#define FX_LOSS_NB 128          /* row blocks per term */
 
 typedef struct fx_loss_term {
   int kind, slot, R, C;

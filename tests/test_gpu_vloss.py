@@ -79,6 +79,7 @@ def test_fused_loss_equals_per_video_tiny(name, monkeypatch):
 
 
 def test_fused_loss_background_weights_and_o2m(monkeypatch):
+    label = _tiny("tiny_clip")[4]
     net, cfg, meta, feats, label = _tiny("tiny_clip", bg_ids=(int(label[0]),))
     cfg.Loss.bgw = 0.3
     seqs, labs = _two_videos(meta, feats, label, seed=5)

@@ -1,15 +1,16 @@
 """Diagnostic: idle gaps between kernels in a rocprofv3 kernel trace (last step of a bench run).
 
-python tools/gaps.py <kernel_trace.csv> [steps]
+python tools/gaps.py <kernel_trace.csv> [steps] [marker]
+(marker: a kernel launched once per step, default adam_kernel; combine_kernel without Adam)
 """
 import csv
 import sys
 
 
-def main(path, steps=1):
+def main(path, steps=1, marker="adam_kernel"):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     # the last `steps` steps: cut at the Adam kernel (end of every step)
-    ends = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
+    ends = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
     a = ends[-1 - steps] + 1
     b = ends[-1] + 1
     seq = rows[a:b]
@@ -26,4 +27,4 @@ def main(path, steps=1):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 1)
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 1, sys.argv[3] if len(sys.argv) > 3 else "adam_kernel")
