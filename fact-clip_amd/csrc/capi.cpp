@@ -4,6 +4,8 @@
 // orchestrated here in C++ so one Python call launches the whole sequence on
 // the caller's stream; kernels live in gemm_f32.hip, rowops.hip, segments.hip.
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <cmath>
 #include <cstring>
 #include <mutex>
@@ -183,13 +185,42 @@ long long dwdb_ws(int M, int K, int N) { return split_ws(N, K + 1, M); }
 
 namespace {
 
+// ---- side stream for overlapping independent GEMMs (one per device, created on first use) ----
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t to_side[3] = {};
+  hipEvent_t layer_done[4] = {};
+  hipEvent_t join = nullptr;
+};
+
+SideStream* side_stream() {
+  static std::mutex mu;
+  static std::map<int, SideStream*> pool;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = pool.find(dev);
+  if (it != pool.end()) return it->second;
+  SideStream* ss = new SideStream();
+  bool ok = hipStreamCreateWithFlags(&ss->s, hipStreamNonBlocking) == hipSuccess;
+  for (auto& e : ss->to_side) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+  for (auto& e : ss->layer_done) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&ss->join, hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    delete ss;   // (a partially created set leaks its handles; the caller falls back to one stream)
+    return nullptr;
+  }
+  pool[dev] = ss;
+  return ss;
+}
+
 // ---- MS-TCN layout of saved activations / workspace --------------------------------
 struct MstcnLayout {
   long long rowsF;
   // saved
   long long h, z, xh, rs, total_saved;
   // workspace
-  long long wf, wb, buf0, buf1, buf2, split, colsum, total_ws;
+  long long wf, wb, buf0, buf1, buf2, buf3, buf4, split, split2, colsum, total_ws;
 };
 
 MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
@@ -208,7 +239,9 @@ MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
   L.buf0 = L.wb + NL * wsz;
   L.buf1 = L.buf0 + L.rowsF;
   L.buf2 = L.buf1 + L.rowsF;
-  L.split = L.buf2 + L.rowsF;
+  L.buf3 = L.buf2 + L.rowsF;                 // backward: third dH buffer, second dZ buffer (side stream)
+  L.buf4 = L.buf3 + L.rowsF;
+  L.split = L.buf4 + L.rowsF;
   long long sp = 0;
   sp = std::max(sp, split_ws(p->F, 3 * p->F + 1, rows));      // conv dW (+ bias column)
   sp = std::max(sp, dwdb_ws(rows, p->F, p->F));               // pointwise dW
@@ -217,7 +250,8 @@ MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
   sp = std::max(sp, split_ws(rows, p->F, p->cout));           // dH_L
   if (p->in_map) sp = std::max(sp, split_ws(rows, p->cin, p->F));
   sp = std::max(sp, layernorm_bwd_ws_floats(rows, p->F));
-  L.colsum = L.split + sp;
+  L.split2 = L.split + sp;                   // split-K partials of the main stream's GEMMs
+  L.colsum = L.split2 + sp;
   long long cs = colsum_workspace_floats(rows, std::max(std::max(p->F, p->cout), p->cin));
   L.total_ws = L.colsum + cs;
   return L;
@@ -382,34 +416,67 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   hipStream_t s = (hipStream_t)stream;
   const int rows = T * nvid;
   const int F = p->F;
+  const int NL = p->num_layers;
   const MstcnLayout L = mstcn_layout(p, rows);
   float* ws = workspace;
   FX_TRY(pack_conv_weights(p, ws, L, s));
-  float* spl = ws + L.split;
+  float* spl = ws + L.split;     // split-K partials of the weight-gradient GEMMs (side stream)
+  float* spm = ws + L.split2;    // ... of the main stream's GEMMs / LN backward
   WsBound wb(spl, L.colsum - L.split);
-  float* dH = ws + L.buf0;   // gradient w.r.t. the current layer output
-  float* dU = ws + L.buf1;   // gradient at the residual sum (pre-LN)
-  float* dZ = ws + L.buf2;   // gradient at the conv output (pre-ReLU)
+  // Weight-gradient GEMMs (dW_out, per layer dW_pw and the dilated-conv dW, dW_in) depend on the
+  // input-gradient chain but nothing in the chain depends on them: they run on a side stream,
+  // overlapping the chain's GEMMs (each alone leaves the matrix pipes ~45 % idle in its prologue,
+  // barriers and epilogue).  Without LayerNorm the chain's buffers rotate (dH over 3, dZ over 2)
+  // so the side stream reads a layer's gU / dZ while the main stream computes the next layer;
+  // a main-stream write waits for the side stream's layer that last read that buffer.
+  SideStream* ss = p->layernorm ? nullptr : side_stream();
+  hipStream_t sd = ss ? ss->s : s;
+  auto fork = [&](int e) -> int {   // side stream waits for the main stream's work so far
+    if (!ss) return FX_OK;
+    FX_CHECK_HIP(hipEventRecord(ss->to_side[e], s));
+    FX_CHECK_HIP(hipStreamWaitEvent(sd, ss->to_side[e], 0));
+    return FX_OK;
+  };
+  auto side_done = [&](int i) -> int {
+    if (!ss) return FX_OK;
+    FX_CHECK_HIP(hipEventRecord(ss->layer_done[i & 3], sd));
+    return FX_OK;
+  };
+  auto wait_side = [&](int i) -> int {   // main waits until the side stream finished layer i
+    if (!ss || i >= NL) return FX_OK;
+    FX_CHECK_HIP(hipStreamWaitEvent(s, ss->layer_done[i & 3], 0));
+    return FX_OK;
+  };
+  float* Hb[3] = {ws + L.buf0, ws + L.buf1, ws + L.buf3};
+  float* Zb[2] = {ws + L.buf2, ws + L.buf4};
+  float* dU = ws + L.buf1;   // LN path (single stream): gradient at the residual sum (pre-LN)
   // weight/bias gradients ACCUMULATE (+=) into g->* (caller zeroes them once per step);
   // every bias gradient rides in its weight-gradient GEMM (virtual ones column).
-  // output map
-  const float* hL = saved + L.h + p->num_layers * L.rowsF;
-  FX_TRY(linear_dwdb(dy, lddy, hL, F, rows, F, p->cout, g->w_out, g->b_out, 1, spl, s));
-  FX_TRY(linear_dx(dy, lddy, p->w_out, rows, F, p->cout, dH, F, 0, nullptr, 0, spl, s));
-  for (int i = p->num_layers - 1; i >= 0; --i) {
+  const float* hL = saved + L.h + NL * L.rowsF;
+  FX_TRY(fork(0));
+  FX_TRY(linear_dwdb(dy, lddy, hL, F, rows, F, p->cout, g->w_out, g->b_out, 1, spl, sd));
+  float* dH = Hb[0];
+  FX_TRY(linear_dx(dy, lddy, p->w_out, rows, F, p->cout, dH, F, 0, nullptr, 0, spm, s));
+  for (int i = NL - 1; i >= 0; --i) {
+    const int step = NL - 1 - i;
     const float* hi = saved + L.h + i * L.rowsF;
     const float* zi = saved + L.z + i * L.rowsF;
     const float* gU = dH;
     if (p->layernorm) {
       FX_TRY(launch_layernorm_bwd(dH, F, nullptr, 0, saved + L.xh + i * L.rowsF, F, p->ln_w[i],
                                   saved + L.rs + (long long)i * rows, rows, F, 0, dU, F, g->ln_w[i], g->ln_b[i],
-                                  spl, s));
+                                  spm, s));
       gU = dU;
     }
-    // pointwise: dW_pw = dU^T z, db_pw = colsum(dU), dZ = (dU . W_pw) * (z > 0)
-    FX_TRY(linear_dwdb(gU, F, zi, F, rows, F, F, g->w_pw[i], g->b_pw[i], 1, spl, s));
-    FX_TRY(linear_dx(gU, F, p->w_pw[i], rows, F, F, dZ, F, 0, zi, F, spl, s));
-    // conv: dW (tap-major columns stored straight into (F,F,3)) + db (ones column), dH_i = dU + conv^T(dZ)
+    // pointwise: dW_pw = dU^T z, db_pw = colsum(dU) (side), dZ = (dU . W_pw) * (z > 0) (main)
+    FX_TRY(fork(1));
+    FX_TRY(linear_dwdb(gU, F, zi, F, rows, F, F, g->w_pw[i], g->b_pw[i], 1, spl, sd));
+    float* dZ = ss ? Zb[step & 1] : Zb[0];
+    FX_TRY(wait_side(i + 2));   // dZ buffer last read by layer i + 2's conv dW
+    FX_TRY(linear_dx(gU, F, p->w_pw[i], rows, F, F, dZ, F, 0, zi, F, spm, s));
+    // conv: dW (tap-major columns stored straight into (F,F,3)) + db (ones column) (side),
+    // dH_i = dU + conv^T(dZ) (main)
+    FX_TRY(fork(2));
     {
       fx_operand b = conv_operand(hi, F, F, layer_dilation(p, i), 1, T, true);
       b.ones_col = 3 * F + 1;
@@ -419,10 +486,17 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
       d.beta = 1.f;
       d.split_k = pick_split(F, 3 * F + 1, rows);
       d.workspace = spl;
-      FX_TRY(launch_gemm(d, s));
+      FX_TRY(launch_gemm(d, sd));
     }
+    FX_TRY(side_done(i));
     {
-      float* dHn = (gU == dH) ? dU : dH;  // write into the buffer not holding gU
+      float* dHn;
+      if (p->layernorm) {
+        dHn = (gU == dH) ? dU : dH;   // (LN: single stream) write into the buffer not holding gU
+      } else {
+        dHn = Hb[(step + 1) % 3];
+        FX_TRY(wait_side(i + 2));     // that buffer was gU of layer i + 2
+      }
       fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dZ, F, F, layer_dilation(p, i), -1, T, false),
                                  op_rows(ws + L.wb + (long long)i * 3 * F * F, 3 * F), dHn, F);
       d.resid = gU;
@@ -430,15 +504,26 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
       prof_begin(0, s);
       FX_TRY(launch_gemm(d, s));
       prof_end(0, s, 2.0 * rows * F * 3.0 * F, 4.0 * (3.0 * rows * F + 3.0 * F * F));
-      if (dHn != dH) std::swap(dH, dU);  // dH now holds dH_i
+      if (p->layernorm) {
+        if (dHn != dH) std::swap(dH, dU);   // dH now holds dH_i
+      } else {
+        dH = dHn;
+      }
     }
   }
   if (p->in_map) {
-    if (g->w_in) FX_TRY(linear_dwdb(dH, F, x, ldx, rows, p->cin, F, g->w_in, g->b_in, 1, spl, s));
-    if (dx) FX_TRY(linear_dx(dH, F, p->w_in, rows, p->cin, F, dx, lddx, 0, nullptr, 0, spl, s));
+    if (g->w_in) {
+      FX_TRY(fork(0));
+      FX_TRY(linear_dwdb(dH, F, x, ldx, rows, p->cin, F, g->w_in, g->b_in, 1, spl, sd));
+    }
+    if (dx) FX_TRY(linear_dx(dH, F, p->w_in, rows, p->cin, F, dx, lddx, 0, nullptr, 0, spm, s));
   } else if (dx) {
     FX_CHECK_HIP(hipMemcpy2DAsync(dx, lddx * sizeof(float), dH, F * sizeof(float), F * sizeof(float), rows,
                                   hipMemcpyDeviceToDevice, s));
+  }
+  if (ss) {   // join: everything the side stream did is ordered before the caller's later work
+    FX_CHECK_HIP(hipEventRecord(ss->join, sd));
+    FX_CHECK_HIP(hipStreamWaitEvent(s, ss->join, 0));
   }
   return FX_OK;
 }

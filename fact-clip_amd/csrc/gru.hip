@@ -126,6 +126,17 @@ __global__ __launch_bounds__(GT) void gru_fwd_kernel(GruArgs args) {
   }
   const float bias = act ? a.bhh[row] : 0.f;
   for (int k = tid; k < 256; k += GT) h[k] = 0.f;
+  // the input projections of step s are loaded during step s-1 (their latency hides behind the
+  // exchange instead of opening every step)
+  const bool own = tid < U && u0 + tid < Hh;
+  const int uo = u0 + (own ? tid : 0);
+  float pr = 0.f, pz = 0.f, pn = 0.f;
+  if (own && S > 0) {
+    const float* gg = a.gi + (long long)(r0 + (a.reverse ? S - 1 : 0)) * a.ldgi;
+    pr = gg[uo];
+    pz = gg[Hh + uo];
+    pn = gg[2 * Hh + uo];
+  }
   __syncthreads();
   for (int s = 0; s < S; ++s) {
     const int t = r0 + (a.reverse ? S - 1 - s : s);
@@ -136,12 +147,18 @@ __global__ __launch_bounds__(GT) void gru_fwd_kernel(GruArgs args) {
     acc += __shfl_xor(acc, 2, 64);
     if (act && c == 0) gh[o] = acc + bias;
     __syncthreads();
-    if (tid < U && u0 + tid < Hh) {
-      const int u = u0 + tid;
-      const float* gg = a.gi + (long long)t * a.ldgi;
-      const float r = sigm(gg[u] + gh[tid]);
-      const float z = sigm(gg[Hh + u] + gh[U + tid]);
-      const float n = tanhf(gg[2 * Hh + u] + r * gh[2 * U + tid]);
+    if (own) {
+      const int u = uo;
+      const float gr = pr, gz = pz, gn = pn;
+      if (s + 1 < S) {
+        const float* gg = a.gi + (long long)(r0 + (a.reverse ? S - 2 - s : s + 1)) * a.ldgi;
+        pr = gg[u];
+        pz = gg[Hh + u];
+        pn = gg[2 * Hh + u];
+      }
+      const float r = sigm(gr + gh[tid]);
+      const float z = sigm(gz + gh[U + tid]);
+      const float n = tanhf(gn + r * gh[2 * U + tid]);
       const float hp = h[u];
       const float hn = (1.f - z) * n + z * hp;
       a.out[(long long)t * a.ldo + u] = hn;
@@ -204,16 +221,29 @@ __global__ __launch_bounds__(GT) void gru_bwd_kernel(GruBwdArgs args) {
     w[r] = (act && row < H3) ? a.whh[(long long)row * Hh + u0 + i] : 0.f;
   }
   if (tid < MAXU) dh[tid] = 0.f;
+  // step s's saved gates, h_{t-1} and output gradient are loaded during step s-1
+  const bool own = tid < U && u0 + tid < Hh;
+  const int uo = u0 + (own ? tid : 0);
+  float nr = 0.f, nz = 0.f, nn = 0.f, ng = 0.f, nh = 0.f, nd = 0.f;
+  auto fetch = [&](int t) {
+    const float* gs = a.gates + (long long)t * 4 * Hh;
+    nr = gs[uo];
+    nz = gs[Hh + uo];
+    nn = gs[2 * Hh + uo];
+    ng = gs[3 * Hh + uo];
+    nh = a.hprev[(long long)t * Hh + uo];
+    nd = a.dout[(long long)t * a.lddo + uo];
+  };
+  if (own && S > 0) fetch(r0 + (a.reverse ? 0 : S - 1));
   __syncthreads();
   for (int s = 0; s < S; ++s) {
     const int t = r0 + (a.reverse ? s : S - 1 - s);   // reverse of the forward visiting order
     unsigned long long* slot = gran + (long long)(s & 1) * H3;
-    if (tid < U && u0 + tid < Hh) {
-      const int u = u0 + tid;
-      const float* gs = a.gates + (long long)t * 4 * Hh;
-      const float r = gs[u], z = gs[Hh + u], n = gs[2 * Hh + u], ghn = gs[3 * Hh + u];
-      const float hp = a.hprev[(long long)t * Hh + u];
-      const float d = a.dout[(long long)t * a.lddo + u] + dh[tid];
+    if (own) {
+      const int u = uo;
+      const float r = nr, z = nz, n = nn, ghn = ng, hp = nh, dcur = nd;
+      if (s + 1 < S) fetch(r0 + (a.reverse ? s + 1 : S - 2 - s));
+      const float d = dcur + dh[tid];
       const float dnp = d * (1.f - z) * (1.f - n * n);
       const float dzp = d * (hp - n) * z * (1.f - z);
       const float drp = dnp * ghn * r * (1.f - r);
