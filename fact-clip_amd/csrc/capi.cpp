@@ -298,6 +298,12 @@ extern "C" {
 int fx_version(void) { return FX_ABI_VERSION; }
 const char* fx_last_error(void) { return g_last_error.c_str(); }
 
+int fx_dropout(const float* x, long long ldx, int rows, int cols, long long idx_ld, long long idx_col0, float p,
+               unsigned long long seed, float* y, long long ldy, void* stream) {
+  FX_REQUIRE(x && y && rows >= 0 && cols >= 0, "dropout: bad arguments");
+  return launch_dropout(x, ldx, rows, cols, idx_ld, idx_col0, p, seed, y, ldy, (hipStream_t)stream);
+}
+
 long long fx_struct_size(int which) {
   switch (which) {
     case 0: return (long long)sizeof(fx_gemm_desc);
@@ -401,6 +407,8 @@ int fx_mstcn_fwd(const fx_mstcn_params* p, const float* x, long long ldx, int T,
     e.bias = p->b_pw[i];
     e.resid = hi;
     e.ld_resid = F;
+    e.drop_p = p->dropout;   // h' = h + dropout(z . Wpw^T + b)   (basic.py:160)
+    e.drop_seed = fx_drop_subseed(p->seed, i);
     FX_TRY(launch_gemm(e, s));
     if (p->layernorm)
       FX_TRY(launch_layernorm_fwd(u, F, nullptr, 0, p->ln_w[i], p->ln_b[i], 1e-5f, rows, F, 0, hn, F, nullptr,
@@ -429,7 +437,9 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   // barriers and epilogue).  Without LayerNorm the chain's buffers rotate (dH over 3, dZ over 2)
   // so the side stream reads a layer's gU / dZ while the main stream computes the next layer;
   // a main-stream write waits for the side stream's layer that last read that buffer.
-  SideStream* ss = p->layernorm ? nullptr : side_stream();
+  FX_REQUIRE(p->dropout >= 0.f && p->dropout < 1.f, "mstcn: dropout must be in [0, 1)");
+  const bool drop = p->dropout > 0.f;
+  SideStream* ss = (p->layernorm || drop) ? nullptr : side_stream();
   hipStream_t sd = ss ? ss->s : s;
   auto fork = [&](int e) -> int {   // side stream waits for the main stream's work so far
     if (!ss) return FX_OK;
@@ -468,12 +478,19 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
                                   spm, s));
       gU = dU;
     }
-    // pointwise: dW_pw = dU^T z, db_pw = colsum(dU) (side), dZ = (dU . W_pw) * (z > 0) (main)
+    // the 1x1 branch saw dropout: its gradient is gU masked the same way (the residual keeps gU)
+    const float* gB = gU;
+    if (drop) {
+      float* gm = ws + L.buf4;   // (single-stream path: dZ stays in buf2, buf4 is free)
+      FX_TRY(launch_dropout(gU, F, rows, F, F, 0, p->dropout, fx_drop_subseed(p->seed, i), gm, F, s));
+      gB = gm;
+    }
+    // pointwise: dW_pw = dB^T z, db_pw = colsum(dB) (side), dZ = (dB . W_pw) * (z > 0) (main)
     FX_TRY(fork(1));
-    FX_TRY(linear_dwdb(gU, F, zi, F, rows, F, F, g->w_pw[i], g->b_pw[i], 1, spl, sd));
+    FX_TRY(linear_dwdb(gB, F, zi, F, rows, F, F, g->w_pw[i], g->b_pw[i], 1, spl, sd));
     float* dZ = ss ? Zb[step & 1] : Zb[0];
     FX_TRY(wait_side(i + 2));   // dZ buffer last read by layer i + 2's conv dW
-    FX_TRY(linear_dx(gU, F, p->w_pw[i], rows, F, F, dZ, F, 0, zi, F, spm, s));
+    FX_TRY(linear_dx(gB, F, p->w_pw[i], rows, F, F, dZ, F, 0, zi, F, spm, s));
     // conv: dW (tap-major columns stored straight into (F,F,3)) + db (ones column) (side),
     // dH_i = dU + conv^T(dZ) (main)
     FX_TRY(fork(2));
@@ -590,7 +607,7 @@ int fx_add(const float* a, long long lda, const float* b, long long ldb, int row
 // ---------------------------------------------------------------- MHA core
 long long fx_mha_core_workspace_floats(int Lq, int Lk, int E, int nhead) {
   const int hd = E / std::max(nhead, 1);
-  long long ws = (long long)nhead * Lq * Lk;  // dS
+  long long ws = 2LL * nhead * Lq * Lk;   // dropped probabilities, dS
   long long sp = 0;
   sp = std::max(sp, split_ws(Lq, hd, Lk, nhead));
   sp = std::max(sp, split_ws(Lk, hd, Lq, nhead));
@@ -599,13 +616,16 @@ long long fx_mha_core_workspace_floats(int Lq, int Lk, int E, int nhead) {
 }
 
 int fx_mha_core_fwd(const float* q, long long ldq, const float* k, long long ldk, const float* v, long long ldv,
-                    int Lq, int Lk, int E, int nhead, float* probs, float* o, long long ldo, float* workspace,
-                    void* stream) {
+                    int Lq, int Lk, int E, int nhead, float drop_p, unsigned long long seed, float* probs, float* o,
+                    long long ldo, float* workspace, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   FX_REQUIRE(nhead > 0 && E % nhead == 0, "mha: E must be divisible by nhead");
+  FX_REQUIRE(drop_p == 0.f || workspace, "mha: dropout needs the workspace");
   const int hd = E / nhead;
   const float scale = 1.0f / std::sqrt((float)hd);
-  WsBound wb(workspace, workspace ? fx_mha_core_workspace_floats(Lq, Lk, E, nhead) : 0);
+  const long long nLL = (long long)nhead * Lq * Lk;
+  float* spl = workspace ? workspace + 2 * nLL : nullptr;
+  WsBound wb(spl, workspace ? fx_mha_core_workspace_floats(Lq, Lk, E, nhead) - 2 * nLL : 0);
   // S_h = (Q_h K_h^T) * scale  -> probs buffer, then row softmax in place
   fx_gemm_desc d = gemm_desc(Lq, Lk, hd, op_rows(q, ldq), op_rows(k, ldk), probs, Lk);
   d.batch = nhead;
@@ -615,35 +635,50 @@ int fx_mha_core_fwd(const float* q, long long ldq, const float* k, long long ldk
   d.alpha = scale;
   FX_TRY(launch_gemm(d, s));
   FX_TRY(launch_softmax_rows(probs, Lk, nhead * Lq, Lk, 1.f, probs, Lk, s));
+  // attention dropout (nn.MultiheadAttention dropout=attn_dropout): O = dropout(P) V, mask index
+  // (h Lq + i) Lk + j
+  const float* pv = probs;
+  if (drop_p > 0.f) {
+    FX_TRY(launch_dropout(probs, Lk, nhead * Lq, Lk, Lk, 0, drop_p, seed, workspace, Lk, s));
+    pv = workspace;
+  }
   // O_h = P_h V_h
-  fx_gemm_desc e = gemm_desc(Lq, hd, Lk, op_rows(probs, Lk), op_cols(v, ldv), o, ldo);
+  fx_gemm_desc e = gemm_desc(Lq, hd, Lk, op_rows(pv, Lk), op_cols(v, ldv), o, ldo);
   e.batch = nhead;
   e.a.batch_stride = (long long)Lq * Lk;
   e.b.batch_stride = hd;
   e.c_batch_stride = hd;
   e.split_k = workspace ? pick_split(Lq, hd, Lk, nhead) : 1;
-  e.workspace = workspace;
+  e.workspace = spl;
   return launch_gemm(e, s);
 }
 
 int fx_mha_core_bwd(const float* q, long long ldq, const float* k, long long ldk, const float* v, long long ldv,
                     const float* probs, const float* dout, long long lddo, int Lq, int Lk, int E, int nhead,
-                    float* dq, long long lddq, float* dk, long long lddk, float* dv, long long lddv,
-                    float* workspace, void* stream) {
+                    float drop_p, unsigned long long seed, float* dq, long long lddq, float* dk, long long lddk,
+                    float* dv, long long lddv, float* workspace, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   FX_REQUIRE(nhead > 0 && E % nhead == 0, "mha: E must be divisible by nhead");
   const int hd = E / nhead;
   const float scale = 1.0f / std::sqrt((float)hd);
-  float* dS = workspace;
-  float* spl = workspace + (long long)nhead * Lq * Lk;
-  WsBound wb(spl, fx_mha_core_workspace_floats(Lq, Lk, E, nhead) - (long long)nhead * Lq * Lk);
-  // dP_h = dO_h V_h^T
+  const long long nLL = (long long)nhead * Lq * Lk;
+  float* pd = workspace;
+  float* dS = workspace + nLL;
+  float* spl = workspace + 2 * nLL;
+  WsBound wb(spl, fx_mha_core_workspace_floats(Lq, Lk, E, nhead) - 2 * nLL);
+  // dP_h = dO_h V_h^T   (through the dropout: the same mask and scale)
   fx_gemm_desc d = gemm_desc(Lq, Lk, hd, op_rows(dout, lddo), op_rows(v, ldv), dS, Lk);
   d.batch = nhead;
   d.a.batch_stride = hd;
   d.b.batch_stride = hd;
   d.c_batch_stride = (long long)Lq * Lk;
   FX_TRY(launch_gemm(d, s));
+  const float* pv = probs;
+  if (drop_p > 0.f) {
+    FX_TRY(launch_dropout(dS, Lk, nhead * Lq, Lk, Lk, 0, drop_p, seed, dS, Lk, s));
+    FX_TRY(launch_dropout(probs, Lk, nhead * Lq, Lk, Lk, 0, drop_p, seed, pd, Lk, s));
+    pv = pd;
+  }
   // dS = softmax_bwd(P, dP)
   FX_TRY(launch_softmax_rows_bwd(probs, Lk, dS, Lk, nullptr, 0, nhead * Lq, Lk, 1.f, dS, Lk, s));
   // dQ_h = scale * dS_h K_h
@@ -670,9 +705,9 @@ int fx_mha_core_bwd(const float* q, long long ldq, const float* k, long long ldk
     e.workspace = spl;
     FX_TRY(launch_gemm(e, s));
   }
-  // dV_h = P_h^T dO_h
+  // dV_h = dropout(P_h)^T dO_h
   if (dv) {
-    fx_gemm_desc e = gemm_desc(Lk, hd, Lq, op_cols(probs, Lk), op_cols(dout, lddo), dv, lddv);
+    fx_gemm_desc e = gemm_desc(Lk, hd, Lq, op_cols(pv, Lk), op_cols(dout, lddo), dv, lddv);
     e.batch = nhead;
     e.a.batch_stride = (long long)Lq * Lk;
     e.b.batch_stride = hd;
@@ -774,21 +809,36 @@ long long fx_x2y_saved_floats(int Nx, int xdim, int Ny, int ydim, int Hd) {
   return x2y_layout(Nx, xdim, Ny, ydim, Hd).total;
 }
 
-long long fx_x2y_workspace_floats(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim, int nvid,
-                                  const int* x_off, const int* y_off) {
-  const VidRows v = vid_rows(Nx, Ny, nvid, x_off, y_off);
+// [dcat][dL][dxv][dxk][dyq][dXk][dYq][split-K][colsum][catd: dropped cat[Y, feat] (dropout only)]
+static long long x2y_ws_nocatd(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim, const VidRows& v) {
   long long w = (long long)Ny * (ydim + Hd) + v.a[v.n] + 2LL * Nx * Hd + (long long)Ny * Hd +
                 (long long)Nx * xdim + (long long)Ny * ydim;
   return w + x2y_split_ws(v, xdim, ydim, Hd, outdim) + colsum_workspace_floats(std::max(Nx, Ny), std::max(Hd, outdim));
+}
+
+long long fx_x2y_workspace_floats(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim, int nvid,
+                                  const int* x_off, const int* y_off) {
+  const VidRows v = vid_rows(Nx, Ny, nvid, x_off, y_off);
+  return x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, v) + (long long)Ny * (ydim + Hd);
+}
+
+// catd = dropout(cat[Y, feat]) (basic.py:382), mask index r (ydim + Hd) + c
+static int x2y_drop_cat(const float* Y, long long ldy, const float* feat, int Ny, int ydim, int Hd, float p,
+                        unsigned long long seed, float* catd, hipStream_t s) {
+  const int cw = ydim + Hd;
+  FX_TRY(launch_dropout(Y, ldy, Ny, ydim, cw, 0, p, seed, catd, cw, s));
+  return launch_dropout(feat, Hd, Ny, Hd, cw, ydim, p, seed, catd + ydim, cw, s);
 }
 
 int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpos, long long ldxp, int xpos_cols,
                const float* Y, long long ldy, int Ny, int ydim, const float* Ypos, long long ldyp, int ypos_cols,
                const float* wk, const float* bk, const float* wv, const float* bv, const float* wq, const float* bq,
                const float* wy, const float* by, int Hd, int outdim, int nvid, const int* x_off, const int* y_off,
-               float* out, long long ldo, float* logit, float* attn, float* saved, float* workspace, void* stream) {
+               float drop_p, unsigned long long seed, float* out, long long ldo, float* logit, float* attn,
+               float* saved, float* workspace, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const VidRows V = vid_rows(Nx, Ny, nvid, x_off, y_off);
+  FX_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "x2y: dropout must be in [0, 1)");
   FX_REQUIRE(V.x[V.n] == Nx && V.y[V.n] == Ny, "x2y: offsets must end at Nx / Ny");
   const X2YLayout L = x2y_layout(Nx, xdim, Ny, ydim, Hd);
   WsBound wb(workspace, x2y_split_ws(V, xdim, ydim, Hd, outdim));
@@ -841,11 +891,17 @@ int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpo
       FX_TRY(launch_gemm(d, s));
     }
   }
-  // Y_W(cat[Y, feat]) with the concatenation folded into the A-operand loader
+  // Y_W(cat[Y, feat]) with the concatenation folded into the A-operand loader; with dropout the
+  // dropped concatenation is materialised (training only)
   fx_operand a = op_rows(Y, ldy);
   a.ptr1 = feat;
   a.ld1 = Hd;
   a.k_split = ydim;
+  if (drop_p > 0.f) {
+    float* catd = workspace + x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, V);
+    FX_TRY(x2y_drop_cat(Y, ldy, feat, Ny, ydim, Hd, drop_p, seed, catd, s));
+    a = op_rows(catd, ydim + Hd);
+  }
   fx_gemm_desc d = gemm_desc(Ny, outdim, ydim + Hd, a, op_rows(wy, ydim + Hd), out, ldo);
   d.bias = by;
   return launch_gemm(d, s);
@@ -853,7 +909,8 @@ int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpo
 
 int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, const float* Y, long long ldy, int Ny,
                int ydim, int ypos_cols, const float* wk, const float* wv, const float* wq, const float* wy, int Hd,
-               int outdim, int nvid, const int* x_off, const int* y_off, const float* attn, const float* saved,
+               int outdim, int nvid, const int* x_off, const int* y_off, float drop_p, unsigned long long seed,
+               const float* attn, const float* saved,
                const float* dout, long long lddo, const float* dlogit, const float* dattn, float* dX, float* dXpos,
                float* dY, float* dYpos, float* dwk, float* dbk, float* dwv, float* dbv, float* dwq, float* dbq,
                float* dwy, float* dby, int has_xpos, int has_ypos, float* workspace, void* stream) {
@@ -880,10 +937,18 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
   float* spl = dYq + (long long)Ny * ydim;
   WsBound wb(spl, x2y_split_ws(V, xdim, ydim, Hd, outdim));
   const float scale = 1.0f / std::sqrt((float)Hd);
-  // Y_W: dcat = dout . Wy, dWy = dout^T [Y, feat], dby
+  // Y_W: dcat = dout . Wy, dWy = dout^T [Y, feat], dby  (dropout: the dropped concatenation and
+  // the same mask on dcat)
   FX_TRY(linear_dx(dout, lddo, wy, Ny, cw, outdim, dcat, cw, 0, nullptr, 0, spl, s));
-  FX_TRY(linear_dwdb(dout, lddo, Y, ldy, Ny, ydim, outdim, dwy, dby, 1, spl, s, cw));
-  FX_TRY(linear_dw(dout, lddo, feat, Hd, Ny, Hd, outdim, dwy + ydim, 1, spl, s, cw));
+  if (drop_p > 0.f) {
+    float* catd = workspace + x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, V);
+    FX_TRY(x2y_drop_cat(Y, ldy, feat, Ny, ydim, Hd, drop_p, seed, catd, s));
+    FX_TRY(linear_dwdb(dout, lddo, catd, cw, Ny, cw, outdim, dwy, dby, 1, spl, s, cw));
+    FX_TRY(launch_dropout(dcat, cw, Ny, cw, cw, 0, drop_p, seed, dcat, cw, s));
+  } else {
+    FX_TRY(linear_dwdb(dout, lddo, Y, ldy, Ny, ydim, outdim, dwy, dby, 1, spl, s, cw));
+    FX_TRY(linear_dw(dout, lddo, feat, Hd, Ny, Hd, outdim, dwy + ydim, 1, spl, s, cw));
+  }
   for (int v = 0; v < V.n; ++v) {
     const int nx = V.x[v + 1] - V.x[v], ny = V.y[v + 1] - V.y[v];
     if (nx == 0 || ny == 0) continue;

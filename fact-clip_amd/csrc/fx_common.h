@@ -69,6 +69,29 @@ int launch_colsum(const float* x, long long ld, int M, int N, float* out, int ac
 constexpr long long kArrivalCounters = 1 << 16;
 unsigned* arrival_counters(hipStream_t s);
 
+// ------------------------------------------------------------------------
+// Dropout mask (counter-based, regenerated in backward): element idx of a dropout site with seed
+// `seed` is kept iff fx_drop_bits(seed, idx) >= fx_drop_thresh(p); kept values are scaled by
+// 1 / (1 - p) as nn.Dropout does.  splitmix64 of (seed + (idx + 1) * golden ratio).
+__host__ __device__ inline unsigned fx_drop_bits(unsigned long long seed, unsigned long long idx) {
+  unsigned long long z = seed + (idx + 1ull) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (unsigned)(z >> 32);
+}
+inline unsigned fx_drop_thresh(float p) {
+  const double t = (double)p * 4294967296.0;
+  return t >= 4294967295.0 ? 4294967295u : (unsigned)t;
+}
+// seed of sub-site i of a site (MS-TCN layer i, ...)
+inline unsigned long long fx_drop_subseed(unsigned long long seed, int i) {
+  return seed + 0xD1B54A32D192ED03ull * (unsigned long long)(i + 1);
+}
+// y[r, c] = x[r, c] * keep(seed, r * idx_ld + idx_col0 + c) / (1 - p)   (y may alias x)
+int launch_dropout(const float* x, long long ldx, int rows, int cols, long long idx_ld, long long idx_col0, float p,
+                   unsigned long long seed, float* y, long long ldy, hipStream_t s);
+
 // event-based timing hooks around launches of one kernel class (bench roofline)
 void prof_begin(int kind, hipStream_t s);
 void prof_end(int kind, hipStream_t s, double flops, double bytes);

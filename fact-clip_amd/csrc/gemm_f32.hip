@@ -64,6 +64,9 @@ struct GemmDev {
   long long* stamps;
   unsigned* tile_cnt;   // split-K arrival counters (one per output tile), NULL -> separate reduce kernel
   int w8_stagger;       // wide8: waves 4-7 run the staggered stage schedule
+  unsigned drop_thr;    // dropout (fx_drop_bits >= drop_thr keeps); 0 = off
+  float drop_scale;
+  unsigned long long drop_seed;
 };
 
 // Diagnostic builds (-DFX_STAMPS) record s_memtime / s_memrealtime at fixed points of
@@ -331,6 +334,10 @@ __device__ __forceinline__ void epilogue_store(const GemmDev& g, int b, int m, i
   }
   if (g.bias) v += g.bias[n];
   if (g.relu == 2) v = fmaxf(v, 0.f);
+  if (g.drop_thr) {
+    const unsigned long long idx = ((unsigned long long)b * g.M + m) * g.N + n;
+    v = fx_drop_bits(g.drop_seed, idx) >= g.drop_thr ? v * g.drop_scale : 0.f;
+  }
   if (g.resid) v += g.resid[(long long)b * g.resid_bs + (long long)m * g.ld_resid + n];
   if (g.beta != 0.f) v += g.beta * (pre ? cold : *cp);
   if (g.gate && !(g.gate[(long long)m * g.ld_gate + n] > 0.f)) v = 0.f;
@@ -512,7 +519,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_f32_kernel(GemmDev g) {
     return;
   }
   if (col >= g.N) return;
-  if (!g.c_last && !g.c_tap_cin && !g.gate && g.beta == 0.f) {
+  if (!g.c_last && !g.c_tap_cin && !g.gate && g.beta == 0.f && !g.drop_thr) {
     // common forward epilogue: every read (bias, residual) is issued before the first store,
     // so the 16 loads overlap instead of queueing behind stores they might alias
     const float bv = g.bias ? g.bias[col] : 0.f;
@@ -654,7 +661,7 @@ __device__ __forceinline__ void wide_kloop(const Loader<AK, true>& la0, const Lo
 
 __device__ __forceinline__ void tile_epilogue(const GemmDev& g, int bidx, int rbase, int col, const f32x16& acc) {
   if (col >= g.N) return;
-  if (!g.c_last && !g.c_tap_cin && !g.gate && g.beta == 0.f) {
+  if (!g.c_last && !g.c_tap_cin && !g.gate && g.beta == 0.f && !g.drop_thr) {
     const float bv = g.bias ? g.bias[col] : 0.f;
     float res[16];
 #pragma unroll
@@ -1336,6 +1343,13 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
   g.c_tap_cin = d.c_tap_cin;
   g.c_last = d.c_last_col;
   g.stamps = d.dbg_stamps;
+  FX_REQUIRE(d.drop_p >= 0.f && d.drop_p < 1.f, "gemm: dropout p must be in [0, 1)");
+  FX_REQUIRE(d.drop_p == 0.f || (!d.c_last_col && !d.c_tap_cin && !d.gate && d.beta == 0.f &&
+                                 !(d.relu == 1 && d.resid)),
+             "gemm: dropout only on plain outputs (before the residual add)");
+  g.drop_thr = d.drop_p > 0.f ? std::max(fx_drop_thresh(d.drop_p), 1u) : 0u;
+  g.drop_scale = 1.f / (1.f - d.drop_p);
+  g.drop_seed = d.drop_seed;
   g.a_vec = operand_vec_ok(d.a);
   g.b_vec = operand_vec_ok(d.b);
   g.ws = d.workspace;

@@ -452,6 +452,29 @@ int launch_layernorm_bwd(const float* dy, long long lddy, const float* y, long l
   return FX_OK;
 }
 
+__global__ __launch_bounds__(256) void dropout_kernel(const float* x, long long ldx, int rows, int cols,
+                                                     long long idx_ld, long long idx_col0, unsigned thr, float scale,
+                                                     unsigned long long seed, float* y, long long ldy) {
+  const long long total = (long long)rows * cols;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int r = (int)(e / cols), c = (int)(e - (long long)r * cols);
+    const float v = x[(long long)r * ldx + c];
+    const bool keep = fx_drop_bits(seed, (unsigned long long)((long long)r * idx_ld + idx_col0 + c)) >= thr;
+    y[(long long)r * ldy + c] = keep ? v * scale : 0.f;
+  }
+}
+
+int launch_dropout(const float* x, long long ldx, int rows, int cols, long long idx_ld, long long idx_col0, float p,
+                   unsigned long long seed, float* y, long long ldy, hipStream_t s) {
+  FX_REQUIRE(p >= 0.f && p < 1.f, "dropout: p must be in [0, 1)");
+  if ((long long)rows * cols == 0) return FX_OK;
+  const int blocks = (int)std::min<long long>(cdiv((long long)rows * cols, 256), 4096);
+  hipLaunchKernelGGL(dropout_kernel, dim3(blocks), dim3(256), 0, s, x, ldx, rows, cols, idx_ld, idx_col0,
+                     p > 0.f ? std::max(fx_drop_thresh(p), 1u) : 0u, 1.f / (1.f - p), seed, y, ldy);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
 int launch_softmax_rows(const float* x, long long ldx, int rows, int cols, float scale, float* p, long long ldp,
                         hipStream_t s) {
   if (rows == 0 || cols == 0) return FX_OK;

@@ -265,11 +265,7 @@ __device__ void infonce_cols(const fx_loss_term& t, int b0, int b1, float* cp) {
         sx += x;
       }
     }
-    float* o = cp + ((long long)blockIdx.x * t.C + c) * 4;
-    o[0] = m;
-    o[1] = s;
-    o[2] = cnt;
-    o[3] = sx;
+    reinterpret_cast<float4*>(cp)[(long long)blockIdx.x * t.C + c] = make_float4(m, s, cnt, sx);
   }
 }
 
@@ -323,7 +319,7 @@ __global__ __launch_bounds__(VT) void terms_fwd_kernel(const fx_loss_term* terms
   else if (t.kind == FX_TERM_ATTN) attn_fwd(t, lane, gw, r0, r1, a, b);
   else {
     infonce_rows(t, lane, r0, r1, a, b);
-    infonce_cols(t, b0, b1, t.colz + t.C + 1);
+    infonce_cols(t, b0, b1, t.colz + ((t.C + 4) & ~3));
   }
   a = vsum(a);
   b = vsum(b);
@@ -368,9 +364,10 @@ __global__ __launch_bounds__(64) void combine_bwd_kernel(const float* gout, cons
 // x = sim (R frames x C classes), y = class per frame (-1: masked); the column partials of the row
 // blocks merge into the column lse (lse2), the class counts (colz, colz[C] = valid frames) and
 //   value = c_ce * ( v2t / n_valid + (1/C) sum_c -(sum_{y_t = c} sim[t, c] - count_c lse_c) / max(count_c, 1) )
-__global__ __launch_bounds__(VT) void terms_finish_kernel(const fx_loss_term* terms, const float* part, int nb,
+constexpr int FT = 1024;   // finish: one wave per InfoNCE column group
+__global__ __launch_bounds__(FT) void terms_finish_kernel(const fx_loss_term* terms, const float* part, int nb,
                                                           float* vals) {
-  __shared__ float red[VT / 64];
+  __shared__ float red[FT / 64];
   const int i = blockIdx.x;
   const fx_loss_term& t = terms[i];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -387,32 +384,42 @@ __global__ __launch_bounds__(VT) void terms_finish_kernel(const fx_loss_term* te
     if (threadIdx.x == 0) vals[i] = t.c_sm != 0.f ? t.c_ce * a + t.c_sm * b : t.c_ce * a;
     return;
   }
-  const float* cp = t.colz + t.C + 1;
+  if (wv == 0 && lane == 0) red[0] = a, red[1] = b;   // (slots reused below after a barrier)
+  __syncthreads();
+  a = red[0];
+  b = red[1];
+  __syncthreads();
+  // one wave per column, lanes over the row-block partials (float4 {max, sum exp, count, sum x})
+  const float4* cp = reinterpret_cast<const float4*>(t.colz + ((t.C + 4) & ~3));
   float t2v = 0.f;
-  for (int c = threadIdx.x; c < t.C; c += VT) {
-    float m = -INFINITY, cnt = 0.f, sx = 0.f;
-    for (int k = 0; k < nb; ++k) {
-      const float* o = cp + ((long long)k * t.C + c) * 4;
-      if (o[1] > 0.f) m = fmaxf(m, o[0]);
-      cnt += o[2];
-      sx += o[3];
+  for (int c = wv; c < t.C; c += FT / 64) {
+    float m = -INFINITY, cnt = 0.f, sx = 0.f, s = 0.f;
+    for (int k = lane; k < nb; k += 64) {
+      const float4 o = cp[(long long)k * t.C + c];
+      if (o.y > 0.f) {
+        const float mn = fmaxf(m, o.x);
+        s = s * __expf(m - mn) + o.y * __expf(o.x - mn);
+        m = mn;
+      }
+      cnt += o.z;
+      sx += o.w;
     }
-    float s = 0.f;
-    for (int k = 0; k < nb; ++k) {
-      const float* o = cp + ((long long)k * t.C + c) * 4;
-      if (o[1] > 0.f) s += o[1] * __expf(o[0] - m);
+    const float M = vmax(m);
+    s = vsum(m == -INFINITY ? 0.f : s * __expf(m - M));
+    cnt = vsum(cnt);
+    sx = vsum(sx);
+    const float l = M + __logf(s);
+    if (lane == 0) {
+      t.lse2[c] = l;
+      t.colz[c] = cnt;
+      t2v += cnt > 0.f ? -(sx - cnt * l) / cnt : 0.f;
     }
-    const float l = m + __logf(s);
-    t.lse2[c] = l;
-    t.colz[c] = cnt;
-    t2v += cnt > 0.f ? -(sx - cnt * l) / cnt : 0.f;
   }
-  t2v = vsum(t2v);
   if (lane == 0) red[wv] = t2v;
   __syncthreads();
   if (threadIdx.x == 0) {
     float tt = 0.f;
-    for (int k = 0; k < VT / 64; ++k) tt += red[k];
+    for (int k = 0; k < FT / 64; ++k) tt += red[k];
     t.colz[t.C] = b;
     vals[i] = b > 0.f ? t.c_ce * (a / b + tt / (float)t.C) : 0.f;
   }
@@ -618,7 +625,7 @@ int fx_loss_terms_fwd(const fx_loss_term* terms_host, const fx_loss_term* terms_
   }
   hipLaunchKernelGGL(terms_fwd_kernel, dim3(nb, nterms), dim3(VT), 0, s, terms_dev, part);
   FX_CHECK_HIP(hipGetLastError());
-  hipLaunchKernelGGL(terms_finish_kernel, dim3(nterms), dim3(VT), 0, s, terms_dev, part, nb, vals);
+  hipLaunchKernelGGL(terms_finish_kernel, dim3(nterms), dim3(FT), 0, s, terms_dev, part, nb, vals);
   FX_CHECK_HIP(hipGetLastError());
   hipLaunchKernelGGL(combine_kernel, dim3(nout), dim3(64), 0, s, vals, coef_dev, nterms, nout, out);
   FX_CHECK_HIP(hipGetLastError());

@@ -29,6 +29,24 @@ def _ws(n, device):
     return torch.empty(max(int(n), 1), device=device, dtype=_f32)
 
 
+def dropout_seed():
+    """Seed of one training dropout site, drawn from torch's default CPU generator (so
+    torch.manual_seed fixes the masks, as it fixes nn.Dropout's); the kernels derive every mask
+    element from it by a counter-based hash and regenerate it in backward."""
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+def dropout(x, p, seed):
+    """fx_dropout on a (rows, cols) tensor: x * keep / (1 - p) with the kernels' mask."""
+    lib = nx.load()
+    x2 = _2d(x).contiguous()
+    y = torch.empty_like(x2)
+    rows, cols = x2.shape
+    _check(lib.fx_dropout(nx.ptr(x2), cols, rows, cols, cols, 0, float(p), int(seed), nx.ptr(y), cols, nx.stream()),
+           "fx_dropout")
+    return y
+
+
 def _2d(t):
     """(N, 1, C) or (N, C) -> (N, C) view with unit column stride."""
     if t.dim() == 3:
@@ -302,7 +320,7 @@ class MHAFn(torch.autograd.Function):
     ``w_packed`` (3E, E) is the packed in_proj_weight (kdim == E) or None with wq/wk/wv given."""
 
     @staticmethod
-    def forward(ctx, q_in, k_in, v_in, w_packed, wq, wk, wv, b_in, wo, bo, nhead):
+    def forward(ctx, q_in, k_in, v_in, w_packed, wq, wk, wv, b_in, wo, bo, nhead, drop_p=0.0, seed=0):
         lib = nx.load()
         dev = q_in.device
         Lq, Lk = q_in.shape[0], k_in.shape[0]
@@ -315,10 +333,11 @@ class MHAFn(torch.autograd.Function):
         probs = _empty(nhead, Lq, Lk, device=dev)
         o = _empty(Lq, E, device=dev)
         ws = _ws(lib.fx_mha_core_workspace_floats(Lq, Lk, E, nhead), dev)
-        _check(lib.fx_mha_core_fwd(nx.ptr(q), E, nx.ptr(k), E, nx.ptr(v), E, Lq, Lk, E, nhead, nx.ptr(probs),
-                                   nx.ptr(o), E, nx.ptr(ws), nx.stream()), "fx_mha_core_fwd")
+        _check(lib.fx_mha_core_fwd(nx.ptr(q), E, nx.ptr(k), E, nx.ptr(v), E, Lq, Lk, E, nhead, float(drop_p),
+                                   int(seed), nx.ptr(probs), nx.ptr(o), E, nx.ptr(ws), nx.stream()), "fx_mha_core_fwd")
         out = lin_fwd(o, wo, bo)
         ctx.nhead = nhead
+        ctx.drop = (float(drop_p), int(seed))
         ctx.packed = w_packed is not None
         ctx.save_for_backward(q_in, k_in, v_in, w_packed, wq, wk, wv, b_in, wo, bo, q, k, v, probs, o)
         return out
@@ -341,8 +360,8 @@ class MHAFn(torch.autograd.Function):
         dv = _empty(Lk, E, device=dev)
         ws = _ws(lib.fx_mha_core_workspace_floats(Lq, Lk, E, nh), dev)
         _check(lib.fx_mha_core_bwd(nx.ptr(q), E, nx.ptr(k), E, nx.ptr(v), E, nx.ptr(probs), nx.ptr(d_o), E, Lq, Lk,
-                                   E, nh, nx.ptr(dq), E, nx.ptr(dk), E, nx.ptr(dv), E, nx.ptr(ws), nx.stream()),
-               "fx_mha_core_bwd")
+                                   E, nh, ctx.drop[0], ctx.drop[1], nx.ptr(dq), E, nx.ptr(dk), E, nx.ptr(dv), E,
+                                   nx.ptr(ws), nx.stream()), "fx_mha_core_bwd")
         dbin, dbin_ret = grad_target(b_in, nd[7])
         rets = [None, None, None, None]
         if ctx.packed:
@@ -356,17 +375,20 @@ class MHAFn(torch.autograd.Function):
         dq_in = lin_bwd(dq, q_in, wq, nd[0], tq, bq)
         dk_in = lin_bwd(dk, k_in, wk, nd[1], tk, bk)
         dv_in = lin_bwd(dv, v_in, wv, nd[2], tv, bv)
-        return (dq_in, dk_in, dv_in, rets[0], rets[1], rets[2], rets[3], dbin_ret, dwo_ret, dbo_ret, None)
+        return (dq_in, dk_in, dv_in, rets[0], rets[1], rets[2], rets[3], dbin_ret, dwo_ret, dbo_ret, None, None,
+                None)
 
 
 def mha(mod, query, key, value):
-    """Run an nn.MultiheadAttention module's parameters through MHAFn (dropout must be off)."""
+    """Run an nn.MultiheadAttention module's parameters through MHAFn; in training its dropout
+    (on the attention probabilities) uses the kernels' counter-based mask."""
     if mod._qkv_same_embed_dim:
         args = (mod.in_proj_weight, None, None, None)
     else:
         args = (None, mod.q_proj_weight, mod.k_proj_weight, mod.v_proj_weight)
+    p = float(mod.dropout) if mod.training else 0.0
     return MHAFn.apply(_2d(query), _2d(key), _2d(value), *args, mod.in_proj_bias, mod.out_proj.weight,
-                       mod.out_proj.bias, mod.num_heads)
+                       mod.out_proj.bias, mod.num_heads, p, dropout_seed() if p > 0 else 0)
 
 
 # ---------------------------------------------------------------------------
@@ -379,7 +401,7 @@ class X2YFn(torch.autograd.Function):
     each video's (ny_v, nx_v) block in video order."""
 
     @staticmethod
-    def forward(ctx, X, Y, Xpos, Ypos, rows, wk, bk, wv, bv, wq, bq, wy, by):
+    def forward(ctx, X, Y, Xpos, Ypos, rows, wk, bk, wv, bv, wq, bq, wy, by, drop_p=0.0, seed=0):
         lib = nx.load()
         dev = X.device
         Nx, xdim = X.shape
@@ -402,9 +424,11 @@ class X2YFn(torch.autograd.Function):
         _check(lib.fx_x2y_fwd(nx.ptr(X), nx.ld(X), Nx, xdim, nx.ptr(Xpos), nx.ld(Xpos), xpc,
                               nx.ptr(Y), nx.ld(Y), Ny, ydim, nx.ptr(Ypos), nx.ld(Ypos), ypc,
                               nx.ptr(wk), nx.ptr(bk), nx.ptr(wv), nx.ptr(bv), nx.ptr(wq), nx.ptr(bq),
-                              nx.ptr(wy), nx.ptr(by), Hd, outdim, nvid, xo, yo, nx.ptr(out), outdim, nx.ptr(logit),
-                              nx.ptr(attn), nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_x2y_fwd")
+                              nx.ptr(wy), nx.ptr(by), Hd, outdim, nvid, xo, yo, float(drop_p), int(seed),
+                              nx.ptr(out), outdim, nx.ptr(logit), nx.ptr(attn), nx.ptr(saved), nx.ptr(ws),
+                              nx.stream()), "fx_x2y_fwd")
         ctx.dims = (Nx, xdim, Ny, ydim, Hd, outdim, xpc, ypc)
+        ctx.drop = (float(drop_p), int(seed))
         ctx.rows = rows
         ctx.has_pos = (Xpos is not None, Ypos is not None)
         ctx.save_for_backward(X, Y, wk, bk, wv, bv, wq, bq, wy, by, attn, saved)
@@ -441,17 +465,19 @@ class X2YFn(torch.autograd.Function):
         bufs = [b if b is not None else torch.zeros_like(p) for b, p in zip(bufs, (wk, bk, wv, bv, wq, bq, wy, by))]
         ws = _ws(lib.fx_x2y_workspace_floats(Nx, xdim, Ny, ydim, Hd, outdim, nvid, xo, yo), dev)
         _check(lib.fx_x2y_bwd(nx.ptr(X), nx.ld(X), Nx, xdim, xpc, nx.ptr(Y), nx.ld(Y), Ny, ydim, ypc,
-                              nx.ptr(wk), nx.ptr(wv), nx.ptr(wq), nx.ptr(wy), Hd, outdim, nvid, xo, yo, nx.ptr(attn),
+                              nx.ptr(wk), nx.ptr(wv), nx.ptr(wq), nx.ptr(wy), Hd, outdim, nvid, xo, yo,
+                              ctx.drop[0], ctx.drop[1], nx.ptr(attn),
                               nx.ptr(saved), nx.ptr(dout), outdim, nx.ptr(dlogit), nx.ptr(dattn), nx.ptr(dX),
                               nx.ptr(dXp), nx.ptr(dY), nx.ptr(dYp), *[nx.ptr(t) for t in bufs], int(hx), int(hy),
                               nx.ptr(ws), nx.stream()), "fx_x2y_bwd")
-        return (dX, dY, dXp, dYp, None) + tuple(t[1] for t in tg)
+        return (dX, dY, dXp, dYp, None) + tuple(t[1] for t in tg) + (None, None)
 
 
 def x2y(mod, X, Y, Xpos, Ypos, rows=None):
+    p = float(mod.dropout.p) if mod.training else 0.0
     return X2YFn.apply(_2d(X), _2d(Y), None if Xpos is None else _2d(Xpos), None if Ypos is None else _2d(Ypos),
                        rows, mod.X_K.weight, mod.X_K.bias, mod.X_V.weight, mod.X_V.bias, mod.Y_Q.weight,
-                       mod.Y_Q.bias, mod.Y_W.weight, mod.Y_W.bias)
+                       mod.Y_Q.bias, mod.Y_W.weight, mod.Y_W.bias, p, dropout_seed() if p > 0 else 0)
 
 
 # ---------------------------------------------------------------------------
@@ -463,11 +489,12 @@ def _ptr_array(ts):
 
 
 class MSTCNFn(torch.autograd.Function):
-    """Whole ``MSTCN.forward`` (basic.py:200-220) in one C call (eval-mode dropout)."""
+    """Whole ``MSTCN.forward`` (basic.py:200-220) in one C call; training dropout on every layer's
+    1x1 branch (basic.py:160) with the kernels' counter-based mask (seed in meta)."""
 
     @staticmethod
     def _unpack(meta, params):
-        T, nvid, cin, F, cout, nl, ln, in_map, d0, dfac = meta
+        T, nvid, cin, F, cout, nl, ln, in_map, d0, dfac = meta[:10]
         it = iter(params)
         w_in = b_in = None
         if in_map:
@@ -483,7 +510,7 @@ class MSTCNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, meta, *params):
         lib = nx.load()
-        T, nvid, cin, F, cout, nl, ln, in_map, d0, dfac = meta
+        T, nvid, cin, F, cout, nl, ln, in_map, d0, dfac, drop_p, seed = meta
         w_in, b_in, layers, w_out, b_out = MSTCNFn._unpack(meta, params)
         keep = []
         prm = nx.MstcnParams()
@@ -495,6 +522,7 @@ class MSTCNFn(torch.autograd.Function):
             keep.append(arr)
             setattr(prm, field, ctypes.cast(arr, ctypes.c_void_p))
         prm.w_out, prm.b_out = nx.ptr(w_out), nx.ptr(b_out)
+        prm.dropout, prm.seed = float(drop_p), int(seed)
         rows = x.shape[0]
         dev = x.device
         y = _empty(rows, cout, device=dev)
@@ -512,7 +540,7 @@ class MSTCNFn(torch.autograd.Function):
     def backward(ctx, dy):
         lib = nx.load()
         x, saved, *params = ctx.saved_tensors
-        T, nvid, cin, F, cout, nl, ln, in_map, d0, dfac = ctx.meta
+        T, nvid, cin, F, cout, nl, ln, in_map, d0, dfac = ctx.meta[:10]
         dev = x.device
         dy = dy.contiguous()
         tg = [grad_target(p) for p in params]
@@ -545,8 +573,9 @@ def mstcn(mod, x, T, nvid=1):
             params += [lyr.norm.weight, lyr.norm.bias]
     params += [mod.conv_out.weight, mod.conv_out.bias]
     ln = mod.layers[0].norm is not None if len(mod.layers) else False
+    p = float(mod.dropout_rate) if (mod.training and mod.dropout_rate) else 0.0
     meta = (T, nvid, x2.shape[1], mod.hid_dim, mod.out_dim, mod.num_layers, bool(ln), bool(mod.in_map),
-            mod.dilation0, mod.dilation_factor)
+            mod.dilation0, mod.dilation_factor, p, dropout_seed() if p > 0 else 0)
     return MSTCNFn.apply(x2, meta, *params)
 
 

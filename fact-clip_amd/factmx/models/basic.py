@@ -6,10 +6,11 @@ forwards run through ``factmx.functional`` (hand-written HIP kernels behind the
 libfactmx C ABI).  Tensors at the module boundary keep the reference's
 sequence-first (N, 1, C) layout; internally everything is (N, C) row-major.
 
-Dropout: the fused kernels run eval-mode dropout.  Dropout on materialised
-tensors (residual branches, FFN, projection head, channel masking) is applied
-with torch's GPU dropout; a non-zero dropout *inside* a fused kernel (MS-TCN
-layer output, attention probabilities, X2Y concat) raises in training mode.
+Dropout: inside the fused kernels (MS-TCN 1x1 branch, attention probabilities,
+X2Y concat) training dropout uses a counter-based hash mask (functional.dropout_seed
+draws the site seed from torch's CPU generator; the backward regenerates the mask).
+Dropout on materialised tensors (decoder residual branches and FFN on the per-layer
+path, projection head, channel masking) is torch's GPU dropout.
 """
 import copy
 import math
@@ -25,12 +26,6 @@ from .. import functional as fxf
 
 def _as3d(t2d):
     return t2d.unsqueeze(1)
-
-
-def _no_fused_dropout(module, p, where):
-    if module.training and p > 0:
-        raise NotImplementedError(f"dropout={p} inside the fused {where} kernel is not implemented; "
-                                  "use dropout 0 (parity/benchmark configs do)")
 
 
 def _dropout(x, p, training):
@@ -133,12 +128,11 @@ class DilatedResidualLayer(nn.Module):
     def forward(self, x, mask=None):
         """x: (B=1, C, T) as in the reference."""
         assert mask is None
-        _no_fused_dropout(self, self.dropout_rate, "dilated residual layer")
         T = x.shape[-1]
         h = x[0].t().contiguous()
         z = fxf.conv3(h, self.conv_dilated.weight, self.conv_dilated.bias, self.dilation, T)
         z = torch.relu(z)
-        y = fxf.linear(z, self.conv_1x1.weight, self.conv_1x1.bias) + h
+        y = _dropout(fxf.linear(z, self.conv_1x1.weight, self.conv_1x1.bias), self.dropout.p, self.training) + h
         if self.norm is not None:
             y = fxf.layer_norm(y, self.norm.weight, self.norm.bias, self.norm.eps)
         return y.t().unsqueeze(0)
@@ -172,7 +166,6 @@ class MSTCN(nn.Module):
     def forward(self, x, mask=None):
         """x: (T, 1, C) -> (T, 1, out_dim)."""
         assert mask is None
-        _no_fused_dropout(self, self.dropout_rate, "MS-TCN")
         out = fxf.mstcn(self, x, T=x.shape[0])
         self.output = _as3d(out)
         return self.output
@@ -265,7 +258,6 @@ class X2Y_map(nn.Module):
 
     def forward(self, X_feature, Y_feature, X_pos=None, Y_pos=None, X_pad_mask=None, Y_pad_mask=None):
         assert X_pad_mask is None and Y_pad_mask is None
-        _no_fused_dropout(self, self.dropout.p, "X2Y concat")
         xp = X_pos if (X_pos is not None and self.kq_pos) else None
         yp = Y_pos if (Y_pos is not None and self.kq_pos) else None
         out, logit, attn = fxf.x2y(self, X_feature, Y_feature, xp, yp)
@@ -301,7 +293,6 @@ class SALayer(nn.Module):
 
     def forward(self, tgt, key, value, query_pos: Optional[Tensor] = None, key_pos: Optional[Tensor] = None,
                 value_pos: Optional[Tensor] = None):
-        _no_fused_dropout(self, self.multihead_attn.dropout, "attention")
         query = add_positional_encoding(tgt, query_pos)
         key = add_positional_encoding(key, key_pos)
         if self.use_vpos:
@@ -346,7 +337,6 @@ class SCALayer(nn.Module):
         return self.string
 
     def forward(self, tgt, memory, pos: Optional[Tensor] = None, query_pos: Optional[Tensor] = None):
-        _no_fused_dropout(self, self.self_attn.dropout, "attention")
         q = add_positional_encoding(tgt, query_pos)
         t2 = fxf.mha(self.self_attn, q, q, q if self.sa_value_w_pos else tgt)
         t = fxf.layer_norm(_dropout(t2, self.dropout1.p, self.training), self.norm1.weight, self.norm1.bias,

@@ -331,7 +331,7 @@ def run(net, vb, compute_loss, early=None):
         offs = []
         for n in (n_lse, n_lse2, n_colz):
             offs.append(scratch[0])
-            scratch[0] += max(n, 1)
+            scratch[0] += (max(n, 1) + 3) & ~3        # 16-byte aligned slots
         specs.append((k, v, f, offs))
 
     for k, blk in enumerate(blocks):
@@ -383,7 +383,7 @@ def run(net, vb, compute_loss, early=None):
         Cs = text_seen.shape[0]
         Dc = text_seen.shape[1]
         sims = torch.empty(2, nvid * T, Cs, device=dev)
-        ncolz = Cs + 1 + 4 * nx.LOSS_NB * Cs
+        ncolz = ((Cs + 4) & ~3) + 4 * nx.LOSS_NB * Cs
         gp = grad_of(proj)
         if not all(con_on):
             gp.zero_()
@@ -423,13 +423,8 @@ def run(net, vb, compute_loss, early=None):
         t = terms[i]
         t.slot = i
         for name, val in f.items():
-            if name in ("ka", "kgs", "kge"):
-                arr = getattr(t, name)
-                for j, x in enumerate(val):
-                    arr[j] = int(x)
-            elif name == "ksw":
-                for j, x in enumerate(val):
-                    t.ksw[j] = float(x)
+            if name in ("ka", "kgs", "kge", "ksw"):
+                getattr(t, name)[:len(val)] = val.tolist() if isinstance(val, np.ndarray) else val
             elif isinstance(val, tuple):
                 setattr(t, name, bases[val[0]] + val[1])
             elif val is not None:

@@ -12,13 +12,14 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FACTMX_LIB", os.path.join(_HERE, "_lib", "libfactmx.so"))
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 P = ctypes.c_void_p
 I = ctypes.c_int
 L = ctypes.c_longlong
 F = ctypes.c_float
 D = ctypes.c_double
+U = ctypes.c_ulonglong
 
 
 class FactmxNativeError(RuntimeError):
@@ -35,13 +36,14 @@ class GemmDesc(ctypes.Structure):
     _fields_ = [("M", I), ("N", I), ("K", I), ("batch", I), ("a", Operand), ("b", Operand), ("c", P), ("ldc", L),
                 ("c_batch_stride", L), ("alpha", F), ("beta", F), ("bias", P), ("resid", P), ("ld_resid", L),
                 ("resid_batch_stride", L), ("gate", P), ("ld_gate", L), ("relu", I), ("c_tap_cin", I),
-                ("split_k", I), ("workspace", P), ("c_last_col", P), ("dbg_stamps", P)]
+                ("split_k", I), ("workspace", P), ("c_last_col", P), ("dbg_stamps", P), ("drop_p", F),
+                ("drop_seed", U)]
 
 
 class MstcnParams(ctypes.Structure):
     _fields_ = [("cin", I), ("F", I), ("cout", I), ("num_layers", I), ("layernorm", I), ("in_map", I),
                 ("dil0", I), ("dil_factor", I), ("w_in", P), ("b_in", P), ("w_dil", P), ("b_dil", P), ("w_pw", P), ("b_pw", P),
-                ("ln_w", P), ("ln_b", P), ("w_out", P), ("b_out", P)]
+                ("ln_w", P), ("ln_b", P), ("w_out", P), ("b_out", P), ("dropout", F), ("seed", U)]
 
 
 class MstcnGrads(ctypes.Structure):
@@ -98,10 +100,10 @@ SIGNATURES = {
     "fx_linear_bwd": (I, [P, L, P, L, P, L, P, L, I, I, I, P, L, P, L, P, I, I, P, P]),
     "fx_x2y_saved_floats": (L, [I, I, I, I, I]),
     "fx_x2y_workspace_floats": (L, [I, I, I, I, I, I, I, P, P]),
-    "fx_x2y_fwd": (I, [P, L, I, I, P, L, I, P, L, I, I, P, L, I, P, P, P, P, P, P, P, P, I, I, I, P, P, P, L, P, P,
-                       P, P, P]),
-    "fx_x2y_bwd": (I, [P, L, I, I, I, P, L, I, I, I, P, P, P, P, I, I, I, P, P, P, P, P, L, P, P, P, P, P, P, P, P,
-                       P, P, P, P, P, P, I, I, P, P]),
+    "fx_x2y_fwd": (I, [P, L, I, I, P, L, I, P, L, I, I, P, L, I, P, P, P, P, P, P, P, P, I, I, I, P, P, F, U, P, L, P,
+                       P, P, P, P]),
+    "fx_x2y_bwd": (I, [P, L, I, I, I, P, L, I, I, I, P, P, P, P, I, I, I, P, P, F, U, P, P, P, L, P, P, P, P, P, P,
+                       P, P, P, P, P, P, P, P, I, I, P, P]),
     "fx_decoder_saved_floats": (L, [ctypes.POINTER(DecoderParams), I, I, I, I, I]),
     "fx_decoder_workspace_floats": (L, [ctypes.POINTER(DecoderParams), I, I, I, I, I]),
     "fx_decoder_fwd": (I, [ctypes.POINTER(DecoderParams), P, L, I, P, L, P, L, I, I, P, L, P, L, P, P, P]),
@@ -126,8 +128,9 @@ SIGNATURES = {
     "fx_mha_t_fwd": (I, [P, L, P, L, P, L, I, I, I, I, I, F, P, L, P, P, P]),
     "fx_mha_t_bwd": (I, [P, L, P, L, P, L, P, L, P, L, P, I, I, I, I, I, F, P, L, P, L, P, L, P, P]),
     "fx_mha_core_workspace_floats": (L, [I, I, I, I]),
-    "fx_mha_core_fwd": (I, [P, L, P, L, P, L, I, I, I, I, P, P, L, P, P]),
-    "fx_mha_core_bwd": (I, [P, L, P, L, P, L, P, P, L, I, I, I, I, P, L, P, L, P, L, P, P]),
+    "fx_mha_core_fwd": (I, [P, L, P, L, P, L, I, I, I, I, F, U, P, P, L, P, P]),
+    "fx_mha_core_bwd": (I, [P, L, P, L, P, L, P, P, L, I, I, I, I, F, U, P, L, P, L, P, L, P, P]),
+    "fx_dropout": (I, [P, L, I, I, L, L, F, U, P, L, P]),
     "fx_gru_saved_floats": (L, [I, I]),
     "fx_gru_workspace_floats": (L, [I, I, I, I]),
     "fx_gru_bidir_fwd": (I, [P, L, I, I, P, I, I, P, P, P, P, P, P, P, P, P, L, P, P, P]),

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FX_ABI_VERSION 8
+#define FX_ABI_VERSION 9
 
 enum {
   FX_OK = 0,
@@ -105,6 +105,8 @@ typedef struct fx_gemm_desc {
   float* workspace;
   float* c_last_col;          /* != NULL: output column N-1 goes to c_last_col[m] (bias grad) */
   long long* dbg_stamps;      /* diagnostic builds (-DFX_STAMPS) only: per-block timestamps */
+  float drop_p;               /* > 0: dropout on (alpha acc + bias [relu]) before the residual add */
+  unsigned long long drop_seed; /* mask of output (b, m, n): fx_dropout index (b M + m) N + n */
 } fx_gemm_desc;
 
 int fx_gemm(const fx_gemm_desc* desc, void* stream);
@@ -148,6 +150,8 @@ int fx_linear_bwd(const float* dy, long long lddy, const float* x, long long ldx
  * Positional tensors cover the first *pos_cols channels (nullable).
  * bwd: dout, optional direct dlogit / dattn (Ny, Nx) -> dX, dXpos, dY, dYpos
  *   (nullable) and every weight/bias gradient (accumulated, all required).
+ * drop_p > 0 (training): Y_W(dropout(cat[Y, attn . xv])) (basic.py:382), fx_dropout mask
+ * index r (ydim + Hd) + c over the concatenated row, regenerated by the backward.
  * ---------------------------------------------------------------------- */
 long long fx_x2y_saved_floats(int Nx, int xdim, int Ny, int ydim, int Hd);
 long long fx_x2y_workspace_floats(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim, int nvid,
@@ -156,12 +160,14 @@ int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpo
                int xpos_cols, const float* Y, long long ldy, int Ny, int ydim, const float* Ypos,
                long long ldyp, int ypos_cols, const float* wk, const float* bk, const float* wv,
                const float* bv, const float* wq, const float* bq, const float* wy, const float* by,
-               int Hd, int outdim, int nvid, const int* x_off, const int* y_off, float* out,
-               long long ldo, float* logit, float* attn, float* saved, float* workspace, void* stream);
+               int Hd, int outdim, int nvid, const int* x_off, const int* y_off, float drop_p,
+               unsigned long long seed, float* out, long long ldo, float* logit, float* attn,
+               float* saved, float* workspace, void* stream);
 int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, const float* Y,
                long long ldy, int Ny, int ydim, int ypos_cols, const float* wk, const float* wv,
                const float* wq, const float* wy, int Hd, int outdim, int nvid, const int* x_off,
-               const int* y_off, const float* attn, const float* saved, const float* dout,
+               const int* y_off, float drop_p, unsigned long long seed, const float* attn,
+               const float* saved, const float* dout,
                long long lddo, const float* dlogit, const float* dattn, float* dX, float* dXpos,
                float* dY, float* dYpos, float* dwk, float* dbk, float* dwv, float* dbv, float* dwq,
                float* dbq, float* dwy, float* dby, int has_xpos, int has_ypos, float* workspace,
@@ -250,6 +256,9 @@ typedef struct fx_mstcn_params {
   const float* const* w_pw; const float* const* b_pw;
   const float* const* ln_w; const float* const* ln_b;
   const float* w_out; const float* b_out;
+  float dropout;              /* training dropout on each layer's 1x1 branch (basic.py:160); 0 = eval */
+  unsigned long long seed;    /* layer i mask: fx_dropout seed fx_drop_subseed(seed, i) = seed +
+                                 0xD1B54A32D192ED03 (i + 1), index row * F + channel */
 } fx_mstcn_params;
 
 typedef struct fx_mstcn_grads {
@@ -318,17 +327,20 @@ int fx_l2norm_bwd(const float* y, long long ldy, const float* norm, const float*
  * Multi-head attention core (nn.MultiheadAttention math as called at
  * basic.py:442, 500, 513): per head h, P_h = softmax(Q_h K_h^T / sqrt(hd)),
  * O_h = P_h V_h.  q (Lq, E) ldq, k/v (Lk, E) ldk/ldv, o (Lq, E) ldo.
- * probs (nhead, Lq, Lk) saved for backward.  bwd gives dq, dk, dv
- * (accumulate flags per output).
+ * probs (nhead, Lq, Lk) saved for backward.  bwd gives dq, dk, dv.
+ * drop_p > 0: attention dropout on P (fx_dropout mask, index (h Lq + i) Lk + j), regenerated
+ * by the backward.
  * ---------------------------------------------------------------------- */
 long long fx_mha_core_workspace_floats(int Lq, int Lk, int E, int nhead);
 int fx_mha_core_fwd(const float* q, long long ldq, const float* k, long long ldk, const float* v,
-                    long long ldv, int Lq, int Lk, int E, int nhead, float* probs, float* o,
-                    long long ldo, float* workspace, void* stream);
+                    long long ldv, int Lq, int Lk, int E, int nhead, float drop_p,
+                    unsigned long long seed, float* probs, float* o, long long ldo, float* workspace,
+                    void* stream);
 int fx_mha_core_bwd(const float* q, long long ldq, const float* k, long long ldk, const float* v,
                     long long ldv, const float* probs, const float* dout, long long lddo, int Lq,
-                    int Lk, int E, int nhead, float* dq, long long lddq, float* dk, long long lddk,
-                    float* dv, long long lddv, float* workspace, void* stream);
+                    int Lk, int E, int nhead, float drop_p, unsigned long long seed, float* dq,
+                    long long lddq, float* dk, long long lddk, float* dv, long long lddv,
+                    float* workspace, void* stream);
 
 /* ------------------------------------------------------------------------
  * Multi-head attention of a few queries over T frames, ONE fused launch for every video and
@@ -403,6 +415,16 @@ int fx_gru_bidir_bwd(const float* x, long long ldx, int S, int nseq, const int* 
                      float* dx, long long lddx, float* dw_ih_f, float* dw_hh_f, float* db_ih_f,
                      float* db_hh_f, float* dw_ih_r, float* dw_hh_r, float* db_ih_r, float* db_hh_r,
                      float* workspace, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Dropout (nn.Dropout in training: basic.py:158-160 MS-TCN residual branch, 382 X2Y concat,
+ * MultiheadAttention probabilities, 442-450 / 504-523 decoder residual and FFN branches).
+ * Counter-based mask, regenerated by every backward: element (r, c) is kept iff
+ * splitmix64(seed + (r * idx_ld + idx_col0 + c + 1) * 0x9E3779B97F4A7C15) >> 32 >= p * 2^32;
+ * kept values are scaled by 1 / (1 - p).  y may alias x.
+ * ---------------------------------------------------------------------- */
+int fx_dropout(const float* x, long long ldx, int rows, int cols, long long idx_ld, long long idx_col0,
+               float p, unsigned long long seed, float* y, long long ldy, void* stream);
 
 /* ------------------------------------------------------------------------
  * Elementwise helpers: dz = dy * (y > 0) (ReLU backward, basic.py:158,
@@ -486,8 +508,9 @@ int fx_attn_loss_bwd(const float* L, long long sr, long long sc, int R, int Q, i
  *   FX_TERM_INFONCE x (R x C) <- emb . text^T * inv_temp (one GEMM), y class per
  *                   frame (-1 = held out), c_ce * (row CE mean + per-class column
  *                   log-softmax mean); backward writes demb.
- * Scratch per term: lse (R), lse2 (R + K or C), colz (K, or C + 1 + 4 * FX_LOSS_NB * C for
- * InfoNCE: counts, valid frames, per-row-block column partials) floats.
+ * Scratch per term: lse (R), lse2 (R + K or C), colz (K, or for InfoNCE: C counts + valid
+ * frames padded to a multiple of 4, then 4 * FX_LOSS_NB * C per-row-block column partials)
+ * floats; InfoNCE colz 16-byte aligned.
  * bwd: gout (nout) upstream gradient of out; every term's dx (and demb) written whole.
  * ---------------------------------------------------------------------- */
 enum { FX_TERM_CLASS = 0, FX_TERM_ATTN = 1, FX_TERM_INFONCE = 2 };

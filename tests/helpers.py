@@ -163,3 +163,22 @@ class GruKinks:
                 out.add(p)
         assert nblk * nvid == len(gpu_parts)
         return out
+
+
+def drop_mask(seed, idx, p):
+    """The kernels' dropout keep-mask (include/factmx.h fx_dropout): splitmix64 of
+    seed + (idx + 1) * 0x9E3779B97F4A7C15, kept iff the high 32 bits >= p * 2^32 (p as float32)."""
+    idx = np.asarray(idx, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed % 2 ** 64) + (idx + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    bits = (z >> np.uint64(32)).astype(np.uint64)
+    thr = min(int(float(np.float32(p)) * 4294967296.0), 4294967295)
+    return bits >= np.uint64(max(thr, 1))
+
+
+def drop_subseed(seed, i):
+    """fx_drop_subseed: the seed of sub-site i (MS-TCN layer i) of a dropout site."""
+    return (seed + 0xD1B54A32D192ED03 * (i + 1)) % 2 ** 64

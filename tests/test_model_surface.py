@@ -6,6 +6,7 @@ tests/golden/make_golden.py), so reference ``.net`` checkpoints load with
 ``load_state_dict`` unchanged (reference blocks.py:919-920).
 """
 import pytest
+import numpy as np
 import torch
 
 from helpers import cfg_from_meta, load_fixture, tiny_inputs, tiny_meta
@@ -60,11 +61,19 @@ def test_block_layout_follows_config():
     assert net.action_query.shape == (meta["FACT"]["ntoken"], 1, meta["Bi"]["a_dim"])
 
 
-def test_fused_dropout_refuses_training():
-    # the fused kernels have no dropout masks; asking for it in training must not silently run without it
-    from factmx.models.basic import X2Y_map
-    m = X2Y_map(16, 16, 16, 16, dropout=0.1)
-    assert m.training
-    x = torch.zeros(4, 1, 16)
-    with pytest.raises(NotImplementedError):
-        m(x, x)
+def test_dropout_seed_follows_torch_manual_seed():
+    # training dropout inside the fused kernels draws one seed per site from torch's CPU generator:
+    # torch.manual_seed fixes the masks as it fixes nn.Dropout's
+    from factmx import functional as fxf
+    torch.manual_seed(3)
+    a = [fxf.dropout_seed() for _ in range(3)]
+    torch.manual_seed(3)
+    b = [fxf.dropout_seed() for _ in range(3)]
+    assert a == b and len(set(a)) == 3
+
+
+def test_dropout_mask_keep_rate_host_restatement():
+    from helpers import drop_mask
+    keep = drop_mask(12345, np.arange(200000), 0.2)
+    assert abs(keep.mean() - 0.8) < 4 * np.sqrt(0.16 / 200000)
+    assert drop_mask(7, np.arange(1000), 0.0).all()
