@@ -538,10 +538,23 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
     FX_CHECK_HIP(hipMemcpy2DAsync(dx, lddx * sizeof(float), dH, F * sizeof(float), F * sizeof(float), rows,
                                   hipMemcpyDeviceToDevice, s));
   }
-  if (ss) {   // join: everything the side stream did is ordered before the caller's later work
+  if (ss && !p->side_defer) {   // join: everything the side stream did is ordered before later work
     FX_CHECK_HIP(hipEventRecord(ss->join, sd));
     FX_CHECK_HIP(hipStreamWaitEvent(s, ss->join, 0));
   }
+  return FX_OK;
+}
+
+void* fx_side_stream(void) {
+  SideStream* ss = side_stream();
+  return ss ? (void*)ss->s : nullptr;
+}
+
+int fx_side_join(void* stream) {
+  SideStream* ss = side_stream();
+  FX_REQUIRE(ss, "side stream unavailable");
+  FX_CHECK_HIP(hipEventRecord(ss->join, ss->s));
+  FX_CHECK_HIP(hipStreamWaitEvent((hipStream_t)stream, ss->join, 0));
   return FX_OK;
 }
 

@@ -171,9 +171,13 @@ __global__ __launch_bounds__(GT) void gru_fwd_kernel(GruArgs args) {
       put_granule(gran + (long long)(s & 1) * Hh + u, (unsigned)(s + 1), hn);
     }
     __syncthreads();   // every wave is done with the old h
-    if (s + 1 < S && tid < 64 &&
-        !gather_granules(gran + (long long)(s & 1) * Hh, Hh, (unsigned)(s + 1), h, args.tmo, lane))
-      dead = 1;
+    if (s + 1 < S) {   // the 4 waves gather a quarter of h each (one round trip instead of several)
+      const int q = (Hh + 4 * 64 - 1) / (4 * 64) * 64, b0 = (tid >> 6) * q;
+      if (b0 < Hh &&
+          !gather_granules(gran + (long long)(s & 1) * Hh + b0, min(q, Hh - b0), (unsigned)(s + 1), h + b0, args.tmo,
+                           lane))
+        dead = 1;
+    }
     __syncthreads();
     if (dead) break;
   }
@@ -261,7 +265,11 @@ __global__ __launch_bounds__(GT) void gru_bwd_kernel(GruBwdArgs args) {
       dhd[tid] = d * z;   // direct path; W^T dgh added below
     }
     if (s + 1 == S) break;   // the last step's recurrent gradient feeds nothing
-    if (tid < 64 && !gather_granules(slot, H3, (unsigned)(s + 1), dg, args.tmo, lane)) dead = 1;
+    {   // the 4 waves gather a quarter of the 3Hh gate gradients each
+      const int q = (H3 + 4 * 64 - 1) / (4 * 64) * 64, b0 = wv * q;
+      if (b0 < H3 && !gather_granules(slot + b0, min(q, H3 - b0), (unsigned)(s + 1), dg + b0, args.tmo, lane))
+        dead = 1;
+    }
     __syncthreads();
     if (dead) break;
     float acc = 0.f;

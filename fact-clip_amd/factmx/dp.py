@@ -26,6 +26,8 @@ more equal buckets reduced after backward), for models without a block list.
 import torch
 import torch.distributed as dist
 
+from . import functional as fxf
+
 
 def _dist_world(group=None):
     if not (dist.is_available() and dist.is_initialized()):
@@ -186,6 +188,7 @@ class DataParallel:
         self._launched.add(k)
         if from_hook:
             self.hook_launched.append(k)
+        fxf.side_join()   # weight gradients still running on the library's side stream land first
         for b in self.block_buckets.get(k, []):
             self._pending.append(_all_reduce_mean_async(b, self.group))
 

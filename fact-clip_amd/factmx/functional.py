@@ -29,6 +29,46 @@ def _ws(n, device):
     return torch.empty(max(int(n), 1), device=device, dtype=_f32)
 
 
+# ---------------------------------------------------------------------------
+# The library's side stream: weight-gradient GEMMs (MS-TCN backward) run there and are joined
+# only when the gradients are needed (end of the backward pass, or before a DP bucket all-reduce),
+# so they overlap the following blocks' latency-bound token-side backward.
+# ---------------------------------------------------------------------------
+DEFER_SIDE = True
+_side = None
+_join_pending = False
+
+
+def side_stream():
+    """torch view of fx_side_stream() (None when the library has none)."""
+    global _side
+    if _side is None:
+        h = nx.load().fx_side_stream()
+        _side = torch.cuda.ExternalStream(h, device=torch.cuda.current_device()) if h else False
+    return _side or None
+
+
+def side_join():
+    """Make the current stream wait for the work deferred to the side stream (no-op when none)."""
+    global _join_pending
+    if _join_pending:
+        _join_pending = False
+        _check(nx.load().fx_side_join(nx.stream()), "fx_side_join")
+
+
+def _defer_to_side(*tensors):
+    """The side stream still reads `tensors`: keep the allocator from reusing them early, and join
+    at the end of the running backward pass."""
+    global _join_pending
+    s = side_stream()
+    for t in tensors:
+        if t is not None:
+            t.record_stream(s)
+    if not _join_pending:
+        _join_pending = True
+        torch.autograd.Variable._execution_engine.queue_callback(side_join)
+
+
 def dropout_seed():
     """Seed of one training dropout site, drawn from torch's default CPU generator (so
     torch.manual_seed fixes the masks, as it fixes nn.Dropout's); the kernels derive every mask
@@ -556,8 +596,12 @@ class MSTCNFn(torch.autograd.Function):
         g.w_out, g.b_out = nx.ptr(w_out), nx.ptr(b_out)
         dx = _empty(*x.shape, device=dev) if ctx.needs_input_grad[0] else None
         ws = _ws(lib.fx_mstcn_workspace_floats(ctypes.byref(ctx.prm), x.shape[0]), dev)
+        defer = DEFER_SIDE and side_stream() is not None
+        ctx.prm.side_defer = int(defer)
         _check(lib.fx_mstcn_bwd(ctypes.byref(ctx.prm), ctypes.byref(g), nx.ptr(x), nx.ld(x), T, nvid, nx.ptr(dy),
                                 cout, nx.ptr(dx), nx.ld(dx), nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_mstcn_bwd")
+        if defer:
+            _defer_to_side(x, dy, saved, ws)
         return (dx, None) + tuple(t[1] for t in tg)
 
 

@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FACTMX_LIB", os.path.join(_HERE, "_lib", "libfactmx.so"))
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -43,7 +43,8 @@ class GemmDesc(ctypes.Structure):
 class MstcnParams(ctypes.Structure):
     _fields_ = [("cin", I), ("F", I), ("cout", I), ("num_layers", I), ("layernorm", I), ("in_map", I),
                 ("dil0", I), ("dil_factor", I), ("w_in", P), ("b_in", P), ("w_dil", P), ("b_dil", P), ("w_pw", P), ("b_pw", P),
-                ("ln_w", P), ("ln_b", P), ("w_out", P), ("b_out", P), ("dropout", F), ("seed", U)]
+                ("ln_w", P), ("ln_b", P), ("w_out", P), ("b_out", P), ("dropout", F), ("seed", U),
+                ("side_defer", I)]
 
 
 class MstcnGrads(ctypes.Structure):
@@ -110,6 +111,8 @@ SIGNATURES = {
     "fx_decoder_bwd": (I, [ctypes.POINTER(DecoderParams), ctypes.POINTER(DecoderGrads), P, L, I, P, P, L, I, I, P, L,
                            P, L, P, L, P, P, L, P, L, P, P, P]),
     "fx_mstcn_saved_floats": (L, [ctypes.POINTER(MstcnParams), I]),
+    "fx_side_stream": (P, []),
+    "fx_side_join": (I, [P]),
     "fx_mstcn_workspace_floats": (L, [ctypes.POINTER(MstcnParams), I]),
     "fx_mstcn_fwd": (I, [ctypes.POINTER(MstcnParams), P, L, I, I, P, L, P, P, P]),
     "fx_mstcn_bwd": (I, [ctypes.POINTER(MstcnParams), ctypes.POINTER(MstcnGrads), P, L, I, I, P, L, P, L, P, P, P]),

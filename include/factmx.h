@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FX_ABI_VERSION 9
+#define FX_ABI_VERSION 10
 
 enum {
   FX_OK = 0,
@@ -259,6 +259,10 @@ typedef struct fx_mstcn_params {
   float dropout;              /* training dropout on each layer's 1x1 branch (basic.py:160); 0 = eval */
   unsigned long long seed;    /* layer i mask: fx_dropout seed fx_drop_subseed(seed, i) = seed +
                                  0xD1B54A32D192ED03 (i + 1), index row * F + channel */
+  int side_defer;             /* bwd: leave the weight-gradient GEMMs running on the library's side
+                                 stream (no join before return); the caller joins with fx_side_join
+                                 before reading those gradients and keeps x / dy / saved / workspace
+                                 alive until then (torch: record_stream on fx_side_stream()) */
 } fx_mstcn_params;
 
 typedef struct fx_mstcn_grads {
@@ -270,6 +274,10 @@ typedef struct fx_mstcn_grads {
 } fx_mstcn_grads;
 
 long long fx_mstcn_saved_floats(const fx_mstcn_params* p, int rows);
+/* the library's side stream of the current device (hipStream_t, created on first use; NULL on
+ * failure) and the join: `stream` waits for everything enqueued on it so far */
+void* fx_side_stream(void);
+int fx_side_join(void* stream);
 long long fx_mstcn_workspace_floats(const fx_mstcn_params* p, int rows);
 int fx_mstcn_fwd(const fx_mstcn_params* p, const float* x, long long ldx, int T, int nvid,
                  float* y, long long ldy, float* saved, float* workspace, void* stream);

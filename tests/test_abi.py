@@ -21,7 +21,7 @@ def _declarations():
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     src = re.sub(r"//[^\n]*", "", src)
     decls = {}
-    for m in re.finditer(r"\b(?:int|void|long long|const char\s*\*)\s+(fx_\w+)\s*\(([^;{]*?)\)\s*;", src, flags=re.S):
+    for m in re.finditer(r"\b(?:int|void\s*\*|void|long long|const char\s*\*)\s*(fx_\w+)\s*\(([^;{]*?)\)\s*;", src, flags=re.S):
         args = m.group(2).strip()
         n = 0 if args in ("", "void") else len([a for a in args.split(",") if a.strip()])
         decls[m.group(1)] = n
