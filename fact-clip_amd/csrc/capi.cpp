@@ -7,6 +7,7 @@
 #include <map>
 #include <mutex>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -75,10 +76,13 @@ struct PackArgs {
   const float* w[32];
   float* wf[32];
   float* wb[32];
+  const float* wpw[32];   // 1x1 weights (F_out, F_in) -> wpt = transposed (fused backward chain)
+  float* wpt[32];
   int F;
 };
 
-// Conv1d weight (F_out=F, F_in=F, 3) -> Wf[n][j*F+c] (forward B) and Wb[c][j*F+n] (dX B)
+// Conv1d weight (F_out=F, F_in=F, 3) -> Wf[n][j*F+c] (forward B) and Wb[c][j*F+n] (dX B);
+// 1x1 weight W[o][c] -> Wt[c][o]
 __global__ void pack_conv_kernel(PackArgs p) {
   const int l = blockIdx.y;
   const int F = p.F;
@@ -91,6 +95,12 @@ __global__ void pack_conv_kernel(PackArgs p) {
     p.wf[l][(long long)n * 3 * F + j * F + c] = v;
     p.wb[l][(long long)c * 3 * F + j * F + n] = v;
   }
+  if (p.wpt[l])
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < (long long)F * F;
+         i += (long long)gridDim.x * blockDim.x) {
+      const int o = (int)(i / F), c = (int)(i % F);
+      p.wpt[l][(long long)c * F + o] = p.wpw[l][i];
+    }
 }
 
 }  // namespace
@@ -194,6 +204,8 @@ struct SideStream {
 };
 
 SideStream* side_stream() {
+  const char* e = std::getenv("FX_SIDE_STREAM");   // 0: everything on the caller's stream (A/B, debug)
+  if (e && e[0] == '0') return nullptr;
   static std::mutex mu;
   static std::map<int, SideStream*> pool;
   int dev = 0;
@@ -220,7 +232,7 @@ struct MstcnLayout {
   // saved
   long long h, z, xh, rs, total_saved;
   // workspace
-  long long wf, wb, buf0, buf1, buf2, buf3, buf4, split, split2, colsum, total_ws;
+  long long wf, wb, wpt, buf0, buf1, buf2, buf3, buf4, buf5, split, split2, colsum, total_ws;
 };
 
 MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
@@ -236,15 +248,18 @@ MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
   const long long wsz = 3 * F * F;
   L.wf = 0;
   L.wb = L.wf + NL * wsz;
-  L.buf0 = L.wb + NL * wsz;
+  L.wpt = L.wb + NL * wsz;                   // transposed 1x1 weights (fused backward chain)
+  L.buf0 = L.wpt + NL * F * F;
   L.buf1 = L.buf0 + L.rowsF;
   L.buf2 = L.buf1 + L.rowsF;
   L.buf3 = L.buf2 + L.rowsF;                 // backward: third dH buffer, second dZ buffer (side stream)
   L.buf4 = L.buf3 + L.rowsF;
-  L.split = L.buf4 + L.rowsF;
+  L.buf5 = L.buf4 + L.rowsF;                 // third dZ buffer (fused backward chain)
+  L.split = L.buf5 + L.rowsF;
   long long sp = 0;
   sp = std::max(sp, split_ws(p->F, 3 * p->F + 1, rows));      // conv dW (+ bias column)
   sp = std::max(sp, dwdb_ws(rows, p->F, p->F));               // pointwise dW
+  sp = std::max(sp, split_ws(rows, p->F, p->F));              // pointwise dX (few rows: split K)
   sp = std::max(sp, dwdb_ws(rows, p->F, p->cout));            // out dW
   if (p->in_map) sp = std::max(sp, dwdb_ws(rows, p->cin, p->F));  // in dW
   sp = std::max(sp, split_ws(rows, p->F, p->cout));           // dH_L
@@ -257,7 +272,7 @@ MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
   return L;
 }
 
-int pack_conv_weights(const fx_mstcn_params* p, float* ws, const MstcnLayout& L, hipStream_t s) {
+int pack_conv_weights(const fx_mstcn_params* p, float* ws, const MstcnLayout& L, hipStream_t s, bool want_wpt) {
   PackArgs a{};
   a.F = p->F;
   const long long wsz = 3LL * p->F * p->F;
@@ -265,6 +280,8 @@ int pack_conv_weights(const fx_mstcn_params* p, float* ws, const MstcnLayout& L,
     a.w[l] = p->w_dil[l];
     a.wf[l] = ws + L.wf + l * wsz;
     a.wb[l] = ws + L.wb + l * wsz;
+    a.wpw[l] = p->w_pw[l];
+    a.wpt[l] = want_wpt ? ws + L.wpt + (long long)l * p->F * p->F : nullptr;
   }
   hipLaunchKernelGGL(pack_conv_kernel, dim3(std::min<int>(cdiv(wsz, 256), 512), p->num_layers), dim3(256), 0, s, a);
   FX_CHECK_HIP(hipGetLastError());
@@ -381,7 +398,7 @@ int fx_mstcn_fwd(const fx_mstcn_params* p, const float* x, long long ldx, int T,
   const int rows = T * nvid;
   const int F = p->F;
   const MstcnLayout L = mstcn_layout(p, rows);
-  FX_TRY(pack_conv_weights(p, workspace, L, s));
+  FX_TRY(pack_conv_weights(p, workspace, L, s, false));
   float* h0 = saved + L.h;
   if (p->in_map) {
     FX_TRY(linear_fwd(x, ldx, rows, p->cin, p->w_in, p->b_in, h0, F, F, 0, s));
@@ -389,10 +406,19 @@ int fx_mstcn_fwd(const fx_mstcn_params* p, const float* x, long long ldx, int T,
     FX_CHECK_HIP(hipMemcpy2DAsync(h0, F * sizeof(float), x, ldx * sizeof(float), F * sizeof(float), rows,
                                   hipMemcpyDeviceToDevice, s));
   }
+  const bool fused = !p->layernorm && frl_supported(F, saved, F, F);
   for (int i = 0; i < p->num_layers; ++i) {
     const float* hi = saved + L.h + i * L.rowsF;
     float* hn = saved + L.h + (i + 1) * L.rowsF;
     float* zi = saved + L.z + i * L.rowsF;
+    if (fused) {   // z = relu(conv(h) + b); h' = h + dropout(z . Wpw^T + b): one kernel (mstcn_fused.hip)
+      prof_begin(0, s);
+      FX_TRY(launch_frl(hi, F, rows, T, layer_dilation(p, i), 1, workspace + L.wf + (long long)i * 3 * F * F,
+                        p->b_dil[i], 1, nullptr, 0, zi, F, p->w_pw[i], p->b_pw[i], hi, F, nullptr, 0, hn, F,
+                        p->dropout, fx_drop_subseed(p->seed, i), s));
+      prof_end(0, s, 2.0 * rows * F * 4.0 * F, 4.0 * (3.0 * rows * F + 4.0 * F * F));
+      continue;
+    }
     // z = relu(dilated_conv(h) + b)      (basic.py:158)
     fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(hi, F, F, layer_dilation(p, i), 1, T, false),
                                op_rows(workspace + L.wf + (long long)i * 3 * F * F, 3 * F), zi, F);
@@ -427,7 +453,11 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   const int NL = p->num_layers;
   const MstcnLayout L = mstcn_layout(p, rows);
   float* ws = workspace;
-  FX_TRY(pack_conv_weights(p, ws, L, s));
+  FX_REQUIRE(p->dropout >= 0.f && p->dropout < 1.f, "mstcn: dropout must be in [0, 1)");
+  const bool drop = p->dropout > 0.f;
+  // Fused chain (no LayerNorm, no dropout, FX_MSTCN_FUSED=1): see below
+  const bool fchain = !p->layernorm && !drop && NL > 0 && frl_supported(F, ws + L.buf0, F, F);
+  FX_TRY(pack_conv_weights(p, ws, L, s, fchain));
   float* spl = ws + L.split;     // split-K partials of the weight-gradient GEMMs (side stream)
   float* spm = ws + L.split2;    // ... of the main stream's GEMMs / LN backward
   WsBound wb(spl, L.colsum - L.split);
@@ -437,8 +467,6 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   // barriers and epilogue).  Without LayerNorm the chain's buffers rotate (dH over 3, dZ over 2)
   // so the side stream reads a layer's gU / dZ while the main stream computes the next layer;
   // a main-stream write waits for the side stream's layer that last read that buffer.
-  FX_REQUIRE(p->dropout >= 0.f && p->dropout < 1.f, "mstcn: dropout must be in [0, 1)");
-  const bool drop = p->dropout > 0.f;
   SideStream* ss = (p->layernorm || drop) ? nullptr : side_stream();
   hipStream_t sd = ss ? ss->s : s;
   auto fork = [&](int e) -> int {   // side stream waits for the main stream's work so far
@@ -458,7 +486,7 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
     return FX_OK;
   };
   float* Hb[3] = {ws + L.buf0, ws + L.buf1, ws + L.buf3};
-  float* Zb[2] = {ws + L.buf2, ws + L.buf4};
+  float* Zb[3] = {ws + L.buf2, ws + L.buf4, ws + L.buf5};
   float* dU = ws + L.buf1;   // LN path (single stream): gradient at the residual sum (pre-LN)
   // weight/bias gradients ACCUMULATE (+=) into g->* (caller zeroes them once per step);
   // every bias gradient rides in its weight-gradient GEMM (virtual ones column).
@@ -467,7 +495,59 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   FX_TRY(linear_dwdb(dy, lddy, hL, F, rows, F, p->cout, g->w_out, g->b_out, 1, spl, sd));
   float* dH = Hb[0];
   FX_TRY(linear_dx(dy, lddy, p->w_out, rows, F, p->cout, dH, F, 0, nullptr, 0, spm, s));
-  for (int i = NL - 1; i >= 0; --i) {
+  // Fused chain: dH_i = gU_i + conv^T(dZ_i) and the next layer's dZ_i-1 = (dH_i . W_pw,i-1) *
+  // (z_i-1 > 0) in ONE kernel per layer (mstcn_fused.hip).  dH_i lives in Hb[(NL - i) % 3], dZ_i in
+  // Zb[(NL - 1 - i) % 3]; a kernel overwriting a buffer first waits for the side stream's layer
+  // that last read it (layer i + 2 for both).
+  auto conv_dw = [&](int i, const float* dZi) -> int {
+    fx_operand b = conv_operand(saved + L.h + i * L.rowsF, F, F, layer_dilation(p, i), 1, T, true);
+    b.ones_col = 3 * F + 1;
+    fx_gemm_desc d = gemm_desc(F, 3 * F + 1, rows, op_cols(dZi, F), b, g->w_dil[i], 3 * F);
+    d.c_tap_cin = F;
+    d.c_last_col = g->b_dil[i];
+    d.beta = 1.f;
+    d.split_k = pick_split(F, 3 * F + 1, rows);
+    d.workspace = spl;
+    return launch_gemm(d, sd);
+  };
+  for (int i = NL - 1; fchain && i >= NL - 1; --i) {   // top layer: dZ by the 1x1 backward GEMM
+    const float* zi = saved + L.z + i * L.rowsF;
+    FX_TRY(fork(1));
+    FX_TRY(linear_dwdb(dH, F, zi, F, rows, F, F, g->w_pw[i], g->b_pw[i], 1, spl, sd));
+    FX_TRY(linear_dx(dH, F, p->w_pw[i], rows, F, F, Zb[0], F, 0, zi, F, spm, s));
+    FX_TRY(fork(2));
+    FX_TRY(conv_dw(i, Zb[0]));
+    FX_TRY(side_done(i));
+  }
+  for (int i = NL - 1; fchain && i >= 0; --i) {
+    float* gU = Hb[(NL - 1 - i) % 3];           // dH_{i+1}
+    float* dZi = Zb[(NL - 1 - i) % 3];
+    float* dHi = Hb[(NL - i) % 3];
+    FX_TRY(wait_side(i + 2));
+    if (i == 0) {   // the bottom layer: conv backward only
+      fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dZi, F, F, layer_dilation(p, 0), -1, T, false),
+                                 op_rows(ws + L.wb, 3 * F), dHi, F);
+      d.resid = gU;
+      d.ld_resid = F;
+      prof_begin(0, s);
+      FX_TRY(launch_gemm(d, s));
+      prof_end(0, s, 2.0 * rows * F * 3.0 * F, 4.0 * (3.0 * rows * F + 3.0 * F * F));
+    } else {
+      float* dZn = Zb[(NL - i) % 3];
+      const float* zn = saved + L.z + (i - 1) * L.rowsF;
+      prof_begin(0, s);
+      FX_TRY(launch_frl(dZi, F, rows, T, layer_dilation(p, i), -1, ws + L.wb + (long long)i * 3 * F * F, nullptr, 0,
+                        gU, F, dHi, F, ws + L.wpt + (long long)(i - 1) * F * F, nullptr, nullptr, 0, zn, F, dZn, F,
+                        0.f, 0, s));
+      prof_end(0, s, 2.0 * rows * F * 4.0 * F, 4.0 * (4.0 * rows * F + 4.0 * F * F));
+      FX_TRY(fork(1));
+      FX_TRY(linear_dwdb(dHi, F, zn, F, rows, F, F, g->w_pw[i - 1], g->b_pw[i - 1], 1, spl, sd));
+      FX_TRY(conv_dw(i - 1, dZn));
+      FX_TRY(side_done(i - 1));
+    }
+    dH = dHi;
+  }
+  for (int i = NL - 1; !fchain && i >= 0; --i) {
     const int step = NL - 1 - i;
     const float* hi = saved + L.h + i * L.rowsF;
     const float* zi = saved + L.z + i * L.rowsF;

@@ -89,4 +89,11 @@ int launch_tattn_bwd(const float* q, long long ldq, const float* k, long long ld
                      int Qv, int Tv, int hd, int nhead, float scale, float* dq, long long lddq, float* dk,
                      long long lddk, float* dv, long long lddv, float* ws, hipStream_t s);
 
+// fused MS-TCN layer step (mstcn_fused.hip): conv GEMM (K = 3F) -> row-local epilogue -> 1x1 GEMM
+bool frl_supported(int F, const void* x, long long ldx, long long ld_other);
+int launch_frl(const float* x, long long ldx, int M, int T, int dil, int dir, const float* w1, const float* bias1,
+               int relu1, const float* resid1, long long ldr1, float* out1, long long ldo1, const float* w2,
+               const float* bias2, const float* resid2, long long ldr2, const float* gate2, long long ldg2, float* out2,
+               long long ldo2, float drop_p, unsigned long long drop_seed, hipStream_t s);
+
 }  // namespace fx

@@ -225,3 +225,46 @@ def test_linear_padded_k_on_wider_input(M, K, N):
     _close(xwd.grad, xr.grad, rtol=1e-4, atol=1e-4, what="dx")
     _close(wd.grad, wr.grad, rtol=1e-4, atol=1e-4, what="dw")
     _close(bd.grad, br.grad, rtol=1e-4, atol=1e-4, what="db")
+
+
+@pytest.mark.parametrize("fused", ["0", "1"])
+@pytest.mark.parametrize("T,nvid,nl", [(1000, 2, 10), (4096, 1, 3), (37, 3, 4)])
+def test_mstcn_fused_layers_match_fp64(T, nvid, nl, fused, monkeypatch):
+    """F = 256, both MS-TCN paths: the two-GEMM layers and (FX_MSTCN_FUSED=1) the fused layer
+    kernel (mstcn_fused.hip) forward + fused dX chain backward: output, input gradient and every
+    weight gradient vs the float64 MS-TCN restatement (ragged row counts, dilations up to
+    2^(nl-1), several videos: no leakage across video edges)."""
+    from factmx.models.basic import MSTCN
+    monkeypatch.setenv("FX_MSTCN_FUSED", fused)
+    torch.manual_seed(0)
+    mod = MSTCN(96, 256, 40, nl, dropout=0.0, ln=False, in_map=True).to(DEV).train()
+    rows = T * nvid
+    x = _r(rows, 96, seed=11)
+    g = _r(rows, 40, seed=12)
+    xd = x.float().to(DEV).requires_grad_(True)
+    y = fxf.mstcn(mod, xd, T=T, nvid=nvid)
+    saved = y.grad_fn.saved_tensors[1].detach().double().cpu()   # (freed by the backward)
+    (y * g.float().to(DEV)).sum().backward()
+    # the float64 restatement takes the GPU's own ReLU decisions (z > 0 of the saved activations):
+    # a pre-activation within ~1e-6 of 0 may land on the other side in fp32 (either summation order
+    # is valid), which would move single dZ entries -- whole conv-weight-gradient rows -- by O(1)
+    # (the GRU kink of tests/helpers.GruKinks); with the same gates everything agrees at fp32 noise
+    n = rows * 256
+    gates = [(saved[(nl + 1 + i) * n:(nl + 2 + i) * n].view(rows, 256) > 0).double() for i in range(nl)]
+    P = {n_: t.detach().double().cpu().requires_grad_(True) for n_, t in mod.named_parameters()}
+    xr = x.clone().requires_grad_(True)
+    outs = []
+    for v in range(nvid):
+        sl = slice(v * T, (v + 1) * T)
+        h = fo.linear(xr[sl], P["conv_1x1.weight"], P["conv_1x1.bias"])
+        for i in range(nl):
+            q = f"layers.{i}."
+            z = fo.dilated_conv3(h, P[q + "conv_dilated.weight"], P[q + "conv_dilated.bias"], 2 ** i) * gates[i][sl]
+            h = h + fo.linear(z, P[q + "conv_1x1.weight"], P[q + "conv_1x1.bias"])
+        outs.append(fo.linear(h, P["conv_out.weight"], P["conv_out.bias"]))
+    yr = torch.cat(outs, 0)
+    (yr * g).sum().backward()
+    _close(y, yr, rtol=1e-4, atol=1e-4, what="y")
+    _close(xd.grad, xr.grad, rtol=1e-4, atol=1e-4, what="dx")
+    for n_, t in mod.named_parameters():
+        _close(t.grad, P[n_].grad, rtol=2e-4, atol=2e-4, what=f"d{n_}")

@@ -12,7 +12,7 @@ def main(d):
         for r in csv.DictReader(open(f)):
             acc[r["Kernel_Name"][:90]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k, cs in acc.items():
-        if "gemm" not in k:
+        if os.environ.get("KFILTER", "gemm") not in k:
             continue
         print(k)
         for c, v in sorted(cs.items()):
