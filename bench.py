@@ -161,6 +161,28 @@ def traffic_from_profiles(kernel_prefix):
     return None
 
 
+def prof_collect(lib, kind):
+    """(total ms, flops, bytes, launches) of the HIP-event timed launches of one profiling kind."""
+    from factmx import native
+    ms, fl, by, cnt = native.D(), native.D(), native.D(), native.I()
+    native.check(lib.fx_prof_collect(kind, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(by),
+                                     ctypes.byref(cnt)), "fx_prof_collect")
+    return ms, fl, by, cnt
+
+
+def attention_roofline(kernel, ms, fl, by, cnt):
+    """Attention over T (SCA cross-attention): HBM-bound, algorithmic bytes
+    per launch = K and V rows of every frame (+ the 32-query q / o / lse) as stated in DESIGN.md."""
+    n = max(cnt.value, 1)
+    avg_ms = ms.value / n
+    if avg_ms <= 0:
+        return None
+    gbs = by.value / n / (avg_ms * 1e-3) / 1e9
+    return dict(kernel=kernel, bound="hbm", achieved=round(gbs, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(gbs / HBM_PEAK_GBS, 4),
+                traffic=None, launches=cnt.value, avg_launch_ms=round(avg_ms, 5), bytes_per_launch=by.value / n,
+                tflops=round(fl.value / n / (avg_ms * 1e-3) / 1e12, 2))
+
+
 def cpu_baseline(wl, T, videos_seeds, min_seconds=10.0, min_steps=2):
     """The CPU oracle (fp32 PyTorch restatement pinned to the reference) timed on host cores: one
     video per step, full T, forward + prediction + loss + backward with FIXED weights (the same
@@ -261,6 +283,8 @@ def main():
 
     max_ev = args.steps * nv * 4 * 10 * 2 + 64
     native.check(lib.fx_prof_enable(0, max_ev), "fx_prof_enable")
+    for kind in (1, 2):       # attention over T, forward and backward (one launch per SCA decoder layer)
+        native.check(lib.fx_prof_enable(kind, args.steps * 16 + 64), "fx_prof_enable")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -271,9 +295,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ms, fl, by, cnt = native.D(), native.D(), native.D(), native.I()
-    native.check(lib.fx_prof_collect(0, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(by), ctypes.byref(cnt)),
-                 "fx_prof_collect")
+    ms, fl, by, cnt = prof_collect(lib, 0)
+    attn_prof = {name: prof_collect(lib, kind) for kind, name in ((1, "fwd"), (2, "bwd"))}
     lib.fx_prof_disable()
     S_after = video_segments(net)
     if world > 1:
@@ -320,6 +343,8 @@ def main():
                         kernel=("gemm_f32_wide8_kernel (implicit dilated-conv GEMM: conv fwd + conv dX)"),
                         launches=cnt.value, avg_launch_ms=round(avg_ms, 5),
                         flops_per_launch=flops_per_launch)
+        roofline_attention = {name: attention_roofline(f"tattn_{name}_kernel (+ tattn_merge_kernel over T splits)", *v)
+                              for name, v in attn_prof.items()}
         line = dict(metric=metric, value=round(value, 1), unit="frames/s", n_gpus=world, steps=args.steps,
                     warmup=args.warmup, ms_per_step=round(1e3 * elapsed / args.steps, 3), higher_is_better=True,
                     scaling="weak", vs_baseline=None, dtype="fp32", data="synthetic",
@@ -329,7 +354,7 @@ def main():
                                 videos_per_rank=nv, global_batch=world * nv, seq_len=T,
                                 parallelism=f"dp{world}", weights="fixed (no optimizer update in the timed steps)",
                                 tdu_segments=S, tdu_segments_after_timing=S_after),
-                    roofline=roofline, train_step_with_adam=adam)
+                    roofline=roofline, roofline_attention=roofline_attention, train_step_with_adam=adam)
         if world == 1 and not args.no_cpu_baseline:
             cb, step_flops, S_oracle = cpu_baseline(args.config, T, seeds)
             line["cpu_baseline"] = cb

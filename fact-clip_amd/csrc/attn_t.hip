@@ -580,12 +580,16 @@ int launch_tattn_fwd(const float* q, long long ldq, const float* k, long long ld
   a.Qv = Qv; a.Tv = Tv; a.hd = hd; a.nh = nh; a.Qp = g.Qp; a.Hp = g.Hp; a.Tc = g.Tc; a.nsplit = g.nsplit;
   a.scale = scale;
   a.vec = (hd % 4 == 0) && a16(q, ldq) && a16(k, ldk) && a16(v, ldv);
+  // algorithmic traffic: K and V rows read once, q read, o and lse written
+  const double kv = (double)nvid * Tv * nh * hd, qo = (double)nvid * Qv * nh * hd;
+  prof_begin(1, s);
   hipLaunchKernelGGL(tattn_fwd_kernel, dim3(g.nsplit, nh, nvid), dim3(AT), g.lds, s, a);
   FX_CHECK_HIP(hipGetLastError());
   if (g.nsplit > 1) {
     hipLaunchKernelGGL(tattn_merge_kernel, dim3(nh, nvid), dim3(AT), merge_lds(g), s, a, 1, 1.f);
     FX_CHECK_HIP(hipGetLastError());
   }
+  prof_end(1, s, 4.0 * qo * Tv, 4.0 * (2.0 * kv + 2.0 * qo + (double)nvid * nh * Qv));
   return FX_OK;
 }
 
@@ -606,12 +610,17 @@ int launch_tattn_bwd(const float* q, long long ldq, const float* k, long long ld
   a.Qv = Qv; a.Tv = Tv; a.hd = hd; a.nh = nh; a.Qp = g.Qp; a.Hp = g.Hp; a.Tc = g.Tc; a.nsplit = g.nsplit;
   a.scale = scale;
   a.vec = (hd % 4 == 0) && a16(q, ldq) && a16(k, ldk) && a16(v, ldv) && a16(o, ldo) && a16(dout, lddo);
+  // algorithmic traffic: K, V read and dK, dV written once; q, o, dout, lse read, dq written.
+  // flops: S = qK^T recomputed, dP = dO V^T, dV = P^T dO, dK = dS^T q, dq = dS K
+  const double kv = (double)nvid * Tv * nh * hd, qo = (double)nvid * Qv * nh * hd;
+  prof_begin(2, s);
   hipLaunchKernelGGL(tattn_bwd_kernel, dim3(g.nsplit, nh, nvid), dim3(AT), g.lds, s, a);
   FX_CHECK_HIP(hipGetLastError());
   if (g.nsplit > 1) {
     hipLaunchKernelGGL(tattn_merge_kernel, dim3(nh, nvid), dim3(AT), 0, s, a, 0, scale);
     FX_CHECK_HIP(hipGetLastError());
   }
+  prof_end(2, s, 10.0 * qo * Tv, 4.0 * (4.0 * kv + 4.0 * qo + (double)nvid * nh * Qv));
   return FX_OK;
 }
 

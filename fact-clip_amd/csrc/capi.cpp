@@ -24,30 +24,38 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 // ---- profiling (opt-in diagnostic used by bench.py) ---------------------------
 namespace {
 struct ProfState {
-  int kind = -1;
   int max_events = 0;
   std::vector<hipEvent_t> ev;
   std::vector<double> flops, bytes;
   int used = 0;
-  hipEvent_t pending = nullptr;
 };
+constexpr int kProfKinds = 4;
 std::mutex g_prof_mu;
-ProfState g_prof;
+ProfState g_prof[kProfKinds];
+
+void prof_reset(ProfState& p) {
+  for (auto& e : p.ev) (void)hipEventDestroy(e);
+  p = ProfState{};
+}
 }  // namespace
 
 void prof_begin(int kind, hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_prof_mu);
-  if (g_prof.kind != kind || g_prof.used >= g_prof.max_events) return;
-  (void)hipEventRecord(g_prof.ev[2 * g_prof.used], s);
+  if (kind < 0 || kind >= kProfKinds) return;
+  ProfState& p = g_prof[kind];
+  if (p.used >= p.max_events) return;
+  (void)hipEventRecord(p.ev[2 * p.used], s);
 }
 
 void prof_end(int kind, hipStream_t s, double flops, double bytes) {
   std::lock_guard<std::mutex> lk(g_prof_mu);
-  if (g_prof.kind != kind || g_prof.used >= g_prof.max_events) return;
-  (void)hipEventRecord(g_prof.ev[2 * g_prof.used + 1], s);
-  g_prof.flops[g_prof.used] = flops;
-  g_prof.bytes[g_prof.used] = bytes;
-  g_prof.used++;
+  if (kind < 0 || kind >= kProfKinds) return;
+  ProfState& p = g_prof[kind];
+  if (p.used >= p.max_events) return;
+  (void)hipEventRecord(p.ev[2 * p.used + 1], s);
+  p.flops[p.used] = flops;
+  p.bytes[p.used] = bytes;
+  p.used++;
 }
 
 // ---- helpers -------------------------------------------------------------------
@@ -1217,40 +1225,40 @@ int fx_seg_sum_rows(const float* dx, long long lddx, const int32_t* seg_start, c
 // ---------------------------------------------------------------- profiling
 int fx_prof_enable(int kind, int max_events) {
   std::lock_guard<std::mutex> lk(g_prof_mu);
-  for (auto& e : g_prof.ev) (void)hipEventDestroy(e);
-  g_prof = ProfState{};
-  g_prof.ev.resize(2 * (size_t)max_events);
-  for (auto& e : g_prof.ev) FX_CHECK_HIP(hipEventCreate(&e));
-  g_prof.flops.assign(max_events, 0.0);
-  g_prof.bytes.assign(max_events, 0.0);
-  g_prof.max_events = max_events;
-  g_prof.kind = kind;
+  FX_REQUIRE(kind >= 0 && kind < kProfKinds && max_events >= 0, "prof: kind out of range");
+  ProfState& p = g_prof[kind];
+  prof_reset(p);
+  p.ev.resize(2 * (size_t)max_events);
+  for (auto& e : p.ev) FX_CHECK_HIP(hipEventCreate(&e));
+  p.flops.assign(max_events, 0.0);
+  p.bytes.assign(max_events, 0.0);
+  p.max_events = max_events;
   return FX_OK;
 }
 
 int fx_prof_collect(int kind, double* total_ms, double* total_flops, double* total_bytes, int* count) {
   std::lock_guard<std::mutex> lk(g_prof_mu);
-  FX_REQUIRE(g_prof.kind == kind, "prof: kind not enabled");
+  FX_REQUIRE(kind >= 0 && kind < kProfKinds && g_prof[kind].max_events > 0, "prof: kind not enabled");
+  const ProfState& p = g_prof[kind];
   double ms = 0, fl = 0, by = 0;
-  for (int i = 0; i < g_prof.used; ++i) {
-    FX_CHECK_HIP(hipEventSynchronize(g_prof.ev[2 * i + 1]));
+  for (int i = 0; i < p.used; ++i) {
+    FX_CHECK_HIP(hipEventSynchronize(p.ev[2 * i + 1]));
     float t = 0.f;
-    FX_CHECK_HIP(hipEventElapsedTime(&t, g_prof.ev[2 * i], g_prof.ev[2 * i + 1]));
+    FX_CHECK_HIP(hipEventElapsedTime(&t, p.ev[2 * i], p.ev[2 * i + 1]));
     ms += t;
-    fl += g_prof.flops[i];
-    by += g_prof.bytes[i];
+    fl += p.flops[i];
+    by += p.bytes[i];
   }
   *total_ms = ms;
   *total_flops = fl;
   *total_bytes = by;
-  *count = g_prof.used;
+  *count = p.used;
   return FX_OK;
 }
 
 void fx_prof_disable(void) {
   std::lock_guard<std::mutex> lk(g_prof_mu);
-  for (auto& e : g_prof.ev) (void)hipEventDestroy(e);
-  g_prof = ProfState{};
+  for (auto& p : g_prof) prof_reset(p);
 }
 
 }  // extern "C"

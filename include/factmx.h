@@ -578,8 +578,12 @@ int fx_eval_pred(const fx_video_attn* vids_host, const fx_video_attn* vids_dev, 
                  int32_t* pred, void* stream);
 
 /* ------------------------------------------------------------------------
- * Profiling hooks: HIP-event timing of every launch of one kernel class
- * (bench.py roofline).  kind: 0 = dilated-conv implicit GEMM forward.
+ * Profiling hooks: HIP-event timing of every launch of a kernel class
+ * (bench.py roofline).  Kinds are enabled independently:
+ *   0 = dilated-conv implicit GEMM (conv forward, conv dX),
+ *   1 = attention over T forward (tattn_fwd_kernel + split merge),
+ *   2 = attention over T backward (tattn_bwd_kernel + split merge).
+ * fx_prof_enable resets one kind; fx_prof_disable resets all.
  * ---------------------------------------------------------------------- */
 int fx_prof_enable(int kind, int max_events);
 int fx_prof_collect(int kind, double* total_ms, double* total_flops, double* total_bytes,

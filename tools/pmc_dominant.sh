@@ -15,3 +15,6 @@ for set in "FETCH_SIZE" "WRITE_SIZE" \
 done
 python tools/pmc_dominant.py $OUT "${KERNEL:-gemm_f32_wide8_kernel<1, 0>}" > gpurun_out/pmc_dominant.json
 cat gpurun_out/pmc_dominant.json
+# the same FETCH/WRITE passes, averaged over the attention-over-T kernels
+python tools/pmc_dominant.py $OUT "tattn_fwd_kernel" > gpurun_out/pmc_tattn_fwd.json
+python tools/pmc_dominant.py $OUT "tattn_bwd_kernel" > gpurun_out/pmc_tattn_bwd.json
