@@ -17,7 +17,9 @@
 // also writes dK, dV).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <mutex>
+#include <string>
 
 #include "fx_common.h"
 #include "ops.h"
@@ -125,10 +127,13 @@ struct TAttnArgs {
   float* dv; long long lddv;            // bwd
   float* lse;                           // (nvid, h, Qv): fwd writes, bwd reads
   float* ws;                            // partials
+  unsigned* cnt;                        // per (video, head) arrival counters: in-launch merge; NULL -> merge launch
   int Qv, Tv, hd, nh, Qp, Hp, Tc, nsplit;
   float scale;
   int vec;                              // 16-B loads of every q / k / v / o / dout row slice
 };
+
+__device__ void tattn_finish(const TAttnArgs& a, int h, int vid, int stats, float mul, float* sm);
 
 // Strips of row-major sources staged into LDS images (row stride ld, zero outside the `nvalid` rows and
 // `hd` columns).  Every load of a workgroup's strips is issued before the first LDS store (a store
@@ -317,23 +322,23 @@ __global__ __launch_bounds__(AT) void tattn_fwd_kernel(TAttnArgs a) {
     pl[pid * Qp + r] = rowl[r];
   }
   TSTAMP(4);
+  if (a.cnt) tattn_finish(a, h, vid, 1, 1.f, sm);
 }
 
 // Ordered merge of the nsplit partials of one (video, head) per workgroup, chunk order fixed
 // (deterministic).  Forward (stats != 0): w_s(r) = e^(m_s - M) / L, o = sum_s w_s O_s, lse = M + log L;
 // backward: dq = scale * sum_s dq_s.  A thread owns 4 consecutive columns of a row with 16 splits'
 // float4 loads in flight.
-__global__ __launch_bounds__(AT) void tattn_merge_kernel(TAttnArgs a, int stats, float mul) {
-  extern __shared__ float sm[];
-  const int h = blockIdx.x, vid = blockIdx.y, tid = threadIdx.x;
+__device__ void tattn_merge(const TAttnArgs& a, int h, int vid, int nvid, int stats, float mul, float* sm) {
+  const int tid = threadIdx.x;
   const int Qp = a.Qp, Hp = a.Hp, hd = a.hd, ns = a.nsplit;
   const long long pbase = ((long long)vid * a.nh + h) * ns;
   const float* part = a.ws + pbase * Qp * Hp;
   float* w = sm;                         // [ns][Qp] weights
   float* wl = sm + ns * Qp;              // [ns][Qp] l partials
   if (stats) {
-    const float* pm = a.ws + (long long)gridDim.y * a.nh * ns * Qp * Hp + pbase * Qp;
-    const float* pl = pm + (long long)gridDim.y * a.nh * ns * Qp;
+    const float* pm = a.ws + (long long)nvid * a.nh * ns * Qp * Hp + pbase * Qp;
+    const float* pl = pm + (long long)nvid * a.nh * ns * Qp;
     for (int e = tid; e < ns * Qp; e += AT) {
       w[e] = pm[e];
       wl[e] = pl[e];
@@ -377,6 +382,37 @@ __global__ __launch_bounds__(AT) void tattn_merge_kernel(TAttnArgs a, int stats,
     for (int j = 0; j < 4; ++j)
       if (col + j < hd) o[j] = v[j] * mul;
   }
+}
+
+__global__ __launch_bounds__(AT) void tattn_merge_kernel(TAttnArgs a, int stats, float mul) {
+  extern __shared__ float sm[];
+  tattn_merge(a, blockIdx.x, blockIdx.y, gridDim.y, stats, mul, sm);
+}
+
+// In-launch merge: the workgroup of a (video, head) that writes the LAST chunk partial merges them all
+// (arrival counter per (video, head); partial stores drained, one agent-scope release by lane 0
+// before the ticket, one acquire in the merger; the counter is re-armed for the next launch).
+__device__ void tattn_finish(const TAttnArgs& a, int h, int vid, int stats, float mul, float* sm) {
+  int* flag = reinterpret_cast<int*>(sm);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned* cnt = a.cnt + (long long)vid * a.nh + h;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == (unsigned)a.nsplit - 1;
+    if (last) {
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  const int last = *flag;
+  __syncthreads();
+  if (last) tattn_merge(a, h, vid, gridDim.z, stats, mul, sm);
 }
 
 // ------------------------------------------------------------------------------------------ backward
@@ -503,6 +539,7 @@ __global__ __launch_bounds__(AT) void tattn_bwd_kernel(TAttnArgs a) {
       for (int r = 0; r < 16; ++r) po[(rt * 32 + acc_row(r, lane)) * Hp + col] = acc[r];
     }
   }
+  if (a.nsplit > 1 && a.cnt) tattn_finish(a, h, vid, 0, a.scale, sm);
 }
 
 struct TAttnGeom {
@@ -524,7 +561,11 @@ TAttnGeom tattn_geom(int nvid, int Qv, int Tv, int hd, int nh, bool bwd) {
   int Tc = 256;
   // (forward: at most 8 score tiles, two per wave, in registers)
   while (Tc > 32 && (lds_b(Tc) > 150 * 1024 || Tc * g.Hp > NVK * 4 * AT || Tc * g.Qp > 8 * 1024)) Tc >>= 1;
-  while (Tc > 32 && (long long)nvid * nh * ((Tv + Tc - 1) / Tc) < 256) Tc >>= 1;
+  static const int min_wg = [] {   // FX_TATTN_MINWG: workgroups the split aims for (diagnostic A/B)
+    const char* p = std::getenv("FX_TATTN_MINWG");
+    return p ? std::max(1, std::atoi(p)) : 256;
+  }();
+  while (Tc > 32 && (long long)nvid * nh * ((Tv + Tc - 1) / Tc) < min_wg) Tc >>= 1;
   g.Tc = Tc;
   g.nsplit = std::max(1, (Tv + Tc - 1) / Tc);
   g.lds = lds_b(Tc);
@@ -550,6 +591,18 @@ long long tattn_ws_floats(int nvid, int Qv, int Tv, int hd, int nh) {
 }
 
 static size_t merge_lds(const TAttnGeom& g) { return sizeof(float) * 2 * (size_t)g.nsplit * g.Qp; }
+
+// FX_TATTN_MERGE=in: the in-launch last-arriver merge instead of the separate ordered merge launch
+// (diagnostic A/B; both add the partials in chunk order, so the results are bitwise equal).  Measured
+// at the bench shape: fwd 22.4 vs 18.2 us, bwd 44.8 vs 33.2 us -- the agent-scope release / acquire
+// of the arrival hand-off (L2 write-back / invalidate on a multi-XCD part) costs more than the launch.
+static bool merge_in_launch() {
+  static const bool on = [] {
+    const char* p = std::getenv("FX_TATTN_MERGE");
+    return p && std::string(p) == "in";
+  }();
+  return on;
+}
 
 static bool a16(const void* p, long long ld) { return p == nullptr || (((uintptr_t)p & 15) == 0 && (ld & 3) == 0); }
 
@@ -582,10 +635,11 @@ int launch_tattn_fwd(const float* q, long long ldq, const float* k, long long ld
   a.vec = (hd % 4 == 0) && a16(q, ldq) && a16(k, ldk) && a16(v, ldv);
   // algorithmic traffic: K and V rows read once, q read, o and lse written
   const double kv = (double)nvid * Tv * nh * hd, qo = (double)nvid * Qv * nh * hd;
+  a.cnt = g.nsplit > 1 && merge_in_launch() ? arrival_counters(s) : nullptr;
   prof_begin(1, s);
-  hipLaunchKernelGGL(tattn_fwd_kernel, dim3(g.nsplit, nh, nvid), dim3(AT), g.lds, s, a);
+  hipLaunchKernelGGL(tattn_fwd_kernel, dim3(g.nsplit, nh, nvid), dim3(AT), std::max(g.lds, merge_lds(g) + 16), s, a);
   FX_CHECK_HIP(hipGetLastError());
-  if (g.nsplit > 1) {
+  if (g.nsplit > 1 && !a.cnt) {
     hipLaunchKernelGGL(tattn_merge_kernel, dim3(nh, nvid), dim3(AT), merge_lds(g), s, a, 1, 1.f);
     FX_CHECK_HIP(hipGetLastError());
   }
@@ -613,10 +667,11 @@ int launch_tattn_bwd(const float* q, long long ldq, const float* k, long long ld
   // algorithmic traffic: K, V read and dK, dV written once; q, o, dout, lse read, dq written.
   // flops: S = qK^T recomputed, dP = dO V^T, dV = P^T dO, dK = dS^T q, dq = dS K
   const double kv = (double)nvid * Tv * nh * hd, qo = (double)nvid * Qv * nh * hd;
+  a.cnt = g.nsplit > 1 && merge_in_launch() ? arrival_counters(s) : nullptr;
   prof_begin(2, s);
-  hipLaunchKernelGGL(tattn_bwd_kernel, dim3(g.nsplit, nh, nvid), dim3(AT), g.lds, s, a);
+  hipLaunchKernelGGL(tattn_bwd_kernel, dim3(g.nsplit, nh, nvid), dim3(AT), std::max(g.lds, merge_lds(g) + 16), s, a);
   FX_CHECK_HIP(hipGetLastError());
-  if (g.nsplit > 1) {
+  if (g.nsplit > 1 && !a.cnt) {
     hipLaunchKernelGGL(tattn_merge_kernel, dim3(nh, nvid), dim3(AT), 0, s, a, 0, scale);
     FX_CHECK_HIP(hipGetLastError());
   }

@@ -164,23 +164,34 @@ int linear_fwd(const float* x, long long ldx, int M, int K, const float* w, cons
 }
 
 // dx (+)= dy . w  [* (gate > 0)];  w (N,K)
-int linear_dx(const float* dy, long long lddy, const float* w, int M, int K, int N, float* dx, long long lddx,
-              int accumulate, const float* gate, long long ld_gate, float* ws, hipStream_t s, long long ldw) {
+fx_gemm_desc desc_linear_dx(const float* dy, long long lddy, const float* w, int M, int K, int N, float* dx,
+                            long long lddx, int accumulate, const float* gate, long long ld_gate, float* ws,
+                            long long ldw) {
   fx_gemm_desc d = gemm_desc(M, K, N, op_rows(dy, lddy), op_cols(w, ldw < 0 ? K : ldw), dx, lddx);
   d.beta = accumulate ? 1.f : 0.f;
   d.gate = gate;
   d.ld_gate = ld_gate;
   d.split_k = pick_split(M, K, N);
   d.workspace = ws;
-  return launch_gemm(d, s);
+  return d;
+}
+
+int linear_dx(const float* dy, long long lddy, const float* w, int M, int K, int N, float* dx, long long lddx,
+              int accumulate, const float* gate, long long ld_gate, float* ws, hipStream_t s, long long ldw) {
+  return launch_gemm(desc_linear_dx(dy, lddy, w, M, K, N, dx, lddx, accumulate, gate, ld_gate, ws, ldw), s);
 }
 
 // dw (+)= dy^T . x  and  db (+)= colsum(dy)  in ONE GEMM: x gets a virtual all-ones column K
 // whose output column (the bias gradient) is routed to db.  dy (M,N), x (M,K) -> dw (N,K), ld lddw.
-int linear_dwdb(const float* dy, long long lddy, const float* x, long long ldx, int M, int K, int N, float* dw,
-                float* db, int accumulate, float* ws, hipStream_t s, long long lddw) {
-  if (!dw && !db) return FX_OK;
-  FX_REQUIRE(dw, "linear_dwdb: bias-only gradient needs dw");
+// (no dw and no db: an empty desc, M = 0, that launch_gemm / launch_gemm_group skip)
+fx_gemm_desc desc_linear_dwdb(const float* dy, long long lddy, const float* x, long long ldx, int M, int K, int N,
+                              float* dw, float* db, int accumulate, float* ws, long long lddw) {
+  if (!dw) {
+    fx_gemm_desc e{};
+    e.batch = 1;
+    e.c_last_col = db;   // (a bias-only request: linear_bwd_pair refuses it like linear_dwdb)
+    return e;
+  }
   fx_operand b = op_cols(x, ldx);
   const int Kc = K + (db ? 1 : 0);
   if (db) b.ones_col = K + 1;
@@ -191,7 +202,22 @@ int linear_dwdb(const float* dy, long long lddy, const float* x, long long ldx, 
   // only K columns can pick a larger split (fewer tiles) than the reservation holds
   d.split_k = pick_split(N, K + 1, M);
   d.workspace = ws;
-  return launch_gemm(d, s);
+  return d;
+}
+
+int linear_dwdb(const float* dy, long long lddy, const float* x, long long ldx, int M, int K, int N, float* dw,
+                float* db, int accumulate, float* ws, hipStream_t s, long long lddw) {
+  if (!dw && !db) return FX_OK;
+  FX_REQUIRE(dw, "linear_dwdb: bias-only gradient needs dw");
+  return launch_gemm(desc_linear_dwdb(dy, lddy, x, ldx, M, K, N, dw, db, accumulate, ws, lddw), s);
+}
+
+// The two independent backward GEMMs of one linear layer (dW/db = dY^T X, dX = dY W): one launch
+// when both take the direct kernel (token-level shapes), else two.
+int linear_bwd_pair(const fx_gemm_desc& dwdb, const fx_gemm_desc& dx, hipStream_t s) {
+  FX_REQUIRE(!(dwdb.c_last_col && !dwdb.c), "linear_dwdb: bias-only gradient needs dw");
+  const fx_gemm_desc pr[2] = {dwdb, dx};
+  return launch_gemm_group(pr, 2, s);
 }
 
 int linear_dw(const float* dy, long long lddy, const float* x, long long ldx, int M, int K, int N, float* dw,
@@ -950,7 +976,11 @@ int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpo
   // keep X+Xpos / Y+Ypos for the weight gradients (basic.py:357-369)
   const float* xin = X;
   long long ldxin = ldx;
-  if (Xpos) {
+  if (Xpos && xpos_cols == xdim) {
+    FX_TRY(add2(X, ldx, Xpos, ldxp, Nx, xdim, saved + L.xin, xdim, 0, s));
+    xin = saved + L.xin;
+    ldxin = xdim;
+  } else if (Xpos) {
     FX_CHECK_HIP(hipMemcpy2DAsync(saved + L.xin, xdim * sizeof(float), X, ldx * sizeof(float), xdim * sizeof(float), Nx,
                                   hipMemcpyDeviceToDevice, s));
     FX_TRY(add2(Xpos, ldxp, nullptr, 0, Nx, xpos_cols, saved + L.xin, xdim, 1, s));
@@ -959,7 +989,11 @@ int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpo
   }
   const float* yin = Y;
   long long ldyin = ldy;
-  if (Ypos) {
+  if (Ypos && ypos_cols == ydim) {
+    FX_TRY(add2(Y, ldy, Ypos, ldyp, Ny, ydim, saved + L.yin, ydim, 0, s));
+    yin = saved + L.yin;
+    ldyin = ydim;
+  } else if (Ypos) {
     FX_CHECK_HIP(hipMemcpy2DAsync(saved + L.yin, ydim * sizeof(float), Y, ldy * sizeof(float), ydim * sizeof(float), Ny,
                                   hipMemcpyDeviceToDevice, s));
     FX_TRY(add2(Ypos, ldyp, nullptr, 0, Ny, ypos_cols, saved + L.yin, ydim, 1, s));
@@ -970,27 +1004,33 @@ int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpo
   FX_TRY(linear_fwd(X, ldx, Nx, xdim, wv, bv, xv, Hd, Hd, 0, s));
   FX_TRY(linear_fwd(yin, ldyin, Ny, ydim, wq, bq, yq, Hd, Hd, 0, s));
   const float scale = 1.0f / std::sqrt((float)Hd);
-  for (int v = 0; v < V.n; ++v) {
-    const int nx = V.x[v + 1] - V.x[v], ny = V.y[v + 1] - V.y[v];
-    if (nx == 0 || ny == 0) continue;
-    float* lg = logit + V.a[v];
-    float* at = attn + V.a[v];
-    {
+  // per video: logits = scale yq . xk^T, attn = softmax(logits), feat = attn . xv  (the GEMMs of up to
+  // two videos in one grouped launch each)
+  for (int v0 = 0; v0 < V.n; v0 += 2) {
+    fx_gemm_desc g1[2], g2[2];
+    int n1 = 0, n2 = 0;
+    for (int v = v0; v < std::min(V.n, v0 + 2); ++v) {
+      const int nx = V.x[v + 1] - V.x[v], ny = V.y[v + 1] - V.y[v];
+      if (nx == 0 || ny == 0) continue;
       fx_gemm_desc d = gemm_desc(ny, nx, Hd, op_rows(yq + (long long)V.y[v] * Hd, Hd),
-                                 op_rows(xk + (long long)V.x[v] * Hd, Hd), lg, nx);
+                                 op_rows(xk + (long long)V.x[v] * Hd, Hd), logit + V.a[v], nx);
       d.alpha = scale;
       d.split_k = pick_split(ny, nx, Hd);
       d.workspace = workspace;
-      FX_TRY(launch_gemm(d, s));
-    }
-    FX_TRY(launch_softmax_rows(lg, nx, ny, nx, 1.f, at, nx, s));
-    {
-      fx_gemm_desc d = gemm_desc(ny, Hd, nx, op_rows(at, nx), op_cols(xv + (long long)V.x[v] * Hd, Hd),
-                                 feat + (long long)V.y[v] * Hd, Hd);
+      g1[n1++] = d;
+      d = gemm_desc(ny, Hd, nx, op_rows(attn + V.a[v], nx), op_cols(xv + (long long)V.x[v] * Hd, Hd),
+                    feat + (long long)V.y[v] * Hd, Hd);
       d.split_k = pick_split(ny, Hd, nx);
       d.workspace = workspace;
-      FX_TRY(launch_gemm(d, s));
+      g2[n2++] = d;
     }
+    FX_TRY(launch_gemm_group(g1, n1, s));
+    for (int v = v0; v < std::min(V.n, v0 + 2); ++v) {
+      const int nx = V.x[v + 1] - V.x[v], ny = V.y[v + 1] - V.y[v];
+      if (nx == 0 || ny == 0) continue;
+      FX_TRY(launch_softmax_rows(logit + V.a[v], nx, ny, nx, 1.f, attn + V.a[v], nx, s));
+    }
+    FX_TRY(launch_gemm_group(g2, n2, s));
   }
   // Y_W(cat[Y, feat]) with the concatenation folded into the A-operand loader; with dropout the
   // dropped concatenation is materialised (training only)
@@ -1050,44 +1090,49 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
     FX_TRY(linear_dwdb(dout, lddo, Y, ldy, Ny, ydim, outdim, dwy, dby, 1, spl, s, cw));
     FX_TRY(linear_dw(dout, lddo, feat, Hd, Ny, Hd, outdim, dwy + ydim, 1, spl, s, cw));
   }
-  for (int v = 0; v < V.n; ++v) {
-    const int nx = V.x[v + 1] - V.x[v], ny = V.y[v + 1] - V.y[v];
-    if (nx == 0 || ny == 0) continue;
-    const float* dfeat = dcat + (long long)V.y[v] * cw + ydim;
-    const float* at = attn + V.a[v];
-    float* dl = dL + V.a[v];
-    const long long xr = (long long)V.x[v] * Hd, yr = (long long)V.y[v] * Hd;
-    // dP = dfeat . xv^T (+ dattn) ; dxv = attn^T . dfeat
-    {
+  // per video: dP = dfeat . xv^T (+ dattn), dxv = attn^T . dfeat  (independent: one grouped launch
+  // for up to two videos), softmax backward, then dyq = dlogit . xk, dxk = dlogit^T . yq (grouped)
+  for (int v0 = 0; v0 < V.n; v0 += 2) {
+    fx_gemm_desc g1[4], g2[4];
+    int n1 = 0, n2 = 0;
+    for (int v = v0; v < std::min(V.n, v0 + 2); ++v) {
+      const int nx = V.x[v + 1] - V.x[v], ny = V.y[v + 1] - V.y[v];
+      if (nx == 0 || ny == 0) continue;
+      const float* dfeat = dcat + (long long)V.y[v] * cw + ydim;
+      const float* at = attn + V.a[v];
+      float* dl = dL + V.a[v];
+      const long long xr = (long long)V.x[v] * Hd, yr = (long long)V.y[v] * Hd;
       fx_gemm_desc d = gemm_desc(ny, nx, Hd, op_rows(dfeat, cw), op_rows(xv + xr, Hd), dl, nx);
       d.resid = dattn ? dattn + V.a[v] : nullptr;
       d.ld_resid = nx;
       d.split_k = pick_split(ny, nx, Hd);
       d.workspace = spl;
-      FX_TRY(launch_gemm(d, s));
-    }
-    {
-      fx_gemm_desc d = gemm_desc(nx, Hd, ny, op_cols(at, nx), op_cols(dfeat, cw), dxv + xr, Hd);
+      g1[n1++] = d;
+      d = gemm_desc(nx, Hd, ny, op_cols(at, nx), op_cols(dfeat, cw), dxv + xr, Hd);
       d.split_k = pick_split(nx, Hd, ny);
       d.workspace = spl;
-      FX_TRY(launch_gemm(d, s));
-    }
-    // dlogit = softmax_bwd(attn, dP) + dlogit_direct   (in place)
-    FX_TRY(launch_softmax_rows_bwd(at, nx, dl, nx, dlogit ? dlogit + V.a[v] : nullptr, nx, ny, nx, 1.f, dl, nx, s));
-    {
-      fx_gemm_desc d = gemm_desc(ny, Hd, nx, op_rows(dl, nx), op_cols(xk + xr, Hd), dyq + yr, Hd);
+      g1[n1++] = d;
+      d = gemm_desc(ny, Hd, nx, op_rows(dl, nx), op_cols(xk + xr, Hd), dyq + yr, Hd);
       d.alpha = scale;
       d.split_k = pick_split(ny, Hd, nx);
       d.workspace = spl;
-      FX_TRY(launch_gemm(d, s));
-    }
-    {
-      fx_gemm_desc d = gemm_desc(nx, Hd, ny, op_cols(dl, nx), op_cols(yq + yr, Hd), dxk + xr, Hd);
+      g2[n2++] = d;
+      d = gemm_desc(nx, Hd, ny, op_cols(dl, nx), op_cols(yq + yr, Hd), dxk + xr, Hd);
       d.alpha = scale;
       d.split_k = pick_split(nx, Hd, ny);
       d.workspace = spl;
-      FX_TRY(launch_gemm(d, s));
+      g2[n2++] = d;
     }
+    FX_TRY(launch_gemm_group(g1, n1, s));
+    // dlogit = softmax_bwd(attn, dP) + dlogit_direct   (in place)
+    for (int v = v0; v < std::min(V.n, v0 + 2); ++v) {
+      const int nx = V.x[v + 1] - V.x[v], ny = V.y[v + 1] - V.y[v];
+      if (nx == 0 || ny == 0) continue;
+      float* dl = dL + V.a[v];
+      FX_TRY(launch_softmax_rows_bwd(attn + V.a[v], nx, dl, nx, dlogit ? dlogit + V.a[v] : nullptr, nx, ny, nx, 1.f,
+                                     dl, nx, s));
+    }
+    FX_TRY(launch_gemm_group(g2, n2, s));
   }
   // projections
   FX_TRY(linear_dwdb(dxk, Hd, xin, ldxin, Nx, xdim, Hd, dwk, dbk, 1, spl, s));

@@ -91,6 +91,16 @@ int linear_fwd_res(const float* x, long long ldx, int M, int K, const float* w, 
 }
 
 // dx = dy . w + resid   (w (N, K) row stride ldw)
+fx_gemm_desc dx_res_desc(const float* dy, long long lddy, const float* w, long long ldw, int M, int K, int N,
+                         const float* resid, long long ldr, float* dx, long long lddx, float* ws) {
+  fx_gemm_desc d = gemm_desc(M, K, N, op_rows(dy, lddy), op_cols(w, ldw), dx, lddx);
+  d.resid = resid;
+  d.ld_resid = ldr;
+  d.split_k = pick_split(M, K, N);
+  d.workspace = ws;
+  return d;
+}
+
 int linear_dx_res(const float* dy, long long lddy, const float* w, long long ldw, int M, int K, int N,
                   const float* resid, long long ldr, float* dx, long long lddx, float* ws, hipStream_t s) {
   fx_gemm_desc d = gemm_desc(M, K, N, op_rows(dy, lddy), op_cols(w, ldw), dx, lddx);
@@ -273,9 +283,7 @@ int fx_decoder_fwd(const fx_decoder_params* p, const float* tgt, long long ldt, 
       FX_TRY(linear_fwd(mem, ldm, T, p->Hm, workspace + L.wkv + (long long)AL * p->Hm, workspace + L.bkv + AL,
                         kv + AL, AL2, AL, 0, s));
       // keep mem + pos for the key weight gradient
-      FX_CHECK_HIP(hipMemcpy2DAsync(saved + L.mpos, p->Hm * sizeof(float), mem, ldm * sizeof(float),
-                                    p->Hm * sizeof(float), T, hipMemcpyDeviceToDevice, s));
-      FX_TRY(add2(mpos, ldmp, nullptr, 0, T, p->Hm, saved + L.mpos, p->Hm, 1, s));
+      FX_TRY(add2(mem, ldm, mpos, ldmp, T, p->Hm, saved + L.mpos, p->Hm, 0, s));
     }
   }
   const float* x = tgt;
@@ -370,8 +378,10 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
   // out_linear and the final LayerNorm
   const float* xl = saved + L.layers + (NL - 1) * L.per_layer + L.t3;   // last layer output
   const float* fin = p->final_norm ? saved + L.fo : xl;
-  FX_TRY(linear_dwdb(dout, lddo, fin, A, R, A, p->out_dim, g->out_w, g->out_b, 1, spl, s));
-  FX_TRY(linear_dx(dout, lddo, p->out_w, R, A, p->out_dim, p->final_norm ? dS : dT, A, 0, nullptr, 0, spl, s));
+  FX_TRY(linear_bwd_pair(desc_linear_dwdb(dout, lddo, fin, A, R, A, p->out_dim, g->out_w, g->out_b, 1, spl),
+                         desc_linear_dx(dout, lddo, p->out_w, R, A, p->out_dim, p->final_norm ? dS : dT, A, 0, nullptr,
+                                        0, spl),
+                         s));
   if (p->final_norm)
     FX_TRY(launch_layernorm_bwd(dS, A, nullptr, 0, saved + L.fxh, A, p->fn_w, saved + L.frs, R, A, 0, dT, A, g->fn_w,
                                 g->fn_b, lnws, s));
@@ -385,43 +395,45 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
     // --- FFN + its LayerNorm:  dU = LN_bwd(dT) ; dF = (dU W2) * (f1 > 0) ; dT2 = dU + dF W1
     FX_TRY(launch_layernorm_bwd(dT, A, nullptr, 0, b + L.xh3, A, p->ln_ff_w[l], b + L.rs3, R, A, 0, dU, A,
                                 g->ln_ff_w[l], g->ln_ff_b[l], lnws, s));
-    FX_TRY(linear_dwdb(dU, A, b + L.f1, FF, R, FF, A, g->ff2_w[l], g->ff2_b[l], 1, spl, s));
-    FX_TRY(linear_dx(dU, A, p->ff2_w[l], R, FF, A, dF, FF, 0, b + L.f1, FF, spl, s));
-    FX_TRY(linear_dwdb(dF, FF, t2, A, R, A, FF, g->ff1_w[l], g->ff1_b[l], 1, spl, s));
-    FX_TRY(linear_dx_res(dF, FF, p->ff1_w[l], A, R, A, FF, dU, A, dT, A, spl, s));   // dT <- dT2
+    FX_TRY(linear_bwd_pair(desc_linear_dwdb(dU, A, b + L.f1, FF, R, FF, A, g->ff2_w[l], g->ff2_b[l], 1, spl),
+                           desc_linear_dx(dU, A, p->ff2_w[l], R, FF, A, dF, FF, 0, b + L.f1, FF, spl), s));
+    FX_TRY(linear_bwd_pair(desc_linear_dwdb(dF, FF, t2, A, R, A, FF, g->ff1_w[l], g->ff1_b[l], 1, spl),
+                           dx_res_desc(dF, FF, p->ff1_w[l], A, R, A, FF, dU, A, dT, A, spl), s));   // dT <- dT2
     if (p->cross) {
       // --- cross-attention + LN2
       FX_TRY(launch_layernorm_bwd(dT, A, nullptr, 0, b + L.xh2, A, p->ln_ca_w[l], b + L.rs2, R, A, 0, dU, A,
                                   g->ln_ca_w[l], g->ln_ca_b[l], lnws, s));
-      FX_TRY(linear_dwdb(dU, A, b + L.oca, A, R, A, A, g->ca_out_w[l], g->ca_out_b[l], 1, spl, s));
-      FX_TRY(linear_dx(dU, A, p->ca_out_w[l], R, A, A, dO, A, 0, nullptr, 0, spl, s));
+      FX_TRY(linear_bwd_pair(desc_linear_dwdb(dU, A, b + L.oca, A, R, A, A, g->ca_out_w[l], g->ca_out_b[l], 1, spl),
+                             desc_linear_dx(dU, A, p->ca_out_w[l], R, A, A, dO, A, 0, nullptr, 0, spl), s));
       const float* kv = saved + L.kv;
       FX_TRY(launch_tattn_bwd(b + L.qc, A, kv + (long long)l * A, AL2, kv + (long long)(NL + l) * A, AL2, b + L.oca, A,
                               dO, A, b + L.pca, nvid, Qv, Tv, hd, h, scale, dq, A, dkv + (long long)l * A, AL2,
                               dkv + (long long)(NL + l) * A, AL2, ws + L.core, s));
       const float* tq = qpos ? b + L.t1q : b + L.t1;
-      FX_TRY(linear_dwdb(dq, A, tq, A, R, A, A, g->ca_q_w[l], g->ca_in_b[l], 1, spl, s));
+      const fx_gemm_desc dwq = desc_linear_dwdb(dq, A, tq, A, R, A, A, g->ca_q_w[l], g->ca_in_b[l], 1, spl);
       if (qpos) {
-        FX_TRY(linear_dx(dq, A, p->ca_q_w[l], R, A, A, P, A, 0, nullptr, 0, spl, s));
+        FX_TRY(linear_bwd_pair(dwq, desc_linear_dx(dq, A, p->ca_q_w[l], R, A, A, P, A, 0, nullptr, 0, spl), s));
         FX_TRY(add_acc(dU, P, dT, G, RA, s));                                     // dT1 = dU + P ; G += P
       } else {
-        FX_TRY(linear_dx_res(dq, A, p->ca_q_w[l], A, R, A, A, dU, A, dT, A, spl, s));
+        FX_TRY(linear_bwd_pair(dwq, dx_res_desc(dq, A, p->ca_q_w[l], A, R, A, A, dU, A, dT, A, spl), s));
       }
     }
     // --- self-attention + LN1
     FX_TRY(launch_layernorm_bwd(dT, A, nullptr, 0, b + L.xh1, A, p->ln_sa_w[l], b + L.rs1, R, A, 0, dU, A,
                                 g->ln_sa_w[l], g->ln_sa_b[l], lnws, s));
-    FX_TRY(linear_dwdb(dU, A, b + L.osa, A, R, A, A, g->sa_out_w[l], g->sa_out_b[l], 1, spl, s));
-    FX_TRY(linear_dx(dU, A, p->sa_out_w[l], R, A, A, dO, A, 0, nullptr, 0, spl, s));
+    FX_TRY(linear_bwd_pair(desc_linear_dwdb(dU, A, b + L.osa, A, R, A, A, g->sa_out_w[l], g->sa_out_b[l], 1, spl),
+                           desc_linear_dx(dU, A, p->sa_out_w[l], R, A, A, dO, A, 0, nullptr, 0, spl), s));
     const float* qkv = b + L.qkv;
     FX_TRY(launch_mha_small_bwd(qkv, 3 * A, qkv + A, 3 * A, qkv + 2 * A, 3 * A, b + L.psa, dO, A, Qv, Qv, hd, h, scale,
                                 dQKV, 3 * A, dQKV + A, 3 * A, dQKV + 2 * A, 3 * A, s, nvid));
     float* dX = l == 0 ? nullptr : dT;   // the next (earlier) layer's output gradient, in place
     if (!qpos) {
-      FX_TRY(linear_dwdb(dQKV, 3 * A, x, ldx, R, A, 3 * A, g->sa_in_w[l], g->sa_in_b[l], 1, spl, s));
+      const fx_gemm_desc dwi = desc_linear_dwdb(dQKV, 3 * A, x, ldx, R, A, 3 * A, g->sa_in_w[l], g->sa_in_b[l], 1, spl);
       if (l > 0 || dtgt)
-        FX_TRY(linear_dx_res(dQKV, 3 * A, p->sa_in_w[l], A, R, A, 3 * A, dU, A, l > 0 ? dX : dtgt,
-                             l > 0 ? A : lddt, spl, s));
+        FX_TRY(linear_bwd_pair(dwi, dx_res_desc(dQKV, 3 * A, p->sa_in_w[l], A, R, A, 3 * A, dU, A, l > 0 ? dX : dtgt,
+                                                l > 0 ? A : lddt, spl), s));
+      else
+        FX_TRY(launch_gemm(dwi, s));
     } else {
       FX_TRY(linear_dwdb(dQKV, 3 * A, xq, ldxq, R, A, 2 * A, g->sa_in_w[l], g->sa_in_b[l], 1, spl, s));
       FX_TRY(linear_dwdb(dQKV + 2 * A, 3 * A, x, ldx, R, A, A, g->sa_in_w[l] + 2LL * A * A, g->sa_in_b[l] + 2 * A, 1,

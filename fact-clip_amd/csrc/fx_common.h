@@ -41,6 +41,9 @@ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 // GEMM (internal C++ view of fx_gemm_desc; see include/factmx.h)
 // ------------------------------------------------------------------------
 int launch_gemm(const fx_gemm_desc& d, hipStream_t s);
+// independent GEMMs (disjoint outputs, at most one split-K workspace user) in one launch when all take
+// the direct (small-shape) kernel, else launched one by one in order
+int launch_gemm_group(const fx_gemm_desc* d, int n, hipStream_t s);
 
 // Bound on the split-K slabs of the GEMMs issued while one of these is alive (thread-local, nests):
 // launch_gemm refuses a split whose slabs would leave [base, base + floats) -- a too-small

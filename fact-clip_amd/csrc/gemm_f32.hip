@@ -890,14 +890,47 @@ __global__ __launch_bounds__(W8T) void gemm_f32_wide8_kernel(GemmDev g) {
   tile_epilogue(g, bidx, rbase, col, acc);
 }
 
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmDev g) {
+// Separate split-K reduce: a thread sums 4 consecutive elements (float4 over the slabs when M*N % 4 == 0
+// and the workspace is 16-B aligned) with up to 8 slab loads in flight, slabs added in order
+// (deterministic); the epilogue runs per element.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmDev g, int vec) {
   const long long total = (long long)g.M * g.N;
   const int bidx = blockIdx.y;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int sk = 0; sk < g.split; ++sk) s += g.ws[((long long)bidx * g.split + sk) * total + i];
-    epilogue_store(g, bidx, (int)(i / g.N), (int)(i % g.N), s);
+  const float* ws = g.ws + (long long)bidx * g.split * total;
+  const long long n4 = (total + 3) >> 2;
+  for (long long i4 = (long long)blockIdx.x * blockDim.x + threadIdx.x; i4 < n4; i4 += (long long)gridDim.x * blockDim.x) {
+    const long long i = i4 * 4;
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    if (vec) {
+      for (int k0 = 0; k0 < g.split; k0 += 8) {
+        float4 x[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          x[j] = *reinterpret_cast<const float4*>(ws + (long long)min(k0 + j, g.split - 1) * total + i);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (k0 + j < g.split) {
+            s[0] += x[j].x;
+            s[1] += x[j].y;
+            s[2] += x[j].z;
+            s[3] += x[j].w;
+          }
+        }
+      }
+    } else {
+      for (int e = 0; e < 4; ++e)
+        if (i + e < total)
+          for (int k = 0; k < g.split; ++k) s[e] += ws[(long long)k * total + i + e];
+    }
+    int m = (int)(i / g.N), n = (int)(i - (long long)m * g.N);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (i + e < total) epilogue_store(g, bidx, m, n, s[e]);
+      if (++n == g.N) {
+        n = 0;
+        ++m;
+      }
+    }
   }
 }
 
@@ -958,12 +991,11 @@ __device__ __forceinline__ void direct_finish(const GemmDev& g, int bidx, int sk
 }
 
 template <int AK, int BKd>
-__global__ __launch_bounds__(DMAXW * 64) void gemm_direct_kernel(GemmDev g) {
-  __shared__ float red[DMAXW * 16 * 64 + 1];   // wave partials + the split-K "last block" flag
+__device__ __forceinline__ void direct_body(const GemmDev& g, int bx, int by, int z, float* red) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
   const int li = lane & 31, lh = lane >> 5;
-  const int n0 = blockIdx.x * 32, m0 = blockIdx.y * 32;
-  const int z = blockIdx.z, bidx = z / g.split, sk = z - bidx * g.split;
+  const int n0 = bx * 32, m0 = by * 32;
+  const int bidx = z / g.split, sk = z - bidx * g.split;
   const int nch = (g.K + DCH - 1) / DCH;
   const int c0 = sk * g.kt_per_split, c1 = min(nch, c0 + g.kt_per_split);
   const float* pa = g.a.ptr + (long long)bidx * g.a.batch_stride;
@@ -1029,8 +1061,49 @@ __global__ __launch_bounds__(DMAXW * 64) void gemm_direct_kernel(GemmDev g) {
     for (int r = 0; r < 16; ++r) direct_finish(g, bidx, sk, m0 + (r & 3) + 8 * (r >> 2) + 4 * lh, n0 + li, acc[r]);
   }
   if (g.split > 1 && g.tile_cnt)
-    splitk_finish<32, 32>(g, bidx, m0, n0, (bidx * g.tiles_y + blockIdx.y) * g.tiles_x + blockIdx.x,
+    splitk_finish<32, 32>(g, bidx, m0, n0, (bidx * g.tiles_y + by) * g.tiles_x + bx,
                           reinterpret_cast<int*>(&red[DMAXW * 16 * 64]));
+}
+
+template <int AK, int BKd>
+__global__ __launch_bounds__(DMAXW * 64) void gemm_direct_kernel(GemmDev g) {
+  __shared__ float red[DMAXW * 16 * 64 + 1];   // wave partials + the split-K "last block" flag
+  direct_body<AK, BKd>(g, blockIdx.x, blockIdx.y, blockIdx.z, red);
+}
+
+// Several independent small GEMMs in ONE launch (e.g. the dW/db and dX GEMMs of one linear layer, both
+// reading the same dY): the flat block index picks the problem (block-uniform), each problem keeps
+// its own grid, operand kinds, split and epilogue.  Saves a launch (~2.7 us back to back) per member.
+constexpr int GMAX = 4;
+struct GemmGroup {
+  GemmDev g[GMAX];
+  int kinds[GMAX];         // ak * 8 + bk
+  int start[GMAX + 1];     // first flat block of each problem
+  int n;
+};
+
+__device__ __forceinline__ void direct_dispatch(const GemmDev& g, int kinds, int local, float* red) {
+  const int txy = g.tiles_x * g.tiles_y;
+  const int z = local / txy, r = local - z * txy, by = r / g.tiles_x, bx = r - by * g.tiles_x;
+  switch (kinds) {
+    case ROWS * 8 + ROWS: direct_body<ROWS, ROWS>(g, bx, by, z, red); break;
+    case ROWS * 8 + COLS: direct_body<ROWS, COLS>(g, bx, by, z, red); break;
+    case ROWS_GEN * 8 + ROWS: direct_body<ROWS_GEN, ROWS>(g, bx, by, z, red); break;
+    case ROWS_GEN * 8 + COLS: direct_body<ROWS_GEN, COLS>(g, bx, by, z, red); break;
+    case COLS * 8 + ROWS: direct_body<COLS, ROWS>(g, bx, by, z, red); break;
+    case COLS * 8 + COLS: direct_body<COLS, COLS>(g, bx, by, z, red); break;
+    default: break;
+  }
+}
+
+__global__ __launch_bounds__(DMAXW * 64) void gemm_direct_group_kernel(GemmGroup G) {
+  __shared__ float red[DMAXW * 16 * 64 + 1];
+  const int id = blockIdx.x;
+  // constant member indices only (a runtime index into the kernel argument would copy it to scratch)
+  if (id < G.start[1]) direct_dispatch(G.g[0], G.kinds[0], id, red);
+  else if (id < G.start[2]) direct_dispatch(G.g[1], G.kinds[1], id - G.start[1], red);
+  else if (id < G.start[3]) direct_dispatch(G.g[2], G.kinds[2], id - G.start[2], red);
+  else direct_dispatch(G.g[3], G.kinds[3], id - G.start[3], red);
 }
 
 // bias-gradient column sums, two deterministic stages (used only where no dW GEMM carries them)
@@ -1311,9 +1384,20 @@ long long gemm_workspace_floats(const fx_gemm_desc& d) {
   return (long long)d.batch * d.split_k * d.M * d.N;
 }
 
-int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
+namespace {
+
+struct GemmPlan {
+  GemmDev g;
+  dim3 grid, block;
+  int ak, bk;
+  bool direct, wide;
+};
+
+// Everything launch_gemm decides before launching: operand kinds, kernel, tiles, split, counters.
+// tile_cnt_base: first arrival counter this launch may use (problems of one grouped launch get
+// disjoint counter ranges).
+int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_cnt_base = 0) {
   FX_REQUIRE(d.M >= 0 && d.N >= 0 && d.K >= 0 && d.batch >= 1, "gemm: bad sizes");
-  if (d.M == 0 || d.N == 0) return FX_OK;
   FX_REQUIRE(d.a.ptr && d.b.ptr && d.c, "gemm: null operand");
   FX_REQUIRE(!(d.a.conv_taps && d.a.seq_len <= 0) && !(d.b.conv_taps && d.b.seq_len <= 0),
              "gemm: conv operand needs seq_len");
@@ -1322,7 +1406,8 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
              "gemm: conv B needs N == taps*cin (+1 with a ones column)");
   FX_REQUIRE(!(d.a.ones_col && !d.a.trans) && !(d.b.ones_col && !d.b.trans), "gemm: ones_col needs trans==1");
   FX_REQUIRE(!(d.b.conv_taps && !d.b.trans), "gemm: row-major conv B operand is not supported");
-  GemmDev g{};
+  GemmDev& g = P.g;
+  g = GemmDev{};
   g.M = d.M;
   g.N = d.N;
   g.K = d.K;
@@ -1359,6 +1444,8 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
   }();
   g.w8_stagger = stagger;
   const int ak = kind_of(d.a, g.a_vec), bk = kind_of(d.b, g.b_vec);
+  P.ak = ak;
+  P.bk = bk;
   const bool direct = use_direct(d, ak, bk);
   bool wide = false;
   const int cap = (d.split_k > 1 && d.workspace) ? d.split_k : 1;   // workspace holds `cap` slabs
@@ -1396,27 +1483,118 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
   // in-launch reduction only while the last block's serial slab read stays small (<= 32 KB per
   // tile); bigger ones pay less as a separate reduce launch (conv dW split 5: 78 vs 56 us)
   const long long slab_bytes = (long long)g.split * (direct ? 32 * 32 : (wide ? WBM : BM) * BN) * 4;
-  if (g.split > 1 && slab_bytes <= 32768 && (long long)g.tiles_x * g.tiles_y * d.batch <= kMaxTileCounters)
-    g.tile_cnt = tile_counters(s);
+  if (g.split > 1 && slab_bytes <= 32768 &&
+      tile_cnt_base + (long long)g.tiles_x * g.tiles_y * d.batch <= kMaxTileCounters) {
+    unsigned* pool = tile_counters(s);
+    g.tile_cnt = pool ? pool + tile_cnt_base : nullptr;
+  }
+  P.grid = grid;
+  P.block = block;
+  P.direct = direct;
+  P.wide = wide;
+  return FX_OK;
+}
+
+void log_gemm(const fx_gemm_desc& d, const GemmPlan& P) {
   // FX_GEMM_LOG=<file>: append one line per launch (diagnostic shape census, tools/gemm_census.py)
   static FILE* glog = [] {
     const char* p = std::getenv("FX_GEMM_LOG");
     return p ? std::fopen(p, "a") : nullptr;
   }();
   if (glog)
-    std::fprintf(glog, "%d %d %d %d %d %d %d %d %d %d %d\n", d.M, d.N, d.K, d.batch, ak, bk, g.split,
-                 d.a.conv_taps, d.b.conv_taps, d.relu, direct ? (int)block.x / 64 : (wide ? -1 : 0));
-  int st = direct ? launch_direct(ak, bk, grid, block, s, g)
-                  : (wide ? (wide8() ? launch_wide8(ak, bk, grid, s, g) : launch_wide(ak, bk, grid, s, g))
-                          : launch_tiled(ak, bk, grid, s, g));
-  if (st != FX_OK) return st;
-  FX_CHECK_HIP(hipGetLastError());
-  if (g.split > 1 && !g.tile_cnt) {
+    std::fprintf(glog, "%d %d %d %d %d %d %d %d %d %d %d\n", d.M, d.N, d.K, d.batch, P.ak, P.bk, P.g.split,
+                 d.a.conv_taps, d.b.conv_taps, d.relu, P.direct ? (int)P.block.x / 64 : (P.wide ? -1 : 0));
+}
+
+int launch_reduce(const fx_gemm_desc& d, const GemmPlan& P, hipStream_t s) {
+  if (P.g.split > 1 && !P.g.tile_cnt) {
     const long long total = (long long)d.M * d.N;
-    int blocks = (int)std::min<long long>(cdiv(total, 256), 2048);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks, d.batch), dim3(256), 0, s, g);
+    const int vec = (total % 4) == 0 && ((uintptr_t)P.g.ws & 15) == 0;
+    int blocks = (int)std::min<long long>(cdiv(cdiv(total, 4), 256), 2048);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks, d.batch), dim3(256), 0, s, P.g, vec);
     FX_CHECK_HIP(hipGetLastError());
   }
+  return FX_OK;
+}
+
+}  // namespace
+
+int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
+  FX_REQUIRE(d.M >= 0 && d.N >= 0 && d.K >= 0 && d.batch >= 1, "gemm: bad sizes");
+  if (d.M == 0 || d.N == 0) return FX_OK;
+  GemmPlan P;
+  FX_TRY(plan_gemm(d, s, P));
+  log_gemm(d, P);
+  const GemmDev& g = P.g;
+  int st = P.direct ? launch_direct(P.ak, P.bk, P.grid, P.block, s, g)
+                    : (P.wide ? (wide8() ? launch_wide8(P.ak, P.bk, P.grid, s, g) : launch_wide(P.ak, P.bk, P.grid, s, g))
+                              : launch_tiled(P.ak, P.bk, P.grid, s, g));
+  if (st != FX_OK) return st;
+  FX_CHECK_HIP(hipGetLastError());
+  return launch_reduce(d, P, s);
+}
+
+// Independent GEMMs (no member reads another's output; disjoint outputs and workspaces) in one
+// launch when every member takes the direct kernel; otherwise one launch each, in order.
+// FX_GEMM_GROUP=0 disables the grouping (diagnostic A/B).
+int launch_gemm_group(const fx_gemm_desc* d, int n, hipStream_t s) {
+  static const bool on = [] {
+    const char* p = std::getenv("FX_GEMM_GROUP");
+    return !(p && p[0] == '0');
+  }();
+  FX_REQUIRE(n >= 0 && n <= GMAX, "gemm group: 0..4 members");
+  int live = 0, nsplit = 0;   // members with M, N > 0; of those, split-K members
+  bool all_direct = on;
+  GemmPlan P[GMAX];
+  long long cnt_base = 0;
+  for (int i = 0; i < n && all_direct; ++i) {
+    FX_REQUIRE(d[i].M >= 0 && d[i].N >= 0 && d[i].K >= 0 && d[i].batch >= 1, "gemm: bad sizes");
+    if (d[i].M == 0 || d[i].N == 0) continue;
+    FX_TRY(plan_gemm(d[i], s, P[i], cnt_base));
+    if (P[i].g.tile_cnt) cnt_base += (long long)P[i].g.tiles_x * P[i].g.tiles_y * d[i].batch;
+    all_direct = all_direct && P[i].direct;
+    nsplit += P[i].g.split > 1 ? 1 : 0;
+    ++live;
+  }
+  // split members given the same workspace get consecutive slab ranges in it (checked against the
+  // entry point's reservation); split members on different workspaces are not grouped
+  bool ws_ok = true;
+  if (all_direct && nsplit > 1) {
+    const float* base = nullptr;
+    long long off = 0;
+    for (int i = 0; i < n && ws_ok; ++i) {
+      if (d[i].M == 0 || d[i].N == 0 || P[i].g.split <= 1) continue;
+      if (!base) base = d[i].workspace;
+      ws_ok = d[i].workspace == base && t_ws_hi != nullptr;
+      P[i].g.ws = d[i].workspace + off;
+      off += (long long)P[i].g.split * d[i].M * d[i].N * d[i].batch;
+      ws_ok = ws_ok && P[i].g.ws >= t_ws_lo && P[i].g.ws + (long long)P[i].g.split * d[i].M * d[i].N * d[i].batch <= t_ws_hi;
+    }
+  }
+  if (!all_direct || live < 2 || !ws_ok) {
+    for (int i = 0; i < n; ++i) FX_TRY(launch_gemm(d[i], s));
+    return FX_OK;
+  }
+  GemmGroup G{};
+  unsigned nw = 64;
+  int m = 0;
+  G.start[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    if (d[i].M == 0 || d[i].N == 0) continue;
+    log_gemm(d[i], P[i]);
+    G.g[m] = P[i].g;
+    const int ak = P[i].ak == ROWS_CAT ? ROWS_GEN : P[i].ak;
+    G.kinds[m] = ak * 8 + P[i].bk;
+    G.start[m + 1] = G.start[m] + (int)(P[i].grid.x * P[i].grid.y * P[i].grid.z);
+    nw = std::max(nw, P[i].block.x);
+    ++m;
+  }
+  for (int i = m + 1; i <= GMAX; ++i) G.start[i] = G.start[m];
+  G.n = m;
+  hipLaunchKernelGGL(gemm_direct_group_kernel, dim3(G.start[m]), dim3(nw), 0, s, G);
+  FX_CHECK_HIP(hipGetLastError());
+  for (int i = 0; i < n; ++i)
+    if (d[i].M != 0 && d[i].N != 0) FX_TRY(launch_reduce(d[i], P[i], s));
   return FX_OK;
 }
 

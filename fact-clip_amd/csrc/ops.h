@@ -64,6 +64,14 @@ int linear_dwdb(const float* dy, long long lddy, const float* x, long long ldx, 
 int linear_dw(const float* dy, long long lddy, const float* x, long long ldx, int M, int K, int N, float* dw,
               int accumulate, float* ws, hipStream_t s, long long lddw = -1);
 long long dwdb_ws(int M, int K, int N);
+// the same products as descriptors, for launch_gemm_group / linear_bwd_pair
+fx_gemm_desc desc_linear_dx(const float* dy, long long lddy, const float* w, int M, int K, int N, float* dx,
+                            long long lddx, int accumulate, const float* gate, long long ld_gate, float* ws,
+                            long long ldw = -1);
+fx_gemm_desc desc_linear_dwdb(const float* dy, long long lddy, const float* x, long long ldx, int M, int K, int N,
+                              float* dw, float* db, int accumulate, float* ws, long long lddw = -1);
+// dW/db and dX of one linear layer from the same dY: one launch when both are direct-kernel shapes
+int linear_bwd_pair(const fx_gemm_desc& dwdb, const fx_gemm_desc& dx, hipStream_t s);
 
 // ---- fused small multi-head attention (attn_small.hip): Lq, Lk, head_dim <= 64 ----
 // nvid independent problems stacked by rows (video v: q/o rows v*Lq.., k/v rows v*Lk..);

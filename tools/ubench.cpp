@@ -82,8 +82,8 @@ int main() {
     gemm_case("tok dW+db beta1 (cols,cols+1)", 256, 257, 32, cols(big, 256), bo, c, 256, 1, nullptr, 1.f, c + 300000);
   }
   {
-    float* xh = dalloc(64 * 1024, 1.f);
-    float* rs = dalloc(1024, 1.f);
+    float* xh = dalloc(4096 * 256, 1.f);   // sized for the 4096-row (frames) case
+    float* rs = dalloc(4096, 1.f);
     float* lw = dalloc(1024, 1.f);
     float* dw = dalloc(1024, 0.f);
     float* lws = dalloc(1 << 20, 0.f);
