@@ -1495,15 +1495,16 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
   return FX_OK;
 }
 
-void log_gemm(const fx_gemm_desc& d, const GemmPlan& P) {
+// member: index inside a grouped launch (members > 0 share the kernel of member 0)
+void log_gemm(const fx_gemm_desc& d, const GemmPlan& P, int member = 0) {
   // FX_GEMM_LOG=<file>: append one line per launch (diagnostic shape census, tools/gemm_census.py)
   static FILE* glog = [] {
     const char* p = std::getenv("FX_GEMM_LOG");
     return p ? std::fopen(p, "a") : nullptr;
   }();
   if (glog)
-    std::fprintf(glog, "%d %d %d %d %d %d %d %d %d %d %d\n", d.M, d.N, d.K, d.batch, P.ak, P.bk, P.g.split,
-                 d.a.conv_taps, d.b.conv_taps, d.relu, P.direct ? (int)P.block.x / 64 : (P.wide ? -1 : 0));
+    std::fprintf(glog, "%d %d %d %d %d %d %d %d %d %d %d %d\n", d.M, d.N, d.K, d.batch, P.ak, P.bk, P.g.split,
+                 d.a.conv_taps, d.b.conv_taps, d.relu, P.direct ? (int)P.block.x / 64 : (P.wide ? -1 : 0), member);
 }
 
 int launch_reduce(const fx_gemm_desc& d, const GemmPlan& P, hipStream_t s) {
@@ -1575,24 +1576,34 @@ int launch_gemm_group(const fx_gemm_desc* d, int n, hipStream_t s) {
     for (int i = 0; i < n; ++i) FX_TRY(launch_gemm(d[i], s));
     return FX_OK;
   }
-  GemmGroup G{};
-  unsigned nw = 64;
-  int m = 0;
-  G.start[0] = 0;
-  for (int i = 0; i < n; ++i) {
-    if (d[i].M == 0 || d[i].N == 0) continue;
-    log_gemm(d[i], P[i]);
-    G.g[m] = P[i].g;
-    const int ak = P[i].ak == ROWS_CAT ? ROWS_GEN : P[i].ak;
-    G.kinds[m] = ak * 8 + P[i].bk;
-    G.start[m + 1] = G.start[m] + (int)(P[i].grid.x * P[i].grid.y * P[i].grid.z);
-    nw = std::max(nw, P[i].block.x);
-    ++m;
+  // one launch per distinct block size: a member planned with fewer waves per tile would otherwise run
+  // with idle waves in every block (measured: a K = 32 member beside a K = 4096 one, 2x slower)
+  bool done[GMAX] = {};
+  for (int i0 = 0; i0 < n; ++i0) {
+    if (done[i0] || d[i0].M == 0 || d[i0].N == 0) continue;
+    const unsigned nw = P[i0].block.x;
+    GemmGroup G{};
+    int m = 0;
+    G.start[0] = 0;
+    for (int i = i0; i < n; ++i) {
+      if (done[i] || d[i].M == 0 || d[i].N == 0 || P[i].block.x != nw) continue;
+      done[i] = true;
+      log_gemm(d[i], P[i], m);
+      G.g[m] = P[i].g;
+      const int ak = P[i].ak == ROWS_CAT ? ROWS_GEN : P[i].ak;
+      G.kinds[m] = ak * 8 + P[i].bk;
+      G.start[m + 1] = G.start[m] + (int)(P[i].grid.x * P[i].grid.y * P[i].grid.z);
+      ++m;
+    }
+    for (int i = m + 1; i <= GMAX; ++i) G.start[i] = G.start[m];
+    G.n = m;
+    if (m == 1) {
+      FX_TRY(P[i0].direct ? launch_direct(P[i0].ak, P[i0].bk, P[i0].grid, P[i0].block, s, P[i0].g) : FX_ERR_UNSUPPORTED);
+    } else {
+      hipLaunchKernelGGL(gemm_direct_group_kernel, dim3(G.start[m]), dim3(nw), 0, s, G);
+    }
+    FX_CHECK_HIP(hipGetLastError());
   }
-  for (int i = m + 1; i <= GMAX; ++i) G.start[i] = G.start[m];
-  G.n = m;
-  hipLaunchKernelGGL(gemm_direct_group_kernel, dim3(G.start[m]), dim3(nw), 0, s, G);
-  FX_CHECK_HIP(hipGetLastError());
   for (int i = 0; i < n; ++i)
     if (d[i].M != 0 && d[i].N != 0) FX_TRY(launch_reduce(d[i], P[i], s));
   return FX_OK;

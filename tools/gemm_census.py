@@ -10,9 +10,12 @@ KIND = ["rows", "rconv", "rgen", "cols", "cconv", "rcat"]
 
 
 def main(log_path, trace_path):
+    # one kernel per log line, except the members > 0 of a grouped launch (12th field), which share
+    # the kernel of the line before: their time is booked to the group's first line
     shapes = [tuple(int(v) for v in ln.split()) for ln in open(log_path) if ln.strip()]
+    shapes = [sh for sh in shapes if len(sh) < 12 or sh[11] == 0]
     rows = sorted(csv.DictReader(open(trace_path)), key=lambda r: int(r["Start_Timestamp"]))
-    g = [r for r in rows if "gemm_f32_kernel" in r["Kernel_Name"] or "gemm_f32_wide" in r["Kernel_Name"] or "gemm_direct_kernel" in r["Kernel_Name"]]
+    g = [r for r in rows if "gemm_f32_kernel" in r["Kernel_Name"] or "gemm_f32_wide" in r["Kernel_Name"] or "gemm_direct_kernel" in r["Kernel_Name"] or "gemm_direct_group" in r["Kernel_Name"]]
     red = [r for r in rows if "splitk_reduce" in r["Kernel_Name"]]
     n = min(len(g), len(shapes))
     g, shapes = g[-n:], shapes[-n:]
