@@ -161,6 +161,35 @@ def traffic_from_profiles(kernel_prefix):
     return None
 
 
+def bf16_mode(net, step, nv, T, steps, warmup, fxf):
+    """Time `steps` fixed-weight steps with fx_set_gemm_precision(FX_PREC_BF16) and compare its frame
+    logits (last block, every video) and TDU segment counts with the fp32 path's."""
+    def logits():
+        step()
+        torch.cuda.synchronize()
+        return [r["frame_clogit"].detach().clone() for r in net.block_list[-1]._vrec], video_segments(net)
+    z32, s32 = logits()
+    with fxf.gemm_precision("bf16"):
+        z16, s16 = logits()
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    dev = max((a - b).abs().max().item() for a, b in zip(z16, z32))
+    scale = max(b.abs().max().item() for b in z32)
+    agree = sum(int((a.argmax(-1) == b.argmax(-1)).sum()) for a, b in zip(z16, z32)) / sum(b.shape[0] for b in z32)
+    return dict(value=round(nv * T * steps / el, 1), unit="frames/s", ms_per_step=round(1e3 * el / steps, 3),
+                dtype="bf16 products, fp32 accumulation/storage (FX_PREC_BF16)",
+                frame_logit_max_abs_dev=round(dev, 5), frame_logit_max_abs=round(scale, 4),
+                frame_argmax_agreement=round(agree, 5), tdu_segments=s16, tdu_segments_fp32=s32,
+                note="same weights and videos as the fp32 line; weight-gradient GEMMs, attention, "
+                     "normalisation and losses stay fp32")
+
+
 def prof_collect(lib, kind):
     """(total ms, flops, bytes, launches) of the HIP-event timed launches of one profiling kind."""
     from factmx import native
@@ -238,6 +267,7 @@ def main():
     ap.add_argument("--adam-steps", type=int, default=None,
                     help="extra timed steps with clip_grad_norm_ + Adam after the fixed-weight steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-bf16", action="store_true", help="skip the bf16-mode extra measurement (N=1 only)")
     args = ap.parse_args()
     cfg, D, C, T_def, vids_def, clip, metric = workload(args.config)
     T = args.T or T_def
@@ -304,6 +334,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
 
+    # BASELINE configs[1]: the same fixed-weight step with the frame-level GEMMs in bf16 arithmetic
+    # (FX_PREC_BF16, fp32 accumulation / storage), its frame-logit deviation from the fp32 path on the
+    # same weights and videos, and its TDU segment counts (N=1 only; the headline stays fp32)
+    bf16 = None
+    if world == 1 and not args.no_bf16:
+        from factmx import functional as fxf
+        bf16 = bf16_mode(net, step, nv, T, args.steps, args.warmup, fxf)
+
     # the reference train step (clip_grad_norm_ + Adam), timed after the fixed-weight steps
     adam = None
     if adam_steps > 0:
@@ -354,7 +392,8 @@ def main():
                                 videos_per_rank=nv, global_batch=world * nv, seq_len=T,
                                 parallelism=f"dp{world}", weights="fixed (no optimizer update in the timed steps)",
                                 tdu_segments=S, tdu_segments_after_timing=S_after),
-                    roofline=roofline, roofline_attention=roofline_attention, train_step_with_adam=adam)
+                    roofline=roofline, roofline_attention=roofline_attention, train_step_with_adam=adam,
+                    bf16_mode=bf16)
         if world == 1 and not args.no_cpu_baseline:
             cb, step_flops, S_oracle = cpu_baseline(args.config, T, seeds)
             line["cpu_baseline"] = cb

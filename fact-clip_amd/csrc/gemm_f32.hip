@@ -23,6 +23,7 @@
 //   col-major kinds -> LDS image [k][row], stride 65 (b32 reads conflict-free over 64 lanes)
 // Blocks are remapped so that consecutive output tiles share an XCD (L2).
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <map>
@@ -890,6 +891,180 @@ __global__ __launch_bounds__(W8T) void gemm_f32_wide8_kernel(GemmDev g) {
   tile_epilogue(g, bidx, rbase, col, acc);
 }
 
+// ---------------------------------------------------------------- bf16 arithmetic (FX_PREC_BF16)
+// The precision mode's frame-level GEMM: the same 128 x 64 tile, 8 waves and operand loaders as the
+// f32 wide8 kernel, fp32 storage and fp32 accumulation, but the products on
+// v_mfma_f32_32x32x16_bf16 (16x the f32 MFMA rate): each stage's fp32 float4 loads are rounded to
+// bf16 (v_cvt_pk_bf16_f32, round to nearest even) when they are written to LDS, so the LDS images
+// are half the bytes ([row][k] bf16, 144-B rows: ds_write_b64 in, conflict-free ds_read_b128 out,
+// one read = one MFMA operand).  Lane half h of an MFMA takes k in [32h, 32h + 32) of the 64-deep
+// stage (8 per instruction), for A and B alike.  With 4 MFMAs per wave per stage the loop is bound
+// by operand delivery, not the matrix core, so the ring is deeper than the f32 kernel's: 4 LDS
+// slots and 3 register sets, a stage's loads issued 5 stages ahead of its MFMAs and written to LDS
+// 2 stages after they were issued.  A row-major (forward and input-gradient GEMMs), B row- or
+// column-major (W or W^T); weight gradients (A column-major) stay on the f32 kernels.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+constexpr int BRS = 72;                 // bf16 row stride of a [row][k] stage image (144 B)
+constexpr int BIMG = 64 * BRS;          // bf16 per operand image
+constexpr int BSLOT = 3 * BIMG;         // [A0 | A1 | B]
+constexpr int BNSL = 4;                 // LDS slots
+constexpr int BLAG = 5;                 // stages between a load and the MFMAs that use it
+
+// Row-major kinds: a thread's float4 is 4 consecutive k of one row -> one 8-byte LDS write.
+// COLS (B = W stored [k][n], the input-gradient products): the float4 is 4 consecutive rows n at one
+// k, written transposed into the [n][k] image as 4 two-byte writes (same bytes, 4x the instructions).
+template <int KIND>
+__device__ __forceinline__ void store_bf16(const Loader<KIND, true, 2>& L, __bf16* img, const float4* v, unsigned vm) {
+  if (Loader<KIND, true, 2>::kRowImg) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float4 x = ((vm >> j) & 1u) ? v[j] : zero4();
+      bf16x4 b;
+      b[0] = (__bf16)x.x;
+      b[1] = (__bf16)x.y;
+      b[2] = (__bf16)x.z;
+      b[3] = (__bf16)x.w;
+      *reinterpret_cast<bf16x4*>(img + (L.ta + 32 * j) * BRS + L.tb) = b;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float e[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float one = ((L.omask >> q) & 1u) ? 1.f : 0.f;
+        const float x = ((L.emask >> q) & 1u) ? e[q] : one;
+        img[(L.tb + q) * BRS + L.ta + 32 * j] = (__bf16)x;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ bf16x8 bfrag(const __bf16* img, int row, int h, int q) {
+  return *reinterpret_cast<const bf16x8*>(img + row * BRS + 32 * h + 8 * q);
+}
+
+template <int AK, int BKd>
+struct BfSet {
+  float4 a0[2], a1[2], b[2];
+  unsigned m0, m1, mb;
+};
+
+template <int AK, int BKd>
+__device__ __forceinline__ void bf_load(const Loader<AK, true, 2>& la0, const Loader<AK, true, 2>& la1,
+                                        const Loader<BKd, true, 2>& lb, int k0, BfSet<AK, BKd>& r) {
+  la0.load(k0, r.a0, r.m0);
+  la1.load(k0, r.a1, r.m1);
+  lb.load(k0, r.b, r.mb);
+}
+
+template <int AK, int BKd>
+__device__ __forceinline__ void bf_store(const Loader<AK, true, 2>& la0, const Loader<AK, true, 2>& la1,
+                                         const Loader<BKd, true, 2>& lb, __bf16* slot, const BfSet<AK, BKd>& r) {
+  store_bf16<AK>(la0, slot, r.a0, r.m0);
+  store_bf16<AK>(la1, slot + BIMG, r.a1, r.m1);
+  store_bf16<BKd>(lb, slot + 2 * BIMG, r.b, r.mb);
+}
+
+template <int AK, int BKd>
+__global__ __launch_bounds__(W8T) void gemm_bf16_wide8_kernel(GemmDev g) {
+  __shared__ __bf16 lds[BNSL * BSLOT];
+  __shared__ int flag[1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, li = lane & 31, lh = lane >> 5;
+  const int ai = wm >> 1, wr = (wm & 1) * 32;
+  int tx, ty;
+  {
+    const int nt = g.tiles_x * g.tiles_y;
+    const int id = blockIdx.y * g.tiles_x + blockIdx.x;
+    const int q = nt / 8, rr = nt % 8, x8 = id % 8, i8 = id / 8;
+    const int nid = (x8 < rr ? x8 * (q + 1) : rr * (q + 1) + (x8 - rr) * q) + i8;
+    ty = nid / g.tiles_x;
+    tx = nid - ty * g.tiles_x;
+  }
+  const int n0 = tx * BN, m0 = ty * WBM;
+  const int z = blockIdx.z, bidx = z / g.split, sk = z - bidx * g.split;
+  const int nkt = (g.K + BK - 1) / BK;
+  const int kt0 = sk * g.kt_per_split;
+  const int kt1 = min(nkt, kt0 + g.kt_per_split);
+  Loader<AK, true, 2> la0, la1;
+  Loader<BKd, true, 2> lb;
+  const float* pa = g.a.ptr + (long long)bidx * g.a.batch_stride;
+  la0.init(g.a, pa, m0, g.M, g.K, tid);
+  la1.init(g.a, pa, m0 + BM, g.M, g.K, tid);
+  lb.init(g.b, g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid);
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    acc0[i] = 0.f;
+    acc1[i] = 0.f;
+  }
+  const int n = kt1 - kt0;
+  if (n > 0) {
+    const int klast = (kt1 - 1) * BK;
+    auto kof = [&](int i) { return min((kt0 + i) * BK, klast); };
+    // prologue: stages 0..2 staged in LDS slots 0..2, stages 3 and 4 in flight (register sets)
+    BfSet<AK, BKd> r0, r1, r2;
+    bf_load<AK, BKd>(la0, la1, lb, kof(0), r0);
+    bf_load<AK, BKd>(la0, la1, lb, kof(1), r1);
+    bf_load<AK, BKd>(la0, la1, lb, kof(2), r2);
+    bf_store<AK, BKd>(la0, la1, lb, lds, r0);
+    bf_load<AK, BKd>(la0, la1, lb, kof(3), r0);
+    bf_store<AK, BKd>(la0, la1, lb, lds + BSLOT, r1);
+    bf_load<AK, BKd>(la0, la1, lb, kof(4), r1);
+    bf_store<AK, BKd>(la0, la1, lb, lds + 2 * BSLOT, r2);
+    __syncthreads();
+    // stage i: MFMAs on slot i % 4; loads of stage i + 5 into one set; the set loaded at stage i - 2
+    // (stage i + 3) written to slot (i + 3) % 4 -- the slot read at stage i - 1, free after the barrier
+    auto stage = [&](int i, BfSet<AK, BKd>& ld, const BfSet<AK, BKd>& st) FX_INLINE {
+      const __bf16* cur = lds + (i & 3) * BSLOT;
+      const __bf16* ia = cur + ai * BIMG;
+      const __bf16* ib = cur + 2 * BIMG;
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        fa[q] = bfrag(ia, wr + li, lh, q);
+        fb[q] = bfrag(ib, wn * 32 + li, lh, q);
+      }
+      bf_load<AK, BKd>(la0, la1, lb, kof(i + BLAG), ld);
+      __builtin_amdgcn_sched_barrier(0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[2], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[3], fb[3], acc1, 0, 0, 0);
+      bf_store<AK, BKd>(la0, la1, lb, lds + ((i + 3) & 3) * BSLOT, st);
+      __syncthreads();
+    };
+    // register sets rotate with period 3: at stage i, load into set i % 3 ... the set stored is the
+    // one loaded two stages earlier, (i + 1) % 3
+    int i = 0;
+    for (; i + 2 < n; i += 3) {
+      stage(i, r2, r0);        // loads stage i+5 -> r2; stores stage i+3 (r0, loaded at i-2)
+      stage(i + 1, r0, r1);    // loads i+6 -> r0; stores i+4 (r1)
+      stage(i + 2, r1, r2);    // loads i+7 -> r1; stores i+5 (r2)
+    }
+    if (i < n) stage(i, r2, r0);
+    if (i + 1 < n) stage(i + 1, r0, r1);
+  }
+  const f32x16 acc = acc0 + acc1;
+  const int col = n0 + wn * 32 + li;
+  const int rbase = m0 + wm * 32 + 4 * lh;
+  if (g.split > 1) {
+    if (col < g.N) {
+      float* slab = g.ws + ((long long)bidx * g.split + sk) * g.M * (long long)g.N;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rbase + (r & 3) + 8 * (r >> 2);
+        if (row < g.M) slab[(long long)row * g.N + col] = acc[r];
+      }
+    }
+    if (g.tile_cnt) splitk_finish<WBM, BN>(g, bidx, m0, n0, (bidx * g.tiles_y + ty) * g.tiles_x + tx, flag);
+    return;
+  }
+  tile_epilogue(g, bidx, rbase, col, acc);
+}
+
 // Separate split-K reduce: a thread sums 4 consecutive elements (float4 over the slabs when M*N % 4 == 0
 // and the workspace is 16-B aligned) with up to 8 slab loads in flight, slabs added in order
 // (deterministic); the epilogue runs per element.
@@ -1520,6 +1695,34 @@ int launch_reduce(const fx_gemm_desc& d, const GemmPlan& P, hipStream_t s) {
 
 }  // namespace
 
+std::atomic<int> g_gemm_prec{FX_PREC_F32};
+
+// FX_PREC_BF16: the 128x64-tile launches with row-major operands take the bf16-arithmetic kernel
+bool bf16_eligible(const GemmPlan& P) {
+  return g_gemm_prec.load(std::memory_order_relaxed) == FX_PREC_BF16 && P.wide && (P.bk == ROWS || P.bk == COLS) &&
+         (P.ak == ROWS || P.ak == ROWS_CONV || P.ak == ROWS_CAT);
+}
+
+template <int AK>
+int launch_bf16_b(const GemmPlan& P, hipStream_t s) {
+  if (P.bk == ROWS)
+    hipLaunchKernelGGL((gemm_bf16_wide8_kernel<AK, ROWS>), P.grid, dim3(W8T), 0, s, P.g);
+  else
+    hipLaunchKernelGGL((gemm_bf16_wide8_kernel<AK, COLS>), P.grid, dim3(W8T), 0, s, P.g);
+  return FX_OK;
+}
+
+int launch_bf16(const GemmPlan& P, hipStream_t s) {
+  switch (P.ak) {
+    case ROWS: return launch_bf16_b<ROWS>(P, s);
+    case ROWS_CONV: return launch_bf16_b<ROWS_CONV>(P, s);
+    case ROWS_CAT: return launch_bf16_b<ROWS_CAT>(P, s);
+    default: break;
+  }
+  set_error("gemm(bf16): unsupported A operand kind");
+  return FX_ERR_UNSUPPORTED;
+}
+
 int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
   FX_REQUIRE(d.M >= 0 && d.N >= 0 && d.K >= 0 && d.batch >= 1, "gemm: bad sizes");
   if (d.M == 0 || d.N == 0) return FX_OK;
@@ -1527,7 +1730,8 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
   FX_TRY(plan_gemm(d, s, P));
   log_gemm(d, P);
   const GemmDev& g = P.g;
-  int st = P.direct ? launch_direct(P.ak, P.bk, P.grid, P.block, s, g)
+  int st = bf16_eligible(P) ? launch_bf16(P, s)
+         : P.direct ? launch_direct(P.ak, P.bk, P.grid, P.block, s, g)
                     : (P.wide ? (wide8() ? launch_wide8(P.ak, P.bk, P.grid, s, g) : launch_wide(P.ak, P.bk, P.grid, s, g))
                               : launch_tiled(P.ak, P.bk, P.grid, s, g));
   if (st != FX_OK) return st;
@@ -1626,3 +1830,15 @@ int launch_colsum(const float* x, long long ld, int M, int N, float* out, int ac
 long long colsum_workspace_floats(int M, int N) { return (long long)cdiv(M, CS_ROWS) * N; }
 
 }  // namespace fx
+
+extern "C" {
+
+int fx_set_gemm_precision(int prec) {
+  FX_REQUIRE(prec == FX_PREC_F32 || prec == FX_PREC_BF16, "gemm precision: FX_PREC_F32 or FX_PREC_BF16");
+  fx::g_gemm_prec.store(prec, std::memory_order_relaxed);
+  return FX_OK;
+}
+
+int fx_get_gemm_precision(void) { return fx::g_gemm_prec.load(std::memory_order_relaxed); }
+
+}  // extern "C"

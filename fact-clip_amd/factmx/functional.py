@@ -69,6 +69,27 @@ def _defer_to_side(*tensors):
         torch.autograd.Variable._execution_engine.queue_callback(side_join)
 
 
+class gemm_precision:
+    """Context manager (or plain call) for the library's GEMM arithmetic: "fp32" (default, the parity
+    path) or "bf16" (FX_PREC_BF16: frame-level forward / input-gradient products on bf16 MFMA with
+    fp32 accumulation and storage; a performance mode whose deviation bench.py reports)."""
+
+    def __init__(self, mode):
+        modes = {"fp32": nx.PREC_F32, "bf16": nx.PREC_BF16}
+        if mode not in modes:
+            raise ValueError(f"gemm precision {mode!r}: 'fp32' or 'bf16'")
+        lib = nx.load()
+        self._prev = lib.fx_get_gemm_precision()
+        nx.check(lib.fx_set_gemm_precision(modes[mode]), "fx_set_gemm_precision")
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        nx.check(nx.load().fx_set_gemm_precision(self._prev), "fx_set_gemm_precision")
+        return False
+
+
 def dropout_seed():
     """Seed of one training dropout site, drawn from torch's default CPU generator (so
     torch.manual_seed fixes the masks, as it fixes nn.Dropout's); the kernels derive every mask

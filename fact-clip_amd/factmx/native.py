@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FACTMX_LIB", os.path.join(_HERE, "_lib", "libfactmx.so"))
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -71,6 +71,7 @@ class DecoderGrads(ctypes.Structure):
 LOSS_MAXK = 64
 LOSS_NB = 128          # FX_LOSS_NB: row blocks per loss term
 TERM_CLASS, TERM_ATTN, TERM_INFONCE = 0, 1, 2
+PREC_F32, PREC_BF16 = 0, 1   # FX_PREC_*: GEMM arithmetic precision (fx_set_gemm_precision)
 
 
 class LossTerm(ctypes.Structure):
@@ -157,6 +158,8 @@ SIGNATURES = {
     "fx_loss_terms_bwd": (I, [P, P, I, P, I, P, P, P]),
     "fx_match_cost": (I, [P, P, I, F, F, I, P, P]),
     "fx_eval_pred": (I, [P, P, I, F, P, P]),
+    "fx_set_gemm_precision": (I, [I]),
+    "fx_get_gemm_precision": (I, []),
     "fx_prof_enable": (I, [I, I]),
     "fx_prof_collect": (I, [I, ctypes.POINTER(D), ctypes.POINTER(D), ctypes.POINTER(D), ctypes.POINTER(I)]),
     "fx_prof_disable": (None, []),

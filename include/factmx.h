@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FX_ABI_VERSION 10
+#define FX_ABI_VERSION 11
 
 enum {
   FX_OK = 0,
@@ -578,6 +578,21 @@ int fx_eval_pred(const fx_video_attn* vids_host, const fx_video_attn* vids_dev, 
                  int32_t* pred, void* stream);
 
 /* ------------------------------------------------------------------------
+ * GEMM arithmetic precision (process-wide).  FX_PREC_F32 (default): every
+ * product on v_mfma_f32_32x32x2_f32, the parity path.  FX_PREC_BF16: the
+ * frame-level GEMMs with row-major operands (forward and input-gradient
+ * products of the MS-TCN convs, in/out maps, projections) round their
+ * operands to bf16 on the way into LDS and multiply on
+ * v_mfma_f32_32x32x16_bf16, accumulating in fp32; storage, weight
+ * gradients, attention, normalisation and losses stay fp32.  A performance
+ * mode (BASELINE configs[1]): its deviation from the fp32 path is reported,
+ * not bounded by the parity tests.
+ * ---------------------------------------------------------------------- */
+enum { FX_PREC_F32 = 0, FX_PREC_BF16 = 1 };
+int fx_set_gemm_precision(int prec);
+int fx_get_gemm_precision(void);
+
+/* ----------------------------------------------------------------------
  * Profiling hooks: HIP-event timing of every launch of a kernel class
  * (bench.py roofline).  Kinds are enabled independently:
  *   0 = dilated-conv implicit GEMM (conv forward, conv dX),
