@@ -503,6 +503,12 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   // a main-stream write waits for the side stream's layer that last read that buffer.
   SideStream* ss = (p->layernorm || drop) ? nullptr : side_stream();
   hipStream_t sd = ss ? ss->s : s;
+  // FX_SIDE_MAXWG=n: the side stream's split-K GEMMs keep within n workgroups (A/B diagnostic)
+  static const int side_maxwg = [] {
+    const char* e = std::getenv("FX_SIDE_MAXWG");
+    return e ? std::max(0, std::atoi(e)) : 0;
+  }();
+  GridCap gcap(ss ? side_maxwg : 0);
   auto fork = [&](int e) -> int {   // side stream waits for the main stream's work so far
     if (!ss) return FX_OK;
     FX_CHECK_HIP(hipEventRecord(ss->to_side[e], s));

@@ -54,6 +54,14 @@ struct WsBound {
   const float* prev_lo;
   const float* prev_hi;
 };
+// While alive, split-K launches planned on this thread keep tiles x split within `blocks` workgroups
+// (0: no cap) -- for the side stream's weight-gradient GEMMs, so that they leave CUs to the main
+// stream's latency-bound kernels instead of filling every CU's LDS.
+struct GridCap {
+  explicit GridCap(int blocks);
+  ~GridCap();
+  int prev;
+};
 // workspace floats needed by a split-K descriptor
 long long gemm_workspace_floats(const fx_gemm_desc& d);
 

@@ -1513,6 +1513,10 @@ unsigned* tile_counters(hipStream_t s) {
 
 unsigned* arrival_counters(hipStream_t s) { return tile_counters(s); }
 
+thread_local int t_max_blocks = 0;
+GridCap::GridCap(int blocks) : prev(t_max_blocks) { t_max_blocks = blocks; }
+GridCap::~GridCap() { t_max_blocks = prev; }
+
 thread_local const float* t_ws_lo = nullptr;
 thread_local const float* t_ws_hi = nullptr;
 
@@ -1649,6 +1653,12 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
     g.tiles_x = cdiv(d.N, BN);
     wide = use_wide(g, ak, bk, d.batch);
     g.tiles_y = cdiv(d.M, wide ? WBM : BM);
+    if (t_max_blocks > 0 && g.split > 1) {
+      const long long tiles = (long long)g.tiles_x * g.tiles_y * d.batch;
+      const int sp = (int)std::max<long long>(1, std::min<long long>(g.split, t_max_blocks / std::max(tiles, 1LL)));
+      g.kt_per_split = cdiv(nkt, sp);   // (the tile shape chosen above stays)
+      g.split = cdiv(nkt, g.kt_per_split);
+    }
     grid = dim3(g.tiles_x, g.tiles_y, d.batch * g.split);
     block = dim3(NTHREADS);
   }
