@@ -167,7 +167,10 @@ def bf16_mode(net, step, nv, T, steps, warmup, fxf):
     def logits():
         step()
         torch.cuda.synchronize()
-        return [r["frame_clogit"].detach().clone() for r in net.block_list[-1]._vrec], video_segments(net)
+        last = net.block_list[-1]
+        recs = getattr(last, "_vrec", None)   # lockstep batch: every video; else the last video run
+        z = [r["frame_clogit"] for r in recs] if recs else [last.frame_clogit]
+        return [t.detach().clone() for t in z], video_segments(net)
     z32, s32 = logits()
     with fxf.gemm_precision("bf16"):
         z16, s16 = logits()

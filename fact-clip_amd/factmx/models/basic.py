@@ -202,8 +202,10 @@ class MSTCN2(nn.Module):
     def __repr__(self):
         return self.string
 
-    def forward(self, x):
-        T = x.shape[0]
+    def forward(self, x, T=None):
+        """x: (T, 1, dim) or, lockstep, (nvid*T, dim) rows of nvid stacked videos of T frames each (the
+        dilated convs zero-pad at every video's ends)."""
+        T = T or x.shape[0]
         f = fxf.linear(x, self.conv_1x1_in.weight, self.conv_1x1_in.bias) if self.in_map else fxf._2d(x)
         L = self.num_layers
         for i in range(L):

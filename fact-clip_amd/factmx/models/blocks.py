@@ -153,6 +153,14 @@ class Block(nn.Module):
         return self._eval_w_transcript(transcript, self.a2f_attn, self.frame_clogit, self.cfg.FACT.mwt)
 
 
+def _frame_branch_batch(branch, f, vb):
+    """The frame branch over vb.nvid stacked videos: MS-TCN as one fused stack call, MS-TCN++ (MSTCN2)
+    layer by layer with per-video zero padding."""
+    if isinstance(branch, basic.MSTCN2):
+        return fxf._2d(branch(f, T=vb.T))
+    return fxf.mstcn(branch, f, T=vb.T, nvid=vb.nvid)
+
+
 class InputBlock(Block):
     """blocks.py:284-320."""
 
@@ -177,7 +185,7 @@ class InputBlock(Block):
     def forward_batch(self, f2, a2, fpos, apos, vb):
         """``forward`` over vb.nvid stacked videos (frames (nvid*T, C), tokens (nvid*Q, A));
         per-video side-channel attributes go to ``self._vrec``."""
-        f = fxf.mstcn(self.frame_branch, f2, T=vb.T, nvid=vb.nvid)
+        f = _frame_branch_batch(self.frame_branch, f2, vb)
         f_out, f_cl = fxf.process_feature(f, self.nclass)
         a = fxf.decoder(self.action_branch, a2, f_out, pos=fpos, query_pos=apos, nvid=vb.nvid)
         a_out, a_cl = fxf.process_feature(a, self.nclass + 1)
@@ -234,7 +242,7 @@ class UpdateBlock(Block):
                                     rows=(vb.a_off, vb.f_off))
         if vb.on_a2f is not None and vb.last is self:
             vb.on_a2f(vb, a_cl, a2f_at)         # the loss phase's matching starts here (vloss.EarlyMatch)
-        f = fxf.mstcn(self.frame_branch, f, T=vb.T, nvid=vb.nvid)
+        f = _frame_branch_batch(self.frame_branch, f, vb)
         f_out, f_cl = fxf.process_feature(f, self.nclass)
         n, Q, T = self.nclass + 1, vb.Q, vb.T
         recs = []
@@ -338,7 +346,7 @@ class UpdateBlockTDU(Block):
             vb.on_a2f(vb, a_cl, a2f_at, (s_off, local))
         lin = self.sf_merge[0]
         f = fxf.SegMergeFn.apply(sg, f2, gid, gst, gen, lin.weight, lin.bias)
-        f = fxf.mstcn(self.frame_branch, f, T=vb.T, nvid=vb.nvid)
+        f = _frame_branch_batch(self.frame_branch, f, vb)
         f_out, f_cl = fxf.process_feature(f, self.nclass)
         n, Q = self.nclass + 1, vb.Q
         recs = []
@@ -636,8 +644,6 @@ def _batchable(net, seq_list):
         return False
     for blk in net.block_list:
         if not basic._fused_decoder_ok(blk.action_branch) or not hasattr(blk, "forward_batch"):
-            return False
-        if isinstance(blk.frame_branch, basic.MSTCN2):
             return False
     return True
 

@@ -1,5 +1,6 @@
 """Lockstep multi-video path (blocks._forward_videos -> _FACTBase._forward_batch) vs the reference's
-one-video-at-a-time loop on the same model and inputs (GPU): per-video predictions and TDU segment
+one-video-at-a-time loop on the same model and inputs (GPU; FACT_CLIP, and vanilla FACT with the
+MS-TCN++ 'm2' frame branch of the Breakfast config): per-video predictions and TDU segment
 boundaries identical, per-video losses / the batch loss and every parameter gradient within fp32
 tolerance, the side-channel attributes (last video) equal; the first video also against the
 reference golden vectors, and at the benchmark shape both videos against the CPU oracle."""
@@ -17,11 +18,14 @@ DEV = "cuda"
 
 
 def _model(meta, cfg):
-    from factmx.models.blocks import FACT_CLIP
+    from factmx.models.blocks import FACT, FACT_CLIP
     from factmx.models.loss import MatchCriterion
     C, D = meta["C"], meta["D"]
     _, _, text = tiny_inputs(meta)
-    net = FACT_CLIP(cfg, D, C, text_embeddings=torch.from_numpy(text).float())
+    if meta["model"] == "FACT_CLIP":
+        net = FACT_CLIP(cfg, D, C, text_embeddings=torch.from_numpy(text).float())
+    else:
+        net = FACT(cfg, D, C)
     with torch.no_grad():
         for n, p in net.named_parameters():
             p.copy_(torch.from_numpy(pg.param_value(n, p.shape, meta["seed"])))
@@ -46,7 +50,8 @@ def _run(net, seqs, labs, batched, monkeypatch):
             attrs[f"{i}/f2a_attn_logit"] = blk.f2a_attn_logit.detach().clone()
         if hasattr(blk, "tdu"):
             attrs[f"{i}/seg_start"] = blk.tdu.start32.cpu().clone()
-    attrs["proj"] = net.projected_frame_embeddings.detach().clone()
+    if hasattr(net, "projected_frame_embeddings"):
+        attrs["proj"] = net.projected_frame_embeddings.detach().clone()
     grads = {n: p.grad.detach().clone() for n, p in net.named_parameters()}
     return total.item(), saves, attrs, grads
 
@@ -57,7 +62,7 @@ def _keep_impl():
     yield
 
 
-@pytest.mark.parametrize("name", ["tiny_clip", "tiny_clip_iid"])
+@pytest.mark.parametrize("name", ["tiny_clip", "tiny_clip_iid", "tiny_fact_m2"])
 def test_lockstep_equals_per_video(name, monkeypatch):
     fx = load_fixture(name)
     meta = tiny_meta(fx)

@@ -17,6 +17,6 @@ rc=$?; echo "bench exit $rc"; cat gpurun_out/bench_$TAG.json; tail -3 gpurun_out
 timeout -k 10 400 python bench.py --config breakfast --steps 10 --warmup 3 > gpurun_out/bench_bf_$TAG.json 2> gpurun_out/bench_bf_$TAG.err
 rc=$?; echo "bench breakfast exit $rc"; cat gpurun_out/bench_bf_$TAG.json; tail -3 gpurun_out/bench_bf_$TAG.err
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --adam-steps 0 --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --adam-steps 0 --no-cpu-baseline --no-bf16 > gpurun_out/prof_$TAG.log 2>&1
 rc=$?; echo "prof exit $rc"; tail -1 gpurun_out/prof_$TAG.log
 exit $rc

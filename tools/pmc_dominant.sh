@@ -11,7 +11,7 @@ for set in "FETCH_SIZE" "WRITE_SIZE" \
            "GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_VALU_MFMA_COEXEC_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"; do
   i=$((i+1))
   timeout -s KILL 240 rocprofv3 --pmc $set -d $OUT/p$i -o p$i --output-format csv -- \
-    python bench.py --steps 1 --warmup 1 --no-cpu-baseline > $OUT/p$i.log 2>&1 || { echo "pass $i ($set) failed"; tail -5 $OUT/p$i.log; exit 1; }
+    python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-bf16 > $OUT/p$i.log 2>&1 || { echo "pass $i ($set) failed"; tail -5 $OUT/p$i.log; exit 1; }
 done
 python tools/pmc_dominant.py $OUT "${KERNEL:-gemm_f32_wide8_kernel<1, 0>}" > gpurun_out/pmc_dominant.json
 cat gpurun_out/pmc_dominant.json
