@@ -248,7 +248,13 @@ SideStream* side_stream() {
   auto it = pool.find(dev);
   if (it != pool.end()) return it->second;
   SideStream* ss = new SideStream();
-  bool ok = hipStreamCreateWithFlags(&ss->s, hipStreamNonBlocking) == hipSuccess;
+  // FX_SIDE_PRIORITY=low|normal|high: the side stream's queue priority (A/B diagnostic; default normal)
+  int prio = 0, least = 0, greatest = 0;
+  if (const char* pe = std::getenv("FX_SIDE_PRIORITY")) {
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+      prio = std::string(pe) == "low" ? least : std::string(pe) == "high" ? greatest : 0;
+  }
+  bool ok = hipStreamCreateWithPriority(&ss->s, hipStreamNonBlocking, prio) == hipSuccess;
   for (auto& e : ss->to_side) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
   for (auto& e : ss->layer_done) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
   ok = ok && hipEventCreateWithFlags(&ss->join, hipEventDisableTiming) == hipSuccess;
