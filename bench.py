@@ -146,9 +146,10 @@ def video_segments(net):
     return [list(s) for s in getattr(net, "video_segments", [])]
 
 
-def traffic_from_profiles(kernel_prefix):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary, if any."""
-    path = os.path.join(ROOT, "profiles", "pmc_dominant.json")
+def traffic_from_profiles(kernel_prefix, name="pmc_dominant.json"):
+    """HBM bytes per launch of a kernel from a committed rocprofv3 PMC summary (FETCH_SIZE / WRITE_SIZE
+    passes, tools/pmc_dominant.sh), if any."""
+    path = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(path):
         return None
     try:
@@ -386,6 +387,9 @@ def main():
                         flops_per_launch=flops_per_launch)
         roofline_attention = {name: attention_roofline(f"tattn_{name}_kernel (+ tattn_merge_kernel over T splits)", *v)
                               for name, v in attn_prof.items()}
+        for name, r in roofline_attention.items():
+            if r is not None and default_shape:   # PMC bytes of the main kernel (the merge launch excluded)
+                r["traffic"] = traffic_from_profiles(f"tattn_{name}_kernel", f"r02_pmc_tattn_{name}.json")
         line = dict(metric=metric, value=round(value, 1), unit="frames/s", n_gpus=world, steps=args.steps,
                     warmup=args.warmup, ms_per_step=round(1e3 * elapsed / args.steps, 3), higher_is_better=True,
                     scaling="weak", vs_baseline=None, dtype="fp32", data="synthetic",
