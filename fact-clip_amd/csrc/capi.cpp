@@ -272,7 +272,7 @@ struct MstcnLayout {
   // saved
   long long h, z, xh, rs, total_saved;
   // workspace
-  long long wf, wb, wpt, buf0, buf1, buf2, buf3, buf4, buf5, split, split2, colsum, total_ws;
+  long long wf, wb, wpt, buf0, buf1, buf2, buf3, buf4, buf5, split, split2, colsum, dzall, dhall, csb, bsl, total_ws;
 };
 
 MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
@@ -308,7 +308,13 @@ MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
   L.split2 = L.split + sp;                   // split-K partials of the main stream's GEMMs
   L.colsum = L.split2 + sp;
   long long cs = colsum_workspace_floats(rows, std::max(std::max(p->F, p->cout), p->cin));
-  L.total_ws = L.colsum + cs;
+  // deferred weight gradients (fx_mstcn_bwd): every layer's dZ_i and dH_i+1 kept for the batched
+  // dW GEMMs, and the batched conv-bias column sums
+  L.dzall = L.colsum + cs;
+  L.dhall = L.dzall + NL * L.rowsF;
+  L.csb = L.dhall + NL * L.rowsF;
+  L.bsl = L.csb + (long long)NL * colsum_workspace_floats(rows, p->F);
+  L.total_ws = L.bsl + split_ws(p->F, p->F + 1, rows, std::max(NL, 1));
   return L;
 }
 
@@ -333,6 +339,26 @@ int layer_dilation(const fx_mstcn_params* p, int i) {
   const int f = p->dil_factor > 0 ? p->dil_factor : 2;
   for (int k = 0; k < i; ++k) d *= f;
   return (int)d;
+}
+
+// The batched weight-gradient GEMMs of fx_mstcn_bwd address layer i's gradients as layer 0's plus
+// i times one stride: true for views of one flat gradient buffer in parameter order (FlatGradReducer).
+// FX_MSTCN_DEFER=0 keeps the per-layer interleaved GEMMs (A/B).
+bool mstcn_defer_ok(const fx_mstcn_params* p, const fx_mstcn_grads* g) {
+  static const bool off = [] {
+    const char* e = std::getenv("FX_MSTCN_DEFER");
+    return e && e[0] == '0';
+  }();
+  if (off) return false;
+  const int NL = p->num_layers;
+  for (int i = 0; i < NL; ++i)
+    if (!g->w_dil[i] || !g->b_dil[i] || !g->w_pw[i] || !g->b_pw[i]) return false;
+  auto uniform = [&](float* const* v) {
+    for (int i = 2; i < NL; ++i)
+      if (v[i] - v[i - 1] != v[1] - v[0]) return false;
+    return true;
+  };
+  return uniform(g->w_dil) && uniform(g->b_dil) && uniform(g->w_pw) && uniform(g->b_pw);
 }
 
 fx_operand conv_operand(const float* h, long long ld, int cin, int dil, int dir, int T, bool trans) {
@@ -368,6 +394,7 @@ long long fx_struct_size(int which) {
     case 2: return (long long)sizeof(fx_mstcn_params);
     case 3: return (long long)sizeof(fx_loss_term);
     case 4: return (long long)sizeof(fx_video_attn);
+    case 5: return (long long)sizeof(fx_mstcn2_params);
     default: return -1;
   }
 }
@@ -509,6 +536,7 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   // a main-stream write waits for the side stream's layer that last read that buffer.
   SideStream* ss = (p->layernorm || drop) ? nullptr : side_stream();
   hipStream_t sd = ss ? ss->s : s;
+  const bool defer = !fchain && !p->layernorm && !drop && NL > 0 && mstcn_defer_ok(p, g);
   // FX_SIDE_MAXWG=n: the side stream's split-K GEMMs keep within n workgroups (A/B diagnostic)
   static const int side_maxwg = [] {
     const char* e = std::getenv("FX_SIDE_MAXWG");
@@ -539,7 +567,7 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   const float* hL = saved + L.h + NL * L.rowsF;
   FX_TRY(fork(0));
   FX_TRY(linear_dwdb(dy, lddy, hL, F, rows, F, p->cout, g->w_out, g->b_out, 1, spl, sd));
-  float* dH = Hb[0];
+  float* dH = defer ? ws + L.dhall + (NL - 1) * L.rowsF : Hb[0];   // (deferred: dH_NL kept for the 1x1 dW)
   FX_TRY(linear_dx(dy, lddy, p->w_out, rows, F, p->cout, dH, F, 0, nullptr, 0, spm, s));
   // Fused chain: dH_i = gU_i + conv^T(dZ_i) and the next layer's dZ_i-1 = (dH_i . W_pw,i-1) *
   // (z_i-1 > 0) in ONE kernel per layer (mstcn_fused.hip).  dH_i lives in Hb[(NL - i) % 3], dZ_i in
@@ -593,7 +621,66 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
     }
     dH = dHi;
   }
-  for (int i = NL - 1; !fchain && i >= 0; --i) {
+  // Deferred weight gradients (default when the gradient buffers are uniformly strided, as views of
+  // one flat buffer are): the chain keeps every layer's dZ_i and dH_i+1, and the weight gradients of
+  // ALL layers follow it as two batched GEMMs on the side stream -- the dilated-conv dW of every layer
+  // in one launch (per-layer dilation via b_dil_growth; NL x 24 tiles of 128x64 over the full K = rows,
+  // no split-K slabs) and the 1x1 dW + db in another -- plus one batched column sum for the conv
+  // biases.  Per layer the interleaved version paid two split-K GEMMs and their reduce launches,
+  // competing with the chain for the CUs.
+  if (defer) {
+    float* dZall = ws + L.dzall;
+    float* dHall = ws + L.dhall;   // dHall[i] = dH_{i+1} (gradient at layer i's output)
+    for (int i = NL - 1; i >= 0; --i) {
+      const float* zi = saved + L.z + i * L.rowsF;
+      const float* gU = dHall + i * L.rowsF;
+      float* dZ = dZall + i * L.rowsF;
+      FX_TRY(linear_dx(gU, F, p->w_pw[i], rows, F, F, dZ, F, 0, zi, F, spm, s));
+      float* dHn = i > 0 ? dHall + (i - 1) * L.rowsF : Hb[0];
+      fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dZ, F, F, layer_dilation(p, i), -1, T, false),
+                                 op_rows(ws + L.wb + (long long)i * 3 * F * F, 3 * F), dHn, F);
+      d.resid = gU;
+      d.ld_resid = F;
+      prof_begin(0, s);
+      FX_TRY(launch_gemm(d, s));
+      prof_end(0, s, 2.0 * rows * F * 3.0 * F, 4.0 * (3.0 * rows * F + 3.0 * F * F));
+    }
+    dH = Hb[0];
+    FX_TRY(fork(1));
+    {   // 1x1: dW_pw,i += dH_{i+1}^T z_i, db_pw,i += colsum(dH_{i+1})   (batched over layers)
+      fx_operand b = op_cols(saved + L.z, F);
+      b.batch_stride = L.rowsF;
+      b.ones_col = F + 1;
+      fx_operand a = op_cols(dHall, F);
+      a.batch_stride = L.rowsF;
+      fx_gemm_desc d = gemm_desc(F, F + 1, rows, a, b, g->w_pw[0], F);
+      d.batch = NL;
+      d.c_batch_stride = NL > 1 ? g->w_pw[1] - g->w_pw[0] : 0;
+      d.c_last_col = g->b_pw[0];
+      d.c_last_batch_stride = NL > 1 ? g->b_pw[1] - g->b_pw[0] : 0;
+      d.beta = 1.f;
+      d.split_k = pick_split(F, F + 1, rows, NL);
+      d.workspace = ws + L.bsl;
+      WsBound wbb(ws + L.bsl, split_ws(F, F + 1, rows, NL));
+      FX_TRY(launch_gemm(d, sd));
+    }
+    {   // dilated conv: dW_i += dZ_i^T taps(h_i) stored straight into (F, F, 3)   (batched over layers)
+      fx_operand b = conv_operand(saved + L.h, F, F, layer_dilation(p, 0), 1, T, true);
+      b.batch_stride = L.rowsF;
+      fx_operand a = op_cols(dZall, F);
+      a.batch_stride = L.rowsF;
+      fx_gemm_desc d = gemm_desc(F, 3 * F, rows, a, b, g->w_dil[0], 3 * F);
+      d.batch = NL;
+      d.c_batch_stride = NL > 1 ? g->w_dil[1] - g->w_dil[0] : 0;
+      d.b_dil_growth = p->dil_factor > 0 ? p->dil_factor : 2;
+      d.c_tap_cin = F;
+      d.beta = 1.f;
+      FX_TRY(launch_gemm(d, sd));
+      FX_TRY(launch_colsum_batched(dZall, F, L.rowsF, rows, F, NL, g->b_dil[0],
+                                   NL > 1 ? g->b_dil[1] - g->b_dil[0] : 0, 1, ws + L.csb, sd));
+    }
+  }
+  for (int i = NL - 1; !fchain && !defer && i >= 0; --i) {
     const int step = NL - 1 - i;
     const float* hi = saved + L.h + i * L.rowsF;
     const float* zi = saved + L.z + i * L.rowsF;
@@ -665,6 +752,279 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
                                   hipMemcpyDeviceToDevice, s));
   }
   if (ss && !p->side_defer) {   // join: everything the side stream did is ordered before later work
+    FX_CHECK_HIP(hipEventRecord(ss->join, sd));
+    FX_CHECK_HIP(hipStreamWaitEvent(s, ss->join, 0));
+  }
+  return FX_OK;
+}
+
+// ---------------------------------------------------------------- MS-TCN++ (MSTCN2)
+}  // extern "C"
+
+namespace fx {
+namespace {
+
+struct Mstcn2Layout {
+  long long rowsF;
+  long long f, cat, r, total_saved;                       // saved: f_0..f_L, cat_i (2F), r_i
+  long long wf1, wf2, wb1, wb2, hb0, hb1, du, dcat, spm, spl, bsl, total_ws;
+};
+
+Mstcn2Layout mstcn2_layout(const fx_mstcn2_params* p, int rows) {
+  Mstcn2Layout L{};
+  const long long F = p->F;
+  const int NL = p->num_layers;
+  L.rowsF = (long long)rows * F;
+  L.f = 0;
+  L.cat = L.f + (NL + 1) * L.rowsF;
+  L.r = L.cat + 2 * NL * L.rowsF;
+  L.total_saved = L.r + NL * L.rowsF;
+  const long long wsz = 3 * F * F;
+  L.wf1 = 0;
+  L.wf2 = L.wf1 + NL * wsz;
+  L.wb1 = L.wf2 + NL * wsz;
+  L.wb2 = L.wb1 + NL * wsz;
+  L.hb0 = L.wb2 + NL * wsz;                 // input-gradient chain: dF ping-pong
+  L.hb1 = L.hb0 + L.rowsF;
+  L.du = L.hb1 + L.rowsF;                   // every layer's dU_i (fusion pre-activation gradient)
+  L.dcat = L.du + NL * L.rowsF;             // every layer's dCat_i = [dA_i | dB_i]
+  L.spm = L.dcat + 2 * NL * L.rowsF;        // split-K partials: main-stream GEMMs
+  long long sp = 0;
+  sp = std::max(sp, split_ws(rows, F, p->cout));
+  sp = std::max(sp, split_ws(rows, 2 * F, F));
+  sp = std::max(sp, split_ws(rows, F, 3 * F));
+  if (p->in_map) sp = std::max(sp, split_ws(rows, p->cin, F));
+  L.spl = L.spm + sp;                       // ... side stream (out / in map dW)
+  long long sl = std::max(dwdb_ws(rows, F, p->cout), p->in_map ? dwdb_ws(rows, p->cin, F) : 0LL);
+  L.bsl = L.spl + sl;                       // ... the (batched) layer dW GEMMs
+  long long sb = 0;
+  for (int nb : {1, std::max(NL, 1)}) {
+    sb = std::max(sb, split_ws(F, 2 * F + 1, rows, nb));
+    sb = std::max(sb, split_ws(F, 3 * F + 1, rows, nb));
+  }
+  L.total_ws = L.bsl + sb;
+  return L;
+}
+
+int mstcn2_dil(const fx_mstcn2_params* p, int e) {   // dil_factor^e
+  const int f = p->dil_factor > 0 ? p->dil_factor : 2;
+  long long d = 1;
+  for (int k = 0; k < e; ++k) d *= f;
+  return (int)d;
+}
+
+int pack_conv_set(const float* const* w, int NL, int F, float* wf, float* wb, hipStream_t s) {
+  PackArgs a{};
+  a.F = F;
+  const long long wsz = 3LL * F * F;
+  for (int l = 0; l < NL; ++l) {
+    a.w[l] = w[l];
+    a.wf[l] = wf + l * wsz;
+    a.wb[l] = wb + l * wsz;
+  }
+  hipLaunchKernelGGL(pack_conv_kernel, dim3(std::min<int>(cdiv(wsz, 256), 512), NL), dim3(256), 0, s, a);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+template <typename V>
+bool uniform_stride(V v, int n) {
+  for (int i = 0; i < n; ++i)
+    if (!v[i]) return false;
+  for (int i = 2; i < n; ++i)
+    if (v[i] - v[i - 1] != v[1] - v[0]) return false;
+  return true;
+}
+
+}  // namespace
+}  // namespace fx
+
+extern "C" {
+
+long long fx_mstcn2_saved_floats(const fx_mstcn2_params* p, int rows) { return mstcn2_layout(p, rows).total_saved; }
+long long fx_mstcn2_workspace_floats(const fx_mstcn2_params* p, int rows) { return mstcn2_layout(p, rows).total_ws; }
+
+int fx_mstcn2_fwd(const fx_mstcn2_params* p, const float* x, long long ldx, int T, int nvid, float* y, long long ldy,
+                  float* saved, float* workspace, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  FX_REQUIRE(p && p->num_layers >= 0 && p->num_layers <= 32, "mstcn2: 0..32 layers");
+  FX_REQUIRE(p->in_map || p->cin == p->F, "mstcn2: in_map=0 needs cin == F");
+  FX_REQUIRE(p->dropout >= 0.f && p->dropout < 1.f, "mstcn2: dropout must be in [0, 1)");
+  FX_REQUIRE(T >= 1 && nvid >= 1 && saved && workspace && y, "mstcn2: bad arguments");
+  const int rows = T * nvid, F = p->F, NL = p->num_layers;
+  const Mstcn2Layout L = mstcn2_layout(p, rows);
+  float* ws = workspace;
+  if (NL > 0) {
+    FX_TRY(pack_conv_set(p->w_d1, NL, F, ws + L.wf1, ws + L.wb1, s));
+    FX_TRY(pack_conv_set(p->w_d2, NL, F, ws + L.wf2, ws + L.wb2, s));
+  }
+  float* f0 = saved + L.f;
+  if (p->in_map) {
+    FX_TRY(linear_fwd(x, ldx, rows, p->cin, p->w_in, p->b_in, f0, F, F, 0, s));
+  } else {
+    FX_CHECK_HIP(hipMemcpy2DAsync(f0, F * sizeof(float), x, ldx * sizeof(float), F * sizeof(float), rows,
+                                  hipMemcpyDeviceToDevice, s));
+  }
+  for (int i = 0; i < NL; ++i) {
+    const float* fi = saved + L.f + i * L.rowsF;
+    float* fn = saved + L.f + (i + 1) * L.rowsF;
+    float* cat = saved + L.cat + 2 * i * L.rowsF;
+    float* ri = saved + L.r + i * L.rowsF;
+    // cat = [conv_d1(f) | conv_d2(f)]: the two dilated convs store into the halves of one buffer
+    // (no torch.cat)   (basic.py:276)
+    for (int h = 0; h < 2; ++h) {
+      const int dil = h == 0 ? mstcn2_dil(p, NL - 1 - i) : mstcn2_dil(p, i);
+      fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(fi, F, F, dil, 1, T, false),
+                                 op_rows(ws + (h == 0 ? L.wf1 : L.wf2) + (long long)i * 3 * F * F, 3 * F), cat + h * F,
+                                 2 * F);
+      d.bias = h == 0 ? p->b_d1[i] : p->b_d2[i];
+      prof_begin(0, s);
+      FX_TRY(launch_gemm(d, s));
+      prof_end(0, s, 2.0 * rows * F * 3.0 * F, 4.0 * (2.0 * rows * F + 3.0 * F * F));
+    }
+    // r = dropout(relu(W_fu . cat + b_fu)) (no dropout on the last layer), f' = f + r  (basic.py:276-280)
+    fx_gemm_desc e = gemm_desc(rows, F, 2 * F, op_rows(cat, 2 * F), op_rows(p->w_fu[i], 2 * F), ri, F);
+    e.bias = p->b_fu[i];
+    e.relu = 2;
+    if (i != NL - 1) {
+      e.drop_p = p->dropout;
+      e.drop_seed = fx_drop_subseed(p->seed, i);
+    }
+    FX_TRY(launch_gemm(e, s));
+    FX_TRY(add2(fi, F, ri, F, rows, F, fn, F, 0, s));
+  }
+  return linear_fwd(saved + L.f + NL * L.rowsF, F, rows, F, p->w_out, p->b_out, y, ldy, p->cout, 0, s);
+}
+
+int fx_mstcn2_bwd(const fx_mstcn2_params* p, const fx_mstcn2_grads* g, const float* x, long long ldx, int T, int nvid,
+                  const float* dy, long long lddy, float* dx, long long lddx, const float* saved, float* workspace,
+                  void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  FX_REQUIRE(p && g && saved && workspace && dy, "mstcn2 bwd: bad arguments");
+  const int rows = T * nvid, F = p->F, NL = p->num_layers;
+  const Mstcn2Layout L = mstcn2_layout(p, rows);
+  float* ws = workspace;
+  if (NL > 0) {   // (the forward's packed images live in the forward's workspace: repack)
+    FX_TRY(pack_conv_set(p->w_d1, NL, F, ws + L.wf1, ws + L.wb1, s));
+    FX_TRY(pack_conv_set(p->w_d2, NL, F, ws + L.wf2, ws + L.wb2, s));
+  }
+  SideStream* ss = side_stream();
+  hipStream_t sd = ss ? ss->s : s;
+  auto fork = [&](int e) -> int {
+    if (!ss) return FX_OK;
+    FX_CHECK_HIP(hipEventRecord(ss->to_side[e], s));
+    FX_CHECK_HIP(hipStreamWaitEvent(sd, ss->to_side[e], 0));
+    return FX_OK;
+  };
+  float* spm = ws + L.spm;
+  float* spl = ws + L.spl;
+  const float* fL = saved + L.f + NL * L.rowsF;
+  FX_TRY(fork(0));
+  {
+    WsBound wb(spl, L.bsl - L.spl);
+    FX_TRY(linear_dwdb(dy, lddy, fL, F, rows, F, p->cout, g->w_out, g->b_out, 1, spl, sd));
+  }
+  WsBound wbm(spm, L.spl - L.spm);
+  float* Hb[2] = {ws + L.hb0, ws + L.hb1};
+  float* gF = Hb[0];
+  FX_TRY(linear_dx(dy, lddy, p->w_out, rows, F, p->cout, gF, F, 0, nullptr, 0, spm, s));
+  for (int i = NL - 1; i >= 0; --i) {
+    const float* ri = saved + L.r + i * L.rowsF;
+    float* dU = ws + L.du + i * L.rowsF;
+    float* dCat = ws + L.dcat + 2 * i * L.rowsF;
+    // dU = dropout_i(gF) * (r_i > 0)   (r_i is stored after the dropout: zero where dropped)
+    if (i != NL - 1 && p->dropout > 0.f) {
+      FX_TRY(launch_dropout(gF, F, rows, F, F, 0, p->dropout, fx_drop_subseed(p->seed, i), dU, F, s));
+      FX_TRY(relu_bwd(dU, F, ri, F, rows, F, dU, F, s));
+    } else {
+      FX_TRY(relu_bwd(gF, F, ri, F, rows, F, dU, F, s));
+    }
+    // dCat = dU . W_fu   (rows x 2F)
+    FX_TRY(launch_gemm(gemm_desc(rows, 2 * F, F, op_rows(dU, F), op_cols(p->w_fu[i], 2 * F), dCat, 2 * F), s));
+    // dF_i = gF + conv_d1^T(dA) + conv_d2^T(dB)
+    float* dFn = Hb[(NL - i) & 1];
+    for (int h = 0; h < 2; ++h) {
+      const int dil = h == 0 ? mstcn2_dil(p, NL - 1 - i) : mstcn2_dil(p, i);
+      fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dCat + h * F, 2 * F, F, dil, -1, T, false),
+                                 op_rows(ws + (h == 0 ? L.wb1 : L.wb2) + (long long)i * 3 * F * F, 3 * F), dFn, F);
+      if (h == 0) {
+        d.resid = gF;
+        d.ld_resid = F;
+      } else {
+        d.beta = 1.f;
+      }
+      prof_begin(0, s);
+      FX_TRY(launch_gemm(d, s));
+      prof_end(0, s, 2.0 * rows * F * 3.0 * F, 4.0 * (3.0 * rows * F + 3.0 * F * F));
+    }
+    gF = dFn;
+  }
+  // weight gradients of every layer, after the chain (side stream): batched over the layers when the
+  // gradient buffers are uniformly strided (views of one flat buffer), else one launch per layer
+  FX_TRY(fork(1));
+  if (NL > 0) {
+    WsBound wbb(ws + L.bsl, L.total_ws - L.bsl);
+    const bool uni = uniform_stride(g->w_fu, NL) && uniform_stride(g->b_fu, NL) && uniform_stride(g->w_d1, NL) &&
+                     uniform_stride(g->b_d1, NL) && uniform_stride(g->w_d2, NL) && uniform_stride(g->b_d2, NL);
+    const int growth = p->dil_factor > 0 ? p->dil_factor : 2;
+    auto st = [&](float* const* v) -> long long { return NL > 1 ? v[1] - v[0] : 0; };
+    const int nb = uni ? NL : 1;
+    for (int i0 = 0; i0 < NL; i0 += nb) {
+      {   // fusion 1x1: dW_fu,i += dU_i^T cat_i, db_fu,i += colsum(dU_i)
+        fx_operand a = op_cols(ws + L.du + i0 * L.rowsF, F);
+        a.batch_stride = L.rowsF;
+        fx_operand b = op_cols(saved + L.cat + 2 * i0 * L.rowsF, 2 * F);
+        b.batch_stride = 2 * L.rowsF;
+        b.ones_col = 2 * F + 1;
+        fx_gemm_desc d = gemm_desc(F, 2 * F + 1, rows, a, b, g->w_fu[i0], 2 * F);
+        d.batch = nb;
+        d.c_batch_stride = st(g->w_fu);
+        d.c_last_col = g->b_fu[i0];
+        d.c_last_batch_stride = st(g->b_fu);
+        d.beta = 1.f;
+        d.split_k = pick_split(F, 2 * F + 1, rows, nb);
+        d.workspace = ws + L.bsl;
+        FX_TRY(launch_gemm(d, sd));
+      }
+      for (int h = 0; h < 2; ++h) {
+        // dilated conv h: dW_i += dC_h,i^T taps(f_i), db_i += colsum(dC_h,i); conv_d2's dilation grows with
+        // the layer (batch b = layer i0 + b), conv_d1's shrinks: its batch b is layer NL-1-b (negative strides)
+        const int il = (h == 0 && uni) ? NL - 1 : i0;
+        const long long dir = (h == 0 && uni) ? -1 : 1;
+        fx_operand a = op_cols(ws + L.dcat + 2 * il * L.rowsF + h * F, 2 * F);
+        a.batch_stride = dir * 2 * L.rowsF;
+        const int dil = h == 0 ? mstcn2_dil(p, NL - 1 - il) : mstcn2_dil(p, il);
+        fx_operand b = conv_operand(saved + L.f + il * L.rowsF, F, F, dil, 1, T, true);
+        b.batch_stride = dir * L.rowsF;
+        b.ones_col = 3 * F + 1;
+        float* const* gw = h == 0 ? g->w_d1 : g->w_d2;
+        float* const* gb = h == 0 ? g->b_d1 : g->b_d2;
+        fx_gemm_desc d = gemm_desc(F, 3 * F + 1, rows, a, b, gw[il], 3 * F);
+        d.batch = nb;
+        d.c_batch_stride = dir * st(gw);
+        d.c_last_col = gb[il];
+        d.c_last_batch_stride = dir * st(gb);
+        d.b_dil_growth = nb > 1 ? growth : 0;
+        d.c_tap_cin = F;
+        d.beta = 1.f;
+        d.split_k = pick_split(F, 3 * F + 1, rows, nb);
+        d.workspace = ws + L.bsl;
+        FX_TRY(launch_gemm(d, sd));
+      }
+    }
+  }
+  if (p->in_map) {
+    if (g->w_in) {
+      FX_TRY(fork(2));
+      WsBound wb(spl, L.bsl - L.spl);
+      FX_TRY(linear_dwdb(gF, F, x, ldx, rows, p->cin, F, g->w_in, g->b_in, 1, spl, sd));
+    }
+    if (dx) FX_TRY(linear_dx(gF, F, p->w_in, rows, p->cin, F, dx, lddx, 0, nullptr, 0, spm, s));
+  } else if (dx) {
+    FX_CHECK_HIP(hipMemcpy2DAsync(dx, lddx * sizeof(float), gF, F * sizeof(float), F * sizeof(float), rows,
+                                  hipMemcpyDeviceToDevice, s));
+  }
+  if (ss && !p->side_defer) {
     FX_CHECK_HIP(hipEventRecord(ss->join, sd));
     FX_CHECK_HIP(hipStreamWaitEvent(s, ss->join, 0));
   }

@@ -71,6 +71,8 @@ fx_operand op_cols(const float* p, long long ld);        // (r,k) at p[k*ld+r]
 fx_gemm_desc gemm_desc(int M, int N, int K, fx_operand a, fx_operand b, float* c, long long ldc);
 
 // column sums: out[n] (+)= sum_m X[m*ld + n]   (bias gradients)
+int launch_colsum_batched(const float* x, long long ld, long long x_bs, int M, int N, int nb, float* out,
+                          long long out_bs, int accumulate, float* ws, hipStream_t s);
 int launch_colsum(const float* x, long long ld, int M, int N, float* out, int accumulate,
                   float* ws, hipStream_t s);
 

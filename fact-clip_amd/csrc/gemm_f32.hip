@@ -68,6 +68,8 @@ struct GemmDev {
   unsigned drop_thr;    // dropout (fx_drop_bits >= drop_thr keeps); 0 = off
   float drop_scale;
   unsigned long long drop_seed;
+  long long c_last_bs;  // c_last of batch b at c_last + b * c_last_bs
+  int b_dil_growth;     // > 1: B's conv dilation of batch b is conv_dil * growth^b
 };
 
 // Diagnostic builds (-DFX_STAMPS) record s_memtime / s_memrealtime at fixed points of
@@ -90,6 +92,14 @@ struct GemmDev {
 
 __device__ __forceinline__ int conv_shift(const fx_operand& o, int tap) {
   return (tap - (o.conv_taps - 1) / 2) * o.conv_dil * o.conv_dir;
+}
+
+// B operand of batch bidx: a per-batch conv dilation (dilation stacks: layer b's conv_dil * growth^b)
+__device__ __forceinline__ fx_operand batch_op_b(const fx_operand& b, int growth, int bidx) {
+  fx_operand o = b;
+  if (growth > 1)
+    for (int i = 0; i < bidx; ++i) o.conv_dil *= growth;
+  return o;
 }
 
 // ---------------------------------------------------------------- generic element fetch
@@ -314,7 +324,7 @@ struct Loader {
 // c_tap_cin != 0: output column n = tap*c_tap_cin + c is stored at c*3 + tap (Conv1d weight layout)
 // c_last != NULL: output column N-1 goes to c_last[m] (fused bias gradient)
 __device__ __forceinline__ float* epilogue_ptr(const GemmDev& g, int b, int m, int n) {
-  if (g.c_last && n == g.N - 1) return g.c_last + (long long)b * g.M + m;
+  if (g.c_last && n == g.N - 1) return g.c_last + (long long)b * g.c_last_bs + m;
   long long col = n;
   if (g.c_tap_cin) {
     const int j = n / g.c_tap_cin;
@@ -490,7 +500,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_f32_kernel(GemmDev g) {
   Loader<AK, FAST> la;
   Loader<BKIND, FAST> lb;
   la.init(g.a, g.a.ptr + (long long)bidx * g.a.batch_stride, m0, g.M, g.K, tid);
-  lb.init(g.b, g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid);
+  lb.init(batch_op_b(g.b, g.b_dil_growth, bidx), g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid);
 
   f32x16 acc0, acc1;
 #pragma unroll
@@ -714,7 +724,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_f32_wide_kernel(GemmDev g) {
   const float* pa = g.a.ptr + (long long)bidx * g.a.batch_stride;
   la0.init(g.a, pa, m0, g.M, g.K, tid);
   la1.init(g.a, pa, m0 + BM, g.M, g.K, tid);
-  lb.init(g.b, g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid);
+  lb.init(batch_op_b(g.b, g.b_dil_growth, bidx), g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid);
   f32x16 acc0, acc1;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -860,7 +870,7 @@ __global__ __launch_bounds__(W8T) void gemm_f32_wide8_kernel(GemmDev g) {
   const float* pa = g.a.ptr + (long long)bidx * g.a.batch_stride;
   la0.init(g.a, pa, m0, g.M, g.K, tid);
   la1.init(g.a, pa, m0 + BM, g.M, g.K, tid);
-  lb.init(g.b, g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid);
+  lb.init(batch_op_b(g.b, g.b_dil_growth, bidx), g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid);
   f32x16 acc0, acc1;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -993,7 +1003,7 @@ __global__ __launch_bounds__(W8T) void gemm_bf16_wide8_kernel(GemmDev g) {
   const float* pa = g.a.ptr + (long long)bidx * g.a.batch_stride;
   la0.init(g.a, pa, m0, g.M, g.K, tid);
   la1.init(g.a, pa, m0 + BM, g.M, g.K, tid);
-  lb.init(g.b, g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid);
+  lb.init(batch_op_b(g.b, g.b_dil_growth, bidx), g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid);
   f32x16 acc0, acc1;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -1283,10 +1293,14 @@ __global__ __launch_bounds__(DMAXW * 64) void gemm_direct_group_kernel(GemmGroup
 
 // bias-gradient column sums, two deterministic stages (used only where no dW GEMM carries them)
 constexpr int CS_ROWS = 128;
-__global__ __launch_bounds__(256) void colsum_stage1(const float* x, long long ld, int M, int N, float* ws) {
+// batch z: x + z * x_bs, partials at ws + z * nblk * N, out + z * out_bs
+__global__ __launch_bounds__(256) void colsum_stage1(const float* x, long long ld, long long x_bs, int M, int N,
+                                                     float* ws) {
   const int n = blockIdx.x * 64 + (threadIdx.x & 63);
   const int rg = threadIdx.x >> 6;
   const int r0 = blockIdx.y * CS_ROWS;
+  x += (long long)blockIdx.z * x_bs;
+  ws += (long long)blockIdx.z * gridDim.y * N;
   float s = 0.f;
   if (n < N)
     for (int r = r0 + rg; r < min(M, r0 + CS_ROWS); r += 4) s += x[(long long)r * ld + n];
@@ -1297,9 +1311,12 @@ __global__ __launch_bounds__(256) void colsum_stage1(const float* x, long long l
                                                             red[2][threadIdx.x] + red[3][threadIdx.x];
 }
 
-__global__ __launch_bounds__(256) void colsum_stage2(const float* ws, int nblk, int N, float* out, int acc) {
+__global__ __launch_bounds__(256) void colsum_stage2(const float* ws, int nblk, int N, float* out, long long out_bs,
+                                                     int acc) {
   const int n = blockIdx.x * 256 + threadIdx.x;
   if (n >= N) return;
+  ws += (long long)blockIdx.y * nblk * N;
+  out += (long long)blockIdx.y * out_bs;
   float s = 0.f;
   for (int b = 0; b < nblk; ++b) s += ws[(long long)b * N + n];
   out[n] = acc ? out[n] + s : s;
@@ -1606,6 +1623,9 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
   g.relu = d.relu;
   g.c_tap_cin = d.c_tap_cin;
   g.c_last = d.c_last_col;
+  g.c_last_bs = d.c_last_batch_stride ? d.c_last_batch_stride : d.M;
+  g.b_dil_growth = d.b_dil_growth;
+  FX_REQUIRE(d.b_dil_growth <= 1 || (d.b.conv_taps && d.b.trans), "gemm: b_dil_growth needs a column-major conv B");
   g.stamps = d.dbg_stamps;
   FX_REQUIRE(d.drop_p >= 0.f && d.drop_p < 1.f, "gemm: dropout p must be in [0, 1)");
   FX_REQUIRE(d.drop_p == 0.f || (!d.c_last_col && !d.c_tap_cin && !d.gate && d.beta == 0.f &&
@@ -1625,7 +1645,7 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
   const int ak = kind_of(d.a, g.a_vec), bk = kind_of(d.b, g.b_vec);
   P.ak = ak;
   P.bk = bk;
-  const bool direct = use_direct(d, ak, bk);
+  const bool direct = d.b_dil_growth <= 1 && use_direct(d, ak, bk);   // (the direct kernel: one dilation)
   bool wide = false;
   const int cap = (d.split_k > 1 && d.workspace) ? d.split_k : 1;   // workspace holds `cap` slabs
   FX_REQUIRE(!(d.split_k > 1 && !d.workspace), "gemm: split-K needs a workspace");
@@ -1823,18 +1843,24 @@ int launch_gemm_group(const fx_gemm_desc* d, int n, hipStream_t s) {
   return FX_OK;
 }
 
-int launch_colsum(const float* x, long long ld, int M, int N, float* out, int accumulate, float* ws,
-                  hipStream_t s) {
-  if (N == 0) return FX_OK;
+int launch_colsum_batched(const float* x, long long ld, long long x_bs, int M, int N, int nb, float* out,
+                          long long out_bs, int accumulate, float* ws, hipStream_t s) {
+  if (N == 0 || nb == 0) return FX_OK;
   if (M == 0) {
-    if (!accumulate) FX_CHECK_HIP(hipMemsetAsync(out, 0, sizeof(float) * N, s));
+    if (!accumulate)
+      for (int b = 0; b < nb; ++b) FX_CHECK_HIP(hipMemsetAsync(out + (long long)b * out_bs, 0, sizeof(float) * N, s));
     return FX_OK;
   }
   const int nblk = cdiv(M, CS_ROWS);
-  hipLaunchKernelGGL(colsum_stage1, dim3(cdiv(N, 64), nblk), dim3(256), 0, s, x, ld, M, N, ws);
-  hipLaunchKernelGGL(colsum_stage2, dim3(cdiv(N, 256)), dim3(256), 0, s, ws, nblk, N, out, accumulate);
+  hipLaunchKernelGGL(colsum_stage1, dim3(cdiv(N, 64), nblk, nb), dim3(256), 0, s, x, ld, x_bs, M, N, ws);
+  hipLaunchKernelGGL(colsum_stage2, dim3(cdiv(N, 256), nb), dim3(256), 0, s, ws, nblk, N, out, out_bs, accumulate);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
+}
+
+int launch_colsum(const float* x, long long ld, int M, int N, float* out, int accumulate, float* ws,
+                  hipStream_t s) {
+  return launch_colsum_batched(x, ld, 0, M, N, 1, out, 0, accumulate, ws, s);
 }
 
 long long colsum_workspace_floats(int M, int N) { return (long long)cdiv(M, CS_ROWS) * N; }

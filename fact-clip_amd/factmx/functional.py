@@ -644,6 +644,92 @@ def mstcn(mod, x, T, nvid=1):
     return MSTCNFn.apply(x2, meta, *params)
 
 
+class MSTCN2Fn(torch.autograd.Function):
+    """Whole ``MSTCN2.forward`` (basic.py:263-281, MS-TCN++) in one C call: per layer the two dilated
+    convs store into the halves of one concat buffer, the 1x1 fusion GEMM applies bias + ReLU (+ the
+    training dropout of every layer but the last, counter-based mask from the seed in meta), one add
+    forms the residual.  Backward: the input-gradient chain, then the weight gradients of all layers
+    as batched GEMMs on the side stream.
+    params: [w_in, b_in] (in_map) + w_d1 x L, b_d1 x L, w_d2 x L, b_d2 x L, w_fu x L, b_fu x L + w_out, b_out."""
+
+    @staticmethod
+    def _unpack(meta, params):
+        nl, in_map = meta[5], meta[6]
+        it = list(params)
+        w_in = b_in = None
+        if in_map:
+            w_in, b_in, it = it[0], it[1], it[2:]
+        groups = [it[k * nl:(k + 1) * nl] for k in range(6)]
+        return w_in, b_in, groups, it[6 * nl], it[6 * nl + 1]
+
+    @staticmethod
+    def _prm(meta, params, keep, cls, grads=False):
+        T, nvid, cin, F, cout, nl, in_map, dfac, drop_p, seed = meta
+        w_in, b_in, groups, w_out, b_out = MSTCN2Fn._unpack(meta, params)
+        prm = cls()
+        if not grads:
+            prm.cin, prm.F, prm.cout, prm.num_layers, prm.in_map, prm.dil_factor = cin, F, cout, nl, int(in_map), dfac
+            prm.dropout, prm.seed = float(drop_p), int(seed)
+        prm.w_in, prm.b_in = nx.ptr(w_in), nx.ptr(b_in)
+        for field, grp in zip(("w_d1", "b_d1", "w_d2", "b_d2", "w_fu", "b_fu"), groups):
+            arr = _ptr_array(grp)
+            keep.append(arr)
+            setattr(prm, field, ctypes.cast(arr, ctypes.c_void_p))
+        prm.w_out, prm.b_out = nx.ptr(w_out), nx.ptr(b_out)
+        return prm
+
+    @staticmethod
+    def forward(ctx, x, meta, *params):
+        lib = nx.load()
+        T, nvid, cout = meta[0], meta[1], meta[4]
+        keep = []
+        prm = MSTCN2Fn._prm(meta, params, keep, nx.Mstcn2Params)
+        rows = x.shape[0]
+        dev = x.device
+        y = _empty(rows, cout, device=dev)
+        saved = _ws(lib.fx_mstcn2_saved_floats(ctypes.byref(prm), rows), dev)
+        ws = _ws(lib.fx_mstcn2_workspace_floats(ctypes.byref(prm), rows), dev)
+        _check(lib.fx_mstcn2_fwd(ctypes.byref(prm), nx.ptr(x), nx.ld(x), T, nvid, nx.ptr(y), cout, nx.ptr(saved),
+                                 nx.ptr(ws), nx.stream()), "fx_mstcn2_fwd")
+        ctx.meta, ctx.prm, ctx.keep = meta, prm, keep
+        ctx.save_for_backward(x, saved, *params)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = nx.load()
+        x, saved, *params = ctx.saved_tensors
+        T, nvid, cout = ctx.meta[0], ctx.meta[1], ctx.meta[4]
+        dev = x.device
+        dy = dy.contiguous()
+        tg = [grad_target(p) for p in params]
+        keep = []
+        g = MSTCN2Fn._prm(ctx.meta, [t[0] for t in tg], keep, nx.Mstcn2Grads, grads=True)
+        dx = _empty(*x.shape, device=dev) if ctx.needs_input_grad[0] else None
+        ws = _ws(lib.fx_mstcn2_workspace_floats(ctypes.byref(ctx.prm), x.shape[0]), dev)
+        defer = DEFER_SIDE and side_stream() is not None
+        ctx.prm.side_defer = int(defer)
+        _check(lib.fx_mstcn2_bwd(ctypes.byref(ctx.prm), ctypes.byref(g), nx.ptr(x), nx.ld(x), T, nvid, nx.ptr(dy),
+                                 cout, nx.ptr(dx), nx.ld(dx), nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_mstcn2_bwd")
+        if defer:
+            _defer_to_side(x, dy, saved, ws)
+        return (dx, None) + tuple(t[1] for t in tg)
+
+
+def mstcn2(mod, x, T, nvid=1, drop_p=0.0):
+    """Run a factmx.models.basic.MSTCN2 through MSTCN2Fn (x: (nvid*T, dim) rows)."""
+    x2 = _2d(x)
+    L = mod.num_layers
+    params = [mod.conv_1x1_in.weight, mod.conv_1x1_in.bias] if mod.in_map else []
+    params += [c.weight for c in mod.conv_dilated_1] + [c.bias for c in mod.conv_dilated_1]
+    params += [c.weight for c in mod.conv_dilated_2] + [c.bias for c in mod.conv_dilated_2]
+    params += [c.weight for c in mod.conv_fusion] + [c.bias for c in mod.conv_fusion]
+    params += [mod.conv_out.weight, mod.conv_out.bias]
+    meta = (T, nvid, x2.shape[1], mod.conv_out.weight.shape[1], mod.conv_out.weight.shape[0], L, bool(mod.in_map),
+            int(mod.dilation_factor), float(drop_p), dropout_seed() if drop_p > 0 else 0)
+    return MSTCN2Fn.apply(x2, meta, *params)
+
+
 # ---------------------------------------------------------------------------
 # generic dilated Conv1d(k=3) (MSTCN2 / standalone DilatedResidualLayer pieces)
 # ---------------------------------------------------------------------------

@@ -204,20 +204,11 @@ class MSTCN2(nn.Module):
 
     def forward(self, x, T=None):
         """x: (T, 1, dim) or, lockstep, (nvid*T, dim) rows of nvid stacked videos of T frames each (the
-        dilated convs zero-pad at every video's ends)."""
-        T = T or x.shape[0]
-        f = fxf.linear(x, self.conv_1x1_in.weight, self.conv_1x1_in.bias) if self.in_map else fxf._2d(x)
-        L = self.num_layers
-        for i in range(L):
-            f_in = f
-            a = fxf.conv3(f, self.conv_dilated_1[i].weight, self.conv_dilated_1[i].bias,
-                          self.dilation_factor ** (L - 1 - i), T)
-            b = fxf.conv3(f, self.conv_dilated_2[i].weight, self.conv_dilated_2[i].bias, self.dilation_factor ** i, T)
-            f = fxf.linear(torch.cat([a, b], 1), self.conv_fusion[i].weight, self.conv_fusion[i].bias, relu=True)
-            if i != L - 1:
-                f = _dropout(f, self.dropout.p, self.training)
-            f = f + f_in
-        return _as3d(fxf.linear(f, self.conv_out.weight, self.conv_out.bias))
+        dilated convs zero-pad at every video's ends).  The whole stack is one fx_mstcn2 call."""
+        x2 = fxf._2d(x)
+        T = T or x2.shape[0]
+        p = float(self.dropout.p) if (self.training and self.dropout.p) else 0.0
+        return _as3d(fxf.mstcn2(self, x2, T, x2.shape[0] // T, drop_p=p))
 
 
 class ActionUpdate_GRU(nn.Module):

@@ -154,8 +154,8 @@ class Block(nn.Module):
 
 
 def _frame_branch_batch(branch, f, vb):
-    """The frame branch over vb.nvid stacked videos: MS-TCN as one fused stack call, MS-TCN++ (MSTCN2)
-    layer by layer with per-video zero padding."""
+    """The frame branch over vb.nvid stacked videos: MS-TCN and MS-TCN++ (MSTCN2) each as one fused
+    stack call with per-video zero padding."""
     if isinstance(branch, basic.MSTCN2):
         return fxf._2d(branch(f, T=vb.T))
     return fxf.mstcn(branch, f, T=vb.T, nvid=vb.nvid)

@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FACTMX_LIB", os.path.join(_HERE, "_lib", "libfactmx.so"))
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -37,7 +37,7 @@ class GemmDesc(ctypes.Structure):
                 ("c_batch_stride", L), ("alpha", F), ("beta", F), ("bias", P), ("resid", P), ("ld_resid", L),
                 ("resid_batch_stride", L), ("gate", P), ("ld_gate", L), ("relu", I), ("c_tap_cin", I),
                 ("split_k", I), ("workspace", P), ("c_last_col", P), ("dbg_stamps", P), ("drop_p", F),
-                ("drop_seed", U)]
+                ("drop_seed", U), ("c_last_batch_stride", L), ("b_dil_growth", I)]
 
 
 class MstcnParams(ctypes.Structure):
@@ -45,6 +45,17 @@ class MstcnParams(ctypes.Structure):
                 ("dil0", I), ("dil_factor", I), ("w_in", P), ("b_in", P), ("w_dil", P), ("b_dil", P), ("w_pw", P), ("b_pw", P),
                 ("ln_w", P), ("ln_b", P), ("w_out", P), ("b_out", P), ("dropout", F), ("seed", U),
                 ("side_defer", I)]
+
+
+class Mstcn2Params(ctypes.Structure):
+    _fields_ = [("cin", I), ("F", I), ("cout", I), ("num_layers", I), ("in_map", I), ("dil_factor", I),
+                ("w_in", P), ("b_in", P), ("w_d1", P), ("b_d1", P), ("w_d2", P), ("b_d2", P), ("w_fu", P),
+                ("b_fu", P), ("w_out", P), ("b_out", P), ("dropout", F), ("seed", U), ("side_defer", I)]
+
+
+class Mstcn2Grads(ctypes.Structure):
+    _fields_ = [("w_in", P), ("b_in", P), ("w_d1", P), ("b_d1", P), ("w_d2", P), ("b_d2", P), ("w_fu", P),
+                ("b_fu", P), ("w_out", P), ("b_out", P)]
 
 
 class MstcnGrads(ctypes.Structure):
@@ -87,7 +98,7 @@ class VideoAttn(ctypes.Structure):
                 ("seg_id", P), ("flogit", P), ("ldf", L), ("gs", P), ("ge", P), ("gl", P), ("pred_off", L)]
 
 
-ABI_STRUCTS = (GemmDesc, DecoderParams, MstcnParams, LossTerm, VideoAttn)   # fx_struct_size ids
+ABI_STRUCTS = (GemmDesc, DecoderParams, MstcnParams, LossTerm, VideoAttn, Mstcn2Params)   # fx_struct_size ids
 
 
 # name -> (restype, argtypes); every fx_* symbol declared in include/factmx.h
@@ -117,6 +128,10 @@ SIGNATURES = {
     "fx_mstcn_workspace_floats": (L, [ctypes.POINTER(MstcnParams), I]),
     "fx_mstcn_fwd": (I, [ctypes.POINTER(MstcnParams), P, L, I, I, P, L, P, P, P]),
     "fx_mstcn_bwd": (I, [ctypes.POINTER(MstcnParams), ctypes.POINTER(MstcnGrads), P, L, I, I, P, L, P, L, P, P, P]),
+    "fx_mstcn2_saved_floats": (L, [ctypes.POINTER(Mstcn2Params), I]),
+    "fx_mstcn2_workspace_floats": (L, [ctypes.POINTER(Mstcn2Params), I]),
+    "fx_mstcn2_fwd": (I, [ctypes.POINTER(Mstcn2Params), P, L, I, I, P, L, P, P, P]),
+    "fx_mstcn2_bwd": (I, [ctypes.POINTER(Mstcn2Params), ctypes.POINTER(Mstcn2Grads), P, L, I, I, P, L, P, L, P, P, P]),
     "fx_layernorm_fwd": (I, [P, L, P, L, P, P, F, I, I, I, P, L, P, L, P, P]),
     "fx_layernorm_bwd_workspace_floats": (L, [I, I]),
     "fx_layernorm_bwd": (I, [P, L, P, L, P, L, P, P, I, I, I, P, L, P, P, P, P]),

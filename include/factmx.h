@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FX_ABI_VERSION 11
+#define FX_ABI_VERSION 12
 
 enum {
   FX_OK = 0,
@@ -39,7 +39,7 @@ enum {
 int fx_version(void);
 const char* fx_last_error(void);
 /* sizeof of the ABI structs (0 gemm_desc, 1 decoder_params, 2 mstcn_params, 3 loss_term,
- * 4 video_attn) so bindings can check their layouts; -1 for an unknown id */
+ * 4 video_attn, 5 mstcn2_params) so bindings can check their layouts; -1 for an unknown id */
 long long fx_struct_size(int which);
 
 /* ------------------------------------------------------------------------
@@ -107,6 +107,9 @@ typedef struct fx_gemm_desc {
   long long* dbg_stamps;      /* diagnostic builds (-DFX_STAMPS) only: per-block timestamps */
   float drop_p;               /* > 0: dropout on (alpha acc + bias [relu]) before the residual add */
   unsigned long long drop_seed; /* mask of output (b, m, n): fx_dropout index (b M + m) N + n */
+  long long c_last_batch_stride; /* c_last_col of batch b at c_last_col + b*stride (0: M) */
+  int b_dil_growth;           /* > 1: B's conv_dil of batch b is conv_dil * growth^b (one launch for
+                                 the dilated-conv weight gradients of every layer of a stack) */
 } fx_gemm_desc;
 
 int fx_gemm(const fx_gemm_desc* desc, void* stream);
@@ -284,6 +287,45 @@ int fx_mstcn_fwd(const fx_mstcn_params* p, const float* x, long long ldx, int T,
 int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float* x, long long ldx,
                  int T, int nvid, const float* dy, long long lddy, float* dx, long long lddx,
                  const float* saved, float* workspace, void* stream);
+
+/* ------------------------------------------------------------------------
+ * MSTCN2 -- the MS-TCN++ frame branch of vanilla FACT (Breakfast config, BASELINE configs[0]).
+ * Replaces basic.py:222-281 MSTCN2.forward (in_map 1x1, per layer i:
+ *   f' = f + dropout_i(relu(W_fu,i . cat[conv_d1,i(f), conv_d2,i(f)] + b_fu,i)),
+ * conv_d1,i dilation dil_factor^(L-1-i), conv_d2,i dilation dil_factor^i, no dropout on the last
+ * layer, then conv_out) for nvid stacked videos of T rows (zero padding at every video's ends).
+ * Weight shapes as the reference's Conv1d (w_d*: (F, F, 3), w_fu: (F, 2F)); ngroup 1, no LN.
+ * Gradients ACCUMULATE; the weight-gradient GEMMs of all layers run after the input-gradient chain
+ * as batched launches on the side stream (per layer when the gradient buffers are not uniformly
+ * strided).  side_defer as fx_mstcn_params.
+ * ---------------------------------------------------------------------- */
+typedef struct fx_mstcn2_params {
+  int cin, F, cout, num_layers, in_map, dil_factor;
+  const float* w_in; const float* b_in;
+  const float* const* w_d1; const float* const* b_d1;
+  const float* const* w_d2; const float* const* b_d2;
+  const float* const* w_fu; const float* const* b_fu;
+  const float* w_out; const float* b_out;
+  float dropout;
+  unsigned long long seed;
+  int side_defer;
+} fx_mstcn2_params;
+
+typedef struct fx_mstcn2_grads {
+  float* w_in; float* b_in;
+  float* const* w_d1; float* const* b_d1;
+  float* const* w_d2; float* const* b_d2;
+  float* const* w_fu; float* const* b_fu;
+  float* w_out; float* b_out;
+} fx_mstcn2_grads;
+
+long long fx_mstcn2_saved_floats(const fx_mstcn2_params* p, int rows);
+long long fx_mstcn2_workspace_floats(const fx_mstcn2_params* p, int rows);
+int fx_mstcn2_fwd(const fx_mstcn2_params* p, const float* x, long long ldx, int T, int nvid,
+                  float* y, long long ldy, float* saved, float* workspace, void* stream);
+int fx_mstcn2_bwd(const fx_mstcn2_params* p, const fx_mstcn2_grads* g, const float* x, long long ldx,
+                  int T, int nvid, const float* dy, long long lddy, float* dx, long long lddx,
+                  const float* saved, float* workspace, void* stream);
 
 /* ------------------------------------------------------------------------
  * Row-wise LayerNorm with fused residual (post-norm residual blocks,

@@ -23,13 +23,22 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _gpu_step(net, vids):
+def _gpu_step(net, vids, dp=None):
+    """One forward + loss + backward.  dp (factmx.dp.DataParallel, world size 1): gradients land in
+    its flat buffer exactly as in bench.py's timed step -- the MS-TCN backward then takes the deferred
+    batched weight-gradient GEMMs (uniformly strided gradient views); without it every .grad is its
+    own allocation and the per-layer interleaved GEMMs run."""
     seqs = [torch.from_numpy(f).to(DEV) for f, _ in vids]
     labs = [torch.from_numpy(l_).to(DEV) for _, l_ in vids]
-    for p in net.parameters():
-        p.grad = None
+    if dp is not None:
+        dp.zero_grad()
+    else:
+        for p in net.parameters():
+            p.grad = None
     loss, saves = net(seqs, labs, compute_loss=True)
     loss.backward()
+    if dp is not None:
+        dp.finish_gradients()
     torch.cuda.synchronize()
     return loss.item(), saves
 
@@ -64,7 +73,8 @@ def test_north_star_lockstep_backward_vs_oracle(monkeypatch):
     vids = [bench.make_video(T, D, C, cfg, seed=s) for s in (1, 2)]
     assert blocks_mod._batchable(net, [torch.zeros(T, 1, device=DEV)] * 2)
     kinks = GruKinks(monkeypatch)
-    loss, saves = _gpu_step(net, vids)
+    from factmx.dp import DataParallel
+    loss, saves = _gpu_step(net, vids, dp=DataParallel(net))
     S = _segments(net)
     grads = {n: p.grad.detach().clone() for n, p in net.named_parameters()}
     spec = fo.resolve_spec(cfg, D, C, clip=True)
