@@ -275,6 +275,17 @@ struct MstcnLayout {
   long long wf, wb, wpt, buf0, buf1, buf2, buf3, buf4, buf5, split, split2, colsum, dzall, dhall, csb, bsl, total_ws;
 };
 
+// Split of the deferred batched weight-gradient GEMMs (fx_mstcn_bwd): each workgroup of a batched
+// launch otherwise walks all K = rows and holds its CU for the whole launch, so the main stream's
+// next kernels wait for CUs; FX_DEFER_SPLIT=n caps a workgroup's share at K / n (A/B knob).
+int defer_split_impl(int rows) {
+  static const int sp = [] {
+    const char* e = std::getenv("FX_DEFER_SPLIT");
+    return e ? std::max(1, std::min(16, std::atoi(e))) : 8;
+  }();
+  return std::max(1, std::min(sp, rows / 512));
+}
+
 MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
   MstcnLayout L{};
   const long long F = p->F;
@@ -314,7 +325,9 @@ MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
   L.dhall = L.dzall + NL * L.rowsF;
   L.csb = L.dhall + NL * L.rowsF;
   L.bsl = L.csb + (long long)NL * colsum_workspace_floats(rows, p->F);
-  L.total_ws = L.bsl + split_ws(p->F, p->F + 1, rows, std::max(NL, 1));
+  const int dsp = defer_split_impl(rows);
+  L.total_ws = L.bsl + std::max(split_ws(p->F, p->F + 1, rows, std::max(NL, 1)),
+                                dsp > 1 ? (long long)dsp * std::max(NL, 1) * p->F * (3LL * p->F) : 0LL);
   return L;
 }
 
@@ -659,9 +672,9 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
       d.c_last_col = g->b_pw[0];
       d.c_last_batch_stride = NL > 1 ? g->b_pw[1] - g->b_pw[0] : 0;
       d.beta = 1.f;
-      d.split_k = pick_split(F, F + 1, rows, NL);
+      d.split_k = std::max(pick_split(F, F + 1, rows, NL), defer_split_impl(rows));
       d.workspace = ws + L.bsl;
-      WsBound wbb(ws + L.bsl, split_ws(F, F + 1, rows, NL));
+      WsBound wbb(ws + L.bsl, L.total_ws - L.bsl);
       FX_TRY(launch_gemm(d, sd));
     }
     {   // dilated conv: dW_i += dZ_i^T taps(h_i) stored straight into (F, F, 3)   (batched over layers)
@@ -675,6 +688,9 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
       d.b_dil_growth = p->dil_factor > 0 ? p->dil_factor : 2;
       d.c_tap_cin = F;
       d.beta = 1.f;
+      d.split_k = defer_split_impl(rows);
+      d.workspace = ws + L.bsl;
+      WsBound wbb(ws + L.bsl, L.total_ws - L.bsl);
       FX_TRY(launch_gemm(d, sd));
       FX_TRY(launch_colsum_batched(dZall, F, L.rowsF, rows, F, NL, g->b_dil[0],
                                    NL > 1 ? g->b_dil[1] - g->b_dil[0] : 0, 1, ws + L.csb, sd));
@@ -1030,6 +1046,30 @@ int fx_mstcn2_bwd(const fx_mstcn2_params* p, const fx_mstcn2_grads* g, const flo
   }
   return FX_OK;
 }
+
+}  // extern "C"
+
+namespace fx {
+hipStream_t side_fork(hipStream_t s, int e) {
+  SideStream* ss = side_stream();
+  if (!ss) return s;
+  if (hipEventRecord(ss->to_side[e], s) != hipSuccess || hipStreamWaitEvent(ss->s, ss->to_side[e], 0) != hipSuccess)
+    return s;
+  return ss->s;
+}
+
+int side_join_into(hipStream_t s) {
+  SideStream* ss = side_stream();
+  if (!ss) return FX_OK;
+  FX_CHECK_HIP(hipEventRecord(ss->join, ss->s));
+  FX_CHECK_HIP(hipStreamWaitEvent(s, ss->join, 0));
+  return FX_OK;
+}
+
+int defer_split(int rows) { return defer_split_impl(rows); }
+}  // namespace fx
+
+extern "C" {
 
 void* fx_side_stream(void) {
   SideStream* ss = side_stream();

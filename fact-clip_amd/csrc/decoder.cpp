@@ -141,6 +141,8 @@ long long dec_split_ws(const fx_decoder_params* p, int R, int T) {
     sp = std::max(sp, split_ws(T, p->Hm, (int)AL2));
     // key rows only (the memory-pos gradient and its dW piece): half the tiles, up to twice the split
     sp = std::max(sp, dwdb_ws(T, p->Hm, (int)(AL2 / 2)));
+    // the K/V weight gradient on the side stream, split defer_split(T) ways
+    sp = std::max(sp, (long long)defer_split(T) * AL2 * (p->Hm + 1));
     sp = std::max(sp, split_ws(T, p->Hm, (int)(AL2 / 2)));
   }
   return sp;
@@ -478,12 +480,21 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
       if (dmem) FX_TRY(linear_dx(dkv, AL2, wkv, T, p->Hm, AL2, dmem, lddm, 0, nullptr, 0, spl, s));
       if (dmpos) FX_TRY(linear_dx(dkv, AL2, wkv, T, p->Hm, AL, dmpos, lddmp, 0, nullptr, 0, spl, s));
     }
+    // dWkv = dKV^T [mem+pos | mem] and its unpacking into the parameter gradients depend on nothing
+    // the rest of the backward needs: side stream (the frame-level GEMM, K = T rows, leaves the main
+    // stream), split so each workgroup holds its CU for a short K range
+    hipStream_t sd = side_fork(s, 2);
+    const int ksp = sd != s ? defer_split(T) : 1;
+    auto dw = [&](const float* a, const float* x, long long ldx_, int N, float* w, float* b) -> int {
+      fx_gemm_desc d = desc_linear_dwdb(a, AL2, x, ldx_, T, p->Hm, N, w, b, 0, spl);
+      d.split_k = std::max(d.split_k, ksp);
+      return launch_gemm(d, sd);
+    };
     if (!mpos) {
-      FX_TRY(linear_dwdb(dkv, AL2, mem, ldm, T, p->Hm, AL2, wkv, ws + L.dbkv, 0, spl, s));
+      FX_TRY(dw(dkv, mem, ldm, AL2, wkv, ws + L.dbkv));
     } else {
-      FX_TRY(linear_dwdb(dkv, AL2, saved + L.mpos, p->Hm, T, p->Hm, AL, wkv, ws + L.dbkv, 0, spl, s));
-      FX_TRY(linear_dwdb(dkv + AL, AL2, mem, ldm, T, p->Hm, AL, wkv + (long long)AL * p->Hm, ws + L.dbkv + AL, 0, spl,
-                         s));
+      FX_TRY(dw(dkv, saved + L.mpos, p->Hm, AL, wkv, ws + L.dbkv));
+      FX_TRY(dw(dkv + AL, mem, ldm, AL, wkv + (long long)AL * p->Hm, ws + L.dbkv + AL));
     }
     UnpackKV uk{};
     for (int l = 0; l < NL; ++l) {
@@ -498,8 +509,9 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
     uk.Hm = p->Hm;
     uk.L = NL;
     hipLaunchKernelGGL(unpack_kv_acc_kernel, dim3(std::min(cdiv((long long)A * p->Hm, 256), 256), 2 * NL), dim3(256),
-                       0, s, uk);
+                       0, sd, uk);
     FX_CHECK_HIP(hipGetLastError());
+    if (sd != s && !p->side_defer) FX_TRY(side_join_into(s));
   }
   return FX_OK;
 }

@@ -62,6 +62,14 @@ struct GridCap {
   ~GridCap();
   int prev;
 };
+// The library's side stream (one per device; FX_SIDE_STREAM=0: none).  side_fork: the side stream
+// (after making it wait for everything enqueued on s so far), or s itself when there is none;
+// side_join_into: s waits for everything enqueued on the side stream.
+hipStream_t side_fork(hipStream_t s, int event);
+int side_join_into(hipStream_t s);
+// split-K factor for weight-gradient GEMMs deferred to the side stream over `rows` rows (keeps each
+// workgroup's share of K short, so the main stream's kernels find free CUs)
+int defer_split(int rows);
 // workspace floats needed by a split-K descriptor
 long long gemm_workspace_floats(const fx_gemm_desc& d);
 

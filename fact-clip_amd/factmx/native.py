@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FACTMX_LIB", os.path.join(_HERE, "_lib", "libfactmx.so"))
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -72,7 +72,8 @@ DECODER_GLOBAL_FIELDS = ["fn_w", "fn_b", "out_w", "out_b"]
 
 class DecoderParams(ctypes.Structure):
     _fields_ = ([("A", I), ("FF", I), ("nhead", I), ("num_layers", I), ("cross", I), ("Hm", I), ("out_dim", I),
-                 ("final_norm", I), ("eps", F)] + [(n, P) for n in _DEC_PTRS] + [(n, P) for n in DECODER_GLOBAL_FIELDS])
+                 ("final_norm", I), ("eps", F)] + [(n, P) for n in _DEC_PTRS] + [(n, P) for n in DECODER_GLOBAL_FIELDS]
+                + [("side_defer", I)])
 
 
 class DecoderGrads(ctypes.Structure):

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FX_ABI_VERSION 12
+#define FX_ABI_VERSION 13
 
 enum {
   FX_OK = 0,
@@ -210,6 +210,8 @@ typedef struct fx_decoder_params {
   const float* const* ln_ff_w; const float* const* ln_ff_b;
   const float* fn_w; const float* fn_b;
   const float* out_w; const float* out_b;
+  int side_defer;             /* bwd (cross): leave the frame-memory K/V weight-gradient GEMM running on the
+                                 library's side stream (joined by fx_side_join), as fx_mstcn_params */
 } fx_decoder_params;
 
 typedef struct fx_decoder_grads {
