@@ -270,7 +270,7 @@ SideStream* side_stream() {
 struct MstcnLayout {
   long long rowsF;
   // saved
-  long long h, z, xh, rs, total_saved;
+  long long h, z, xh, rs, wbs, total_saved;
   // workspace
   long long wf, wb, wpt, buf0, buf1, buf2, buf3, buf4, buf5, split, split2, colsum, dzall, dhall, csb, bsl, total_ws;
 };
@@ -295,8 +295,9 @@ MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
   L.z = L.h + (NL + 1) * L.rowsF;            // z_0 .. z_{NL-1}
   L.xh = L.z + NL * L.rowsF;                 // LN xhat_i
   L.rs = L.xh + (p->layernorm ? NL * L.rowsF : 0);
-  L.total_saved = L.rs + (p->layernorm ? (long long)NL * rows : 0);
+  L.wbs = L.rs + (p->layernorm ? (long long)NL * rows : 0);   // dX-packed conv weights (fwd packs, bwd reads)
   const long long wsz = 3 * F * F;
+  L.total_saved = L.wbs + NL * wsz;
   L.wf = 0;
   L.wb = L.wf + NL * wsz;
   L.wpt = L.wb + NL * wsz;                   // transposed 1x1 weights (fused backward chain)
@@ -331,14 +332,15 @@ MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
   return L;
 }
 
-int pack_conv_weights(const fx_mstcn_params* p, float* ws, const MstcnLayout& L, hipStream_t s, bool want_wpt) {
+int pack_conv_weights(const fx_mstcn_params* p, float* ws, float* wbdst, const MstcnLayout& L, hipStream_t s,
+                      bool want_wpt) {
   PackArgs a{};
   a.F = p->F;
   const long long wsz = 3LL * p->F * p->F;
   for (int l = 0; l < p->num_layers; ++l) {
     a.w[l] = p->w_dil[l];
     a.wf[l] = ws + L.wf + l * wsz;
-    a.wb[l] = ws + L.wb + l * wsz;
+    a.wb[l] = wbdst + l * wsz;
     a.wpw[l] = p->w_pw[l];
     a.wpt[l] = want_wpt ? ws + L.wpt + (long long)l * p->F * p->F : nullptr;
   }
@@ -478,7 +480,7 @@ int fx_mstcn_fwd(const fx_mstcn_params* p, const float* x, long long ldx, int T,
   const int rows = T * nvid;
   const int F = p->F;
   const MstcnLayout L = mstcn_layout(p, rows);
-  FX_TRY(pack_conv_weights(p, workspace, L, s, false));
+  FX_TRY(pack_conv_weights(p, workspace, saved + L.wbs, L, s, false));
   float* h0 = saved + L.h;
   if (p->in_map) {
     FX_TRY(linear_fwd(x, ldx, rows, p->cin, p->w_in, p->b_in, h0, F, F, 0, s));
@@ -537,7 +539,10 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   const bool drop = p->dropout > 0.f;
   // Fused chain (no LayerNorm, no dropout, FX_MSTCN_FUSED=1): see below
   const bool fchain = !p->layernorm && !drop && NL > 0 && frl_supported(F, ws + L.buf0, F, F);
-  FX_TRY(pack_conv_weights(p, ws, L, s, fchain));
+  // the dX-packed conv weights come from the forward (saved); the fused chain also needs the
+  // transposed 1x1 weights (repacked here, into the workspace)
+  if (fchain) FX_TRY(pack_conv_weights(p, ws, ws + L.wb, L, s, true));
+  const float* wbp = fchain ? ws + L.wb : saved + L.wbs;
   float* spl = ws + L.split;     // split-K partials of the weight-gradient GEMMs (side stream)
   float* spm = ws + L.split2;    // ... of the main stream's GEMMs / LN backward
   WsBound wb(spl, L.colsum - L.split);
@@ -651,7 +656,7 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
       FX_TRY(linear_dx(gU, F, p->w_pw[i], rows, F, F, dZ, F, 0, zi, F, spm, s));
       float* dHn = i > 0 ? dHall + (i - 1) * L.rowsF : Hb[0];
       fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dZ, F, F, layer_dilation(p, i), -1, T, false),
-                                 op_rows(ws + L.wb + (long long)i * 3 * F * F, 3 * F), dHn, F);
+                                 op_rows(wbp + (long long)i * 3 * F * F, 3 * F), dHn, F);
       d.resid = gU;
       d.ld_resid = F;
       prof_begin(0, s);
@@ -744,7 +749,7 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
         FX_TRY(wait_side(i + 2));     // that buffer was gU of layer i + 2
       }
       fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dZ, F, F, layer_dilation(p, i), -1, T, false),
-                                 op_rows(ws + L.wb + (long long)i * 3 * F * F, 3 * F), dHn, F);
+                                 op_rows(wbp + (long long)i * 3 * F * F, 3 * F), dHn, F);
       d.resid = gU;
       d.ld_resid = F;
       prof_begin(0, s);
@@ -782,8 +787,8 @@ namespace {
 
 struct Mstcn2Layout {
   long long rowsF;
-  long long f, cat, r, total_saved;                       // saved: f_0..f_L, cat_i (2F), r_i
-  long long wf1, wf2, wb1, wb2, hb0, hb1, du, dcat, spm, spl, bsl, total_ws;
+  long long f, cat, r, wb1, wb2, total_saved;            // saved: f_0..f_L, cat_i (2F), r_i, dX-packed weights
+  long long wf1, wf2, hb0, hb1, du, dcat, spm, spl, bsl, total_ws;
 };
 
 Mstcn2Layout mstcn2_layout(const fx_mstcn2_params* p, int rows) {
@@ -794,13 +799,13 @@ Mstcn2Layout mstcn2_layout(const fx_mstcn2_params* p, int rows) {
   L.f = 0;
   L.cat = L.f + (NL + 1) * L.rowsF;
   L.r = L.cat + 2 * NL * L.rowsF;
-  L.total_saved = L.r + NL * L.rowsF;
   const long long wsz = 3 * F * F;
+  L.wb1 = L.r + NL * L.rowsF;
+  L.wb2 = L.wb1 + NL * wsz;
+  L.total_saved = L.wb2 + NL * wsz;
   L.wf1 = 0;
   L.wf2 = L.wf1 + NL * wsz;
-  L.wb1 = L.wf2 + NL * wsz;
-  L.wb2 = L.wb1 + NL * wsz;
-  L.hb0 = L.wb2 + NL * wsz;                 // input-gradient chain: dF ping-pong
+  L.hb0 = L.wf2 + NL * wsz;                 // input-gradient chain: dF ping-pong
   L.hb1 = L.hb0 + L.rowsF;
   L.du = L.hb1 + L.rowsF;                   // every layer's dU_i (fusion pre-activation gradient)
   L.dcat = L.du + NL * L.rowsF;             // every layer's dCat_i = [dA_i | dB_i]
@@ -870,9 +875,9 @@ int fx_mstcn2_fwd(const fx_mstcn2_params* p, const float* x, long long ldx, int 
   const int rows = T * nvid, F = p->F, NL = p->num_layers;
   const Mstcn2Layout L = mstcn2_layout(p, rows);
   float* ws = workspace;
-  if (NL > 0) {
-    FX_TRY(pack_conv_set(p->w_d1, NL, F, ws + L.wf1, ws + L.wb1, s));
-    FX_TRY(pack_conv_set(p->w_d2, NL, F, ws + L.wf2, ws + L.wb2, s));
+  if (NL > 0) {   // forward images into the workspace, dX images into `saved` for the backward
+    FX_TRY(pack_conv_set(p->w_d1, NL, F, ws + L.wf1, saved + L.wb1, s));
+    FX_TRY(pack_conv_set(p->w_d2, NL, F, ws + L.wf2, saved + L.wb2, s));
   }
   float* f0 = saved + L.f;
   if (p->in_map) {
@@ -920,10 +925,6 @@ int fx_mstcn2_bwd(const fx_mstcn2_params* p, const fx_mstcn2_grads* g, const flo
   const int rows = T * nvid, F = p->F, NL = p->num_layers;
   const Mstcn2Layout L = mstcn2_layout(p, rows);
   float* ws = workspace;
-  if (NL > 0) {   // (the forward's packed images live in the forward's workspace: repack)
-    FX_TRY(pack_conv_set(p->w_d1, NL, F, ws + L.wf1, ws + L.wb1, s));
-    FX_TRY(pack_conv_set(p->w_d2, NL, F, ws + L.wf2, ws + L.wb2, s));
-  }
   SideStream* ss = side_stream();
   hipStream_t sd = ss ? ss->s : s;
   auto fork = [&](int e) -> int {
@@ -962,7 +963,7 @@ int fx_mstcn2_bwd(const fx_mstcn2_params* p, const fx_mstcn2_grads* g, const flo
     for (int h = 0; h < 2; ++h) {
       const int dil = h == 0 ? mstcn2_dil(p, NL - 1 - i) : mstcn2_dil(p, i);
       fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dCat + h * F, 2 * F, F, dil, -1, T, false),
-                                 op_rows(ws + (h == 0 ? L.wb1 : L.wb2) + (long long)i * 3 * F * F, 3 * F), dFn, F);
+                                 op_rows(saved + (h == 0 ? L.wb1 : L.wb2) + (long long)i * 3 * F * F, 3 * F), dFn, F);
       if (h == 0) {
         d.resid = gF;
         d.ld_resid = F;
@@ -1349,6 +1350,17 @@ long long fx_x2y_saved_floats(int Nx, int xdim, int Ny, int ydim, int Hd) {
 }
 
 // [dcat][dL][dxv][dxk][dyq][dXk][dYq][split-K][colsum][catd: dropped cat[Y, feat] (dropout only)]
+// split-K slabs of the weight-gradient GEMMs on the side stream (their own region: the main stream's
+// GEMMs keep using the x2y split region meanwhile)
+static long long x2y_side_ws(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim) {
+  auto one = [](int rows, int M, int N) {
+    const int sp = std::max(pick_split(M, N, rows), defer_split(rows));
+    return sp > 1 ? (long long)sp * M * N : 0LL;
+  };
+  long long w = std::max(one(Ny, outdim, ydim + Hd + 1), one(Nx, Hd, xdim + 1));
+  return std::max(w, one(Ny, Hd, ydim + 1));
+}
+
 static long long x2y_ws_nocatd(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim, const VidRows& v) {
   long long w = (long long)Ny * (ydim + Hd) + v.a[v.n] + 2LL * Nx * Hd + (long long)Ny * Hd +
                 (long long)Nx * xdim + (long long)Ny * ydim;
@@ -1358,7 +1370,8 @@ static long long x2y_ws_nocatd(int Nx, int xdim, int Ny, int ydim, int Hd, int o
 long long fx_x2y_workspace_floats(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim, int nvid,
                                   const int* x_off, const int* y_off) {
   const VidRows v = vid_rows(Nx, Ny, nvid, x_off, y_off);
-  return x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, v) + (long long)Ny * (ydim + Hd);
+  return x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, v) + (long long)Ny * (ydim + Hd) +
+         x2y_side_ws(Nx, xdim, Ny, ydim, Hd, outdim);
 }
 
 // catd = dropout(cat[Y, feat]) (basic.py:382), mask index r (ydim + Hd) + c
@@ -1466,7 +1479,7 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
                const float* attn, const float* saved,
                const float* dout, long long lddo, const float* dlogit, const float* dattn, float* dX, float* dXpos,
                float* dY, float* dYpos, float* dwk, float* dbk, float* dwv, float* dbv, float* dwq, float* dbq,
-               float* dwy, float* dby, int has_xpos, int has_ypos, float* workspace, void* stream) {
+               float* dwy, float* dby, int has_xpos, int has_ypos, float* workspace, int side_defer, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const VidRows V = vid_rows(Nx, Ny, nvid, x_off, y_off);
   FX_REQUIRE(V.x[V.n] == Nx && V.y[V.n] == Ny, "x2y: offsets must end at Nx / Ny");
@@ -1493,14 +1506,12 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
   // Y_W: dcat = dout . Wy, dWy = dout^T [Y, feat], dby  (dropout: the dropped concatenation and
   // the same mask on dcat)
   FX_TRY(linear_dx(dout, lddo, wy, Ny, cw, outdim, dcat, cw, 0, nullptr, 0, spl, s));
+  const float* catd = nullptr;
   if (drop_p > 0.f) {
-    float* catd = workspace + x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, V);
-    FX_TRY(x2y_drop_cat(Y, ldy, feat, Ny, ydim, Hd, drop_p, seed, catd, s));
-    FX_TRY(linear_dwdb(dout, lddo, catd, cw, Ny, cw, outdim, dwy, dby, 1, spl, s, cw));
+    float* cd = workspace + x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, V);
+    FX_TRY(x2y_drop_cat(Y, ldy, feat, Ny, ydim, Hd, drop_p, seed, cd, s));
     FX_TRY(launch_dropout(dcat, cw, Ny, cw, cw, 0, drop_p, seed, dcat, cw, s));
-  } else {
-    FX_TRY(linear_dwdb(dout, lddo, Y, ldy, Ny, ydim, outdim, dwy, dby, 1, spl, s, cw));
-    FX_TRY(linear_dw(dout, lddo, feat, Hd, Ny, Hd, outdim, dwy + ydim, 1, spl, s, cw));
+    catd = cd;
   }
   // per video: dP = dfeat . xv^T (+ dattn), dxv = attn^T . dfeat  (independent: one grouped launch
   // for up to two videos), softmax backward, then dyq = dlogit . xk, dxk = dlogit^T . yq (grouped)
@@ -1546,10 +1557,29 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
     }
     FX_TRY(launch_gemm_group(g2, n2, s));
   }
-  // projections
-  FX_TRY(linear_dwdb(dxk, Hd, xin, ldxin, Nx, xdim, Hd, dwk, dbk, 1, spl, s));
-  FX_TRY(linear_dwdb(dxv, Hd, X, ldx, Nx, xdim, Hd, dwv, dbv, 1, spl, s));
-  FX_TRY(linear_dwdb(dyq, Hd, yin, ldyin, Ny, ydim, Hd, dwq, dbq, 1, spl, s));
+  // weight gradients (Y_W; projections X_K, X_V, Y_Q): nothing below needs them -> side stream, each
+  // frame-level GEMM split defer_split(rows) ways into its own slab region
+  {
+    hipStream_t sd = side_fork(s, 1);
+    float* sps = workspace + x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, V) + (long long)Ny * cw;
+    WsBound wbs(sps, x2y_side_ws(Nx, xdim, Ny, ydim, Hd, outdim));
+    auto dw = [&](const float* dy, long long lddy, const float* x, long long ldx_, int rows, int K, int N, float* w,
+                  float* b, long long ldw) -> int {
+      fx_gemm_desc d = desc_linear_dwdb(dy, lddy, x, ldx_, rows, K, N, w, b, 1, sps, ldw);
+      if (sd != s) d.split_k = std::max(d.split_k, defer_split(rows));
+      return launch_gemm(d, sd);
+    };
+    if (catd) {
+      FX_TRY(dw(dout, lddo, catd, cw, Ny, cw, outdim, dwy, dby, cw));
+    } else {
+      FX_TRY(dw(dout, lddo, Y, ldy, Ny, ydim, outdim, dwy, dby, cw));
+      FX_TRY(dw(dout, lddo, feat, Hd, Ny, Hd, outdim, dwy + ydim, nullptr, cw));
+    }
+    FX_TRY(dw(dxk, Hd, xin, ldxin, Nx, xdim, Hd, dwk, dbk, -1));
+    FX_TRY(dw(dxv, Hd, X, ldx, Nx, xdim, Hd, dwv, dbv, -1));
+    FX_TRY(dw(dyq, Hd, yin, ldyin, Ny, ydim, Hd, dwq, dbq, -1));
+    if (sd != s && !side_defer) FX_TRY(side_join_into(s));
+  }
   if (dX || dXpos) {
     FX_TRY(linear_dx(dxk, Hd, wk, Nx, xdim, Hd, dXk, xdim, 0, nullptr, 0, spl, s));
     if (dXpos)

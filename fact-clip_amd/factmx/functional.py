@@ -525,12 +525,15 @@ class X2YFn(torch.autograd.Function):
         # the kernel needs every weight-gradient target; absent ones go to scratch
         bufs = [b if b is not None else torch.zeros_like(p) for b, p in zip(bufs, (wk, bk, wv, bv, wq, bq, wy, by))]
         ws = _ws(lib.fx_x2y_workspace_floats(Nx, xdim, Ny, ydim, Hd, outdim, nvid, xo, yo), dev)
+        defer = DEFER_SIDE and side_stream() is not None
         _check(lib.fx_x2y_bwd(nx.ptr(X), nx.ld(X), Nx, xdim, xpc, nx.ptr(Y), nx.ld(Y), Ny, ydim, ypc,
                               nx.ptr(wk), nx.ptr(wv), nx.ptr(wq), nx.ptr(wy), Hd, outdim, nvid, xo, yo,
                               ctx.drop[0], ctx.drop[1], nx.ptr(attn),
                               nx.ptr(saved), nx.ptr(dout), outdim, nx.ptr(dlogit), nx.ptr(dattn), nx.ptr(dX),
                               nx.ptr(dXp), nx.ptr(dY), nx.ptr(dYp), *[nx.ptr(t) for t in bufs], int(hx), int(hy),
-                              nx.ptr(ws), nx.stream()), "fx_x2y_bwd")
+                              nx.ptr(ws), int(defer), nx.stream()), "fx_x2y_bwd")
+        if defer:
+            _defer_to_side(X, Y, saved, dout, ws, *bufs)
         return (dX, dY, dXp, dYp, None) + tuple(t[1] for t in tg) + (None, None)
 
 

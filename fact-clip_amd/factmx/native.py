@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FACTMX_LIB", os.path.join(_HERE, "_lib", "libfactmx.so"))
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -117,7 +117,7 @@ SIGNATURES = {
     "fx_x2y_fwd": (I, [P, L, I, I, P, L, I, P, L, I, I, P, L, I, P, P, P, P, P, P, P, P, I, I, I, P, P, F, U, P, L, P,
                        P, P, P, P]),
     "fx_x2y_bwd": (I, [P, L, I, I, I, P, L, I, I, I, P, P, P, P, I, I, I, P, P, F, U, P, P, P, L, P, P, P, P, P, P,
-                       P, P, P, P, P, P, P, P, I, I, P, P]),
+                       P, P, P, P, P, P, P, P, I, I, P, I, P]),
     "fx_decoder_saved_floats": (L, [ctypes.POINTER(DecoderParams), I, I, I, I, I]),
     "fx_decoder_workspace_floats": (L, [ctypes.POINTER(DecoderParams), I, I, I, I, I]),
     "fx_decoder_fwd": (I, [ctypes.POINTER(DecoderParams), P, L, I, P, L, P, L, I, I, P, L, P, L, P, P, P]),

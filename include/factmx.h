@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FX_ABI_VERSION 13
+#define FX_ABI_VERSION 14
 
 enum {
   FX_OK = 0,
@@ -155,6 +155,8 @@ int fx_linear_bwd(const float* dy, long long lddy, const float* x, long long ldx
  *   (nullable) and every weight/bias gradient (accumulated, all required).
  * drop_p > 0 (training): Y_W(dropout(cat[Y, attn . xv])) (basic.py:382), fx_dropout mask
  * index r (ydim + Hd) + c over the concatenated row, regenerated by the backward.
+ * bwd: the four weight-gradient GEMMs run on the library's side stream after the attention
+ * gradients exist; side_defer = 1 leaves them running there (fx_side_join), 0 joins before return.
  * ---------------------------------------------------------------------- */
 long long fx_x2y_saved_floats(int Nx, int xdim, int Ny, int ydim, int Hd);
 long long fx_x2y_workspace_floats(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim, int nvid,
@@ -174,7 +176,7 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
                long long lddo, const float* dlogit, const float* dattn, float* dX, float* dXpos,
                float* dY, float* dYpos, float* dwk, float* dbk, float* dwv, float* dbv, float* dwq,
                float* dbq, float* dwy, float* dby, int has_xpos, int has_ypos, float* workspace,
-               void* stream);
+               int side_defer, void* stream);
 
 /* ------------------------------------------------------------------------
  * Action-token decoder, whole stack in one call (eval-mode dropout, post-norm, ReLU FFN):
