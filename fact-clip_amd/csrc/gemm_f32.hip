@@ -70,6 +70,7 @@ struct GemmDev {
   unsigned long long drop_seed;
   long long c_last_bs;  // c_last of batch b at c_last + b * c_last_bs
   int b_dil_growth;     // > 1: B's conv dilation of batch b is conv_dil * growth^b
+  int xcd_planes;       // wide8: whole z-planes (batch x split-K slice) per XCD, see block_tile
 };
 
 // Diagnostic builds (-DFX_STAMPS) record s_memtime / s_memrealtime at fixed points of
@@ -476,23 +477,41 @@ __device__ __forceinline__ void kloop(const Loader<AK, FAST>& la, const Loader<B
   if (i < n) iter(i, ra0, rb0, ma0, mb0, ra1, rb1, ma1, mb1);
 }
 
+// Output tile (tx, ty) and z-plane (batch x split-K slice) of this block.  Workgroups go to the 8 XCDs
+// round robin by linear dispatch id.  Default: within each z-plane, runs of consecutive tiles (one
+// row band's column tiles) share an XCD and its L2.  xcd_planes (launches whose plane count is a
+// multiple of 8, e.g. the batched / split weight-gradient GEMMs, K = 8192 rows): plane p runs whole
+// on XCD p % 8, so every tile reading the plane's A rows and B rows hits one L2 instead of all eight
+// XCDs fetching them from MALL / HBM.
+__device__ __forceinline__ void block_tile(const GemmDev& g, int& tx, int& ty, int& z) {
+  const int nt = g.tiles_x * g.tiles_y;
+  if (g.xcd_planes) {
+    const int L = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    const int x8 = L & 7, sl = L >> 3;
+    const int pl = sl / nt, t = sl - pl * nt;
+    z = pl * 8 + x8;
+    ty = t / g.tiles_x;
+    tx = t - ty * g.tiles_x;
+    return;
+  }
+  const int id = blockIdx.y * g.tiles_x + blockIdx.x;
+  const int q = nt / 8, rr = nt % 8, x8 = id % 8, i8 = id / 8;
+  const int nid = (x8 < rr ? x8 * (q + 1) : rr * (q + 1) + (x8 - rr) * q) + i8;
+  ty = nid / g.tiles_x;
+  tx = nid - ty * g.tiles_x;
+  z = blockIdx.z;
+}
+
 template <int AK, int BKIND, bool FAST>
 __global__ __launch_bounds__(NTHREADS) void gemm_f32_kernel(GemmDev g) {
   __shared__ float lds[NSLOT * 2 * IMG];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, li = lane & 31, lh = lane >> 5;
   // XCD-aware remap of (x, y) tiles: consecutive remapped ids share an XCD (L2)
-  int tx, ty;
-  {
-    const int nt = g.tiles_x * g.tiles_y;
-    const int id = blockIdx.y * g.tiles_x + blockIdx.x;
-    const int q = nt / 8, rr = nt % 8, x8 = id % 8, i8 = id / 8;
-    const int nid = (x8 < rr ? x8 * (q + 1) : rr * (q + 1) + (x8 - rr) * q) + i8;
-    ty = nid / g.tiles_x;
-    tx = nid - ty * g.tiles_x;
-  }
+  int tx, ty, z;
+  block_tile(g, tx, ty, z);
   const int n0 = tx * BN, m0 = ty * BM;
-  const int z = blockIdx.z, bidx = z / g.split, sk = z - bidx * g.split;
+  const int bidx = z / g.split, sk = z - bidx * g.split;
   const int nkt = (g.K + BK - 1) / BK;
   const int kt0 = sk * g.kt_per_split;
   const int kt1 = min(nkt, kt0 + g.kt_per_split);
@@ -705,17 +724,10 @@ __global__ __launch_bounds__(NTHREADS) void gemm_f32_wide_kernel(GemmDev g) {
   __shared__ float lds[NSLOT * 3 * IMG];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, li = lane & 31, lh = lane >> 5;
-  int tx, ty;
-  {
-    const int nt = g.tiles_x * g.tiles_y;
-    const int id = blockIdx.y * g.tiles_x + blockIdx.x;
-    const int q = nt / 8, rr = nt % 8, x8 = id % 8, i8 = id / 8;
-    const int nid = (x8 < rr ? x8 * (q + 1) : rr * (q + 1) + (x8 - rr) * q) + i8;
-    ty = nid / g.tiles_x;
-    tx = nid - ty * g.tiles_x;
-  }
+  int tx, ty, z;
+  block_tile(g, tx, ty, z);
   const int n0 = tx * BN, m0 = ty * WBM;
-  const int z = blockIdx.z, bidx = z / g.split, sk = z - bidx * g.split;
+  const int bidx = z / g.split, sk = z - bidx * g.split;
   const int nkt = (g.K + BK - 1) / BK;
   const int kt0 = sk * g.kt_per_split;
   const int kt1 = min(nkt, kt0 + g.kt_per_split);
@@ -851,17 +863,10 @@ __global__ __launch_bounds__(W8T) void gemm_f32_wide8_kernel(GemmDev g) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, li = lane & 31, lh = lane >> 5;
   const int ai = wm >> 1, wr = (wm & 1) * 32;   // A image (rows m0 / m0 + 64) and row offset in it
-  int tx, ty;
-  {
-    const int nt = g.tiles_x * g.tiles_y;
-    const int id = blockIdx.y * g.tiles_x + blockIdx.x;
-    const int q = nt / 8, rr = nt % 8, x8 = id % 8, i8 = id / 8;
-    const int nid = (x8 < rr ? x8 * (q + 1) : rr * (q + 1) + (x8 - rr) * q) + i8;
-    ty = nid / g.tiles_x;
-    tx = nid - ty * g.tiles_x;
-  }
+  int tx, ty, z;
+  block_tile(g, tx, ty, z);
   const int n0 = tx * BN, m0 = ty * WBM;
-  const int z = blockIdx.z, bidx = z / g.split, sk = z - bidx * g.split;
+  const int bidx = z / g.split, sk = z - bidx * g.split;
   const int nkt = (g.K + BK - 1) / BK;
   const int kt0 = sk * g.kt_per_split;
   const int kt1 = min(nkt, kt0 + g.kt_per_split);
@@ -984,17 +989,10 @@ __global__ __launch_bounds__(W8T) void gemm_bf16_wide8_kernel(GemmDev g) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, li = lane & 31, lh = lane >> 5;
   const int ai = wm >> 1, wr = (wm & 1) * 32;
-  int tx, ty;
-  {
-    const int nt = g.tiles_x * g.tiles_y;
-    const int id = blockIdx.y * g.tiles_x + blockIdx.x;
-    const int q = nt / 8, rr = nt % 8, x8 = id % 8, i8 = id / 8;
-    const int nid = (x8 < rr ? x8 * (q + 1) : rr * (q + 1) + (x8 - rr) * q) + i8;
-    ty = nid / g.tiles_x;
-    tx = nid - ty * g.tiles_x;
-  }
+  int tx, ty, z;
+  block_tile(g, tx, ty, z);
   const int n0 = tx * BN, m0 = ty * WBM;
-  const int z = blockIdx.z, bidx = z / g.split, sk = z - bidx * g.split;
+  const int bidx = z / g.split, sk = z - bidx * g.split;
   const int nkt = (g.K + BK - 1) / BK;
   const int kt0 = sk * g.kt_per_split;
   const int kt1 = min(nkt, kt0 + g.kt_per_split);
@@ -1693,6 +1691,13 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
     unsigned* pool = tile_counters(s);
     g.tile_cnt = pool ? pool + tile_cnt_base : nullptr;
   }
+  // FX_GEMM_XCDPLANES=0: the per-plane tile mapping for every launch (A/B)
+  static const bool planes_on = [] {
+    const char* p = std::getenv("FX_GEMM_XCDPLANES");
+    return !(p && p[0] == '0');
+  }();
+  const long long nz = (long long)d.batch * g.split;
+  g.xcd_planes = planes_on && wide && wide8() && nz >= 8 && nz % 8 == 0;
   P.grid = grid;
   P.block = block;
   P.direct = direct;

@@ -58,6 +58,11 @@ def main():
     bo.batch_stride = K * 256
     us = timeit(lambda: fxf.gemm(M, N, K, op(a_cm, True, K * M), bo, c, N, batch=B, c_bs=M * N, c_tap_cin=256))
     print(f"A cols, B cols_conv: {us:8.1f} us  {fl / us / 1e6:6.1f} TF/s", flush=True)
+    # split 8 (the deferred weight-gradient launches): 10 x 8 = 80 z-planes (plane-per-XCD mapping)
+    for name, (a, b) in (("A cols, B cols", cases["A cols, B cols"]), ("A cols, B cols_conv", (op(a_cm, True, K * M), bo))):
+        tap = 256 if b is bo else 0
+        us = timeit(lambda: fxf.gemm(M, N, K, a, b, c, N, batch=B, c_bs=M * N, c_tap_cin=tap, split=8))
+        print(f"{name} split 8: {us:8.1f} us  {fl / us / 1e6:6.1f} TF/s", flush=True)
 
 
 if __name__ == "__main__":
