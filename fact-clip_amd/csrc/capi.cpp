@@ -893,15 +893,20 @@ int fx_mstcn2_fwd(const fx_mstcn2_params* p, const float* x, long long ldx, int 
     float* ri = saved + L.r + i * L.rowsF;
     // cat = [conv_d1(f) | conv_d2(f)]: the two dilated convs store into the halves of one buffer
     // (no torch.cat)   (basic.py:276)
-    for (int h = 0; h < 2; ++h) {
-      const int dil = h == 0 ? mstcn2_dil(p, NL - 1 - i) : mstcn2_dil(p, i);
-      fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(fi, F, F, dil, 1, T, false),
-                                 op_rows(ws + (h == 0 ? L.wf1 : L.wf2) + (long long)i * 3 * F * F, 3 * F), cat + h * F,
-                                 2 * F);
-      d.bias = h == 0 ? p->b_d1[i] : p->b_d2[i];
+    // (one batch-2 launch: batch h takes conv h's dilation, packed weights, bias and output half --
+    // at Breakfast's 2048 rows the pair fills the chip with 128x64 tiles where one conv could not)
+    {
+      fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(fi, F, F, mstcn2_dil(p, NL - 1 - i), 1, T, false),
+                                 op_rows(ws + L.wf1 + (long long)i * 3 * F * F, 3 * F), cat, 2 * F);
+      d.batch = 2;
+      d.a_dil_b1 = mstcn2_dil(p, i);
+      d.b.batch_stride = L.wf2 - L.wf1;
+      d.c_batch_stride = F;
+      d.bias = p->b_d1[i];
+      d.bias_batch_stride = p->b_d2[i] - p->b_d1[i];
       prof_begin(0, s);
       FX_TRY(launch_gemm(d, s));
-      prof_end(0, s, 2.0 * rows * F * 3.0 * F, 4.0 * (2.0 * rows * F + 3.0 * F * F));
+      prof_end(0, s, 2.0 * 2.0 * rows * F * 3.0 * F, 4.0 * (3.0 * rows * F + 6.0 * F * F));
     }
     // r = dropout(relu(W_fu . cat + b_fu)) (no dropout on the last layer), f' = f + r  (basic.py:276-280)
     fx_gemm_desc e = gemm_desc(rows, F, 2 * F, op_rows(cat, 2 * F), op_rows(p->w_fu[i], 2 * F), ri, F);

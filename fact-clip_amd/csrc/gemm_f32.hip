@@ -71,6 +71,8 @@ struct GemmDev {
   long long c_last_bs;  // c_last of batch b at c_last + b * c_last_bs
   int b_dil_growth;     // > 1: B's conv dilation of batch b is conv_dil * growth^b
   int xcd_planes;       // wide8: whole z-planes (batch x split-K slice) per XCD, see block_tile
+  int a_dil_b1;         // > 0: A's conv dilation of batch 1 (two dilated convs of one input in one launch)
+  long long bias_bs;    // bias of batch b at bias + b * bias_bs
 };
 
 // Diagnostic builds (-DFX_STAMPS) record s_memtime / s_memrealtime at fixed points of
@@ -93,6 +95,13 @@ struct GemmDev {
 
 __device__ __forceinline__ int conv_shift(const fx_operand& o, int tap) {
   return (tap - (o.conv_taps - 1) / 2) * o.conv_dil * o.conv_dir;
+}
+
+// A operand of batch bidx: batch 1 may take its own conv dilation (MS-TCN++'s two dilated convs)
+__device__ __forceinline__ fx_operand batch_op_a(const fx_operand& a, int dil_b1, int bidx) {
+  fx_operand o = a;
+  if (dil_b1 > 0 && bidx == 1) o.conv_dil = dil_b1;
+  return o;
 }
 
 // B operand of batch bidx: a per-batch conv dilation (dilation stacks: layer b's conv_dil * growth^b)
@@ -344,7 +353,7 @@ __device__ __forceinline__ void epilogue_store(const GemmDev& g, int b, int m, i
     *cp = v;
     return;
   }
-  if (g.bias) v += g.bias[n];
+  if (g.bias) v += g.bias[(long long)b * g.bias_bs + n];
   if (g.relu == 2) v = fmaxf(v, 0.f);
   if (g.drop_thr) {
     const unsigned long long idx = ((unsigned long long)b * g.M + m) * g.N + n;
@@ -518,7 +527,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_f32_kernel(GemmDev g) {
 
   Loader<AK, FAST> la;
   Loader<BKIND, FAST> lb;
-  la.init(g.a, g.a.ptr + (long long)bidx * g.a.batch_stride, m0, g.M, g.K, tid);
+  la.init(batch_op_a(g.a, g.a_dil_b1, bidx), g.a.ptr + (long long)bidx * g.a.batch_stride, m0, g.M, g.K, tid);
   lb.init(batch_op_b(g.b, g.b_dil_growth, bidx), g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid);
 
   f32x16 acc0, acc1;
@@ -552,7 +561,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_f32_kernel(GemmDev g) {
   if (!g.c_last && !g.c_tap_cin && !g.gate && g.beta == 0.f && !g.drop_thr) {
     // common forward epilogue: every read (bias, residual) is issued before the first store,
     // so the 16 loads overlap instead of queueing behind stores they might alias
-    const float bv = g.bias ? g.bias[col] : 0.f;
+    const float bv = g.bias ? g.bias[(long long)bidx * g.bias_bs + col] : 0.f;
     float res[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -692,7 +701,7 @@ __device__ __forceinline__ void wide_kloop(const Loader<AK, true>& la0, const Lo
 __device__ __forceinline__ void tile_epilogue(const GemmDev& g, int bidx, int rbase, int col, const f32x16& acc) {
   if (col >= g.N) return;
   if (!g.c_last && !g.c_tap_cin && !g.gate && g.beta == 0.f && !g.drop_thr) {
-    const float bv = g.bias ? g.bias[col] : 0.f;
+    const float bv = g.bias ? g.bias[(long long)bidx * g.bias_bs + col] : 0.f;
     float res[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -734,8 +743,8 @@ __global__ __launch_bounds__(NTHREADS) void gemm_f32_wide_kernel(GemmDev g) {
   Loader<AK, true> la0, la1;
   Loader<BKIND, true> lb;
   const float* pa = g.a.ptr + (long long)bidx * g.a.batch_stride;
-  la0.init(g.a, pa, m0, g.M, g.K, tid);
-  la1.init(g.a, pa, m0 + BM, g.M, g.K, tid);
+  la0.init(batch_op_a(g.a, g.a_dil_b1, bidx), pa, m0, g.M, g.K, tid);
+  la1.init(batch_op_a(g.a, g.a_dil_b1, bidx), pa, m0 + BM, g.M, g.K, tid);
   lb.init(batch_op_b(g.b, g.b_dil_growth, bidx), g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid);
   f32x16 acc0, acc1;
 #pragma unroll
@@ -873,8 +882,8 @@ __global__ __launch_bounds__(W8T) void gemm_f32_wide8_kernel(GemmDev g) {
   Loader<AK, true, 2> la0, la1;
   Loader<BKIND, true, 2> lb;
   const float* pa = g.a.ptr + (long long)bidx * g.a.batch_stride;
-  la0.init(g.a, pa, m0, g.M, g.K, tid);
-  la1.init(g.a, pa, m0 + BM, g.M, g.K, tid);
+  la0.init(batch_op_a(g.a, g.a_dil_b1, bidx), pa, m0, g.M, g.K, tid);
+  la1.init(batch_op_a(g.a, g.a_dil_b1, bidx), pa, m0 + BM, g.M, g.K, tid);
   lb.init(batch_op_b(g.b, g.b_dil_growth, bidx), g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid);
   f32x16 acc0, acc1;
 #pragma unroll
@@ -999,8 +1008,8 @@ __global__ __launch_bounds__(W8T) void gemm_bf16_wide8_kernel(GemmDev g) {
   Loader<AK, true, 2> la0, la1;
   Loader<BKd, true, 2> lb;
   const float* pa = g.a.ptr + (long long)bidx * g.a.batch_stride;
-  la0.init(g.a, pa, m0, g.M, g.K, tid);
-  la1.init(g.a, pa, m0 + BM, g.M, g.K, tid);
+  la0.init(batch_op_a(g.a, g.a_dil_b1, bidx), pa, m0, g.M, g.K, tid);
+  la1.init(batch_op_a(g.a, g.a_dil_b1, bidx), pa, m0 + BM, g.M, g.K, tid);
   lb.init(batch_op_b(g.b, g.b_dil_growth, bidx), g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid);
   f32x16 acc0, acc1;
 #pragma unroll
@@ -1623,6 +1632,9 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
   g.c_last = d.c_last_col;
   g.c_last_bs = d.c_last_batch_stride ? d.c_last_batch_stride : d.M;
   g.b_dil_growth = d.b_dil_growth;
+  g.a_dil_b1 = d.a_dil_b1;
+  g.bias_bs = d.bias_batch_stride;
+  FX_REQUIRE(d.a_dil_b1 <= 0 || (d.a.conv_taps && !d.a.trans), "gemm: a_dil_b1 needs a row-major conv A");
   FX_REQUIRE(d.b_dil_growth <= 1 || (d.b.conv_taps && d.b.trans), "gemm: b_dil_growth needs a column-major conv B");
   g.stamps = d.dbg_stamps;
   FX_REQUIRE(d.drop_p >= 0.f && d.drop_p < 1.f, "gemm: dropout p must be in [0, 1)");
@@ -1643,7 +1655,7 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
   const int ak = kind_of(d.a, g.a_vec), bk = kind_of(d.b, g.b_vec);
   P.ak = ak;
   P.bk = bk;
-  const bool direct = d.b_dil_growth <= 1 && use_direct(d, ak, bk);   // (the direct kernel: one dilation)
+  const bool direct = d.b_dil_growth <= 1 && d.a_dil_b1 <= 0 && use_direct(d, ak, bk);   // (the direct kernel: one dilation)
   bool wide = false;
   const int cap = (d.split_k > 1 && d.workspace) ? d.split_k : 1;   // workspace holds `cap` slabs
   FX_REQUIRE(!(d.split_k > 1 && !d.workspace), "gemm: split-K needs a workspace");

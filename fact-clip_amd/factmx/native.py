@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FACTMX_LIB", os.path.join(_HERE, "_lib", "libfactmx.so"))
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -37,7 +37,8 @@ class GemmDesc(ctypes.Structure):
                 ("c_batch_stride", L), ("alpha", F), ("beta", F), ("bias", P), ("resid", P), ("ld_resid", L),
                 ("resid_batch_stride", L), ("gate", P), ("ld_gate", L), ("relu", I), ("c_tap_cin", I),
                 ("split_k", I), ("workspace", P), ("c_last_col", P), ("dbg_stamps", P), ("drop_p", F),
-                ("drop_seed", U), ("c_last_batch_stride", L), ("b_dil_growth", I)]
+                ("drop_seed", U), ("c_last_batch_stride", L), ("b_dil_growth", I),
+                ("a_dil_b1", I), ("bias_batch_stride", L)]
 
 
 class MstcnParams(ctypes.Structure):

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FX_ABI_VERSION 14
+#define FX_ABI_VERSION 15
 
 enum {
   FX_OK = 0,
@@ -110,6 +110,9 @@ typedef struct fx_gemm_desc {
   long long c_last_batch_stride; /* c_last_col of batch b at c_last_col + b*stride (0: M) */
   int b_dil_growth;           /* > 1: B's conv_dil of batch b is conv_dil * growth^b (one launch for
                                  the dilated-conv weight gradients of every layer of a stack) */
+  int a_dil_b1;               /* > 0: A's conv_dil for batch 1 (two dilated convs of one input, e.g.
+                                 MS-TCN++'s pair, as one batch-2 launch) */
+  long long bias_batch_stride; /* bias of batch b at bias + b*stride */
 } fx_gemm_desc;
 
 int fx_gemm(const fx_gemm_desc* desc, void* stream);
