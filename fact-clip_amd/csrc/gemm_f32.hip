@@ -1483,8 +1483,9 @@ bool use_direct(const fx_gemm_desc& d, int ak, int bk) {
   // 32-row case pays off there (64 x 256 x 1024 concat: 54 us direct vs 29 us tiled)
   const int lim = (ak == ROWS_GEN || ak == ROWS_CAT) ? 32 : 64;
   // a shallow K that is not a whole number of 64-deep stages would take the generic tiled kernel
-  // (InfoNCE dF: 4096 x 512 x 70, 80 us there); one pass of the direct kernel per tile is ~10x faster
-  return d.M <= lim || d.N <= lim || d.K <= 64 || (d.K <= 128 && d.K % 64 != 0);
+  // (InfoNCE dF: 4096 x 512 x 70, 80 us there; Breakfast's token dW over 4 x 60 = 240 token rows,
+  // 512 x 513 x 240: 61 us there); one pass of the direct kernel per tile is ~10x faster
+  return d.M <= lim || d.N <= lim || d.K <= 64 || (d.K <= 512 && d.K % 64 != 0);
 }
 
 // 128x64 tiles where the launch still has ~3/4 of a block per CU: FAST operands only.
