@@ -270,7 +270,7 @@ SideStream* side_stream() {
 struct MstcnLayout {
   long long rowsF;
   // saved
-  long long h, z, xh, rs, wbs, total_saved;
+  long long h, z, xh, rs, wbs, wpts, total_saved;
   // workspace
   long long wf, wb, wpt, buf0, buf1, buf2, buf3, buf4, buf5, split, split2, colsum, dzall, dhall, csb, bsl, total_ws;
 };
@@ -297,7 +297,8 @@ MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
   L.rs = L.xh + (p->layernorm ? NL * L.rowsF : 0);
   L.wbs = L.rs + (p->layernorm ? (long long)NL * rows : 0);   // dX-packed conv weights (fwd packs, bwd reads)
   const long long wsz = 3 * F * F;
-  L.total_saved = L.wbs + NL * wsz;
+  L.wpts = L.wbs + NL * wsz;                 // transposed 1x1 weights (fwd packs, bwd dZ GEMM reads)
+  L.total_saved = L.wpts + NL * F * F;
   L.wf = 0;
   L.wb = L.wf + NL * wsz;
   L.wpt = L.wb + NL * wsz;                   // transposed 1x1 weights (fused backward chain)
@@ -332,8 +333,8 @@ MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
   return L;
 }
 
-int pack_conv_weights(const fx_mstcn_params* p, float* ws, float* wbdst, const MstcnLayout& L, hipStream_t s,
-                      bool want_wpt) {
+int pack_conv_weights(const fx_mstcn_params* p, float* ws, float* wbdst, float* wptdst, const MstcnLayout& L,
+                      hipStream_t s) {
   PackArgs a{};
   a.F = p->F;
   const long long wsz = 3LL * p->F * p->F;
@@ -342,7 +343,7 @@ int pack_conv_weights(const fx_mstcn_params* p, float* ws, float* wbdst, const M
     a.wf[l] = ws + L.wf + l * wsz;
     a.wb[l] = wbdst + l * wsz;
     a.wpw[l] = p->w_pw[l];
-    a.wpt[l] = want_wpt ? ws + L.wpt + (long long)l * p->F * p->F : nullptr;
+    a.wpt[l] = wptdst ? wptdst + (long long)l * p->F * p->F : nullptr;
   }
   hipLaunchKernelGGL(pack_conv_kernel, dim3(std::min<int>(cdiv(wsz, 256), 512), p->num_layers), dim3(256), 0, s, a);
   FX_CHECK_HIP(hipGetLastError());
@@ -480,7 +481,7 @@ int fx_mstcn_fwd(const fx_mstcn_params* p, const float* x, long long ldx, int T,
   const int rows = T * nvid;
   const int F = p->F;
   const MstcnLayout L = mstcn_layout(p, rows);
-  FX_TRY(pack_conv_weights(p, workspace, saved + L.wbs, L, s, false));
+  FX_TRY(pack_conv_weights(p, workspace, saved + L.wbs, saved + L.wpts, L, s));
   float* h0 = saved + L.h;
   if (p->in_map) {
     FX_TRY(linear_fwd(x, ldx, rows, p->cin, p->w_in, p->b_in, h0, F, F, 0, s));
@@ -541,10 +542,20 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   const bool fchain = !p->layernorm && !drop && NL > 0 && frl_supported(F, ws + L.buf0, F, F);
   // the dX-packed conv weights come from the forward (saved); the fused chain also needs the
   // transposed 1x1 weights (repacked here, into the workspace)
-  if (fchain) FX_TRY(pack_conv_weights(p, ws, ws + L.wb, L, s, true));
+  if (fchain) FX_TRY(pack_conv_weights(p, ws, ws + L.wb, ws + L.wpt, L, s));
   const float* wbp = fchain ? ws + L.wb : saved + L.wbs;
   float* spl = ws + L.split;     // split-K partials of the weight-gradient GEMMs (side stream)
   float* spm = ws + L.split2;    // ... of the main stream's GEMMs / LN backward
+  // dZ_i = (g . W_pw,i) * (z_i > 0) with W_pw,i^T packed row-major by the forward: the B operand
+  // loads as k-contiguous rows (b128 fragment reads) instead of the column-major weight
+  auto pw_dx = [&](const float* g, int i, float* dZ, const float* zi) -> int {
+    fx_gemm_desc d = gemm_desc(rows, F, F, op_rows(g, F), op_rows(saved + L.wpts + (long long)i * F * F, F), dZ, F);
+    d.gate = zi;
+    d.ld_gate = F;
+    d.split_k = pick_split(rows, F, F);
+    d.workspace = spm;
+    return launch_gemm(d, s);
+  };
   WsBound wb(spl, L.colsum - L.split);
   // Weight-gradient GEMMs (dW_out, per layer dW_pw and the dilated-conv dW, dW_in) depend on the
   // input-gradient chain but nothing in the chain depends on them: they run on a side stream,
@@ -653,7 +664,7 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
       const float* zi = saved + L.z + i * L.rowsF;
       const float* gU = dHall + i * L.rowsF;
       float* dZ = dZall + i * L.rowsF;
-      FX_TRY(linear_dx(gU, F, p->w_pw[i], rows, F, F, dZ, F, 0, zi, F, spm, s));
+      FX_TRY(pw_dx(gU, i, dZ, zi));
       float* dHn = i > 0 ? dHall + (i - 1) * L.rowsF : Hb[0];
       fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dZ, F, F, layer_dilation(p, i), -1, T, false),
                                  op_rows(wbp + (long long)i * 3 * F * F, 3 * F), dHn, F);
@@ -724,7 +735,7 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
     FX_TRY(linear_dwdb(gB, F, zi, F, rows, F, F, g->w_pw[i], g->b_pw[i], 1, spl, sd));
     float* dZ = ss ? Zb[step & 1] : Zb[0];
     FX_TRY(wait_side(i + 2));   // dZ buffer last read by layer i + 2's conv dW
-    FX_TRY(linear_dx(gB, F, p->w_pw[i], rows, F, F, dZ, F, 0, zi, F, spm, s));
+    FX_TRY(pw_dx(gB, i, dZ, zi));
     // conv: dW (tap-major columns stored straight into (F,F,3)) + db (ones column) (side),
     // dH_i = dU + conv^T(dZ) (main)
     FX_TRY(fork(2));
