@@ -16,7 +16,10 @@ namespace {
 
 constexpr int SM = 64;        // max Lq, Lk, head_dim
 constexpr int SP = SM + 1;    // padded LDS row stride (no bank conflicts on column walks)
-constexpr int NT = 256;
+// 1024 threads: each output element is one thread's serial FMA chain (fixed order, so the result does
+// not depend on NT); at Breakfast's 60 tokens x head dim 64 a 256-thread block left each thread ~15
+// elements of 64-deep chains (bwd 72 us per launch over only heads x videos = 32 workgroups)
+constexpr int NT = 1024;
 
 __device__ __forceinline__ float wsum(float v) {
 #pragma unroll
