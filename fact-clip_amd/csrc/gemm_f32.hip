@@ -73,6 +73,7 @@ struct GemmDev {
   int xcd_planes;       // wide8: whole z-planes (batch x split-K slice) per XCD, see block_tile
   int a_dil_b1;         // > 0: A's conv dilation of batch 1 (two dilated convs of one input in one launch)
   long long bias_bs;    // bias of batch b at bias + b * bias_bs
+  int nt_store;         // FX_GEMM_NTSTORE=1 (A/B): the fast epilogue stores non-temporally
 };
 
 // Diagnostic builds (-DFX_STAMPS) record s_memtime / s_memrealtime at fixed points of
@@ -717,7 +718,12 @@ __device__ __forceinline__ void tile_epilogue(const GemmDev& g, int bidx, int rb
       if (g.relu == 2) v = fmaxf(v, 0.f);
       v += res[r];
       if (g.relu == 1) v = fmaxf(v, 0.f);
-      if (row < g.M) cb[(long long)row * g.ldc] = v;
+      if (row < g.M) {
+        if (g.nt_store)
+          __builtin_nontemporal_store(v, cb + (long long)row * g.ldc);
+        else
+          cb[(long long)row * g.ldc] = v;
+      }
     }
   } else {   // (a preloaded-C variant here costs the 128x64 kernel 416 B of scratch)
 #pragma unroll
@@ -1711,6 +1717,11 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
   }();
   const long long nz = (long long)d.batch * g.split;
   g.xcd_planes = planes_on && wide && wide8() && nz >= 8 && nz % 8 == 0;
+  static const bool nt_on = [] {
+    const char* p = std::getenv("FX_GEMM_NTSTORE");
+    return p && p[0] == '1';
+  }();
+  g.nt_store = nt_on ? 1 : 0;
   P.grid = grid;
   P.block = block;
   P.direct = direct;
