@@ -118,7 +118,7 @@ struct DecLayout {
   // workspace (fwd)
   long long wkv, bkv, wsp, total_ws_fwd;
   // workspace (bwd)
-  long long dkv, dwkv, dbkv, dT, dS, dU, dF, dQKV, dO, dq, G, P, lnws, core, split, total_ws_bwd;
+  long long dkv, dwkv, dbkv, dT, dS, dU, dF, dQKV, dO, dq, G, P, lnws, core, split, gdu, gdf, gdq, gdqkv, total_ws_bwd;
 };
 
 long long dec_split_ws(const fx_decoder_params* p, int R, int T) {
@@ -207,6 +207,12 @@ DecLayout dec_layout(const fx_decoder_params* p, int R, int T, int has_qpos, int
   L.lnws = o; o += layernorm_bwd_ws_floats(R, (int)A);
   L.core = o; o += p->cross ? tattn_ws_floats(nvid, (int)Qv, (int)Tv, (int)(A / h), (int)h) : 0;
   L.split = o; o += sp;
+  // every layer's output gradients of its token linears, kept for the weight-gradient GEMMs that run
+  // after the chain (side stream): dU of the three LayerNorms, dF, dq, dQKV
+  L.gdu = o; o += 3LL * p->num_layers * RA;
+  L.gdf = o; o += (long long)p->num_layers * R * FF;
+  L.gdq = o; o += (long long)p->num_layers * RA;
+  L.gdqkv = o; o += 3LL * p->num_layers * RA;
   L.total_ws_bwd = o;
   (void)FF;
   return L;
@@ -368,11 +374,7 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
   float* lnws = ws + L.lnws;
   float* dT = ws + L.dT;     // gradient w.r.t. the current layer output
   float* dS = ws + L.dS;
-  float* dU = ws + L.dU;
-  float* dF = ws + L.dF;
-  float* dQKV = ws + L.dQKV;
   float* dO = ws + L.dO;
-  float* dq = ws + L.dq;
   float* G = ws + L.G;       // sum of the query-position gradients over layers
   float* P = ws + L.P;
   float* dkv = ws + L.dkv;
@@ -387,59 +389,53 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
   if (p->final_norm)
     FX_TRY(launch_layernorm_bwd(dS, A, nullptr, 0, saved + L.fxh, A, p->fn_w, saved + L.frs, R, A, 0, dT, A, g->fn_w,
                                 g->fn_b, lnws, s));
+  // Weight gradients of the token linears: the chain below writes each layer's dU (three LayerNorm
+  // outputs), dF, dq and dQKV into per-layer slots and computes only the input gradients; the dW/db
+  // GEMMs of every layer follow the chain on the side stream, batched over the layers where the
+  // gradient buffers are uniformly strided (~35 one-wave launches per step left the main stream).
+  auto slot_u = [&](int k, int l) { return ws + L.gdu + ((long long)k * NL + l) * RA; };   // k: 0 ff, 1 ca, 2 sa
   for (int l = NL - 1; l >= 0; --l) {
     const float* b = saved + L.layers + l * L.per_layer;
-    const float* x = l == 0 ? tgt : saved + L.layers + (l - 1) * L.per_layer + L.t3;
-    const long long ldx = l == 0 ? ldt : A;
-    const float* xq = qpos ? b + L.xq : x;
-    const long long ldxq = qpos ? A : ldx;
-    const float* t2 = p->cross ? b + L.t2 : b + L.t1;
+    float* dU = slot_u(0, l);
+    float* dF = ws + L.gdf + (long long)l * R * FF;
+    float* dq = ws + L.gdq + (long long)l * RA;
+    float* dQKV = ws + L.gdqkv + (long long)l * 3 * RA;
     // --- FFN + its LayerNorm:  dU = LN_bwd(dT) ; dF = (dU W2) * (f1 > 0) ; dT2 = dU + dF W1
     FX_TRY(launch_layernorm_bwd(dT, A, nullptr, 0, b + L.xh3, A, p->ln_ff_w[l], b + L.rs3, R, A, 0, dU, A,
                                 g->ln_ff_w[l], g->ln_ff_b[l], lnws, s));
-    FX_TRY(linear_bwd_pair(desc_linear_dwdb(dU, A, b + L.f1, FF, R, FF, A, g->ff2_w[l], g->ff2_b[l], 1, spl),
-                           desc_linear_dx(dU, A, p->ff2_w[l], R, FF, A, dF, FF, 0, b + L.f1, FF, spl), s));
-    FX_TRY(linear_bwd_pair(desc_linear_dwdb(dF, FF, t2, A, R, A, FF, g->ff1_w[l], g->ff1_b[l], 1, spl),
-                           dx_res_desc(dF, FF, p->ff1_w[l], A, R, A, FF, dU, A, dT, A, spl), s));   // dT <- dT2
+    FX_TRY(launch_gemm(desc_linear_dx(dU, A, p->ff2_w[l], R, FF, A, dF, FF, 0, b + L.f1, FF, spl), s));
+    FX_TRY(launch_gemm(dx_res_desc(dF, FF, p->ff1_w[l], A, R, A, FF, dU, A, dT, A, spl), s));   // dT <- dT2
     if (p->cross) {
       // --- cross-attention + LN2
+      dU = slot_u(1, l);
       FX_TRY(launch_layernorm_bwd(dT, A, nullptr, 0, b + L.xh2, A, p->ln_ca_w[l], b + L.rs2, R, A, 0, dU, A,
                                   g->ln_ca_w[l], g->ln_ca_b[l], lnws, s));
-      FX_TRY(linear_bwd_pair(desc_linear_dwdb(dU, A, b + L.oca, A, R, A, A, g->ca_out_w[l], g->ca_out_b[l], 1, spl),
-                             desc_linear_dx(dU, A, p->ca_out_w[l], R, A, A, dO, A, 0, nullptr, 0, spl), s));
+      FX_TRY(launch_gemm(desc_linear_dx(dU, A, p->ca_out_w[l], R, A, A, dO, A, 0, nullptr, 0, spl), s));
       const float* kv = saved + L.kv;
       FX_TRY(launch_tattn_bwd(b + L.qc, A, kv + (long long)l * A, AL2, kv + (long long)(NL + l) * A, AL2, b + L.oca, A,
                               dO, A, b + L.pca, nvid, Qv, Tv, hd, h, scale, dq, A, dkv + (long long)l * A, AL2,
                               dkv + (long long)(NL + l) * A, AL2, ws + L.core, s));
-      const float* tq = qpos ? b + L.t1q : b + L.t1;
-      const fx_gemm_desc dwq = desc_linear_dwdb(dq, A, tq, A, R, A, A, g->ca_q_w[l], g->ca_in_b[l], 1, spl);
       if (qpos) {
-        FX_TRY(linear_bwd_pair(dwq, desc_linear_dx(dq, A, p->ca_q_w[l], R, A, A, P, A, 0, nullptr, 0, spl), s));
+        FX_TRY(launch_gemm(desc_linear_dx(dq, A, p->ca_q_w[l], R, A, A, P, A, 0, nullptr, 0, spl), s));
         FX_TRY(add_acc(dU, P, dT, G, RA, s));                                     // dT1 = dU + P ; G += P
       } else {
-        FX_TRY(linear_bwd_pair(dwq, dx_res_desc(dq, A, p->ca_q_w[l], A, R, A, A, dU, A, dT, A, spl), s));
+        FX_TRY(launch_gemm(dx_res_desc(dq, A, p->ca_q_w[l], A, R, A, A, dU, A, dT, A, spl), s));
       }
     }
     // --- self-attention + LN1
+    dU = slot_u(2, l);
     FX_TRY(launch_layernorm_bwd(dT, A, nullptr, 0, b + L.xh1, A, p->ln_sa_w[l], b + L.rs1, R, A, 0, dU, A,
                                 g->ln_sa_w[l], g->ln_sa_b[l], lnws, s));
-    FX_TRY(linear_bwd_pair(desc_linear_dwdb(dU, A, b + L.osa, A, R, A, A, g->sa_out_w[l], g->sa_out_b[l], 1, spl),
-                           desc_linear_dx(dU, A, p->sa_out_w[l], R, A, A, dO, A, 0, nullptr, 0, spl), s));
+    FX_TRY(launch_gemm(desc_linear_dx(dU, A, p->sa_out_w[l], R, A, A, dO, A, 0, nullptr, 0, spl), s));
     const float* qkv = b + L.qkv;
     FX_TRY(launch_mha_small_bwd(qkv, 3 * A, qkv + A, 3 * A, qkv + 2 * A, 3 * A, b + L.psa, dO, A, Qv, Qv, hd, h, scale,
                                 dQKV, 3 * A, dQKV + A, 3 * A, dQKV + 2 * A, 3 * A, s, nvid));
     float* dX = l == 0 ? nullptr : dT;   // the next (earlier) layer's output gradient, in place
     if (!qpos) {
-      const fx_gemm_desc dwi = desc_linear_dwdb(dQKV, 3 * A, x, ldx, R, A, 3 * A, g->sa_in_w[l], g->sa_in_b[l], 1, spl);
       if (l > 0 || dtgt)
-        FX_TRY(linear_bwd_pair(dwi, dx_res_desc(dQKV, 3 * A, p->sa_in_w[l], A, R, A, 3 * A, dU, A, l > 0 ? dX : dtgt,
-                                                l > 0 ? A : lddt, spl), s));
-      else
-        FX_TRY(launch_gemm(dwi, s));
+        FX_TRY(launch_gemm(dx_res_desc(dQKV, 3 * A, p->sa_in_w[l], A, R, A, 3 * A, dU, A, l > 0 ? dX : dtgt,
+                                       l > 0 ? A : lddt, spl), s));
     } else {
-      FX_TRY(linear_dwdb(dQKV, 3 * A, xq, ldxq, R, A, 2 * A, g->sa_in_w[l], g->sa_in_b[l], 1, spl, s));
-      FX_TRY(linear_dwdb(dQKV + 2 * A, 3 * A, x, ldx, R, A, A, g->sa_in_w[l] + 2LL * A * A, g->sa_in_b[l] + 2 * A, 1,
-                         spl, s));
       // P = dq W_q + dk W_k  (the position path);  dX = dU + dv W_v + P ; G += P
       FX_TRY(linear_dx(dQKV, 3 * A, p->sa_in_w[l], R, A, 2 * A, P, A, 0, nullptr, 0, spl, s));
       if (l > 0 || dtgt) {
@@ -454,6 +450,61 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
       } else {
         FX_TRY(add2(P, A, nullptr, 0, R, A, G, A, 1, s));
       }
+    }
+  }
+  hipStream_t sd = side_fork(s, 1);
+  {
+    // one weight-gradient kind over all layers: dW_l (+)= dy_l^T x_l (+ db_l), layer l's operands at layer
+    // 0's plus l times a stride; batched when the parameter gradients are uniformly strided (views of
+    // one flat buffer), else one launch per layer.  Split 1: the side stream must not touch `spl`,
+    // which the main stream's remaining GEMMs use.
+    auto kind = [&](int l0, int nl, const float* dy, long long lddy, long long dy_bs, const float* xx, long long ldxx,
+                    long long x_bs, int K, int N, float* const* gw, float* const* gb, long long b_off,
+                    long long w_off) -> int {
+      if (nl <= 0) return FX_OK;
+      bool uni = nl > 1;
+      for (int l = l0; l < l0 + nl && uni; ++l)
+        uni = gw[l] && (!gb || gb[l]) && gw[l] - gw[l0] == (long long)(l - l0) * (gw[l0 + 1] - gw[l0]) &&
+              (!gb || gb[l] - gb[l0] == (long long)(l - l0) * (gb[l0 + 1] - gb[l0]));
+      const int step = uni ? nl : 1;
+      for (int l = l0; l < l0 + nl; l += step) {
+        if (!gw[l]) continue;
+        fx_gemm_desc d = desc_linear_dwdb(dy + (l - l0) * dy_bs, lddy, xx + (l - l0) * x_bs, ldxx, R, K, N,
+                                          gw[l] + w_off, gb ? gb[l] + b_off : nullptr, 1, nullptr);
+        d.split_k = 1;
+        d.workspace = nullptr;
+        if (step > 1) {
+          d.batch = step;
+          d.a.batch_stride = dy_bs;
+          d.b.batch_stride = x_bs;
+          d.c_batch_stride = gw[l0 + 1] - gw[l0];
+          d.c_last_batch_stride = gb ? gb[l0 + 1] - gb[l0] : 0;
+        }
+        FX_TRY(launch_gemm(d, sd));
+      }
+      return FX_OK;
+    };
+    const long long PL = L.per_layer;
+    const float* b0 = saved + L.layers;
+    FX_TRY(kind(0, NL, slot_u(0, 0), A, RA, b0 + L.f1, FF, PL, FF, A, g->ff2_w, g->ff2_b, 0, 0));
+    FX_TRY(kind(0, NL, ws + L.gdf, FF, (long long)R * FF, b0 + (p->cross ? L.t2 : L.t1), A, PL, A, FF, g->ff1_w,
+                g->ff1_b, 0, 0));
+    if (p->cross) {
+      FX_TRY(kind(0, NL, slot_u(1, 0), A, RA, b0 + L.oca, A, PL, A, A, g->ca_out_w, g->ca_out_b, 0, 0));
+      FX_TRY(kind(0, NL, ws + L.gdq, A, RA, b0 + (qpos ? L.t1q : L.t1), A, PL, A, A, g->ca_q_w, g->ca_in_b, 0, 0));
+    }
+    FX_TRY(kind(0, NL, slot_u(2, 0), A, RA, b0 + L.osa, A, PL, A, A, g->sa_out_w, g->sa_out_b, 0, 0));
+    // self-attention in-projection: layer 0's input is tgt (its own pointer), layers >= 1 read the
+    // previous layer's output from `saved`
+    const float* dq0 = ws + L.gdqkv;
+    if (!qpos) {
+      FX_TRY(kind(0, 1, dq0, 3 * A, 3 * RA, tgt, ldt, 0, A, 3 * A, g->sa_in_w, g->sa_in_b, 0, 0));
+      FX_TRY(kind(1, NL - 1, dq0 + 3 * RA, 3 * A, 3 * RA, b0 + L.t3, A, PL, A, 3 * A, g->sa_in_w, g->sa_in_b, 0, 0));
+    } else {
+      FX_TRY(kind(0, NL, dq0, 3 * A, 3 * RA, b0 + L.xq, A, PL, A, 2 * A, g->sa_in_w, g->sa_in_b, 0, 0));
+      FX_TRY(kind(0, 1, dq0 + 2 * A, 3 * A, 3 * RA, tgt, ldt, 0, A, A, g->sa_in_w, g->sa_in_b, 2 * A, 2LL * A * A));
+      FX_TRY(kind(1, NL - 1, dq0 + 3 * RA + 2 * A, 3 * A, 3 * RA, b0 + L.t3, A, PL, A, A, g->sa_in_w, g->sa_in_b,
+                  2 * A, 2LL * A * A));
     }
   }
   if (qpos && dqpos) FX_CHECK_HIP(hipMemcpyAsync(dqpos, G, RA * sizeof(float), hipMemcpyDeviceToDevice, s));
@@ -483,7 +534,7 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
     // dWkv = dKV^T [mem+pos | mem] and its unpacking into the parameter gradients depend on nothing
     // the rest of the backward needs: side stream (the frame-level GEMM, K = T rows, leaves the main
     // stream), split so each workgroup holds its CU for a short K range
-    hipStream_t sd = side_fork(s, 2);
+    sd = side_fork(s, 2);
     const int ksp = sd != s ? defer_split(T) : 1;
     auto dw = [&](const float* a, const float* x, long long ldx_, int N, float* w, float* b) -> int {
       fx_gemm_desc d = desc_linear_dwdb(a, AL2, x, ldx_, T, p->Hm, N, w, b, 0, spl);
@@ -511,8 +562,8 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
     hipLaunchKernelGGL(unpack_kv_acc_kernel, dim3(std::min(cdiv((long long)A * p->Hm, 256), 256), 2 * NL), dim3(256),
                        0, sd, uk);
     FX_CHECK_HIP(hipGetLastError());
-    if (sd != s && !p->side_defer) FX_TRY(side_join_into(s));
   }
+  if (sd != s && !p->side_defer) FX_TRY(side_join_into(s));
   return FX_OK;
 }
 

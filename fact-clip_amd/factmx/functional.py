@@ -1170,8 +1170,9 @@ class DecoderFn(torch.autograd.Function):
         dmem = _empty(*mem.shape, device=dev) if (mem is not None and nd[2]) else None
         dmpos = _empty(*mpos.shape, device=dev) if (hm and nd[3]) else None
         ws = _ws(lib.fx_decoder_workspace_floats(ctypes.byref(prm), R, T, nvid, hq, hm), dev)
-        # cross-attention decoders leave the frame-memory K/V weight gradient on the side stream
-        defer = bool(meta["cross"]) and DEFER_SIDE and side_stream() is not None
+        # the token linears' weight gradients (and, cross-attention decoders, the frame-memory K/V one)
+        # stay on the side stream
+        defer = DEFER_SIDE and side_stream() is not None
         prm.side_defer = int(defer)
         _check(lib.fx_decoder_bwd(ctypes.byref(prm), ctypes.byref(g), nx.ptr(tgt), nx.ld(tgt), R, nx.ptr(qpos),
                                   nx.ptr(mem), nx.ld(mem), T, nvid, nx.ptr(mpos), nx.ld(mpos), nx.ptr(dout),
@@ -1179,7 +1180,7 @@ class DecoderFn(torch.autograd.Function):
                                   nx.ptr(dtgt), nx.ld(dtgt), nx.ptr(dqpos), nx.ptr(dmem), nx.ld(dmem), nx.ptr(dmpos),
                                   nx.ld(dmpos), nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_decoder_bwd")
         if defer:
-            _defer_to_side(mem, mpos, saved, ws)
+            _defer_to_side(tgt, mem, mpos, saved, ws)
         return (dtgt, dqpos, dmem, dmpos, None, None) + tuple(t[1] for t in tg)
 
 

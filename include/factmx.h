@@ -215,8 +215,9 @@ typedef struct fx_decoder_params {
   const float* const* ln_ff_w; const float* const* ln_ff_b;
   const float* fn_w; const float* fn_b;
   const float* out_w; const float* out_b;
-  int side_defer;             /* bwd (cross): leave the frame-memory K/V weight-gradient GEMM running on the
-                                 library's side stream (joined by fx_side_join), as fx_mstcn_params */
+  int side_defer;             /* bwd: leave the weight-gradient GEMMs (token linears of every layer, and
+                                 the frame-memory K/V projection when cross) running on the library's
+                                 side stream (joined by fx_side_join), as fx_mstcn_params */
 } fx_decoder_params;
 
 typedef struct fx_decoder_grads {
