@@ -20,7 +20,9 @@ the weights and therefore S; the S it ends with is reported there).
   python bench.py --config breakfast         # BASELINE configs[0]: vanilla FACT, T=512
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-Rank 0 prints one JSON line.  ``value`` = all frames processed by all ranks /
+``python bench.py --gpus N`` (N > 1, no launcher environment) starts the N ranks itself as a
+torchrun child before anything touches the GPU, and refuses (exit 2) when fewer than N GPUs are
+visible or when WORLD_SIZE disagrees with --gpus.  Rank 0 prints one JSON line.  ``value`` = all frames processed by all ranks /
 max-over-ranks wall time of the K timed steps.
 """
 import argparse
@@ -259,6 +261,31 @@ def cpu_baseline(wl, T, videos_seeds, min_seconds=10.0, min_steps=2):
                        f"oracle fp32 (1 untimed warm-up step, {dt:.1f} s timed)"), flops, S
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """``--gpus N`` without a torch.distributed launcher: start N ranks (one process per GPU) as a
+    torchrun child and return its exit code.  Runs BEFORE anything touches the GPU (counting devices
+    does not initialise it); refuses loudly when fewer than N GPUs are visible, so an N-GPU request is
+    never timed as one rank."""
+    import subprocess
+    visible = torch.cuda.device_count()
+    if visible < n:
+        log(f"bench.py: --gpus {n} requested but only {visible} GPU(s) are visible; refusing to time "
+            f"fewer ranks than requested")
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    log("bench.py: launching " + " ".join(cmd))
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -278,7 +305,12 @@ def main():
     nv = args.videos or vids_def
     adam_steps = args.steps if args.adam_steps is None else args.adam_steps
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank per requested GPU")
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch.distributed as dist

@@ -34,7 +34,7 @@ constexpr int GT = 256;         // threads per workgroup
 constexpr int MAXU = 16;        // hidden units per workgroup (Hh <= 256)
 constexpr int KCH = 64;         // fwd: k-chunk per thread (4 chunks cover Hh <= 256)
 constexpr int RCH = 48;         // bwd: gate rows per thread (16 chunks cover 3Hh <= 768)
-constexpr unsigned SPIN_MAX = 1u << 20;   // ~1 s of polling: a lost peer ends the kernel, never hangs it
+constexpr unsigned SPIN_MAX = 1u << 20;   // default: ~1 s of polling; a lost peer ends the kernel, never hangs it
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
@@ -48,7 +48,7 @@ __device__ __forceinline__ void put_granule(unsigned long long* g, unsigned epoc
 
 // one wave gathers n granules of `epoch` into LDS dst (bounded spin; on timeout flags *tmo)
 __device__ __forceinline__ bool gather_granules(unsigned long long* g, int n, unsigned epoch, float* dst,
-                                                unsigned* tmo, int lane) {
+                                                unsigned* tmo, unsigned spin_max, int lane) {
   for (int base = 0; base < n; base += 64 * 4) {
     unsigned long long x[4];
     bool done[4];
@@ -69,7 +69,7 @@ __device__ __forceinline__ bool gather_granules(unsigned long long* g, int n, un
         }
       }
       if (__all(ok)) break;
-      if (spins > SPIN_MAX) {
+      if (spins > spin_max) {
         if (lane == 0) __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return false;
       }
@@ -97,7 +97,8 @@ struct GruDirArgs {
 struct GruArgs {
   GruDirArgs d[2];
   unsigned long long* gran;
-  unsigned* tmo;
+  unsigned* tmo;        // the caller's status word (fx_gru_bidir_*: FX_STATUS_GRU_TIMEOUT on a lost peer)
+  unsigned spin_max;
   int off[MAXSEQ + 1];
 };
 
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(GT) void gru_fwd_kernel(GruArgs args) {
       const int q = (Hh + 4 * 64 - 1) / (4 * 64) * 64, b0 = (tid >> 6) * q;
       if (b0 < Hh &&
           !gather_granules(gran + (long long)(s & 1) * Hh + b0, min(q, Hh - b0), (unsigned)(s + 1), h + b0, args.tmo,
-                           lane))
+                           args.spin_max, lane))
         dead = 1;
     }
     __syncthreads();
@@ -198,7 +199,8 @@ struct GruBwdDirArgs {
 struct GruBwdArgs {
   GruBwdDirArgs d[2];
   unsigned long long* gran;
-  unsigned* tmo;
+  unsigned* tmo;        // the caller's status word (fx_gru_bidir_*: FX_STATUS_GRU_TIMEOUT on a lost peer)
+  unsigned spin_max;
   int off[MAXSEQ + 1];
 };
 
@@ -267,7 +269,8 @@ __global__ __launch_bounds__(GT) void gru_bwd_kernel(GruBwdArgs args) {
     if (s + 1 == S) break;   // the last step's recurrent gradient feeds nothing
     {   // the 4 waves gather a quarter of the 3Hh gate gradients each
       const int q = (H3 + 4 * 64 - 1) / (4 * 64) * 64, b0 = wv * q;
-      if (b0 < H3 && !gather_granules(slot + b0, min(q, H3 - b0), (unsigned)(s + 1), dg + b0, args.tmo, lane))
+      if (b0 < H3 && !gather_granules(slot + b0, min(q, H3 - b0), (unsigned)(s + 1), dg + b0, args.tmo, args.spin_max,
+                                           lane))
         dead = 1;
     }
     __syncthreads();
@@ -294,7 +297,8 @@ __global__ __launch_bounds__(GT) void gru_bwd_kernel(GruBwdArgs args) {
 long long gru_sync_floats(int Hh, int nseq) { return 4 + (long long)std::max(nseq, 1) * 2 * 2 * 3 * Hh * 2; }
 
 int launch_gru_fwd(const float* gi, long long ldgi, int nseq, const int* seq_off, int Hh, const float* const whh[2],
-                   const float* const bhh[2], float* out, long long ldo, float* saved, float* ws, hipStream_t s) {
+                   const float* const bhh[2], float* out, long long ldo, float* saved, float* ws, unsigned* status,
+                   int spin_max, hipStream_t s) {
   FX_REQUIRE(Hh > 0 && Hh <= NW * MAXU, "gru: hidden size per direction must be <= 256");
   const int Stot = seq_off[nseq];
   if (Stot == 0) return FX_OK;
@@ -304,7 +308,8 @@ int launch_gru_fwd(const float* gi, long long ldgi, int nseq, const int* seq_off
   for (int c0 = 0; c0 < nseq; c0 += MAXSEQ) {
     const int nc = std::min(MAXSEQ, nseq - c0);
     GruArgs args{};
-    args.tmo = tmo;
+    args.tmo = status ? status : tmo;
+    args.spin_max = spin_max > 0 ? (unsigned)spin_max : SPIN_MAX;
     args.gran = gran + (long long)c0 * 2 * 2 * 3 * Hh;
     for (int q = 0; q <= nc; ++q) args.off[q] = seq_off[c0 + q];
     for (int d = 0; d < 2; ++d) {
@@ -327,7 +332,8 @@ int launch_gru_fwd(const float* gi, long long ldgi, int nseq, const int* seq_off
 }
 
 int launch_gru_bwd(const float* dout, long long lddo, int nseq, const int* seq_off, int Hh, const float* const whh[2],
-                   const float* saved, float* dgi, long long lddgi, float* dgh, float* sync_ws, hipStream_t s) {
+                   const float* saved, float* dgi, long long lddgi, float* dgh, float* sync_ws, unsigned* status,
+                   int spin_max, hipStream_t s) {
   FX_REQUIRE(Hh > 0 && Hh <= NW * MAXU, "gru: hidden size per direction must be <= 256");
   const int Stot = seq_off[nseq];
   if (Stot == 0) return FX_OK;
@@ -338,7 +344,8 @@ int launch_gru_bwd(const float* dout, long long lddo, int nseq, const int* seq_o
   for (int c0 = 0; c0 < nseq; c0 += MAXSEQ) {
     const int nc = std::min(MAXSEQ, nseq - c0);
     GruBwdArgs args{};
-    args.tmo = tmo;
+    args.tmo = status ? status : tmo;
+    args.spin_max = spin_max > 0 ? (unsigned)spin_max : SPIN_MAX;
     args.gran = gran + (long long)c0 * 2 * 2 * H3;
     for (int q = 0; q <= nc; ++q) args.off[q] = seq_off[c0 + q];
     for (int d = 0; d < 2; ++d) {

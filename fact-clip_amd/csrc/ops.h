@@ -37,10 +37,12 @@ int launch_seg_mean_bwd(const float* dy, long long lddy, const int32_t* sid, con
                         int T, int cols, float* dx, long long lddx, int accumulate, hipStream_t s);
 // nseq independent sequences stacked by rows: sequence q owns rows [seq_off[q], seq_off[q+1]) (host)
 int launch_gru_fwd(const float* gi, long long ldgi, int nseq, const int* seq_off, int Hh, const float* const whh[2],
-                   const float* const bhh[2], float* out, long long ldo, float* saved, float* ws, hipStream_t s);
+                   const float* const bhh[2], float* out, long long ldo, float* saved, float* ws, unsigned* status,
+                   int spin_max, hipStream_t s);
 long long gru_sync_floats(int Hh, int nseq);
 int launch_gru_bwd(const float* dout, long long lddo, int nseq, const int* seq_off, int Hh, const float* const whh[2],
-                   const float* saved, float* dgi, long long lddgi, float* dgh, float* sync_ws, hipStream_t s);
+                   const float* saved, float* dgi, long long lddgi, float* dgh, float* sync_ws, unsigned* status,
+                   int spin_max, hipStream_t s);
 
 // ---- composite helpers (capi.cpp) --------------------------------------------
 int ew_grid(long long total);

@@ -173,6 +173,11 @@ class DataParallel:
     def _arm(self, k, x):
         # one arm per video that ran block k (the per-video path runs the blocks once per video):
         # the bucket launches when the LAST of them has its input gradient
+        if k in self._launched:
+            # a second backward without zero_grad would add unreduced gradients on top of reduced ones
+            raise RuntimeError("factmx DataParallel: each step must be zero_grad(), one forward + backward, "
+                               "finish_gradients(); gradient accumulation over several backward passes "
+                               "between zero_grad() calls is not supported")
         if k in self.block_buckets:
             self._armed[k] = self._armed.get(k, 0) + 1
             x.register_hook(lambda g, k=k: self._fired(k))

@@ -847,6 +847,39 @@ def conv3(x, w, b, dil, T):
 # bidirectional GRU over segments
 # ---------------------------------------------------------------------------
 
+# Polls a BiGRU workgroup makes for a peer's step before it gives up (0: the library default,
+# ~1 s).  Tests lower it to force the timeout path.
+GRU_SPIN_MAX = 0
+_status = {}
+
+
+def device_status(dev):
+    """The per-device int32 status word the kernels set on a failure they cannot report through a
+    return code (FX_STATUS_GRU_TIMEOUT: a BiGRU workgroup gave up waiting for a peer, so that
+    launch's outputs are wrong).  Read at the step's host read-back (status_raise)."""
+    dev = torch.device(dev)
+    t = _status.get(dev)
+    if t is None:
+        t = torch.zeros(4, dtype=torch.int32, device=dev)
+        _status[dev] = t
+    return t
+
+
+def status_raise(value, dev):
+    """Raise FactmxNativeError for a non-zero status word read back from the device (and clear it)."""
+    if value:
+        device_status(dev).zero_()
+        raise nx.FactmxNativeError(f"device status {value}: a BiGRU workgroup timed out waiting for its peers "
+                                   "(FX_STATUS_GRU_TIMEOUT) -- the GRU outputs of this step are invalid")
+
+
+def check_device_status(dev=None):
+    """Synchronous check of the status word (e.g. after the last backward of a run)."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if dev is None else torch.device(dev)
+    if dev in _status:
+        status_raise(int(_status[dev][0].item()), dev)
+
+
 class GRUFn(torch.autograd.Function):
     """One bidirectional ``nn.GRU`` layer (blocks.py:401,432) on (S, In) rows -> (S, 2Hh).
     ``seq_off`` = None (one sequence) or the host prefix list of several sequences stacked by
@@ -865,7 +898,8 @@ class GRUFn(torch.autograd.Function):
         ws = _ws(lib.fx_gru_workspace_floats(S, nq, In, Hh), dev)
         _check(lib.fx_gru_bidir_fwd(nx.ptr(x), nx.ld(x), S, nq, so, In, Hh, nx.ptr(w_ih), nx.ptr(w_hh), nx.ptr(b_ih),
                                     nx.ptr(b_hh), nx.ptr(w_ih_r), nx.ptr(w_hh_r), nx.ptr(b_ih_r), nx.ptr(b_hh_r),
-                                    nx.ptr(out), 2 * Hh, nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_gru_bidir_fwd")
+                                    nx.ptr(out), 2 * Hh, nx.ptr(saved), nx.ptr(ws), nx.ptr(device_status(dev)),
+                                    GRU_SPIN_MAX, nx.stream()), "fx_gru_bidir_fwd")
         ctx.seq_off = seq_off
         ctx.save_for_backward(x, w_ih, w_hh, b_ih, b_hh, w_ih_r, w_hh_r, b_ih_r, b_hh_r, saved)
         return out
@@ -889,7 +923,8 @@ class GRUFn(torch.autograd.Function):
         ws = _ws(lib.fx_gru_workspace_floats(S, nq, In, Hh), dev)
         _check(lib.fx_gru_bidir_bwd(nx.ptr(x), nx.ld(x), S, nq, so, In, Hh, nx.ptr(w_ih), nx.ptr(w_hh), nx.ptr(w_ih_r),
                                     nx.ptr(w_hh_r), nx.ptr(saved), nx.ptr(dout), 2 * Hh, nx.ptr(dx), nx.ld(dx),
-                                    *[nx.ptr(t) for t in bufs], nx.ptr(ws), nx.stream()), "fx_gru_bidir_bwd")
+                                    *[nx.ptr(t) for t in bufs], nx.ptr(ws), nx.ptr(device_status(dev)), GRU_SPIN_MAX,
+                                    nx.stream()), "fx_gru_bidir_bwd")
         return (dx, None) + tuple(t[1] for t in tg)
 
 

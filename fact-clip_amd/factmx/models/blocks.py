@@ -710,7 +710,11 @@ def _forward_videos(net, seq_list, label_list, compute_loss):
             net.video_segments.append([blk.tdu.num_seg for blk in net.block_list if hasattr(blk, "tdu")])
             finish_video(v, trans)
     # one read-back for every video's predictions (+ loss floats)
-    host = torch.cat([p.reshape(-1).to(torch.int64) for p in preds]).cpu().numpy()
+    st = fxf._status.get(preds[0].device) if preds[0].is_cuda else None    # kernel-side failures (GRU timeout)
+    host = torch.cat([p.reshape(-1).to(torch.int64) for p in preds] +
+                     ([st[:1].to(torch.int64)] if st is not None else [])).cpu().numpy()
+    if st is not None:
+        fxf.status_raise(int(host[-1]), preds[0].device)
     off = 0
     for save, p in zip(save_list, preds):
         save["pred"] = host[off:off + p.numel()].copy()

@@ -261,7 +261,8 @@ def run(net, vb, compute_loss, early=None):
         pk.send()
         nx.check(lib.fx_eval_pred(ctypes.addressof(va), base + va_off, nvid, float(cfg.FACT.mwt), nx.ptr(pred),
                                   nx.stream()), "fx_eval_pred")
-        host = pred.cpu().numpy()
+        host = torch.cat([pred, fxf.device_status(dev)[:1]]).cpu().numpy()
+        fxf.status_raise(int(host[-1]), dev)
         return [{"pred": host[v * T:(v + 1) * T].astype(np.int64)} for v in range(nvid)]
 
     assert early is not None and early.done, "the last block did not run the early matching stage"
@@ -453,9 +454,12 @@ def run(net, vb, compute_loss, early=None):
     # one synchronisation for the predictions and every loss value
     out_h = torch.empty(out.shape, dtype=torch.float32, pin_memory=True)
     pred_h = torch.empty(pred.shape, dtype=torch.int32, pin_memory=True)
+    st_h = torch.empty(1, dtype=torch.int32, pin_memory=True)
     out_h.copy_(out.detach(), non_blocking=True)
     pred_h.copy_(pred, non_blocking=True)
+    st_h.copy_(fxf.device_status(dev)[:1], non_blocking=True)   # kernel-side failures (GRU timeout)
     torch.cuda.current_stream().synchronize()
+    fxf.status_raise(int(st_h[0]), dev)
     vals = out_h.tolist()
     ph = pred_h.numpy()
     save_list = [{"pred": ph[v * T:(v + 1) * T].astype(np.int64)} for v in range(nvid)]

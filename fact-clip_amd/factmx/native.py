@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FACTMX_LIB", os.path.join(_HERE, "_lib", "libfactmx.so"))
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -81,6 +81,7 @@ class DecoderGrads(ctypes.Structure):
     _fields_ = [(n, P) for n in _DEC_PTRS] + [(n, P) for n in DECODER_GLOBAL_FIELDS]
 
 
+STATUS_GRU_TIMEOUT = 1   # FX_STATUS_GRU_TIMEOUT: a BiGRU workgroup gave up waiting for a peer
 LOSS_MAXK = 64
 LOSS_NB = 128          # FX_LOSS_NB: row blocks per loss term
 TERM_CLASS, TERM_ATTN, TERM_INFONCE = 0, 1, 2
@@ -154,8 +155,8 @@ SIGNATURES = {
     "fx_dropout": (I, [P, L, I, I, L, L, F, U, P, L, P]),
     "fx_gru_saved_floats": (L, [I, I]),
     "fx_gru_workspace_floats": (L, [I, I, I, I]),
-    "fx_gru_bidir_fwd": (I, [P, L, I, I, P, I, I, P, P, P, P, P, P, P, P, P, L, P, P, P]),
-    "fx_gru_bidir_bwd": (I, [P, L, I, I, P, I, I, P, P, P, P, P, P, L, P, L, P, P, P, P, P, P, P, P, P, P]),
+    "fx_gru_bidir_fwd": (I, [P, L, I, I, P, I, I, P, P, P, P, P, P, P, P, P, L, P, P, P, I, P]),
+    "fx_gru_bidir_bwd": (I, [P, L, I, I, P, I, I, P, P, P, P, P, P, L, P, L, P, P, P, P, P, P, P, P, P, P, I, P]),
     "fx_segments_from_probs": (I, [P, L, I, I, I, I, P, P, P, P, P, P]),
     "fx_segments_globalize": (I, [I, I, P, P, P, P, P, P, P, P]),
     "fx_seg_mean_fwd": (I, [P, L, P, P, I, I, P, L, P]),

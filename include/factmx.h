@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FX_ABI_VERSION 15
+#define FX_ABI_VERSION 16
 
 enum {
   FX_OK = 0,
@@ -459,20 +459,27 @@ int fx_seg_sum_rows(const float* dx, long long lddx, const int32_t* seg_start, c
  *   saved (fx_gru_saved_floats): per-step h_{t-1} and gates for backward.
  * bwd: dout (S, 2Hh) -> dx (nullable) and every weight/bias gradient
  *   (accumulated +=; each pointer nullable).
+ * The 2 x 16 workgroups of a sequence exchange the hidden state / gate gradients
+ *   through L2 with bounded spins; a peer that does not arrive within spin_max polls
+ *   (0: the default, ~1 s) ends the kernel early and sets *status = FX_STATUS_GRU_TIMEOUT
+ *   (status: caller-owned device int32, nullable, never cleared by the library).  The
+ *   outputs are then wrong: the caller reads the word at its next host read-back and
+ *   fails (factmx raises FactmxNativeError).
  * ---------------------------------------------------------------------- */
+#define FX_STATUS_GRU_TIMEOUT 1
 long long fx_gru_saved_floats(int S, int Hh);
 long long fx_gru_workspace_floats(int S, int nseq, int In, int Hh);
 int fx_gru_bidir_fwd(const float* x, long long ldx, int S, int nseq, const int* seq_off, int In,
                      int Hh, const float* w_ih_f, const float* w_hh_f, const float* b_ih_f,
                      const float* b_hh_f, const float* w_ih_r, const float* w_hh_r, const float* b_ih_r,
                      const float* b_hh_r, float* out, long long ldo, float* saved, float* workspace,
-                     void* stream);
+                     int32_t* status, int spin_max, void* stream);
 int fx_gru_bidir_bwd(const float* x, long long ldx, int S, int nseq, const int* seq_off, int In,
                      int Hh, const float* w_ih_f, const float* w_hh_f, const float* w_ih_r,
                      const float* w_hh_r, const float* saved, const float* dout, long long lddo,
                      float* dx, long long lddx, float* dw_ih_f, float* dw_hh_f, float* db_ih_f,
                      float* db_hh_f, float* dw_ih_r, float* dw_hh_r, float* db_ih_r, float* db_hh_r,
-                     float* workspace, void* stream);
+                     float* workspace, int32_t* status, int spin_max, void* stream);
 
 /* ------------------------------------------------------------------------
  * Dropout (nn.Dropout in training: basic.py:158-160 MS-TCN residual branch, 382 X2Y concat,

@@ -142,6 +142,49 @@ def test_data_parallel_hooks_broadcast_and_mean(tmp_path):
         torch.testing.assert_close(got["grads"][n], p.grad, rtol=1e-5, atol=1e-7)
 
 
+def _accum_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        net = _ToyBlocks(seed=0)
+        dp = DataParallel(net, bucket_mb=0.0002)
+        x = _videos()[rank]
+        dp.zero_grad()
+        net(x).pow(2).mean().backward()
+        raised = False
+        try:             # a second forward before zero_grad: its hooks would add unreduced gradients
+            net(x).pow(2).mean().backward()
+        except RuntimeError:
+            raised = True
+        dp.finish_gradients()
+        if rank == 0:
+            torch.save(torch.tensor([raised]), out_path)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_refuses_gradient_accumulation(tmp_path):
+    out = str(tmp_path / "acc.pt")
+    mp.spawn(_accum_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    assert torch.load(out, weights_only=True).tolist() == [True]
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """bench.py --gpus N must start N ranks or refuse: never time one rank for an N-GPU request."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HIP_VISIBLE_DEVICES"] = ""          # no GPU visible (as in this container)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and "refusing" in r.stderr, r.stderr[-2000:]
+    env["WORLD_SIZE"] = "1"                  # a launcher that started fewer ranks than --gpus asks for
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr, r.stderr[-2000:]
+
+
 class _NamesDataset:
     def __init__(self, n):
         self.names = [f"v{i}" for i in range(n)]

@@ -48,19 +48,32 @@ def _segments(net):
     return bench.video_segments(net)
 
 
-def _check_forward(net, spec, outs, saves, text, last_only_attrs=True):
-    """Per-video predictions identical; the side-channel attributes (the last video's) give logits
-    within 1e-3 and TDU boundaries identical."""
+def _video_records(net, nvid):
+    """Per video, per block: (frame_clogit (T, C), tdu) of the last forward.  A lockstep batch keeps
+    every video's views in blk._vrec; the per-video path leaves only the last video's attributes."""
+    blocks = list(net.block_list)
+    if all(getattr(b, "_vrec", None) is not None and len(b._vrec) == nvid for b in blocks):
+        return [[(b._vrec[v]["frame_clogit"], b._vrec[v].get("tdu")) for b in blocks] for v in range(nvid)]
+    return [None] * (nvid - 1) + [[(b.frame_clogit, getattr(b, "tdu", None)) for b in blocks]]
+
+
+def _check_forward(net, spec, outs, saves, text):
+    """Per-video predictions identical; for EVERY video of a lockstep batch (the last one on the
+    per-video path) per-frame logits of every block within 1e-3 and TDU boundaries identical."""
     for v, out in enumerate(outs):
         pred = fo.predict(spec, out, None if text is None else text.double().cpu())
         np.testing.assert_array_equal(saves[v]["pred"], pred.numpy(), err_msg=f"video {v}")
-    rec_last = outs[-1]
-    for i, (blk, rec) in enumerate(zip(net.block_list, rec_last["blocks"])):
-        if rec["type"] == "U":
-            np.testing.assert_array_equal(blk.tdu.start32.cpu().numpy(), rec["tdu"].starts, err_msg=f"block {i}")
-            np.testing.assert_array_equal(blk.tdu.end32.cpu().numpy(), rec["tdu"].ends, err_msg=f"block {i}")
-        err = (blk.frame_clogit[:, 0].double().cpu() - rec["frame_clogit"]).abs().max().item()
-        assert err < 1e-3, f"block {i}: per-frame logits differ by {err}"
+    recs = _video_records(net, len(outs))
+    assert recs[-1] is not None
+    for v, (got, out) in enumerate(zip(recs, outs)):
+        if got is None:
+            continue
+        for i, ((fcl, tdu), rec) in enumerate(zip(got, out["blocks"])):
+            if rec["type"] == "U":
+                np.testing.assert_array_equal(tdu.start32.cpu().numpy(), rec["tdu"].starts, err_msg=f"v{v} block {i}")
+                np.testing.assert_array_equal(tdu.end32.cpu().numpy(), rec["tdu"].ends, err_msg=f"v{v} block {i}")
+            err = (fcl[:, 0].double().cpu() - rec["frame_clogit"]).abs().max().item()
+            assert err < 1e-3, f"video {v} block {i}: per-frame logits differ by {err}"
 
 
 def test_north_star_lockstep_backward_vs_oracle(monkeypatch):

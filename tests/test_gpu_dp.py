@@ -1,0 +1,94 @@
+"""Data parallelism on the real model, on the GPU (BASELINE configs[3] leg; reference semantics:
+the per-video loss mean of blocks.py:913-915).
+
+Two ranks share the one leased MI355X (gloo over CUDA tensors: RCCL refuses two ranks on one
+device), each running bench.py's FACT_CLIP lockstep step (HAViD-holdout dims, T=2048) on two of
+the four videos of a global batch through factmx.dp.DataParallel.  Checked:
+  * the reduced flat gradient is identical on both ranks and equals the single-process gradient
+    of the 4-video lockstep batch (mean of the per-video losses, the bench's flat-buffer path);
+  * the blocks' buckets were launched from the backward hooks, last block first;
+  * the rank-0 broadcast made the weights identical (rank 1 starts from another seed).
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+T, VIDS_PER_RANK, WORLD = 2048, 2, 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run_ranks(out):
+    port = str(_free_port())
+    procs = []
+    for r in range(WORLD):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(WORLD), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "dp_worker.py"), "--out", out,
+                                       "--T", str(T), "--videos", str(VIDS_PER_RANK)], env=env))
+    codes = []
+    for p in procs:
+        try:
+            codes.append(p.wait(timeout=300))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    assert codes == [0] * WORLD, codes
+
+
+def test_dp_two_ranks_equal_single_process_lockstep(tmp_path):
+    import bench
+    from factmx.dp import DataParallel
+    out = str(tmp_path)
+    _run_ranks(out)
+    rk = [np.load(os.path.join(out, f"rank{r}.npz")) for r in range(WORLD)]
+    # broadcast: identical weights on both ranks
+    np.testing.assert_array_equal(rk[0]["wsum"], rk[1]["wsum"])
+    # all-reduce: identical gradients on both ranks
+    np.testing.assert_array_equal(rk[0]["flat"], rk[1]["flat"])
+    # buckets from hooks, in backward order (block 0's input is the data: launched at finish)
+    nblk = int(rk[0]["nblk"])
+    for r in rk:
+        assert r["early"].tolist() == list(range(nblk - 1, 0, -1)), r["early"]
+    # single process, the same 4 videos in one lockstep batch, seed-0 weights (= rank 0's)
+    dev = torch.device("cuda", 0)
+    cfg = bench.make_cfg()
+    net, _ = bench.build_model(cfg, bench.D_IN, bench.NCLS, dev, seed=0)
+    net.train()
+    w = torch.cat([p.detach().reshape(-1).double() for p in net.parameters()])
+    np.testing.assert_allclose(rk[0]["wsum"], [float(w.sum()), float((w * w).sum())], rtol=0, atol=0)
+    dp = DataParallel(net)
+    vids = [bench.make_video(T, bench.D_IN, bench.NCLS, cfg, seed=s) for s in range(1, 1 + WORLD * VIDS_PER_RANK)]
+    dp.zero_grad()
+    loss, _ = net([torch.from_numpy(f).to(dev) for f, _ in vids], [torch.from_numpy(l_).to(dev) for _, l_ in vids],
+                  compute_loss=True)
+    loss.backward()
+    dp.finish_gradients()
+    torch.cuda.synchronize()
+    S = bench.video_segments(net)
+    assert S == rk[0]["S"].tolist() + rk[1]["S"].tolist(), (S, rk[0]["S"], rk[1]["S"])
+    assert abs((rk[0]["loss"] + rk[1]["loss"]) / 2 - loss.item()) <= 1e-5 * abs(loss.item())
+    ref = dp.flat.detach().cpu().numpy()
+    got = rk[0]["flat"]
+    off, bad = 0, []
+    for n, p in net.named_parameters():
+        k = p.numel()
+        g, r = got[off:off + k].astype(np.float64), ref[off:off + k].astype(np.float64)
+        off += k
+        rms = float(np.sqrt((r * r).mean()))
+        tol = 1e-5 * np.abs(r) + 1e-3 * rms + 1e-9
+        if (np.abs(g - r) > tol).any():
+            bad.append(f"{n}: max |dg| {np.abs(g - r).max():.3g} (rms {rms:.3g})")
+    assert not bad, "DP gradient != single-process gradient:\n" + "\n".join(bad[:20])

@@ -1,0 +1,43 @@
+"""BiGRU timeouts are reported, not silent (GPU).
+
+The persistent BiGRU kernel (gru.hip) spreads each direction over 16 workgroups that exchange the
+hidden state through L2 with bounded spins; a workgroup that gives up on a peer ends the launch and
+sets the caller's status word (FX_STATUS_GRU_TIMEOUT).  Forcing a tiny spin bound must surface as
+FactmxNativeError at the step's single host read-back, and the next normal step must succeed.
+"""
+import pytest
+import torch
+
+from helpers import load_fixture, tiny_meta, cfg_from_meta, tiny_inputs
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def test_gru_timeout_raises_at_readback(monkeypatch):
+    import paramgen as pg
+    from factmx import functional as fxf
+    from factmx import native as nx
+    from factmx.models.blocks import FACT_CLIP
+    from factmx.models.loss import MatchCriterion
+    fx = load_fixture("tiny_clip_iid")          # many TDU segments: long GRU sequences
+    meta = tiny_meta(fx)
+    cfg = cfg_from_meta(meta)
+    feats, label, text = tiny_inputs(meta)
+    net = FACT_CLIP(cfg, meta["D"], meta["C"], text_embeddings=torch.from_numpy(text).float())
+    with torch.no_grad():
+        for n, p in net.named_parameters():
+            p.copy_(torch.from_numpy(pg.param_value(n, p.shape, meta["seed"])))
+    net.mcriterion = MatchCriterion(cfg, meta["C"], [])
+    net = net.to(DEV).train()
+    seqs = [torch.from_numpy(feats).float().to(DEV)] * 2
+    labs = [torch.from_numpy(label).to(DEV)] * 2
+    monkeypatch.setattr(fxf, "GRU_SPIN_MAX", 1)      # give up after two empty polls
+    with pytest.raises(nx.FactmxNativeError, match="GRU"):
+        net(seqs, labs, compute_loss=True)
+    torch.cuda.synchronize()
+    monkeypatch.setattr(fxf, "GRU_SPIN_MAX", 0)
+    loss, _ = net(seqs, labs, compute_loss=True)
+    loss.backward()
+    fxf.check_device_status()
+    assert torch.isfinite(loss).item()
