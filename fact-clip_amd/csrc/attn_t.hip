@@ -116,6 +116,8 @@ __device__ __forceinline__ void zero16(f32x16& a) {
 // accumulator element r of a lane: row (r&3) + 8 (r>>2) + 4 (lane>>5), column lane&31
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
+constexpr int MAXV = 32;  // videos per launch (per-video key row offsets live in the kernel arguments)
+
 struct TAttnArgs {
   const float* q; long long ldq;
   const float* k; long long ldk;
@@ -125,15 +127,25 @@ struct TAttnArgs {
   float* out; long long ld_out;         // fwd: o;  bwd: dq
   float* dk; long long lddk;            // bwd
   float* dv; long long lddv;            // bwd
-  float* lse;                           // (nvid, h, Qv): fwd writes, bwd reads
+  float* lse;                           // (nvid, h, qs): fwd writes, bwd reads
   float* ws;                            // partials
-  unsigned* cnt;                        // per (video, head) arrival counters: in-launch merge; NULL -> merge launch
-  int Qv, Tv, hd, nh, Qp, Hp, Tc, nsplit;
+  int Qv, hd, nh, Qp, Hp, Tc, nsplit;   // Qv: queries of this block; nsplit: max chunks over the videos
+  int qs, q0;                           // query rows per video (q / o / lse stride), first query of the block
+  int acc_kv;                           // bwd: dK / dV += (later query blocks of the same keys)
   float scale;
   int vec;                              // 16-B loads of every q / k / v / o / dout row slice
+  float drop_p;                         // attention-probability dropout (training), counter-based mask
+  unsigned drop_thr;
+  unsigned long long drop_seed;
+  long long ktot;                       // key rows over all videos (mask index stride)
+  int koff[MAXV + 1];                   // key / value rows of video v: [koff[v], koff[v+1])
 };
 
-__device__ void tattn_finish(const TAttnArgs& a, int h, int vid, int stats, float mul, float* sm);
+// keep-scale of probability (global query row qg, head h, global key row kg): 1/(1-p) or 0
+__device__ __forceinline__ float drop_keep(const TAttnArgs& a, long long qg, int h, long long kg) {
+  const unsigned long long idx = ((unsigned long long)qg * a.nh + h) * (unsigned long long)a.ktot + kg;
+  return fx_drop_bits(a.drop_seed, idx) >= a.drop_thr ? 1.f / (1.f - a.drop_p) : 0.f;
+}
 
 // Strips of row-major sources staged into LDS images (row stride ld, zero outside the `nvalid` rows and
 // `hd` columns).  Every load of a workgroup's strips is issued before the first LDS store (a store
@@ -198,8 +210,10 @@ __global__ __launch_bounds__(AT) void tattn_fwd_kernel(TAttnArgs a) {
   float* red = ss + Qp * ls;            // [4][1024] wave partials
   float* rowm = red + 4 * 1024;         // [Qp]
   float* rowl = rowm + Qp;              // [Qp]
-  const int t0 = c * Tc, nk = min(Tc, a.Tv - t0);
-  const long long qrow = (long long)vid * a.Qv, krow = (long long)vid * a.Tv + t0;
+  const int Tv = a.koff[vid + 1] - a.koff[vid];
+  const int t0 = c * Tc, nk = min(Tc, Tv - t0);
+  if (nk <= 0) return;                  // a shorter video of a ragged batch has fewer chunks
+  const long long qrow = (long long)vid * a.qs + a.q0, krow = (long long)a.koff[vid] + t0;
   const float* qsrc = a.q + qrow * a.ldq + h * hd;
   const float* ksrc = a.k + krow * a.ldk + h * hd;
   const float* vsrc = a.v + krow * a.ldv + h * hd;
@@ -263,8 +277,10 @@ __global__ __launch_bounds__(AT) void tattn_fwd_kernel(TAttnArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float p = __expf(st[u][r] - M);
-      ls_ += p;
-      ss[myq * ls + kt * 32 + acc_row(r, lane)] = p;     // P image [query][key] for P V
+      ls_ += p;                                          // the softmax normaliser sees every key
+      const int key = kt * 32 + acc_row(r, lane);
+      const float kp = (a.drop_p > 0.f && key < nk) ? drop_keep(a, qrow + myq, h, krow + key) : 1.f;
+      ss[myq * ls + key] = p * kp;                       // (dropped) P image [query][key] for P V
     }
   }
   ls_ += __shfl_xor(ls_, 32, 64);
@@ -312,7 +328,8 @@ __global__ __launch_bounds__(AT) void tattn_fwd_kernel(TAttnArgs a) {
     }
   }
   if (a.nsplit == 1) {
-    for (int r = tid; r < a.Qv; r += AT) a.lse[((long long)vid * a.nh + h) * a.Qv + r] = rowm[r] + __logf(rowl[r]);
+    for (int r = tid; r < a.Qv; r += AT)
+      a.lse[((long long)vid * a.nh + h) * a.qs + a.q0 + r] = rowm[r] + __logf(rowl[r]);
     return;
   }
   float* pm = a.ws + (long long)gridDim.z * a.nh * a.nsplit * Qp * Hp;   // m partials, then l partials
@@ -322,7 +339,6 @@ __global__ __launch_bounds__(AT) void tattn_fwd_kernel(TAttnArgs a) {
     pl[pid * Qp + r] = rowl[r];
   }
   TSTAMP(4);
-  if (a.cnt) tattn_finish(a, h, vid, 1, 1.f, sm);
 }
 
 // Ordered merge of the nsplit partials of one (video, head) per workgroup, chunk order fixed
@@ -331,14 +347,15 @@ __global__ __launch_bounds__(AT) void tattn_fwd_kernel(TAttnArgs a) {
 // float4 loads in flight.
 __device__ void tattn_merge(const TAttnArgs& a, int h, int vid, int nvid, int stats, float mul, float* sm) {
   const int tid = threadIdx.x;
-  const int Qp = a.Qp, Hp = a.Hp, hd = a.hd, ns = a.nsplit;
-  const long long pbase = ((long long)vid * a.nh + h) * ns;
+  const int Qp = a.Qp, Hp = a.Hp, hd = a.hd, nsm = a.nsplit;
+  const int ns = (a.koff[vid + 1] - a.koff[vid] + a.Tc - 1) / a.Tc;   // this video's chunks
+  const long long pbase = ((long long)vid * a.nh + h) * nsm;
   const float* part = a.ws + pbase * Qp * Hp;
   float* w = sm;                         // [ns][Qp] weights
   float* wl = sm + ns * Qp;              // [ns][Qp] l partials
   if (stats) {
-    const float* pm = a.ws + (long long)nvid * a.nh * ns * Qp * Hp + pbase * Qp;
-    const float* pl = pm + (long long)nvid * a.nh * ns * Qp;
+    const float* pm = a.ws + (long long)nvid * a.nh * nsm * Qp * Hp + pbase * Qp;
+    const float* pl = pm + (long long)nvid * a.nh * nsm * Qp;
     for (int e = tid; e < ns * Qp; e += AT) {
       w[e] = pm[e];
       wl[e] = pl[e];
@@ -351,11 +368,11 @@ __device__ void tattn_merge(const TAttnArgs& a, int h, int vid, int nvid, int st
       for (int sp = 0; sp < ns; ++sp) L += __expf(w[sp * Qp + r] - M) * wl[sp * Qp + r];
       const float inv = 1.f / L;
       for (int sp = 0; sp < ns; ++sp) w[sp * Qp + r] = __expf(w[sp * Qp + r] - M) * inv;
-      if (r < a.Qv) a.lse[((long long)vid * a.nh + h) * a.Qv + r] = M + __logf(L);
+      if (r < a.Qv) a.lse[((long long)vid * a.nh + h) * a.qs + a.q0 + r] = M + __logf(L);
     }
     __syncthreads();
   }
-  float* out = a.out + (long long)vid * a.Qv * a.ld_out + h * hd;
+  float* out = a.out + ((long long)vid * a.qs + a.q0) * a.ld_out + h * hd;
   const int c4 = Hp >> 2;
   for (int e = tid; e < a.Qv * c4; e += AT) {
     const int r = e / c4, col = (e - r * c4) * 4;
@@ -389,32 +406,6 @@ __global__ __launch_bounds__(AT) void tattn_merge_kernel(TAttnArgs a, int stats,
   tattn_merge(a, blockIdx.x, blockIdx.y, gridDim.y, stats, mul, sm);
 }
 
-// In-launch merge: the workgroup of a (video, head) that writes the LAST chunk partial merges them all
-// (arrival counter per (video, head); partial stores drained, one agent-scope release by lane 0
-// before the ticket, one acquire in the merger; the counter is re-armed for the next launch).
-__device__ void tattn_finish(const TAttnArgs& a, int h, int vid, int stats, float mul, float* sm) {
-  int* flag = reinterpret_cast<int*>(sm);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned* cnt = a.cnt + (long long)vid * a.nh + h;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = prev == (unsigned)a.nsplit - 1;
-    if (last) {
-      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    *flag = last;
-  }
-  __syncthreads();
-  const int last = *flag;
-  __syncthreads();
-  if (last) tattn_merge(a, h, vid, gridDim.z, stats, mul, sm);
-}
-
 // ------------------------------------------------------------------------------------------ backward
 __global__ __launch_bounds__(AT) void tattn_bwd_kernel(TAttnArgs a) {
   extern __shared__ float sm[];
@@ -431,14 +422,16 @@ __global__ __launch_bounds__(AT) void tattn_bwd_kernel(TAttnArgs a) {
   float* red = ds + Qp * ls;            // [4][1024]
   float* rl = red + 4 * 1024;           // [Qp] lse
   float* rd = rl + Qp;                  // [Qp] D
-  const int t0 = c * Tc, nk = min(Tc, a.Tv - t0);
-  const long long qrow = (long long)vid * a.Qv, krow = (long long)vid * a.Tv + t0;
+  const int Tv = a.koff[vid + 1] - a.koff[vid];
+  const int t0 = c * Tc, nk = min(Tc, Tv - t0);
+  if (nk <= 0) return;
+  const long long qrow = (long long)vid * a.qs + a.q0, krow = (long long)a.koff[vid] + t0;
   const float* qsrc = a.q + qrow * a.ldq + h * hd;
   const float* dsrc = a.dout + qrow * a.lddo + h * hd;
   const float* osrc = a.o + qrow * a.ldo + h * hd;
   const float* ksrc = a.k + krow * a.ldk + h * hd;
   const float* vsrc = a.v + krow * a.ldv + h * hd;
-  if (tid < Qp) rl[tid] = tid < a.Qv ? a.lse[((long long)vid * a.nh + h) * a.Qv + tid] : 0.f;
+  if (tid < Qp) rl[tid] = tid < a.Qv ? a.lse[((long long)vid * a.nh + h) * a.qs + a.q0 + tid] : 0.f;
   if (a.vec) {
     Strip<NVQ> sq, sd, so;
     Strip<NVK> sk, sv;
@@ -481,8 +474,10 @@ __global__ __launch_bounds__(AT) void tattn_bwd_kernel(TAttnArgs a) {
     for (int r = 0; r < 16; ++r) {
       const int row = rt * 32 + acc_row(r, lane);
       const float p = (col < nk && row < a.Qv) ? __expf(s[r] * a.scale - rl[row]) : 0.f;
-      ps[row * ls + col] = p;
-      ds[row * ls + col] = p * (dp[r] - rd[row]);
+      // dropout: P_d = P keep / (1-p) multiplies V; dP = (dO V^T) keep / (1-p); D = rowsum(dO o) still
+      const float kp = (a.drop_p > 0.f && p != 0.f) ? drop_keep(a, qrow + row, h, krow + col) : 1.f;
+      ps[row * ls + col] = p * kp;
+      ds[row * ls + col] = p * (dp[r] * kp - rd[row]);
     }
   }
   __syncthreads();
@@ -504,7 +499,10 @@ __global__ __launch_bounds__(AT) void tattn_bwd_kernel(TAttnArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = kt * 32 + acc_row(r, lane);
-        if (key < nk) dst[(krow + key) * ld + h * hd + col] = acc[r] * mul;
+        if (key < nk) {
+          float* d = dst + (krow + key) * ld + h * hd + col;
+          *d = a.acc_kv ? *d + acc[r] * mul : acc[r] * mul;
+        }
       }
     }
   }
@@ -539,7 +537,6 @@ __global__ __launch_bounds__(AT) void tattn_bwd_kernel(TAttnArgs a) {
       for (int r = 0; r < 16; ++r) po[(rt * 32 + acc_row(r, lane)) * Hp + col] = acc[r];
     }
   }
-  if (a.nsplit > 1 && a.cnt) tattn_finish(a, h, vid, 0, a.scale, sm);
 }
 
 struct TAttnGeom {
@@ -547,11 +544,13 @@ struct TAttnGeom {
   size_t lds;
 };
 
+constexpr int QB = 64;    // queries per launch (query blocks of more tokens run as successive launches)
+
 // chunk: the largest power of two in [32, 256] whose LDS images fit (Tc * Hp <= NVK float4 per thread),
-// halved while the launch has fewer than ~256 workgroups
+// halved while the launch has fewer than ~256 workgroups.  Tv: the longest video's key count.
 TAttnGeom tattn_geom(int nvid, int Qv, int Tv, int hd, int nh, bool bwd) {
   TAttnGeom g{};
-  g.Qp = std::max(32, (Qv + 31) / 32 * 32);
+  g.Qp = std::max(32, (std::min(Qv, QB) + 31) / 32 * 32);
   g.Hp = std::max(32, (hd + 31) / 32 * 32);
   auto lds_b = [&](int Tc) {
     const size_t q = bwd ? 2 : 1, p = bwd ? 2 : 1;
@@ -561,11 +560,8 @@ TAttnGeom tattn_geom(int nvid, int Qv, int Tv, int hd, int nh, bool bwd) {
   int Tc = 256;
   // (forward: at most 8 score tiles, two per wave, in registers)
   while (Tc > 32 && (lds_b(Tc) > 150 * 1024 || Tc * g.Hp > NVK * 4 * AT || Tc * g.Qp > 8 * 1024)) Tc >>= 1;
-  static const int min_wg = [] {   // FX_TATTN_MINWG: workgroups the split aims for (diagnostic A/B)
-    const char* p = std::getenv("FX_TATTN_MINWG");
-    return p ? std::max(1, std::atoi(p)) : 256;
-  }();
-  while (Tc > 32 && (long long)nvid * nh * ((Tv + Tc - 1) / Tc) < min_wg) Tc >>= 1;
+  constexpr int kMinWorkgroups = 256;   // one per CU
+  while (Tc > 32 && (long long)nvid * nh * ((Tv + Tc - 1) / Tc) < kMinWorkgroups) Tc >>= 1;
   g.Tc = Tc;
   g.nsplit = std::max(1, (Tv + Tc - 1) / Tc);
   g.lds = lds_b(Tc);
@@ -592,90 +588,114 @@ long long tattn_ws_floats(int nvid, int Qv, int Tv, int hd, int nh) {
 
 static size_t merge_lds(const TAttnGeom& g) { return sizeof(float) * 2 * (size_t)g.nsplit * g.Qp; }
 
-// FX_TATTN_MERGE=in: the in-launch last-arriver merge instead of the separate ordered merge launch
-// (diagnostic A/B; both add the partials in chunk order, so the results are bitwise equal).  Measured
-// at the bench shape: fwd 22.4 vs 18.2 us, bwd 44.8 vs 33.2 us -- the agent-scope release / acquire
-// of the arrival hand-off (L2 write-back / invalidate on a multi-XCD part) costs more than the launch.
-static bool merge_in_launch() {
-  static const bool on = [] {
-    const char* p = std::getenv("FX_TATTN_MERGE");
-    return p && std::string(p) == "in";
-  }();
-  return on;
-}
-
 static bool a16(const void* p, long long ld) { return p == nullptr || (((uintptr_t)p & 15) == 0 && (ld & 3) == 0); }
 
-static int tattn_check(int nvid, int Qv, int Tv, int hd, int nh) {
+// shared argument set-up: key offsets (uniform Tv per video when opt->koff is NULL), dropout
+static int tattn_setup(TAttnArgs& a, int nvid, int Qv, int Tv, int hd, int nh, const TAttnOpts* opt, int& Tmax,
+                       long long& ktot) {
   static std::once_flag once;
   std::call_once(once, [] {   // dynamic LDS above the 64 KB default (gfx950: 160 KB per workgroup)
     (void)hipFuncSetAttribute((const void*)tattn_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)tattn_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)tattn_merge_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   });
-  FX_REQUIRE(nvid >= 1 && Qv >= 1 && Qv <= 64 && hd >= 1 && hd <= 64 && nh >= 1 && Tv >= 1,
-             "attention over T: 1..64 queries and head dim <= 64 per video, T >= 1");
-  FX_REQUIRE((long long)nvid * nh <= kArrivalCounters, "attention over T: too many (video, head) pairs");
+  FX_REQUIRE(nvid >= 1 && nvid <= MAXV && Qv >= 1 && hd >= 1 && hd <= 64 && nh >= 1,
+             "attention over T: 1..32 videos, >= 1 query, head dim <= 64");
+  Tmax = 0;
+  a.koff[0] = 0;
+  for (int v = 0; v < nvid; ++v) {
+    const int k0 = opt && opt->koff ? opt->koff[v] : v * Tv, k1 = opt && opt->koff ? opt->koff[v + 1] : (v + 1) * Tv;
+    FX_REQUIRE(k1 > k0 && k0 >= 0, "attention over T: every video needs >= 1 key row, offsets increasing");
+    a.koff[v] = k0;
+    a.koff[v + 1] = k1;
+    Tmax = std::max(Tmax, k1 - k0);
+  }
+  ktot = a.koff[nvid];
+  const float p = opt ? opt->drop_p : 0.f;
+  FX_REQUIRE(p >= 0.f && p < 1.f, "attention over T: dropout p in [0, 1)");
+  a.drop_p = p;
+  a.drop_thr = p > 0.f ? std::max(fx_drop_thresh(p), 1u) : 0u;
+  a.drop_seed = opt ? opt->drop_seed : 0ull;
+  a.ktot = ktot;
+  a.hd = hd;
+  a.nh = nh;
+  a.qs = Qv;
   return FX_OK;
 }
 
 int launch_tattn_fwd(const float* q, long long ldq, const float* k, long long ldk, const float* v, long long ldv,
                      int nvid, int Qv, int Tv, int hd, int nh, float scale, float* o, long long ldo, float* lse,
-                     float* ws, hipStream_t s) {
-  FX_TRY(tattn_check(nvid, Qv, Tv, hd, nh));
-  const TAttnGeom g = tattn_geom(nvid, Qv, Tv, hd, nh, false);
+                     float* ws, hipStream_t s, const TAttnOpts* opt) {
+  TAttnArgs a{};
+  int Tmax = 0;
+  long long ktot = 0;
+  FX_TRY(tattn_setup(a, nvid, Qv, Tv, hd, nh, opt, Tmax, ktot));
+  const TAttnGeom g = tattn_geom(nvid, Qv, Tmax, hd, nh, false);
   FX_REQUIRE(ws || g.nsplit == 1, "attention over T: workspace required");
   FX_REQUIRE(g.lds <= 160 * 1024, "attention over T: LDS images too large");
   FX_REQUIRE(merge_lds(g) <= 160 * 1024, "attention over T: too many frames per video for the in-LDS merge");
-  TAttnArgs a{};
   a.q = q; a.ldq = ldq; a.k = k; a.ldk = ldk; a.v = v; a.ldv = ldv;
   a.out = o; a.ld_out = ldo; a.lse = lse; a.ws = ws;
-  a.Qv = Qv; a.Tv = Tv; a.hd = hd; a.nh = nh; a.Qp = g.Qp; a.Hp = g.Hp; a.Tc = g.Tc; a.nsplit = g.nsplit;
+  a.Qp = g.Qp; a.Hp = g.Hp; a.Tc = g.Tc; a.nsplit = g.nsplit;
   a.scale = scale;
   a.vec = (hd % 4 == 0) && a16(q, ldq) && a16(k, ldk) && a16(v, ldv);
-  // algorithmic traffic: K and V rows read once, q read, o and lse written
-  const double kv = (double)nvid * Tv * nh * hd, qo = (double)nvid * Qv * nh * hd;
-  a.cnt = g.nsplit > 1 && merge_in_launch() ? arrival_counters(s) : nullptr;
+  // algorithmic traffic: K and V rows read once per query block, q read, o and lse written
+  const int nqb = (Qv + QB - 1) / QB;
+  const double kv = (double)ktot * nh * hd * nqb, qo = (double)nvid * Qv * nh * hd;
   prof_begin(1, s);
-  hipLaunchKernelGGL(tattn_fwd_kernel, dim3(g.nsplit, nh, nvid), dim3(AT), std::max(g.lds, merge_lds(g) + 16), s, a);
-  FX_CHECK_HIP(hipGetLastError());
-  if (g.nsplit > 1 && !a.cnt) {
-    hipLaunchKernelGGL(tattn_merge_kernel, dim3(nh, nvid), dim3(AT), merge_lds(g), s, a, 1, 1.f);
+  for (int q0 = 0; q0 < Qv; q0 += QB) {
+    a.q0 = q0;
+    a.Qv = std::min(QB, Qv - q0);
+    hipLaunchKernelGGL(tattn_fwd_kernel, dim3(g.nsplit, nh, nvid), dim3(AT), std::max(g.lds, merge_lds(g) + 16), s,
+                       a);
     FX_CHECK_HIP(hipGetLastError());
+    if (g.nsplit > 1) {
+      hipLaunchKernelGGL(tattn_merge_kernel, dim3(nh, nvid), dim3(AT), merge_lds(g), s, a, 1, 1.f);
+      FX_CHECK_HIP(hipGetLastError());
+    }
   }
-  prof_end(1, s, 4.0 * qo * Tv, 4.0 * (2.0 * kv + 2.0 * qo + (double)nvid * nh * Qv));
+  prof_end(1, s, 4.0 * qo * (double)ktot / nvid, 4.0 * (2.0 * kv + 2.0 * qo + (double)nvid * nh * Qv));
   return FX_OK;
 }
 
 int launch_tattn_bwd(const float* q, long long ldq, const float* k, long long ldk, const float* v, long long ldv,
                      const float* o, long long ldo, const float* dout, long long lddo, const float* lse, int nvid,
                      int Qv, int Tv, int hd, int nh, float scale, float* dq, long long lddq, float* dk, long long lddk,
-                     float* dv, long long lddv, float* ws, hipStream_t s) {
-  FX_TRY(tattn_check(nvid, Qv, Tv, hd, nh));
-  const TAttnGeom g = tattn_geom(nvid, Qv, Tv, hd, nh, true);
+                     float* dv, long long lddv, float* ws, hipStream_t s, const TAttnOpts* opt) {
+  TAttnArgs a{};
+  int Tmax = 0;
+  long long ktot = 0;
+  FX_TRY(tattn_setup(a, nvid, Qv, Tv, hd, nh, opt, Tmax, ktot));
+  const TAttnGeom g = tattn_geom(nvid, Qv, Tmax, hd, nh, true);
   FX_REQUIRE(ws || g.nsplit == 1, "attention over T: workspace required");
   FX_REQUIRE(g.lds <= 160 * 1024, "attention over T: LDS images too large");
   FX_REQUIRE(dq && dk && dv, "attention over T backward: dq, dk, dv required");
-  TAttnArgs a{};
   a.q = q; a.ldq = ldq; a.k = k; a.ldk = ldk; a.v = v; a.ldv = ldv;
   a.o = o; a.ldo = ldo; a.dout = dout; a.lddo = lddo;
   a.out = dq; a.ld_out = lddq; a.dk = dk; a.lddk = lddk; a.dv = dv; a.lddv = lddv;
   a.lse = const_cast<float*>(lse); a.ws = ws;
-  a.Qv = Qv; a.Tv = Tv; a.hd = hd; a.nh = nh; a.Qp = g.Qp; a.Hp = g.Hp; a.Tc = g.Tc; a.nsplit = g.nsplit;
+  a.Qp = g.Qp; a.Hp = g.Hp; a.Tc = g.Tc; a.nsplit = g.nsplit;
   a.scale = scale;
   a.vec = (hd % 4 == 0) && a16(q, ldq) && a16(k, ldk) && a16(v, ldv) && a16(o, ldo) && a16(dout, lddo);
-  // algorithmic traffic: K, V read and dK, dV written once; q, o, dout, lse read, dq written.
+  // algorithmic traffic: K, V read and dK, dV written once per query block; q, o, dout, lse read, dq written.
   // flops: S = qK^T recomputed, dP = dO V^T, dV = P^T dO, dK = dS^T q, dq = dS K
-  const double kv = (double)nvid * Tv * nh * hd, qo = (double)nvid * Qv * nh * hd;
-  a.cnt = g.nsplit > 1 && merge_in_launch() ? arrival_counters(s) : nullptr;
+  const int nqb = (Qv + QB - 1) / QB;
+  const double kv = (double)ktot * nh * hd * nqb, qo = (double)nvid * Qv * nh * hd;
   prof_begin(2, s);
-  hipLaunchKernelGGL(tattn_bwd_kernel, dim3(g.nsplit, nh, nvid), dim3(AT), std::max(g.lds, merge_lds(g) + 16), s, a);
-  FX_CHECK_HIP(hipGetLastError());
-  if (g.nsplit > 1 && !a.cnt) {
-    hipLaunchKernelGGL(tattn_merge_kernel, dim3(nh, nvid), dim3(AT), 0, s, a, 0, scale);
+  // query blocks one after another: a later block ADDS its dK / dV to the earlier blocks' (same key rows)
+  for (int q0 = 0; q0 < Qv; q0 += QB) {
+    a.q0 = q0;
+    a.Qv = std::min(QB, Qv - q0);
+    a.acc_kv = (q0 > 0) || (opt && opt->acc_kv);
+    hipLaunchKernelGGL(tattn_bwd_kernel, dim3(g.nsplit, nh, nvid), dim3(AT), std::max(g.lds, merge_lds(g) + 16), s,
+                       a);
     FX_CHECK_HIP(hipGetLastError());
+    if (g.nsplit > 1) {
+      hipLaunchKernelGGL(tattn_merge_kernel, dim3(nh, nvid), dim3(AT), 0, s, a, 0, scale);
+      FX_CHECK_HIP(hipGetLastError());
+    }
   }
-  prof_end(2, s, 10.0 * qo * Tv, 4.0 * (4.0 * kv + 4.0 * qo + (double)nvid * nh * Qv));
+  prof_end(2, s, 10.0 * qo * (double)ktot / nvid, 4.0 * (4.0 * kv + 4.0 * qo + (double)nvid * nh * Qv));
   return FX_OK;
 }
 

@@ -24,6 +24,7 @@ namespace fx {
 namespace {
 
 constexpr int MAXL = 16;
+constexpr int kSmallTok = 64;   // tokens per video the fused small-MHA kernel holds in LDS
 
 struct PackKV {
   const float* src[2 * MAXL];   // k_w[0..L-1], v_w[0..L-1]   (A x Hm each)
@@ -118,7 +119,8 @@ struct DecLayout {
   // workspace (fwd)
   long long wkv, bkv, wsp, total_ws_fwd;
   // workspace (bwd)
-  long long dkv, dwkv, dbkv, dT, dS, dU, dF, dQKV, dO, dq, G, P, lnws, core, split, gdu, gdf, gdq, gdqkv, total_ws_bwd;
+  long long dkv, dwkv, dbkv, dT, dS, dU, dF, dQKV, dO, dq, G, P, lnws, core, dmask, split, gdu, gdf, gdq, gdqkv,
+      total_ws_bwd;
 };
 
 long long dec_split_ws(const fx_decoder_params* p, int R, int T) {
@@ -148,10 +150,27 @@ long long dec_split_ws(const fx_decoder_params* p, int R, int T) {
   return sp;
 }
 
+// frames of the longest video (ragged memory: mem_off; else T / nvid each)
+int dec_tmax(const fx_decoder_params* p, int T, int nvid) {
+  if (!p->cross) return 0;
+  if (!p->mem_off) return T / nvid;
+  int m = 0;
+  for (int v = 0; v < nvid; ++v) m = std::max(m, p->mem_off[v + 1] - p->mem_off[v]);
+  return m;
+}
+
+// the attention-core workspace: cross attention over the frames, self attention over > 64 tokens
+long long dec_attn_ws(const fx_decoder_params* p, int nvid, int Qv, int Tv) {
+  const int hd = p->A / p->nhead;
+  long long w = p->cross ? tattn_ws_floats(nvid, Qv, Tv, hd, p->nhead) : 0;
+  if (Qv > kSmallTok) w = std::max(w, tattn_ws_floats(nvid, Qv, Qv, hd, p->nhead));
+  return w;
+}
+
 DecLayout dec_layout(const fx_decoder_params* p, int R, int T, int has_qpos, int has_mpos, int nvid) {
   DecLayout L{};
   const long long A = p->A, FF = p->FF, h = p->nhead, RA = (long long)R * A;
-  const long long Qv = R / nvid, Tv = T / nvid;   // tokens / frames per video
+  const long long Qv = R / nvid, Tv = dec_tmax(p, T, nvid);   // tokens / frames (longest video) per video
   long long o = 0;
   L.xq = o; o += has_qpos ? RA : 0;
   L.qkv = o; o += 3 * RA;
@@ -188,7 +207,8 @@ DecLayout dec_layout(const fx_decoder_params* p, int R, int T, int has_qpos, int
   o = 0;
   L.wkv = o; o += p->cross ? AL2 * p->Hm : 0;
   L.bkv = o; o += p->cross ? AL2 : 0;
-  L.wsp = o; o += std::max(sp, p->cross ? tattn_ws_floats(nvid, (int)Qv, (int)Tv, (int)(A / h), (int)h) : 0LL) + RA;
+  const long long att = dec_attn_ws(p, nvid, (int)Qv, (int)Tv);
+  L.wsp = o; o += std::max(sp, att) + RA;
   L.total_ws_fwd = o;
   // backward workspace
   o = 0;
@@ -205,7 +225,8 @@ DecLayout dec_layout(const fx_decoder_params* p, int R, int T, int has_qpos, int
   L.G = o; o += RA;
   L.P = o; o += RA;
   L.lnws = o; o += layernorm_bwd_ws_floats(R, (int)A);
-  L.core = o; o += p->cross ? tattn_ws_floats(nvid, (int)Qv, (int)Tv, (int)(A / h), (int)h) : 0;
+  L.core = o; o += att;
+  L.dmask = o; o += (p->dropout > 0.f) ? RA : 0;   // masked branch gradient (training dropout)
   L.split = o; o += sp;
   // every layer's output gradients of its token linears, kept for the weight-gradient GEMMs that run
   // after the chain (side stream): dU of the three LayerNorms, dF, dq, dQKV
@@ -220,16 +241,41 @@ DecLayout dec_layout(const fx_decoder_params* p, int R, int T, int has_qpos, int
 
 int dec_check(const fx_decoder_params* p, int R, int T, int nvid) {
   FX_REQUIRE(p && p->num_layers >= 1 && p->num_layers <= MAXL, "decoder: 1..16 layers");
-  FX_REQUIRE(nvid >= 1 && R % nvid == 0 && (!p->cross || T % nvid == 0),
-             "decoder: token and memory rows must split evenly over the videos");
+  FX_REQUIRE(nvid >= 1 && nvid <= 32 && R % nvid == 0, "decoder: 1..32 videos, token rows split evenly");
+  if (p->cross) {
+    if (p->mem_off) {
+      FX_REQUIRE(p->mem_off[0] == 0 && p->mem_off[nvid] == T, "decoder: memory offsets must span [0, T]");
+      for (int v = 0; v < nvid; ++v) FX_REQUIRE(p->mem_off[v + 1] > p->mem_off[v], "decoder: empty video memory");
+    } else {
+      FX_REQUIRE(T % nvid == 0 && T >= nvid, "decoder: memory rows must split evenly over the videos");
+    }
+    FX_REQUIRE(p->Hm > 0, "decoder: cross attention needs memory rows");
+  }
   R /= nvid;
-  T /= nvid;
   FX_REQUIRE(p->nhead > 0 && p->A % p->nhead == 0, "decoder: A must be divisible by nhead");
-  FX_REQUIRE(R >= 1 && R <= 64, "decoder: 1..64 tokens per video (fused self-attention core)");
+  FX_REQUIRE(R >= 1, "decoder: >= 1 token per video");
   FX_REQUIRE(p->A / p->nhead <= 64, "decoder: head dim must be <= 64");
   FX_REQUIRE(p->A <= 1024, "decoder: A <= 1024 (LayerNorm row kernel)");
-  FX_REQUIRE(!p->cross || (T >= 1 && p->Hm > 0), "decoder: cross attention needs memory rows");
+  FX_REQUIRE(p->dropout >= 0.f && p->dropout < 1.f && p->attn_dropout >= 0.f && p->attn_dropout < 1.f,
+             "decoder: dropout p in [0, 1)");
   return FX_OK;
+}
+
+// dropout site s of layer l (0 self-attn probs, 1 its residual branch, 2 cross-attn probs, 3 its residual
+// branch, 4 FFN hidden, 5 FFN residual branch)
+unsigned long long dec_seed(const fx_decoder_params* p, int l, int site) { return fx_drop_subseed(p->seed, 8 * l + site); }
+
+// y = drop(x . w^T + b) + resid  (w (N, K) row stride ldw); p_drop 0: no mask
+int linear_fwd_res_drop(const float* x, long long ldx, int M, int K, const float* w, long long ldw, const float* b,
+                        const float* resid, long long ldr, float* y, long long ldy, int N, float p_drop,
+                        unsigned long long seed, hipStream_t s) {
+  fx_gemm_desc d = gemm_desc(M, N, K, op_rows(x, ldx), op_rows(w, ldw), y, ldy);
+  d.bias = b;
+  d.resid = resid;
+  d.ld_resid = ldr;
+  d.drop_p = p_drop;
+  d.drop_seed = seed;
+  return launch_gemm(d, s);
 }
 
 }  // namespace
@@ -253,11 +299,12 @@ int fx_decoder_fwd(const fx_decoder_params* p, const float* tgt, long long ldt, 
                    long long ldqp, const float* mem, long long ldm, int T, int nvid, const float* mpos, long long ldmp,
                    float* out, long long ldo, float* saved, float* workspace, void* stream) {
   FX_TRY(dec_check(p, R, T, nvid));
-  const int Qv = R / nvid, Tv = T / nvid;
+  const int Qv = R / nvid, Tv = dec_tmax(p, T, nvid);
   hipStream_t s = (hipStream_t)stream;
   const int A = p->A, FF = p->FF, h = p->nhead, hd = A / h, NL = p->num_layers;
   const long long RA = (long long)R * A;
   const float eps = p->eps > 0.f ? p->eps : 1e-5f;
+  const float pd = p->dropout, pa = p->attn_dropout;
   const float scale = 1.0f / std::sqrt((float)hd);
   const DecLayout L = dec_layout(p, R, T, qpos != nullptr, mpos != nullptr, nvid);
   FX_REQUIRE(!qpos || ldqp == A, "decoder: query_pos must be dense (R, A)");
@@ -314,11 +361,20 @@ int fx_decoder_fwd(const fx_decoder_params* p, const float* tgt, long long ldt, 
       FX_TRY(linear_fwd(x, ldx, R, A, p->sa_in_w[l] + 2LL * A * A, p->sa_in_b[l] + 2 * A, qkv + 2 * A, 3 * A, A, 0,
                         s));
     }
-    FX_TRY(launch_mha_small_fwd(qkv, 3 * A, qkv + A, 3 * A, qkv + 2 * A, 3 * A, Qv, Qv, hd, h, scale, b + L.psa,
-                                b + L.osa, A, s, nvid));
-    // t1 = LN(x + out_proj(o))
+    if (Qv <= kSmallTok) {
+      FX_TRY(launch_mha_small_fwd(qkv, 3 * A, qkv + A, 3 * A, qkv + 2 * A, 3 * A, Qv, Qv, hd, h, scale, b + L.psa,
+                                  b + L.osa, A, s, nvid, pa, dec_seed(p, l, 0)));
+    } else {   // more tokens than the LDS-resident kernel holds: the attention-over-T kernels, lse kept in psa
+      TAttnOpts o;
+      o.drop_p = pa;
+      o.drop_seed = dec_seed(p, l, 0);
+      FX_TRY(launch_tattn_fwd(qkv, 3 * A, qkv + A, 3 * A, qkv + 2 * A, 3 * A, nvid, Qv, Qv, hd, h, scale, b + L.osa, A,
+                              b + L.psa, spl, s, &o));
+    }
+    // t1 = LN(x + dropout1(out_proj(o)))
     float* u = spl + (std::max(L.total_ws_fwd - L.wsp, RA) - RA);   // last RA floats of the scratch
-    FX_TRY(linear_fwd_res(b + L.osa, A, R, A, p->sa_out_w[l], A, p->sa_out_b[l], x, ldx, u, A, A, s));
+    FX_TRY(linear_fwd_res_drop(b + L.osa, A, R, A, p->sa_out_w[l], A, p->sa_out_b[l], x, ldx, u, A, A, pd,
+                               dec_seed(p, l, 1), s));
     FX_TRY(launch_layernorm_fwd(u, A, nullptr, 0, p->ln_sa_w[l], p->ln_sa_b[l], eps, R, A, 0, b + L.t1, A, nullptr,
                                 b + L.rs1, b + L.xh1, A, s));
     const float* t2 = b + L.t1;
@@ -331,16 +387,31 @@ int fx_decoder_fwd(const fx_decoder_params* p, const float* tgt, long long ldt, 
       }
       FX_TRY(linear_fwd(tq, A, R, A, p->ca_q_w[l], p->ca_in_b[l], b + L.qc, A, A, 0, s));
       // every video's tokens over its own frames, all heads, one fused launch (attn_t.hip)
+      TAttnOpts o;
+      o.koff = p->mem_off;
+      o.drop_p = pa;
+      o.drop_seed = dec_seed(p, l, 2);
       FX_TRY(launch_tattn_fwd(b + L.qc, A, kv + (long long)l * A, AL2, kv + (long long)(NL + l) * A, AL2, nvid, Qv, Tv,
-                              hd, h, scale, b + L.oca, A, b + L.pca, spl, s));
-      FX_TRY(linear_fwd_res(b + L.oca, A, R, A, p->ca_out_w[l], A, p->ca_out_b[l], b + L.t1, A, u, A, A, s));
+                              hd, h, scale, b + L.oca, A, b + L.pca, spl, s, &o));
+      FX_TRY(linear_fwd_res_drop(b + L.oca, A, R, A, p->ca_out_w[l], A, p->ca_out_b[l], b + L.t1, A, u, A, A, pd,
+                                 dec_seed(p, l, 3), s));
       FX_TRY(launch_layernorm_fwd(u, A, nullptr, 0, p->ln_ca_w[l], p->ln_ca_b[l], eps, R, A, 0, b + L.t2, A,
                                   nullptr, b + L.rs2, b + L.xh2, A, s));
       t2 = b + L.t2;
     }
     // --- FFN: t3 = LN(t2 + W2 relu(W1 t2 + b1) + b2)   (basic.py:516-522 / 446-450)
-    FX_TRY(linear_fwd(t2, A, R, A, p->ff1_w[l], p->ff1_b[l], b + L.f1, FF, FF, 1, s));
-    FX_TRY(linear_fwd_res(b + L.f1, FF, R, FF, p->ff2_w[l], FF, p->ff2_b[l], t2, A, u, A, A, s));
+    if (pd > 0.f) {   // f1 = dropout(relu(W1 t2 + b1)) (the saved f1 is the dropped activation)
+      fx_gemm_desc d = gemm_desc(R, FF, A, op_rows(t2, A), op_rows(p->ff1_w[l], A), b + L.f1, FF);
+      d.bias = p->ff1_b[l];
+      d.relu = 2;
+      d.drop_p = pd;
+      d.drop_seed = dec_seed(p, l, 4);
+      FX_TRY(launch_gemm(d, s));
+    } else {
+      FX_TRY(linear_fwd(t2, A, R, A, p->ff1_w[l], p->ff1_b[l], b + L.f1, FF, FF, 1, s));
+    }
+    FX_TRY(linear_fwd_res_drop(b + L.f1, FF, R, FF, p->ff2_w[l], FF, p->ff2_b[l], t2, A, u, A, A, pd,
+                               dec_seed(p, l, 5), s));
     FX_TRY(launch_layernorm_fwd(u, A, nullptr, 0, p->ln_ff_w[l], p->ln_ff_b[l], eps, R, A, 0, b + L.t3, A, nullptr,
                                 b + L.rs3, b + L.xh3, A, s));
     x = b + L.t3;
@@ -361,11 +432,12 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
                    float* dmem, long long lddm, float* dmpos, long long lddmp, const float* saved, float* workspace,
                    void* stream) {
   FX_TRY(dec_check(p, R, T, nvid));
-  const int Qv = R / nvid, Tv = T / nvid;
+  const int Qv = R / nvid, Tv = dec_tmax(p, T, nvid);
   hipStream_t s = (hipStream_t)stream;
   const int A = p->A, FF = p->FF, h = p->nhead, hd = A / h, NL = p->num_layers;
   const long long RA = (long long)R * A;
   const float scale = 1.0f / std::sqrt((float)hd);
+  const float pd = p->dropout, pa = p->attn_dropout;
   const DecLayout L = dec_layout(p, R, T, qpos != nullptr, mpos != nullptr, nvid);
   const int AL2 = 2 * A * NL;
   float* ws = workspace;
@@ -400,46 +472,74 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
     float* dF = ws + L.gdf + (long long)l * R * FF;
     float* dq = ws + L.gdq + (long long)l * RA;
     float* dQKV = ws + L.gdqkv + (long long)l * 3 * RA;
-    // --- FFN + its LayerNorm:  dU = LN_bwd(dT) ; dF = (dU W2) * (f1 > 0) ; dT2 = dU + dF W1
-    FX_TRY(launch_layernorm_bwd(dT, A, nullptr, 0, b + L.xh3, A, p->ln_ff_w[l], b + L.rs3, R, A, 0, dU, A,
+    // --- FFN + its LayerNorm:  dR = LN_bwd(dT) ; dU = dR * mask5 ; dF = (dU W2) * (f1 > 0) / (1 - p4) ;
+    //     dT2 = dR + dF W1.  Without dropout dR and dU are the same buffer.
+    float* dR = pd > 0.f ? ws + L.dmask : dU;   // residual-path gradient (un-masked)
+    auto branch_mask = [&](float* du, int site) -> int {   // dU = dR * keep / (1 - p) of the site's mask
+      if (pd <= 0.f) return FX_OK;
+      return launch_dropout(dR, A, R, A, A, 0, pd, dec_seed(p, l, site), du, A, s);
+    };
+    FX_TRY(launch_layernorm_bwd(dT, A, nullptr, 0, b + L.xh3, A, p->ln_ff_w[l], b + L.rs3, R, A, 0, dR, A,
                                 g->ln_ff_w[l], g->ln_ff_b[l], lnws, s));
-    FX_TRY(launch_gemm(desc_linear_dx(dU, A, p->ff2_w[l], R, FF, A, dF, FF, 0, b + L.f1, FF, spl), s));
-    FX_TRY(launch_gemm(dx_res_desc(dF, FF, p->ff1_w[l], A, R, A, FF, dU, A, dT, A, spl), s));   // dT <- dT2
+    FX_TRY(branch_mask(dU, 5));
+    {
+      fx_gemm_desc d = desc_linear_dx(dU, A, p->ff2_w[l], R, FF, A, dF, FF, 0, b + L.f1, FF, spl);
+      if (pd > 0.f) d.alpha = 1.f / (1.f - pd);   // f1 > 0 <=> kept and active: the gate is relu' * mask
+      FX_TRY(launch_gemm(d, s));
+    }
+    FX_TRY(launch_gemm(dx_res_desc(dF, FF, p->ff1_w[l], A, R, A, FF, dR, A, dT, A, spl), s));   // dT2 = dR + dF W1
     if (p->cross) {
       // --- cross-attention + LN2
       dU = slot_u(1, l);
-      FX_TRY(launch_layernorm_bwd(dT, A, nullptr, 0, b + L.xh2, A, p->ln_ca_w[l], b + L.rs2, R, A, 0, dU, A,
+      if (pd <= 0.f) dR = dU;
+      FX_TRY(launch_layernorm_bwd(dT, A, nullptr, 0, b + L.xh2, A, p->ln_ca_w[l], b + L.rs2, R, A, 0, dR, A,
                                   g->ln_ca_w[l], g->ln_ca_b[l], lnws, s));
+      FX_TRY(branch_mask(dU, 3));
       FX_TRY(launch_gemm(desc_linear_dx(dU, A, p->ca_out_w[l], R, A, A, dO, A, 0, nullptr, 0, spl), s));
       const float* kv = saved + L.kv;
+      TAttnOpts o;
+      o.koff = p->mem_off;
+      o.drop_p = pa;
+      o.drop_seed = dec_seed(p, l, 2);
       FX_TRY(launch_tattn_bwd(b + L.qc, A, kv + (long long)l * A, AL2, kv + (long long)(NL + l) * A, AL2, b + L.oca, A,
                               dO, A, b + L.pca, nvid, Qv, Tv, hd, h, scale, dq, A, dkv + (long long)l * A, AL2,
-                              dkv + (long long)(NL + l) * A, AL2, ws + L.core, s));
+                              dkv + (long long)(NL + l) * A, AL2, ws + L.core, s, &o));
       if (qpos) {
         FX_TRY(launch_gemm(desc_linear_dx(dq, A, p->ca_q_w[l], R, A, A, P, A, 0, nullptr, 0, spl), s));
-        FX_TRY(add_acc(dU, P, dT, G, RA, s));                                     // dT1 = dU + P ; G += P
+        FX_TRY(add_acc(dR, P, dT, G, RA, s));                                     // dT1 = dR + P ; G += P
       } else {
-        FX_TRY(launch_gemm(dx_res_desc(dq, A, p->ca_q_w[l], A, R, A, A, dU, A, dT, A, spl), s));
+        FX_TRY(launch_gemm(dx_res_desc(dq, A, p->ca_q_w[l], A, R, A, A, dR, A, dT, A, spl), s));
       }
     }
     // --- self-attention + LN1
     dU = slot_u(2, l);
-    FX_TRY(launch_layernorm_bwd(dT, A, nullptr, 0, b + L.xh1, A, p->ln_sa_w[l], b + L.rs1, R, A, 0, dU, A,
+    if (pd <= 0.f) dR = dU;
+    FX_TRY(launch_layernorm_bwd(dT, A, nullptr, 0, b + L.xh1, A, p->ln_sa_w[l], b + L.rs1, R, A, 0, dR, A,
                                 g->ln_sa_w[l], g->ln_sa_b[l], lnws, s));
+    FX_TRY(branch_mask(dU, 1));
     FX_TRY(launch_gemm(desc_linear_dx(dU, A, p->sa_out_w[l], R, A, A, dO, A, 0, nullptr, 0, spl), s));
     const float* qkv = b + L.qkv;
-    FX_TRY(launch_mha_small_bwd(qkv, 3 * A, qkv + A, 3 * A, qkv + 2 * A, 3 * A, b + L.psa, dO, A, Qv, Qv, hd, h, scale,
-                                dQKV, 3 * A, dQKV + A, 3 * A, dQKV + 2 * A, 3 * A, s, nvid));
+    if (Qv <= kSmallTok) {
+      FX_TRY(launch_mha_small_bwd(qkv, 3 * A, qkv + A, 3 * A, qkv + 2 * A, 3 * A, b + L.psa, dO, A, Qv, Qv, hd, h,
+                                  scale, dQKV, 3 * A, dQKV + A, 3 * A, dQKV + 2 * A, 3 * A, s, nvid, pa,
+                                  dec_seed(p, l, 0)));
+    } else {
+      TAttnOpts o;
+      o.drop_p = pa;
+      o.drop_seed = dec_seed(p, l, 0);
+      FX_TRY(launch_tattn_bwd(qkv, 3 * A, qkv + A, 3 * A, qkv + 2 * A, 3 * A, b + L.osa, A, dO, A, b + L.psa, nvid, Qv,
+                              Qv, hd, h, scale, dQKV, 3 * A, dQKV + A, 3 * A, dQKV + 2 * A, 3 * A, ws + L.core, s, &o));
+    }
     float* dX = l == 0 ? nullptr : dT;   // the next (earlier) layer's output gradient, in place
     if (!qpos) {
       if (l > 0 || dtgt)
-        FX_TRY(launch_gemm(dx_res_desc(dQKV, 3 * A, p->sa_in_w[l], A, R, A, 3 * A, dU, A, l > 0 ? dX : dtgt,
+        FX_TRY(launch_gemm(dx_res_desc(dQKV, 3 * A, p->sa_in_w[l], A, R, A, 3 * A, dR, A, l > 0 ? dX : dtgt,
                                        l > 0 ? A : lddt, spl), s));
     } else {
-      // P = dq W_q + dk W_k  (the position path);  dX = dU + dv W_v + P ; G += P
+      // P = dq W_q + dk W_k  (the position path);  dX = dR + dv W_v + P ; G += P
       FX_TRY(linear_dx(dQKV, 3 * A, p->sa_in_w[l], R, A, 2 * A, P, A, 0, nullptr, 0, spl, s));
       if (l > 0 || dtgt) {
-        FX_TRY(linear_dx_res(dQKV + 2 * A, 3 * A, p->sa_in_w[l] + 2LL * A * A, A, R, A, A, dU, A, dS, A, spl, s));
+        FX_TRY(linear_dx_res(dQKV + 2 * A, 3 * A, p->sa_in_w[l] + 2LL * A * A, A, R, A, A, dR, A, dS, A, spl, s));
         if (l > 0) {
           FX_TRY(add_acc(dS, P, dX, G, RA, s));
         } else {

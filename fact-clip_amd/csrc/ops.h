@@ -76,28 +76,39 @@ fx_gemm_desc desc_linear_dwdb(const float* dy, long long lddy, const float* x, l
 int linear_bwd_pair(const fx_gemm_desc& dwdb, const fx_gemm_desc& dx, hipStream_t s);
 
 // ---- fused small multi-head attention (attn_small.hip): Lq, Lk, head_dim <= 64 ----
+// drop_p > 0: attention-probability dropout with attn_t.hip's mask (TAttnOpts), probs saved un-dropped
 // nvid independent problems stacked by rows (video v: q/o rows v*Lq.., k/v rows v*Lk..);
 // probs (nvid, nhead, Lq, Lk) saved; o (Lq, nhead*hd) with row stride ldo.
 int launch_mha_small_fwd(const float* q, long long ldq, const float* k, long long ldk, const float* v,
                          long long ldv, int Lq, int Lk, int hd, int nhead, float scale, float* probs, float* o,
-                         long long ldo, hipStream_t s, int nvid = 1);
+                         long long ldo, hipStream_t s, int nvid = 1, float drop_p = 0.f,
+                         unsigned long long seed = 0);
 // dq, dk, dv written (nullable) with their row strides
 int launch_mha_small_bwd(const float* q, long long ldq, const float* k, long long ldk, const float* v,
                          long long ldv, const float* probs, const float* dout, long long lddo, int Lq, int Lk, int hd,
                          int nhead, float scale, float* dq, long long lddq, float* dk, long long lddk, float* dv,
-                         long long lddv, hipStream_t s, int nvid = 1);
+                         long long lddv, hipStream_t s, int nvid = 1, float drop_p = 0.f, unsigned long long seed = 0);
 
-// ---- fused multi-head attention of <= 64 queries over T frames (attn_t.hip) ----------------
-// nvid videos stacked by rows (queries v*Qv.., keys/values v*Tv..); head h = columns [h*hd, h*hd+hd)
-// of q/k/v/o.  fwd writes o and lse (nvid, nhead, Qv); bwd writes dq, dk, dv (dk/dv rows: one per key).
+// ---- fused multi-head attention of queries over T frames (attn_t.hip) ---------------------
+// nvid videos stacked by rows (queries v*Qv.., keys/values v*Tv.. or opt->koff); head h = columns
+// [h*hd, h*hd+hd) of q/k/v/o.  fwd writes o and lse (nvid, nhead, Qv); bwd writes (or with acc_kv adds)
+// dk, dv (rows: one per key) and writes dq.  More than 64 queries run as blocks of 64.
+struct TAttnOpts {
+  const int* koff = nullptr;        // host (nvid + 1) key-row offsets of ragged videos; Tv = the longest
+  float drop_p = 0.f;               // attention-probability dropout (training)
+  unsigned long long drop_seed = 0; // mask of probability (query row qg, head h, key row kg):
+                                    // fx_drop_bits(seed, (qg * nhead + h) * total_key_rows + kg)
+  int acc_kv = 0;                   // bwd: dk / dv += instead of =
+};
 long long tattn_ws_floats(int nvid, int Qv, int Tv, int hd, int nhead);
 int launch_tattn_fwd(const float* q, long long ldq, const float* k, long long ldk, const float* v, long long ldv,
                      int nvid, int Qv, int Tv, int hd, int nhead, float scale, float* o, long long ldo, float* lse,
-                     float* ws, hipStream_t s);
+                     float* ws, hipStream_t s, const TAttnOpts* opt = nullptr);
 int launch_tattn_bwd(const float* q, long long ldq, const float* k, long long ldk, const float* v, long long ldv,
                      const float* o, long long ldo, const float* dout, long long lddo, const float* lse, int nvid,
                      int Qv, int Tv, int hd, int nhead, float scale, float* dq, long long lddq, float* dk,
-                     long long lddk, float* dv, long long lddv, float* ws, hipStream_t s);
+                     long long lddk, float* dv, long long lddv, float* ws, hipStream_t s,
+                     const TAttnOpts* opt = nullptr);
 
 // fused MS-TCN layer step (mstcn_fused.hip): conv GEMM (K = 3F) -> row-local epilogue -> 1x1 GEMM
 bool frl_supported(int F, const void* x, long long ldx, long long ld_other);

@@ -182,13 +182,16 @@ __device__ __forceinline__ float attn_target(const fx_loss_term& t, int r, int i
 }
 
 __device__ void attn_fwd(const fx_loss_term& t, int lane, int gw, int r0, int r1, float& xe, float& sm) {
-  if (t.axis == 1) {
+  if (t.axis == 1) {   // log_softmax over the K matched columns of each row (K may exceed a wave)
     for (int r = r0; r < r1; ++r) {
-      const float v = lane < t.K ? at(t, r, t.ka[lane]) : -INFINITY;
-      const float m = vmax(v);
-      const float l = m + __logf(vsum(lane < t.K ? __expf(v - m) : 0.f));
+      float m = -INFINITY;
+      for (int i = lane; i < t.K; i += 64) m = fmaxf(m, at(t, r, t.ka[i]));
+      m = vmax(m);
+      float se = 0.f;
+      for (int i = lane; i < t.K; i += 64) se += __expf(at(t, r, t.ka[i]) - m);
+      const float l = m + __logf(vsum(se));
       if (lane == 0) t.lse[r] = l;
-      xe += lane < t.K ? -(v - l) * attn_target(t, r, lane) * t.ksw[lane] : 0.f;
+      for (int i = lane; i < t.K; i += 64) xe += -(at(t, r, t.ka[i]) - l) * attn_target(t, r, i) * t.ksw[i];
     }
   } else if (gw < t.K) {   // one wave per matched column: log_softmax over the rows
     const int i = gw, q = t.ka[i];
@@ -281,7 +284,10 @@ __device__ void attn_bwd(const fx_loss_term& t, int lane, int r0, int r1, float 
       for (int c = lane; c < t.C; c += 64) gsum += smooth_g(t, r, c, l0, lm, lp1, t.R) * g_sm;
     gsum = vsum(gsum);
     float zrow = 0.f;
-    if (t.axis == 1) zrow = vsum(lane < t.K ? attn_target(t, r, lane) * t.ksw[lane] : 0.f);
+    if (t.axis == 1) {
+      for (int i = lane; i < t.K; i += 64) zrow += attn_target(t, r, i) * t.ksw[i];
+      zrow = vsum(zrow);
+    }
     for (int c = lane; c < t.C; c += 64) {
       float g = 0.f;
       if (smooth) g = smooth_g(t, r, c, l0, lm, lp1, t.R) * g_sm - __expf(at(t, r, c) - l0) * gsum;
@@ -609,8 +615,9 @@ int fx_loss_terms_fwd(const fx_loss_term* terms_host, const fx_loss_term* terms_
     const fx_loss_term& t = terms_host[i];
     FX_REQUIRE(t.kind >= 0 && t.kind <= 2, "loss_terms: unknown term kind");
     FX_REQUIRE(t.R > 0 && t.C > 0 && t.x && t.lse, "loss_terms: empty term");
-    FX_REQUIRE(t.kind != FX_TERM_ATTN || (t.K >= 0 && t.K <= FX_LOSS_MAXK && t.lse2 && t.colz),
-               "loss_terms: attention term needs K <= 64 matched columns and scratch");
+    FX_REQUIRE(t.kind != FX_TERM_ATTN || (t.K >= 0 && t.K <= FX_LOSS_MAXK && t.lse2 && t.colz &&
+                                          (t.K == 0 || (t.ka && t.kgs && t.kge && t.ksw))),
+               "loss_terms: attention term needs K <= FX_LOSS_MAXK matched columns, their tables and scratch");
     FX_REQUIRE(t.kind != FX_TERM_CLASS || t.w, "loss_terms: class term needs weights");
     FX_REQUIRE(t.kind != FX_TERM_INFONCE || (t.y && t.lse2 && t.colz && t.emb && t.text && t.dx && t.sc == 1 &&
                                              t.dsc == 1 && t.D > 0),

@@ -1154,7 +1154,14 @@ class DecoderFn(torch.autograd.Function):
     per direction (fx_decoder_fwd / fx_decoder_bwd)."""
 
     @staticmethod
-    def forward(ctx, tgt, qpos, mem, mpos, spec, nvid, *params):
+    def _set_call(prm, call):
+        """Per-call fields (dropout p's and seed, ragged memory offsets) of the cached param struct."""
+        pd, pa, seed, mem_off = call
+        prm.dropout, prm.attn_dropout, prm.seed = pd, pa, seed
+        prm.mem_off = None if mem_off is None else ctypes.cast(mem_off, ctypes.c_void_p)
+
+    @staticmethod
+    def forward(ctx, tgt, qpos, mem, mpos, spec, nvid, call, *params):
         lib = nx.load()
         meta, slots, gl, cache = spec
         prm = cache.get("prm")
@@ -1164,6 +1171,8 @@ class DecoderFn(torch.autograd.Function):
             keep = []
             _fill_decoder_struct(prm, slots, gl, params, keep)
             cache.update(prm=prm, key=key, keep=keep)
+        DecoderFn._set_call(prm, call)
+        ctx.call = call
         R = tgt.shape[0]
         T = mem.shape[0] if mem is not None else 0
         hq, hm = int(qpos is not None), int(mpos is not None)
@@ -1189,7 +1198,7 @@ class DecoderFn(torch.autograd.Function):
         dev = dout.device
         dout = dout.contiguous()
         R = tgt.shape[0]
-        tg = [grad_target(p, nd[6 + i]) for i, p in enumerate(params)]
+        tg = [grad_target(p, nd[7 + i]) for i, p in enumerate(params)]
         bufs = [t[0] for t in tg]
         gkey = tuple(0 if b is None else b.data_ptr() for b in bufs)
         g = cache.get("grads")
@@ -1199,6 +1208,7 @@ class DecoderFn(torch.autograd.Function):
             _fill_decoder_struct(g, slots, gl, bufs, keep)
             cache.update(grads=g, gkey=gkey, gkeep=keep)
         prm = cache["prm"]
+        DecoderFn._set_call(prm, ctx.call)        # the module may have run again since this forward
         A = meta["A"]
         dtgt = _empty(R, A, device=dev) if nd[0] else None
         dqpos = _empty(R, A, device=dev) if (hq and nd[1]) else None
@@ -1216,12 +1226,14 @@ class DecoderFn(torch.autograd.Function):
                                   nx.ld(dmpos), nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_decoder_bwd")
         if defer:
             _defer_to_side(tgt, mem, mpos, saved, ws)
-        return (dtgt, dqpos, dmem, dmpos, None, None) + tuple(t[1] for t in tg)
+        return (dtgt, dqpos, dmem, dmpos, None, None, None) + tuple(t[1] for t in tg)
 
 
-def decoder(mod, tgt, memory=None, pos=None, query_pos=None, nvid=1):
+def decoder(mod, tgt, memory=None, pos=None, query_pos=None, nvid=1, mem_off=None):
     """Run an SCADecoder (memory given) or SADecoder through DecoderFn; returns (R, out_dim).
-    ``nvid`` videos stacked by rows (tokens and memory frames split evenly)."""
+    ``nvid`` videos stacked by rows: tokens split evenly, memory frames evenly or by the host prefix
+    list ``mem_off`` (ragged videos).  In training the layers' dropout runs inside the kernels
+    (counter-based masks from one drawn seed)."""
     spec = getattr(mod, "_fx_spec", None)
     if spec is None:
         meta, params, slots, gl = _decoder_slots(mod)
@@ -1233,7 +1245,11 @@ def decoder(mod, tgt, memory=None, pos=None, query_pos=None, nvid=1):
     qp = None if query_pos is None else _2d(query_pos).contiguous()
     mem = None if memory is None else _2d(memory)
     mp = None if pos is None else _2d(pos)
-    return DecoderFn.apply(t2, qp, mem, mp, spec, int(nvid), *params)
+    from .models.basic import decoder_dropout
+    pd, pa = decoder_dropout(mod) if mod.training else (0.0, 0.0)
+    seed = dropout_seed() if (pd > 0 or pa > 0) else 0
+    off = None if (mem_off is None or memory is None) else nx.int_array(mem_off)
+    return DecoderFn.apply(t2, qp, mem, mp, spec, int(nvid), (float(pd), float(pa), seed, off), *params)
 
 
 # ---------------------------------------------------------------------------

@@ -344,17 +344,30 @@ class SCALayer(nn.Module):
         return _as3d(fxf.layer_norm(t2, self.norm3.weight, self.norm3.bias, self.norm3.eps, residual=t))
 
 
+def decoder_dropout(dec):
+    """(branch p, attention p) of a decoder's layers: the residual-branch / FFN-hidden nn.Dropout p and
+    the MultiheadAttention probability dropout (basic.py:398-412, 457-478: every layer is a clone of one
+    layer, so one value each); None when the layers disagree."""
+    br, at = set(), set()
+    for lyr in dec.layers:
+        br.update(float(m.p) for m in lyr.modules() if isinstance(m, nn.Dropout))
+        at.add(float(lyr.multihead_attn.dropout))
+        if hasattr(lyr, "self_attn"):
+            at.add(float(lyr.self_attn.dropout))
+    if len(br) > 1 or len(at) > 1:
+        return None
+    return (br.pop() if br else 0.0), (at.pop() if at else 0.0)
+
+
 def _fused_decoder_ok(dec):
-    """The whole-decoder kernel path (fx_decoder_*) runs eval-mode dropout and the default layer
-    options; training with non-zero dropout, sa/ca value positions or pre-norm takes the per-layer
-    path (still HIP kernels)."""
+    """The whole-decoder kernel path (fx_decoder_*) covers the layer options the reference builds
+    (post-norm, values without positions), any token count and training dropout; other options take
+    the per-layer path (still HIP kernels)."""
     if len(dec.layers) == 0 or len(dec.layers) > 16:
         return False
+    if decoder_dropout(dec) is None:
+        return False
     for lyr in dec.layers:
-        drops = [m.p for m in lyr.modules() if isinstance(m, nn.Dropout)]
-        attn = [lyr.multihead_attn.dropout] + ([lyr.self_attn.dropout] if hasattr(lyr, "self_attn") else [])
-        if dec.training and any(p > 0 for p in drops + attn):
-            return False
         if getattr(lyr, "sa_value_w_pos", False) or getattr(lyr, "ca_value_w_pos", False) or \
                 getattr(lyr, "use_vpos", False) or getattr(lyr, "normalize_before", False):
             return False

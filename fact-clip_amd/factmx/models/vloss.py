@@ -102,14 +102,13 @@ def segment_weights(mc, transcript):
 
 def supported(net):
     """The fused phase covers FACT / FACT_CLIP without transcripts whose last block has token->frame
-    attention (every reference config: the matching reads it) and <= 64 tokens."""
+    attention (every reference config: the matching reads it); a video whose matching pairs more
+    than FX_LOSS_MAXK columns fails loudly in run()."""
     from .blocks import UpdateBlock, UpdateBlockTDU
     mc = getattr(net, "mcriterion", None)
     if mc is None or net.cfg.FACT.trans or net.cfg.Loss.match not in ("o2o", "o2m", "seq"):
         return False
-    if not isinstance(net.block_list[-1], (UpdateBlock, UpdateBlockTDU)):
-        return False
-    return net.cfg.FACT.ntoken <= nx.LOSS_MAXK
+    return isinstance(net.block_list[-1], (UpdateBlock, UpdateBlockTDU))
 
 
 def _ptr_rows(t, row0, ld):
@@ -312,7 +311,12 @@ def run(net, vb, compute_loss, early=None):
         K = len(ai)
         if len(swn) not in (K, 1):
             raise RuntimeError(f"cross_attn_loss: {K} matched columns vs {len(swn)} segment weights")
-        sw_list.append([float(swn[i if len(swn) == K else 0]) for i in range(K)])
+        if K > nx.LOSS_MAXK:
+            raise nx.FactmxNativeError(f"video {v}: {K} matched token/segment pairs > FX_LOSS_MAXK "
+                                       f"({nx.LOSS_MAXK}) of the fused loss table")
+        ksw = np.asarray([float(swn[i if len(swn) == K else 0]) for i in range(K)], dtype=np.float32)
+        sw_list.append((pk2.array(ai, np.int32), pk2.array(gts[v][0][si], np.int32),
+                        pk2.array(gts[v][1][si], np.int32), pk2.array(ksw, np.float32)))
     ycon_off = [pk2.array(y, np.int32) if y is not None and con_on[v] else None for v, y in enumerate(y_con)]
 
     inputs, grads, gidx = [], [], {}
@@ -355,8 +359,7 @@ def run(net, vb, compute_loss, early=None):
                 continue
             ai, si = matches[v]
             K = len(ai)
-            kgs = gts[v][0][si]
-            kge = gts[v][1][si]
+            ka_o, kgs_o, kge_o, ksw_o = sw_list[v]
             if is_tdu:
                 Sv, s0 = bt["S"][v], bt["s_off"][v]
                 st, en = bt["local"][v][1], bt["local"][v][2]
@@ -372,8 +375,8 @@ def run(net, vb, compute_loss, early=None):
                 c_xe, c_sm = 1.0 / T, (sw_coef / ((T - 1) * Q) if sw_coef and T > 1 else 0.0)
             f2a, a2f = bt["f2a_lg"], bt["a2f_lg"]
             gfa, gaf = grad_of(f2a), grad_of(a2f)
-            common = dict(kind=nx.TERM_ATTN, R=R, C=Q, rs=ivs[0], re=ivs[1], K=K, ka=ai, kgs=kgs, kge=kge,
-                          ksw=sw_list[v], c_ce=c_xe, c_sm=c_sm)
+            common = dict(kind=nx.TERM_ATTN, R=R, C=Q, rs=ivs[0], re=ivs[1], K=K, ka=("p2", ka_o),
+                          kgs=("p2", kgs_o), kge=("p2", kge_o), ksw=("p2", ksw_o), c_ce=c_xe, c_sm=c_sm)
             # f2a logits (Q, R) read as (R, Q): log_softmax over rows per matched column (dim=1)
             add(k, v, dict(common, x=f2a.data_ptr() + 4 * off, sr=1, sc=R, dx=gfa.data_ptr() + 4 * off, dsr=1,
                            dsc=R, axis=0), R, R + K, K)
@@ -424,9 +427,7 @@ def run(net, vb, compute_loss, early=None):
         t = terms[i]
         t.slot = i
         for name, val in f.items():
-            if name in ("ka", "kgs", "kge", "ksw"):
-                getattr(t, name)[:len(val)] = val.tolist() if isinstance(val, np.ndarray) else val
-            elif isinstance(val, tuple):
+            if isinstance(val, tuple):
                 setattr(t, name, bases[val[0]] + val[1])
             elif val is not None:
                 setattr(t, name, val)

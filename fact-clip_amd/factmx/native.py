@@ -74,7 +74,7 @@ DECODER_GLOBAL_FIELDS = ["fn_w", "fn_b", "out_w", "out_b"]
 class DecoderParams(ctypes.Structure):
     _fields_ = ([("A", I), ("FF", I), ("nhead", I), ("num_layers", I), ("cross", I), ("Hm", I), ("out_dim", I),
                  ("final_norm", I), ("eps", F)] + [(n, P) for n in _DEC_PTRS] + [(n, P) for n in DECODER_GLOBAL_FIELDS]
-                + [("side_defer", I)])
+                + [("side_defer", I), ("dropout", F), ("attn_dropout", F), ("seed", U), ("mem_off", P)])
 
 
 class DecoderGrads(ctypes.Structure):
@@ -82,7 +82,7 @@ class DecoderGrads(ctypes.Structure):
 
 
 STATUS_GRU_TIMEOUT = 1   # FX_STATUS_GRU_TIMEOUT: a BiGRU workgroup gave up waiting for a peer
-LOSS_MAXK = 64
+LOSS_MAXK = 512        # FX_LOSS_MAXK: matched columns of an attention loss term
 LOSS_NB = 128          # FX_LOSS_NB: row blocks per loss term
 TERM_CLASS, TERM_ATTN, TERM_INFONCE = 0, 1, 2
 PREC_F32, PREC_BF16 = 0, 1   # FX_PREC_*: GEMM arithmetic precision (fx_set_gemm_precision)
@@ -93,7 +93,7 @@ class LossTerm(ctypes.Structure):
                 ("dsc", L), ("y", P), ("rs", P), ("re", P), ("gs", P), ("ge", P), ("gl", P), ("G", I), ("axis", I),
                 ("K", I), ("D", I), ("w", P), ("c_ce", F), ("c_sm", F), ("inv_temp", F), ("pad0", F), ("lse", P),
                 ("lse2", P), ("colz", P), ("emb", P), ("ld_emb", L), ("text", P), ("demb", P), ("ld_demb", L),
-                ("ka", I * LOSS_MAXK), ("kgs", I * LOSS_MAXK), ("kge", I * LOSS_MAXK), ("ksw", F * LOSS_MAXK)]
+                ("ka", P), ("kgs", P), ("kge", P), ("ksw", P)]
 
 
 class VideoAttn(ctypes.Structure):

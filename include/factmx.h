@@ -182,7 +182,7 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
                int side_defer, void* stream);
 
 /* ------------------------------------------------------------------------
- * Action-token decoder, whole stack in one call (eval-mode dropout, post-norm, ReLU FFN):
+ * Action-token decoder, whole stack in one call (post-norm, ReLU FFN):
  *   cross = 1: SCADecoder (basic.py:525-557) of SCALayer (basic.py:454-523):
  *     per layer  t1 = LN_sa(x + SA(x+qpos, x+qpos, x))
  *                t2 = LN_ca(t1 + CA(t1+qpos, mem+mpos, mem))
@@ -190,13 +190,15 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
  *     then the optional final LayerNorm (SCADecoder.norm) and out_linear.
  *   cross = 0: SADecoder (basic.py:561-593) of SALayer (basic.py:391-452): the same
  *     without the CA stage (SALayer.norm1 -> ln_sa, norm2 -> ln_ff).
+ * Any number of tokens per video (more than 64: the self-attention runs on the attention-over-T
+ * kernels in query blocks of 64); training dropout per fx_decoder_params.dropout / attn_dropout.
  * SA/CA = nn.MultiheadAttention math with nhead heads (head dim A/nhead <= 64); the
  * self-attention in-projection is the packed (3A, A) in_proj_weight, the cross one
  * separate q (A,A), k (A,Hm), v (A,Hm) weights with the packed (3A) in_proj_bias.
  * Shapes: tgt (R, A) ld, qpos (R, A) dense or NULL, mem (T, Hm) ld, mpos (T, Hm) or
  * NULL, out (R, out_dim).  nvid videos stacked by rows: video v owns token rows
- * [v*R/nvid, (v+1)*R/nvid) and memory rows [v*T/nvid, (v+1)*T/nvid); attention never
- * crosses videos, every projection runs over all rows at once.  R/nvid <= 64.
+ * [v*R/nvid, (v+1)*R/nvid) and memory rows [v*T/nvid, (v+1)*T/nvid) (or mem_off); attention
+ * never crosses videos, every projection runs over all rows at once.
  * bwd: every weight gradient ACCUMULATES (+=) into g; dtgt, dqpos (dense (R,A)),
  * dmem, dmpos are written (each nullable).
  * ---------------------------------------------------------------------- */
@@ -218,6 +220,16 @@ typedef struct fx_decoder_params {
   int side_defer;             /* bwd: leave the weight-gradient GEMMs (token linears of every layer, and
                                  the frame-memory K/V projection when cross) running on the library's
                                  side stream (joined by fx_side_join), as fx_mstcn_params */
+  float dropout;              /* training: nn.Dropout p of the residual branches (dropout1/2/3) and the
+                                 FFN hidden layer (basic.py:444-449, 504-522); 0 = eval */
+  float attn_dropout;         /* training: attention-probability dropout (MultiheadAttention dropout) */
+  unsigned long long seed;    /* dropout site s of layer l: fx_dropout seed fx_drop_subseed(seed, 8 l + s),
+                                 s = 0 self-attn probs, 1 its residual branch, 2 cross-attn probs,
+                                 3 its residual branch, 4 FFN hidden, 5 FFN residual branch; branch masks
+                                 index r * A + c (FFN hidden r * FF + c); probability masks index
+                                 (query_row * nhead + head) * key_rows_total + key_row */
+  const int* mem_off;         /* host (nvid + 1) frame-memory row offsets of ragged videos; NULL: video v
+                                 owns memory rows [v T/nvid, (v+1) T/nvid) */
 } fx_decoder_params;
 
 typedef struct fx_decoder_grads {
@@ -565,7 +577,7 @@ int fx_attn_loss_bwd(const float* L, long long sr, long long sc, int R, int Q, i
  *                   covers frames [rs[r], re[r]] (NULL: frame r) and z[r, gl[j]] is
  *                   its overlap with ground-truth segment j / its length
  *                   (frame_loss, frame_loss_tdu, action_token_loss, loss.py:195-277).
- *   FX_TERM_ATTN    c_ce * cross-attention CE of the K matched token columns ka
+ *   FX_TERM_ATTN    c_ce * cross-attention CE of the K (<= FX_LOSS_MAXK) matched token columns ka
  *                   (axis 1: log_softmax over them per row, axis 0: over the rows of
  *                   each), targets = overlap(row frames, [kgs[i], kge[i]]) / row
  *                   length, column weights ksw; + c_sm * smooth over all C columns
@@ -579,8 +591,8 @@ int fx_attn_loss_bwd(const float* L, long long sr, long long sc, int R, int Q, i
  * bwd: gout (nout) upstream gradient of out; every term's dx (and demb) written whole.
  * ---------------------------------------------------------------------- */
 enum { FX_TERM_CLASS = 0, FX_TERM_ATTN = 1, FX_TERM_INFONCE = 2 };
-#define FX_LOSS_MAXK 64
 #define FX_LOSS_NB 128          /* row blocks per term */
+#define FX_LOSS_MAXK 512        /* matched columns of an attention term (one wave each on axis 0) */
 
 typedef struct fx_loss_term {
   int kind, slot, R, C;
@@ -596,8 +608,8 @@ typedef struct fx_loss_term {
   const float* emb; long long ld_emb;
   const float* text;
   float* demb; long long ld_demb;
-  int32_t ka[FX_LOSS_MAXK]; int32_t kgs[FX_LOSS_MAXK]; int32_t kge[FX_LOSS_MAXK];
-  float ksw[FX_LOSS_MAXK];
+  const int32_t* ka; const int32_t* kgs; const int32_t* kge;   /* device (K): matched token columns and their */
+  const float* ksw;                                            /* ground-truth segments [kgs, kge], weights */
 } fx_loss_term;
 
 long long fx_loss_terms_workspace_floats(int nterms);
