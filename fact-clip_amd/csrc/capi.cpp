@@ -396,14 +396,50 @@ bool mstcn_defer_ok(const fx_mstcn_params* p, const fx_mstcn_grads* g) {
   return uniform(g->w_dil) && uniform(g->b_dil) && uniform(g->w_pw) && uniform(g->b_pw);
 }
 
-fx_operand conv_operand(const float* h, long long ld, int cin, int dil, int dir, int T, bool trans) {
+// The videos of a frame-level call: nvid of T rows each, or ragged host offsets off (nvid + 1).
+struct Seqs {
+  int T, nvid;
+  const int* off;
+  int rows() const { return off ? off[nvid] : T * nvid; }
+  int start(int v) const { return off ? off[v] : v * T; }
+  int len(int v) const { return off ? off[v + 1] - off[v] : T; }
+};
+
+int check_seqs(const Seqs& q) {
+  FX_REQUIRE(q.nvid >= 1, "frame branch: nvid >= 1");
+  if (!q.off) {
+    FX_REQUIRE(q.T >= 1, "frame branch: T >= 1");
+    return FX_OK;
+  }
+  FX_REQUIRE(q.nvid <= 16 && q.off[0] == 0, "frame branch: ragged offsets start at 0, <= 16 videos");
+  for (int v = 0; v < q.nvid; ++v) FX_REQUIRE(q.off[v + 1] > q.off[v], "frame branch: empty video");
+  return FX_OK;
+}
+
+// dilated-conv operand over the call's videos (zero outside each video).  The column-major (weight-
+// gradient) form needs uniform videos: ragged calls run their weight gradients video by video.
+fx_operand conv_operand(const float* h, long long ld, int cin, int dil, int dir, const Seqs& q, bool trans) {
   fx_operand o = trans ? op_cols(h, ld) : op_rows(h, ld);
   o.conv_taps = 3;
   o.conv_cin = cin;
   o.conv_dil = dil;
   o.conv_dir = dir;
-  o.seq_len = T;
+  if (q.off && !trans) {
+    o.seq_off = q.off;
+    o.nseq = q.nvid;
+  } else {
+    o.seq_len = q.T;
+  }
   return o;
+}
+
+// fn(row0, rows, seqs) once over all rows (uniform videos) or once per video (ragged): the weight-
+// gradient GEMMs whose K runs over frames
+template <typename Fn>
+int per_video(const Seqs& q, Fn fn) {
+  if (!q.off) return fn(0, q.rows(), q);
+  for (int v = 0; v < q.nvid; ++v) FX_TRY(fn(q.start(v), q.len(v), Seqs{q.len(v), 1, nullptr}));
+  return FX_OK;
 }
 
 }  // namespace
@@ -497,7 +533,9 @@ int fx_mstcn_fwd(const fx_mstcn_params* p, const float* x, long long ldx, int T,
   hipStream_t s = (hipStream_t)stream;
   FX_REQUIRE(p && p->num_layers >= 0 && p->num_layers <= 32, "mstcn: 0..32 layers");
   FX_REQUIRE(p->in_map || p->cin == p->F, "mstcn: in_map=0 needs cin == F");
-  const int rows = T * nvid;
+  const Seqs q{T, nvid, p->seq_off};
+  FX_TRY(check_seqs(q));
+  const int rows = q.rows();
   const int F = p->F;
   const MstcnLayout L = mstcn_layout(p, rows);
   FX_TRY(pack_conv_weights(p, workspace, saved + L.wbs, saved + L.wpts, L, s));
@@ -508,7 +546,7 @@ int fx_mstcn_fwd(const fx_mstcn_params* p, const float* x, long long ldx, int T,
     FX_CHECK_HIP(hipMemcpy2DAsync(h0, F * sizeof(float), x, ldx * sizeof(float), F * sizeof(float), rows,
                                   hipMemcpyDeviceToDevice, s));
   }
-  const bool fused = !p->layernorm && frl_supported(F, saved, F, F);
+  const bool fused = !p->layernorm && !q.off && frl_supported(F, saved, F, F);
   for (int i = 0; i < p->num_layers; ++i) {
     const float* hi = saved + L.h + i * L.rowsF;
     float* hn = saved + L.h + (i + 1) * L.rowsF;
@@ -522,7 +560,7 @@ int fx_mstcn_fwd(const fx_mstcn_params* p, const float* x, long long ldx, int T,
       continue;
     }
     // z = relu(dilated_conv(h) + b)      (basic.py:158)
-    fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(hi, F, F, layer_dilation(p, i), 1, T, false),
+    fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(hi, F, F, layer_dilation(p, i), 1, q, false),
                                op_rows(workspace + L.wf + (long long)i * 3 * F * F, 3 * F), zi, F);
     d.bias = p->b_dil[i];
     d.relu = 1;
@@ -550,15 +588,17 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
                  const float* dy, long long lddy, float* dx, long long lddx, const float* saved, float* workspace,
                  void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  const int rows = T * nvid;
+  const Seqs q{T, nvid, p->seq_off};
+  FX_TRY(check_seqs(q));
+  const int rows = q.rows();
   const int F = p->F;
   const int NL = p->num_layers;
   const MstcnLayout L = mstcn_layout(p, rows);
   float* ws = workspace;
   FX_REQUIRE(p->dropout >= 0.f && p->dropout < 1.f, "mstcn: dropout must be in [0, 1)");
   const bool drop = p->dropout > 0.f;
-  // Fused chain (no LayerNorm, no dropout, FX_MSTCN_FUSED=1): see below
-  const bool fchain = !p->layernorm && !drop && NL > 0 && frl_supported(F, ws + L.buf0, F, F);
+  // Fused chain (no LayerNorm, no dropout, uniform videos, FX_MSTCN_FUSED=1): see below
+  const bool fchain = !p->layernorm && !drop && !q.off && NL > 0 && frl_supported(F, ws + L.buf0, F, F);
   // the dX-packed conv weights come from the forward (saved); the fused chain also needs the
   // transposed 1x1 weights (repacked here, into the workspace)
   if (fchain) FX_TRY(pack_conv_weights(p, ws, ws + L.wb, ws + L.wpt, L, s));
@@ -622,15 +662,18 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   // Zb[(NL - 1 - i) % 3]; a kernel overwriting a buffer first waits for the side stream's layer
   // that last read it (layer i + 2 for both).
   auto conv_dw = [&](int i, const float* dZi) -> int {
-    fx_operand b = conv_operand(saved + L.h + i * L.rowsF, F, F, layer_dilation(p, i), 1, T, true);
-    b.ones_col = 3 * F + 1;
-    fx_gemm_desc d = gemm_desc(F, 3 * F + 1, rows, op_cols(dZi, F), b, g->w_dil[i], 3 * F);
-    d.c_tap_cin = F;
-    d.c_last_col = g->b_dil[i];
-    d.beta = 1.f;
-    d.split_k = pick_split(F, 3 * F + 1, rows);
-    d.workspace = spl;
-    return launch_gemm(d, sd);
+    return per_video(q, [&](int r0, int nr, const Seqs& qv) -> int {
+      fx_operand b = conv_operand(saved + L.h + i * L.rowsF + (long long)r0 * F, F, F, layer_dilation(p, i), 1, qv,
+                                  true);
+      b.ones_col = 3 * F + 1;
+      fx_gemm_desc d = gemm_desc(F, 3 * F + 1, nr, op_cols(dZi + (long long)r0 * F, F), b, g->w_dil[i], 3 * F);
+      d.c_tap_cin = F;
+      d.c_last_col = g->b_dil[i];
+      d.beta = 1.f;
+      d.split_k = pick_split(F, 3 * F + 1, nr);
+      d.workspace = spl;
+      return launch_gemm(d, sd);
+    });
   };
   for (int i = NL - 1; fchain && i >= NL - 1; --i) {   // top layer: dZ by the 1x1 backward GEMM
     const float* zi = saved + L.z + i * L.rowsF;
@@ -647,7 +690,7 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
     float* dHi = Hb[(NL - i) % 3];
     FX_TRY(wait_side(i + 2));
     if (i == 0) {   // the bottom layer: conv backward only
-      fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dZi, F, F, layer_dilation(p, 0), -1, T, false),
+      fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dZi, F, F, layer_dilation(p, 0), -1, q, false),
                                  op_rows(ws + L.wb, 3 * F), dHi, F);
       d.resid = gU;
       d.ld_resid = F;
@@ -685,7 +728,7 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
       float* dZ = dZall + i * L.rowsF;
       FX_TRY(pw_dx(gU, i, dZ, zi));
       float* dHn = i > 0 ? dHall + (i - 1) * L.rowsF : Hb[0];
-      fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dZ, F, F, layer_dilation(p, i), -1, T, false),
+      fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dZ, F, F, layer_dilation(p, i), -1, q, false),
                                  op_rows(wbp + (long long)i * 3 * F * F, 3 * F), dHn, F);
       d.resid = gU;
       d.ld_resid = F;
@@ -712,28 +755,30 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
       WsBound wbb(ws + L.bsl, L.total_ws - L.bsl);
       FX_TRY(launch_gemm(d, sd));
     }
-    {   // dilated conv: dW_i += dZ_i^T taps(h_i) stored straight into (F, F, 3)   (batched over layers)
-      fx_operand b = conv_operand(saved + L.h, F, F, layer_dilation(p, 0), 1, T, true);
-      b.batch_stride = L.rowsF;
-      fx_operand a = op_cols(dZall, F);
-      a.batch_stride = L.rowsF;
-      fx_gemm_desc d = gemm_desc(F, 3 * F, rows, a, b, g->w_dil[0], 3 * F);
-      d.batch = NL;
-      d.c_batch_stride = NL > 1 ? g->w_dil[1] - g->w_dil[0] : 0;
-      d.b_dil_growth = p->dil_factor > 0 ? p->dil_factor : 2;
-      d.c_tap_cin = F;
-      d.beta = 1.f;
-      d.split_k = defer_split_impl(rows);
-      d.workspace = ws + L.bsl;
+    {   // dilated conv: dW_i += dZ_i^T taps(h_i) stored straight into (F, F, 3)   (batched over layers;
+        // ragged videos: one such launch per video, accumulating)
       WsBound wbb(ws + L.bsl, L.total_ws - L.bsl);
-      FX_TRY(launch_gemm(d, sd));
+      FX_TRY(per_video(q, [&](int r0, int nr, const Seqs& qv) -> int {
+        fx_operand b = conv_operand(saved + L.h + (long long)r0 * F, F, F, layer_dilation(p, 0), 1, qv, true);
+        b.batch_stride = L.rowsF;
+        fx_operand a = op_cols(dZall + (long long)r0 * F, F);
+        a.batch_stride = L.rowsF;
+        fx_gemm_desc d = gemm_desc(F, 3 * F, nr, a, b, g->w_dil[0], 3 * F);
+        d.batch = NL;
+        d.c_batch_stride = NL > 1 ? g->w_dil[1] - g->w_dil[0] : 0;
+        d.b_dil_growth = p->dil_factor > 0 ? p->dil_factor : 2;
+        d.c_tap_cin = F;
+        d.beta = 1.f;
+        d.split_k = defer_split_impl(nr);
+        d.workspace = ws + L.bsl;
+        return launch_gemm(d, sd);
+      }));
       FX_TRY(launch_colsum_batched(dZall, F, L.rowsF, rows, F, NL, g->b_dil[0],
                                    NL > 1 ? g->b_dil[1] - g->b_dil[0] : 0, 1, ws + L.csb, sd));
     }
   }
   for (int i = NL - 1; !fchain && !defer && i >= 0; --i) {
     const int step = NL - 1 - i;
-    const float* hi = saved + L.h + i * L.rowsF;
     const float* zi = saved + L.z + i * L.rowsF;
     const float* gU = dH;
     if (p->layernorm) {
@@ -758,17 +803,7 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
     // conv: dW (tap-major columns stored straight into (F,F,3)) + db (ones column) (side),
     // dH_i = dU + conv^T(dZ) (main)
     FX_TRY(fork(2));
-    {
-      fx_operand b = conv_operand(hi, F, F, layer_dilation(p, i), 1, T, true);
-      b.ones_col = 3 * F + 1;
-      fx_gemm_desc d = gemm_desc(F, 3 * F + 1, rows, op_cols(dZ, F), b, g->w_dil[i], 3 * F);
-      d.c_tap_cin = F;
-      d.c_last_col = g->b_dil[i];
-      d.beta = 1.f;
-      d.split_k = pick_split(F, 3 * F + 1, rows);
-      d.workspace = spl;
-      FX_TRY(launch_gemm(d, sd));
-    }
+    FX_TRY(conv_dw(i, dZ));
     FX_TRY(side_done(i));
     {
       float* dHn;
@@ -778,7 +813,7 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
         dHn = Hb[(step + 1) % 3];
         FX_TRY(wait_side(i + 2));     // that buffer was gU of layer i + 2
       }
-      fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dZ, F, F, layer_dilation(p, i), -1, T, false),
+      fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dZ, F, F, layer_dilation(p, i), -1, q, false),
                                  op_rows(wbp + (long long)i * 3 * F * F, 3 * F), dHn, F);
       d.resid = gU;
       d.ld_resid = F;
@@ -901,8 +936,10 @@ int fx_mstcn2_fwd(const fx_mstcn2_params* p, const float* x, long long ldx, int 
   FX_REQUIRE(p && p->num_layers >= 0 && p->num_layers <= 32, "mstcn2: 0..32 layers");
   FX_REQUIRE(p->in_map || p->cin == p->F, "mstcn2: in_map=0 needs cin == F");
   FX_REQUIRE(p->dropout >= 0.f && p->dropout < 1.f, "mstcn2: dropout must be in [0, 1)");
-  FX_REQUIRE(T >= 1 && nvid >= 1 && saved && workspace && y, "mstcn2: bad arguments");
-  const int rows = T * nvid, F = p->F, NL = p->num_layers;
+  FX_REQUIRE(saved && workspace && y, "mstcn2: bad arguments");
+  const Seqs q{T, nvid, p->seq_off};
+  FX_TRY(check_seqs(q));
+  const int rows = q.rows(), F = p->F, NL = p->num_layers;
   const Mstcn2Layout L = mstcn2_layout(p, rows);
   float* ws = workspace;
   if (NL > 0) {   // forward images into the workspace, dX images into `saved` for the backward
@@ -926,7 +963,7 @@ int fx_mstcn2_fwd(const fx_mstcn2_params* p, const float* x, long long ldx, int 
     // (one batch-2 launch: batch h takes conv h's dilation, packed weights, bias and output half --
     // at Breakfast's 2048 rows the pair fills the chip with 128x64 tiles where one conv could not)
     {
-      fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(fi, F, F, mstcn2_dil(p, NL - 1 - i), 1, T, false),
+      fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(fi, F, F, mstcn2_dil(p, NL - 1 - i), 1, q, false),
                                  op_rows(ws + L.wf1 + (long long)i * 3 * F * F, 3 * F), cat, 2 * F);
       d.batch = 2;
       d.a_dil_b1 = mstcn2_dil(p, i);
@@ -957,7 +994,9 @@ int fx_mstcn2_bwd(const fx_mstcn2_params* p, const fx_mstcn2_grads* g, const flo
                   void* stream) {
   hipStream_t s = (hipStream_t)stream;
   FX_REQUIRE(p && g && saved && workspace && dy, "mstcn2 bwd: bad arguments");
-  const int rows = T * nvid, F = p->F, NL = p->num_layers;
+  const Seqs q{T, nvid, p->seq_off};
+  FX_TRY(check_seqs(q));
+  const int rows = q.rows(), F = p->F, NL = p->num_layers;
   const Mstcn2Layout L = mstcn2_layout(p, rows);
   float* ws = workspace;
   SideStream* ss = side_stream();
@@ -997,7 +1036,7 @@ int fx_mstcn2_bwd(const fx_mstcn2_params* p, const fx_mstcn2_grads* g, const flo
     float* dFn = Hb[(NL - i) & 1];
     for (int h = 0; h < 2; ++h) {
       const int dil = h == 0 ? mstcn2_dil(p, NL - 1 - i) : mstcn2_dil(p, i);
-      fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dCat + h * F, 2 * F, F, dil, -1, T, false),
+      fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dCat + h * F, 2 * F, F, dil, -1, q, false),
                                  op_rows(saved + (h == 0 ? L.wb1 : L.wb2) + (long long)i * 3 * F * F, 3 * F), dFn, F);
       if (h == 0) {
         d.resid = gF;
@@ -1043,25 +1082,27 @@ int fx_mstcn2_bwd(const fx_mstcn2_params* p, const fx_mstcn2_grads* g, const flo
         // the layer (batch b = layer i0 + b), conv_d1's shrinks: its batch b is layer NL-1-b (negative strides)
         const int il = (h == 0 && uni) ? NL - 1 : i0;
         const long long dir = (h == 0 && uni) ? -1 : 1;
-        fx_operand a = op_cols(ws + L.dcat + 2 * il * L.rowsF + h * F, 2 * F);
-        a.batch_stride = dir * 2 * L.rowsF;
         const int dil = h == 0 ? mstcn2_dil(p, NL - 1 - il) : mstcn2_dil(p, il);
-        fx_operand b = conv_operand(saved + L.f + il * L.rowsF, F, F, dil, 1, T, true);
-        b.batch_stride = dir * L.rowsF;
-        b.ones_col = 3 * F + 1;
         float* const* gw = h == 0 ? g->w_d1 : g->w_d2;
         float* const* gb = h == 0 ? g->b_d1 : g->b_d2;
-        fx_gemm_desc d = gemm_desc(F, 3 * F + 1, rows, a, b, gw[il], 3 * F);
-        d.batch = nb;
-        d.c_batch_stride = dir * st(gw);
-        d.c_last_col = gb[il];
-        d.c_last_batch_stride = dir * st(gb);
-        d.b_dil_growth = nb > 1 ? growth : 0;
-        d.c_tap_cin = F;
-        d.beta = 1.f;
-        d.split_k = pick_split(F, 3 * F + 1, rows, nb);
-        d.workspace = ws + L.bsl;
-        FX_TRY(launch_gemm(d, sd));
+        FX_TRY(per_video(q, [&](int r0, int nr, const Seqs& qv) -> int {
+          fx_operand a = op_cols(ws + L.dcat + 2 * il * L.rowsF + (long long)r0 * 2 * F + h * F, 2 * F);
+          a.batch_stride = dir * 2 * L.rowsF;
+          fx_operand b = conv_operand(saved + L.f + il * L.rowsF + (long long)r0 * F, F, F, dil, 1, qv, true);
+          b.batch_stride = dir * L.rowsF;
+          b.ones_col = 3 * F + 1;
+          fx_gemm_desc d = gemm_desc(F, 3 * F + 1, nr, a, b, gw[il], 3 * F);
+          d.batch = nb;
+          d.c_batch_stride = dir * st(gw);
+          d.c_last_col = gb[il];
+          d.c_last_batch_stride = dir * st(gb);
+          d.b_dil_growth = nb > 1 ? growth : 0;
+          d.c_tap_cin = F;
+          d.beta = 1.f;
+          d.split_k = pick_split(F, 3 * F + 1, nr, nb);
+          d.workspace = ws + L.bsl;
+          return launch_gemm(d, sd);
+        }));
       }
     }
   }
@@ -1718,16 +1759,18 @@ int fx_gru_bidir_bwd(const float* x, long long ldx, int S, int nseq, const int* 
 }
 
 // ---------------------------------------------------------------- segments
-int fx_segments_from_probs(const float* x, long long ldx, int col0, int ncls, int T, int nvid, int32_t* pred,
-                           int32_t* seg_id, int32_t* seg_start, int32_t* seg_end, int32_t* num_seg, void* stream) {
-  return launch_segments(x, ldx, col0, ncls, T, nvid, pred, seg_id, seg_start, seg_end, num_seg, (hipStream_t)stream);
+int fx_segments_from_probs(const float* x, long long ldx, int col0, int ncls, int T, int nvid, const int* row_off,
+                           int32_t* pred, int32_t* seg_id, int32_t* seg_start, int32_t* seg_end, int32_t* num_seg,
+                           void* stream) {
+  return launch_segments(x, ldx, col0, ncls, T, nvid, row_off, pred, seg_id, seg_start, seg_end, num_seg,
+                         (hipStream_t)stream);
 }
 
-int fx_segments_globalize(int nvid, int T, const int32_t* num_seg_host, const int32_t* seg_id,
+int fx_segments_globalize(int nvid, int T, const int* row_off, const int32_t* num_seg_host, const int32_t* seg_id,
                           const int32_t* seg_start, const int32_t* seg_end, int32_t* gseg_id, int32_t* gstart,
                           int32_t* gend, void* stream) {
-  FX_REQUIRE(nvid >= 1 && T > 0 && num_seg_host, "segments_globalize: bad arguments");
-  return launch_seg_globalize(nvid, T, num_seg_host, seg_id, seg_start, seg_end, gseg_id, gstart, gend,
+  FX_REQUIRE(nvid >= 1 && (T > 0 || row_off) && num_seg_host, "segments_globalize: bad arguments");
+  return launch_seg_globalize(nvid, T, row_off, num_seg_host, seg_id, seg_start, seg_end, gseg_id, gstart, gend,
                               (hipStream_t)stream);
 }
 

@@ -45,6 +45,8 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // ROWS_CAT: [src0[rows0[r]] | src1[rows1[r]]] split at k_split (a multiple of the 64-deep stage),
 //           either gather optional -- the FAST form of the concatenation / gather operands
+constexpr int kMaxSeq = 16;        // ragged videos per conv operand
+
 enum Kind { ROWS = 0, ROWS_CONV = 1, ROWS_GEN = 2, COLS = 3, COLS_CONV = 4, ROWS_CAT = 5 };
 
 struct GemmDev {
@@ -74,7 +76,35 @@ struct GemmDev {
   int a_dil_b1;         // > 0: A's conv dilation of batch 1 (two dilated convs of one input in one launch)
   long long bias_bs;    // bias of batch b at bias + b * bias_bs
   int nt_store;         // FX_GEMM_NTSTORE=1 (A/B): the fast epilogue stores non-temporally
+  int nsoff;            // > 0: the conv operand's videos are ragged: video v owns rows [soff[v], soff[v+1])
+  int soff[kMaxSeq + 1];
 };
+
+// Position of row r inside its video and the video's length (the conv operand's zero padding):
+// uniform videos of seq_len rows, or the ragged offsets soff (nsoff videos; read from the kernel
+// arguments, a branch-free count of the video starts at or before r).
+typedef int SeqOff[kMaxSeq + 1];
+
+__device__ __forceinline__ void seq_pos(int seq_len, const SeqOff& soff, int nsoff, int r, int& pos, int& len) {
+  if (nsoff > 0) {
+    // fully unrolled (constant indices: scalar loads from the kernel arguments, no private copy):
+    // start = the last offset <= r, end = the first offset > r (offsets increase)
+    int start = 0, end = 0x7fffffff;
+#pragma unroll
+    for (int i = 1; i <= kMaxSeq; ++i) {
+      if (i <= nsoff) {
+        const int o = soff[i];
+        if (o <= r) start = o;
+        else end = min(end, o);
+      }
+    }
+    pos = r - start;
+    len = end - start;
+  } else {
+    pos = r % seq_len;
+    len = seq_len;
+  }
+}
 
 // Diagnostic builds (-DFX_STAMPS) record s_memtime / s_memrealtime at fixed points of
 // every block; the shipped library compiles the macro to nothing.
@@ -114,11 +144,14 @@ __device__ __forceinline__ fx_operand batch_op_b(const fx_operand& b, int growth
 }
 
 // ---------------------------------------------------------------- generic element fetch
-__device__ __forceinline__ float fetch_rm(const fx_operand& o, const float* p0, int r, int k) {
+__device__ __forceinline__ float fetch_rm(const fx_operand& o, const float* p0, int r, int k, const SeqOff& soff,
+                                         int nsoff) {
   if (o.conv_taps) {
     const int j = k / o.conv_cin, c = k - j * o.conv_cin, s = conv_shift(o, j);
-    const int t = r % o.seq_len + s;
-    if (t < 0 || t >= o.seq_len) return 0.f;
+    int pos, len;
+    seq_pos(o.seq_len, soff, nsoff, r, pos, len);
+    const int t = pos + s;
+    if (t < 0 || t >= len) return 0.f;
     return p0[(long long)(r + s) * o.ld + c];
   }
   if (o.ptr1 && k >= o.k_split) {
@@ -133,7 +166,7 @@ __device__ __forceinline__ float fetch_rm(const fx_operand& o, const float* p0, 
 
 __device__ __forceinline__ float fetch_cm(const fx_operand& o, const float* p0, int r, int k) {
   if (o.ones_col && r == o.ones_col - 1) return 1.f;
-  if (o.conv_taps) {
+  if (o.conv_taps) {   // uniform videos only (ragged weight gradients run per video)
     const int j = r / o.conv_cin, c = r - j * o.conv_cin, s = conv_shift(o, j);
     const int t = k % o.seq_len + s;
     if (t < 0 || t >= o.seq_len) return 0.f;
@@ -167,7 +200,10 @@ struct Loader {
   int ta, tb;          // tid>>4, (tid&15)*4
   int rowc[4];         // row-major: clamped row of j (ROWS_CAT: gathered row of the first source)
   int rowc1[4];        // ROWS_CAT: gathered row of the second source
-  int rmod[4];         // ROWS_CONV: row % seq_len of j
+  int rmod[4];         // ROWS_CONV: position of row j in its video
+  int rlen[4];         // ROWS_CONV: that video's length
+  SeqOff soff;         // ragged conv videos: a register copy of GemmDev::soff (constant indices only; a
+  int nsoff;           // pointer into the kernel arguments would force them into private memory)
   unsigned rok;        // row-major: bit j = row j in range
   int rc;              // col-major: clamped first row of the 4
   unsigned emask, omask;   // col-major: bit e = row rc+e in storage / is the ones row
@@ -178,9 +214,15 @@ struct Loader {
   const float* prow1[4];   // ROWS_CAT: row j of the second source at k = tb
   const float* pcol;       // COLS: k = ta, first of the thread's 4 rows
 
-  __device__ __forceinline__ void init(const fx_operand& op, const float* p0, int r0_, int R_, int K_, int tid) {
+  __device__ __forceinline__ void init(const fx_operand& op, const float* p0, int r0_, int R_, int K_, int tid,
+                                       const SeqOff& soff_, int nsoff_) {
     o = op;
     base = p0;
+    nsoff = (KIND == ROWS_CONV || KIND == ROWS_GEN) ? nsoff_ : 0;
+    if (KIND == ROWS_GEN) {   // the generic element fetch (edge shapes) looks rows up per element
+#pragma unroll
+      for (int i = 0; i <= kMaxSeq; ++i) soff[i] = soff_[i];
+    }
     R = R_;
     K = K_;
     r0 = r0_;
@@ -194,7 +236,7 @@ struct Loader {
         const int r = r0 + ta + RSTEP * j;
         rok |= (r < R ? 1u : 0u) << j;
         rowc[j] = min(r, R - 1);
-        if (KIND == ROWS_CONV) rmod[j] = rowc[j] % op.seq_len;
+        if (KIND == ROWS_CONV) seq_pos(op.seq_len, soff_, nsoff_, rowc[j], rmod[j], rlen[j]);
         if (KIND == ROWS_CAT) {
           const int rr = rowc[j];
           rowc1[j] = op.rows1 ? op.rows1[rr] : rr;
@@ -248,7 +290,7 @@ struct Loader {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int t = rmod[j] + s;
-        const bool ok = ((rok >> j) & 1u) && t >= 0 && t < o.seq_len;
+        const bool ok = ((rok >> j) & 1u) && t >= 0 && t < rlen[j];
         vm |= (ok ? 1u : 0u) << j;
         v[j] = ldg4(prow[j] + c + (ok ? soff : 0ll));
       }
@@ -267,7 +309,8 @@ struct Loader {
       vm = 0;
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const int k = k0 + ta + RSTEP * j, t = k % o.seq_len + tap_s;
+        const int k = k0 + ta + RSTEP * j;
+        const int t = k % o.seq_len + tap_s;   // (uniform videos only: ragged weight gradients run per video)
         const bool ok = t >= 0 && t < o.seq_len;
         vm |= (ok ? 1u : 0u) << j;
         v[j] = ldg4(base + (long long)(ok ? k + tap_s : k) * o.ld + tapc);
@@ -284,7 +327,7 @@ struct Loader {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int k = k0 + tb + q;
-          e[q] = (r < R && k < K) ? fetch_rm(o, base, r, k) : 0.f;
+          e[q] = (r < R && k < K) ? fetch_rm(o, base, r, k, soff, nsoff) : 0.f;
         }
       } else {
         const int k = k0 + ta + RSTEP * j;
@@ -528,8 +571,8 @@ __global__ __launch_bounds__(NTHREADS) void gemm_f32_kernel(GemmDev g) {
 
   Loader<AK, FAST> la;
   Loader<BKIND, FAST> lb;
-  la.init(batch_op_a(g.a, g.a_dil_b1, bidx), g.a.ptr + (long long)bidx * g.a.batch_stride, m0, g.M, g.K, tid);
-  lb.init(batch_op_b(g.b, g.b_dil_growth, bidx), g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid);
+  la.init(batch_op_a(g.a, g.a_dil_b1, bidx), g.a.ptr + (long long)bidx * g.a.batch_stride, m0, g.M, g.K, tid, g.soff, g.nsoff);
+  lb.init(batch_op_b(g.b, g.b_dil_growth, bidx), g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid, g.soff, g.nsoff);
 
   f32x16 acc0, acc1;
 #pragma unroll
@@ -749,9 +792,9 @@ __global__ __launch_bounds__(NTHREADS) void gemm_f32_wide_kernel(GemmDev g) {
   Loader<AK, true> la0, la1;
   Loader<BKIND, true> lb;
   const float* pa = g.a.ptr + (long long)bidx * g.a.batch_stride;
-  la0.init(batch_op_a(g.a, g.a_dil_b1, bidx), pa, m0, g.M, g.K, tid);
-  la1.init(batch_op_a(g.a, g.a_dil_b1, bidx), pa, m0 + BM, g.M, g.K, tid);
-  lb.init(batch_op_b(g.b, g.b_dil_growth, bidx), g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid);
+  la0.init(batch_op_a(g.a, g.a_dil_b1, bidx), pa, m0, g.M, g.K, tid, g.soff, g.nsoff);
+  la1.init(batch_op_a(g.a, g.a_dil_b1, bidx), pa, m0 + BM, g.M, g.K, tid, g.soff, g.nsoff);
+  lb.init(batch_op_b(g.b, g.b_dil_growth, bidx), g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid, g.soff, g.nsoff);
   f32x16 acc0, acc1;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -888,9 +931,9 @@ __global__ __launch_bounds__(W8T) void gemm_f32_wide8_kernel(GemmDev g) {
   Loader<AK, true, 2> la0, la1;
   Loader<BKIND, true, 2> lb;
   const float* pa = g.a.ptr + (long long)bidx * g.a.batch_stride;
-  la0.init(batch_op_a(g.a, g.a_dil_b1, bidx), pa, m0, g.M, g.K, tid);
-  la1.init(batch_op_a(g.a, g.a_dil_b1, bidx), pa, m0 + BM, g.M, g.K, tid);
-  lb.init(batch_op_b(g.b, g.b_dil_growth, bidx), g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid);
+  la0.init(batch_op_a(g.a, g.a_dil_b1, bidx), pa, m0, g.M, g.K, tid, g.soff, g.nsoff);
+  la1.init(batch_op_a(g.a, g.a_dil_b1, bidx), pa, m0 + BM, g.M, g.K, tid, g.soff, g.nsoff);
+  lb.init(batch_op_b(g.b, g.b_dil_growth, bidx), g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid, g.soff, g.nsoff);
   f32x16 acc0, acc1;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -1014,9 +1057,9 @@ __global__ __launch_bounds__(W8T) void gemm_bf16_wide8_kernel(GemmDev g) {
   Loader<AK, true, 2> la0, la1;
   Loader<BKd, true, 2> lb;
   const float* pa = g.a.ptr + (long long)bidx * g.a.batch_stride;
-  la0.init(batch_op_a(g.a, g.a_dil_b1, bidx), pa, m0, g.M, g.K, tid);
-  la1.init(batch_op_a(g.a, g.a_dil_b1, bidx), pa, m0 + BM, g.M, g.K, tid);
-  lb.init(batch_op_b(g.b, g.b_dil_growth, bidx), g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid);
+  la0.init(batch_op_a(g.a, g.a_dil_b1, bidx), pa, m0, g.M, g.K, tid, g.soff, g.nsoff);
+  la1.init(batch_op_a(g.a, g.a_dil_b1, bidx), pa, m0 + BM, g.M, g.K, tid, g.soff, g.nsoff);
+  lb.init(batch_op_b(g.b, g.b_dil_growth, bidx), g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid, g.soff, g.nsoff);
   f32x16 acc0, acc1;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -1146,7 +1189,7 @@ constexpr int DCH = 32, DMAXW = 8;
 
 template <int KIND>
 __device__ __forceinline__ void dload(const fx_operand& o, const float* base, int r, int R, int k0, int K, bool vec,
-                                      float* v) {
+                                      float* v, const SeqOff& soff, int nsoff) {
   if (KIND == ROWS) {
     if (vec && r < R && k0 + 16 <= K) {
       const float* p = base + (long long)r * o.ld + k0;
@@ -1176,7 +1219,7 @@ __device__ __forceinline__ void dload(const fx_operand& o, const float* base, in
     }
   } else {  // ROWS_GEN
 #pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = (r < R && k0 + j < K) ? fetch_rm(o, base, r, k0 + j) : 0.f;
+    for (int j = 0; j < 16; ++j) v[j] = (r < R && k0 + j < K) ? fetch_rm(o, base, r, k0 + j, soff, nsoff) : 0.f;
   }
 }
 
@@ -1207,21 +1250,21 @@ __device__ __forceinline__ void direct_body(const GemmDev& g, int bx, int by, in
   float a0[16], b0[16], a1[16], b1[16];
   int c = c0 + w;
   if (c < c1) {
-    dload<AK>(g.a, pa, ra, g.M, c * DCH + ko, g.K, av, a0);
-    dload<BKd>(g.b, pb, rb, g.N, c * DCH + ko, g.K, bv, b0);
+    dload<AK>(g.a, pa, ra, g.M, c * DCH + ko, g.K, av, a0, g.soff, g.nsoff);
+    dload<BKd>(g.b, pb, rb, g.N, c * DCH + ko, g.K, bv, b0, g.soff, g.nsoff);
   }
   for (; c < c1; c += 2 * nw) {
     const int cn = c + nw;
     if (cn < c1) {
-      dload<AK>(g.a, pa, ra, g.M, cn * DCH + ko, g.K, av, a1);
-      dload<BKd>(g.b, pb, rb, g.N, cn * DCH + ko, g.K, bv, b1);
+      dload<AK>(g.a, pa, ra, g.M, cn * DCH + ko, g.K, av, a1, g.soff, g.nsoff);
+      dload<BKd>(g.b, pb, rb, g.N, cn * DCH + ko, g.K, bv, b1, g.soff, g.nsoff);
     }
 #pragma unroll
     for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b0[s], acc, 0, 0, 0);
     const int cnn = cn + nw;
     if (cnn < c1) {
-      dload<AK>(g.a, pa, ra, g.M, cnn * DCH + ko, g.K, av, a0);
-      dload<BKd>(g.b, pb, rb, g.N, cnn * DCH + ko, g.K, bv, b0);
+      dload<AK>(g.a, pa, ra, g.M, cnn * DCH + ko, g.K, av, a0, g.soff, g.nsoff);
+      dload<BKd>(g.b, pb, rb, g.N, cnn * DCH + ko, g.K, bv, b0, g.soff, g.nsoff);
     }
     if (cn < c1) {
 #pragma unroll
@@ -1609,8 +1652,11 @@ struct GemmPlan {
 int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_cnt_base = 0) {
   FX_REQUIRE(d.M >= 0 && d.N >= 0 && d.K >= 0 && d.batch >= 1, "gemm: bad sizes");
   FX_REQUIRE(d.a.ptr && d.b.ptr && d.c, "gemm: null operand");
-  FX_REQUIRE(!(d.a.conv_taps && d.a.seq_len <= 0) && !(d.b.conv_taps && d.b.seq_len <= 0),
-             "gemm: conv operand needs seq_len");
+  FX_REQUIRE(!(d.a.conv_taps && d.a.seq_len <= 0 && d.a.nseq <= 0) &&
+                 !(d.b.conv_taps && d.b.seq_len <= 0 && d.b.nseq <= 0),
+             "gemm: conv operand needs seq_len or seq_off");
+  FX_REQUIRE(d.b.nseq <= 0 && (d.a.nseq <= 0 || !d.a.trans),
+             "gemm: ragged conv offsets only on a row-major A operand (weight gradients run per video)");
   FX_REQUIRE(!(d.a.conv_taps && d.K != d.a.conv_taps * d.a.conv_cin), "gemm: conv A needs K == taps*cin");
   FX_REQUIRE(!(d.b.conv_taps && d.b.trans && d.N != d.b.conv_taps * d.b.conv_cin + (d.b.ones_col ? 1 : 0)),
              "gemm: conv B needs N == taps*cin (+1 with a ones column)");
@@ -1623,6 +1669,19 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
   g.K = d.K;
   g.a = d.a;
   g.b = d.b;
+  {   // ragged conv videos: the offsets travel in the kernel arguments
+    const fx_operand& o = d.a;
+    if (o.nseq > 0) {
+      FX_REQUIRE(o.conv_taps && o.seq_off && o.nseq <= kMaxSeq, "gemm: seq_off needs a conv operand, <= 16 videos");
+      const int rows = d.M;
+      FX_REQUIRE(o.seq_off[0] == 0 && o.seq_off[o.nseq] == rows, "gemm: seq_off must span the operand's rows");
+      for (int v = 0; v <= o.nseq; ++v) {
+        FX_REQUIRE(v == 0 || o.seq_off[v] > o.seq_off[v - 1], "gemm: seq_off must increase");
+        g.soff[v] = o.seq_off[v];
+      }
+      g.nsoff = o.nseq;
+    }
+  }
   g.c = d.c;
   g.ldc = d.ldc;
   g.c_bs = d.c_batch_stride;

@@ -27,10 +27,13 @@ int launch_l2n_fwd(const float* x, long long ldx, int rows, int cols, float* y, 
                    hipStream_t s);
 int launch_l2n_bwd(const float* y, long long ldy, const float* nrm, const float* dy, long long lddy, int rows,
                    int cols, float* dx, long long lddx, hipStream_t s);
-int launch_segments(const float* x, long long ldx, int col0, int ncls, int T, int nvid, int32_t* pred,
-                    int32_t* seg_id, int32_t* seg_start, int32_t* seg_end, int32_t* num_seg, hipStream_t s);
-int launch_seg_globalize(int nvid, int T, const int32_t* num_seg_host, const int32_t* seg_id, const int32_t* st,
-                         const int32_t* en, int32_t* gseg_id, int32_t* gst, int32_t* gen, hipStream_t s);
+// nvid videos of T rows, or of the ragged host row offsets row_off (nvid + 1; NULL: uniform)
+int launch_segments(const float* x, long long ldx, int col0, int ncls, int T, int nvid, const int* row_off,
+                    int32_t* pred, int32_t* seg_id, int32_t* seg_start, int32_t* seg_end, int32_t* num_seg,
+                    hipStream_t s);
+int launch_seg_globalize(int nvid, int T, const int* row_off, const int32_t* num_seg_host, const int32_t* seg_id,
+                         const int32_t* st, const int32_t* en, int32_t* gseg_id, int32_t* gst, int32_t* gen,
+                         hipStream_t s);
 int launch_seg_reduce(const float* x, long long ldx, const int32_t* st, const int32_t* en, int S, int cols, int mean,
                       float* y, long long ldy, int accumulate, hipStream_t s);
 int launch_seg_mean_bwd(const float* dy, long long lddy, const int32_t* sid, const int32_t* st, const int32_t* en,

@@ -44,11 +44,17 @@ __global__ __launch_bounds__(256) void argmax_rows_kernel(const float* x, long l
 
 constexpr int SCAN_THREADS = 1024;
 
-__global__ __launch_bounds__(SCAN_THREADS) void boundary_scan_kernel(const int32_t* pred, int T, int32_t* seg_id,
+constexpr int MAXV = 32;
+struct RowOff {
+  int off[MAXV + 1];   // video v of the launch owns rows [off[v], off[v+1])
+};
+
+__global__ __launch_bounds__(SCAN_THREADS) void boundary_scan_kernel(const int32_t* pred, RowOff ro, int32_t* seg_id,
                                                                      int32_t* seg_start, int32_t* seg_end,
                                                                      int32_t* num_seg) {
-  // one block per video: rows [v*T, (v+1)*T), video-local segment numbering and frame indices
-  const long long vo = (long long)blockIdx.x * T;
+  // one block per video: its rows, video-local segment numbering and frame indices
+  const long long vo = ro.off[blockIdx.x];
+  const int T = ro.off[blockIdx.x + 1] - ro.off[blockIdx.x];
   pred += vo;
   seg_id += vo;
   seg_start += vo;
@@ -134,7 +140,6 @@ __global__ __launch_bounds__(256) void seg_mean_bwd_kernel(const float* dy, long
   *p = accumulate ? *p + v : v;
 }
 
-constexpr int MAXV = 32;
 struct GlobalizeArgs {
   const int32_t* seg_id;  // (nvid*T) video-local ids
   int32_t* gseg_id;       // (nvid*T) global ids
@@ -142,17 +147,17 @@ struct GlobalizeArgs {
   const int32_t* en;
   int32_t* gst;           // (sum S) global frame rows
   int32_t* gen;
-  int T, nv;
+  int nv;
   int soff[MAXV + 1];     // segment prefix offsets of this chunk's videos
-  int v0;                 // first video of the chunk
+  int roff[MAXV + 1];     // frame-row offsets of this chunk's videos
 };
 
 __global__ __launch_bounds__(256) void seg_globalize_kernel(GlobalizeArgs a) {
   const int v = blockIdx.y;
-  const int vg = a.v0 + v;
   const int S = a.soff[v + 1] - a.soff[v];
-  const long long base = (long long)vg * a.T;
-  for (int t = blockIdx.x * 256 + threadIdx.x; t < a.T; t += gridDim.x * 256) {
+  const long long base = a.roff[v];
+  const int T = a.roff[v + 1] - a.roff[v];
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < T; t += gridDim.x * 256) {
     a.gseg_id[base + t] = a.seg_id[base + t] + a.soff[v];
     if (t < S) {
       a.gst[a.soff[v] + t] = a.st[base + t] + (int)base;
@@ -163,8 +168,11 @@ __global__ __launch_bounds__(256) void seg_globalize_kernel(GlobalizeArgs a) {
 
 }  // namespace
 
-int launch_seg_globalize(int nvid, int T, const int32_t* num_seg_host, const int32_t* seg_id, const int32_t* st,
-                         const int32_t* en, int32_t* gseg_id, int32_t* gst, int32_t* gen, hipStream_t s) {
+static int row_of(int T, const int* row_off, int v) { return row_off ? row_off[v] : v * T; }
+
+int launch_seg_globalize(int nvid, int T, const int* row_off, const int32_t* num_seg_host, const int32_t* seg_id,
+                         const int32_t* st, const int32_t* en, int32_t* gseg_id, int32_t* gst, int32_t* gen,
+                         hipStream_t s) {
   int off = 0;
   for (int c0 = 0; c0 < nvid; c0 += MAXV) {
     GlobalizeArgs a{};
@@ -174,28 +182,38 @@ int launch_seg_globalize(int nvid, int T, const int32_t* num_seg_host, const int
     a.en = en;
     a.gst = gst;
     a.gen = gen;
-    a.T = T;
     a.nv = std::min(MAXV, nvid - c0);
-    a.v0 = c0;
+    int tmax = 1;
+    for (int v = 0; v <= a.nv; ++v) {
+      a.roff[v] = row_of(T, row_off, c0 + v);
+      if (v > 0) tmax = std::max(tmax, a.roff[v] - a.roff[v - 1]);
+    }
     for (int v = 0; v < a.nv; ++v) {
       a.soff[v] = off;
       off += num_seg_host[c0 + v];
     }
     a.soff[a.nv] = off;
-    hipLaunchKernelGGL(seg_globalize_kernel, dim3(std::max(1, std::min(cdiv(T, 256), 64)), a.nv), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(seg_globalize_kernel, dim3(std::max(1, std::min(cdiv(tmax, 256), 64)), a.nv), dim3(256), 0, s,
+                       a);
     FX_CHECK_HIP(hipGetLastError());
   }
   return FX_OK;
 }
 
-int launch_segments(const float* x, long long ldx, int col0, int ncls, int T, int nvid, int32_t* pred,
-                    int32_t* seg_id, int32_t* seg_start, int32_t* seg_end, int32_t* num_seg, hipStream_t s) {
-  FX_REQUIRE(T > 0 && ncls > 0, "segments: need T > 0 and ncls > 0");
-  FX_REQUIRE(nvid >= 1, "segments: nvid >= 1");
-  hipLaunchKernelGGL(argmax_rows_kernel, dim3(cdiv((long long)T * nvid, 4)), dim3(256), 0, s, x, ldx, col0, ncls, T * nvid,
-                     pred);
-  hipLaunchKernelGGL(boundary_scan_kernel, dim3(nvid), dim3(SCAN_THREADS), 0, s, pred, T, seg_id, seg_start, seg_end,
-                     num_seg);
+int launch_segments(const float* x, long long ldx, int col0, int ncls, int T, int nvid, const int* row_off,
+                    int32_t* pred, int32_t* seg_id, int32_t* seg_start, int32_t* seg_end, int32_t* num_seg,
+                    hipStream_t s) {
+  FX_REQUIRE(ncls > 0 && nvid >= 1 && (row_off || T > 0), "segments: need T > 0 (or row offsets) and ncls > 0");
+  const int rows = row_of(T, row_off, nvid);
+  for (int v = 0; v < nvid; ++v) FX_REQUIRE(row_of(T, row_off, v + 1) > row_of(T, row_off, v), "segments: empty video");
+  hipLaunchKernelGGL(argmax_rows_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, col0, ncls, rows, pred);
+  for (int c0 = 0; c0 < nvid; c0 += MAXV) {
+    RowOff ro{};
+    const int nv = std::min(MAXV, nvid - c0);
+    for (int v = 0; v <= nv; ++v) ro.off[v] = row_of(T, row_off, c0 + v);
+    hipLaunchKernelGGL(boundary_scan_kernel, dim3(nv), dim3(SCAN_THREADS), 0, s, pred, ro, seg_id, seg_start, seg_end,
+                       num_seg + c0);
+  }
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }

@@ -574,10 +574,14 @@ class MSTCNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, meta, *params):
         lib = nx.load()
-        T, nvid, cin, F, cout, nl, ln, in_map, d0, dfac, drop_p, seed = meta
+        T, nvid, cin, F, cout, nl, ln, in_map, d0, dfac, drop_p, seed, seq_off = meta
         w_in, b_in, layers, w_out, b_out = MSTCNFn._unpack(meta, params)
         keep = []
         prm = nx.MstcnParams()
+        if seq_off is not None:     # ragged videos: host row offsets
+            so = nx.int_array(seq_off)
+            keep.append(so)
+            prm.seq_off = ctypes.cast(so, ctypes.c_void_p)
         prm.cin, prm.F, prm.cout, prm.num_layers, prm.layernorm, prm.in_map = cin, F, cout, nl, int(ln), int(in_map)
         prm.dil0, prm.dil_factor = d0, dfac
         prm.w_in, prm.b_in = nx.ptr(w_in), nx.ptr(b_in)
@@ -629,8 +633,9 @@ class MSTCNFn(torch.autograd.Function):
         return (dx, None) + tuple(t[1] for t in tg)
 
 
-def mstcn(mod, x, T, nvid=1):
-    """Run a factmx.models.basic.MSTCN through MSTCNFn."""
+def mstcn(mod, x, T, nvid=1, seq_off=None):
+    """Run a factmx.models.basic.MSTCN through MSTCNFn: nvid videos of T rows stacked in x, or the
+    ragged videos of the host row-offset list seq_off (zero padding at every video's own ends)."""
     x2 = _2d(x)
     params = []
     if mod.in_map:
@@ -643,7 +648,8 @@ def mstcn(mod, x, T, nvid=1):
     ln = mod.layers[0].norm is not None if len(mod.layers) else False
     p = float(mod.dropout_rate) if (mod.training and mod.dropout_rate) else 0.0
     meta = (T, nvid, x2.shape[1], mod.hid_dim, mod.out_dim, mod.num_layers, bool(ln), bool(mod.in_map),
-            mod.dilation0, mod.dilation_factor, p, dropout_seed() if p > 0 else 0)
+            mod.dilation0, mod.dilation_factor, p, dropout_seed() if p > 0 else 0,
+            None if seq_off is None else tuple(int(v) for v in seq_off))
     return MSTCNFn.apply(x2, meta, *params)
 
 
@@ -667,12 +673,16 @@ class MSTCN2Fn(torch.autograd.Function):
 
     @staticmethod
     def _prm(meta, params, keep, cls, grads=False):
-        T, nvid, cin, F, cout, nl, in_map, dfac, drop_p, seed = meta
+        T, nvid, cin, F, cout, nl, in_map, dfac, drop_p, seed, seq_off = meta
         w_in, b_in, groups, w_out, b_out = MSTCN2Fn._unpack(meta, params)
         prm = cls()
         if not grads:
             prm.cin, prm.F, prm.cout, prm.num_layers, prm.in_map, prm.dil_factor = cin, F, cout, nl, int(in_map), dfac
             prm.dropout, prm.seed = float(drop_p), int(seed)
+            if seq_off is not None:
+                so = nx.int_array(seq_off)
+                keep.append(so)
+                prm.seq_off = ctypes.cast(so, ctypes.c_void_p)
         prm.w_in, prm.b_in = nx.ptr(w_in), nx.ptr(b_in)
         for field, grp in zip(("w_d1", "b_d1", "w_d2", "b_d2", "w_fu", "b_fu"), groups):
             arr = _ptr_array(grp)
@@ -719,8 +729,9 @@ class MSTCN2Fn(torch.autograd.Function):
         return (dx, None) + tuple(t[1] for t in tg)
 
 
-def mstcn2(mod, x, T, nvid=1, drop_p=0.0):
-    """Run a factmx.models.basic.MSTCN2 through MSTCN2Fn (x: (nvid*T, dim) rows)."""
+def mstcn2(mod, x, T, nvid=1, drop_p=0.0, seq_off=None):
+    """Run a factmx.models.basic.MSTCN2 through MSTCN2Fn (x: (nvid*T, dim) rows, or the ragged videos of
+    the host row-offset list seq_off)."""
     x2 = _2d(x)
     L = mod.num_layers
     params = [mod.conv_1x1_in.weight, mod.conv_1x1_in.bias] if mod.in_map else []
@@ -729,7 +740,8 @@ def mstcn2(mod, x, T, nvid=1, drop_p=0.0):
     params += [c.weight for c in mod.conv_fusion] + [c.bias for c in mod.conv_fusion]
     params += [mod.conv_out.weight, mod.conv_out.bias]
     meta = (T, nvid, x2.shape[1], mod.conv_out.weight.shape[1], mod.conv_out.weight.shape[0], L, bool(mod.in_map),
-            int(mod.dilation_factor), float(drop_p), dropout_seed() if drop_p > 0 else 0)
+            int(mod.dilation_factor), float(drop_p), dropout_seed() if drop_p > 0 else 0,
+            None if seq_off is None else tuple(int(v) for v in seq_off))
     return MSTCN2Fn.apply(x2, meta, *params)
 
 
@@ -951,31 +963,35 @@ def segments_from_probs(x2d, col0, ncls):
     buf = torch.empty(4 * T + 1, device=dev, dtype=torch.int32)
     pred, seg_id, st, en = buf[:T], buf[T:2 * T], buf[2 * T:3 * T], buf[3 * T:4 * T]
     ns = buf[4 * T:]
-    _check(lib.fx_segments_from_probs(nx.ptr(x2d), nx.ld(x2d), col0, ncls, T, 1, nx.ptr(pred), nx.ptr(seg_id),
+    _check(lib.fx_segments_from_probs(nx.ptr(x2d), nx.ld(x2d), col0, ncls, T, 1, None, nx.ptr(pred), nx.ptr(seg_id),
                                       nx.ptr(st), nx.ptr(en), nx.ptr(ns), nx.stream()), "fx_segments_from_probs")
     S = int(ns.item())
     return S, seg_id, st[:S], en[:S]
 
 
-def segments_from_probs_batched(x2d, col0, ncls, T, nvid):
-    """``segments_from_probs`` for nvid videos of T rows stacked in x2d, with ONE host read of all
-    segment counts.  Returns (S list, per-video local (seg_id, start, end) views, global
-    (seg_id, start, end) over the stacked frame rows / concatenated segments)."""
+def segments_from_probs_batched(x2d, col0, ncls, f_off):
+    """``segments_from_probs`` for the videos stacked in x2d (host frame-row prefix list f_off, ragged
+    lengths allowed), with ONE host read of all segment counts.  Returns (S list, per-video local
+    (seg_id, start, end) views, global (seg_id, start, end) over the stacked frame rows /
+    concatenated segments)."""
     lib = nx.load()
     dev = x2d.device
-    n = nvid * T
+    nvid = len(f_off) - 1
+    n = f_off[-1]
+    ro = nx.int_array(f_off)
     buf = torch.empty(4 * n + nvid, device=dev, dtype=torch.int32)
     pred, seg_id, st, en = buf[:n], buf[n:2 * n], buf[2 * n:3 * n], buf[3 * n:4 * n]
     ns = buf[4 * n:]
-    _check(lib.fx_segments_from_probs(nx.ptr(x2d), nx.ld(x2d), col0, ncls, T, nvid, nx.ptr(pred), nx.ptr(seg_id),
+    _check(lib.fx_segments_from_probs(nx.ptr(x2d), nx.ld(x2d), col0, ncls, 0, nvid, ro, nx.ptr(pred), nx.ptr(seg_id),
                                       nx.ptr(st), nx.ptr(en), nx.ptr(ns), nx.stream()), "fx_segments_from_probs")
     S = [int(v) for v in ns.tolist()]
     tot = sum(S)
     g = torch.empty(n + 2 * tot, device=dev, dtype=torch.int32)
     gid, gst, gen = g[:n], g[n:n + tot], g[n + tot:]
-    _check(lib.fx_segments_globalize(nvid, T, nx.int_array(S), nx.ptr(seg_id), nx.ptr(st), nx.ptr(en), nx.ptr(gid),
+    _check(lib.fx_segments_globalize(nvid, 0, ro, nx.int_array(S), nx.ptr(seg_id), nx.ptr(st), nx.ptr(en), nx.ptr(gid),
                                      nx.ptr(gst), nx.ptr(gen), nx.stream()), "fx_segments_globalize")
-    local = [(seg_id[v * T:(v + 1) * T], st[v * T:v * T + S[v]], en[v * T:v * T + S[v]]) for v in range(nvid)]
+    local = [(seg_id[f_off[v]:f_off[v + 1]], st[f_off[v]:f_off[v] + S[v]], en[f_off[v]:f_off[v] + S[v]])
+             for v in range(nvid)]
     return S, local, (gid, gst, gen)
 
 

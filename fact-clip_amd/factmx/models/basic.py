@@ -202,12 +202,15 @@ class MSTCN2(nn.Module):
     def __repr__(self):
         return self.string
 
-    def forward(self, x, T=None):
-        """x: (T, 1, dim) or, lockstep, (nvid*T, dim) rows of nvid stacked videos of T frames each (the
-        dilated convs zero-pad at every video's ends).  The whole stack is one fx_mstcn2 call."""
+    def forward(self, x, T=None, seq_off=None):
+        """x: (T, 1, dim) or, lockstep, (nvid*T, dim) rows of nvid stacked videos of T frames each -- or of
+        the ragged host row offsets seq_off (the dilated convs zero-pad at every video's ends).  The
+        whole stack is one fx_mstcn2 call."""
         x2 = fxf._2d(x)
-        T = T or x2.shape[0]
         p = float(self.dropout.p) if (self.training and self.dropout.p) else 0.0
+        if seq_off is not None:
+            return _as3d(fxf.mstcn2(self, x2, 0, len(seq_off) - 1, drop_p=p, seq_off=seq_off))
+        T = T or x2.shape[0]
         return _as3d(fxf.mstcn2(self, x2, T, x2.shape[0] // T, drop_p=p))
 
 

@@ -155,10 +155,11 @@ class Block(nn.Module):
 
 def _frame_branch_batch(branch, f, vb):
     """The frame branch over vb.nvid stacked videos: MS-TCN and MS-TCN++ (MSTCN2) each as one fused
-    stack call with per-video zero padding."""
+    stack call with per-video zero padding (ragged lengths through the row offsets)."""
+    so = vb.f_off if vb.ragged else None
     if isinstance(branch, basic.MSTCN2):
-        return fxf._2d(branch(f, T=vb.T))
-    return fxf.mstcn(branch, f, T=vb.T, nvid=vb.nvid)
+        return fxf._2d(branch(f, T=vb.T, seq_off=so))
+    return fxf.mstcn(branch, f, T=vb.T or 0, nvid=vb.nvid, seq_off=so)
 
 
 class InputBlock(Block):
@@ -187,7 +188,8 @@ class InputBlock(Block):
         per-video side-channel attributes go to ``self._vrec``."""
         f = _frame_branch_batch(self.frame_branch, f2, vb)
         f_out, f_cl = fxf.process_feature(f, self.nclass)
-        a = fxf.decoder(self.action_branch, a2, f_out, pos=fpos, query_pos=apos, nvid=vb.nvid)
+        a = fxf.decoder(self.action_branch, a2, f_out, pos=fpos, query_pos=apos, nvid=vb.nvid,
+                        mem_off=vb.f_off if vb.ragged else None)
         a_out, a_cl = fxf.process_feature(a, self.nclass + 1)
         n = self.nclass + 1
         fc, ac, ao = vb.frames(f_cl), vb.tokens(a_cl), vb.tokens(a_out)
@@ -244,11 +246,13 @@ class UpdateBlock(Block):
             vb.on_a2f(vb, a_cl, a2f_at)         # the loss phase's matching starts here (vloss.EarlyMatch)
         f = _frame_branch_batch(self.frame_branch, f, vb)
         f_out, f_cl = fxf.process_feature(f, self.nclass)
-        n, Q, T = self.nclass + 1, vb.Q, vb.T
+        n, Q = self.nclass + 1, vb.Q
         recs = []
         fc, ac, ao = vb.frames(f_cl), vb.tokens(a_cl), vb.tokens(a_out)
-        fat, aat, flg, alg = (torch.split(t, Q * T) for t in (f2a_at, a2f_at, f2a_lg, a2f_lg))
+        qt = [Q * T for T in vb.Ts]
+        fat, aat, flg, alg = (torch.split(t, qt) for t in (f2a_at, a2f_at, f2a_lg, a2f_lg))
         for v in range(vb.nvid):
+            T = vb.Ts[v]
             recs.append(dict(frame_clogit=fc[v].unsqueeze(1), action_clogit=ac[v].unsqueeze(1),
                              action_feature=ao[v][:, :-n].unsqueeze(1),
                              f2a_attn=fat[v].view(1, Q, T), a2f_attn=aat[v].view(1, T, Q),
@@ -323,7 +327,7 @@ class UpdateBlockTDU(Block):
     def forward_batch(self, f2, a2, fpos, apos, vb):
         # temporal downsample: one segmentation launch + ONE host read of every video's S
         S, local, (gid, gst, gen) = fxf.segments_from_probs_batched(f2, f2.shape[1] - self.nclass, self.nclass,
-                                                                     vb.T, vb.nvid)
+                                                                     vb.f_off)
         s_off = [0]
         for n_ in S:
             s_off.append(s_off[-1] + n_)
@@ -440,9 +444,9 @@ class _FACTBase(nn.Module):
         """All videos through the blocks in lockstep (see _forward_videos); returns restore(v), which
         points every side-channel attribute at video v's views.  ``on_a2f`` (vloss.EarlyMatch) runs
         when the last block's token logits and token->frame attention exist."""
-        nvid, T = len(seq_list), seq_list[0].shape[0]
+        nvid = len(seq_list)
         Q = self.cfg.FACT.ntoken
-        vb = _VideoBatch(nvid, T, Q)
+        vb = _VideoBatch(nvid, [int(s.shape[0]) for s in seq_list], Q)
         vb.on_a2f, vb.last = on_a2f, self.block_list[-1]
         frames = []
         for seq in seq_list:
@@ -453,8 +457,8 @@ class _FACTBase(nn.Module):
                 x = time_mask(x, self.cfg.TM.t, self.cfg.TM.m, self.cfg.TM.p, replace_with_zero=True)
             frames.append(x.squeeze(1))
         f2 = torch.cat(frames, 0)
-        fpe = _frame_pos(self.frame_pe, seq_list[0].unsqueeze(1))
-        fpos = None if fpe is None else fpe.squeeze(1).repeat(nvid, 1)
+        fpe = [_frame_pos(self.frame_pe, s.unsqueeze(1)) for s in seq_list]
+        fpos = None if fpe[0] is None else torch.cat([p.squeeze(1) for p in fpe], 0)
         apos = self.action_query.squeeze(1).repeat(nvid, 1)
         a2 = torch.zeros_like(apos)
         for k, blk in enumerate(self.block_list):
@@ -606,17 +610,22 @@ def _sum_terms(terms):
 
 
 class _VideoBatch:
-    """Row layout of nvid equal-length videos stacked for one batched pass: frames of video v are
-    rows [v*T, (v+1)*T), its action tokens rows [v*Q, (v+1)*Q)."""
+    """Row layout of nvid videos stacked for one batched pass: frames of video v are rows
+    [f_off[v], f_off[v+1]) (lengths Ts, ragged allowed), its action tokens rows [v*Q, (v+1)*Q).
+    T is the common length of an equal-length batch (None when ragged)."""
 
-    def __init__(self, nvid, T, Q):
-        self.nvid, self.T, self.Q = nvid, T, Q
-        self.f_off = [v * T for v in range(nvid + 1)]
+    def __init__(self, nvid, Ts, Q):
+        self.nvid, self.Ts, self.Q = nvid, list(Ts), Q
+        self.ragged = len(set(self.Ts)) > 1
+        self.T = None if self.ragged else self.Ts[0]
+        self.f_off = [0]
+        for T in self.Ts:
+            self.f_off.append(self.f_off[-1] + T)
         self.a_off = [v * Q for v in range(nvid + 1)]
         self.on_a2f = self.last = None
 
     def fr(self, v):
-        return slice(v * self.T, (v + 1) * self.T)
+        return slice(self.f_off[v], self.f_off[v + 1])
 
     def tk(self, v):
         return slice(v * self.Q, (v + 1) * self.Q)
@@ -625,7 +634,7 @@ class _VideoBatch:
     # gradients once, where per-video slicing costs a zero-filled full-size tensor, a copy and an
     # accumulating add per video (for every side-channel tensor a loss reads).
     def frames(self, t):
-        return torch.split(t, self.T, dim=0)
+        return torch.split(t, self.Ts, dim=0)
 
     def tokens(self, t):
         return torch.split(t, self.Q, dim=0)
@@ -635,12 +644,15 @@ class _VideoBatch:
 FUSED_LOSS = True
 
 
+MAX_LOCKSTEP_VIDEOS = 16   # ragged frame-branch convs carry at most 16 video offsets per launch
+
+
 def _batchable(net, seq_list):
-    """The lockstep path needs equal-length videos, the fused decoders and no transcript input."""
-    if len(seq_list) < 2 or net.cfg.FACT.trans:
+    """The lockstep path (any video lengths, one video included) needs the fused decoders, GPU inputs
+    and no transcript input."""
+    if not seq_list or len(seq_list) > MAX_LOCKSTEP_VIDEOS or net.cfg.FACT.trans:
         return False
-    T = seq_list[0].shape[0]
-    if any(s.shape[0] != T or not s.is_cuda for s in seq_list):
+    if any(not s.is_cuda or s.shape[0] < 1 for s in seq_list):
         return False
     for blk in net.block_list:
         if not basic._fused_decoder_ok(blk.action_branch) or not hasattr(blk, "forward_batch"):

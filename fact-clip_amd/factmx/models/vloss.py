@@ -152,7 +152,7 @@ class EarlyMatch:
     def __call__(self, vb, a_cl, a2f_at, seg=None):
         net, cfg = self.net, self.net.cfg
         lib = nx.load()
-        nvid, T, Q = vb.nvid, vb.T, vb.Q
+        nvid, Q, fo = vb.nvid, vb.Q, vb.f_off
         C1 = net.num_classes + 1
         dev = a_cl.device
         gts, labs = [], []
@@ -173,16 +173,16 @@ class EarlyMatch:
         base = pk.alloc(dev)
         for v in range(nvid):
             a = va[v]
-            a.Q, a.C1, a.T, a.G = Q, C1, T, G[v]
+            a.Q, a.C1, a.T, a.G = Q, C1, vb.Ts[v], G[v]
             a.clogit, a.ldc = _ptr_rows(a_cl, v * Q, C1), C1
             if seg is not None:
                 s_off, local = seg
                 a.attn, a.lda = a2f_at.data_ptr() + 4 * Q * s_off[v], Q
                 a.seg_id = local[v][0].data_ptr()
             else:
-                a.attn, a.lda = a2f_at.data_ptr() + 4 * Q * T * v, Q
+                a.attn, a.lda = a2f_at.data_ptr() + 4 * Q * fo[v], Q
             a.gs, a.ge, a.gl = (base + o for o in gt_off[v])
-            a.pred_off = v * T
+            a.pred_off = fo[v]
         pk.send()
         self.cost_host = None
         if cfg.Loss.match != "seq":
@@ -226,7 +226,7 @@ def run(net, vb, compute_loss, early=None):
     cfg = net.cfg
     blocks = list(net.block_list)
     last = blocks[-1]._bt
-    nvid, T, Q = vb.nvid, vb.T, vb.Q
+    nvid, Q, Ts, fo = vb.nvid, vb.Q, vb.Ts, vb.f_off
     C = net.num_classes
     C1 = C + 1
     dev = last["f_cl"].device
@@ -241,18 +241,18 @@ def run(net, vb, compute_loss, early=None):
         off, va = pk.structs(nx.VideoAttn, nvid)
         for v in range(nvid):
             a = va[v]
-            a.Q, a.C1, a.T = Q, C1, T
+            a.Q, a.C1, a.T = Q, C1, Ts[v]
             a.clogit, a.ldc = _ptr_rows(last["a_cl"], v * Q, C1), C1
             if "S" in last:
                 a.attn, a.lda = last["a2f_at"].data_ptr() + 4 * Q * last["s_off"][v], Q
                 a.seg_id = last["local"][v][0].data_ptr()
             else:
-                a.attn, a.lda = last["a2f_at"].data_ptr() + 4 * Q * T * v, Q
-            a.flogit, a.ldf = _ptr_rows(flog, v * T, C), C
-            a.pred_off = v * T
+                a.attn, a.lda = last["a2f_at"].data_ptr() + 4 * Q * fo[v], Q
+            a.flogit, a.ldf = _ptr_rows(flog, fo[v], C), C
+            a.pred_off = fo[v]
         return off, va
 
-    pred = torch.empty(nvid * T, dtype=torch.int32, device=dev)
+    pred = torch.empty(fo[-1], dtype=torch.int32, device=dev)
     if not compute_loss:
         pk = _Pack()
         va_off, va = eval_structs(pk)
@@ -262,7 +262,7 @@ def run(net, vb, compute_loss, early=None):
                                   nx.stream()), "fx_eval_pred")
         host = torch.cat([pred, fxf.device_status(dev)[:1]]).cpu().numpy()
         fxf.status_raise(int(host[-1]), dev)
-        return [{"pred": host[v * T:(v + 1) * T].astype(np.int64)} for v in range(nvid)]
+        return [{"pred": host[fo[v]:fo[v + 1]].astype(np.int64)} for v in range(nvid)]
 
     assert early is not None and early.done, "the last block did not run the early matching stage"
     matches = early.matches(Q)
@@ -347,9 +347,10 @@ def run(net, vb, compute_loss, early=None):
         fce = 0.5 if is_tdu else 1.0
         for v in range(nvid):
             gs, ge, gl = gt_off[v]
+            T = Ts[v]
             # frame CE (+ smooth) on the block's frame logits
-            add(k, v, dict(kind=nx.TERM_CLASS, R=T, C=C, x=_ptr_rows(f_cl, v * T, C), sr=C, sc=1,
-                           dx=_ptr_rows(gf, v * T, C), dsr=C, dsc=1, y=("p1", lab_off[v]), w=("p1", cw_off),
+            add(k, v, dict(kind=nx.TERM_CLASS, R=T, C=C, x=_ptr_rows(f_cl, fo[v], C), sr=C, sc=1,
+                           dx=_ptr_rows(gf, fo[v], C), dsr=C, dsc=1, y=("p1", lab_off[v]), w=("p1", cw_off),
                            c_ce=fce / T, c_sm=(sw_coef / ((T - 1) * C) if sw_coef and T > 1 else 0.0)), T, 0, 0)
             # token CE
             add(k, v, dict(kind=nx.TERM_CLASS, R=Q, C=C1, x=_ptr_rows(a_cl, v * Q, C1), sr=C1, sc=1,
@@ -371,7 +372,7 @@ def run(net, vb, compute_loss, early=None):
                                c_ce=0.5 / Sv, c_sm=0.0), Sv, 0, 0)
                 R, off, ivs, c_xe, c_sm = Sv, Q * s0, (st.data_ptr(), en.data_ptr()), 1.0 / Sv, 0.0
             else:
-                R, off, ivs = T, Q * T * v, (None, None)
+                R, off, ivs = T, Q * fo[v], (None, None)
                 c_xe, c_sm = 1.0 / T, (sw_coef / ((T - 1) * Q) if sw_coef and T > 1 else 0.0)
             f2a, a2f = bt["f2a_lg"], bt["a2f_lg"]
             gfa, gaf = grad_of(f2a), grad_of(a2f)
@@ -386,7 +387,7 @@ def run(net, vb, compute_loss, early=None):
     if any(con_on):
         Cs = text_seen.shape[0]
         Dc = text_seen.shape[1]
-        sims = torch.empty(2, nvid * T, Cs, device=dev)
+        sims = torch.empty(2, fo[-1], Cs, device=dev)
         ncolz = ((Cs + 4) & ~3) + 4 * nx.LOSS_NB * Cs
         gp = grad_of(proj)
         if not all(con_on):
@@ -394,10 +395,11 @@ def run(net, vb, compute_loss, early=None):
         for v in range(nvid):
             if not con_on[v]:
                 continue
-            add(-1, v, dict(kind=nx.TERM_INFONCE, R=T, C=Cs, x=_ptr_rows(sims[0], v * T, Cs), sr=Cs, sc=1,
-                            dx=_ptr_rows(sims[1], v * T, Cs), dsr=Cs, dsc=1, y=("p2", ycon_off[v]),
-                            emb=_ptr_rows(proj, v * T, Dc), ld_emb=Dc, text=text_seen.data_ptr(), D=Dc,
-                            inv_temp=1.0 / float(cfg.CLIP.temp), demb=_ptr_rows(gp, v * T, Dc), ld_demb=Dc,
+            T = Ts[v]
+            add(-1, v, dict(kind=nx.TERM_INFONCE, R=T, C=Cs, x=_ptr_rows(sims[0], fo[v], Cs), sr=Cs, sc=1,
+                            dx=_ptr_rows(sims[1], fo[v], Cs), dsr=Cs, dsc=1, y=("p2", ycon_off[v]),
+                            emb=_ptr_rows(proj, fo[v], Dc), ld_emb=Dc, text=text_seen.data_ptr(), D=Dc,
+                            inv_temp=1.0 / float(cfg.CLIP.temp), demb=_ptr_rows(gp, fo[v], Dc), ld_demb=Dc,
                             c_ce=0.5), T, Cs, ncolz)
 
     # coefficient matrix: out = [batch loss, per video (loss, fact, contrastive, block values...)]
@@ -463,7 +465,7 @@ def run(net, vb, compute_loss, early=None):
     fxf.status_raise(int(st_h[0]), dev)
     vals = out_h.tolist()
     ph = pred_h.numpy()
-    save_list = [{"pred": ph[v * T:(v + 1) * T].astype(np.int64)} for v in range(nvid)]
+    save_list = [{"pred": ph[fo[v]:fo[v + 1]].astype(np.int64)} for v in range(nvid)]
     for v in range(nvid):
         o = 1 + v * per
         d = {"loss": vals[o]}

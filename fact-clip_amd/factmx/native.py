@@ -29,7 +29,8 @@ class FactmxNativeError(RuntimeError):
 class Operand(ctypes.Structure):
     _fields_ = [("ptr", P), ("ld", L), ("ptr1", P), ("ld1", L), ("k_split", I), ("rows0", P), ("rows1", P),
                 ("pos", P), ("ld_pos", L), ("pos_cols", I), ("trans", I), ("conv_taps", I), ("conv_cin", I),
-                ("conv_dil", I), ("conv_dir", I), ("seq_len", I), ("batch_stride", L), ("ones_col", I)]
+                ("conv_dil", I), ("conv_dir", I), ("seq_len", I), ("batch_stride", L), ("ones_col", I),
+                ("seq_off", P), ("nseq", I)]
 
 
 class GemmDesc(ctypes.Structure):
@@ -45,13 +46,14 @@ class MstcnParams(ctypes.Structure):
     _fields_ = [("cin", I), ("F", I), ("cout", I), ("num_layers", I), ("layernorm", I), ("in_map", I),
                 ("dil0", I), ("dil_factor", I), ("w_in", P), ("b_in", P), ("w_dil", P), ("b_dil", P), ("w_pw", P), ("b_pw", P),
                 ("ln_w", P), ("ln_b", P), ("w_out", P), ("b_out", P), ("dropout", F), ("seed", U),
-                ("side_defer", I)]
+                ("side_defer", I), ("seq_off", P)]
 
 
 class Mstcn2Params(ctypes.Structure):
     _fields_ = [("cin", I), ("F", I), ("cout", I), ("num_layers", I), ("in_map", I), ("dil_factor", I),
                 ("w_in", P), ("b_in", P), ("w_d1", P), ("b_d1", P), ("w_d2", P), ("b_d2", P), ("w_fu", P),
-                ("b_fu", P), ("w_out", P), ("b_out", P), ("dropout", F), ("seed", U), ("side_defer", I)]
+                ("b_fu", P), ("w_out", P), ("b_out", P), ("dropout", F), ("seed", U), ("side_defer", I),
+                ("seq_off", P)]
 
 
 class Mstcn2Grads(ctypes.Structure):
@@ -157,8 +159,8 @@ SIGNATURES = {
     "fx_gru_workspace_floats": (L, [I, I, I, I]),
     "fx_gru_bidir_fwd": (I, [P, L, I, I, P, I, I, P, P, P, P, P, P, P, P, P, L, P, P, P, I, P]),
     "fx_gru_bidir_bwd": (I, [P, L, I, I, P, I, I, P, P, P, P, P, P, L, P, L, P, P, P, P, P, P, P, P, P, P, I, P]),
-    "fx_segments_from_probs": (I, [P, L, I, I, I, I, P, P, P, P, P, P]),
-    "fx_segments_globalize": (I, [I, I, P, P, P, P, P, P, P, P]),
+    "fx_segments_from_probs": (I, [P, L, I, I, I, I, P, P, P, P, P, P, P]),
+    "fx_segments_globalize": (I, [I, I, P, P, P, P, P, P, P, P, P]),
     "fx_seg_mean_fwd": (I, [P, L, P, P, I, I, P, L, P]),
     "fx_seg_mean_bwd": (I, [P, L, P, P, P, I, I, P, L, I, P]),
     "fx_seg_sum_rows": (I, [P, L, P, P, I, I, P, L, I, P]),

@@ -58,7 +58,8 @@ long long fx_struct_size(int which);
  *   k-k_split, leading dim ld1); rows0/rows1 gather source rows; pos adds
  *   pos[r*ld_pos + k] for k < pos_cols (positional encoding add,
  *   basic.py:313-320).
- * conv_taps == 3 (dilated conv, zero padding per video of seq_len rows):
+ * conv_taps == 3 (dilated conv, zero padding per video of seq_len rows, or of the ragged
+ *   row ranges seq_off when nseq > 0):
  *   trans==0: k = tap*conv_cin + c, element = src[(r + s)*ld + c]
  *   trans==1: r = tap*conv_cin + c, element = src[(k + s)*ld + c]
  *   with s = (tap-1) * conv_dil * conv_dir, zero when the shifted row leaves
@@ -83,6 +84,8 @@ typedef struct fx_operand {
   int seq_len;
   long long batch_stride;
   int ones_col;               /* != 0: logical row ones_col-1 reads 1.0 (fused bias gradient) */
+  const int* seq_off;         /* row-major (A) conv operand of ragged videos: host (nseq + 1) row offsets, */
+  int nseq;                   /* video v owns rows [seq_off[v], seq_off[v+1]) (nseq <= 16; 0: seq_len) */
 } fx_operand;
 
 typedef struct fx_gemm_desc {
@@ -286,6 +289,9 @@ typedef struct fx_mstcn_params {
                                  stream (no join before return); the caller joins with fx_side_join
                                  before reading those gradients and keeps x / dy / saved / workspace
                                  alive until then (torch: record_stream on fx_side_stream()) */
+  const int* seq_off;         /* ragged videos: host (nvid + 1) row offsets (video v owns rows
+                                 [seq_off[v], seq_off[v+1]), zero padding at its own ends; nvid <= 16;
+                                 T ignored); NULL: nvid videos of T rows */
 } fx_mstcn_params;
 
 typedef struct fx_mstcn_grads {
@@ -329,6 +335,7 @@ typedef struct fx_mstcn2_params {
   float dropout;
   unsigned long long seed;
   int side_defer;
+  const int* seq_off;         /* ragged videos, as fx_mstcn_params.seq_off */
 } fx_mstcn2_params;
 
 typedef struct fx_mstcn2_grads {
@@ -438,8 +445,9 @@ int fx_mha_t_bwd(const float* q, long long ldq, const float* k, long long ldk, c
  * fx_segments_from_probs: pred[t] = argmax_c x[t, col0 + c] (first max),
  *   boundaries where pred changes, seg_id[t], seg_start[s], seg_end[s]
  *   (inclusive) and *num_seg (device int) — bit-exact run-length encoding.
- *   nvid videos of T rows each: video v's tables live at [v*T, (v+1)*T) with
- *   video-local numbering, num_seg[v] its count.
+ *   nvid videos of T rows each (or of the ragged host row offsets row_off, nvid + 1
+ *   entries; NULL: uniform): video v's tables live at its own rows with video-local
+ *   numbering, num_seg[v] its count.
  * fx_segments_globalize: after the host read num_seg: gseg_id = seg_id + the
  *   segment offset of its video; gstart/gend (sum S) = the videos' segment bounds as
  *   global frame rows, in video order.
@@ -448,11 +456,11 @@ int fx_mha_t_bwd(const float* q, long long ldq, const float* k, long long ldk, c
  * fx_seg_sum_rows: dseg[s] (+)= sum_{t in s} dframe[t]  (gather backward)
  * ---------------------------------------------------------------------- */
 int fx_segments_from_probs(const float* x, long long ldx, int col0, int ncls, int T, int nvid,
-                           int32_t* pred, int32_t* seg_id, int32_t* seg_start, int32_t* seg_end,
-                           int32_t* num_seg, void* stream);
-int fx_segments_globalize(int nvid, int T, const int32_t* num_seg_host, const int32_t* seg_id,
-                          const int32_t* seg_start, const int32_t* seg_end, int32_t* gseg_id,
-                          int32_t* gstart, int32_t* gend, void* stream);
+                           const int* row_off, int32_t* pred, int32_t* seg_id, int32_t* seg_start,
+                           int32_t* seg_end, int32_t* num_seg, void* stream);
+int fx_segments_globalize(int nvid, int T, const int* row_off, const int32_t* num_seg_host,
+                          const int32_t* seg_id, const int32_t* seg_start, const int32_t* seg_end,
+                          int32_t* gseg_id, int32_t* gstart, int32_t* gend, void* stream);
 int fx_seg_mean_fwd(const float* x, long long ldx, const int32_t* seg_start, const int32_t* seg_end,
                     int S, int cols, float* y, long long ldy, void* stream);
 int fx_seg_mean_bwd(const float* dy, long long lddy, const int32_t* seg_id, const int32_t* seg_start,

@@ -154,3 +154,29 @@ def test_breakfast_vanilla_fact_vs_oracle(monkeypatch):
     _check_forward(net, spec, outs, saves, None)
     assert abs(loss - ref_loss) <= 1e-4 * abs(ref_loss), (loss, ref_loss)
     compare_grads(net, ref_grads, rtol=2e-3, relaxed=kinks.flipped_prefixes(len(vids)), what="breakfast: ")
+
+
+def test_ragged_lockstep_backward_vs_oracle(monkeypatch):
+    """A ragged lockstep batch (T = 4096 and 2900, HAViD-holdout dims: the reference's DataLoader yields
+    variable-length videos, dataset.py:106-131) against the fp64 oracle run per video: TDU segments and
+    predictions identical, every video's per-frame logits within 1e-3, loss within 1e-4, gradients."""
+    import bench
+    from factmx.models import blocks as blocks_mod
+    cfg = bench.make_cfg()
+    D, C = 2048, 75
+    net, text = bench.build_model(cfg, D, C, device=DEV, seed=0)
+    net.train()
+    vids = [bench.make_video(T, D, C, cfg, seed=s) for T, s in ((4096, 1), (2900, 5))]
+    seqs = [torch.from_numpy(f).to(DEV) for f, _ in vids]
+    assert blocks_mod._batchable(net, seqs)
+    kinks = GruKinks(monkeypatch)
+    from factmx.dp import DataParallel
+    loss, saves = _gpu_step(net, vids, dp=DataParallel(net))
+    assert net._vb.ragged and net._vb.Ts == [4096, 2900]
+    S = _segments(net)
+    spec = fo.resolve_spec(cfg, D, C, clip=True)
+    ref_loss, ref_grads, outs = oracle_batch(spec, net, vids, text)
+    assert S == [[len(r["tdu"].starts) for r in o["blocks"] if r["type"] == "U"] for o in outs], S
+    _check_forward(net, spec, outs, saves, text)
+    assert abs(loss - ref_loss) <= 1e-4 * abs(ref_loss), (loss, ref_loss)
+    compare_grads(net, ref_grads, rtol=2e-3, relaxed=kinks.flipped_prefixes(len(vids)), what="ragged: ")

@@ -62,15 +62,18 @@ def _keep_impl():
     yield
 
 
-@pytest.mark.parametrize("name", ["tiny_clip", "tiny_clip_iid", "tiny_fact_m2"])
-def test_lockstep_equals_per_video(name, monkeypatch):
+@pytest.mark.parametrize("name,dT", [("tiny_clip", 0), ("tiny_clip_iid", 0), ("tiny_fact_m2", 0),
+                                     ("tiny_clip", -37), ("tiny_clip_iid", 23), ("tiny_fact_m2", -61)])
+def test_lockstep_equals_per_video(name, dT, monkeypatch):
+    """dT != 0: a ragged batch (the second video dT frames longer / shorter), as the reference's
+    DataLoader yields (dataset.py:106-131)."""
     fx = load_fixture(name)
     meta = tiny_meta(fx)
     cfg = cfg_from_meta(meta)
     feats, label, _ = tiny_inputs(meta)
     T, D = feats.shape
     seen = sorted(set(label.tolist()))
-    f2, l2 = pg.segmented_video(T, D, seen, 5, seed=11, noise=0.4)
+    f2, l2 = pg.segmented_video(T + dT, D, seen, 5, seed=11, noise=0.4)
     seqs = [torch.from_numpy(feats).float().to(DEV), torch.from_numpy(f2).float().to(DEV)]
     labs = [torch.from_numpy(label).to(DEV), torch.from_numpy(l2).to(DEV)]
     assert blocks_mod._batchable(_model(meta, cfg), seqs)

@@ -88,11 +88,11 @@ def test_dp_two_ranks_equal_single_process_lockstep(tmp_path):
         g, r = got[off:off + k].astype(np.float64), ref[off:off + k].astype(np.float64)
         off += k
         rms = float(np.sqrt((r * r).mean()))
-        # rtol 1e-5 + the suite's floor (1e-2 x rms, helpers.compare_grads): the weight gradients are
-        # sums over 4096 vs 8192 stacked rows with other split-K orders, whose terms cancel; and
-        # normwise within 1e-4
-        tol = 1e-5 * np.abs(r) + 1e-2 * rms + 1e-9
+        # rtol 1e-5 + the suite's floors (1e-2 x rms + 1e-7, helpers.compare_grads: the weight gradients
+        # are sums over 4096 vs 8192 stacked rows with other split-K orders, whose terms cancel; key
+        # biases under a row softmax have analytically zero gradients); normwise within 1e-4
+        tol = 1e-5 * np.abs(r) + 1e-2 * rms + 1e-7
         dn, rn = float(np.linalg.norm(g - r)), float(np.linalg.norm(r))
-        if (np.abs(g - r) > tol).any() or dn > 1e-4 * rn + 1e-9:
+        if (np.abs(g - r) > tol).any() or dn > 1e-4 * rn + 1e-7:
             bad.append(f"{n}: max |dg| {np.abs(g - r).max():.3g} (rms {rms:.3g}), |dg| {dn:.3g} vs |r| {rn:.3g}")
     assert not bad, "DP gradient != single-process gradient:\n" + "\n".join(bad[:20])

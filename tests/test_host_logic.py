@@ -1,15 +1,20 @@
 """Host-side helpers of the lockstep path (CPU): per-video chunk views and loss-term summation
 give the same values and gradients as the slicing / `+` chains they replace."""
+import pytest
 import torch
 
 from factmx.models.blocks import _sum_terms, _VideoBatch
 
 
-def test_video_chunks_match_slices_in_value_and_grad():
-    vb = _VideoBatch(nvid=3, T=5, Q=2)
-    x = torch.randn(15, 4, dtype=torch.float64, requires_grad=True)
+@pytest.mark.parametrize("Ts", [[5, 5, 5], [5, 3, 7]])
+def test_video_chunks_match_slices_in_value_and_grad(Ts):
+    """Per-video frame / token chunks of a lockstep batch (equal or ragged video lengths)."""
+    vb = _VideoBatch(nvid=3, Ts=Ts, Q=2)
+    assert vb.ragged == (len(set(Ts)) > 1) and vb.f_off == [0, Ts[0], Ts[0] + Ts[1], sum(Ts)]
+    n = sum(Ts)
+    x = torch.randn(n, 4, dtype=torch.float64, requires_grad=True)
     y = torch.randn(6, 3, dtype=torch.float64, requires_grad=True)
-    w = torch.randn(15, 4, dtype=torch.float64)
+    w = torch.randn(n, 4, dtype=torch.float64)
     # only videos 0 and 2 contribute to the loss (video 1's chunk gets no gradient)
     xs, ys = vb.frames(x), vb.tokens(y)
     loss = (xs[0] * w[vb.fr(0)]).sum() + (xs[2] ** 2).sum() + ys[1][:, :-1].sum()
@@ -19,7 +24,7 @@ def test_video_chunks_match_slices_in_value_and_grad():
     ref = (x[vb.fr(0)] * w[vb.fr(0)]).sum() + (x[vb.fr(2)] ** 2).sum() + y[vb.tk(1), :-1].sum()
     ref.backward()
     assert torch.equal(gx, x.grad) and torch.equal(gy, y.grad)
-    assert torch.equal(gx[vb.fr(1)], torch.zeros(5, 4, dtype=torch.float64))
+    assert torch.equal(gx[vb.fr(1)], torch.zeros(Ts[1], 4, dtype=torch.float64))
 
 
 def test_sum_terms():
