@@ -165,7 +165,7 @@ def traffic_from_profiles(kernel_prefix, name="pmc_dominant.json"):
 
 
 def bf16_mode(net, step, nv, T, steps, warmup, fxf):
-    """Time `steps` fixed-weight steps with fx_set_gemm_precision(FX_PREC_BF16) and compare its frame
+    """Time `steps` fixed-weight steps with fx_set_stream_precision(FX_PREC_BF16) and compare its frame
     logits (last block, every video) and TDU segment counts with the fp32 path's."""
     def logits():
         step()

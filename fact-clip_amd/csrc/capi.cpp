@@ -257,8 +257,7 @@ struct SideStream {
 };
 
 SideStream* side_stream() {
-  const char* e = std::getenv("FX_SIDE_STREAM");   // 0: everything on the caller's stream (A/B, debug)
-  if (e && e[0] == '0') return nullptr;
+  if (!knobs().side_stream) return nullptr;   // FX_SIDE_STREAM=0: everything on the caller's stream
   static std::mutex mu;
   static std::map<int, SideStream*> pool;
   int dev = 0;
@@ -269,10 +268,8 @@ SideStream* side_stream() {
   SideStream* ss = new SideStream();
   // FX_SIDE_PRIORITY=low|normal|high: the side stream's queue priority (A/B diagnostic; default normal)
   int prio = 0, least = 0, greatest = 0;
-  if (const char* pe = std::getenv("FX_SIDE_PRIORITY")) {
-    if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
-      prio = std::string(pe) == "low" ? least : std::string(pe) == "high" ? greatest : 0;
-  }
+  if (knobs().side_priority != 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+    prio = knobs().side_priority < 0 ? least : greatest;
   bool ok = hipStreamCreateWithPriority(&ss->s, hipStreamNonBlocking, prio) == hipSuccess;
   for (auto& e : ss->to_side) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
   for (auto& e : ss->layer_done) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
@@ -298,10 +295,7 @@ struct MstcnLayout {
 // launch otherwise walks all K = rows and holds its CU for the whole launch, so the main stream's
 // next kernels wait for CUs; FX_DEFER_SPLIT=n caps a workgroup's share at K / n (A/B knob).
 int defer_split_impl(int rows) {
-  static const int sp = [] {
-    const char* e = std::getenv("FX_DEFER_SPLIT");
-    return e ? std::max(1, std::min(16, std::atoi(e))) : 8;
-  }();
+  const int sp = knobs().defer_split;
   return std::max(1, std::min(sp, rows / 512));
 }
 
@@ -380,11 +374,7 @@ int layer_dilation(const fx_mstcn_params* p, int i) {
 // i times one stride: true for views of one flat gradient buffer in parameter order (FlatGradReducer).
 // FX_MSTCN_DEFER=0 keeps the per-layer interleaved GEMMs (A/B).
 bool mstcn_defer_ok(const fx_mstcn_params* p, const fx_mstcn_grads* g) {
-  static const bool off = [] {
-    const char* e = std::getenv("FX_MSTCN_DEFER");
-    return e && e[0] == '0';
-  }();
-  if (off) return false;
+  if (!knobs().mstcn_defer) return false;
   const int NL = p->num_layers;
   for (int i = 0; i < NL; ++i)
     if (!g->w_dil[i] || !g->b_dil[i] || !g->w_pw[i] || !g->b_pw[i]) return false;
@@ -450,6 +440,34 @@ using namespace fx;
 extern "C" {
 
 int fx_version(void) { return FX_ABI_VERSION; }
+
+}  // extern "C"
+
+namespace fx {
+const Knobs& knobs() {
+  static Knobs k;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    auto env = [](const char* n) -> const char* { return std::getenv(n); };
+    if (const char* p = env("FX_GEMM_PATH")) k.gemm_path = std::string(p) == "tiled" ? 1 : std::string(p) == "direct" ? 2 : 0;
+    if (const char* p = env("FX_GEMM_W8")) k.gemm_w8 = p[0] == '1';
+    if (const char* p = env("FX_GEMM_WIDE")) k.gemm_wide = p[0] == '1' ? 1 : 0;
+    if (const char* p = env("FX_GEMM_STAGGER")) k.gemm_stagger = p[0] == '1' ? 1 : 0;
+    if (const char* p = env("FX_GEMM_XCDPLANES")) k.gemm_xcd_planes = p[0] != '0';
+    if (const char* p = env("FX_GEMM_NTSTORE")) k.gemm_nt_store = p[0] == '1';
+    if (const char* p = env("FX_GEMM_LOG")) k.gemm_log = std::fopen(p, "a");
+    if (const char* p = env("FX_GEMM_GROUP")) k.gemm_group = p[0] != '0';
+    if (const char* p = env("FX_SIDE_STREAM")) k.side_stream = p[0] != '0';
+    if (const char* p = env("FX_SIDE_PRIORITY")) k.side_priority = std::string(p) == "low" ? -1 : std::string(p) == "high" ? 1 : 0;
+    if (const char* p = env("FX_DEFER_SPLIT")) k.defer_split = std::max(1, std::min(16, std::atoi(p)));
+    if (const char* p = env("FX_MSTCN_DEFER")) k.mstcn_defer = p[0] != '0';
+    if (const char* p = env("FX_SIDE_MAXWG")) k.side_maxwg = std::max(0, std::atoi(p));
+  });
+  return k;
+}
+}  // namespace fx
+
+extern "C" {
 const char* fx_last_error(void) { return g_last_error.c_str(); }
 
 int fx_dropout(const float* x, long long ldx, int rows, int cols, long long idx_ld, long long idx_col0, float p,
@@ -546,7 +564,7 @@ int fx_mstcn_fwd(const fx_mstcn_params* p, const float* x, long long ldx, int T,
     FX_CHECK_HIP(hipMemcpy2DAsync(h0, F * sizeof(float), x, ldx * sizeof(float), F * sizeof(float), rows,
                                   hipMemcpyDeviceToDevice, s));
   }
-  const bool fused = !p->layernorm && !q.off && frl_supported(F, saved, F, F);
+  const bool fused = p->fused_layers && !p->layernorm && !q.off && frl_supported(F, saved, F, F);
   for (int i = 0; i < p->num_layers; ++i) {
     const float* hi = saved + L.h + i * L.rowsF;
     float* hn = saved + L.h + (i + 1) * L.rowsF;
@@ -598,7 +616,8 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   FX_REQUIRE(p->dropout >= 0.f && p->dropout < 1.f, "mstcn: dropout must be in [0, 1)");
   const bool drop = p->dropout > 0.f;
   // Fused chain (no LayerNorm, no dropout, uniform videos, FX_MSTCN_FUSED=1): see below
-  const bool fchain = !p->layernorm && !drop && !q.off && NL > 0 && frl_supported(F, ws + L.buf0, F, F);
+  const bool fchain =
+      p->fused_layers && !p->layernorm && !drop && !q.off && NL > 0 && frl_supported(F, ws + L.buf0, F, F);
   // the dX-packed conv weights come from the forward (saved); the fused chain also needs the
   // transposed 1x1 weights (repacked here, into the workspace)
   if (fchain) FX_TRY(pack_conv_weights(p, ws, ws + L.wb, ws + L.wpt, L, s));
@@ -626,11 +645,7 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   hipStream_t sd = ss ? ss->s : s;
   const bool defer = !fchain && !p->layernorm && !drop && NL > 0 && mstcn_defer_ok(p, g);
   // FX_SIDE_MAXWG=n: the side stream's split-K GEMMs keep within n workgroups (A/B diagnostic)
-  static const int side_maxwg = [] {
-    const char* e = std::getenv("FX_SIDE_MAXWG");
-    return e ? std::max(0, std::atoi(e)) : 0;
-  }();
-  GridCap gcap(ss ? side_maxwg : 0);
+  GridCap gcap(ss ? knobs().side_maxwg : 0);
   auto fork = [&](int e) -> int {   // side stream waits for the main stream's work so far
     if (!ss) return FX_OK;
     FX_CHECK_HIP(hipEventRecord(ss->to_side[e], s));

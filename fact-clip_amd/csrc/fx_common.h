@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdio>
 #include <string>
 
 #include "../../include/factmx.h"
@@ -112,6 +113,27 @@ inline unsigned long long fx_drop_subseed(unsigned long long seed, int i) {
 // y[r, c] = x[r, c] * keep(seed, r * idx_ld + idx_col0 + c) / (1 - p)   (y may alias x)
 int launch_dropout(const float* x, long long ldx, int rows, int cols, long long idx_ld, long long idx_col0, float p,
                    unsigned long long seed, float* y, long long ldy, hipStream_t s);
+
+// Diagnostic A/B switches (FX_GEMM_PATH, FX_GEMM_W8, FX_GEMM_WIDE, FX_GEMM_STAGGER, FX_GEMM_XCDPLANES,
+// FX_GEMM_NTSTORE, FX_GEMM_LOG, FX_GEMM_GROUP, FX_SIDE_STREAM, FX_SIDE_PRIORITY, FX_DEFER_SPLIT,
+// FX_MSTCN_DEFER, FX_SIDE_MAXWG): read from the environment ONCE, at the library's first use, into this
+// table (std::call_once); no entry point reads the environment itself.  Defaults are the tuned paths.
+struct Knobs {
+  int gemm_path = 0;        // 1 tiled, 2 direct (0: the planner's choice)
+  bool gemm_w8 = true;      // 8-wave 128x64 tiles
+  int gemm_wide = -1;       // 0 / 1 force the 128x64 tiles off / on (-1: the planner's choice)
+  int gemm_stagger = 1;
+  bool gemm_xcd_planes = true;
+  bool gemm_nt_store = false;
+  FILE* gemm_log = nullptr; // FX_GEMM_LOG=<file>: one line per GEMM launch (shape census)
+  bool gemm_group = true;
+  bool side_stream = true;
+  int side_priority = 0;    // -1 low, 0 normal, 1 high
+  int defer_split = 8;
+  bool mstcn_defer = true;
+  int side_maxwg = 0;
+};
+const Knobs& knobs();
 
 // event-based timing hooks around launches of one kernel class (bench roofline)
 void prof_begin(int kind, hipStream_t s);

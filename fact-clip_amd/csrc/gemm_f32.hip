@@ -30,6 +30,7 @@
 #include <mutex>
 #include <string>
 #include <utility>
+#include <vector>
 
 #include "fx_common.h"
 
@@ -1513,11 +1514,7 @@ int launch_direct(int ak, int bk, dim3 grid, dim3 block, hipStream_t s, const Ge
 // 25 vs 32 us at 256x257x4096.)  Conv-gather operands always take the tiled kernel.
 // FX_GEMM_PATH=tiled|direct overrides the choice (diagnostic).
 bool use_direct(const fx_gemm_desc& d, int ak, int bk) {
-  static const int force = [] {
-    const char* p = std::getenv("FX_GEMM_PATH");
-    if (!p) return 0;
-    return std::string(p) == "tiled" ? 1 : std::string(p) == "direct" ? 2 : 0;
-  }();
+  const int force = knobs().gemm_path;
   // the direct kernel addresses ROWS / COLS operands with 32-bit byte offsets (dload)
   auto fits = [&](const fx_operand& o, int kind, int R) {
     const double k = (double)d.K + 2 * DMAXW * DCH + 64, ld = (double)o.ld;
@@ -1541,18 +1538,11 @@ bool use_direct(const fx_gemm_desc& d, int ak, int bk) {
 // FX_GEMM_WIDE=0|1 forces the choice among eligible launches (diagnostic).
 // 128x64 tiles with 8 waves (two per SIMD) instead of 4; FX_GEMM_W8=0|1 overrides (diagnostic)
 bool wide8() {
-  static const bool on = [] {
-    const char* p = std::getenv("FX_GEMM_W8");
-    return p ? p[0] == '1' : true;
-  }();
-  return on;
+  return knobs().gemm_w8;
 }
 
 bool use_wide(const GemmDev& g, int ak, int bk, int batch) {
-  static const int force = [] {
-    const char* p = std::getenv("FX_GEMM_WIDE");
-    return p ? (p[0] == '1' ? 1 : 0) : -1;
-  }();
+  const int force = knobs().gemm_wide;
   const bool fast = g.a_vec && g.b_vec && (g.K % BK) == 0;
   const bool ok = fast && (ak == ROWS || ak == ROWS_CONV || ak == ROWS_CAT || ak == COLS) &&
                   (bk == ROWS || bk == COLS || bk == COLS_CONV);
@@ -1713,11 +1703,7 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
   g.a_vec = operand_vec_ok(d.a);
   g.b_vec = operand_vec_ok(d.b);
   g.ws = d.workspace;
-  static const int stagger = [] {
-    const char* p = std::getenv("FX_GEMM_STAGGER");   // diagnostic A/B: 0 = both halves alike
-    return p ? (p[0] == '1' ? 1 : 0) : 1;
-  }();
-  g.w8_stagger = stagger;
+  g.w8_stagger = knobs().gemm_stagger;
   const int ak = kind_of(d.a, g.a_vec), bk = kind_of(d.b, g.b_vec);
   P.ak = ak;
   P.bk = bk;
@@ -1770,17 +1756,10 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
     g.tile_cnt = pool ? pool + tile_cnt_base : nullptr;
   }
   // FX_GEMM_XCDPLANES=0: the per-plane tile mapping for every launch (A/B)
-  static const bool planes_on = [] {
-    const char* p = std::getenv("FX_GEMM_XCDPLANES");
-    return !(p && p[0] == '0');
-  }();
+  const bool planes_on = knobs().gemm_xcd_planes;
   const long long nz = (long long)d.batch * g.split;
   g.xcd_planes = planes_on && wide && wide8() && nz >= 8 && nz % 8 == 0;
-  static const bool nt_on = [] {
-    const char* p = std::getenv("FX_GEMM_NTSTORE");
-    return p && p[0] == '1';
-  }();
-  g.nt_store = nt_on ? 1 : 0;
+  g.nt_store = knobs().gemm_nt_store ? 1 : 0;
   P.grid = grid;
   P.block = block;
   P.direct = direct;
@@ -1791,10 +1770,7 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
 // member: index inside a grouped launch (members > 0 share the kernel of member 0)
 void log_gemm(const fx_gemm_desc& d, const GemmPlan& P, int member = 0) {
   // FX_GEMM_LOG=<file>: append one line per launch (diagnostic shape census, tools/gemm_census.py)
-  static FILE* glog = [] {
-    const char* p = std::getenv("FX_GEMM_LOG");
-    return p ? std::fopen(p, "a") : nullptr;
-  }();
+  FILE* glog = knobs().gemm_log;
   if (glog)
     std::fprintf(glog, "%d %d %d %d %d %d %d %d %d %d %d %d\n", d.M, d.N, d.K, d.batch, P.ak, P.bk, P.g.split,
                  d.a.conv_taps, d.b.conv_taps, d.relu, P.direct ? (int)P.block.x / 64 : (P.wide ? -1 : 0), member);
@@ -1813,12 +1789,25 @@ int launch_reduce(const fx_gemm_desc& d, const GemmPlan& P, hipStream_t s) {
 
 }  // namespace
 
-std::atomic<int> g_gemm_prec{FX_PREC_F32};
+// GEMM arithmetic precision per caller stream (fx_set_stream_precision): a few (stream, precision)
+// pairs behind a mutex; streams never set run FX_PREC_F32.  Per stream, so two callers with different
+// precisions on different streams (or threads) do not interfere.
+std::mutex g_prec_mu;
+std::vector<std::pair<hipStream_t, int>> g_prec;
+std::atomic<int> g_prec_any{0};   // fast path: no stream has ever left FX_PREC_F32
+
+int stream_precision(hipStream_t s) {
+  if (!g_prec_any.load(std::memory_order_acquire)) return FX_PREC_F32;
+  std::lock_guard<std::mutex> lk(g_prec_mu);
+  for (const auto& e : g_prec)
+    if (e.first == s) return e.second;
+  return FX_PREC_F32;
+}
 
 // FX_PREC_BF16: the 128x64-tile launches with row-major operands take the bf16-arithmetic kernel
-bool bf16_eligible(const GemmPlan& P) {
-  return g_gemm_prec.load(std::memory_order_relaxed) == FX_PREC_BF16 && P.wide && (P.bk == ROWS || P.bk == COLS) &&
-         (P.ak == ROWS || P.ak == ROWS_CONV || P.ak == ROWS_CAT);
+bool bf16_eligible(const GemmPlan& P, hipStream_t s) {
+  return P.wide && (P.bk == ROWS || P.bk == COLS) && (P.ak == ROWS || P.ak == ROWS_CONV || P.ak == ROWS_CAT) &&
+         stream_precision(s) == FX_PREC_BF16;
 }
 
 template <int AK>
@@ -1848,7 +1837,7 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
   FX_TRY(plan_gemm(d, s, P));
   log_gemm(d, P);
   const GemmDev& g = P.g;
-  int st = bf16_eligible(P) ? launch_bf16(P, s)
+  int st = bf16_eligible(P, s) ? launch_bf16(P, s)
          : P.direct ? launch_direct(P.ak, P.bk, P.grid, P.block, s, g)
                     : (P.wide ? (wide8() ? launch_wide8(P.ak, P.bk, P.grid, s, g) : launch_wide(P.ak, P.bk, P.grid, s, g))
                               : launch_tiled(P.ak, P.bk, P.grid, s, g));
@@ -1861,10 +1850,7 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
 // launch when every member takes the direct kernel; otherwise one launch each, in order.
 // FX_GEMM_GROUP=0 disables the grouping (diagnostic A/B).
 int launch_gemm_group(const fx_gemm_desc* d, int n, hipStream_t s) {
-  static const bool on = [] {
-    const char* p = std::getenv("FX_GEMM_GROUP");
-    return !(p && p[0] == '0');
-  }();
+  const bool on = knobs().gemm_group;
   FX_REQUIRE(n >= 0 && n <= GMAX, "gemm group: 0..4 members");
   int live = 0, nsplit = 0;   // members with M, N > 0; of those, split-K members
   bool all_direct = on;
@@ -1957,12 +1943,21 @@ long long colsum_workspace_floats(int M, int N) { return (long long)cdiv(M, CS_R
 
 extern "C" {
 
-int fx_set_gemm_precision(int prec) {
+int fx_set_stream_precision(void* stream, int prec) {
   FX_REQUIRE(prec == FX_PREC_F32 || prec == FX_PREC_BF16, "gemm precision: FX_PREC_F32 or FX_PREC_BF16");
-  fx::g_gemm_prec.store(prec, std::memory_order_relaxed);
+  std::lock_guard<std::mutex> lk(fx::g_prec_mu);
+  const hipStream_t s = (hipStream_t)stream;
+  auto& v = fx::g_prec;
+  for (auto it = v.begin(); it != v.end(); ++it)
+    if (it->first == s) {
+      v.erase(it);
+      break;
+    }
+  if (prec != FX_PREC_F32) v.emplace_back(s, prec);
+  fx::g_prec_any.store(v.empty() ? 0 : 1, std::memory_order_release);
   return FX_OK;
 }
 
-int fx_get_gemm_precision(void) { return fx::g_gemm_prec.load(std::memory_order_relaxed); }
+int fx_get_stream_precision(void* stream) { return fx::stream_precision((hipStream_t)stream); }
 
 }  // extern "C"

@@ -212,8 +212,6 @@ __global__ __launch_bounds__(FT) void frl_kernel(FrlArgs g) {
 }  // namespace
 
 bool frl_supported(int F, const void* x, long long ldx, long long ld_other) {
-  const char* e = std::getenv("FX_MSTCN_FUSED");   // read per call: tests switch it at run time
-  if (!e || e[0] != '1') return false;
   return F == FN && ldx % 4 == 0 && ((uintptr_t)x & 15) == 0 && ld_other % 4 == 0;
 }
 

@@ -113,7 +113,8 @@ int launch_tattn_bwd(const float* q, long long ldq, const float* k, long long ld
                      long long lddk, float* dv, long long lddv, float* ws, hipStream_t s,
                      const TAttnOpts* opt = nullptr);
 
-// fused MS-TCN layer step (mstcn_fused.hip): conv GEMM (K = 3F) -> row-local epilogue -> 1x1 GEMM
+// fused MS-TCN layer step (mstcn_fused.hip, opt-in per call: fx_mstcn_params.fused_layers): conv GEMM
+// (K = 3F) -> row-local epilogue -> 1x1 GEMM
 bool frl_supported(int F, const void* x, long long ldx, long long ld_other);
 int launch_frl(const float* x, long long ldx, int M, int T, int dil, int dir, const float* w1, const float* bias1,
                int relu1, const float* resid1, long long ldr1, float* out1, long long ldo1, const float* w2,

@@ -70,23 +70,26 @@ def _defer_to_side(*tensors):
 
 
 class gemm_precision:
-    """Context manager (or plain call) for the library's GEMM arithmetic: "fp32" (default, the parity
-    path) or "bf16" (FX_PREC_BF16: frame-level forward / input-gradient products on bf16 MFMA with
-    fp32 accumulation and storage; a performance mode whose deviation bench.py reports)."""
+    """Context manager (or plain call) for the GEMM arithmetic of work enqueued on the CURRENT torch
+    stream: "fp32" (default, the parity path) or "bf16" (FX_PREC_BF16: frame-level forward /
+    input-gradient products on bf16 MFMA with fp32 accumulation and storage; a performance mode whose
+    deviation bench.py reports).  Per stream (fx_set_stream_precision): other streams and threads keep
+    their own setting."""
 
-    def __init__(self, mode):
+    def __init__(self, mode, stream=None):
         modes = {"fp32": nx.PREC_F32, "bf16": nx.PREC_BF16}
         if mode not in modes:
             raise ValueError(f"gemm precision {mode!r}: 'fp32' or 'bf16'")
         lib = nx.load()
-        self._prev = lib.fx_get_gemm_precision()
-        nx.check(lib.fx_set_gemm_precision(modes[mode]), "fx_set_gemm_precision")
+        self._stream = nx.stream() if stream is None else stream.cuda_stream
+        self._prev = lib.fx_get_stream_precision(self._stream)
+        nx.check(lib.fx_set_stream_precision(self._stream, modes[mode]), "fx_set_stream_precision")
 
     def __enter__(self):
         return self
 
     def __exit__(self, *exc):
-        nx.check(nx.load().fx_set_gemm_precision(self._prev), "fx_set_gemm_precision")
+        nx.check(nx.load().fx_set_stream_precision(self._stream, self._prev), "fx_set_stream_precision")
         return False
 
 
@@ -548,6 +551,11 @@ def x2y(mod, X, Y, Xpos, Ypos, rows=None):
 # MS-TCN stack
 # ---------------------------------------------------------------------------
 
+# fx_mstcn_params.fused_layers: the opt-in one-kernel MS-TCN layer (slower than the two tuned GEMMs at
+# the benchmark shape; kept for A/B and its own tests)
+MSTCN_FUSED_LAYERS = False
+
+
 def _ptr_array(ts):
     return (ctypes.c_void_p * max(len(ts), 1))(*[nx.ptr(t) for t in ts])
 
@@ -591,6 +599,7 @@ class MSTCNFn(torch.autograd.Function):
             setattr(prm, field, ctypes.cast(arr, ctypes.c_void_p))
         prm.w_out, prm.b_out = nx.ptr(w_out), nx.ptr(b_out)
         prm.dropout, prm.seed = float(drop_p), int(seed)
+        prm.fused_layers = int(MSTCN_FUSED_LAYERS)
         rows = x.shape[0]
         dev = x.device
         y = _empty(rows, cout, device=dev)

@@ -46,7 +46,7 @@ class MstcnParams(ctypes.Structure):
     _fields_ = [("cin", I), ("F", I), ("cout", I), ("num_layers", I), ("layernorm", I), ("in_map", I),
                 ("dil0", I), ("dil_factor", I), ("w_in", P), ("b_in", P), ("w_dil", P), ("b_dil", P), ("w_pw", P), ("b_pw", P),
                 ("ln_w", P), ("ln_b", P), ("w_out", P), ("b_out", P), ("dropout", F), ("seed", U),
-                ("side_defer", I), ("seq_off", P)]
+                ("side_defer", I), ("seq_off", P), ("fused_layers", I)]
 
 
 class Mstcn2Params(ctypes.Structure):
@@ -87,7 +87,7 @@ STATUS_GRU_TIMEOUT = 1   # FX_STATUS_GRU_TIMEOUT: a BiGRU workgroup gave up wait
 LOSS_MAXK = 512        # FX_LOSS_MAXK: matched columns of an attention loss term
 LOSS_NB = 128          # FX_LOSS_NB: row blocks per loss term
 TERM_CLASS, TERM_ATTN, TERM_INFONCE = 0, 1, 2
-PREC_F32, PREC_BF16 = 0, 1   # FX_PREC_*: GEMM arithmetic precision (fx_set_gemm_precision)
+PREC_F32, PREC_BF16 = 0, 1   # FX_PREC_*: GEMM arithmetic precision (fx_set_stream_precision)
 
 
 class LossTerm(ctypes.Structure):
@@ -178,8 +178,8 @@ SIGNATURES = {
     "fx_loss_terms_bwd": (I, [P, P, I, P, I, P, P, P]),
     "fx_match_cost": (I, [P, P, I, F, F, I, P, P]),
     "fx_eval_pred": (I, [P, P, I, F, P, P]),
-    "fx_set_gemm_precision": (I, [I]),
-    "fx_get_gemm_precision": (I, []),
+    "fx_set_stream_precision": (I, [P, I]),
+    "fx_get_stream_precision": (I, [P]),
     "fx_prof_enable": (I, [I, I]),
     "fx_prof_collect": (I, [I, ctypes.POINTER(D), ctypes.POINTER(D), ctypes.POINTER(D), ctypes.POINTER(I)]),
     "fx_prof_disable": (None, []),

@@ -292,6 +292,9 @@ typedef struct fx_mstcn_params {
   const int* seq_off;         /* ragged videos: host (nvid + 1) row offsets (video v owns rows
                                  [seq_off[v], seq_off[v+1]), zero padding at its own ends; nvid <= 16;
                                  T ignored); NULL: nvid videos of T rows */
+  int fused_layers;           /* 1: the fused one-kernel layer (conv -> epilogue -> 1x1, F = 256, no LN,
+                                 uniform videos) where it applies -- opt-in, measured even with the
+                                 two tuned GEMMs */
 } fx_mstcn_params;
 
 typedef struct fx_mstcn_grads {
@@ -655,7 +658,10 @@ int fx_eval_pred(const fx_video_attn* vids_host, const fx_video_attn* vids_dev, 
                  int32_t* pred, void* stream);
 
 /* ------------------------------------------------------------------------
- * GEMM arithmetic precision (process-wide).  FX_PREC_F32 (default): every
+ * GEMM arithmetic precision, per caller stream (the stream every entry point
+ * receives): fx_set_stream_precision(stream, prec) applies to the GEMMs later
+ * enqueued on that stream; streams never set (and the library's side stream, where
+ * weight gradients run) use FX_PREC_F32.  FX_PREC_F32 (default): every
  * product on v_mfma_f32_32x32x2_f32, the parity path.  FX_PREC_BF16: the
  * frame-level GEMMs with row-major operands (forward and input-gradient
  * products of the MS-TCN convs, in/out maps, projections) round their
@@ -666,8 +672,8 @@ int fx_eval_pred(const fx_video_attn* vids_host, const fx_video_attn* vids_dev, 
  * not bounded by the parity tests.
  * ---------------------------------------------------------------------- */
 enum { FX_PREC_F32 = 0, FX_PREC_BF16 = 1 };
-int fx_set_gemm_precision(int prec);
-int fx_get_gemm_precision(void);
+int fx_set_stream_precision(void* stream, int prec);
+int fx_get_stream_precision(void* stream);
 
 /* ----------------------------------------------------------------------
  * Profiling hooks: HIP-event timing of every launch of a kernel class

@@ -1,4 +1,4 @@
-"""FX_PREC_BF16 performance mode (fx_set_gemm_precision, BASELINE configs[1]).
+"""FX_PREC_BF16 performance mode (fx_set_stream_precision, BASELINE configs[1]).
 
 The bf16 kernel rounds both operands to bf16 and accumulates in fp32, so it is checked against a
 float64 product of the bf16-ROUNDED inputs (fp32-accumulation tolerance), on the shapes the mode
@@ -65,7 +65,7 @@ def test_bf16_gemm_matches_rounded_product(M, N, K, split, epi, bt):
     assert err <= 2e-5 * (1 + ref_bf.abs().max().item()) + 1e-6 * math.sqrt(K), err
     # the bf16 arithmetic really ran: nearer the rounded product than the exact one
     assert (got - ref).abs().max().item() > 10 * err
-    assert nx.load().fx_get_gemm_precision() == nx.PREC_F32
+    assert nx.load().fx_get_stream_precision(nx.stream()) == nx.PREC_F32
 
 
 def test_bf16_conv_gemm_matches_rounded_product():
@@ -96,31 +96,58 @@ def test_bf16_conv_gemm_matches_rounded_product():
     assert err <= 2e-5 * (1 + ref.abs().max().item()), err
 
 
-def test_bf16_mode_fact_clip_step_deviation():
-    """One FACT_CLIP forward + loss + backward at T=1024 in each mode: the bf16 frame logits stay
-    within a loose bound of the fp32 ones (the mode's deviation is reported by bench.py), and the
-    loss and every gradient are finite."""
+def test_bf16_precision_is_per_stream():
+    """fx_set_stream_precision: a GEMM enqueued on another stream while one stream is in bf16 mode runs
+    fp32 (bitwise the fp32 result), and the bf16 stream's GEMM differs from it."""
+    M, N, K = 8192, 256, 512
+    A, B = _r(M, K, seed=1).float().to(DEV), _r(N, K, seed=2, scale=K ** -0.5).float().to(DEV)
+    c32, c_other, c16 = (torch.zeros(M, N, device=DEV) for _ in range(3))
+    fxf.gemm(M, N, K, _rows(A), _rows(B), c32, N)
+    other = torch.cuda.Stream()
+    with fxf.gemm_precision("bf16"):
+        fxf.gemm(M, N, K, _rows(A), _rows(B), c16, N)
+        other.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(other):
+            assert nx.load().fx_get_stream_precision(nx.stream()) == nx.PREC_F32
+            fxf.gemm(M, N, K, _rows(A), _rows(B), c_other, N)
+        torch.cuda.current_stream().wait_stream(other)
+    torch.cuda.synchronize()
+    assert torch.equal(c_other, c32)
+    assert not torch.equal(c16, c32)
+
+
+def test_bf16_mode_fact_clip_T2048_deviation():
+    """BASELINE configs[1] as stated: FACT_CLIP, HAViD-holdout dims, T=2048, 2 videos in one lockstep
+    batch, forward + loss + backward in each mode on the same weights and videos.  The bf16 mode's
+    last-block per-frame logits stay within 5e-3 of the fp32 path's (the bench reports ~1e-3 at
+    T=4096), per-frame argmax agrees on >= 99.9 % of frames, the loss within 1e-2 relative, and every
+    gradient is finite; the TDU segment counts of both modes are reported (near-tied argmax decisions
+    may move them)."""
     import bench
     cfg = bench.make_cfg()
-    T = 1024
+    T = 2048
     net, _ = bench.build_model(cfg, bench.D_IN, bench.NCLS, DEV, seed=0)
     net.train()
-    f, lab = bench.make_video(T, bench.D_IN, bench.NCLS, cfg, seed=1)
-    seqs = [torch.from_numpy(f).to(DEV)]
-    labels = [torch.from_numpy(lab).to(DEV)]
+    vids = [bench.make_video(T, bench.D_IN, bench.NCLS, cfg, seed=s) for s in (3, 4)]
+    seqs = [torch.from_numpy(f).to(DEV) for f, _ in vids]
+    labels = [torch.from_numpy(l_).to(DEV) for _, l_ in vids]
 
     def run():
         net.zero_grad(set_to_none=True)
         loss, _ = net(seqs, labels, compute_loss=True)
         loss.backward()
-        logits = net.block_list[-1].frame_clogit.detach().clone()
+        last = net.block_list[-1]
+        logits = [r["frame_clogit"][:, 0].detach().clone() for r in last._vrec]
         grads = [p.grad.detach().clone() for p in net.parameters() if p.grad is not None]
-        return float(loss), logits, grads
+        return float(loss), logits, grads, bench.video_segments(net)
 
-    l32, z32, g32 = run()
+    l32, z32, g32, s32 = run()
     with fxf.gemm_precision("bf16"):
-        l16, z16, g16 = run()
+        l16, z16, g16, s16 = run()
+    print(f"TDU segments fp32 {s32} bf16 {s16}")
     assert math.isfinite(l16) and all(torch.isfinite(g).all() for g in g16)
-    dev = (z16 - z32).abs().max().item()
-    assert dev < 0.25 * (1 + z32.abs().max().item()), dev
-    assert abs(l16 - l32) < 0.05 * (1 + abs(l32))
+    dev = max((a - b).abs().max().item() for a, b in zip(z16, z32))
+    agree = sum(int((a.argmax(-1) == b.argmax(-1)).sum()) for a, b in zip(z16, z32)) / sum(b.shape[0] for b in z32)
+    assert dev <= 5e-3, (dev, s32, s16)
+    assert agree >= 0.999, (agree, s32, s16)
+    assert abs(l16 - l32) <= 1e-2 * abs(l32), (l16, l32)

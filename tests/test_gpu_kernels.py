@@ -228,21 +228,32 @@ def test_linear_padded_k_on_wider_input(M, K, N):
 
 
 @pytest.mark.parametrize("fused", ["0", "1"])
-@pytest.mark.parametrize("T,nvid,nl", [(1000, 2, 10), (4096, 1, 3), (37, 3, 4)])
+@pytest.mark.parametrize("T,nvid,nl", [(1000, 2, 10), (4096, 1, 3), (37, 3, 4), ((1000, 777, 1301), 3, 10),
+                                       ((64, 5, 200), 3, 4)])
 def test_mstcn_fused_layers_match_fp64(T, nvid, nl, fused, monkeypatch):
-    """F = 256, both MS-TCN paths: the two-GEMM layers and (FX_MSTCN_FUSED=1) the fused layer
-    kernel (mstcn_fused.hip) forward + fused dX chain backward: output, input gradient and every
-    weight gradient vs the float64 MS-TCN restatement (ragged row counts, dilations up to
-    2^(nl-1), several videos: no leakage across video edges)."""
+    """F = 256, both MS-TCN paths: the two-GEMM layers and (fx_mstcn_params.fused_layers) the fused
+    layer kernel (mstcn_fused.hip) forward + fused dX chain backward: output, input gradient and every
+    weight gradient vs the float64 MS-TCN restatement (odd row counts, dilations up to 2^(nl-1),
+    several videos: no leakage across video edges).  A tuple T is a ragged batch (row offsets through
+    the conv GEMMs; per-video weight-gradient launches; the fused layer declines ragged videos)."""
+    from factmx.dp import FlatGradReducer
     from factmx.models.basic import MSTCN
-    monkeypatch.setenv("FX_MSTCN_FUSED", fused)
+    monkeypatch.setattr(fxf, "MSTCN_FUSED_LAYERS", fused == "1")
     torch.manual_seed(0)
     mod = MSTCN(96, 256, 40, nl, dropout=0.0, ln=False, in_map=True).to(DEV).train()
-    rows = T * nvid
+    Ts = list(T) if isinstance(T, tuple) else [T] * nvid
+    off = [0]
+    for t_ in Ts:
+        off.append(off[-1] + t_)
+    rows = off[-1]
     x = _r(rows, 96, seed=11)
     g = _r(rows, 40, seed=12)
     xd = x.float().to(DEV).requires_grad_(True)
-    y = fxf.mstcn(mod, xd, T=T, nvid=nvid)
+    if isinstance(T, tuple):
+        FlatGradReducer(mod.parameters())        # uniformly strided gradients: the deferred batched dW path
+        y = fxf.mstcn(mod, xd, T=0, nvid=nvid, seq_off=off)
+    else:
+        y = fxf.mstcn(mod, xd, T=T, nvid=nvid)
     saved = y.grad_fn.saved_tensors[1].detach().double().cpu()   # (freed by the backward)
     (y * g.float().to(DEV)).sum().backward()
     # the float64 restatement takes the GPU's own ReLU decisions (z > 0 of the saved activations):
@@ -255,7 +266,7 @@ def test_mstcn_fused_layers_match_fp64(T, nvid, nl, fused, monkeypatch):
     xr = x.clone().requires_grad_(True)
     outs = []
     for v in range(nvid):
-        sl = slice(v * T, (v + 1) * T)
+        sl = slice(off[v], off[v + 1])
         h = fo.linear(xr[sl], P["conv_1x1.weight"], P["conv_1x1.bias"])
         for i in range(nl):
             q = f"layers.{i}."

@@ -48,7 +48,7 @@ int main() {
   float* c = dalloc((size_t)M * N);
   if (!a || !b || !c) return 1;
   for (int prec = 0; prec < 2; ++prec) {
-  fx_set_gemm_precision(prec);
+  fx_set_stream_precision(nullptr, prec);
   printf("-- precision %s\n", prec ? "bf16" : "fp32");
   for (int conv = 0; conv < 2; ++conv) {
     for (int K : {192, 384, 768, 1536, 3072}) {
@@ -59,7 +59,7 @@ int main() {
     }
   }
   }
-  fx_set_gemm_precision(0);
+  fx_set_stream_precision(nullptr, 0);
   for (int K : {256, 768}) {
     const double us = run(4096, N, K, a, b, c, 0);
     printf("rows x rows  M=4096 N=%d K=%5d  %8.2f us  %7.1f TF/s\n", N, K, us, 2.0 * 4096 * N * K / us / 1e6);
