@@ -38,7 +38,7 @@ def build_model(meta, cfg):
 
 
 @pytest.mark.parametrize("name", ["tiny_clip", "tiny_clip_iid", "tiny_fact_m2"])
-def test_tiny_end_to_end_vs_reference(name):
+def test_tiny_end_to_end_vs_reference(name, monkeypatch):
     fx = load_fixture(name)
     meta = tiny_meta(fx)
     cfg = cfg_from_meta(meta)
@@ -53,6 +53,15 @@ def test_tiny_end_to_end_vs_reference(name):
         captured["m"] = r
         return r
     net.mcriterion.match = spy
+    # lockstep path (every batch, single videos included): device match cost + host Hungarian
+    from factmx.models import vloss as vl
+    orig_em = vl.EarlyMatch.matches
+
+    def spy_em(self, Q):
+        r = orig_em(self, Q)
+        captured["m"] = tuple(torch.from_numpy(x) for x in r[0])
+        return r
+    monkeypatch.setattr(vl.EarlyMatch, "matches", spy_em)
     seq = torch.from_numpy(feats).float().to(DEV)
     lab = torch.from_numpy(label).to(DEV)
     total, saves = net([seq], [lab], compute_loss=True)

@@ -60,7 +60,12 @@ def test_oracle_end_to_end(name):
     total, fact, con, m = fo.video_loss(spec, out, label, text_t)
     total.backward()
 
-    tol = dict(rtol=1e-9, atol=1e-11)
+    # The reference's sinusoid table is float32 (basic.py:92-99) and ATen's float32 exp/sin/cos
+    # dispatch per host CPU (MKL VML / SLEEF), so the table moves by an ulp between hosts;
+    # every tensor downstream of it is compared at float32-table precision when fpos is on.
+    f32 = spec["fpos"]
+    tol = dict(rtol=1e-5, atol=1e-5) if f32 else dict(rtol=1e-9, atol=1e-11)
+    ltol = 1e-6 if f32 else 1e-10
     for i, rec in enumerate(out["blocks"]):
         p = f"block{i}/"
         np.testing.assert_allclose(rec["frame_clogit"].detach().numpy(), fx[p + "frame_clogit"], **tol)
@@ -77,13 +82,13 @@ def test_oracle_end_to_end(name):
     np.testing.assert_array_equal(pred.numpy(), fx["pred"])
     np.testing.assert_array_equal(m[0].numpy(), fx["match_a"])
     np.testing.assert_array_equal(m[1].numpy(), fx["match_s"])
-    np.testing.assert_allclose(total.item(), fx["loss"][0], rtol=1e-10)
+    np.testing.assert_allclose(total.item(), fx["loss"][0], rtol=ltol)
     if clip:
         np.testing.assert_allclose(out["proj"].detach().numpy(), fx["proj"], **tol)
-        np.testing.assert_allclose(fact.item(), fx["fact_loss"][0], rtol=1e-10)
-        np.testing.assert_allclose(con.item(), fx["contrastive_loss"][0], rtol=1e-10)
+        np.testing.assert_allclose(fact.item(), fx["fact_loss"][0], rtol=ltol)
+        np.testing.assert_allclose(con.item(), fx["contrastive_loss"][0], rtol=ltol)
     for n, t in P.items():
-        check_grad(fx, "", n, t.grad, rtol=1e-7, atol=1e-10)
+        check_grad(fx, "", n, t.grad, rtol=1e-5 if f32 else 1e-7, atol=1e-6 if f32 else 1e-10)
 
 
 # ---------------------------------------------------------------------------
