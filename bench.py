@@ -18,6 +18,7 @@ the weights and therefore S; the S it ends with is reported there).
 
   python bench.py [--gpus N --steps K --warmup W]
   python bench.py --config breakfast         # BASELINE configs[0]: vanilla FACT, T=512
+  python bench.py --config shipped           # havid_view0_lh_pt_holdout.yaml as shipped (training mode)
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 ``python bench.py --gpus N`` (N > 1, no launcher environment) starts the N ranks itself as a
@@ -41,6 +42,9 @@ import torch  # noqa: E402
 DOMINANT_KERNEL = "gemm_f32_wide8_kernel<1, 0>"   # rocprofv3 name: fx::(anonymous namespace)::gemm_f32_wide8_kernel<1, 0>
 METRIC = "frames/sec FACT_CLIP fwd+bwd, T=4096 D=2048 Nact=32, at 1/2/4/8 GPUs"
 METRIC_BREAKFAST = "frames/sec FACT fwd+bwd, Breakfast dims T=512 D=2048 Nact=60 (BASELINE configs[0])"
+METRIC_SHIPPED = ("frames/sec FACT_CLIP fwd+bwd, havid_view0_lh_pt_holdout.yaml as shipped (ntoken 75, dropout 0.2, "
+                  "cmr 0.3, time mask on), ragged T=4096+2900 D=2048")
+SHIPPED_RATIO = 2900 / 4096      # second video's length relative to --T (a ragged batch, dataset.py:106-131)
 F32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 HOLDOUT = [51, 53, 61, 67, 56]   # havid_view0_lh_pt_holdout.yaml
@@ -136,11 +140,31 @@ def build_model(cfg, D, C, device, seed=0, clip=True):
     return net.to(device), text
 
 
+def make_cfg_shipped():
+    """havid_view0_lh_pt_holdout.yaml exactly as the reference ships it for training: ntoken 75,
+    Bi.dropout 0.2, FACT.cmr 0.3 (Dropout2d channel masking), time mask on (m 5, p 0.05, t 30),
+    Loss.nullw -1 (derived by train_tools.py:54-71 from the transcript length, here 10)."""
+    cfg = make_cfg(ntoken=75)
+    cfg.Bi.dropout = 0.2
+    cfg.FACT.cmr = 0.3
+    cfg.TM.update(dict(use=True, inplace=True, m=5, p=0.05, t=30))
+    return cfg
+
+
 def workload(name):
     """(cfg, D, C, T default, videos per rank, FACT_CLIP?, metric) of a named bench workload."""
     if name == "breakfast":
         return make_cfg_breakfast(), D_IN, BF_NCLS, BF_T, 4, False, METRIC_BREAKFAST
+    if name == "shipped":
+        return make_cfg_shipped(), D_IN, NCLS, T_DEFAULT, 2, True, METRIC_SHIPPED
     return make_cfg(), D_IN, NCLS, T_DEFAULT, 2, True, METRIC
+
+
+def video_lengths(name, T, nv):
+    """Frames of each video of a rank's step: equal lengths, except the shipped config's ragged pair."""
+    if name == "shipped":
+        return [T if v % 2 == 0 else int(round(T * SHIPPED_RATIO)) for v in range(nv)]
+    return [T] * nv
 
 
 def video_segments(net):
@@ -164,7 +188,7 @@ def traffic_from_profiles(kernel_prefix, name="pmc_dominant.json"):
     return None
 
 
-def bf16_mode(net, step, nv, T, steps, warmup, fxf):
+def bf16_mode(net, step, frames_per_step, steps, warmup, fxf):
     """Time `steps` fixed-weight steps with fx_set_stream_precision(FX_PREC_BF16) and compare its frame
     logits (last block, every video) and TDU segment counts with the fp32 path's."""
     def logits():
@@ -188,7 +212,7 @@ def bf16_mode(net, step, nv, T, steps, warmup, fxf):
     dev = max((a - b).abs().max().item() for a, b in zip(z16, z32))
     scale = max(b.abs().max().item() for b in z32)
     agree = sum(int((a.argmax(-1) == b.argmax(-1)).sum()) for a, b in zip(z16, z32)) / sum(b.shape[0] for b in z32)
-    return dict(value=round(nv * T * steps / el, 1), unit="frames/s", ms_per_step=round(1e3 * el / steps, 3),
+    return dict(value=round(frames_per_step * steps / el, 1), unit="frames/s", ms_per_step=round(1e3 * el / steps, 3),
                 dtype="bf16 products, fp32 accumulation/storage (FX_PREC_BF16)",
                 frame_logit_max_abs_dev=round(dev, 5), frame_logit_max_abs=round(scale, 4),
                 frame_argmax_agreement=round(agree, 5), tdu_segments=s16, tdu_segments_fp32=s32,
@@ -218,7 +242,7 @@ def attention_roofline(kernel, ms, fl, by, cnt):
                 tflops=round(fl.value / n / (avg_ms * 1e-3) / 1e12, 2))
 
 
-def cpu_baseline(wl, T, videos_seeds, min_seconds=10.0, min_steps=2):
+def cpu_baseline(wl, Ts, videos_seeds, min_seconds=10.0, min_steps=2):
     """The CPU oracle (fp32 PyTorch restatement pinned to the reference) timed on host cores: one
     video per step, full T, forward + prediction + loss + backward with FIXED weights (the same
     unit as the GPU step), repeated until >= min_seconds of CPU work (a bounded sample).  Also
@@ -231,7 +255,7 @@ def cpu_baseline(wl, T, videos_seeds, min_seconds=10.0, min_steps=2):
     spec = fo.resolve_spec(cfg, D, C, clip=clip)
     P = {n: p.detach().clone().float().requires_grad_(True) for n, p in net.named_parameters()}
     txt = text if clip else None
-    vids = [make_video(T, D, C, cfg, seed=s) for s in videos_seeds]
+    vids = [make_video(Tv, D, C, cfg, seed=s) for Tv, s in zip(Ts, videos_seeds)]
 
     def step(v=0):
         for p in P.values():
@@ -247,18 +271,24 @@ def cpu_baseline(wl, T, videos_seeds, min_seconds=10.0, min_steps=2):
         for f, _ in vids:
             out = fo.forward(spec, P, torch.from_numpy(f))
             S.append([len(r["tdu"].starts) for r in out["blocks"] if r["type"] == "U"])
-    with FlopCounterMode(display=False) as fc:
-        step()
-    flops = fc.get_total_flops()
+    flops = 0          # algorithmic FLOPs of one step over every bench video
+    for v in range(len(vids)):
+        with FlopCounterMode(display=False) as fc:
+            step(v)
+        flops += fc.get_total_flops()
     t0 = time.perf_counter()
-    n = 0
+    n = frames = 0
     while n < min_steps or time.perf_counter() - t0 < min_seconds:
         step(n % len(vids))
+        frames += Ts[n % len(vids)]
         n += 1
     dt = time.perf_counter() - t0
-    return dict(value=round(n * T / dt, 1), unit="frames/s", cores=torch.get_num_threads(), kind="port",
-                sample=f"{n} steps x 1 video (T={T}, seg10, the bench videos in turn) fwd+loss+bwd, fixed weights, "
-                       f"oracle fp32 (1 untimed warm-up step, {dt:.1f} s timed)"), flops, S
+    stoch = " (the oracle has no dropout / channel masking / time mask: those stay off in the CPU sample)" \
+        if wl == "shipped" else ""
+    return dict(value=round(frames / dt, 1), unit="frames/s", cores=torch.get_num_threads(), kind="port",
+                sample=f"{n} steps x 1 video (T={'/'.join(str(t) for t in sorted(set(Ts)))}, seg10, the bench videos "
+                       f"in turn) fwd+loss+bwd, fixed weights, oracle fp32 (1 untimed warm-up step, {dt:.1f} s "
+                       f"timed){stoch}"), flops, S
 
 
 def _free_port():
@@ -291,8 +321,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=["havid", "breakfast"], default="havid",
-                    help="havid: FACT_CLIP T=4096 (the BASELINE metric); breakfast: vanilla FACT T=512")
+    ap.add_argument("--config", choices=["havid", "breakfast", "shipped"], default="havid",
+                    help="havid: FACT_CLIP T=4096 (the BASELINE metric); breakfast: vanilla FACT T=512; "
+                         "shipped: the reference's havid holdout yaml unchanged (dropout, cmr, time mask, "
+                         "ntoken 75), ragged T=4096+2900")
     ap.add_argument("--videos", type=int, default=None, help="videos per rank per step (yaml batch_size)")
     ap.add_argument("--T", type=int, default=None)
     ap.add_argument("--adam-steps", type=int, default=None,
@@ -329,9 +361,10 @@ def main():
     net.train()
     dp = DataParallel(net)      # flat gradient buckets (+ rank-0 weight broadcast, overlapped all-reduce)
     seeds = [1 + rank * nv + v for v in range(nv)]
+    Ts = video_lengths(args.config, T, nv)
     seqs, labels = [], []
-    for s in seeds:
-        f, l_ = make_video(T, D, C, cfg, seed=s)
+    for s, Tv in zip(seeds, Ts):
+        f, l_ = make_video(Tv, D, C, cfg, seed=s)
         seqs.append(torch.from_numpy(f).to(dev))
         labels.append(torch.from_numpy(l_).to(dev))
 
@@ -381,7 +414,7 @@ def main():
     bf16 = None
     if world == 1 and not args.no_bf16:
         from factmx import functional as fxf
-        bf16 = bf16_mode(net, step, nv, T, args.steps, args.warmup, fxf)
+        bf16 = bf16_mode(net, step, sum(Ts), args.steps, args.warmup, fxf)
 
     # the reference train step (clip_grad_norm_ + Adam), timed after the fixed-weight steps
     adam = None
@@ -404,12 +437,12 @@ def main():
             t = torch.tensor([ea], device=dev, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             ea = t.item()
-        adam = dict(value=round(world * nv * T * adam_steps / ea, 1), unit="frames/s", steps=adam_steps,
+        adam = dict(value=round(world * sum(Ts) * adam_steps / ea, 1), unit="frames/s", steps=adam_steps,
                     ms_per_step=round(1e3 * ea / adam_steps, 3), tdu_segments_after=video_segments(net),
                     note="zero_grad + fwd + loss + bwd (+all-reduce) + clip_grad_norm_(10) + Adam(lr 1e-4); the "
                          "updates move the weights, so S drifts from the fixed-weight value")
 
-    frames = world * nv * T * args.steps
+    frames = world * sum(Ts) * args.steps
     value = frames / elapsed
     if rank == 0:
         avg_ms = ms.value / max(cnt.value, 1)
@@ -431,23 +464,29 @@ def main():
         line = dict(metric=metric, value=round(value, 1), unit="frames/s", n_gpus=world, steps=args.steps,
                     warmup=args.warmup, ms_per_step=round(1e3 * elapsed / args.steps, 3), higher_is_better=True,
                     scaling="weak", vs_baseline=None, dtype="fp32", data="synthetic",
-                    config=dict(workload=(f"FACT_CLIP HAViD-holdout dims, seg10 synthetic, T={T}" if clip else
+                    config=dict(workload=(f"FACT_CLIP havid_view0_lh_pt_holdout.yaml as shipped (training mode: "
+                                          f"dropout 0.2, cmr 0.3, time mask, ntoken 75), seg10 synthetic, "
+                                          f"ragged T={'+'.join(map(str, Ts))}" if args.config == "shipped" else
+                                          f"FACT_CLIP HAViD-holdout dims, seg10 synthetic, T={T}" if clip else
                                           f"FACT (vanilla) Breakfast dims, seg10 synthetic, T={T}"),
-                                model="FACT_CLIP" if clip else "FACT", T=T, D=D, Nact=cfg.FACT.ntoken, C=C,
+                                model="FACT_CLIP" if clip else "FACT", T=T, video_lengths=Ts, D=D,
+                                Nact=cfg.FACT.ntoken, C=C,
                                 videos_per_rank=nv, global_batch=world * nv, seq_len=T,
                                 parallelism=f"dp{world}", weights="fixed (no optimizer update in the timed steps)",
                                 tdu_segments=S, tdu_segments_after_timing=S_after),
                     roofline=roofline, roofline_attention=roofline_attention, train_step_with_adam=adam,
                     bf16_mode=bf16)
         if world == 1 and not args.no_cpu_baseline:
-            cb, step_flops, S_oracle = cpu_baseline(args.config, T, seeds)
+            cb, step_flops, S_oracle = cpu_baseline(args.config, Ts, seeds)
             line["cpu_baseline"] = cb
             line["tdu_segments_oracle"] = S_oracle
-            line["tdu_segments_match_oracle"] = S_oracle == S
+            # dropout / channel masking / time mask (shipped config) draw new masks every step: S is then
+            # the last timed step's, and the oracle (no stochastic layers) is no reference for it
+            line["tdu_segments_match_oracle"] = None if args.config == "shipped" else S_oracle == S
             step_time = elapsed / args.steps
-            line["step_mfma_frac"] = round(step_flops * nv / step_time / 1e12 / F32_MFMA_PEAK_TFLOPS, 5)
-            line["step_gflop_per_video"] = round(step_flops / 1e9, 2)
-            if S_oracle != S:
+            line["step_mfma_frac"] = round(step_flops / step_time / 1e12 / F32_MFMA_PEAK_TFLOPS, 5)
+            line["step_gflop_per_video"] = round(step_flops / nv / 1e9, 2)
+            if S_oracle != S and args.config != "shipped":
                 log(f"WARNING: GPU TDU segments {S} differ from the oracle's {S_oracle}")
         else:
             line["cpu_baseline"] = None

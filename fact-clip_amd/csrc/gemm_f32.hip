@@ -191,7 +191,9 @@ __device__ __forceinline__ float4 ldg4(const float* p) { return *reinterpret_cas
 // in-range address and replaced by a select (0, or 1 for the virtual ones row) -- so the
 // pipelined loop has no bounds branches for the compiler to drain vmcnt at.  !FAST fetches
 // element by element with full bounds checks (edge shapes, gathers, concatenations).
-template <int KIND, bool FAST, int NJ = 4>
+// KW = 32 (the split-precision kernel's 32-deep stages, 512 threads, NJ = 1): row-major kinds
+// take row tid>>3 and k (tid&7)*4; col-major kinds keep k tid>>4 and rows (tid&15)*4.
+template <int KIND, bool FAST, int NJ = 4, int KW = 64>
 struct Loader {
   static constexpr int RSTEP = 64 / NJ;   // row (or k) step between a thread's NJ vectors
   static constexpr bool kRowImg = KIND <= ROWS_GEN || KIND == ROWS_CAT;
@@ -227,8 +229,13 @@ struct Loader {
     R = R_;
     K = K_;
     r0 = r0_;
-    ta = tid >> 4;
-    tb = (tid & 15) * 4;
+    if (KW == 32 && kRowImg) {
+      ta = tid >> 3;
+      tb = (tid & 7) * 4;
+    } else {
+      ta = tid >> 4;
+      tb = (tid & 15) * 4;
+    }
     if (!FAST) return;
     if (kRowImg) {
       rok = 0;
@@ -1132,6 +1139,186 @@ __global__ __launch_bounds__(W8T) void gemm_bf16_wide8_kernel(GemmDev g) {
   tile_epilogue(g, bidx, rbase, col, acc);
 }
 
+// ---------------------------------------------------------------- fp32 by split bf16 (FX_PREC_F32S)
+// fp32 GEMM arithmetic on the bf16 matrix cores: every fp32 operand x is split into NP bf16 pieces
+// x = p0 + p1 + p2 (p0 = bf16(x), p1 = bf16(x - p0), p2 = bf16(x - p0 - p1): 8 significant bits each,
+// so three pieces carry all 24 bits of an fp32 mantissa) and a.b is summed as the NP (NP + 1) / 2
+// piece products of order <= NP - 1 (NP = 3: p0q0 + p0q1 + p1q0 + p0q2 + p2q0 + p1q1; the dropped
+// terms are below 3 * 2^-24 |a b|, the size of fp32's own rounding of each product's addition).
+// Every piece product is exact in the MFMA's fp32 accumulator.  v_mfma_f32_32x32x16_bf16 runs at 16x
+// the f32 MFMA rate, so NP = 3 (6 products) is 2.7x the f32 matrix rate at fp32 accuracy; NP = 2
+// (3 products, ~2^-16 relative) exists for measurement only.
+// Tile and waves as the f32 wide8 kernel (128 x 64, 8 waves, one 32x32 accumulator pair each), with
+// 32-deep stages: a stage's fp32 float4 loads are split when they are written to LDS (each element
+// once per tile, not once per reading wave), the images hold the NP pieces of A0 | A1 | B as
+// [row][k] bf16 with 80-B rows (conflict-free ds_read_b128: 8 consecutive rows start 20 banks
+// apart), 3 LDS slots (138 KB at NP = 3), a stage's loads issued 4 stages ahead in one of 3 register
+// sets and written to LDS 2 stages later.  Lane half h of MFMA q takes k in [16q + 8h, +8) for A and
+// B alike (the k order inside the sum is free as long as both operands agree).
+constexpr int SKW = 32;                 // k per stage
+constexpr int SRS = 40;                 // bf16 row stride of a piece image (80 B)
+constexpr int SIMG = 64 * SRS;          // bf16 per piece image
+typedef __bf16 bf16x8s __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4s __attribute__((ext_vector_type(4)));
+
+template <int NP>
+__device__ __forceinline__ void split_pieces(float x, __bf16* p) {
+  p[0] = (__bf16)x;
+  if (NP > 1) {
+    const float r1 = x - (float)p[0];
+    p[1] = (__bf16)r1;
+    if (NP > 2) p[2] = (__bf16)(r1 - (float)p[1]);
+  }
+}
+
+// one operand stage (one float4 per thread) into its NP piece images (image p at img + p * SIMG)
+template <int KIND, int NP>
+__device__ __forceinline__ void store_split(const Loader<KIND, true, 1, SKW>& L, __bf16* img, float4 v, unsigned vm) {
+  if (Loader<KIND, true, 1, SKW>::kRowImg) {
+    const float4 x = (vm & 1u) ? v : zero4();
+    const float e[4] = {x.x, x.y, x.z, x.w};
+    bf16x4s b[NP];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      __bf16 pc[3];
+      split_pieces<NP>(e[q], pc);
+#pragma unroll
+      for (int p = 0; p < NP; ++p) b[p][q] = pc[p];
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) *reinterpret_cast<bf16x4s*>(img + p * SIMG + L.ta * SRS + L.tb) = b[p];
+  } else {
+    // COLS (B = W stored [k][n]): 4 consecutive n at one k, written transposed into [n][k]
+    const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float one = ((L.omask >> q) & 1u) ? 1.f : 0.f;
+      const float x = ((L.emask >> q) & 1u) ? e[q] : one;
+      __bf16 pc[3];
+      split_pieces<NP>(x, pc);
+#pragma unroll
+      for (int p = 0; p < NP; ++p) img[p * SIMG + (L.tb + q) * SRS + L.ta] = pc[p];
+    }
+  }
+}
+
+template <int AK, int BKd>
+struct SpSet {
+  float4 a0, a1, b;
+  unsigned m0, m1, mb;
+};
+
+template <int AK, int BKd, int NP>
+__global__ __launch_bounds__(W8T) void gemm_split_wide8_kernel(GemmDev g) {
+  constexpr int SSLOT = 3 * NP * SIMG;   // [A0 pieces | A1 pieces | B pieces]
+  __shared__ __bf16 lds[3 * SSLOT];
+  __shared__ int flag[1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, li = lane & 31, lh = lane >> 5;
+  const int ai = wm >> 1, wr = (wm & 1) * 32;
+  int tx, ty, z;
+  block_tile(g, tx, ty, z);
+  const int n0 = tx * BN, m0 = ty * WBM;
+  const int bidx = z / g.split, sk = z - bidx * g.split;
+  const int nkt = (g.K + SKW - 1) / SKW;
+  // kt_per_split counts 64-deep stages (the host's split plan): two 32-deep stages each
+  const int kt0 = sk * g.kt_per_split * 2;
+  const int kt1 = min(nkt, kt0 + g.kt_per_split * 2);
+  Loader<AK, true, 1, SKW> la0, la1;
+  Loader<BKd, true, 1, SKW> lb;
+  const float* pa = g.a.ptr + (long long)bidx * g.a.batch_stride;
+  la0.init(batch_op_a(g.a, g.a_dil_b1, bidx), pa, m0, g.M, g.K, tid, g.soff, g.nsoff);
+  la1.init(batch_op_a(g.a, g.a_dil_b1, bidx), pa, m0 + BM, g.M, g.K, tid, g.soff, g.nsoff);
+  lb.init(batch_op_b(g.b, g.b_dil_growth, bidx), g.b.ptr + (long long)bidx * g.b.batch_stride, n0, g.N, g.K, tid,
+          g.soff, g.nsoff);
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    acc0[i] = 0.f;
+    acc1[i] = 0.f;
+  }
+  const int n = kt1 - kt0;
+  if (n > 0) {
+    const int klast = (kt1 - 1) * SKW;
+    auto kof = [&](int i) { return min((kt0 + i) * SKW, klast); };
+    auto ld = [&](int i, SpSet<AK, BKd>& r) FX_INLINE {
+      la0.load(kof(i), &r.a0, r.m0);
+      la1.load(kof(i), &r.a1, r.m1);
+      lb.load(kof(i), &r.b, r.mb);
+    };
+    auto st = [&](__bf16* slot, const SpSet<AK, BKd>& r) FX_INLINE {
+      store_split<AK, NP>(la0, slot, r.a0, r.m0);
+      store_split<AK, NP>(la1, slot + NP * SIMG, r.a1, r.m1);
+      store_split<BKd, NP>(lb, slot + 2 * NP * SIMG, r.b, r.mb);
+    };
+    // prologue: stages 0, 1 in LDS slots 0, 1; stages 2, 3 in flight (set s % 3 holds stage s)
+    SpSet<AK, BKd> r0, r1, r2;
+    ld(0, r0);
+    ld(1, r1);
+    ld(2, r2);
+    st(lds, r0);
+    ld(3, r0);
+    st(lds + SSLOT, r1);
+    __syncthreads();
+    // stage i: MFMAs on slot i % 3; loads of stage i + 4 into set (i + 1) % 3; stage i + 2 (set
+    // (i + 2) % 3, loaded two stages ago) written to slot (i + 2) % 3, read at stage i - 1
+    auto stage = [&](int i, SpSet<AK, BKd>& lset, const SpSet<AK, BKd>& sset) FX_INLINE {
+      const __bf16* cur = lds + (i % 3) * SSLOT;
+      const __bf16* ia = cur + ai * NP * SIMG + (wr + li) * SRS + 8 * lh;
+      const __bf16* ib = cur + 2 * NP * SIMG + (wn * 32 + li) * SRS + 8 * lh;
+      bf16x8s fa[2][NP], fb[2][NP];
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          fa[q][p] = *reinterpret_cast<const bf16x8s*>(ia + p * SIMG + 16 * q);
+          fb[q][p] = *reinterpret_cast<const bf16x8s*>(ib + p * SIMG + 16 * q);
+        }
+      ld(i + 4, lset);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if (NP > 2) {
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[q][1], fb[q][1], acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[q][2], fb[q][0], acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[q][0], fb[q][2], acc1, 0, 0, 0);
+        }
+        if (NP > 1) {
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[q][1], fb[q][0], acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[q][0], fb[q][1], acc1, 0, 0, 0);
+        }
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[q][0], fb[q][0], acc0, 0, 0, 0);
+      }
+      st(lds + ((i + 2) % 3) * SSLOT, sset);
+      __syncthreads();
+    };
+    int i = 0;
+    for (; i + 2 < n; i += 3) {
+      stage(i, r1, r2);
+      stage(i + 1, r2, r0);
+      stage(i + 2, r0, r1);
+    }
+    if (i < n) stage(i, r1, r2);
+    if (i + 1 < n) stage(i + 1, r2, r0);
+  }
+  const f32x16 acc = acc0 + acc1;
+  const int col = n0 + wn * 32 + li;
+  const int rbase = m0 + wm * 32 + 4 * lh;
+  if (g.split > 1) {
+    if (col < g.N) {
+      float* slab = g.ws + ((long long)bidx * g.split + sk) * g.M * (long long)g.N;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rbase + (r & 3) + 8 * (r >> 2);
+        if (row < g.M) slab[(long long)row * g.N + col] = acc[r];
+      }
+    }
+    if (g.tile_cnt) splitk_finish<WBM, BN>(g, bidx, m0, n0, (bidx * g.tiles_y + ty) * g.tiles_x + tx, flag);
+    return;
+  }
+  tile_epilogue(g, bidx, rbase, col, acc);
+}
+
 // Separate split-K reduce: a thread sums 4 consecutive elements (float4 over the slabs when M*N % 4 == 0
 // and the workspace is 16-B aligned) with up to 8 slab loads in flight, slabs added in order
 // (deterministic); the epilogue runs per element.
@@ -1804,10 +1991,46 @@ int stream_precision(hipStream_t s) {
   return FX_PREC_F32;
 }
 
-// FX_PREC_BF16: the 128x64-tile launches with row-major operands take the bf16-arithmetic kernel
+// FX_PREC_BF16 / FX_PREC_F32S / FX_PREC_F32S2: the 128x64-tile launches with row-major A take the
+// bf16-arithmetic kernel / the split-bf16 fp32 kernel; everything else (weight gradients: A column-major;
+// direct / small tiles) keeps the f32 MFMA kernels
+bool rowmajor_wide(const GemmPlan& P) {
+  return P.wide && (P.bk == ROWS || P.bk == COLS) && (P.ak == ROWS || P.ak == ROWS_CONV || P.ak == ROWS_CAT);
+}
 bool bf16_eligible(const GemmPlan& P, hipStream_t s) {
-  return P.wide && (P.bk == ROWS || P.bk == COLS) && (P.ak == ROWS || P.ak == ROWS_CONV || P.ak == ROWS_CAT) &&
-         stream_precision(s) == FX_PREC_BF16;
+  return rowmajor_wide(P) && stream_precision(s) == FX_PREC_BF16;
+}
+// the split kernel's 32-deep stages: a conv stage must stay inside one tap, a concatenation stage in
+// one source (the host plan checked 64-alignment for the 64-deep kernels already)
+int split_pieces_for(const GemmPlan& P, hipStream_t s) {
+  if (!rowmajor_wide(P)) return 0;
+  const int prec = stream_precision(s);
+  return prec == FX_PREC_F32S ? 3 : prec == FX_PREC_F32S2 ? 2 : 0;
+}
+
+template <int AK, int NP>
+int launch_split_b(const GemmPlan& P, hipStream_t s) {
+  if (P.bk == ROWS)
+    hipLaunchKernelGGL((gemm_split_wide8_kernel<AK, ROWS, NP>), P.grid, dim3(W8T), 0, s, P.g);
+  else
+    hipLaunchKernelGGL((gemm_split_wide8_kernel<AK, COLS, NP>), P.grid, dim3(W8T), 0, s, P.g);
+  return FX_OK;
+}
+
+template <int NP>
+int launch_split_np(const GemmPlan& P, hipStream_t s) {
+  switch (P.ak) {
+    case ROWS: return launch_split_b<ROWS, NP>(P, s);
+    case ROWS_CONV: return launch_split_b<ROWS_CONV, NP>(P, s);
+    case ROWS_CAT: return launch_split_b<ROWS_CAT, NP>(P, s);
+    default: break;
+  }
+  set_error("gemm(split): unsupported A operand kind");
+  return FX_ERR_UNSUPPORTED;
+}
+
+int launch_split(const GemmPlan& P, int np, hipStream_t s) {
+  return np == 3 ? launch_split_np<3>(P, s) : launch_split_np<2>(P, s);
 }
 
 template <int AK>
@@ -1837,7 +2060,9 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
   FX_TRY(plan_gemm(d, s, P));
   log_gemm(d, P);
   const GemmDev& g = P.g;
-  int st = bf16_eligible(P, s) ? launch_bf16(P, s)
+  const int np = split_pieces_for(P, s);
+  int st = np ? launch_split(P, np, s)
+         : bf16_eligible(P, s) ? launch_bf16(P, s)
          : P.direct ? launch_direct(P.ak, P.bk, P.grid, P.block, s, g)
                     : (P.wide ? (wide8() ? launch_wide8(P.ak, P.bk, P.grid, s, g) : launch_wide(P.ak, P.bk, P.grid, s, g))
                               : launch_tiled(P.ak, P.bk, P.grid, s, g));
@@ -1944,7 +2169,8 @@ long long colsum_workspace_floats(int M, int N) { return (long long)cdiv(M, CS_R
 extern "C" {
 
 int fx_set_stream_precision(void* stream, int prec) {
-  FX_REQUIRE(prec == FX_PREC_F32 || prec == FX_PREC_BF16, "gemm precision: FX_PREC_F32 or FX_PREC_BF16");
+  FX_REQUIRE(prec == FX_PREC_F32 || prec == FX_PREC_BF16 || prec == FX_PREC_F32S || prec == FX_PREC_F32S2,
+             "gemm precision: FX_PREC_F32, FX_PREC_BF16, FX_PREC_F32S or FX_PREC_F32S2");
   std::lock_guard<std::mutex> lk(fx::g_prec_mu);
   const hipStream_t s = (hipStream_t)stream;
   auto& v = fx::g_prec;

@@ -77,9 +77,9 @@ class gemm_precision:
     their own setting."""
 
     def __init__(self, mode, stream=None):
-        modes = {"fp32": nx.PREC_F32, "bf16": nx.PREC_BF16}
+        modes = {"fp32": nx.PREC_F32, "bf16": nx.PREC_BF16, "fp32s": nx.PREC_F32S, "fp32s2": nx.PREC_F32S2}
         if mode not in modes:
-            raise ValueError(f"gemm precision {mode!r}: 'fp32' or 'bf16'")
+            raise ValueError(f"gemm precision {mode!r}: one of {sorted(modes)}")
         lib = nx.load()
         self._stream = nx.stream() if stream is None else stream.cuda_stream
         self._prev = lib.fx_get_stream_precision(self._stream)

@@ -87,7 +87,7 @@ STATUS_GRU_TIMEOUT = 1   # FX_STATUS_GRU_TIMEOUT: a BiGRU workgroup gave up wait
 LOSS_MAXK = 512        # FX_LOSS_MAXK: matched columns of an attention loss term
 LOSS_NB = 128          # FX_LOSS_NB: row blocks per loss term
 TERM_CLASS, TERM_ATTN, TERM_INFONCE = 0, 1, 2
-PREC_F32, PREC_BF16 = 0, 1   # FX_PREC_*: GEMM arithmetic precision (fx_set_stream_precision)
+PREC_F32, PREC_BF16, PREC_F32S, PREC_F32S2 = 0, 1, 2, 3   # FX_PREC_*: GEMM arithmetic (fx_set_stream_precision)
 
 
 class LossTerm(ctypes.Structure):

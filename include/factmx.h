@@ -669,9 +669,14 @@ int fx_eval_pred(const fx_video_attn* vids_host, const fx_video_attn* vids_dev, 
  * v_mfma_f32_32x32x16_bf16, accumulating in fp32; storage, weight
  * gradients, attention, normalisation and losses stay fp32.  A performance
  * mode (BASELINE configs[1]): its deviation from the fp32 path is reported,
- * not bounded by the parity tests.
+ * not bounded by the parity tests.  FX_PREC_F32S: the same GEMMs in fp32
+ * arithmetic on the bf16 matrix cores -- each fp32 operand split into three
+ * bf16 pieces (all 24 mantissa bits), the six piece products of order <= 2
+ * summed in the fp32 accumulator (dropped terms < 3 * 2^-24 |a b|, the size of
+ * fp32's own rounding); fp32-accurate, 2.7x the f32 MFMA rate.  FX_PREC_F32S2:
+ * two pieces / three products (~2^-16 relative; measurement only).
  * ---------------------------------------------------------------------- */
-enum { FX_PREC_F32 = 0, FX_PREC_BF16 = 1 };
+enum { FX_PREC_F32 = 0, FX_PREC_BF16 = 1, FX_PREC_F32S = 2, FX_PREC_F32S2 = 3 };
 int fx_set_stream_precision(void* stream, int prec);
 int fx_get_stream_precision(void* stream);
 

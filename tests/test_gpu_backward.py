@@ -180,3 +180,32 @@ def test_ragged_lockstep_backward_vs_oracle(monkeypatch):
     _check_forward(net, spec, outs, saves, text)
     assert abs(loss - ref_loss) <= 1e-4 * abs(ref_loss), (loss, ref_loss)
     compare_grads(net, ref_grads, rtol=2e-3, relaxed=kinks.flipped_prefixes(len(vids)), what="ragged: ")
+
+
+def test_ntoken75_T4096_train_and_eval_vs_oracle(monkeypatch):
+    """FACT.ntoken 75 (havid_view0_lh_pt_holdout.yaml:75) at T=4096: more than 64 action tokens take the
+    fused decoder (token blocks of 64), the small-MHA / attention-over-T query blocks and the loss table
+    on the lockstep path.  Train mode: loss, segments, logits and gradients vs the fp64 oracle; eval
+    mode: the same forward (predictions, logits, segments) without a loss."""
+    import bench
+    cfg = bench.make_cfg(ntoken=75)
+    T, D, C = 4096, 2048, 75
+    net, text = bench.build_model(cfg, D, C, device=DEV, seed=0)
+    net.train()
+    vids = [bench.make_video(T, D, C, cfg, seed=s) for s in (1, 2)]
+    kinks = GruKinks(monkeypatch)
+    from factmx.dp import DataParallel
+    loss, saves = _gpu_step(net, vids, dp=DataParallel(net))
+    S = _segments(net)
+    spec = fo.resolve_spec(cfg, D, C, clip=True)
+    ref_loss, ref_grads, outs = oracle_batch(spec, net, vids, text)
+    assert S == [[len(r["tdu"].starts) for r in o["blocks"] if r["type"] == "U"] for o in outs], S
+    _check_forward(net, spec, outs, saves, text)
+    assert abs(loss - ref_loss) <= 1e-4 * abs(ref_loss), (loss, ref_loss)
+    compare_grads(net, ref_grads, rtol=2e-3, relaxed=kinks.flipped_prefixes(len(vids)), what="ntoken 75: ")
+    net.eval()
+    with torch.no_grad():
+        saves = net([torch.from_numpy(f).to(DEV) for f, _ in vids], [torch.from_numpy(l_).to(DEV) for _, l_ in vids],
+                    compute_loss=False)
+    torch.cuda.synchronize()
+    _check_forward(net, spec, outs, saves, text)

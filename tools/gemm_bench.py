@@ -80,12 +80,15 @@ def main():
     cases.append(("token     M=32 N=512 K=256", tok_fwd, 2 * 32 * 2 * F * F))
 
     only = os.environ.get("CASE")
+    precs = os.environ.get("PREC", "fp32").split(",")
     for name, fn, fl in cases:
         if only and not name.startswith(only):
             continue
-        us = timeit(fn)
-        tf = fl / (us * 1e-6) / 1e12
-        print(f"{name:40s} {us:8.2f} us  {tf:7.2f} TF/s  {tf / PEAK:6.3f} of peak", flush=True)
+        for prec in precs:
+            with fxf.gemm_precision(prec):
+                us = timeit(fn)
+            tf = fl / (us * 1e-6) / 1e12
+            print(f"{name:40s} {prec:6s} {us:8.2f} us  {tf:7.2f} TF/s  {tf / PEAK:6.3f} of f32 peak", flush=True)
 
 
 if __name__ == "__main__":
