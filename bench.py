@@ -46,6 +46,9 @@ METRIC_SHIPPED = ("frames/sec FACT_CLIP fwd+bwd, havid_view0_lh_pt_holdout.yaml 
                   "cmr 0.3, time mask on), ragged T=4096+2900 D=2048")
 SHIPPED_RATIO = 2900 / 4096      # second video's length relative to --T (a ragged batch, dataset.py:106-131)
 F32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense bf16 MFMA peak (no sparsity)
+SPLIT_PRODUCTS = 6               # FX_PREC_F32S: bf16 piece products per fp32 product
+SPLIT_KERNEL = "gemm_split_wide8_kernel<1, 0, 3>"
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 HOLDOUT = [51, 53, 61, 67, 56]   # havid_view0_lh_pt_holdout.yaml
 D_IN, NCLS, NTOKEN, T_DEFAULT = 2048, 75, 32, 4096
@@ -188,9 +191,20 @@ def traffic_from_profiles(kernel_prefix, name="pmc_dominant.json"):
     return None
 
 
-def bf16_mode(net, step, frames_per_step, steps, warmup, fxf):
-    """Time `steps` fixed-weight steps with fx_set_stream_precision(FX_PREC_BF16) and compare its frame
-    logits (last block, every video) and TDU segment counts with the fp32 path's."""
+PREC_NOTES = {
+    "bf16": ("bf16 products, fp32 accumulation/storage (FX_PREC_BF16)",
+             "same weights and videos as the headline line; weight-gradient GEMMs, attention, normalisation and "
+             "losses stay fp32"),
+    "fp32": ("fp32 (every GEMM product on the f32 MFMA, FX_PREC_F32)",
+             "same weights and videos as the headline line, frame-level GEMMs on v_mfma_f32_32x32x2_f32"),
+    "fp32s": ("fp32 (frame-level GEMMs on the bf16 matrix cores by a 3-piece split, FX_PREC_F32S)",
+              "same weights and videos as the headline line"),
+}
+
+
+def bf16_mode(net, step, frames_per_step, steps, warmup, fxf, mode="bf16"):
+    """Time `steps` fixed-weight steps with the current stream's GEMM precision set to `mode` and compare
+    its frame logits (last block, every video) and TDU segment counts with the headline precision's."""
     def logits():
         step()
         torch.cuda.synchronize()
@@ -199,7 +213,7 @@ def bf16_mode(net, step, frames_per_step, steps, warmup, fxf):
         z = [r["frame_clogit"] for r in recs] if recs else [last.frame_clogit]
         return [t.detach().clone() for t in z], video_segments(net)
     z32, s32 = logits()
-    with fxf.gemm_precision("bf16"):
+    with fxf.gemm_precision(mode):
         z16, s16 = logits()
         for _ in range(warmup):
             step()
@@ -212,12 +226,10 @@ def bf16_mode(net, step, frames_per_step, steps, warmup, fxf):
     dev = max((a - b).abs().max().item() for a, b in zip(z16, z32))
     scale = max(b.abs().max().item() for b in z32)
     agree = sum(int((a.argmax(-1) == b.argmax(-1)).sum()) for a, b in zip(z16, z32)) / sum(b.shape[0] for b in z32)
+    dtype, note = PREC_NOTES[mode]
     return dict(value=round(frames_per_step * steps / el, 1), unit="frames/s", ms_per_step=round(1e3 * el / steps, 3),
-                dtype="bf16 products, fp32 accumulation/storage (FX_PREC_BF16)",
-                frame_logit_max_abs_dev=round(dev, 5), frame_logit_max_abs=round(scale, 4),
-                frame_argmax_agreement=round(agree, 5), tdu_segments=s16, tdu_segments_fp32=s32,
-                note="same weights and videos as the fp32 line; weight-gradient GEMMs, attention, "
-                     "normalisation and losses stay fp32")
+                dtype=dtype, frame_logit_max_abs_dev=round(dev, 6), frame_logit_max_abs=round(scale, 4),
+                frame_argmax_agreement=round(agree, 5), tdu_segments=s16, tdu_segments_headline=s32, note=note)
 
 
 def prof_collect(lib, kind):
@@ -330,7 +342,10 @@ def main():
     ap.add_argument("--adam-steps", type=int, default=None,
                     help="extra timed steps with clip_grad_norm_ + Adam after the fixed-weight steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-bf16", action="store_true", help="skip the bf16-mode extra measurement (N=1 only)")
+    ap.add_argument("--no-bf16", action="store_true", help="skip the extra precision-mode measurements (N=1 only)")
+    ap.add_argument("--prec", choices=["default", "fp32s", "fp32"], default="default",
+                    help="GEMM arithmetic of the headline: the library default, fp32s (fp32 by a 3-piece bf16 split "
+                         "on the bf16 matrix cores) or fp32 (f32 MFMA)")
     args = ap.parse_args()
     cfg, D, C, T_def, vids_def, clip, metric = workload(args.config)
     T = args.T or T_def
@@ -353,9 +368,13 @@ def main():
     dev = torch.device("cuda", local)
 
     from factmx import native
+    from factmx import functional as fxf_
     from factmx.dp import DataParallel
     from factmx.optim import FusedAdam
     lib = native.load()
+    if args.prec != "default":
+        fxf_.set_default_precision(args.prec)
+    headline_prec = fxf_.default_precision()
 
     net, _ = build_model(cfg, D, C, dev, seed=0, clip=clip)
     net.train()
@@ -411,10 +430,13 @@ def main():
     # BASELINE configs[1]: the same fixed-weight step with the frame-level GEMMs in bf16 arithmetic
     # (FX_PREC_BF16, fp32 accumulation / storage), its frame-logit deviation from the fp32 path on the
     # same weights and videos, and its TDU segment counts (N=1 only; the headline stays fp32)
-    bf16 = None
+    bf16 = other = None
     if world == 1 and not args.no_bf16:
         from factmx import functional as fxf
         bf16 = bf16_mode(net, step, sum(Ts), args.steps, args.warmup, fxf)
+        # the other fp32 arithmetic (f32 MFMA when the headline runs the split, and vice versa)
+        other = bf16_mode(net, step, sum(Ts), args.steps, args.warmup, fxf,
+                          "fp32" if headline_prec == "fp32s" else "fp32s")
 
     # the reference train step (clip_grad_norm_ + Adam), timed after the fixed-weight steps
     adam = None
@@ -449,10 +471,17 @@ def main():
         flops_per_launch = fl.value / max(cnt.value, 1)
         achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
         default_shape = args.config == "havid" and T == T_DEFAULT and nv == 2
-        roofline = dict(bound="mfma", achieved=round(achieved, 2), peak=F32_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
-                        frac=round(achieved / F32_MFMA_PEAK_TFLOPS, 4),
-                        traffic=(traffic_from_profiles(DOMINANT_KERNEL) if default_shape else None),
-                        kernel=("gemm_f32_wide8_kernel (implicit dilated-conv GEMM: conv fwd + conv dX)"),
+        split = headline_prec == "fp32s"
+        # split arithmetic: the matrix cores' bound is the bf16 dense peak over the 6 piece products
+        # (fp32 FLOPs counted once); f32 MFMA: the f32 matrix peak
+        peak = BF16_MFMA_PEAK_TFLOPS / SPLIT_PRODUCTS if split else F32_MFMA_PEAK_TFLOPS
+        roofline = dict(bound="mfma", achieved=round(achieved, 2), peak=round(peak, 1), unit="TFLOP/s",
+                        frac=round(achieved / peak, 4),
+                        traffic=(traffic_from_profiles(SPLIT_KERNEL if split else DOMINANT_KERNEL)
+                                 if default_shape else None),
+                        kernel=(f"{SPLIT_KERNEL} (implicit dilated-conv GEMM in fp32 by 3-piece bf16 split: conv fwd "
+                                f"+ conv dX; peak = bf16 dense peak / {SPLIT_PRODUCTS} products)" if split else
+                                "gemm_f32_wide8_kernel (implicit dilated-conv GEMM: conv fwd + conv dX)"),
                         launches=cnt.value, avg_launch_ms=round(avg_ms, 5),
                         flops_per_launch=flops_per_launch,
                         sample=f"HIP events on the first {cnt.value} conv-GEMM launches of the timed region")
@@ -464,6 +493,7 @@ def main():
         line = dict(metric=metric, value=round(value, 1), unit="frames/s", n_gpus=world, steps=args.steps,
                     warmup=args.warmup, ms_per_step=round(1e3 * elapsed / args.steps, 3), higher_is_better=True,
                     scaling="weak", vs_baseline=None, dtype="fp32", data="synthetic",
+                    gemm_arithmetic=PREC_NOTES[headline_prec][0],
                     config=dict(workload=(f"FACT_CLIP havid_view0_lh_pt_holdout.yaml as shipped (training mode: "
                                           f"dropout 0.2, cmr 0.3, time mask, ntoken 75), seg10 synthetic, "
                                           f"ragged T={'+'.join(map(str, Ts))}" if args.config == "shipped" else
@@ -476,6 +506,8 @@ def main():
                                 tdu_segments=S, tdu_segments_after_timing=S_after),
                     roofline=roofline, roofline_attention=roofline_attention, train_step_with_adam=adam,
                     bf16_mode=bf16)
+        if other is not None:
+            line["fp32_f32mfma_mode" if headline_prec == "fp32s" else "fp32_split_mode"] = other
         if world == 1 and not args.no_cpu_baseline:
             cb, step_flops, S_oracle = cpu_baseline(args.config, Ts, seeds)
             line["cpu_baseline"] = cb

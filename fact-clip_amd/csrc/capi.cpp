@@ -462,6 +462,7 @@ const Knobs& knobs() {
     if (const char* p = env("FX_DEFER_SPLIT")) k.defer_split = std::max(1, std::min(16, std::atoi(p)));
     if (const char* p = env("FX_MSTCN_DEFER")) k.mstcn_defer = p[0] != '0';
     if (const char* p = env("FX_SIDE_MAXWG")) k.side_maxwg = std::max(0, std::atoi(p));
+    if (const char* p = env("FX_X2Y_FUSED")) k.x2y_fused = p[0] != '0';
   });
   return k;
 }
@@ -1520,6 +1521,10 @@ int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpo
   FX_TRY(linear_fwd(X, ldx, Nx, xdim, wv, bv, xv, Hd, Hd, 0, s));
   FX_TRY(linear_fwd(yin, ldyin, Ny, ydim, wq, bq, yq, Hd, Hd, 0, s));
   const float scale = 1.0f / std::sqrt((float)Hd);
+  // a short key side (the a2f map: <= 64 action tokens per video): the whole core in one launch
+  if (knobs().x2y_fused && x2y_a2f_fusable(V.n, V.x.data(), Hd)) {
+    FX_TRY(launch_x2y_a2f_fwd(yq, xk, xv, Hd, scale, V.n, V.y.data(), V.x.data(), V.a.data(), logit, attn, feat, s));
+  } else
   // per video: logits = scale yq . xk^T, attn = softmax(logits), feat = attn . xv  (the GEMMs of up to
   // two videos in one grouped launch each)
   for (int v0 = 0; v0 < V.n; v0 += 2) {

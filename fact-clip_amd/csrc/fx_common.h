@@ -132,6 +132,7 @@ struct Knobs {
   int defer_split = 8;
   bool mstcn_defer = true;
   int side_maxwg = 0;
+  bool x2y_fused = true;    // FX_X2Y_FUSED=0: the X2Y attention core as grouped GEMM + softmax launches
 };
 const Knobs& knobs();
 

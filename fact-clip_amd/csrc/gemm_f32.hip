@@ -1276,6 +1276,9 @@ __global__ __launch_bounds__(W8T) void gemm_split_wide8_kernel(GemmDev g) {
         }
       ld(i + 4, lset);
       __builtin_amdgcn_sched_barrier(0);
+      // the split + LDS stores of stage i + 2 (another slot) are issued between the MFMA groups, so
+      // they run while the matrix core works on this stage's products
+      __bf16* wslot = lds + ((i + 2) % 3) * SSLOT;
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         if (NP > 2) {
@@ -1288,8 +1291,15 @@ __global__ __launch_bounds__(W8T) void gemm_split_wide8_kernel(GemmDev g) {
           acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[q][0], fb[q][1], acc1, 0, 0, 0);
         }
         acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[q][0], fb[q][0], acc0, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (q == 0) {
+          store_split<AK, NP>(la0, wslot, sset.a0, sset.m0);
+          store_split<AK, NP>(la1, wslot + NP * SIMG, sset.a1, sset.m1);
+        } else {
+          store_split<BKd, NP>(lb, wslot + 2 * NP * SIMG, sset.b, sset.mb);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      st(lds + ((i + 2) % 3) * SSLOT, sset);
       __syncthreads();
     };
     int i = 0;
@@ -1981,14 +1991,19 @@ int launch_reduce(const fx_gemm_desc& d, const GemmPlan& P, hipStream_t s) {
 // precisions on different streams (or threads) do not interfere.
 std::mutex g_prec_mu;
 std::vector<std::pair<hipStream_t, int>> g_prec;
-std::atomic<int> g_prec_any{0};   // fast path: no stream has ever left FX_PREC_F32
+std::atomic<int> g_prec_any{0};   // fast path: no stream has an explicit setting
+std::atomic<int> g_prec_default{FX_PREC_F32};   // streams without one (fx_set_default_precision)
 
 int stream_precision(hipStream_t s) {
-  if (!g_prec_any.load(std::memory_order_acquire)) return FX_PREC_F32;
+  if (!g_prec_any.load(std::memory_order_acquire)) return g_prec_default.load(std::memory_order_relaxed);
   std::lock_guard<std::mutex> lk(g_prec_mu);
   for (const auto& e : g_prec)
     if (e.first == s) return e.second;
-  return FX_PREC_F32;
+  return g_prec_default.load(std::memory_order_relaxed);
+}
+
+bool valid_precision(int prec) {
+  return prec == FX_PREC_F32 || prec == FX_PREC_BF16 || prec == FX_PREC_F32S || prec == FX_PREC_F32S2;
 }
 
 // FX_PREC_BF16 / FX_PREC_F32S / FX_PREC_F32S2: the 128x64-tile launches with row-major A take the
@@ -2169,8 +2184,8 @@ long long colsum_workspace_floats(int M, int N) { return (long long)cdiv(M, CS_R
 extern "C" {
 
 int fx_set_stream_precision(void* stream, int prec) {
-  FX_REQUIRE(prec == FX_PREC_F32 || prec == FX_PREC_BF16 || prec == FX_PREC_F32S || prec == FX_PREC_F32S2,
-             "gemm precision: FX_PREC_F32, FX_PREC_BF16, FX_PREC_F32S or FX_PREC_F32S2");
+  FX_REQUIRE(prec == FX_PREC_DEFAULT || fx::valid_precision(prec),
+             "gemm precision: FX_PREC_DEFAULT, FX_PREC_F32, FX_PREC_BF16, FX_PREC_F32S or FX_PREC_F32S2");
   std::lock_guard<std::mutex> lk(fx::g_prec_mu);
   const hipStream_t s = (hipStream_t)stream;
   auto& v = fx::g_prec;
@@ -2179,11 +2194,26 @@ int fx_set_stream_precision(void* stream, int prec) {
       v.erase(it);
       break;
     }
-  if (prec != FX_PREC_F32) v.emplace_back(s, prec);
+  if (prec != FX_PREC_DEFAULT) v.emplace_back(s, prec);
   fx::g_prec_any.store(v.empty() ? 0 : 1, std::memory_order_release);
   return FX_OK;
 }
 
 int fx_get_stream_precision(void* stream) { return fx::stream_precision((hipStream_t)stream); }
+
+int fx_stream_precision_explicit(void* stream) {
+  std::lock_guard<std::mutex> lk(fx::g_prec_mu);
+  for (const auto& e : fx::g_prec)
+    if (e.first == (hipStream_t)stream) return e.second;
+  return FX_PREC_DEFAULT;
+}
+
+int fx_set_default_precision(int prec) {
+  FX_REQUIRE(fx::valid_precision(prec), "default gemm precision: FX_PREC_F32, FX_PREC_BF16, FX_PREC_F32S or FX_PREC_F32S2");
+  fx::g_prec_default.store(prec, std::memory_order_relaxed);
+  return FX_OK;
+}
+
+int fx_get_default_precision(void) { return fx::g_prec_default.load(std::memory_order_relaxed); }
 
 }  // extern "C"

@@ -47,6 +47,13 @@ int launch_gru_bwd(const float* dout, long long lddo, int nseq, const int* seq_o
                    const float* saved, float* dgi, long long lddgi, float* dgh, float* sync_ws, unsigned* status,
                    int spin_max, hipStream_t s);
 
+// X2Y attention core with <= 64 keys per video (x2y_core.hip): logit, attn, feat in one launch;
+// yoff / xoff: (nvid + 1) host row offsets, aoff: attention block offsets (ny_v * nx_v row-major each)
+bool x2y_a2f_fusable(int nvid, const int* xoff, int Hd);
+int launch_x2y_a2f_fwd(const float* yq, const float* xk, const float* xv, int Hd, float scale, int nvid,
+                       const int* yoff, const int* xoff, const long long* aoff, float* logit, float* attn,
+                       float* feat, hipStream_t s);
+
 // ---- composite helpers (capi.cpp) --------------------------------------------
 int ew_grid(long long total);
 int relu_bwd(const float* dy, long long lddy, const float* y, long long ldy, int rows, int cols, float* dz,

@@ -1,0 +1,247 @@
+// X2Y attention core for a SHORT key side (X2Y_map.forward, basic.py:349-389, with X = the action
+// tokens: the a2f map of UpdateBlock / UpdateBlockTDU, blocks.py:343-367 and 449-485):
+//
+//   logit = scale * yq . xk^T      (ny x nx, one video: nx <= 64 keys, ny up to T query rows)
+//   attn  = softmax_x(logit)
+//   feat  = attn . xv              (ny x Hd)
+//
+// as ONE launch over every video, instead of a grouped logit GEMM, a softmax launch per video and a
+// grouped feat GEMM.  A workgroup (8 waves) owns 32 query rows of one video:
+//   1. logits: the 32 x nx tile (<= 2 key blocks of 32) on v_mfma_f32_32x32x2_f32, the Hd-deep sum
+//      split over the 8 waves (Hd / 8 each; a lane feeds 16 consecutive k of a 32-deep chunk, float4
+//      loads straight from L2 -- the k order inside the sum is free as long as A and B agree), the
+//      8 partial tiles summed through LDS in wave order (deterministic);
+//   2. the row softmax over the nx keys in LDS; logit and attn written (the losses read both);
+//   3. feat = attn . xv: 16 column tiles of 32 over Hd = 512, two per wave, K = nx from the LDS
+//      probabilities (A) and xv columns (B, 32 lanes read 32 consecutive floats of one key row).
+// Algorithmic bytes per 32-row workgroup: yq rows 32 Hd + feat rows 32 Hd (+ logit / attn 2 x 32 nx)
+// floats; xk / xv (2 nx Hd floats per video) are L2-resident and shared by every workgroup of the video.
+#include "fx_common.h"
+#include "ops.h"
+
+namespace fx {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int XR = 32;            // query rows per workgroup
+constexpr int XT = 512;           // threads (8 waves)
+constexpr int XMAXK = 64;         // keys per video
+constexpr int LS = XMAXK + 1;     // LDS row stride of the logit / probability tile
+constexpr int FX_X2Y_MAXV = 16;   // videos per launch
+
+struct A2fArgs {
+  const float* yq;      // (Ny, Hd) query rows of every video, stacked
+  const float* xk;      // (Nx, Hd) keys of every video, stacked
+  const float* xv;      // (Nx, Hd)
+  float* logit;         // per video: (ny_v, nx_v) row-major at aoff[v]
+  float* attn;
+  float* feat;          // (Ny, Hd)
+  int Hd, nvid;
+  float scale;
+  int yoff[FX_X2Y_MAXV + 1], xoff[FX_X2Y_MAXV + 1];
+  long long aoff[FX_X2Y_MAXV + 1];
+  int wg_off[FX_X2Y_MAXV + 1];    // first workgroup of each video
+};
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+__global__ __launch_bounds__(XT) void x2y_a2f_fwd_kernel(A2fArgs a) {
+  __shared__ float red[8][2][16][64];       // per-wave partial logit tiles (acc register r, lane)
+  __shared__ float P[XR][LS];               // scaled logits, then probabilities
+  __shared__ float rmax[XR], rsum[XR];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 31, lh = lane >> 5;
+  // video of this workgroup (constant indices only: the argument block stays in SGPRs)
+  int v = 0;
+#pragma unroll
+  for (int i = 1; i < FX_X2Y_MAXV; ++i)
+    if (i < a.nvid && (int)blockIdx.x >= a.wg_off[i]) v = i;
+  int y0 = 0, ny = 0, x0 = 0, nx = 0, wg0 = 0;
+  long long ao = 0;
+#pragma unroll
+  for (int i = 0; i < FX_X2Y_MAXV; ++i)
+    if (i == v) {
+      y0 = a.yoff[i];
+      ny = a.yoff[i + 1] - a.yoff[i];
+      x0 = a.xoff[i];
+      nx = a.xoff[i + 1] - a.xoff[i];
+      ao = a.aoff[i];
+      wg0 = a.wg_off[i];
+    }
+  const int r0 = ((int)blockIdx.x - wg0) * XR;     // first query row (video-local)
+  const int Hd = a.Hd;
+  const int nkb = nx > 32 ? 2 : 1;
+
+  // ---- 1. logits: wave w sums k in [w Hd/8, (w+1) Hd/8) ----
+  f32x16 acc[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[c][i] = 0.f;
+  {
+    const int kw = Hd >> 3;
+    const int qr = min(r0 + li, ny - 1);
+    const float* pa = a.yq + (long long)(y0 + qr) * Hd;
+    const bool aok = r0 + li < ny;
+    for (int k0 = w * kw; k0 < (w + 1) * kw; k0 += 32) {
+      const int kk = k0 + 16 * lh;
+      float av[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 t = ld4(pa + kk + 4 * q);
+        av[4 * q] = aok ? t.x : 0.f;
+        av[4 * q + 1] = aok ? t.y : 0.f;
+        av[4 * q + 2] = aok ? t.z : 0.f;
+        av[4 * q + 3] = aok ? t.w : 0.f;
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        if (c < nkb) {
+          const int key = c * 32 + li;
+          const bool bok = key < nx;
+          const float* pb = a.xk + (long long)(x0 + min(key, nx - 1)) * Hd + kk;
+          float bv[16];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 t = ld4(pb + 4 * q);
+            bv[4 * q] = bok ? t.x : 0.f;
+            bv[4 * q + 1] = bok ? t.y : 0.f;
+            bv[4 * q + 2] = bok ? t.z : 0.f;
+            bv[4 * q + 3] = bok ? t.w : 0.f;
+          }
+#pragma unroll
+          for (int s = 0; s < 16; ++s) acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc[c], 0, 0, 0);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[w][c][r][lane] = acc[c][r];
+  __syncthreads();
+  for (int e = tid; e < 2 * 16 * 64; e += XT) {
+    const int c = e >> 10, r = (e >> 6) & 15, l = e & 63;
+    float sum = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) sum += red[q][c][r][l];
+    const int row = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), col = c * 32 + (l & 31);
+    P[row][col] = a.scale * sum;
+  }
+  __syncthreads();
+
+  // ---- 2. row softmax over the nx keys (a half-wave of 32 lanes per row, shuffles in 32) ----
+  {
+    // 16 threads per row, 32 rows = 512 threads: thread t owns row t >> 4, columns (t & 15) + 16 j
+    const int row = tid >> 4, c0 = tid & 15;
+    float m = -3.0e38f;
+#pragma unroll
+    for (int j = 0; j < XMAXK / 16; ++j) {
+      const int col = c0 + 16 * j;
+      if (col < nx) m = fmaxf(m, P[row][col]);
+    }
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 16));
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < XMAXK / 16; ++j) {
+      const int col = c0 + 16 * j;
+      if (col < nx) sum += __expf(P[row][col] - m);
+    }
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 16);
+    if (c0 == 0) {
+      rmax[row] = m;
+      rsum[row] = sum;
+    }
+  }
+  __syncthreads();
+  {
+    // logit and attn out (row-major, ld nx, coalesced over the tile), probabilities kept in LDS
+    const int rows = min(XR, ny - r0);
+    for (int e = tid; e < XR * XMAXK; e += XT) {
+      const int row = e / XMAXK, col = e - row * XMAXK;
+      float p = 0.f;
+      if (col < nx) {
+        const float l = P[row][col];
+        p = __expf(l - rmax[row]) / rsum[row];
+        if (row < rows) {
+          const long long o = ao + (long long)(r0 + row) * nx + col;
+          a.logit[o] = l;
+          a.attn[o] = p;
+        }
+      }
+      P[row][col] = p;   // (each element is read and rewritten by the same thread)
+    }
+  }
+  __syncthreads();
+
+  // ---- 3. feat = P . xv: column tiles n0 = 32 (2 w + t), t = 0, 1 ----
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n0 = 32 * (2 * w + t);
+    if (n0 >= Hd) continue;
+    f32x16 f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) f[i] = 0.f;
+    for (int k0 = 0; k0 < nx; k0 += 32) {
+      float bv[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int key = k0 + 16 * lh + s;
+        const float x = a.xv[(long long)(x0 + min(key, nx - 1)) * Hd + n0 + li];
+        bv[s] = key < nx ? x : 0.f;
+      }
+#pragma unroll
+      for (int s = 0; s < 16; ++s) f = __builtin_amdgcn_mfma_f32_32x32x2f32(P[li][k0 + 16 * lh + s], bv[s], f, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+      if (r0 + row < ny) a.feat[(long long)(y0 + r0 + row) * Hd + n0 + li] = f[r];
+    }
+  }
+}
+
+}  // namespace
+
+bool x2y_a2f_fusable(int nvid, const int* xoff, int Hd) {
+  if (nvid < 1 || nvid > FX_X2Y_MAXV || Hd % 256 != 0 || Hd > XT) return false;
+  for (int v = 0; v < nvid; ++v)
+    if (xoff[v + 1] - xoff[v] > XMAXK) return false;
+  return true;
+}
+
+int launch_x2y_a2f_fwd(const float* yq, const float* xk, const float* xv, int Hd, float scale, int nvid,
+                       const int* yoff, const int* xoff, const long long* aoff, float* logit, float* attn,
+                       float* feat, hipStream_t s) {
+  FX_REQUIRE(x2y_a2f_fusable(nvid, xoff, Hd), "x2y a2f core: <= 64 keys per video, Hd % 256 == 0, <= 16 videos");
+  A2fArgs a{};
+  a.yq = yq;
+  a.xk = xk;
+  a.xv = xv;
+  a.logit = logit;
+  a.attn = attn;
+  a.feat = feat;
+  a.Hd = Hd;
+  a.nvid = nvid;
+  a.scale = scale;
+  int wg = 0;
+  for (int v = 0; v <= nvid; ++v) {
+    a.yoff[v] = yoff[v];
+    a.xoff[v] = xoff[v];
+    a.aoff[v] = aoff[v];
+    a.wg_off[v] = wg;
+    if (v < nvid) {
+      const int ny = yoff[v + 1] - yoff[v], nx = xoff[v + 1] - xoff[v];
+      // an empty key side leaves no workgroup: softmax over nothing has no rows to write
+      if (nx > 0) wg += (ny + XR - 1) / XR;
+    }
+  }
+  for (int v = nvid + 1; v <= FX_X2Y_MAXV; ++v) a.wg_off[v] = wg;
+  if (wg == 0) return FX_OK;
+  hipLaunchKernelGGL(x2y_a2f_fwd_kernel, dim3(wg), dim3(XT), 0, s, a);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+}  // namespace fx

@@ -69,6 +69,14 @@ def _defer_to_side(*tensors):
         torch.autograd.Variable._execution_engine.queue_callback(side_join)
 
 
+def _may_defer(tg):
+    """Weight gradients may stay on the side stream past this backward call only when every target
+    is a leaf's .grad (joined at the end of the backward pass).  A non-leaf parameter's gradient is a
+    fresh buffer handed back to autograd, which reads it on the main stream right away: then the
+    entry point joins its side work before returning (side_defer = 0)."""
+    return DEFER_SIDE and side_stream() is not None and all(t[1] is None for t in tg)
+
+
 class gemm_precision:
     """Context manager (or plain call) for the GEMM arithmetic of work enqueued on the CURRENT torch
     stream: "fp32" (default, the parity path) or "bf16" (FX_PREC_BF16: frame-level forward /
@@ -77,12 +85,12 @@ class gemm_precision:
     their own setting."""
 
     def __init__(self, mode, stream=None):
-        modes = {"fp32": nx.PREC_F32, "bf16": nx.PREC_BF16, "fp32s": nx.PREC_F32S, "fp32s2": nx.PREC_F32S2}
+        modes = PRECISIONS
         if mode not in modes:
             raise ValueError(f"gemm precision {mode!r}: one of {sorted(modes)}")
         lib = nx.load()
         self._stream = nx.stream() if stream is None else stream.cuda_stream
-        self._prev = lib.fx_get_stream_precision(self._stream)
+        self._prev = lib.fx_stream_precision_explicit(self._stream)   # PREC_DEFAULT when never set
         nx.check(lib.fx_set_stream_precision(self._stream, modes[mode]), "fx_set_stream_precision")
 
     def __enter__(self):
@@ -91,6 +99,22 @@ class gemm_precision:
     def __exit__(self, *exc):
         nx.check(nx.load().fx_set_stream_precision(self._stream, self._prev), "fx_set_stream_precision")
         return False
+
+
+PRECISIONS = {"fp32": nx.PREC_F32, "bf16": nx.PREC_BF16, "fp32s": nx.PREC_F32S, "fp32s2": nx.PREC_F32S2}
+
+
+def set_default_precision(mode):
+    """Library-wide GEMM arithmetic of streams without their own setting (fx_set_default_precision):
+    "fp32s" (fp32 on the bf16 matrix cores by a 3-piece split), "fp32" (f32 MFMA), ..."""
+    if mode not in PRECISIONS:
+        raise ValueError(f"gemm precision {mode!r}: one of {sorted(PRECISIONS)}")
+    nx.check(nx.load().fx_set_default_precision(PRECISIONS[mode]), "fx_set_default_precision")
+
+
+def default_precision():
+    inv = {v: k for k, v in PRECISIONS.items()}
+    return inv[nx.load().fx_get_default_precision()]
 
 
 def dropout_seed():
@@ -528,7 +552,7 @@ class X2YFn(torch.autograd.Function):
         # the kernel needs every weight-gradient target; absent ones go to scratch
         bufs = [b if b is not None else torch.zeros_like(p) for b, p in zip(bufs, (wk, bk, wv, bv, wq, bq, wy, by))]
         ws = _ws(lib.fx_x2y_workspace_floats(Nx, xdim, Ny, ydim, Hd, outdim, nvid, xo, yo), dev)
-        defer = DEFER_SIDE and side_stream() is not None
+        defer = _may_defer(tg)
         _check(lib.fx_x2y_bwd(nx.ptr(X), nx.ld(X), Nx, xdim, xpc, nx.ptr(Y), nx.ld(Y), Ny, ydim, ypc,
                               nx.ptr(wk), nx.ptr(wv), nx.ptr(wq), nx.ptr(wy), Hd, outdim, nvid, xo, yo,
                               ctx.drop[0], ctx.drop[1], nx.ptr(attn),
@@ -633,7 +657,7 @@ class MSTCNFn(torch.autograd.Function):
         g.w_out, g.b_out = nx.ptr(w_out), nx.ptr(b_out)
         dx = _empty(*x.shape, device=dev) if ctx.needs_input_grad[0] else None
         ws = _ws(lib.fx_mstcn_workspace_floats(ctypes.byref(ctx.prm), x.shape[0]), dev)
-        defer = DEFER_SIDE and side_stream() is not None
+        defer = _may_defer(tg)
         ctx.prm.side_defer = int(defer)
         _check(lib.fx_mstcn_bwd(ctypes.byref(ctx.prm), ctypes.byref(g), nx.ptr(x), nx.ld(x), T, nvid, nx.ptr(dy),
                                 cout, nx.ptr(dx), nx.ld(dx), nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_mstcn_bwd")
@@ -729,7 +753,7 @@ class MSTCN2Fn(torch.autograd.Function):
         g = MSTCN2Fn._prm(ctx.meta, [t[0] for t in tg], keep, nx.Mstcn2Grads, grads=True)
         dx = _empty(*x.shape, device=dev) if ctx.needs_input_grad[0] else None
         ws = _ws(lib.fx_mstcn2_workspace_floats(ctypes.byref(ctx.prm), x.shape[0]), dev)
-        defer = DEFER_SIDE and side_stream() is not None
+        defer = _may_defer(tg)
         ctx.prm.side_defer = int(defer)
         _check(lib.fx_mstcn2_bwd(ctypes.byref(ctx.prm), ctypes.byref(g), nx.ptr(x), nx.ld(x), T, nvid, nx.ptr(dy),
                                  cout, nx.ptr(dx), nx.ld(dx), nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_mstcn2_bwd")
@@ -1242,7 +1266,7 @@ class DecoderFn(torch.autograd.Function):
         ws = _ws(lib.fx_decoder_workspace_floats(ctypes.byref(prm), R, T, nvid, hq, hm), dev)
         # the token linears' weight gradients (and, cross-attention decoders, the frame-memory K/V one)
         # stay on the side stream
-        defer = DEFER_SIDE and side_stream() is not None
+        defer = _may_defer(tg)
         prm.side_defer = int(defer)
         _check(lib.fx_decoder_bwd(ctypes.byref(prm), ctypes.byref(g), nx.ptr(tgt), nx.ld(tgt), R, nx.ptr(qpos),
                                   nx.ptr(mem), nx.ld(mem), T, nvid, nx.ptr(mpos), nx.ld(mpos), nx.ptr(dout),

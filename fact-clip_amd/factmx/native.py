@@ -87,7 +87,7 @@ STATUS_GRU_TIMEOUT = 1   # FX_STATUS_GRU_TIMEOUT: a BiGRU workgroup gave up wait
 LOSS_MAXK = 512        # FX_LOSS_MAXK: matched columns of an attention loss term
 LOSS_NB = 128          # FX_LOSS_NB: row blocks per loss term
 TERM_CLASS, TERM_ATTN, TERM_INFONCE = 0, 1, 2
-PREC_F32, PREC_BF16, PREC_F32S, PREC_F32S2 = 0, 1, 2, 3   # FX_PREC_*: GEMM arithmetic (fx_set_stream_precision)
+PREC_DEFAULT, PREC_F32, PREC_BF16, PREC_F32S, PREC_F32S2 = -1, 0, 1, 2, 3   # FX_PREC_*: GEMM arithmetic
 
 
 class LossTerm(ctypes.Structure):
@@ -180,6 +180,9 @@ SIGNATURES = {
     "fx_eval_pred": (I, [P, P, I, F, P, P]),
     "fx_set_stream_precision": (I, [P, I]),
     "fx_get_stream_precision": (I, [P]),
+    "fx_stream_precision_explicit": (I, [P]),
+    "fx_set_default_precision": (I, [I]),
+    "fx_get_default_precision": (I, []),
     "fx_prof_enable": (I, [I, I]),
     "fx_prof_collect": (I, [I, ctypes.POINTER(D), ctypes.POINTER(D), ctypes.POINTER(D), ctypes.POINTER(I)]),
     "fx_prof_disable": (None, []),

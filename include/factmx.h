@@ -660,9 +660,10 @@ int fx_eval_pred(const fx_video_attn* vids_host, const fx_video_attn* vids_dev, 
 /* ------------------------------------------------------------------------
  * GEMM arithmetic precision, per caller stream (the stream every entry point
  * receives): fx_set_stream_precision(stream, prec) applies to the GEMMs later
- * enqueued on that stream; streams never set (and the library's side stream, where
- * weight gradients run) use FX_PREC_F32.  FX_PREC_F32 (default): every
- * product on v_mfma_f32_32x32x2_f32, the parity path.  FX_PREC_BF16: the
+ * enqueued on that stream; streams never set follow the library default
+ * (fx_set_default_precision, initially FX_PREC_F32).  Weight-gradient GEMMs
+ * (column-major A) and the small-tile / direct kernels always multiply on the
+ * f32 MFMA.  FX_PREC_F32: every product on v_mfma_f32_32x32x2_f32.  FX_PREC_BF16: the
  * frame-level GEMMs with row-major operands (forward and input-gradient
  * products of the MS-TCN convs, in/out maps, projections) round their
  * operands to bf16 on the way into LDS and multiply on
@@ -676,9 +677,14 @@ int fx_eval_pred(const fx_video_attn* vids_host, const fx_video_attn* vids_dev, 
  * fp32's own rounding); fp32-accurate, 2.7x the f32 MFMA rate.  FX_PREC_F32S2:
  * two pieces / three products (~2^-16 relative; measurement only).
  * ---------------------------------------------------------------------- */
-enum { FX_PREC_F32 = 0, FX_PREC_BF16 = 1, FX_PREC_F32S = 2, FX_PREC_F32S2 = 3 };
+enum { FX_PREC_DEFAULT = -1, FX_PREC_F32 = 0, FX_PREC_BF16 = 1, FX_PREC_F32S = 2, FX_PREC_F32S2 = 3 };
+/* per stream: FX_PREC_DEFAULT clears the stream's setting (it then follows the library default) */
 int fx_set_stream_precision(void* stream, int prec);
-int fx_get_stream_precision(void* stream);
+int fx_get_stream_precision(void* stream);          /* effective precision of the stream */
+int fx_stream_precision_explicit(void* stream);     /* the stream's own setting, or FX_PREC_DEFAULT */
+/* library default for streams without a setting (initially FX_PREC_F32) */
+int fx_set_default_precision(int prec);
+int fx_get_default_precision(void);
 
 /* ----------------------------------------------------------------------
  * Profiling hooks: HIP-event timing of every launch of a kernel class

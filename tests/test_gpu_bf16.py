@@ -65,7 +65,7 @@ def test_bf16_gemm_matches_rounded_product(M, N, K, split, epi, bt):
     assert err <= 2e-5 * (1 + ref_bf.abs().max().item()) + 1e-6 * math.sqrt(K), err
     # the bf16 arithmetic really ran: nearer the rounded product than the exact one
     assert (got - ref).abs().max().item() > 10 * err
-    assert nx.load().fx_get_stream_precision(nx.stream()) == nx.PREC_F32
+    assert nx.load().fx_get_stream_precision(nx.stream()) == nx.load().fx_get_default_precision()
 
 
 def test_bf16_conv_gemm_matches_rounded_product():
@@ -108,7 +108,7 @@ def test_bf16_precision_is_per_stream():
         fxf.gemm(M, N, K, _rows(A), _rows(B), c16, N)
         other.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(other):
-            assert nx.load().fx_get_stream_precision(nx.stream()) == nx.PREC_F32
+            assert nx.load().fx_get_stream_precision(nx.stream()) == nx.load().fx_get_default_precision()
             fxf.gemm(M, N, K, _rows(A), _rows(B), c_other, N)
         torch.cuda.current_stream().wait_stream(other)
     torch.cuda.synchronize()

@@ -53,7 +53,7 @@ def _check(ref, M, N, K, a_fn, b_fn, split=1, **kw):
     print(f"max |err|: native f32 {e32:.3e}  split-3 {es:.3e}  split-2 {es2:.3e}  (|ref| max {scale:.3e})")
     assert es <= 2.0 * e32 + 2 ** -24 * math.sqrt(K) * scale, (es, e32)
     assert es2 > 4 * es, (es2, es)          # the 3-piece split is not the 2-piece (or bf16) arithmetic
-    assert nx.load().fx_get_stream_precision(nx.stream()) == nx.PREC_F32
+    assert nx.load().fx_get_stream_precision(nx.stream()) == nx.load().fx_get_default_precision()
 
 
 @pytest.mark.parametrize("M,N,K,split,epi,bt", [(8192, 256, 256, 1, "plain", False),
