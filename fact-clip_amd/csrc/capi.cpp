@@ -463,6 +463,7 @@ const Knobs& knobs() {
     if (const char* p = env("FX_MSTCN_DEFER")) k.mstcn_defer = p[0] != '0';
     if (const char* p = env("FX_SIDE_MAXWG")) k.side_maxwg = std::max(0, std::atoi(p));
     if (const char* p = env("FX_X2Y_FUSED")) k.x2y_fused = p[0] != '0';
+    if (const char* p = env("FX_SPLIT_VARIANT")) k.split_variant = std::atoi(p);
   });
   return k;
 }
@@ -1379,6 +1380,7 @@ int fx_mha_t_bwd(const float* q, long long ldq, const float* k, long long ldk, c
 // saved: xin (Nx*xdim, X+Xpos when Xpos), yin (Ny*ydim), xk, xv (Nx*Hd), yq, feat (Ny*Hd)
 }  // extern "C"
 namespace {
+constexpr int GMAX_GROUP = 4;   // members of one grouped direct-GEMM launch (gemm_f32.hip GMAX)
 struct X2YLayout {
   long long xin, yin, xk, xv, yq, feat, total;
 };
@@ -1522,7 +1524,7 @@ int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpo
   FX_TRY(linear_fwd(yin, ldyin, Ny, ydim, wq, bq, yq, Hd, Hd, 0, s));
   const float scale = 1.0f / std::sqrt((float)Hd);
   // a short key side (the a2f map: <= 64 action tokens per video): the whole core in one launch
-  if (knobs().x2y_fused && x2y_a2f_fusable(V.n, V.x.data(), Hd)) {
+  if (knobs().x2y_fused && x2y_a2f_fusable(V.n, V.x.data(), Hd) && ((reinterpret_cast<uintptr_t>(yq)) & 15) == 0) {
     FX_TRY(launch_x2y_a2f_fwd(yq, xk, xv, Hd, scale, V.n, V.y.data(), V.x.data(), V.a.data(), logit, attn, feat, s));
   } else
   // per video: logits = scale yq . xk^T, attn = softmax(logits), feat = attn . xv  (the GEMMs of up to
@@ -1609,6 +1611,45 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
     FX_TRY(launch_dropout(dcat, cw, Ny, cw, cw, 0, drop_p, seed, dcat, cw, s));
     catd = cd;
   }
+  // a short key side (the a2f map): dP, the softmax backward and dyq in one launch for every video; the
+  // products that reduce over the query rows (dxv = attn^T dfeat, dxk = scale dlogit^T yq) stay
+  // split-K GEMMs around it
+  const bool fused = knobs().x2y_fused && x2y_a2f_fusable(V.n, V.x.data(), Hd) && (cw & 3) == 0 &&
+                     ((reinterpret_cast<uintptr_t>(dcat + ydim)) & 15) == 0;
+  if (fused) {
+    for (int v0 = 0; v0 < V.n; v0 += GMAX_GROUP) {
+      fx_gemm_desc g1[GMAX_GROUP];
+      int n1 = 0;
+      for (int v = v0; v < std::min(V.n, v0 + GMAX_GROUP); ++v) {
+        const int nx = V.x[v + 1] - V.x[v], ny = V.y[v + 1] - V.y[v];
+        if (nx == 0 || ny == 0) continue;
+        const long long xr = (long long)V.x[v] * Hd;
+        fx_gemm_desc d = gemm_desc(nx, Hd, ny, op_cols(attn + V.a[v], nx), op_cols(dcat + (long long)V.y[v] * cw + ydim, cw),
+                                   dxv + xr, Hd);
+        d.split_k = pick_split(nx, Hd, ny);
+        d.workspace = spl;
+        g1[n1++] = d;
+      }
+      FX_TRY(launch_gemm_group(g1, n1, s));
+    }
+    FX_TRY(launch_x2y_a2f_bwd(dcat + ydim, cw, xv, xk, attn, dattn, dlogit, Hd, scale, V.n, V.y.data(), V.x.data(),
+                              V.a.data(), dL, dyq, s));
+    for (int v0 = 0; v0 < V.n; v0 += GMAX_GROUP) {
+      fx_gemm_desc g2[GMAX_GROUP];
+      int n2 = 0;
+      for (int v = v0; v < std::min(V.n, v0 + GMAX_GROUP); ++v) {
+        const int nx = V.x[v + 1] - V.x[v], ny = V.y[v + 1] - V.y[v];
+        if (nx == 0 || ny == 0) continue;
+        const long long xr = (long long)V.x[v] * Hd, yr = (long long)V.y[v] * Hd;
+        fx_gemm_desc d = gemm_desc(nx, Hd, ny, op_cols(dL + V.a[v], nx), op_cols(yq + yr, Hd), dxk + xr, Hd);
+        d.alpha = scale;
+        d.split_k = pick_split(nx, Hd, ny);
+        d.workspace = spl;
+        g2[n2++] = d;
+      }
+      FX_TRY(launch_gemm_group(g2, n2, s));
+    }
+  } else
   // per video: dP = dfeat . xv^T (+ dattn), dxv = attn^T . dfeat  (independent: one grouped launch
   // for up to two videos), softmax backward, then dyq = dlogit . xk, dxk = dlogit^T . yq (grouped)
   for (int v0 = 0; v0 < V.n; v0 += 2) {

@@ -880,7 +880,90 @@ __device__ __forceinline__ void wide8_stage(const Loader<AK, true, 2>& la0, cons
   }
 }
 
-template <int AK, int BKd, int PH>
+// FX_PREC_F32S on the f32 kernel's LDS ring: the fp32 stage images stay as they are and each wave
+// splits its own MFMA operands in registers (row-major A and B images only).  Per 16-deep k chunk q
+// a lane takes k in [32 lh + 8 q, +8) of the 64-deep stage (two float4 reads per operand: conflict-
+// free on the 68-float rows), splits the 8 values of A and of B into NP bf16x8 pieces and issues the
+// NP (NP + 1) / 2 piece products on v_mfma_f32_32x32x16_bf16: 4 LDS reads per 6 MFMAs where
+// pre-split images need 6, and 4 instead of 6 LDS bytes written per element.
+typedef __bf16 bf16x8r __attribute__((ext_vector_type(8)));
+
+template <int NP>
+__device__ __forceinline__ void split8(const float4& lo, const float4& hi, bf16x8r* p) {
+  const float e[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h = (__bf16)e[j];
+    p[0][j] = h;
+    if (NP > 1) {
+      const float r1 = e[j] - (float)h;
+      const __bf16 m = (__bf16)r1;
+      p[1][j] = m;
+      if (NP > 2) p[2][j] = (__bf16)(r1 - (float)m);
+    }
+  }
+}
+
+template <int NP>
+__device__ __forceinline__ void split_products(const bf16x8r* a, const bf16x8r* b, f32x16& acc0, f32x16& acc1) {
+  if (NP > 2) {
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc1, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc1, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc1, 0, 0, 0);
+  }
+  if (NP > 1) {
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc1, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc1, 0, 0, 0);
+  }
+  acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc0, 0, 0, 0);
+}
+
+template <int AK, int BKd, int PH, int NP>
+__device__ __forceinline__ void wide8s_stage(const Loader<AK, true, 2>& la0, const Loader<AK, true, 2>& la1,
+                                             const Loader<BKd, true, 2>& lb, const float* cur, float* wslot,
+                                             int kload, const float4* rs0, const float4* rs1, const float4* rsb,
+                                             unsigned ms0, unsigned ms1, unsigned msb, float4* rn0, float4* rn1,
+                                             float4* rnb, unsigned& mn0, unsigned& mn1, unsigned& mnb, int ai, int wr,
+                                             int wn, int li, int lh, f32x16& acc0, f32x16& acc1) {
+  const float* ia = cur + ai * IMG + (wr + li) * RS + 32 * lh;
+  const float* ib = cur + 2 * IMG + (wn * 32 + li) * RS + 32 * lh;
+  float4 fa[4][2], fb[4][2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    fa[q][0] = *reinterpret_cast<const float4*>(ia + 8 * q);
+    fa[q][1] = *reinterpret_cast<const float4*>(ia + 8 * q + 4);
+    fb[q][0] = *reinterpret_cast<const float4*>(ib + 8 * q);
+    fb[q][1] = *reinterpret_cast<const float4*>(ib + 8 * q + 4);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    bf16x8r pa[NP], pb[NP];
+    split8<NP>(fa[q][0], fa[q][1], pa);
+    split8<NP>(fb[q][0], fb[q][1], pb);
+    if (q + 2 < 4) {
+      fa[q + 2][0] = *reinterpret_cast<const float4*>(ia + 8 * (q + 2));
+      fa[q + 2][1] = *reinterpret_cast<const float4*>(ia + 8 * (q + 2) + 4);
+      fb[q + 2][0] = *reinterpret_cast<const float4*>(ib + 8 * (q + 2));
+      fb[q + 2][1] = *reinterpret_cast<const float4*>(ib + 8 * (q + 2) + 4);
+    }
+    split_products<NP>(pa, pb, acc0, acc1);
+    // the same staggered load / store placement as the f32 stage (two waves per SIMD)
+    if (q == (PH ? 2 : 0)) {
+      la0.load(kload, rn0, mn0);
+      la1.load(kload, rn1, mn1);
+    }
+    if (q == (PH ? 3 : 1)) lb.load(kload, rnb, mnb);
+    if (q == (PH ? 0 : 2)) {
+      la0.store(wslot, rs0, ms0);
+      la1.store(wslot + IMG, rs1, ms1);
+    }
+    if (q == (PH ? 1 : 3)) lb.store(wslot + 2 * IMG, rsb, msb);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int AK, int BKd, int PH, int NP = 0>
 __device__ __forceinline__ void wide8_kloop(const Loader<AK, true, 2>& la0, const Loader<AK, true, 2>& la1,
                                             const Loader<BKd, true, 2>& lb, float* lds, int kt0, int kt1, int ai,
                                             int wr, int wn, int li, int lh, f32x16& acc0, f32x16& acc1) {
@@ -910,8 +993,12 @@ __device__ __forceinline__ void wide8_kloop(const Loader<AK, true, 2>& la0, cons
   auto iter = [&](int i, const float4* s0, const float4* s1, const float4* sb, unsigned q0, unsigned q1, unsigned qb,
                   float4* n0, float4* n1, float4* nb, unsigned& p0, unsigned& p1, unsigned& pb) FX_INLINE {
     const int ws = slot == 0 ? 2 : slot - 1;
-    wide8_stage<AK, BKd, PH>(la0, la1, lb, lds + slot * SLOT, lds + ws * SLOT, min((kt0 + i + 3) * BK, klast), s0, s1,
-                         sb, q0, q1, qb, n0, n1, nb, p0, p1, pb, ai, wr, wn, li, lh, acc0, acc1);
+    if constexpr (NP == 0)
+      wide8_stage<AK, BKd, PH>(la0, la1, lb, lds + slot * SLOT, lds + ws * SLOT, min((kt0 + i + 3) * BK, klast), s0,
+                               s1, sb, q0, q1, qb, n0, n1, nb, p0, p1, pb, ai, wr, wn, li, lh, acc0, acc1);
+    else
+      wide8s_stage<AK, BKd, PH, NP>(la0, la1, lb, lds + slot * SLOT, lds + ws * SLOT, min((kt0 + i + 3) * BK, klast),
+                                    s0, s1, sb, q0, q1, qb, n0, n1, nb, p0, p1, pb, ai, wr, wn, li, lh, acc0, acc1);
     __syncthreads();   // (a barrier after the next stage's first MFMA group instead measured 3 % slower)
     slot = slot == 2 ? 0 : slot + 1;
   };
@@ -923,7 +1010,7 @@ __device__ __forceinline__ void wide8_kloop(const Loader<AK, true, 2>& la0, cons
   if (i < n) iter(i, a0x, a1x, bx, m0x, m1x, mbx, a0y, a1y, by, m0y, m1y, mby);
 }
 
-template <int AK, int BKIND>
+template <int AK, int BKIND, int NP = 0>
 __global__ __launch_bounds__(W8T) void gemm_f32_wide8_kernel(GemmDev g) {
   __shared__ float lds[NSLOT * 3 * IMG];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -949,9 +1036,9 @@ __global__ __launch_bounds__(W8T) void gemm_f32_wide8_kernel(GemmDev g) {
     acc1[i] = 0.f;
   }
   if (g.w8_stagger && wave >= 4)
-    wide8_kloop<AK, BKIND, 1>(la0, la1, lb, lds, kt0, kt1, ai, wr, wn, li, lh, acc0, acc1);
+    wide8_kloop<AK, BKIND, 1, NP>(la0, la1, lb, lds, kt0, kt1, ai, wr, wn, li, lh, acc0, acc1);
   else
-    wide8_kloop<AK, BKIND, 0>(la0, la1, lb, lds, kt0, kt1, ai, wr, wn, li, lh, acc0, acc1);
+    wide8_kloop<AK, BKIND, 0, NP>(la0, la1, lb, lds, kt0, kt1, ai, wr, wn, li, lh, acc0, acc1);
   const f32x16 acc = acc0 + acc1;
   const int col = n0 + wn * 32 + li;
   const int rbase = m0 + wm * 32 + 4 * lh;
@@ -2025,7 +2112,10 @@ int split_pieces_for(const GemmPlan& P, hipStream_t s) {
 
 template <int AK, int NP>
 int launch_split_b(const GemmPlan& P, hipStream_t s) {
-  if (P.bk == ROWS)
+  const int variant = knobs().split_variant;   // 0: operands split in registers (B row-major), 1: LDS images
+  if (P.bk == ROWS && variant == 0)
+    hipLaunchKernelGGL((gemm_f32_wide8_kernel<AK, ROWS, NP>), P.grid, dim3(W8T), 0, s, P.g);
+  else if (P.bk == ROWS)
     hipLaunchKernelGGL((gemm_split_wide8_kernel<AK, ROWS, NP>), P.grid, dim3(W8T), 0, s, P.g);
   else
     hipLaunchKernelGGL((gemm_split_wide8_kernel<AK, COLS, NP>), P.grid, dim3(W8T), 0, s, P.g);

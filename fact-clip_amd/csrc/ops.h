@@ -53,6 +53,11 @@ bool x2y_a2f_fusable(int nvid, const int* xoff, int Hd);
 int launch_x2y_a2f_fwd(const float* yq, const float* xk, const float* xv, int Hd, float scale, int nvid,
                        const int* yoff, const int* xoff, const long long* aoff, float* logit, float* attn,
                        float* feat, hipStream_t s);
+// backward, input-gradient side: dP = dfeat . xv^T (+ dattn), dlogit = attn (dP - rowsum(attn dP)) (+ dlogit_in),
+// dyq = scale dlogit . xk;  dfeat rows ld ldf (16-B aligned)
+int launch_x2y_a2f_bwd(const float* dfeat, long long ldf, const float* xv, const float* xk, const float* attn,
+                       const float* dattn, const float* dlogit_in, int Hd, float scale, int nvid, const int* yoff,
+                       const int* xoff, const long long* aoff, float* dlogit, float* dyq, hipStream_t s);
 
 // ---- composite helpers (capi.cpp) --------------------------------------------
 int ew_grid(long long total);

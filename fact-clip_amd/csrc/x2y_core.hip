@@ -30,14 +30,18 @@ constexpr int LS = XMAXK + 1;     // LDS row stride of the logit / probability t
 constexpr int FX_X2Y_MAXV = 16;   // videos per launch
 
 struct A2fArgs {
-  const float* yq;      // (Ny, Hd) query rows of every video, stacked
-  const float* xk;      // (Nx, Hd) keys of every video, stacked
-  const float* xv;      // (Nx, Hd)
-  float* logit;         // per video: (ny_v, nx_v) row-major at aoff[v]
-  float* attn;
-  float* feat;          // (Ny, Hd)
+  const float* q;       // query-side rows, (Ny, Hd) ld ldq: forward yq, backward dfeat
+  long long ldq;
+  const float* kmat;    // (Nx, Hd) phase-1 keys: forward xk, backward xv
+  const float* vmat;    // (Nx, Hd) phase-3 values: forward xv, backward xk
+  const float* attn_in; // backward: the forward's attn (per video (ny_v, nx_v) at aoff[v])
+  const float* add_p;   // backward: dattn, added to dP (nullable)
+  const float* add_l;   // backward: the direct dlogit, added to the softmax backward (nullable)
+  float* out_l;         // forward: logit; backward: dlogit
+  float* out_p;         // forward: attn
+  float* out_rows;      // (Ny, Hd): forward feat, backward dyq
   int Hd, nvid;
-  float scale;
+  float scale1, scale3; // forward: logit scale, 1; backward: 1, the logit scale (dyq = scale dlogit . xk)
   int yoff[FX_X2Y_MAXV + 1], xoff[FX_X2Y_MAXV + 1];
   long long aoff[FX_X2Y_MAXV + 1];
   int wg_off[FX_X2Y_MAXV + 1];    // first workgroup of each video
@@ -45,10 +49,15 @@ struct A2fArgs {
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
-__global__ __launch_bounds__(XT) void x2y_a2f_fwd_kernel(A2fArgs a) {
-  __shared__ float red[8][2][16][64];       // per-wave partial logit tiles (acc register r, lane)
-  __shared__ float P[XR][LS];               // scaled logits, then probabilities
-  __shared__ float rmax[XR], rsum[XR];
+// MODE 0: forward (logit, attn, feat); MODE 1: input-gradient side of the backward
+//   dP = dfeat . xv^T (+ dattn);  dlogit = attn (dP - sum_x attn dP) (+ direct dlogit);  dyq = scale dlogit . xk
+// (the weight-side products dxv = attn^T dfeat and dxk = scale dlogit^T yq reduce over the query rows and
+// stay split-K GEMMs)
+template <int MODE>
+__global__ __launch_bounds__(XT) void x2y_a2f_kernel(A2fArgs a) {
+  __shared__ float red[8][2][16][64];       // per-wave partial tiles (acc register r, lane)
+  __shared__ float P[XR][LS];               // phase-1 tile, then probabilities / dlogit
+  __shared__ float rs0[XR], rs1[XR];        // forward: row max, row sum; backward: row sum of attn dP
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 31, lh = lane >> 5;
   // video of this workgroup (constant indices only: the argument block stays in SGPRs)
   int v = 0;
@@ -70,8 +79,9 @@ __global__ __launch_bounds__(XT) void x2y_a2f_fwd_kernel(A2fArgs a) {
   const int r0 = ((int)blockIdx.x - wg0) * XR;     // first query row (video-local)
   const int Hd = a.Hd;
   const int nkb = nx > 32 ? 2 : 1;
+  const int rows = min(XR, ny - r0);
 
-  // ---- 1. logits: wave w sums k in [w Hd/8, (w+1) Hd/8) ----
+  // ---- 1. T = q . kmat^T over Hd: wave w sums k in [w Hd/8, (w+1) Hd/8) ----
   f32x16 acc[2];
 #pragma unroll
   for (int c = 0; c < 2; ++c)
@@ -79,9 +89,8 @@ __global__ __launch_bounds__(XT) void x2y_a2f_fwd_kernel(A2fArgs a) {
     for (int i = 0; i < 16; ++i) acc[c][i] = 0.f;
   {
     const int kw = Hd >> 3;
-    const int qr = min(r0 + li, ny - 1);
-    const float* pa = a.yq + (long long)(y0 + qr) * Hd;
-    const bool aok = r0 + li < ny;
+    const float* pa = a.q + (long long)(y0 + min(r0 + li, ny - 1)) * a.ldq;
+    const bool aok = li < rows;
     for (int k0 = w * kw; k0 < (w + 1) * kw; k0 += 32) {
       const int kk = k0 + 16 * lh;
       float av[16];
@@ -98,7 +107,7 @@ __global__ __launch_bounds__(XT) void x2y_a2f_fwd_kernel(A2fArgs a) {
         if (c < nkb) {
           const int key = c * 32 + li;
           const bool bok = key < nx;
-          const float* pb = a.xk + (long long)(x0 + min(key, nx - 1)) * Hd + kk;
+          const float* pb = a.kmat + (long long)(x0 + min(key, nx - 1)) * Hd + kk;
           float bv[16];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -125,57 +134,71 @@ __global__ __launch_bounds__(XT) void x2y_a2f_fwd_kernel(A2fArgs a) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) sum += red[q][c][r][l];
     const int row = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), col = c * 32 + (l & 31);
-    P[row][col] = a.scale * sum;
+    float t = a.scale1 * sum;
+    if (MODE == 1 && a.add_p && row < rows && col < nx) t += a.add_p[ao + (long long)(r0 + row) * nx + col];
+    P[row][col] = t;
   }
   __syncthreads();
 
-  // ---- 2. row softmax over the nx keys (a half-wave of 32 lanes per row, shuffles in 32) ----
+  // ---- 2. per row over the nx keys: 16 threads per row (row tid >> 4, columns (tid & 15) + 16 j) ----
   {
-    // 16 threads per row, 32 rows = 512 threads: thread t owns row t >> 4, columns (t & 15) + 16 j
     const int row = tid >> 4, c0 = tid & 15;
-    float m = -3.0e38f;
+    const bool rok = row < rows;
+    if (MODE == 0) {
+      float m = -3.0e38f;
 #pragma unroll
-    for (int j = 0; j < XMAXK / 16; ++j) {
-      const int col = c0 + 16 * j;
-      if (col < nx) m = fmaxf(m, P[row][col]);
-    }
+      for (int j = 0; j < XMAXK / 16; ++j) {
+        const int col = c0 + 16 * j;
+        if (col < nx) m = fmaxf(m, P[row][col]);
+      }
 #pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 16));
-    float sum = 0.f;
+      for (int o = 8; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 16));
+      float sum = 0.f;
 #pragma unroll
-    for (int j = 0; j < XMAXK / 16; ++j) {
-      const int col = c0 + 16 * j;
-      if (col < nx) sum += __expf(P[row][col] - m);
-    }
+      for (int j = 0; j < XMAXK / 16; ++j) {
+        const int col = c0 + 16 * j;
+        if (col < nx) sum += __expf(P[row][col] - m);
+      }
 #pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 16);
-    if (c0 == 0) {
-      rmax[row] = m;
-      rsum[row] = sum;
+      for (int o = 8; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 16);
+      if (c0 == 0) {
+        rs0[row] = m;
+        rs1[row] = sum;
+      }
+    } else {
+      float sum = 0.f;
+#pragma unroll
+      for (int j = 0; j < XMAXK / 16; ++j) {
+        const int col = c0 + 16 * j;
+        if (col < nx && rok) sum += a.attn_in[ao + (long long)(r0 + row) * nx + col] * P[row][col];
+      }
+#pragma unroll
+      for (int o = 8; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 16);
+      if (c0 == 0) rs1[row] = sum;
     }
   }
   __syncthreads();
-  {
-    // logit and attn out (row-major, ld nx, coalesced over the tile), probabilities kept in LDS
-    const int rows = min(XR, ny - r0);
-    for (int e = tid; e < XR * XMAXK; e += XT) {
-      const int row = e / XMAXK, col = e - row * XMAXK;
-      float p = 0.f;
-      if (col < nx) {
-        const float l = P[row][col];
-        p = __expf(l - rmax[row]) / rsum[row];
-        if (row < rows) {
-          const long long o = ao + (long long)(r0 + row) * nx + col;
-          a.logit[o] = l;
-          a.attn[o] = p;
-        }
+  for (int e = tid; e < XR * XMAXK; e += XT) {
+    const int row = e / XMAXK, col = e - row * XMAXK;
+    float p = 0.f;
+    if (col < nx && row < rows) {
+      const long long o = ao + (long long)(r0 + row) * nx + col;
+      const float t = P[row][col];
+      if (MODE == 0) {
+        p = __expf(t - rs0[row]) / rs1[row];
+        a.out_l[o] = t;
+        a.out_p[o] = p;
+      } else {
+        p = a.attn_in[o] * (t - rs1[row]);
+        if (a.add_l) p += a.add_l[o];
+        a.out_l[o] = p;
       }
-      P[row][col] = p;   // (each element is read and rewritten by the same thread)
     }
+    P[row][col] = p;   // (each element is read and rewritten by the same thread)
   }
   __syncthreads();
 
-  // ---- 3. feat = P . xv: column tiles n0 = 32 (2 w + t), t = 0, 1 ----
+  // ---- 3. out rows = scale3 P . vmat: column tiles n0 = 32 (2 w + t), t = 0, 1 ----
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int n0 = 32 * (2 * w + t);
@@ -188,7 +211,7 @@ __global__ __launch_bounds__(XT) void x2y_a2f_fwd_kernel(A2fArgs a) {
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
         const int key = k0 + 16 * lh + s;
-        const float x = a.xv[(long long)(x0 + min(key, nx - 1)) * Hd + n0 + li];
+        const float x = a.vmat[(long long)(x0 + min(key, nx - 1)) * Hd + n0 + li];
         bv[s] = key < nx ? x : 0.f;
       }
 #pragma unroll
@@ -197,9 +220,32 @@ __global__ __launch_bounds__(XT) void x2y_a2f_fwd_kernel(A2fArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
-      if (r0 + row < ny) a.feat[(long long)(y0 + r0 + row) * Hd + n0 + li] = f[r];
+      if (row < rows) a.out_rows[(long long)(y0 + r0 + row) * Hd + n0 + li] = a.scale3 * f[r];
     }
   }
+}
+
+int launch_a2f(A2fArgs& a, int mode, const int* yoff, const int* xoff, const long long* aoff, hipStream_t s) {
+  int wg = 0;
+  for (int v = 0; v <= a.nvid; ++v) {
+    a.yoff[v] = yoff[v];
+    a.xoff[v] = xoff[v];
+    a.aoff[v] = aoff[v];
+    a.wg_off[v] = wg;
+    if (v < a.nvid) {
+      const int ny = yoff[v + 1] - yoff[v], nx = xoff[v + 1] - xoff[v];
+      // an empty key side leaves no workgroup: softmax over nothing has no rows to write
+      if (nx > 0) wg += (ny + XR - 1) / XR;
+    }
+  }
+  for (int v = a.nvid + 1; v <= FX_X2Y_MAXV; ++v) a.wg_off[v] = wg;
+  if (wg == 0) return FX_OK;
+  if (mode == 0)
+    hipLaunchKernelGGL(x2y_a2f_kernel<0>, dim3(wg), dim3(XT), 0, s, a);
+  else
+    hipLaunchKernelGGL(x2y_a2f_kernel<1>, dim3(wg), dim3(XT), 0, s, a);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
 }
 
 }  // namespace
@@ -216,32 +262,40 @@ int launch_x2y_a2f_fwd(const float* yq, const float* xk, const float* xv, int Hd
                        float* feat, hipStream_t s) {
   FX_REQUIRE(x2y_a2f_fusable(nvid, xoff, Hd), "x2y a2f core: <= 64 keys per video, Hd % 256 == 0, <= 16 videos");
   A2fArgs a{};
-  a.yq = yq;
-  a.xk = xk;
-  a.xv = xv;
-  a.logit = logit;
-  a.attn = attn;
-  a.feat = feat;
+  a.q = yq;
+  a.ldq = Hd;
+  a.kmat = xk;
+  a.vmat = xv;
+  a.out_l = logit;
+  a.out_p = attn;
+  a.out_rows = feat;
   a.Hd = Hd;
   a.nvid = nvid;
-  a.scale = scale;
-  int wg = 0;
-  for (int v = 0; v <= nvid; ++v) {
-    a.yoff[v] = yoff[v];
-    a.xoff[v] = xoff[v];
-    a.aoff[v] = aoff[v];
-    a.wg_off[v] = wg;
-    if (v < nvid) {
-      const int ny = yoff[v + 1] - yoff[v], nx = xoff[v + 1] - xoff[v];
-      // an empty key side leaves no workgroup: softmax over nothing has no rows to write
-      if (nx > 0) wg += (ny + XR - 1) / XR;
-    }
-  }
-  for (int v = nvid + 1; v <= FX_X2Y_MAXV; ++v) a.wg_off[v] = wg;
-  if (wg == 0) return FX_OK;
-  hipLaunchKernelGGL(x2y_a2f_fwd_kernel, dim3(wg), dim3(XT), 0, s, a);
-  FX_CHECK_HIP(hipGetLastError());
-  return FX_OK;
+  a.scale1 = scale;
+  a.scale3 = 1.f;
+  return launch_a2f(a, 0, yoff, xoff, aoff, s);
+}
+
+int launch_x2y_a2f_bwd(const float* dfeat, long long ldf, const float* xv, const float* xk, const float* attn,
+                       const float* dattn, const float* dlogit_in, int Hd, float scale, int nvid, const int* yoff,
+                       const int* xoff, const long long* aoff, float* dlogit, float* dyq, hipStream_t s) {
+  FX_REQUIRE(x2y_a2f_fusable(nvid, xoff, Hd), "x2y a2f core: <= 64 keys per video, Hd % 256 == 0, <= 16 videos");
+  FX_REQUIRE(ldf % 4 == 0 && (reinterpret_cast<uintptr_t>(dfeat) & 15) == 0, "x2y a2f bwd: dfeat rows must be 16-B aligned");
+  A2fArgs a{};
+  a.q = dfeat;
+  a.ldq = ldf;
+  a.kmat = xv;
+  a.vmat = xk;
+  a.attn_in = attn;
+  a.add_p = dattn;
+  a.add_l = dlogit_in;
+  a.out_l = dlogit;
+  a.out_rows = dyq;
+  a.Hd = Hd;
+  a.nvid = nvid;
+  a.scale1 = 1.f;
+  a.scale3 = scale;
+  return launch_a2f(a, 1, yoff, xoff, aoff, s);
 }
 
 }  // namespace fx
