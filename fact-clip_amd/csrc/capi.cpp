@@ -1465,7 +1465,7 @@ long long fx_x2y_workspace_floats(int Nx, int xdim, int Ny, int ydim, int Hd, in
                                   const int* x_off, const int* y_off) {
   const VidRows v = vid_rows(Nx, Ny, nvid, x_off, y_off);
   return x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, v) + (long long)Ny * (ydim + Hd) +
-         x2y_side_ws(Nx, xdim, Ny, ydim, Hd, outdim);
+         x2y_side_ws(Nx, xdim, Ny, ydim, Hd, outdim) + x2y_f2a_ws_floats(v.n, v.x.data(), Hd);
 }
 
 // catd = dropout(cat[Y, feat]) (basic.py:382), mask index r (ydim + Hd) + c
@@ -1524,8 +1524,15 @@ int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpo
   FX_TRY(linear_fwd(yin, ldyin, Ny, ydim, wq, bq, yq, Hd, Hd, 0, s));
   const float scale = 1.0f / std::sqrt((float)Hd);
   // a short key side (the a2f map: <= 64 action tokens per video): the whole core in one launch
-  if (knobs().x2y_fused && x2y_a2f_fusable(V.n, V.x.data(), Hd) && ((reinterpret_cast<uintptr_t>(yq)) & 15) == 0) {
+  const bool al16 = ((reinterpret_cast<uintptr_t>(yq) | reinterpret_cast<uintptr_t>(xk)) & 15) == 0;
+  if (knobs().x2y_fused && x2y_a2f_fusable(V.n, V.x.data(), Hd) && al16) {
     FX_TRY(launch_x2y_a2f_fwd(yq, xk, xv, Hd, scale, V.n, V.y.data(), V.x.data(), V.a.data(), logit, attn, feat, s));
+  } else if (knobs().x2y_fused && x2y_f2a_fusable(V.n, V.x.data(), V.y.data(), Hd) && al16) {
+    // the f2a map (frames -> tokens): per-chunk partials after every other region of the workspace
+    float* f2a_ws = workspace + x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, V) + (long long)Ny * (ydim + Hd) +
+                    x2y_side_ws(Nx, xdim, Ny, ydim, Hd, outdim);
+    FX_TRY(launch_x2y_f2a_fwd(yq, xk, xv, Hd, scale, V.n, V.y.data(), V.x.data(), V.a.data(), logit, attn, feat,
+                              f2a_ws, s));
   } else
   // per video: logits = scale yq . xk^T, attn = softmax(logits), feat = attn . xv  (the GEMMs of up to
   // two videos in one grouped launch each)

@@ -53,6 +53,13 @@ bool x2y_a2f_fusable(int nvid, const int* xoff, int Hd);
 int launch_x2y_a2f_fwd(const float* yq, const float* xk, const float* xv, int Hd, float scale, int nvid,
                        const int* yoff, const int* xoff, const long long* aoff, float* logit, float* attn,
                        float* feat, hipStream_t s);
+// long key side (f2a: <= 64 queries per video over up to T keys): chunk kernel + ordered merge; ws holds
+// x2y_f2a_ws_floats(...) floats of per-chunk partials
+bool x2y_f2a_fusable(int nvid, const int* xoff, const int* yoff, int Hd);
+long long x2y_f2a_ws_floats(int nvid, const int* xoff, int Hd);
+int launch_x2y_f2a_fwd(const float* yq, const float* xk, const float* xv, int Hd, float scale, int nvid,
+                       const int* yoff, const int* xoff, const long long* aoff, float* logit, float* attn,
+                       float* feat, float* ws, hipStream_t s);
 // backward, input-gradient side: dP = dfeat . xv^T (+ dattn), dlogit = attn (dP - rowsum(attn dP)) (+ dlogit_in),
 // dyq = scale dlogit . xk;  dfeat rows ld ldf (16-B aligned)
 int launch_x2y_a2f_bwd(const float* dfeat, long long ldf, const float* xv, const float* xk, const float* attn,

@@ -19,6 +19,8 @@
 #include "fx_common.h"
 #include "ops.h"
 
+#include <algorithm>
+
 namespace fx {
 namespace {
 
@@ -248,6 +250,212 @@ int launch_a2f(A2fArgs& a, int mode, const int* yoff, const int* xoff, const lon
   return FX_OK;
 }
 
+// ---------------------------------------------------------------- long key side (the f2a map)
+// X = frames (nx up to T keys), Y = the action tokens (ny <= 64 queries per video), Hd = 512:
+//   chunk kernel, one workgroup per 64 keys of a video: S = scale yq . xk_chunk^T (ny x 64, the Hd-deep
+//   sum split over the waves), logit written, chunk row max m_c and sum l_c = sum exp(S - m_c), the
+//   partial F_c = exp(S - m_c) . xv_chunk (ny x Hd) to a workspace slab;
+//   merge kernel, one workgroup per (video, query row): M = max_c m_c, L = sum_c l_c e^(m_c - M),
+//   feat = sum_c e^(m_c - M) F_c / L in chunk order (deterministic), attn = exp(logit - M) / L.
+// Algorithmic bytes per video: xk, xv (2 nx Hd floats) + logit / attn (2 ny nx) + feat; the slabs add
+// 2 ny Hd floats per 64 keys (write + read), 1/32 of the key bytes at ny = 32.
+constexpr int FC = 64;             // keys per chunk
+constexpr int FMAXQ = 64;          // queries per video
+
+struct F2aArgs {
+  const float* yq;      // (Ny, Hd)
+  const float* xk;      // (Nx, Hd)
+  const float* xv;      // (Nx, Hd)
+  float* logit;         // per video (ny_v, nx_v) at aoff[v]
+  float* attn;
+  float* feat;          // (Ny, Hd)
+  float* part;          // (chunks, FMAXQ, Hd) partial F_c
+  float* stats;         // (chunks, FMAXQ, 2): m_c, l_c
+  int Hd, nvid;
+  float scale;
+  int yoff[FX_X2Y_MAXV + 1], xoff[FX_X2Y_MAXV + 1];
+  long long aoff[FX_X2Y_MAXV + 1];
+  int ch_off[FX_X2Y_MAXV + 1];    // first chunk of each video
+};
+
+__device__ __forceinline__ void f2a_video(const F2aArgs& a, int v, int& y0, int& ny, int& x0, int& nx, long long& ao,
+                                          int& c0) {
+#pragma unroll
+  for (int i = 0; i < FX_X2Y_MAXV; ++i)
+    if (i == v) {
+      y0 = a.yoff[i];
+      ny = a.yoff[i + 1] - a.yoff[i];
+      x0 = a.xoff[i];
+      nx = a.xoff[i + 1] - a.xoff[i];
+      ao = a.aoff[i];
+      c0 = a.ch_off[i];
+    }
+}
+
+__global__ __launch_bounds__(XT) void x2y_f2a_chunk_kernel(F2aArgs a) {
+  __shared__ float red[8][16][64];
+  __shared__ float S[FMAXQ][FC + 1];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 31, lh = lane >> 5;
+  int v = 0;
+#pragma unroll
+  for (int i = 1; i < FX_X2Y_MAXV; ++i)
+    if (i < a.nvid && (int)blockIdx.x >= a.ch_off[i]) v = i;
+  int y0 = 0, ny = 0, x0 = 0, nx = 0, c0 = 0;
+  long long ao = 0;
+  f2a_video(a, v, y0, ny, x0, nx, ao, c0);
+  const int chunk = blockIdx.x;
+  const int k0c = ((int)blockIdx.x - c0) * FC;          // first key of the chunk (video-local)
+  const int keys = min(FC, nx - k0c);
+  const int Hd = a.Hd;
+  const int nrb = ny > 32 ? 2 : 1;                      // 32-row query blocks
+  const int nblk = 2 * nrb;                             // output blocks (query block, key block)
+  const int wpb = 8 / nblk;                             // waves per block (4 or 2)
+  const int blk = w % nblk, kpart = w / nblk;
+  const int rb = blk >> 1, cb = blk & 1;
+
+  // ---- 1. S block (rb, cb) partial over k in [kpart Hd/wpb, +Hd/wpb) ----
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  {
+    const int q = rb * 32 + li, key = k0c + cb * 32 + li;
+    const bool aok = q < ny, bok = cb * 32 + li < keys;
+    const float* pa = a.yq + (long long)(y0 + min(q, ny - 1)) * Hd;
+    const float* pb = a.xk + (long long)(x0 + min(key, nx - 1)) * Hd;
+    const int kw = Hd / wpb;
+    for (int k0 = kpart * kw; k0 < (kpart + 1) * kw; k0 += 32) {
+      const int kk = k0 + 16 * lh;
+      float av[16], bv[16];
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) {
+        const float4 ta = ld4(pa + kk + 4 * qd), tb = ld4(pb + kk + 4 * qd);
+        av[4 * qd] = aok ? ta.x : 0.f;
+        av[4 * qd + 1] = aok ? ta.y : 0.f;
+        av[4 * qd + 2] = aok ? ta.z : 0.f;
+        av[4 * qd + 3] = aok ? ta.w : 0.f;
+        bv[4 * qd] = bok ? tb.x : 0.f;
+        bv[4 * qd + 1] = bok ? tb.y : 0.f;
+        bv[4 * qd + 2] = bok ? tb.z : 0.f;
+        bv[4 * qd + 3] = bok ? tb.w : 0.f;
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s2], bv[s2], acc, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) red[w][r][lane] = acc[r];
+  __syncthreads();
+  for (int e = tid; e < nblk * 1024; e += XT) {
+    const int b = e >> 10, r = (e >> 6) & 15, l = e & 63;
+    float sum = 0.f;
+    for (int p = 0; p < wpb; ++p) sum += red[p * nblk + b][r][l];
+    const int row = (b >> 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), col = (b & 1) * 32 + (l & 31);
+    S[row][col] = a.scale * sum;
+  }
+  __syncthreads();
+
+  // ---- 2. logit out; chunk row max / sum; S <- exp(S - m) (0 outside the chunk's keys) ----
+  {
+    // 8 threads per query row (64 rows), 8 keys each
+    const int row = tid >> 3, c8 = tid & 7;
+    float m = -3.0e38f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = c8 + 8 * j;
+      if (col < keys) m = fmaxf(m, S[row][col]);
+    }
+#pragma unroll
+    for (int o = 4; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 8));
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = c8 + 8 * j;
+      const float t = S[row][col];
+      if (row < ny && col < keys) a.logit[ao + (long long)row * nx + k0c + col] = t;
+      const float e = col < keys ? __expf(t - m) : 0.f;
+      sum += e;
+      S[row][col] = e;   // (read and rewritten by the same thread)
+    }
+#pragma unroll
+    for (int o = 4; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 8);
+    if (c8 == 0 && row < ny) {
+      a.stats[((long long)chunk * FMAXQ + row) * 2] = m;
+      a.stats[((long long)chunk * FMAXQ + row) * 2 + 1] = sum;
+    }
+  }
+  __syncthreads();
+
+  // ---- 3. F_c = S . xv_chunk: (nrb x Hd/32) output tiles over the 8 waves, K = 64 keys ----
+  const int ntile = nrb * (Hd >> 5);
+  for (int t = w; t < ntile; t += 8) {
+    const int tr = t / (Hd >> 5), n0 = (t - tr * (Hd >> 5)) * 32;
+    f32x16 f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) f[i] = 0.f;
+#pragma unroll
+    for (int kc = 0; kc < FC; kc += 32) {
+      float bv[16];
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) {
+        const int key = kc + 16 * lh + s2;
+        const float x = a.xv[(long long)(x0 + min(k0c + key, nx - 1)) * Hd + n0 + li];
+        bv[s2] = key < keys ? x : 0.f;
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2)
+        f = __builtin_amdgcn_mfma_f32_32x32x2f32(S[tr * 32 + li][kc + 16 * lh + s2], bv[s2], f, 0, 0, 0);
+    }
+    float* dst = a.part + (long long)chunk * FMAXQ * Hd;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = tr * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      if (row < ny) dst[(long long)row * Hd + n0 + li] = f[r];
+    }
+  }
+}
+
+// one workgroup per (video, query row)
+__global__ __launch_bounds__(XT) void x2y_f2a_merge_kernel(F2aArgs a) {
+  __shared__ float wgt[1024];
+  __shared__ float ML[2];
+  const int tid = threadIdx.x;
+  const int v = blockIdx.y, row = blockIdx.x;
+  int y0 = 0, ny = 0, x0 = 0, nx = 0, c0 = 0;
+  long long ao = 0;
+  f2a_video(a, v, y0, ny, x0, nx, ao, c0);
+  if (row >= ny || nx == 0) return;
+  const int nch = (nx + FC - 1) / FC;
+  if (tid < 64) {
+    // M and L over the video's chunks, one wave, fixed order per lane then a fixed shuffle tree
+    float m = -3.0e38f;
+    for (int c = tid; c < nch; c += 64) m = fmaxf(m, a.stats[((long long)(c0 + c) * FMAXQ + row) * 2]);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    float l = 0.f;
+    for (int c = tid; c < nch; c += 64) {
+      const float* st = a.stats + ((long long)(c0 + c) * FMAXQ + row) * 2;
+      l += st[1] * __expf(st[0] - m);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) l += __shfl_xor(l, o, 64);
+    if (tid == 0) {
+      ML[0] = m;
+      ML[1] = l;
+    }
+  }
+  __syncthreads();
+  const float M = ML[0], invL = 1.f / ML[1];
+  for (int c = tid; c < nch; c += XT) wgt[c] = __expf(a.stats[((long long)(c0 + c) * FMAXQ + row) * 2] - M) * invL;
+  __syncthreads();
+  for (int n = tid; n < a.Hd; n += XT) {
+    float acc = 0.f;
+    for (int c = 0; c < nch; ++c) acc += wgt[c] * a.part[((long long)(c0 + c) * FMAXQ + row) * a.Hd + n];
+    a.feat[(long long)(y0 + row) * a.Hd + n] = acc;
+  }
+  const long long o = ao + (long long)row * nx;
+  for (int x = tid; x < nx; x += XT) a.attn[o + x] = __expf(a.logit[o + x] - M) * invL;
+}
+
 }  // namespace
 
 bool x2y_a2f_fusable(int nvid, const int* xoff, int Hd) {
@@ -296,6 +504,59 @@ int launch_x2y_a2f_bwd(const float* dfeat, long long ldf, const float* xv, const
   a.scale1 = 1.f;
   a.scale3 = scale;
   return launch_a2f(a, 1, yoff, xoff, aoff, s);
+}
+
+bool x2y_f2a_fusable(int nvid, const int* xoff, const int* yoff, int Hd) {
+  if (nvid < 1 || nvid > FX_X2Y_MAXV || Hd % 256 != 0 || Hd > XT) return false;
+  long long nch = 0;
+  for (int v = 0; v < nvid; ++v) {
+    const int nxv = xoff[v + 1] - xoff[v];
+    if (yoff[v + 1] - yoff[v] > FMAXQ) return false;
+    nch += (nxv + FC - 1) / FC;
+    if ((nxv + FC - 1) / FC > 1024) return false;     // merge weights in LDS
+  }
+  return nch > 0;
+}
+
+long long x2y_f2a_ws_floats(int nvid, const int* xoff, int Hd) {
+  long long nch = 0;
+  for (int v = 0; v < nvid; ++v) nch += (xoff[v + 1] - xoff[v] + FC - 1) / FC;
+  return nch * FMAXQ * ((long long)Hd + 2);
+}
+
+int launch_x2y_f2a_fwd(const float* yq, const float* xk, const float* xv, int Hd, float scale, int nvid,
+                       const int* yoff, const int* xoff, const long long* aoff, float* logit, float* attn,
+                       float* feat, float* ws, hipStream_t s) {
+  FX_REQUIRE(x2y_f2a_fusable(nvid, xoff, yoff, Hd), "x2y f2a core: <= 64 queries per video, Hd % 256 == 0");
+  F2aArgs a{};
+  a.yq = yq;
+  a.xk = xk;
+  a.xv = xv;
+  a.logit = logit;
+  a.attn = attn;
+  a.feat = feat;
+  a.Hd = Hd;
+  a.nvid = nvid;
+  a.scale = scale;
+  int nch = 0, maxq = 0;
+  for (int v = 0; v <= nvid; ++v) {
+    a.yoff[v] = yoff[v];
+    a.xoff[v] = xoff[v];
+    a.aoff[v] = aoff[v];
+    a.ch_off[v] = nch;
+    if (v < nvid) {
+      nch += (xoff[v + 1] - xoff[v] + FC - 1) / FC;
+      maxq = std::max(maxq, yoff[v + 1] - yoff[v]);
+    }
+  }
+  for (int v = nvid + 1; v <= FX_X2Y_MAXV; ++v) a.ch_off[v] = nch;
+  a.part = ws;
+  a.stats = ws + (long long)nch * FMAXQ * Hd;
+  if (nch == 0 || maxq == 0) return FX_OK;
+  hipLaunchKernelGGL(x2y_f2a_chunk_kernel, dim3(nch), dim3(XT), 0, s, a);
+  hipLaunchKernelGGL(x2y_f2a_merge_kernel, dim3(maxq, nvid), dim3(XT), 0, s, a);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
 }
 
 }  // namespace fx
