@@ -464,6 +464,7 @@ const Knobs& knobs() {
     if (const char* p = env("FX_SIDE_MAXWG")) k.side_maxwg = std::max(0, std::atoi(p));
     if (const char* p = env("FX_X2Y_FUSED")) k.x2y_fused = p[0] != '0';
     if (const char* p = env("FX_SPLIT_VARIANT")) k.split_variant = std::atoi(p);
+    if (const char* p = env("FX_MSTCN_TAIL")) k.mstcn_tail = p[0] != '0';
   });
   return k;
 }
@@ -645,7 +646,13 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   // a main-stream write waits for the side stream's layer that last read that buffer.
   SideStream* ss = (p->layernorm || drop) ? nullptr : side_stream();
   hipStream_t sd = ss ? ss->s : s;
-  const bool defer = !fchain && !p->layernorm && !drop && NL > 0 && mstcn_defer_ok(p, g);
+  // the input block's stack (in_map) is the LAST work of the backward pass: its batched deferred weight
+  // gradients run after the chain with nothing left to overlap (a ~0.7 ms side-stream tail that the
+  // end-of-backward join waits for).  FX_MSTCN_TAIL=1 gives that stack the per-layer schedule that
+  // overlaps the chain instead; measured even (the per-layer split-K GEMMs slow the chain by as much),
+  // so it is off by default
+  const bool tail = p->in_map && knobs().mstcn_tail;
+  const bool defer = !fchain && !p->layernorm && !drop && NL > 0 && !tail && mstcn_defer_ok(p, g);
   // FX_SIDE_MAXWG=n: the side stream's split-K GEMMs keep within n workgroups (A/B diagnostic)
   GridCap gcap(ss ? knobs().side_maxwg : 0);
   auto fork = [&](int e) -> int {   // side stream waits for the main stream's work so far

@@ -132,8 +132,9 @@ struct Knobs {
   int defer_split = 8;
   bool mstcn_defer = true;
   int side_maxwg = 0;
-  bool x2y_fused = true;
-  int split_variant = 0;    // FX_SPLIT_VARIANT=1: the LDS-image split kernel for every FX_PREC_F32S GEMM    // FX_X2Y_FUSED=0: the X2Y attention core as grouped GEMM + softmax launches
+  bool x2y_fused = true;    // FX_X2Y_FUSED=0: the X2Y attention core as grouped GEMM + softmax launches
+  int split_variant = 0;    // FX_SPLIT_VARIANT=1: the LDS-image split kernel for every FX_PREC_F32S GEMM
+  bool mstcn_tail = false;  // FX_MSTCN_TAIL=1: the input block's MS-TCN keeps per-layer side dW (A/B: even)
 };
 const Knobs& knobs();
 

@@ -920,6 +920,8 @@ def status_raise(value, dev):
 
 def check_device_status(dev=None):
     """Synchronous check of the status word (e.g. after the last backward of a run)."""
+    from .models import vloss
+    vloss.resolve_pending()
     dev = torch.device("cuda", torch.cuda.current_device()) if dev is None else torch.device(dev)
     if dev in _status:
         status_raise(int(_status[dev][0].item()), dev)

@@ -681,6 +681,7 @@ def _forward_videos(net, seq_list, label_list, compute_loss):
     transcript is only built where it is used (FACT.trans), labels reach the host by an async copy
     started before the forward, predictions and loss floats come back in one read-back."""
     clip = isinstance(net, FACT_CLIP)
+    vloss.resolve_pending()     # the previous step's read-back (raises a kernel failure it carried)
     hosts = [_label_to_host(l_) for l_ in label_list]
     save_list, losses, pending, preds = [], [], [], []
 

@@ -115,6 +115,97 @@ def _ptr_rows(t, row0, ld):
     return t.data_ptr() + 4 * row0 * ld
 
 
+_PENDING = []          # read-backs not resolved yet (resolved at the next forward at the latest)
+
+
+class LazySave(dict):
+    """One video's save dict (``pred``, ``loss``) of a step whose host read-back is still in flight:
+    every read resolves the read-back first (waiting for the device only if it has not finished)."""
+    __slots__ = ("_pending",)
+
+    def __init__(self, pending):
+        super().__init__()
+        self._pending = pending
+
+    def _r(self):
+        if self._pending is not None:
+            self._pending.resolve()
+
+    def __getitem__(self, k):
+        self._r()
+        return dict.__getitem__(self, k)
+
+    def get(self, k, default=None):
+        self._r()
+        return dict.get(self, k, default)
+
+    def __contains__(self, k):
+        self._r()
+        return dict.__contains__(self, k)
+
+    def __iter__(self):
+        self._r()
+        return dict.__iter__(self)
+
+    def __len__(self):
+        self._r()
+        return dict.__len__(self)
+
+    def keys(self):
+        self._r()
+        return dict.keys(self)
+
+    def values(self):
+        self._r()
+        return dict.values(self)
+
+    def items(self):
+        self._r()
+        return dict.items(self)
+
+    def copy(self):
+        self._r()
+        return dict(dict.items(self))
+
+    def __eq__(self, other):
+        self._r()
+        return dict.__eq__(self, other)
+
+    def __repr__(self):
+        self._r()
+        return dict.__repr__(self)
+
+
+class PendingReadback:
+    """The step's single read-back (predictions, loss floats, kernel status word) as pinned-memory
+    copies behind an event; ``resolve`` waits for the event (normally long past), raises a kernel-side
+    failure (GRU timeout) and fills the LazySave dicts in place."""
+
+    def __init__(self, ready, check, fill, nvid):
+        self.ready, self.check, self.fill = ready, check, fill
+        self.saves = [LazySave(self) for _ in range(nvid)]
+        self.done = False
+        _PENDING.append(self)
+
+    def resolve(self):
+        if self.done:
+            return
+        self.done = True
+        if self in _PENDING:
+            _PENDING.remove(self)
+        for d in self.saves:
+            d._pending = None
+        self.ready.synchronize()
+        self.check()
+        self.fill(self.saves)
+
+
+def resolve_pending():
+    """Resolve every read-back still in flight (called at the start of each forward)."""
+    while _PENDING:
+        _PENDING[0].resolve()
+
+
 class _LossFn(torch.autograd.Function):
     """out = fx_loss_terms_fwd(term table); backward writes every input's gradient whole."""
 
@@ -136,6 +227,9 @@ class _LossFn(torch.autograd.Function):
         nx.check(lib.fx_loss_terms_bwd(ctypes.addressof(plan["terms_host"]), plan["terms_dev"], plan["nterms"],
                                        plan["coef_dev"], plan["nout"], nx.ptr(gout), nx.ptr(plan["ws"]), nx.stream()),
                  "fx_loss_terms_bwd")
+        rb = plan.get("readback")
+        if rb is not None and not rb.done:       # the step's read-back resolves when the backward pass ends
+            torch.autograd.Variable._execution_engine.queue_callback(rb.resolve)
         return (None,) + tuple(plan["grads"])
 
 
@@ -454,24 +548,32 @@ def run(net, vb, compute_loss, early=None):
         if con_on[v]:
             o = 1 + v * per
             net.fact_loss, net.contrastive_loss = out[o + 1], out[o + 2]
-    # one synchronisation for the predictions and every loss value
+    # ONE device->host read-back for the predictions and every loss value, enqueued here and resolved
+    # later: at the end of the backward pass (autograd callback queued by _LossFn.backward), at the first
+    # read of a save entry, or at the next forward -- whichever comes first -- so loss.backward() is
+    # issued while the device still finishes the forward instead of after a drain
     out_h = torch.empty(out.shape, dtype=torch.float32, pin_memory=True)
     pred_h = torch.empty(pred.shape, dtype=torch.int32, pin_memory=True)
     st_h = torch.empty(1, dtype=torch.int32, pin_memory=True)
     out_h.copy_(out.detach(), non_blocking=True)
     pred_h.copy_(pred, non_blocking=True)
     st_h.copy_(fxf.device_status(dev)[:1], non_blocking=True)   # kernel-side failures (GRU timeout)
-    torch.cuda.current_stream().synchronize()
-    fxf.status_raise(int(st_h[0]), dev)
-    vals = out_h.tolist()
-    ph = pred_h.numpy()
-    save_list = [{"pred": ph[fo[v]:fo[v + 1]].astype(np.int64)} for v in range(nvid)]
-    for v in range(nvid):
-        o = 1 + v * per
-        d = {"loss": vals[o]}
-        if con_on[v]:
-            prev = (vals[o + 1], vals[o + 2])
-        if prev is not None:
-            d["fact_loss"], d["contrastive_loss"] = prev
-        save_list[v]["loss"] = d
-    return out[0], save_list
+    ready = torch.cuda.Event()
+    ready.record()
+
+    def fill(saves):
+        vals = out_h.tolist()
+        ph = pred_h.numpy()
+        prev_ = prev
+        for v in range(nvid):
+            o = 1 + v * per
+            d = {"loss": vals[o]}
+            if con_on[v]:
+                prev_ = (vals[o + 1], vals[o + 2])
+            if prev_ is not None:
+                d["fact_loss"], d["contrastive_loss"] = prev_
+            saves[v]["pred"] = ph[fo[v]:fo[v + 1]].astype(np.int64)
+            saves[v]["loss"] = d
+    pending = PendingReadback(ready, lambda: fxf.status_raise(int(st_h[0]), dev), fill, nvid)
+    plan["readback"] = pending
+    return out[0], pending.saves

@@ -3,7 +3,8 @@
 The persistent BiGRU kernel (gru.hip) spreads each direction over 16 workgroups that exchange the
 hidden state through L2 with bounded spins; a workgroup that gives up on a peer ends the launch and
 sets the caller's status word (FX_STATUS_GRU_TIMEOUT).  Forcing a tiny spin bound must surface as
-FactmxNativeError at the step's single host read-back, and the next normal step must succeed.
+FactmxNativeError at the step's single host read-back -- resolved at the first read of the saves or
+at the end of the backward pass -- and the next normal step must succeed.
 """
 import pytest
 import torch
@@ -34,7 +35,13 @@ def test_gru_timeout_raises_at_readback(monkeypatch):
     labs = [torch.from_numpy(label).to(DEV)] * 2
     monkeypatch.setattr(fxf, "GRU_SPIN_MAX", 1)      # give up after two empty polls
     with pytest.raises(nx.FactmxNativeError, match="GRU"):
-        net(seqs, labs, compute_loss=True)
+        loss, saves = net(seqs, labs, compute_loss=True)
+        saves[0]["pred"]        # the step's read-back resolves here (or at the end of backward)
+    torch.cuda.synchronize()
+    monkeypatch.setattr(fxf, "GRU_SPIN_MAX", 1)
+    with pytest.raises(nx.FactmxNativeError, match="GRU"):
+        loss, _ = net(seqs, labs, compute_loss=True)
+        loss.backward()         # ... resolved by the autograd callback at the end of the backward pass
     torch.cuda.synchronize()
     monkeypatch.setattr(fxf, "GRU_SPIN_MAX", 0)
     loss, _ = net(seqs, labs, compute_loss=True)
