@@ -39,7 +39,7 @@ sys.path.insert(0, os.path.join(ROOT, "fact-clip_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-DOMINANT_KERNEL = "gemm_f32_wide8_kernel<1, 0>"   # rocprofv3 name: fx::(anonymous namespace)::gemm_f32_wide8_kernel<1, 0>
+DOMINANT_KERNEL = "gemm_f32_wide8_kernel<1, 0, 0>"   # rocprofv3 name: fx::(anonymous namespace)::gemm_f32_wide8_kernel<1, 0, 0>
 METRIC = "frames/sec FACT_CLIP fwd+bwd, T=4096 D=2048 Nact=32, at 1/2/4/8 GPUs"
 METRIC_BREAKFAST = "frames/sec FACT fwd+bwd, Breakfast dims T=512 D=2048 Nact=60 (BASELINE configs[0])"
 METRIC_SHIPPED = ("frames/sec FACT_CLIP fwd+bwd, havid_view0_lh_pt_holdout.yaml as shipped (ntoken 75, dropout 0.2, "
