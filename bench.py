@@ -489,7 +489,7 @@ def main():
                               for name, v in attn_prof.items()}
         for name, r in roofline_attention.items():
             if r is not None and default_shape:   # PMC bytes of the main kernel (the merge launch excluded)
-                r["traffic"] = traffic_from_profiles(f"tattn_{name}_kernel", f"r02_pmc_tattn_{name}.json")
+                r["traffic"] = traffic_from_profiles(f"tattn_{name}_kernel", f"r03_pmc_tattn_{name}.json")
         line = dict(metric=metric, value=round(value, 1), unit="frames/s", n_gpus=world, steps=args.steps,
                     warmup=args.warmup, ms_per_step=round(1e3 * elapsed / args.steps, 3), higher_is_better=True,
                     scaling="weak", vs_baseline=None, dtype="fp32", data="synthetic",

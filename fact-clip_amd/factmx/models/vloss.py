@@ -18,6 +18,7 @@ blocks.py:313-320, 369-382, 487-497 over loss.py:195-277) and the CLIP InfoNCE t
      The backward (fx_loss_terms_bwd) writes the gradient of every logit tensor in four launches.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -116,6 +117,7 @@ def _ptr_rows(t, row0, ld):
 
 
 _PENDING = []          # read-backs not resolved yet (resolved at the next forward at the latest)
+LAZY_READBACK = os.environ.get("FX_LAZY_READBACK", "1") != "0"   # 0: resolve inside the forward (A/B)
 
 
 class LazySave(dict):
@@ -576,4 +578,6 @@ def run(net, vb, compute_loss, early=None):
             saves[v]["loss"] = d
     pending = PendingReadback(ready, lambda: fxf.status_raise(int(st_h[0]), dev), fill, nvid)
     plan["readback"] = pending
+    if not LAZY_READBACK:
+        pending.resolve()
     return out[0], pending.saves
