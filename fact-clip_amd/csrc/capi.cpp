@@ -465,6 +465,7 @@ const Knobs& knobs() {
     if (const char* p = env("FX_X2Y_FUSED")) k.x2y_fused = p[0] != '0';
     if (const char* p = env("FX_SPLIT_VARIANT")) k.split_variant = std::atoi(p);
     if (const char* p = env("FX_MSTCN_TAIL")) k.mstcn_tail = p[0] != '0';
+    if (const char* p = env("FX_MSTCN_DW_HALVES")) k.mstcn_dw_halves = p[0] != '0';
   });
   return k;
 }
@@ -746,6 +747,55 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   if (defer) {
     float* dZall = ws + L.dzall;
     float* dHall = ws + L.dhall;   // dHall[i] = dH_{i+1} (gradient at layer i's output)
+    // the batched weight gradients of layers [base, base + nb) on the side stream
+    auto batched_dw = [&](int base, int nb) -> int {
+      if (nb <= 0) return FX_OK;
+      FX_TRY(fork(1));
+      {   // 1x1: dW_pw,i += dH_{i+1}^T z_i, db_pw,i += colsum(dH_{i+1})   (batched over layers)
+        fx_operand b = op_cols(saved + L.z + (long long)base * L.rowsF, F);
+        b.batch_stride = L.rowsF;
+        b.ones_col = F + 1;
+        fx_operand a = op_cols(dHall + (long long)base * L.rowsF, F);
+        a.batch_stride = L.rowsF;
+        fx_gemm_desc d = gemm_desc(F, F + 1, rows, a, b, g->w_pw[base], F);
+        d.batch = nb;
+        d.c_batch_stride = NL > 1 ? g->w_pw[1] - g->w_pw[0] : 0;
+        d.c_last_col = g->b_pw[base];
+        d.c_last_batch_stride = NL > 1 ? g->b_pw[1] - g->b_pw[0] : 0;
+        d.beta = 1.f;
+        d.split_k = std::max(pick_split(F, F + 1, rows, nb), defer_split_impl(rows));
+        d.workspace = ws + L.bsl;
+        WsBound wbb(ws + L.bsl, L.total_ws - L.bsl);
+        FX_TRY(launch_gemm(d, sd));
+      }
+      {   // dilated conv: dW_i += dZ_i^T taps(h_i) stored straight into (F, F, 3)   (batched over layers;
+          // ragged videos: one such launch per video, accumulating)
+        WsBound wbb(ws + L.bsl, L.total_ws - L.bsl);
+        FX_TRY(per_video(q, [&](int r0, int nr, const Seqs& qv) -> int {
+          fx_operand b = conv_operand(saved + L.h + (long long)base * L.rowsF + (long long)r0 * F, F, F,
+                                      layer_dilation(p, base), 1, qv, true);
+          b.batch_stride = L.rowsF;
+          fx_operand a = op_cols(dZall + (long long)base * L.rowsF + (long long)r0 * F, F);
+          a.batch_stride = L.rowsF;
+          fx_gemm_desc d = gemm_desc(F, 3 * F, nr, a, b, g->w_dil[base], 3 * F);
+          d.batch = nb;
+          d.c_batch_stride = NL > 1 ? g->w_dil[1] - g->w_dil[0] : 0;
+          d.b_dil_growth = p->dil_factor > 0 ? p->dil_factor : 2;
+          d.c_tap_cin = F;
+          d.beta = 1.f;
+          d.split_k = defer_split_impl(nr);
+          d.workspace = ws + L.bsl;
+          return launch_gemm(d, sd);
+        }));
+        FX_TRY(launch_colsum_batched(dZall + (long long)base * L.rowsF, F, L.rowsF, rows, F, nb, g->b_dil[base],
+                                     NL > 1 ? g->b_dil[1] - g->b_dil[0] : 0, 1, ws + L.csb, sd));
+      }
+      return FX_OK;
+    };
+    // FX_MSTCN_DW_HALVES=1: the layers above `half` get their weight gradients as soon as the chain has
+    // passed them (overlapping the chain's remaining layers), the rest after the chain.  Measured no
+    // better than one batched launch after the chain (the early half slows the chain it overlaps): off
+    const int half = knobs().mstcn_dw_halves ? NL / 2 : 0;
     for (int i = NL - 1; i >= 0; --i) {
       const float* zi = saved + L.z + i * L.rowsF;
       const float* gU = dHall + i * L.rowsF;
@@ -759,47 +809,10 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
       prof_begin(0, s);
       FX_TRY(launch_gemm(d, s));
       prof_end(0, s, 2.0 * rows * F * 3.0 * F, 4.0 * (3.0 * rows * F + 3.0 * F * F));
+      if (half > 0 && i == half) FX_TRY(batched_dw(half, NL - half));
     }
     dH = Hb[0];
-    FX_TRY(fork(1));
-    {   // 1x1: dW_pw,i += dH_{i+1}^T z_i, db_pw,i += colsum(dH_{i+1})   (batched over layers)
-      fx_operand b = op_cols(saved + L.z, F);
-      b.batch_stride = L.rowsF;
-      b.ones_col = F + 1;
-      fx_operand a = op_cols(dHall, F);
-      a.batch_stride = L.rowsF;
-      fx_gemm_desc d = gemm_desc(F, F + 1, rows, a, b, g->w_pw[0], F);
-      d.batch = NL;
-      d.c_batch_stride = NL > 1 ? g->w_pw[1] - g->w_pw[0] : 0;
-      d.c_last_col = g->b_pw[0];
-      d.c_last_batch_stride = NL > 1 ? g->b_pw[1] - g->b_pw[0] : 0;
-      d.beta = 1.f;
-      d.split_k = std::max(pick_split(F, F + 1, rows, NL), defer_split_impl(rows));
-      d.workspace = ws + L.bsl;
-      WsBound wbb(ws + L.bsl, L.total_ws - L.bsl);
-      FX_TRY(launch_gemm(d, sd));
-    }
-    {   // dilated conv: dW_i += dZ_i^T taps(h_i) stored straight into (F, F, 3)   (batched over layers;
-        // ragged videos: one such launch per video, accumulating)
-      WsBound wbb(ws + L.bsl, L.total_ws - L.bsl);
-      FX_TRY(per_video(q, [&](int r0, int nr, const Seqs& qv) -> int {
-        fx_operand b = conv_operand(saved + L.h + (long long)r0 * F, F, F, layer_dilation(p, 0), 1, qv, true);
-        b.batch_stride = L.rowsF;
-        fx_operand a = op_cols(dZall + (long long)r0 * F, F);
-        a.batch_stride = L.rowsF;
-        fx_gemm_desc d = gemm_desc(F, 3 * F, nr, a, b, g->w_dil[0], 3 * F);
-        d.batch = NL;
-        d.c_batch_stride = NL > 1 ? g->w_dil[1] - g->w_dil[0] : 0;
-        d.b_dil_growth = p->dil_factor > 0 ? p->dil_factor : 2;
-        d.c_tap_cin = F;
-        d.beta = 1.f;
-        d.split_k = defer_split_impl(nr);
-        d.workspace = ws + L.bsl;
-        return launch_gemm(d, sd);
-      }));
-      FX_TRY(launch_colsum_batched(dZall, F, L.rowsF, rows, F, NL, g->b_dil[0],
-                                   NL > 1 ? g->b_dil[1] - g->b_dil[0] : 0, 1, ws + L.csb, sd));
-    }
+    FX_TRY(batched_dw(0, half > 0 ? half : NL));
   }
   for (int i = NL - 1; !fchain && !defer && i >= 0; --i) {
     const int step = NL - 1 - i;
