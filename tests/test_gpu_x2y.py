@@ -28,8 +28,10 @@ def _params(xdim, ydim, outdim, seed):
 
 
 @pytest.mark.parametrize("direction,nq,Ts", [("a2f", 32, (700, 413)), ("a2f", 40, (300, 257)),
-                                             ("a2f", 75, (300, 200)), ("f2a", 32, (700, 413)),
-                                             ("a2f", 32, (1,))])
+                                             ("a2f", 64, (129, 64)), ("a2f", 75, (300, 200)),
+                                             ("f2a", 32, (700, 413)), ("f2a", 40, (300, 257, 65)),
+                                             ("f2a", 64, (64, 1)), ("f2a", 75, (200, 90)),
+                                             ("a2f", 32, (1,)), ("f2a", 7, (3000,))])
 def test_x2y_vs_oracle(direction, nq, Ts):
     g = torch.Generator().manual_seed(7)
     nv = len(Ts)
