@@ -13,6 +13,7 @@ kernel is launched.  Non-leaf weights get a fresh buffer that is returned to
 autograd as usual.
 """
 import ctypes
+import os
 
 import torch
 
@@ -577,7 +578,7 @@ def x2y(mod, X, Y, Xpos, Ypos, rows=None):
 
 # fx_mstcn_params.fused_layers: the opt-in one-kernel MS-TCN layer (slower than the two tuned GEMMs at
 # the benchmark shape; kept for A/B and its own tests)
-MSTCN_FUSED_LAYERS = False
+MSTCN_FUSED_LAYERS = os.environ.get("FX_MSTCN_FUSED_LAYERS", "0") == "1"   # A/B knob
 
 
 def _ptr_array(ts):
