@@ -466,6 +466,7 @@ const Knobs& knobs() {
     if (const char* p = env("FX_SPLIT_VARIANT")) k.split_variant = std::atoi(p);
     if (const char* p = env("FX_MSTCN_TAIL")) k.mstcn_tail = p[0] != '0';
     if (const char* p = env("FX_MSTCN_DW_HALVES")) k.mstcn_dw_halves = p[0] != '0';
+    if (const char* p = env("FX_DIRECT_CPW")) k.direct_cpw = std::max(1, std::min(8, std::atoi(p)));
   });
   return k;
 }

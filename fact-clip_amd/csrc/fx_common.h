@@ -134,6 +134,7 @@ struct Knobs {
   int side_maxwg = 0;
   bool x2y_fused = true;    // FX_X2Y_FUSED=0: the X2Y attention core as grouped GEMM + softmax launches
   int split_variant = 0;    // FX_SPLIT_VARIANT=1: the LDS-image split kernel for every FX_PREC_F32S GEMM
+  int direct_cpw = 1;       // FX_DIRECT_CPW: 32-deep k chunks per wave of the direct (small) GEMM kernel (1 vs 2: direct-kernel time 2.74 -> 2.61 ms/step)
   bool mstcn_dw_halves = false; // FX_MSTCN_DW_HALVES=1: upper half of the batched MS-TCN dW mid-chain (A/B: no gain)
   bool mstcn_tail = false;  // FX_MSTCN_TAIL=1: the input block's MS-TCN keeps per-layer side dW (A/B: even)
 };

@@ -1999,10 +1999,13 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
   if (direct) {
     const int nch = cdiv(d.K, DCH);
     const long long t32 = (long long)cdiv(d.M, 32) * cdiv(d.N, 32) * d.batch;
-    const int nw = std::min(DMAXW, std::max(1, nch / 2));
+    // k chunks per wave (FX_DIRECT_CPW, default 1: up to 8 waves per tile, one 32-deep chunk each; 2 = the
+    // double-buffered loop over two chunks per wave)
+    const int cpw = knobs().direct_cpw;
+    const int nw = std::min(DMAXW, std::max(1, nch / cpw));
     int split = 1;
     if (cap > 1) {
-      const long long want = std::min<long long>(nch / (2 * nw), cdiv(2048, t32 * nw));
+      const long long want = std::min<long long>(nch / (cpw * nw), cdiv(2048, t32 * nw));
       split = (int)std::max<long long>(1, std::min<long long>(cap, want));
     }
     g.kt_per_split = nch > 0 ? cdiv(nch, split) : 0;
