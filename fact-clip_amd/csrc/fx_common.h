@@ -129,7 +129,7 @@ struct Knobs {
   bool gemm_group = true;
   bool side_stream = true;
   int side_priority = 0;    // -1 low, 0 normal, 1 high
-  int defer_split = 8;
+  int defer_split = 16;     // FX_DEFER_SPLIT: split-K of the deferred (side-stream) weight-gradient GEMMs (16 vs 8: 15.78 vs 15.95 ms median of 6 pairs)
   bool mstcn_defer = true;
   int side_maxwg = 0;
   bool x2y_fused = true;    // FX_X2Y_FUSED=0: the X2Y attention core as grouped GEMM + softmax launches
