@@ -427,20 +427,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
 
-    # BASELINE configs[1]: the same fixed-weight step with the frame-level GEMMs in bf16 arithmetic
-    # (FX_PREC_BF16, fp32 accumulation / storage), its frame-logit deviation from the fp32 path on the
-    # same weights and videos, and its TDU segment counts (N=1 only; the headline stays fp32)
-    bf16 = other = None
-    if world == 1 and not args.no_bf16:
-        from factmx import functional as fxf
-        bf16 = bf16_mode(net, step, sum(Ts), args.steps, args.warmup, fxf)
-        # the other fp32 arithmetic (f32 MFMA when the headline runs the split, and vice versa)
-        other = bf16_mode(net, step, sum(Ts), args.steps, args.warmup, fxf,
-                          "fp32" if headline_prec == "fp32s" else "fp32s")
-
-    # the reference train step (clip_grad_norm_ + Adam), timed after the fixed-weight steps
+    # the reference train step (clip_grad_norm_ + Adam), timed right after the fixed-weight steps (same
+    # device state); the weights are restored afterwards, so the precision modes below compare
+    # arithmetic on the headline's weights
     adam = None
     if adam_steps > 0:
+        w0 = [p.detach().clone() for p in net.parameters()]
         opt = FusedAdam(net.parameters(), lr=cfg.lr, max_grad_norm=cfg.clip_grad_norm, grad_flat=dp.flat)
         step()
         opt.step()
@@ -463,6 +455,21 @@ def main():
                     ms_per_step=round(1e3 * ea / adam_steps, 3), tdu_segments_after=video_segments(net),
                     note="zero_grad + fwd + loss + bwd (+all-reduce) + clip_grad_norm_(10) + Adam(lr 1e-4); the "
                          "updates move the weights, so S drifts from the fixed-weight value")
+        with torch.no_grad():
+            for p_, w in zip(net.parameters(), w0):
+                p_.copy_(w)
+        del opt, w0
+
+    # BASELINE configs[1]: the same fixed-weight step with the frame-level GEMMs in bf16 arithmetic
+    # (FX_PREC_BF16, fp32 accumulation / storage), its frame-logit deviation from the fp32 path on the
+    # same weights and videos, and its TDU segment counts (N=1 only; the headline stays fp32)
+    bf16 = other = None
+    if world == 1 and not args.no_bf16:
+        from factmx import functional as fxf
+        bf16 = bf16_mode(net, step, sum(Ts), args.steps, args.warmup, fxf)
+        # the other fp32 arithmetic (f32 MFMA when the headline runs the split, and vice versa)
+        other = bf16_mode(net, step, sum(Ts), args.steps, args.warmup, fxf,
+                          "fp32" if headline_prec == "fp32s" else "fp32s")
 
     frames = world * sum(Ts) * args.steps
     value = frames / elapsed
