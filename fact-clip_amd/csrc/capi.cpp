@@ -1645,31 +1645,22 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
   const bool fused = knobs().x2y_fused && x2y_a2f_fusable(V.n, V.x.data(), Hd) && (cw & 3) == 0 &&
                      ((reinterpret_cast<uintptr_t>(dcat + ydim)) & 15) == 0;
   if (fused) {
-    for (int v0 = 0; v0 < V.n; v0 += GMAX_GROUP) {
-      fx_gemm_desc g1[GMAX_GROUP];
-      int n1 = 0;
-      for (int v = v0; v < std::min(V.n, v0 + GMAX_GROUP); ++v) {
-        const int nx = V.x[v + 1] - V.x[v], ny = V.y[v + 1] - V.y[v];
-        if (nx == 0 || ny == 0) continue;
-        const long long xr = (long long)V.x[v] * Hd;
-        fx_gemm_desc d = gemm_desc(nx, Hd, ny, op_cols(attn + V.a[v], nx), op_cols(dcat + (long long)V.y[v] * cw + ydim, cw),
-                                   dxv + xr, Hd);
-        d.split_k = pick_split(nx, Hd, ny);
-        d.workspace = spl;
-        g1[n1++] = d;
-      }
-      FX_TRY(launch_gemm_group(g1, n1, s));
-    }
     FX_TRY(launch_x2y_a2f_bwd(dcat + ydim, cw, xv, xk, attn, dattn, dlogit, Hd, scale, V.n, V.y.data(), V.x.data(),
                               V.a.data(), dL, dyq, s));
-    for (int v0 = 0; v0 < V.n; v0 += GMAX_GROUP) {
+    // dxv = attn^T dfeat and dxk = scale dlogit^T yq of up to two videos in one grouped launch
+    for (int v0 = 0; v0 < V.n; v0 += GMAX_GROUP / 2) {
       fx_gemm_desc g2[GMAX_GROUP];
       int n2 = 0;
-      for (int v = v0; v < std::min(V.n, v0 + GMAX_GROUP); ++v) {
+      for (int v = v0; v < std::min(V.n, v0 + GMAX_GROUP / 2); ++v) {
         const int nx = V.x[v + 1] - V.x[v], ny = V.y[v + 1] - V.y[v];
         if (nx == 0 || ny == 0) continue;
         const long long xr = (long long)V.x[v] * Hd, yr = (long long)V.y[v] * Hd;
-        fx_gemm_desc d = gemm_desc(nx, Hd, ny, op_cols(dL + V.a[v], nx), op_cols(yq + yr, Hd), dxk + xr, Hd);
+        fx_gemm_desc d = gemm_desc(nx, Hd, ny, op_cols(attn + V.a[v], nx),
+                                   op_cols(dcat + (long long)V.y[v] * cw + ydim, cw), dxv + xr, Hd);
+        d.split_k = pick_split(nx, Hd, ny);
+        d.workspace = spl;
+        g2[n2++] = d;
+        d = gemm_desc(nx, Hd, ny, op_cols(dL + V.a[v], nx), op_cols(yq + yr, Hd), dxk + xr, Hd);
         d.alpha = scale;
         d.split_k = pick_split(nx, Hd, ny);
         d.workspace = spl;
