@@ -6,13 +6,14 @@
 // reduce) per video.  Here ONE launch covers every video and head, flash-decoding style:
 //   grid = (T-chunk c, head h, video v); a workgroup stages q_h (Q x hd), K_c and V_c (Tc x hd) in
 //   LDS, computes S = q K_c^T (MFMA 32x32x2 f32), its row max m_c / sum l_c, and O_c = exp(S - m_c) V_c;
-//   the partials go to a workspace and the LAST workgroup of each (video, head) to arrive (arrival
-//   counter, agent-scope release/acquire) merges them in chunk order -- deterministic -- into
-//   o = sum_c e^(m_c - M) O_c / L and lse = M + log L.  Only lse (Q floats per head) is kept for
-//   backward, not the probabilities.
+//   the partials go to a workspace and a second, small launch (tattn_merge_kernel, one workgroup per
+//   (video, head)) merges them in chunk order -- deterministic -- into o = sum_c e^(m_c - M) O_c / L
+//   and lse = M + log L.  (An in-launch last-arriver merge behind an arrival counter measured slower:
+//   the agent-scope release / acquire hand-off costs more than the second launch)
+//   Only lse (Q floats per head) is kept for backward, not the probabilities.
 // Backward recomputes P = exp(S - lse) per chunk: dV_c = P^T dO, dP = dO V_c^T, dS = P (dP - D)
 // with D = rowsum(dO o), dK_c = scale dS^T q (K/V rows of a chunk belong to ONE workgroup: written,
-// not accumulated), and dq = scale sum_c dS_c K_c through the same ordered last-arriver merge.
+// not accumulated), and dq = scale sum_c dS_c K_c through the same ordered merge launch.
 // HBM bytes per frame and layer: K and V rows read once (2 hd h x 4 B per frame forward; backward
 // also writes dK, dV).
 #include <algorithm>
