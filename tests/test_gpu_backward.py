@@ -209,3 +209,40 @@ def test_ntoken75_T4096_train_and_eval_vs_oracle(monkeypatch):
                     compute_loss=False)
     torch.cuda.synchronize()
     _check_forward(net, spec, outs, saves, text)
+
+
+def test_shipped_yaml_training_step_full_shape():
+    """The reference's havid_view0_lh_pt_holdout.yaml as shipped (Bi.dropout 0.2, FACT.cmr 0.3, time mask
+    on, ntoken 75) at full shape on a ragged lockstep batch (T = 4096 + 2900): the training step runs the
+    fused paths (lockstep, fused decoder with dropout at every site), its loss and every gradient are
+    finite, and the same torch seed reproduces the step bit for bit (counter-based dropout masks, channel
+    masking and time mask drawn from the seeded generators: torch's and Python's).  With dropout, cmr and the time mask off the
+    same shape is held to the oracle by test_ntoken75_T4096_train_and_eval_vs_oracle / the ragged test."""
+    import bench
+    from factmx.models import blocks as blocks_mod
+    cfg = bench.make_cfg_shipped()
+    D, C = 2048, 75
+    net, _ = bench.build_model(cfg, D, C, device=DEV, seed=0)
+    net.train()
+    vids = [bench.make_video(T, D, C, cfg, seed=s) for T, s in ((4096, 1), (2900, 5))]
+    seqs = [torch.from_numpy(f).to(DEV) for f, _ in vids]
+    assert blocks_mod._batchable(net, seqs)
+
+    def run():
+        import random
+        random.seed(123)            # the time mask draws its spans from Python's random (basic.py:35-47)
+        np.random.seed(123)
+        torch.manual_seed(123)
+        torch.cuda.manual_seed(123)
+        loss, saves = _gpu_step(net, vids)
+        grads = [p.grad.detach().clone() for p in net.parameters()]
+        return loss, grads, saves
+
+    l1, g1, s1 = run()
+    l2, g2, s2 = run()
+    assert np.isfinite(l1), l1
+    assert all(torch.isfinite(g).all() for g in g1)
+    assert l1 == l2, (l1, l2)
+    assert all(torch.equal(a, b) for a, b in zip(g1, g2))
+    for a, b in zip(s1, s2):
+        np.testing.assert_array_equal(a["pred"], b["pred"])
