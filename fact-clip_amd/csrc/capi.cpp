@@ -467,6 +467,7 @@ const Knobs& knobs() {
     if (const char* p = env("FX_MSTCN_TAIL")) k.mstcn_tail = p[0] != '0';
     if (const char* p = env("FX_MSTCN_DW_HALVES")) k.mstcn_dw_halves = p[0] != '0';
     if (const char* p = env("FX_DIRECT_CPW")) k.direct_cpw = std::max(1, std::min(8, std::atoi(p)));
+    if (const char* p = env("FX_X2Y_F2A_BWD")) k.x2y_f2a_bwd = p[0] != '0';
   });
   return k;
 }
@@ -1668,6 +1669,13 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
       }
       FX_TRY(launch_gemm_group(g2, n2, s));
     }
+  } else if (knobs().x2y_fused && knobs().x2y_f2a_bwd && x2y_f2a_fusable(V.n, V.x.data(), V.y.data(), Hd) &&
+             (cw & 3) == 0 && ((reinterpret_cast<uintptr_t>(dcat + ydim)) & 15) == 0) {
+    // the f2a map: dP / dxv, then dlogit / dxk / dyq partials per 64-key chunk, then the ordered dyq merge
+    float* f2a_ws = workspace + x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, V) + (long long)Ny * cw +
+                    x2y_side_ws(Nx, xdim, Ny, ydim, Hd, outdim);
+    FX_TRY(launch_x2y_f2a_bwd(dcat + ydim, cw, xv, xk, yq, attn, dattn, dlogit, Hd, scale, V.n, V.y.data(), V.x.data(),
+                              V.a.data(), dL, dxv, dxk, dyq, f2a_ws, s));
   } else
   // per video: dP = dfeat . xv^T (+ dattn), dxv = attn^T . dfeat  (independent: one grouped launch
   // for up to two videos), softmax backward, then dyq = dlogit . xk, dxk = dlogit^T . yq (grouped)

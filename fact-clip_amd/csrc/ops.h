@@ -60,6 +60,11 @@ long long x2y_f2a_ws_floats(int nvid, const int* xoff, int Hd);
 int launch_x2y_f2a_fwd(const float* yq, const float* xk, const float* xv, int Hd, float scale, int nvid,
                        const int* yoff, const int* xoff, const long long* aoff, float* logit, float* attn,
                        float* feat, float* ws, hipStream_t s);
+// f2a backward (dlogit, dxv, dxk, dyq of every video in three launches); ws as the forward's
+int launch_x2y_f2a_bwd(const float* dfeat, long long ldf, const float* xv, const float* xk, const float* yq,
+                       const float* attn, const float* dattn, const float* dlogit_in, int Hd, float scale, int nvid,
+                       const int* yoff, const int* xoff, const long long* aoff, float* dlogit, float* dxv, float* dxk,
+                       float* dyq, float* ws, hipStream_t s);
 // backward, input-gradient side: dP = dfeat . xv^T (+ dattn), dlogit = attn (dP - rowsum(attn dP)) (+ dlogit_in),
 // dyq = scale dlogit . xk;  dfeat rows ld ldf (16-B aligned)
 int launch_x2y_a2f_bwd(const float* dfeat, long long ldf, const float* xv, const float* xk, const float* attn,

@@ -456,6 +456,242 @@ __global__ __launch_bounds__(XT) void x2y_f2a_merge_kernel(F2aArgs a) {
   for (int x = tid; x < nx; x += XT) a.attn[o + x] = __expf(a.logit[o + x] - M) * invL;
 }
 
+// ---------------------------------------------------------------- long key side, backward
+// Input-gradient side of the f2a core (frames = keys, tokens = queries), per 64-key chunk:
+//   pass 1: dP = dfeat . xv_c^T (+ dattn) -> dL (temporarily), the chunk's share of rowdot = sum_x attn dP,
+//           dxv_c = attn_c^T . dfeat (complete: a key row belongs to one chunk);
+//   pass 2: rowdot = sum of the video's chunk shares (fixed order), dlogit = attn (dP - rowdot) (+ direct
+//           dlogit) -> dL, dxk_c = scale dlogit_c^T . yq (complete), dyq partial = scale dlogit_c . xk_c;
+//   merge:  dyq = sum_c partial (chunk order).
+struct F2aBwdArgs {
+  const float* dfeat;   // (Ny, Hd) rows, ld ldf
+  long long ldf;
+  const float* attn;    // per video (ny_v, nx_v) at aoff[v]
+  const float* dattn;   // nullable, same layout
+  const float* dl_in;   // nullable, same layout
+  const float* xv;      // (Nx, Hd)
+  const float* xk;
+  const float* yq;      // (Ny, Hd)
+  float* dL;            // per video (ny_v, nx_v) at aoff[v]
+  float* dxv;           // (Nx, Hd)
+  float* dxk;
+  float* dyq;           // (Ny, Hd)
+  float* part;          // (chunks, FMAXQ, Hd)
+  float* stats;         // (chunks, FMAXQ, 2)
+  int Hd, nvid;
+  float scale;
+  int yoff[FX_X2Y_MAXV + 1], xoff[FX_X2Y_MAXV + 1];
+  long long aoff[FX_X2Y_MAXV + 1];
+  int ch_off[FX_X2Y_MAXV + 1];
+};
+
+__device__ __forceinline__ void f2ab_video(const F2aBwdArgs& a, int v, int& y0, int& ny, int& x0, int& nx, long long& ao,
+                                           int& c0) {
+#pragma unroll
+  for (int i = 0; i < FX_X2Y_MAXV; ++i)
+    if (i == v) {
+      y0 = a.yoff[i];
+      ny = a.yoff[i + 1] - a.yoff[i];
+      x0 = a.xoff[i];
+      nx = a.xoff[i + 1] - a.xoff[i];
+      ao = a.aoff[i];
+      c0 = a.ch_off[i];
+    }
+}
+
+// out[x][n] = mul sum_y L[y][x] Bm[y][n] for the chunk's keys x (rows of out), y < ny (K), n < Hd:
+// (2 key tiles x Hd/32 column tiles) over the 8 waves, A = L^T from LDS, B = Bm columns (global)
+__device__ __forceinline__ void keys_out(const float (*L)[FC + 1], const float* Bm, long long ldb, int ny, int keys,
+                                         int Hd, float mul, float* out, int w, int li, int lh) {
+  const int nct = Hd >> 5;
+  for (int t = w; t < 2 * nct; t += 8) {
+    const int rt = t / nct, n0 = (t - rt * nct) * 32;
+    f32x16 f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) f[i] = 0.f;
+    for (int k0 = 0; k0 < ny; k0 += 32) {
+      float bv[16];
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) {
+        const int y = k0 + 16 * lh + s2;
+        const float x = Bm[(long long)min(y, ny - 1) * ldb + n0 + li];
+        bv[s2] = y < ny ? x : 0.f;
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) {
+        const int y = k0 + 16 * lh + s2;
+        f = __builtin_amdgcn_mfma_f32_32x32x2f32(y < FMAXQ ? L[min(y, FMAXQ - 1)][rt * 32 + li] : 0.f, bv[s2], f, 0, 0,
+                                                 0);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      if (row < keys) out[(long long)row * Hd + n0 + li] = mul * f[r];
+    }
+  }
+}
+
+template <int PASS>
+__global__ __launch_bounds__(XT) void x2y_f2a_bwd_kernel(F2aBwdArgs a) {
+  __shared__ float red[8][16][64];
+  __shared__ float S[FMAXQ][FC + 1];    // dP, then dlogit (rows = queries, cols = the chunk's keys)
+  __shared__ float Pa[FMAXQ][FC + 1];   // attn of the chunk
+  __shared__ float rdot[FMAXQ];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 31, lh = lane >> 5;
+  int v = 0;
+#pragma unroll
+  for (int i = 1; i < FX_X2Y_MAXV; ++i)
+    if (i < a.nvid && (int)blockIdx.x >= a.ch_off[i]) v = i;
+  int y0 = 0, ny = 0, x0 = 0, nx = 0, c0 = 0;
+  long long ao = 0;
+  f2ab_video(a, v, y0, ny, x0, nx, ao, c0);
+  const int chunk = blockIdx.x;
+  const int k0c = ((int)blockIdx.x - c0) * FC;
+  const int keys = min(FC, nx - k0c);
+  const int Hd = a.Hd;
+  // the chunk's attn (and in pass 2 its dP) into LDS, zero outside (queries < ny, keys < keys)
+  for (int e = tid; e < FMAXQ * FC; e += XT) {
+    const int y = e / FC, x = e - y * FC;
+    const bool ok = y < ny && x < keys;
+    const long long o = ao + (long long)y * nx + k0c + x;
+    Pa[y][x] = ok ? a.attn[o] : 0.f;
+    if (PASS == 2) S[y][x] = ok ? a.dL[o] : 0.f;
+  }
+  if (PASS == 2 && tid < FMAXQ) {
+    const int nch = (nx + FC - 1) / FC;
+    float sum = 0.f;
+    if (tid < ny)
+      for (int c = 0; c < nch; ++c) sum += a.stats[((long long)(c0 + c) * FMAXQ + tid) * 2];
+    rdot[tid] = sum;
+  }
+  __syncthreads();
+
+  if (PASS == 1) {
+    // ---- dP = dfeat . xv_c^T (+ dattn): blocks (query block rb, key block cb), waves split Hd ----
+    const int nrb = ny > 32 ? 2 : 1, nblk = 2 * nrb, wpb = 8 / nblk;
+    const int blk = w % nblk, kpart = w / nblk, rb = blk >> 1, cb = blk & 1;
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    {
+      const int q = rb * 32 + li, key = k0c + cb * 32 + li;
+      const bool aok = q < ny, bok = cb * 32 + li < keys;
+      const float* pa = a.dfeat + (long long)(y0 + min(q, ny - 1)) * a.ldf;
+      const float* pb = a.xv + (long long)(x0 + min(key, nx - 1)) * Hd;
+      const int kw = Hd / wpb;
+      for (int k0 = kpart * kw; k0 < (kpart + 1) * kw; k0 += 32) {
+        const int kk = k0 + 16 * lh;
+        float av[16], bv[16];
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd) {
+          const float4 ta = ld4(pa + kk + 4 * qd), tb = ld4(pb + kk + 4 * qd);
+          av[4 * qd] = aok ? ta.x : 0.f;
+          av[4 * qd + 1] = aok ? ta.y : 0.f;
+          av[4 * qd + 2] = aok ? ta.z : 0.f;
+          av[4 * qd + 3] = aok ? ta.w : 0.f;
+          bv[4 * qd] = bok ? tb.x : 0.f;
+          bv[4 * qd + 1] = bok ? tb.y : 0.f;
+          bv[4 * qd + 2] = bok ? tb.z : 0.f;
+          bv[4 * qd + 3] = bok ? tb.w : 0.f;
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s2], bv[s2], acc, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[w][r][lane] = acc[r];
+    __syncthreads();
+    for (int e = tid; e < nblk * 1024; e += XT) {
+      const int b = e >> 10, r = (e >> 6) & 15, l = e & 63;
+      float sum = 0.f;
+      for (int p = 0; p < wpb; ++p) sum += red[p * nblk + b][r][l];
+      const int row = (b >> 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), col = (b & 1) * 32 + (l & 31);
+      if (a.dattn && row < ny && col < keys) sum += a.dattn[ao + (long long)row * nx + k0c + col];
+      S[row][col] = sum;
+    }
+    __syncthreads();
+    // dP out (pass 2 reads it back), the chunk's share of rowdot
+    {
+      const int row = tid >> 3, c8 = tid & 7;
+      float part = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int col = c8 + 8 * j;
+        if (row < ny && col < keys) {
+          a.dL[ao + (long long)row * nx + k0c + col] = S[row][col];
+          part += Pa[row][col] * S[row][col];
+        }
+      }
+#pragma unroll
+      for (int o = 4; o >= 1; o >>= 1) part += __shfl_xor(part, o, 8);
+      if (c8 == 0 && row < ny) a.stats[((long long)chunk * FMAXQ + row) * 2] = part;
+    }
+    // dxv_c = attn_c^T . dfeat
+    keys_out(Pa, a.dfeat + (long long)y0 * a.ldf, a.ldf, ny, keys, Hd, 1.f, a.dxv + (long long)(x0 + k0c) * Hd, w, li,
+             lh);
+  } else {
+    // ---- dlogit = attn (dP - rowdot) (+ direct) -> dL and LDS ----
+    for (int e = tid; e < FMAXQ * FC; e += XT) {
+      const int y = e / FC, x = e - y * FC;
+      float d = 0.f;
+      if (y < ny && x < keys) {
+        const long long o = ao + (long long)y * nx + k0c + x;
+        d = Pa[y][x] * (S[y][x] - rdot[y]);
+        if (a.dl_in) d += a.dl_in[o];
+        a.dL[o] = d;
+      }
+      S[y][x] = d;   // (read and rewritten by the same thread)
+    }
+    __syncthreads();
+    // dxk_c = scale dlogit_c^T . yq
+    keys_out(S, a.yq + (long long)y0 * Hd, Hd, ny, keys, Hd, a.scale, a.dxk + (long long)(x0 + k0c) * Hd, w, li, lh);
+    // partial dyq_c = scale dlogit_c . xk_c: (query blocks x Hd/32) tiles, K = the chunk's keys
+    const int nrb = ny > 32 ? 2 : 1;
+    const int nct = Hd >> 5;
+    for (int t = w; t < nrb * nct; t += 8) {
+      const int tr = t / nct, n0 = (t - tr * nct) * 32;
+      f32x16 f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) f[i] = 0.f;
+#pragma unroll
+      for (int kc = 0; kc < FC; kc += 32) {
+        float bv[16];
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) {
+          const int key = kc + 16 * lh + s2;
+          const float x = a.xk[(long long)(x0 + min(k0c + key, nx - 1)) * Hd + n0 + li];
+          bv[s2] = key < keys ? x : 0.f;
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2)
+          f = __builtin_amdgcn_mfma_f32_32x32x2f32(S[tr * 32 + li][kc + 16 * lh + s2], bv[s2], f, 0, 0, 0);
+      }
+      float* dst = a.part + (long long)chunk * FMAXQ * Hd;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = tr * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row < ny) dst[(long long)row * Hd + n0 + li] = a.scale * f[r];
+      }
+    }
+  }
+}
+
+// dyq = sum of the chunk partials in chunk order, one workgroup per (query row, video)
+__global__ __launch_bounds__(XT) void x2y_f2a_bwd_merge_kernel(F2aBwdArgs a) {
+  const int v = blockIdx.y, row = blockIdx.x;
+  int y0 = 0, ny = 0, x0 = 0, nx = 0, c0 = 0;
+  long long ao = 0;
+  f2ab_video(a, v, y0, ny, x0, nx, ao, c0);
+  if (row >= ny) return;
+  const int nch = (nx + FC - 1) / FC;
+  for (int n = threadIdx.x; n < a.Hd; n += XT) {
+    float acc = 0.f;
+    for (int c = 0; c < nch; ++c) acc += a.part[((long long)(c0 + c) * FMAXQ + row) * a.Hd + n];
+    a.dyq[(long long)(y0 + row) * a.Hd + n] = acc;
+  }
+}
+
 }  // namespace
 
 bool x2y_a2f_fusable(int nvid, const int* xoff, int Hd) {
@@ -555,6 +791,50 @@ int launch_x2y_f2a_fwd(const float* yq, const float* xk, const float* xv, int Hd
   if (nch == 0 || maxq == 0) return FX_OK;
   hipLaunchKernelGGL(x2y_f2a_chunk_kernel, dim3(nch), dim3(XT), 0, s, a);
   hipLaunchKernelGGL(x2y_f2a_merge_kernel, dim3(maxq, nvid), dim3(XT), 0, s, a);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+int launch_x2y_f2a_bwd(const float* dfeat, long long ldf, const float* xv, const float* xk, const float* yq,
+                       const float* attn, const float* dattn, const float* dlogit_in, int Hd, float scale, int nvid,
+                       const int* yoff, const int* xoff, const long long* aoff, float* dlogit, float* dxv, float* dxk,
+                       float* dyq, float* ws, hipStream_t s) {
+  FX_REQUIRE(x2y_f2a_fusable(nvid, xoff, yoff, Hd), "x2y f2a core: <= 64 queries per video, Hd % 256 == 0");
+  FX_REQUIRE(ldf % 4 == 0 && (reinterpret_cast<uintptr_t>(dfeat) & 15) == 0, "x2y f2a bwd: dfeat rows must be 16-B aligned");
+  F2aBwdArgs a{};
+  a.dfeat = dfeat;
+  a.ldf = ldf;
+  a.attn = attn;
+  a.dattn = dattn;
+  a.dl_in = dlogit_in;
+  a.xv = xv;
+  a.xk = xk;
+  a.yq = yq;
+  a.dL = dlogit;
+  a.dxv = dxv;
+  a.dxk = dxk;
+  a.dyq = dyq;
+  a.Hd = Hd;
+  a.nvid = nvid;
+  a.scale = scale;
+  int nch = 0, maxq = 0;
+  for (int v = 0; v <= nvid; ++v) {
+    a.yoff[v] = yoff[v];
+    a.xoff[v] = xoff[v];
+    a.aoff[v] = aoff[v];
+    a.ch_off[v] = nch;
+    if (v < nvid) {
+      nch += (xoff[v + 1] - xoff[v] + FC - 1) / FC;
+      maxq = std::max(maxq, yoff[v + 1] - yoff[v]);
+    }
+  }
+  for (int v = nvid + 1; v <= FX_X2Y_MAXV; ++v) a.ch_off[v] = nch;
+  a.part = ws;
+  a.stats = ws + (long long)nch * FMAXQ * Hd;
+  if (nch == 0 || maxq == 0) return FX_OK;
+  hipLaunchKernelGGL(x2y_f2a_bwd_kernel<1>, dim3(nch), dim3(XT), 0, s, a);
+  hipLaunchKernelGGL(x2y_f2a_bwd_kernel<2>, dim3(nch), dim3(XT), 0, s, a);
+  hipLaunchKernelGGL(x2y_f2a_bwd_merge_kernel, dim3(maxq, nvid), dim3(XT), 0, s, a);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }
