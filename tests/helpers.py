@@ -80,7 +80,7 @@ def oracle_batch(spec, net, vids, text=None, dtype=torch.float64):
         outs.append(out)
     total = total / len(vids)
     total.backward()
-    return float(total), {n: p.grad for n, p in P.items()}, outs
+    return float(total.detach()), {n: p.grad for n, p in P.items()}, outs
 
 
 def compare_grads(net, ref, rtol=2e-3, atol_rms=1e-2, relaxed=(), relaxed_tol=2e-2, what=""):

@@ -246,3 +246,30 @@ def test_shipped_yaml_training_step_full_shape():
     assert all(torch.equal(a, b) for a, b in zip(g1, g2))
     for a, b in zip(s1, s2):
         np.testing.assert_array_equal(a["pred"], b["pred"])
+
+
+@pytest.mark.parametrize("case", [((2, 1),), ((5, 2), (40, 5)), ((12, 3), (300, 10))],
+                         ids=["T2", "T5+40", "T12+300"])
+def test_short_videos_vs_oracle(case, monkeypatch):
+    """Videos far shorter than the benchmark's (2 to 300 frames, one to ten ground-truth segments) at
+    HAViD-holdout dims: MS-TCN dilations beyond the video length (zero padding only), one-segment TDU
+    outputs, fewer keys than the fused attention cores' tiles, and a ragged lockstep batch whose videos
+    differ 8x / 25x in length.  TDU segments and predictions identical to the fp64 oracle, per-frame
+    logits within 1e-3, loss within 1e-4, every gradient.  (T=1 is left out: the reference's smoothing
+    loss averages over the T-1 neighbouring-frame pairs and is NaN there, the oracle's likewise.)"""
+    import bench
+    cfg = bench.make_cfg()
+    D, C = 2048, 75
+    net, text = bench.build_model(cfg, D, C, device=DEV, seed=0)
+    net.train()
+    vids = [bench.make_video(T, D, C, cfg, seed=7 + i, nseg=n) for i, (T, n) in enumerate(case)]
+    kinks = GruKinks(monkeypatch)
+    from factmx.dp import DataParallel
+    loss, saves = _gpu_step(net, vids, dp=DataParallel(net))
+    S = _segments(net)
+    spec = fo.resolve_spec(cfg, D, C, clip=True)
+    ref_loss, ref_grads, outs = oracle_batch(spec, net, vids, text)
+    assert S == [[len(r["tdu"].starts) for r in o["blocks"] if r["type"] == "U"] for o in outs], S
+    _check_forward(net, spec, outs, saves, text)
+    assert abs(loss - ref_loss) <= 1e-4 * abs(ref_loss), (loss, ref_loss)
+    compare_grads(net, ref_grads, rtol=2e-3, relaxed=kinks.flipped_prefixes(len(vids)), what=f"short {case}: ")
