@@ -273,3 +273,34 @@ def test_short_videos_vs_oracle(case, monkeypatch):
     _check_forward(net, spec, outs, saves, text)
     assert abs(loss - ref_loss) <= 1e-4 * abs(ref_loss), (loss, ref_loss)
     compare_grads(net, ref_grads, rtol=2e-3, relaxed=kinks.flipped_prefixes(len(vids)), what=f"short {case}: ")
+
+
+@pytest.mark.parametrize("nvid", [16, 17])
+def test_many_videos_vs_oracle(nvid, monkeypatch):
+    """The widest lockstep batch (MAX_LOCKSTEP_VIDEOS = 16 ragged videos: every per-video offset table
+    of the ragged convolutions, GRUs and fused attention cores full) and one video more (17: the
+    batch leaves the lockstep path for the reference's one-video-at-a-time loop) at HAViD-holdout
+    dims, lengths 33 to 609 frames, against the fp64 oracle: segments, predictions, per-frame logits
+    of every video, the mean loss and every gradient."""
+    import bench
+    from factmx.models import blocks as blocks_mod
+    cfg = bench.make_cfg()
+    D, C = 2048, 75
+    net, text = bench.build_model(cfg, D, C, device=DEV, seed=0)
+    net.train()
+    Ts = [33 + (i * 233) % 589 for i in range(nvid)]
+    vids = [bench.make_video(T, D, C, cfg, seed=20 + i, nseg=min(10, T // 8)) for i, T in enumerate(Ts)]
+    seqs = [torch.from_numpy(f).to(DEV) for f, _ in vids]
+    assert blocks_mod._batchable(net, seqs) == (nvid <= blocks_mod.MAX_LOCKSTEP_VIDEOS)
+    kinks = GruKinks(monkeypatch)
+    from factmx.dp import DataParallel
+    loss, saves = _gpu_step(net, vids, dp=DataParallel(net))
+    spec = fo.resolve_spec(cfg, D, C, clip=True)
+    ref_loss, ref_grads, outs = oracle_batch(spec, net, vids, text)
+    if nvid <= blocks_mod.MAX_LOCKSTEP_VIDEOS:
+        assert net._vb.Ts == Ts
+        S = _segments(net)
+        assert S == [[len(r["tdu"].starts) for r in o["blocks"] if r["type"] == "U"] for o in outs], S
+    _check_forward(net, spec, outs, saves, text)
+    assert abs(loss - ref_loss) <= 1e-4 * abs(ref_loss), (loss, ref_loss)
+    compare_grads(net, ref_grads, rtol=2e-3, relaxed=kinks.flipped_prefixes(len(vids)), what=f"{nvid} videos: ")
