@@ -1473,7 +1473,11 @@ static long long x2y_side_ws(int Nx, int xdim, int Ny, int ydim, int Hd, int out
     const int sp = std::max(pick_split(M, N, rows), defer_split(rows));
     return sp > 1 ? (long long)sp * M * N : 0LL;
   };
+  // without dropout dW_y is two GEMMs ([Y | 1] and feat), each narrower than the concatenation and so
+  // possibly split more ways (fewer tiles): a 1724-row ragged batch split the [Y | 1] piece 7 ways
+  // where the concatenation takes 3
   long long w = std::max(one(Ny, outdim, ydim + Hd + 1), one(Nx, Hd, xdim + 1));
+  w = std::max(w, std::max(one(Ny, outdim, ydim + 1), one(Ny, outdim, Hd + 1)));
   return std::max(w, one(Ny, Hd, ydim + 1));
 }
 

@@ -2031,6 +2031,10 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
     grid = dim3(g.tiles_x, g.tiles_y, d.batch * g.split);
     block = dim3(NTHREADS);
   }
+  if (g.split > 1 && t_ws_hi && !(g.ws >= t_ws_lo && g.ws + (long long)g.split * d.M * d.N * d.batch <= t_ws_hi))
+    std::fprintf(stderr, "factmx: gemm M %d N %d K %d batch %d split %d (cap %d, %s) needs %lld floats at +%lld of a %lld-float reservation\n",
+                 d.M, d.N, d.K, d.batch, g.split, cap, direct ? "direct" : "tiled",
+                 (long long)g.split * d.M * d.N * d.batch, (long long)(g.ws - t_ws_lo), (long long)(t_ws_hi - t_ws_lo));
   FX_REQUIRE(g.split <= 1 || !t_ws_hi ||
                  (g.ws >= t_ws_lo && g.ws + (long long)g.split * d.M * d.N * d.batch <= t_ws_hi),
              "gemm: split-K slabs would overrun the entry point's workspace reservation");

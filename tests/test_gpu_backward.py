@@ -304,3 +304,31 @@ def test_many_videos_vs_oracle(nvid, monkeypatch):
     _check_forward(net, spec, outs, saves, text)
     assert abs(loss - ref_loss) <= 1e-4 * abs(ref_loss), (loss, ref_loss)
     compare_grads(net, ref_grads, rtol=2e-3, relaxed=kinks.flipped_prefixes(len(vids)), what=f"{nvid} videos: ")
+
+
+def test_holdout_labels_vs_oracle(monkeypatch):
+    """Frames labelled with held-out classes (havid_view0_lh_pt_holdout.yaml's holdout_classes) at
+    HAViD-holdout dims on a ragged lockstep batch: in video 0 one stretch of frames carries a held-out
+    class (those frames leave the contrastive loss, blocks.py:728-744), video 1 is held out entirely
+    (the unweighted FACT loss is returned, blocks.py:745-747).  Segments, predictions, logits, loss and every
+    gradient against the fp64 oracle."""
+    import bench
+    cfg = bench.make_cfg()
+    D, C = 2048, 75
+    net, text = bench.build_model(cfg, D, C, device=DEV, seed=0)
+    net.train()
+    (f0, l0), (f1, l1) = [bench.make_video(T, D, C, cfg, seed=s) for T, s in ((1024, 3), (700, 4))]
+    l0 = l0.copy()
+    l0[300:520] = bench.HOLDOUT[0]
+    l1 = np.full_like(l1, bench.HOLDOUT[2])
+    vids = [(f0, l0), (f1, l1)]
+    kinks = GruKinks(monkeypatch)
+    from factmx.dp import DataParallel
+    loss, saves = _gpu_step(net, vids, dp=DataParallel(net))
+    S = _segments(net)
+    spec = fo.resolve_spec(cfg, D, C, clip=True)
+    ref_loss, ref_grads, outs = oracle_batch(spec, net, vids, text)
+    assert S == [[len(r["tdu"].starts) for r in o["blocks"] if r["type"] == "U"] for o in outs], S
+    _check_forward(net, spec, outs, saves, text)
+    assert abs(loss - ref_loss) <= 1e-4 * abs(ref_loss), (loss, ref_loss)
+    compare_grads(net, ref_grads, rtol=2e-3, relaxed=kinks.flipped_prefixes(len(vids)), what="holdout: ")
