@@ -205,7 +205,16 @@ PREC_NOTES = {
 def bf16_mode(net, step, frames_per_step, steps, warmup, fxf, mode="bf16"):
     """Time `steps` fixed-weight steps with the current stream's GEMM precision set to `mode` and compare
     its frame logits (last block, every video) and TDU segment counts with the headline precision's."""
+    # the same random draws for both runs (dropout seeds come from torch's CPU generator, Dropout2d from
+    # the CUDA one, the time mask from Python's `random`, basic.py time_mask): under a stochastic config
+    # both precisions then see identical masks
+    import random
+    rng = (torch.get_rng_state(), torch.cuda.get_rng_state(), random.getstate())
+
     def logits():
+        torch.set_rng_state(rng[0])
+        torch.cuda.set_rng_state(rng[1])
+        random.setstate(rng[2])
         step()
         torch.cuda.synchronize()
         last = net.block_list[-1]
@@ -230,6 +239,51 @@ def bf16_mode(net, step, frames_per_step, steps, warmup, fxf, mode="bf16"):
     return dict(value=round(frames_per_step * steps / el, 1), unit="frames/s", ms_per_step=round(1e3 * el / steps, 3),
                 dtype=dtype, frame_logit_max_abs_dev=round(dev, 6), frame_logit_max_abs=round(scale, 4),
                 frame_argmax_agreement=round(agree, 5), tdu_segments=s16, tdu_segments_headline=s32, note=note)
+
+
+def dp_schedule_overhead(net, seqs, labels, steps, rounds=3):
+    """N=1 only: the data-parallel schedule run for real over RCCL in a one-rank ``nccl`` group --
+    per-block bucket all-reduces (AVG) launched from the backward hooks on a collective stream that
+    waits for the compute and side streams -- against the plain step (schedule off), in alternating
+    rounds of `steps` steps.  Returns the overhead (median forced - median plain, ms/step)."""
+    import statistics
+    import torch.distributed as dist
+    from factmx.dp import DataParallel
+    dev = seqs[0].device
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=dev)
+    try:
+        dp = DataParallel(net, broadcast=False, force_buckets=True)
+
+        def step():
+            dp.zero_grad()
+            loss, _ = net(seqs, labels, compute_loss=True)
+            loss.backward()
+            dp.finish_gradients()
+
+        def timed(active):
+            dp.active = active
+            step()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step()
+            torch.cuda.synchronize()
+            return 1e3 * (time.perf_counter() - t0) / steps
+        plain, forced = [], []
+        for _ in range(rounds):
+            plain.append(timed(False))
+            forced.append(timed(True))
+        early = list(dp.hook_launched)
+        pm, fm = statistics.median(plain), statistics.median(forced)
+        return dict(dp_schedule_overhead_ms=round(fm - pm, 3), plain_ms_per_step=[round(v, 3) for v in plain],
+                    forced_ms_per_step=[round(v, 3) for v in forced], backend=dist.get_backend(),
+                    buckets_per_step=sum(len(b) for b in dp.block_buckets.values()) + len(dp.rest_buckets),
+                    hook_launched_blocks=early,
+                    note="world-size-1 nccl (RCCL) group, DataParallel(force_buckets=True): every block's bucket "
+                         "all-reduced (AVG) from its backward hook; median of alternating rounds")
+    finally:
+        dist.destroy_process_group()
 
 
 def prof_collect(lib, kind):
@@ -343,6 +397,8 @@ def main():
                     help="extra timed steps with clip_grad_norm_ + Adam after the fixed-weight steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-bf16", action="store_true", help="skip the extra precision-mode measurements (N=1 only)")
+    ap.add_argument("--no-dp-overhead", action="store_true",
+                    help="skip the N=1 RCCL measurement of the data-parallel bucket schedule")
     ap.add_argument("--prec", choices=["default", "fp32s", "fp32"], default="default",
                     help="GEMM arithmetic of the headline: the library default, fp32s (fp32 by a 3-piece bf16 split "
                          "on the bf16 matrix cores) or fp32 (f32 MFMA)")
@@ -396,6 +452,11 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    # the host heap built so far (torch, the model, the warm-up's caches) is long-lived: move it out of
+    # the cyclic collector's generations so a full collection does not stall a step for ~60 ms walking
+    # it (factmx.utils.runtime.freeze_host_heap; round-4 diagnosis of the Adam leg)
+    from factmx.utils.runtime import freeze_host_heap
+    freeze_host_heap()
     S = video_segments(net)
     log(f"[rank {rank}] TDU segments per video (per U block): {S}")
 
@@ -471,6 +532,13 @@ def main():
         other = bf16_mode(net, step, sum(Ts), args.steps, args.warmup, fxf,
                           "fp32" if headline_prec == "fp32s" else "fp32s")
 
+    dp_sched = None
+    if world == 1 and not args.no_dp_overhead:
+        try:
+            dp_sched = dp_schedule_overhead(net, seqs, labels, args.steps)
+        except Exception as e:          # reported, never fatal for the headline line
+            dp_sched = dict(error=f"{type(e).__name__}: {e}")
+
     frames = world * sum(Ts) * args.steps
     value = frames / elapsed
     if rank == 0:
@@ -512,7 +580,7 @@ def main():
                                 parallelism=f"dp{world}", weights="fixed (no optimizer update in the timed steps)",
                                 tdu_segments=S, tdu_segments_after_timing=S_after),
                     roofline=roofline, roofline_attention=roofline_attention, train_step_with_adam=adam,
-                    bf16_mode=bf16)
+                    bf16_mode=bf16, dp_schedule=dp_sched)
         if other is not None:
             line["fp32_f32mfma_mode" if headline_prec == "fp32s" else "fp32_split_mode"] = other
         if world == 1 and not args.no_cpu_baseline:

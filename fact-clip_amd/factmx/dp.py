@@ -12,8 +12,11 @@ contiguous slice.  Those slices are the all-reduce buckets: the model marks the
 input of every block during the forward (``mark_block_input``); when autograd
 has produced the gradient of block k's input, every kernel of block k's backward
 has been enqueued, so its bucket's all-reduce is launched right there
-(asynchronously, on the collective stream, ordered after those kernels) and runs
-over xGMI while blocks k-1 .. 0 compute their backward.  ``finish_gradients``
+(asynchronously, from a collective stream that waits on events recorded on the
+compute stream and on the library's side stream -- where block k's deferred
+weight-gradient GEMMs run -- so neither of those streams ever waits for the
+other mid-backward) and runs over xGMI while blocks k-1 .. 0 compute their
+backward.  ``finish_gradients``
 launches what is left (block 0, the action queries and the CLIP projection head,
 whose gradients are only final at the end) and makes the compute stream wait
 for all of them -- no host synchronisation.  Buckets are few and large (xGMI
@@ -95,7 +98,7 @@ def mark_block_input(net, k, x):
     """Called by the model's forward with the input tensor of block k: registers the hook that
     launches block k's gradient bucket once autograd has produced x's gradient."""
     dp = getattr(net, "_fx_dp", None)
-    if dp is None or not torch.is_grad_enabled() or not torch.is_tensor(x) or not x.requires_grad:
+    if dp is None or not dp.active or not torch.is_grad_enabled() or not torch.is_tensor(x) or not x.requires_grad:
         return
     dp._arm(k, x)
 
@@ -108,10 +111,16 @@ class DataParallel:
     optimizer over dp.flat (factmx.optim.FusedAdam(..., grad_flat=dp.flat))
     """
 
-    def __init__(self, net, group=None, broadcast=True, bucket_mb=256):
+    def __init__(self, net, group=None, broadcast=True, bucket_mb=256, force_buckets=False):
         self.net = net
         self.group = group
         self.world = _dist_world(group)
+        # force_buckets: keep the per-block bucket schedule (hooks, collective stream, all-reduces)
+        # even in a one-rank group -- how the RCCL path is exercised and its overhead measured on a
+        # single GPU (tests/test_gpu_rccl.py, bench.py dp_schedule_overhead_ms)
+        if force_buckets and not (dist.is_available() and dist.is_initialized()):
+            raise RuntimeError("DataParallel(force_buckets=True) needs an initialised process group")
+        self.active = self.world > 1 or bool(force_buckets)
         named = [(n, p) for n, p in net.named_parameters() if p.requires_grad]
         self.params = [p for _, p in named]
         if broadcast and self.world > 1:
@@ -145,8 +154,15 @@ class DataParallel:
         self.hook_launched = []
         self._armed = {}
         self._calls = -1
-        if self.world > 1:
+        # the stream the bucket collectives are issued from: it waits for the compute stream (block k's
+        # input-gradient chain) and the library's side stream (block k's deferred weight gradients) at
+        # the bucket's launch, so the compute stream itself never waits mid-backward
+        dev = self.flat.device
+        self._cstream = torch.cuda.Stream(device=dev) if (self.active and dev.type == "cuda") else None
+        if self.active:
             net._fx_dp = self
+        elif getattr(net, "_fx_dp", None) is not None:
+            net._fx_dp = None
 
     @torch.no_grad()
     def _broadcast_from_rank0(self):
@@ -187,24 +203,42 @@ class DataParallel:
         if self._armed[k] == 0:
             self._launch_block(k, True)
 
+    def _issue(self, buckets):
+        """All-reduce `buckets` from the collective stream once everything enqueued so far on the
+        compute stream AND on the library's side stream has run (the side stream carries weight
+        gradients deferred past their block's backward call).  Only the collective stream waits; the
+        collective itself (RCCL's own stream) is ordered after it by torch.distributed."""
+        if not buckets:
+            return
+        cs = self._cstream
+        if cs is None:                   # CPU tensors (gloo tests): nothing to order
+            for b in buckets:
+                self._pending.append(_all_reduce_mean_async(b, self.group))
+            return
+        cs.wait_stream(torch.cuda.current_stream(cs.device))
+        side = fxf.side_stream()
+        if side is not None:
+            cs.wait_stream(side)
+        with torch.cuda.stream(cs):
+            for b in buckets:
+                self._pending.append(_all_reduce_mean_async(b, self.group))
+
     def _launch_block(self, k, from_hook=False):
-        if self.world == 1 or k in self._launched:
+        if not self.active or k in self._launched:
             return
         self._launched.add(k)
         if from_hook:
             self.hook_launched.append(k)
-        fxf.side_join()   # weight gradients still running on the library's side stream land first
-        for b in self.block_buckets.get(k, []):
-            self._pending.append(_all_reduce_mean_async(b, self.group))
+        self._issue(self.block_buckets.get(k, []))
 
     def finish_gradients(self):
         """Launch the buckets no hook has launched and make the current stream wait for all of them."""
-        if self.world == 1:
+        if not self.active:
             return
         for k in sorted(self.block_buckets, reverse=True):
             self._launch_block(k)
-        for b in self.rest_buckets:
-            self._pending.append(_all_reduce_mean_async(b, self.group))
+        fxf.side_join()           # (the backward's end-of-pass callback has normally joined already)
+        self._issue(self.rest_buckets)
         need_div = False
         for w, div in self._pending:
             w.wait()

@@ -582,7 +582,7 @@ MSTCN_FUSED_LAYERS = os.environ.get("FX_MSTCN_FUSED_LAYERS", "0") == "1"   # A/B
 
 
 def _ptr_array(ts):
-    return (ctypes.c_void_p * max(len(ts), 1))(*[nx.ptr(t) for t in ts])
+    return nx.array_type(ctypes.c_void_p, max(len(ts), 1))(*[nx.ptr(t) for t in ts])
 
 
 class MSTCNFn(torch.autograd.Function):
@@ -614,14 +614,14 @@ class MSTCNFn(torch.autograd.Function):
         if seq_off is not None:     # ragged videos: host row offsets
             so = nx.int_array(seq_off)
             keep.append(so)
-            prm.seq_off = ctypes.cast(so, ctypes.c_void_p)
+            prm.seq_off = ctypes.addressof(so)
         prm.cin, prm.F, prm.cout, prm.num_layers, prm.layernorm, prm.in_map = cin, F, cout, nl, int(ln), int(in_map)
         prm.dil0, prm.dil_factor = d0, dfac
         prm.w_in, prm.b_in = nx.ptr(w_in), nx.ptr(b_in)
         for field, k in (("w_dil", 0), ("b_dil", 1), ("w_pw", 2), ("b_pw", 3), ("ln_w", 4), ("ln_b", 5)):
             arr = _ptr_array([lw[k] for lw in layers])
             keep.append(arr)
-            setattr(prm, field, ctypes.cast(arr, ctypes.c_void_p))
+            setattr(prm, field, ctypes.addressof(arr))
         prm.w_out, prm.b_out = nx.ptr(w_out), nx.ptr(b_out)
         prm.dropout, prm.seed = float(drop_p), int(seed)
         prm.fused_layers = int(MSTCN_FUSED_LAYERS)
@@ -654,7 +654,7 @@ class MSTCNFn(torch.autograd.Function):
         for field, k in (("w_dil", 0), ("b_dil", 1), ("w_pw", 2), ("b_pw", 3), ("ln_w", 4), ("ln_b", 5)):
             arr = _ptr_array([lw[k] for lw in layers])
             keep.append(arr)
-            setattr(g, field, ctypes.cast(arr, ctypes.c_void_p))
+            setattr(g, field, ctypes.addressof(arr))
         g.w_out, g.b_out = nx.ptr(w_out), nx.ptr(b_out)
         dx = _empty(*x.shape, device=dev) if ctx.needs_input_grad[0] else None
         ws = _ws(lib.fx_mstcn_workspace_floats(ctypes.byref(ctx.prm), x.shape[0]), dev)
@@ -716,12 +716,12 @@ class MSTCN2Fn(torch.autograd.Function):
             if seq_off is not None:
                 so = nx.int_array(seq_off)
                 keep.append(so)
-                prm.seq_off = ctypes.cast(so, ctypes.c_void_p)
+                prm.seq_off = ctypes.addressof(so)
         prm.w_in, prm.b_in = nx.ptr(w_in), nx.ptr(b_in)
         for field, grp in zip(("w_d1", "b_d1", "w_d2", "b_d2", "w_fu", "b_fu"), groups):
             arr = _ptr_array(grp)
             keep.append(arr)
-            setattr(prm, field, ctypes.cast(arr, ctypes.c_void_p))
+            setattr(prm, field, ctypes.addressof(arr))
         prm.w_out, prm.b_out = nx.ptr(w_out), nx.ptr(b_out)
         return prm
 
@@ -1194,9 +1194,9 @@ def _fill_decoder_struct(st, slots, gl, tensors, keep):
             return None
         return tensors[s[0]].data_ptr() + 4 * s[1]
     for f, lst in slots.items():
-        arr = (ctypes.c_void_p * max(len(lst), 1))(*[addr(s) for s in lst])
+        arr = nx.array_type(ctypes.c_void_p, max(len(lst), 1))(*[addr(s) for s in lst])
         keep.append(arr)
-        setattr(st, f, ctypes.cast(arr, ctypes.c_void_p))
+        setattr(st, f, ctypes.addressof(arr))
     for f, s in gl.items():
         setattr(st, f, addr(s))
 
@@ -1210,7 +1210,7 @@ class DecoderFn(torch.autograd.Function):
         """Per-call fields (dropout p's and seed, ragged memory offsets) of the cached param struct."""
         pd, pa, seed, mem_off = call
         prm.dropout, prm.attn_dropout, prm.seed = pd, pa, seed
-        prm.mem_off = None if mem_off is None else ctypes.cast(mem_off, ctypes.c_void_p)
+        prm.mem_off = None if mem_off is None else ctypes.addressof(mem_off)
 
     @staticmethod
     def forward(ctx, tgt, qpos, mem, mpos, spec, nvid, call, *params):

@@ -216,18 +216,33 @@ def load(path=None):
     return lib
 
 
+# ctypes array TYPES by (element type, length).  ctypes' own cache of ``c_int * n`` holds its types
+# weakly, so a type made per call dies after it -- and every type object sits in a reference cycle:
+# per-step cyclic garbage that only a full (gen-2) collection frees, a ~60 ms host stall every few
+# dozen training steps (round 4, tools/r04_gc_cycles.py).  Keeping the types here makes the per-call
+# arrays plain refcounted objects.
+_ARRAY_TYPES = {}
+
+
+def array_type(ctype, n):
+    t = _ARRAY_TYPES.get((ctype, n))
+    if t is None:
+        t = _ARRAY_TYPES[(ctype, n)] = ctype * n
+    return t
+
+
 def float_array(vals):
     """Host float32 array for the C ABI (None -> NULL)."""
     if vals is None:
         return None
-    return (ctypes.c_float * max(len(vals), 1))(*[float(v) for v in vals])
+    return array_type(ctypes.c_float, max(len(vals), 1))(*[float(v) for v in vals])
 
 
 def int_array(vals):
     """Host int32 array for the C ABI's prefix-offset arguments (None -> NULL)."""
     if vals is None:
         return None
-    return (ctypes.c_int * len(vals))(*[int(v) for v in vals])
+    return array_type(ctypes.c_int, len(vals))(*[int(v) for v in vals])
 
 
 def check(status, what):
