@@ -26,6 +26,8 @@ construction, so every rank starts from identical parameters whatever its seed.
 ``FlatGradReducer`` is the same flat buffer without per-block buckets (one or
 more equal buckets reduced after backward), for models without a block list.
 """
+import time
+
 import torch
 import torch.distributed as dist
 
@@ -154,6 +156,7 @@ class DataParallel:
         self.hook_launched = []
         self._armed = {}
         self._calls = -1
+        self.host_issue_s = 0.0      # host time spent issuing bucket collectives (diagnostics)
         # the stream the bucket collectives are issued from: it waits for the compute stream (block k's
         # input-gradient chain) and the library's side stream (block k's deferred weight gradients) at
         # the bucket's launch, so the compute stream itself never waits mid-backward
@@ -210,6 +213,13 @@ class DataParallel:
         collective itself (RCCL's own stream) is ordered after it by torch.distributed."""
         if not buckets:
             return
+        t0 = time.perf_counter()
+        try:
+            self._issue_on(buckets)
+        finally:
+            self.host_issue_s += time.perf_counter() - t0
+
+    def _issue_on(self, buckets):
         cs = self._cstream
         if cs is None:                   # CPU tensors (gloo tests): nothing to order
             for b in buckets:

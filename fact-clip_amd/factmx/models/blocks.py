@@ -711,7 +711,12 @@ def _forward_videos(net, seq_list, label_list, compute_loss):
             restore(nvid - 1)       # side-channel attributes: the last video's views, as in the reference
             net.video_segments = [[blk._bt["S"][v] for blk in net.block_list if "S" in blk._bt]
                                   for v in range(nvid)]
-            return vloss.run(net, net._vb, compute_loss, early)
+            try:
+                return vloss.run(net, net._vb, compute_loss, early)
+            except vloss.TableTooLarge:
+                # more matched columns than the fused term table holds (o2m past FX_LOSS_MAXK segments):
+                # this batch's losses and predictions run per video on the lockstep outputs
+                net.video_segments = []
         for v in range(len(seq_list)):
             restore(v)
             net.video_segments.append([blk.tdu.num_seg for blk in net.block_list if hasattr(blk, "tdu")])

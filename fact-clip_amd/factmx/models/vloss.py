@@ -103,8 +103,9 @@ def segment_weights(mc, transcript):
 
 def supported(net):
     """The fused phase covers FACT / FACT_CLIP without transcripts whose last block has token->frame
-    attention (every reference config: the matching reads it); a video whose matching pairs more
-    than FX_LOSS_MAXK columns fails loudly in run()."""
+    attention (every reference config: the matching reads it).  A batch in which some video's matching
+    pairs more than FX_LOSS_MAXK columns makes run() raise TableTooLarge before any of its work is
+    enqueued, and the caller computes that batch's losses per video (loss.py's methods)."""
     from .blocks import UpdateBlock, UpdateBlockTDU
     mc = getattr(net, "mcriterion", None)
     if mc is None or net.cfg.FACT.trans or net.cfg.Loss.match not in ("o2o", "o2m", "seq"):
@@ -313,6 +314,11 @@ class EarlyMatch:
         return out
 
 
+class TableTooLarge(Exception):
+    """A video of the batch pairs more matched token/segment columns than the fused term table holds
+    (FX_LOSS_MAXK): the caller runs that batch's losses on the per-video path instead."""
+
+
 def run(net, vb, compute_loss, early=None):
     """Predictions (and with compute_loss the batch loss + per-video loss values) of the lockstep
     batch whose block outputs forward_batch left in ``blk._bt``; ``early`` is the EarlyMatch the last
@@ -362,6 +368,9 @@ def run(net, vb, compute_loss, early=None):
 
     assert early is not None and early.done, "the last block did not run the early matching stage"
     matches = early.matches(Q)
+    big = [v for v, (ai, _) in enumerate(matches) if len(ai) > nx.LOSS_MAXK]
+    if big:      # e.g. o2m matching (every ground-truth segment paired, loss.py:155-193) past 512 segments
+        raise TableTooLarge(big)
     labs, gts, G, gt_off, lab_off = early.labs, early.gts, early.G, early.gt_off, early.lab_off
     cw, cw_off, base = early.cw, early.cw_off, early.base
 

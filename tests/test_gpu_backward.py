@@ -332,3 +332,45 @@ def test_holdout_labels_vs_oracle(monkeypatch):
     _check_forward(net, spec, outs, saves, text)
     assert abs(loss - ref_loss) <= 1e-4 * abs(ref_loss), (loss, ref_loss)
     compare_grads(net, ref_grads, rtol=2e-3, relaxed=kinks.flipped_prefixes(len(vids)), what="holdout: ")
+
+
+def test_o2m_past_loss_table_limit_vs_oracle(monkeypatch):
+    """One-to-many matching (loss.py:155-193) pairs EVERY ground-truth segment with a token, so a video
+    with more than FX_LOSS_MAXK (512) segments overflows the fused loss-term table: the lockstep batch
+    then computes its losses and predictions per video (the reference's MatchCriterion methods) on the
+    lockstep outputs instead of failing.  Video 0 has 683 three-frame segments, video 1 is a seg10 video;
+    segments, predictions, logits, loss and every gradient against the fp64 oracle."""
+    import bench
+    from factmx import native as nx
+    from factmx.models import vloss
+    cfg = bench.make_cfg()
+    cfg.Loss.match = "o2m"
+    D, C = 2048, 75
+    net, text = bench.build_model(cfg, D, C, device=DEV, seed=0)
+    net.train()
+    (f0, _), (f1, l1) = [bench.make_video(T, D, C, cfg, seed=s) for T, s in ((2048, 5), (1500, 6))]
+    seen = [c for c in range(C) if c not in bench.HOLDOUT]
+    l0 = np.asarray([seen[(i // 3) % 7] for i in range(2048)], dtype=np.int64)
+    assert len(np.flatnonzero(np.diff(l0))) + 1 > nx.LOSS_MAXK
+    vids = [(f0, l0), (f1, l1)]
+    raised = []
+    run = vloss.run
+
+    def spy(*a, **k):
+        try:
+            return run(*a, **k)
+        except vloss.TableTooLarge as e:
+            raised.append(e.args[0])
+            raise
+    monkeypatch.setattr(vloss, "run", spy)
+    kinks = GruKinks(monkeypatch)
+    from factmx.dp import DataParallel
+    loss, saves = _gpu_step(net, vids, dp=DataParallel(net))
+    assert raised == [[0]], raised
+    spec = fo.resolve_spec(cfg, D, C, clip=True)
+    ref_loss, ref_grads, outs = oracle_batch(spec, net, vids, text)
+    S = _segments(net)
+    assert S == [[len(r["tdu"].starts) for r in o["blocks"] if r["type"] == "U"] for o in outs], S
+    _check_forward(net, spec, outs, saves, text)
+    assert abs(loss - ref_loss) <= 1e-4 * abs(ref_loss), (loss, ref_loss)
+    compare_grads(net, ref_grads, rtol=2e-3, relaxed=kinks.flipped_prefixes(len(vids)), what="o2m > MAXK: ")

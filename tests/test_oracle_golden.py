@@ -55,17 +55,16 @@ def test_oracle_end_to_end(name):
     P = param_dict(meta["param_shapes"], meta["seed"])
     feats, label, text = tiny_inputs(meta)
     text_t = torch.from_numpy(text) if clip else None
-    out = fo.forward(spec, P, torch.from_numpy(feats))
+    # fpos on: the reference's float32 sinusoid table (basic.py:92-103) depends on the host's float32
+    # exp/sin/cos, so the fixture carries the reference's own table and the oracle takes it as given
+    pe = torch.from_numpy(fx["frame_pe"]) if spec["fpos"] else None
+    out = fo.forward(spec, P, torch.from_numpy(feats), pe_table=pe)
     pred = fo.predict(spec, out, text_t)
     total, fact, con, m = fo.video_loss(spec, out, label, text_t)
     total.backward()
 
-    # The reference's sinusoid table is float32 (basic.py:92-99) and ATen's float32 exp/sin/cos
-    # dispatch per host CPU (MKL VML / SLEEF), so the table moves by an ulp between hosts;
-    # every tensor downstream of it is compared at float32-table precision when fpos is on.
-    f32 = spec["fpos"]
-    tol = dict(rtol=1e-5, atol=1e-5) if f32 else dict(rtol=1e-9, atol=1e-11)
-    ltol = 1e-6 if f32 else 1e-10
+    tol = dict(rtol=1e-9, atol=1e-11)
+    ltol = 1e-10
     for i, rec in enumerate(out["blocks"]):
         p = f"block{i}/"
         np.testing.assert_allclose(rec["frame_clogit"].detach().numpy(), fx[p + "frame_clogit"], **tol)
@@ -88,7 +87,7 @@ def test_oracle_end_to_end(name):
         np.testing.assert_allclose(fact.item(), fx["fact_loss"][0], rtol=ltol)
         np.testing.assert_allclose(con.item(), fx["contrastive_loss"][0], rtol=ltol)
     for n, t in P.items():
-        check_grad(fx, "", n, t.grad, rtol=1e-5 if f32 else 1e-7, atol=1e-6 if f32 else 1e-10)
+        check_grad(fx, "", n, t.grad, rtol=1e-7, atol=1e-10)
 
 
 # ---------------------------------------------------------------------------
