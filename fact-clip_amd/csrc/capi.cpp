@@ -1550,7 +1550,8 @@ int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpo
   FX_TRY(linear_fwd(yin, ldyin, Ny, ydim, wq, bq, yq, Hd, Hd, 0, s));
   const float scale = 1.0f / std::sqrt((float)Hd);
   // a short key side (the a2f map: <= 64 action tokens per video): the whole core in one launch
-  const bool al16 = ((reinterpret_cast<uintptr_t>(yq) | reinterpret_cast<uintptr_t>(xk)) & 15) == 0;
+  const bool al16 =
+      ((reinterpret_cast<uintptr_t>(yq) | reinterpret_cast<uintptr_t>(xk) | reinterpret_cast<uintptr_t>(xv)) & 15) == 0;
   if (knobs().x2y_fused && x2y_a2f_fusable(V.n, V.x.data(), Hd) && al16) {
     FX_TRY(launch_x2y_a2f_fwd(yq, xk, xv, Hd, scale, V.n, V.y.data(), V.x.data(), V.a.data(), logit, attn, feat, s));
   } else if (knobs().x2y_fused && x2y_f2a_fusable(V.n, V.x.data(), V.y.data(), Hd) && al16) {
@@ -1647,8 +1648,11 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
   // a short key side (the a2f map): dP, the softmax backward and dyq in one launch for every video; the
   // products that reduce over the query rows (dxv = attn^T dfeat, dxk = scale dlogit^T yq) stay
   // split-K GEMMs around it
-  const bool fused = knobs().x2y_fused && x2y_a2f_fusable(V.n, V.x.data(), Hd) && (cw & 3) == 0 &&
-                     ((reinterpret_cast<uintptr_t>(dcat + ydim)) & 15) == 0;
+  // the fused cores do float4 loads of the saved xk / xv / yq rows and of dcat: the same 16-B test as
+  // the forward's (X2YLayout offsets Nx*xdim + Ny*ydim (+k*Nx*Hd) need not be multiples of 4 floats)
+  const bool al16 = ((reinterpret_cast<uintptr_t>(xk) | reinterpret_cast<uintptr_t>(xv) |
+                      reinterpret_cast<uintptr_t>(yq) | reinterpret_cast<uintptr_t>(dcat + ydim)) & 15) == 0;
+  const bool fused = knobs().x2y_fused && x2y_a2f_fusable(V.n, V.x.data(), Hd) && (cw & 3) == 0 && al16;
   if (fused) {
     FX_TRY(launch_x2y_a2f_bwd(dcat + ydim, cw, xv, xk, attn, dattn, dlogit, Hd, scale, V.n, V.y.data(), V.x.data(),
                               V.a.data(), dL, dyq, s));
@@ -1674,7 +1678,7 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
       FX_TRY(launch_gemm_group(g2, n2, s));
     }
   } else if (knobs().x2y_fused && knobs().x2y_f2a_bwd && x2y_f2a_fusable(V.n, V.x.data(), V.y.data(), Hd) &&
-             (cw & 3) == 0 && ((reinterpret_cast<uintptr_t>(dcat + ydim)) & 15) == 0) {
+             (cw & 3) == 0 && al16) {
     // the f2a map: dP / dxv, then dlogit / dxk / dyq partials per 64-key chunk, then the ordered dyq merge
     float* f2a_ws = workspace + x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, V) + (long long)Ny * cw +
                     x2y_side_ws(Nx, xdim, Ny, ydim, Hd, outdim);

@@ -60,10 +60,13 @@ struct AdamArgs {
   float bc2_sqrt;      // sqrt(1 - b2^t)
   float b1, b2, eps, wd;
   float* norm_out;     // nullable: total norm written by block 0
+  const int* status;   // nullable: the device status word; non-zero (a kernel of the step failed, e.g. a
+                       // BiGRU backward timeout) -> the whole update is skipped, p / m / v / g untouched
 };
 
 __global__ __launch_bounds__(TPB) void adam_kernel(AdamArgs a) {
   __shared__ float coef_s;
+  if (a.status && a.status[0] != 0) return;   // uniform over the grid: every block skips
   float coef = 1.f;
   if (a.part) {
     if (threadIdx.x < 64) {
@@ -172,6 +175,13 @@ int fx_clip_grad_scale(float* g, long long n, const float* workspace, float max_
 int fx_adam_step(float* p, float* g, float* m, float* v, long long n, long long step, float lr, float beta1,
                  float beta2, float eps, float weight_decay, float max_norm, float* workspace, float* norm_out,
                  void* stream) {
+  return fx_adam_step_checked(p, g, m, v, n, step, lr, beta1, beta2, eps, weight_decay, max_norm, workspace, norm_out,
+                              nullptr, stream);
+}
+
+int fx_adam_step_checked(float* p, float* g, float* m, float* v, long long n, long long step, float lr, float beta1,
+                         float beta2, float eps, float weight_decay, float max_norm, float* workspace, float* norm_out,
+                         const int* status, void* stream) {
   FX_REQUIRE(n >= 0 && p && g && m && v, "adam_step: null buffer");
   FX_REQUIRE(step >= 1, "adam_step: step counts from 1");
   FX_REQUIRE(((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
@@ -190,6 +200,7 @@ int fx_adam_step(float* p, float* g, float* m, float* v, long long n, long long 
   a.bc2_sqrt = (float)std::sqrt(bc2);
   a.b1 = beta1; a.b2 = beta2; a.eps = eps; a.wd = weight_decay;
   a.norm_out = norm_out;
+  a.status = status;
   if (a.part) hipLaunchKernelGGL(sumsq_partial_kernel, dim3(NPART), dim3(TPB), 0, s, g, n, workspace);
   const long long n4 = (n + 3) / 4;
   const int blocks = (int)std::min<long long>((n4 + TPB - 1) / TPB, 2048);

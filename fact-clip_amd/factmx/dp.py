@@ -96,6 +96,20 @@ class FlatGradReducer:
             self.flat.div_(world)
 
 
+def _merge_adjacent(buckets):
+    """Views of one flat buffer, merged where one ends exactly where the next begins."""
+    out = []
+    for b in sorted(buckets, key=lambda t: t.data_ptr()):
+        if out and out[-1].data_ptr() + out[-1].numel() * out[-1].element_size() == b.data_ptr():
+            p = out[-1]
+            base = p._base if p._base is not None else p
+            off = (p.data_ptr() - base.data_ptr()) // p.element_size()
+            out[-1] = base.view(-1)[off:off + p.numel() + b.numel()]
+        else:
+            out.append(b)
+    return out
+
+
 def mark_block_input(net, k, x):
     """Called by the model's forward with the input tensor of block k: registers the hook that
     launches block k's gradient bucket once autograd has produced x's gradient."""
@@ -157,6 +171,9 @@ class DataParallel:
         self._armed = {}
         self._calls = -1
         self.host_issue_s = 0.0      # host time spent issuing bucket collectives (diagnostics)
+        self.issue_thread = False    # make the collective calls from a helper thread (A/B knob)
+        self._q = None
+        self._worker_error = None
         # the stream the bucket collectives are issued from: it waits for the compute stream (block k's
         # input-gradient chain) and the library's side stream (block k's deferred weight gradients) at
         # the bucket's launch, so the compute stream itself never waits mid-backward
@@ -210,28 +227,59 @@ class DataParallel:
         """All-reduce `buckets` from the collective stream once everything enqueued so far on the
         compute stream AND on the library's side stream has run (the side stream carries weight
         gradients deferred past their block's backward call).  Only the collective stream waits; the
-        collective itself (RCCL's own stream) is ordered after it by torch.distributed."""
+        collective itself (RCCL's own stream) is ordered after it by torch.distributed.  With
+        ``issue_thread`` the hook only records the two events and a helper thread makes the
+        collective calls, so the autograd thread goes straight back to enqueueing the backward."""
         if not buckets:
             return
         t0 = time.perf_counter()
         try:
-            self._issue_on(buckets)
+            cs = self._cstream
+            if cs is None:                   # CPU tensors (gloo tests): nothing to order
+                for b in buckets:
+                    self._pending.append(_all_reduce_mean_async(b, self.group))
+                return
+            evs = [torch.cuda.current_stream(cs.device).record_event()]
+            side = fxf.side_stream()
+            if side is not None:
+                evs.append(side.record_event())
+            if self.issue_thread:
+                self._worker().put((buckets, evs))
+            else:
+                self._issue_after(buckets, evs)
         finally:
             self.host_issue_s += time.perf_counter() - t0
 
-    def _issue_on(self, buckets):
+    def _issue_after(self, buckets, evs):
         cs = self._cstream
-        if cs is None:                   # CPU tensors (gloo tests): nothing to order
-            for b in buckets:
-                self._pending.append(_all_reduce_mean_async(b, self.group))
-            return
-        cs.wait_stream(torch.cuda.current_stream(cs.device))
-        side = fxf.side_stream()
-        if side is not None:
-            cs.wait_stream(side)
+        for e in evs:
+            cs.wait_event(e)
         with torch.cuda.stream(cs):
             for b in buckets:
                 self._pending.append(_all_reduce_mean_async(b, self.group))
+
+    def _worker(self):
+        if self._q is None:
+            import queue
+            import threading
+            self._q = queue.Queue()
+            dev = self._cstream.device
+
+            def run():
+                torch.cuda.set_device(dev)
+                while True:
+                    item = self._q.get()
+                    try:
+                        if item is None:
+                            return
+                        self._issue_after(*item)
+                    except BaseException as e:      # re-raised on the caller's thread at finish
+                        self._worker_error = e
+                    finally:
+                        self._q.task_done()
+            self._thread = threading.Thread(target=run, name="factmx-dp-issue", daemon=True)
+            self._thread.start()
+        return self._q
 
     def _launch_block(self, k, from_hook=False):
         if not self.active or k in self._launched:
@@ -245,10 +293,18 @@ class DataParallel:
         """Launch the buckets no hook has launched and make the current stream wait for all of them."""
         if not self.active:
             return
-        for k in sorted(self.block_buckets, reverse=True):
-            self._launch_block(k)
+        # the buckets no hook launched (block 0: its input is the data) and the tail (action queries,
+        # CLIP head): adjacent slices of the flat buffer are merged into one collective
+        left = [b for k in sorted(self.block_buckets, reverse=True) if k not in self._launched
+                for b in self.block_buckets[k]]
+        self._launched.update(self.block_buckets)
         fxf.side_join()           # (the backward's end-of-pass callback has normally joined already)
-        self._issue(self.rest_buckets)
+        self._issue(_merge_adjacent(left + list(self.rest_buckets)))
+        if self._q is not None:
+            self._q.join()        # every collective has been issued (the helper thread is idle)
+            if self._worker_error is not None:
+                e, self._worker_error = self._worker_error, None
+                raise e
         need_div = False
         for w, div in self._pending:
             w.wait()

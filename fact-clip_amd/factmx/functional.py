@@ -915,14 +915,62 @@ def status_raise(value, dev):
     """Raise FactmxNativeError for a non-zero status word read back from the device (and clear it)."""
     if value:
         device_status(dev).zero_()
+        _bwd_status.clear()       # (the same failure, possibly also seen by a backward-pass copy)
         raise nx.FactmxNativeError(f"device status {value}: a BiGRU workgroup timed out waiting for its peers "
                                    "(FX_STATUS_GRU_TIMEOUT) -- the GRU outputs of this step are invalid")
+
+
+# Backward-pass status read-backs: a BiGRU backward writes the same status word as the forward, but
+# after the forward's read-back was taken.  GRUFn.backward queues (once per backward pass) an end-of-
+# pass callback that copies the word to pinned host memory behind an event -- ordered after every
+# kernel of the backward, no host wait -- and the copy is checked at the next forward (or by
+# check_device_status).  FusedAdam's update is guarded by the same word on the device, so the invalid
+# gradients of such a step are never applied.
+_bwd_status = []
+_bwd_status_queued = False
+
+
+def _queue_backward_status(dev):
+    global _bwd_status_queued
+    if _bwd_status_queued:
+        return
+    _bwd_status_queued = True
+    stream = torch.cuda.current_stream(dev)
+
+    def copy_status():
+        global _bwd_status_queued
+        _bwd_status_queued = False
+        with torch.cuda.stream(stream):
+            h = torch.empty(1, dtype=torch.int32, pin_memory=True)
+            h.copy_(device_status(dev)[:1], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        _bwd_status.append((h, ev, dev))
+    torch.autograd.Variable._execution_engine.queue_callback(copy_status)
+
+
+def resolve_backward_status():
+    """Raise FactmxNativeError if a kernel of an earlier BACKWARD pass set the status word.  (Called
+    between passes: a copy callback an aborted backward never ran must not block later ones.)"""
+    global _bwd_status_queued
+    _bwd_status_queued = False
+    while _bwd_status:
+        h, ev, dev = _bwd_status.pop(0)
+        ev.synchronize()
+        if int(h[0]):
+            _bwd_status.clear()
+            device_status(dev).zero_()
+            raise nx.FactmxNativeError(
+                f"device status {int(h[0])}: a BiGRU workgroup timed out waiting for its peers "
+                "(FX_STATUS_GRU_TIMEOUT) in the BACKWARD pass of the previous step -- its gradients are invalid "
+                "(a factmx FusedAdam step on them was skipped on the device)")
 
 
 def check_device_status(dev=None):
     """Synchronous check of the status word (e.g. after the last backward of a run)."""
     from .models import vloss
     vloss.resolve_pending()
+    resolve_backward_status()
     dev = torch.device("cuda", torch.cuda.current_device()) if dev is None else torch.device(dev)
     if dev in _status:
         status_raise(int(_status[dev][0].item()), dev)
@@ -973,6 +1021,7 @@ class GRUFn(torch.autograd.Function):
                                     nx.ptr(w_hh_r), nx.ptr(saved), nx.ptr(dout), 2 * Hh, nx.ptr(dx), nx.ld(dx),
                                     *[nx.ptr(t) for t in bufs], nx.ptr(ws), nx.ptr(device_status(dev)), GRU_SPIN_MAX,
                                     nx.stream()), "fx_gru_bidir_bwd")
+        _queue_backward_status(dev)
         return (dx, None) + tuple(t[1] for t in tg)
 
 

@@ -123,16 +123,34 @@ LAZY_READBACK = os.environ.get("FX_LAZY_READBACK", "1") != "0"   # 0: resolve in
 
 class LazySave(dict):
     """One video's save dict (``pred``, ``loss``) of a step whose host read-back is still in flight:
-    every read resolves the read-back first (waiting for the device only if it has not finished)."""
-    __slots__ = ("_pending",)
+    every read resolves the read-back first (waiting for the device only if it has not finished).  If
+    the read-back carried a kernel failure, every later read re-raises that error.  Pickling / copying
+    resolves first and yields a plain dict (the reference's Checkpoint pickles these saves)."""
+    __slots__ = ("_pending", "_error")
 
     def __init__(self, pending):
         super().__init__()
         self._pending = pending
+        self._error = None
 
     def _r(self):
         if self._pending is not None:
             self._pending.resolve()
+        if self._error is not None:
+            raise self._error
+
+    def __reduce__(self):
+        self._r()
+        return (dict, (dict(dict.items(self)),))
+
+    def __copy__(self):
+        self._r()
+        return dict(dict.items(self))
+
+    def __deepcopy__(self, memo):
+        import copy
+        self._r()
+        return copy.deepcopy(dict(dict.items(self)), memo)
 
     def __getitem__(self, k):
         self._r()
@@ -199,14 +217,21 @@ class PendingReadback:
         for d in self.saves:
             d._pending = None
         self.ready.synchronize()
-        self.check()
+        try:
+            self.check()
+        except Exception as e:           # every later read of these saves raises it again
+            for d in self.saves:
+                d._error = e
+            raise
         self.fill(self.saves)
 
 
 def resolve_pending():
-    """Resolve every read-back still in flight (called at the start of each forward)."""
+    """Resolve every read-back still in flight (called at the start of each forward), then the
+    status copies taken after earlier backward passes (functional.resolve_backward_status)."""
     while _PENDING:
         _PENDING[0].resolve()
+    fxf.resolve_backward_status()
 
 
 class _LossFn(torch.autograd.Function):

@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FACTMX_LIB", os.path.join(_HERE, "_lib", "libfactmx.so"))
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -168,6 +168,7 @@ SIGNATURES = {
     "fx_grad_norm": (I, [P, L, P, P, P]),
     "fx_clip_grad_scale": (I, [P, L, P, F, P]),
     "fx_adam_step": (I, [P, P, P, P, L, L, F, F, F, F, F, F, P, P, P]),
+    "fx_adam_step_checked": (I, [P, P, P, P, L, L, F, F, F, F, F, F, P, P, P, P]),
     "fx_loss_workspace_floats": (L, []),
     "fx_class_loss_fwd": (I, [P, L, L, I, I, P, P, P, F, F, P, P, P, P]),
     "fx_class_loss_bwd": (I, [P, L, L, I, I, P, P, P, P, F, F, P, P, P]),

@@ -71,10 +71,15 @@ class FusedAdam:
         self.step_count += 1
         mx = float(self.max_grad_norm) if self.max_grad_norm else 0.0
         b1, b2 = self.betas
-        nx.check(lib.fx_adam_step(nx.ptr(self.flat), nx.ptr(self.grad_flat), nx.ptr(self.exp_avg),
-                                  nx.ptr(self.exp_avg_sq), self.flat.numel(), self.step_count, float(self.lr),
-                                  float(b1), float(b2), float(self.eps), float(self.weight_decay), mx,
-                                  nx.ptr(self._ws), nx.ptr(self.total_norm), nx.stream()), "fx_adam_step")
+        # guarded by the device status word: a step whose kernels failed (BiGRU timeout in the backward)
+        # leaves the parameters and moments untouched; the failure is raised by the next status read-back
+        from .functional import device_status
+        nx.check(lib.fx_adam_step_checked(nx.ptr(self.flat), nx.ptr(self.grad_flat), nx.ptr(self.exp_avg),
+                                          nx.ptr(self.exp_avg_sq), self.flat.numel(), self.step_count,
+                                          float(self.lr), float(b1), float(b2), float(self.eps),
+                                          float(self.weight_decay), mx, nx.ptr(self._ws), nx.ptr(self.total_norm),
+                                          nx.ptr(device_status(self.flat.device)), nx.stream()),
+                 "fx_adam_step_checked")
 
     def zero_grad(self, set_to_none=False):
         self.grad_flat.zero_()

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FX_ABI_VERSION 16
+#define FX_ABI_VERSION 17
 
 enum {
   FX_OK = 0,
@@ -541,6 +541,14 @@ int fx_clip_grad_scale(float* g, long long n, const float* workspace, float max_
 int fx_adam_step(float* p, float* g, float* m, float* v, long long n, long long step, float lr,
                  float beta1, float beta2, float eps, float weight_decay, float max_norm,
                  float* workspace, float* norm_out, void* stream);
+/* fx_adam_step_checked: the same, guarded by the device status word `status` (fx_gru_bidir_*'s
+ *   status argument): when status[0] != 0 at the time the update runs -- a kernel of the step failed,
+ *   e.g. a BiGRU backward timed out, so the gradients are invalid -- every block returns without
+ *   touching p, g, m or v (no host synchronisation; the failure is raised on the host by the step's
+ *   next status read-back).  status NULL: unguarded (= fx_adam_step). */
+int fx_adam_step_checked(float* p, float* g, float* m, float* v, long long n, long long step, float lr,
+                         float beta1, float beta2, float eps, float weight_decay, float max_norm,
+                         float* workspace, float* norm_out, const int* status, void* stream);
 
 /* ------------------------------------------------------------------------
  * Fused loss terms (fact_clip/models/loss.py); each returns ONE scalar

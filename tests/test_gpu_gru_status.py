@@ -48,3 +48,51 @@ def test_gru_timeout_raises_at_readback(monkeypatch):
     loss.backward()
     fxf.check_device_status()
     assert torch.isfinite(loss).item()
+
+
+def test_gru_backward_timeout_raises_and_skips_adam(monkeypatch):
+    """A BiGRU timeout in the BACKWARD pass only (the forward ran normally): the status word is copied
+    after the backward's kernels, FusedAdam's update on the invalid gradients is skipped on the device
+    (parameters and moments unchanged), and the failure is raised at the next forward, naming the
+    backward pass; the step after that trains normally."""
+    import paramgen as pg
+    from factmx import functional as fxf
+    from factmx import native as nx
+    from factmx.dp import DataParallel
+    from factmx.models.blocks import FACT_CLIP
+    from factmx.models.loss import MatchCriterion
+    from factmx.optim import FusedAdam
+    fx = load_fixture("tiny_clip_iid")
+    meta = tiny_meta(fx)
+    cfg = cfg_from_meta(meta)
+    feats, label, text = tiny_inputs(meta)
+    net = FACT_CLIP(cfg, meta["D"], meta["C"], text_embeddings=torch.from_numpy(text).float())
+    with torch.no_grad():
+        for n, p in net.named_parameters():
+            p.copy_(torch.from_numpy(pg.param_value(n, p.shape, meta["seed"])))
+    net.mcriterion = MatchCriterion(cfg, meta["C"], [])
+    net = net.to(DEV).train()
+    dp = DataParallel(net)
+    opt = FusedAdam(net.parameters(), lr=1e-3, max_grad_norm=10.0, grad_flat=dp.flat)
+    seqs = [torch.from_numpy(feats).float().to(DEV)] * 2
+    labs = [torch.from_numpy(label).to(DEV)] * 2
+    monkeypatch.setattr(fxf, "GRU_SPIN_MAX", 0)
+    dp.zero_grad()
+    loss, saves = net(seqs, labs, compute_loss=True)
+    saves[0]["pred"]                           # the forward's own read-back: clean
+    monkeypatch.setattr(fxf, "GRU_SPIN_MAX", 1)   # only the backward's GRU gives up
+    loss.backward()
+    w0, m0 = opt.flat.clone(), opt.exp_avg.clone()
+    opt.step()
+    torch.cuda.synchronize()
+    assert torch.equal(opt.flat, w0) and torch.equal(opt.exp_avg, m0), "Adam applied invalid gradients"
+    monkeypatch.setattr(fxf, "GRU_SPIN_MAX", 0)
+    with pytest.raises(nx.FactmxNativeError, match="BACKWARD"):
+        net(seqs, labs, compute_loss=True)
+    dp.zero_grad()
+    loss, _ = net(seqs, labs, compute_loss=True)
+    loss.backward()
+    opt.step()
+    fxf.check_device_status()
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss).item() and not torch.equal(opt.flat, w0)

@@ -2,14 +2,27 @@
 stacked ragged batch: the a2f direction (keys = action tokens: the fused one-launch core of
 x2y_core.hip for <= 64 keys, including two key blocks at 40 keys, and the grouped-GEMM path past 64
 keys), the f2a direction (keys = frames), and the core switched off (FX_X2Y_FUSED=0 equivalent: the
-grouped path) -- out, logit and attn forward, every input / weight gradient backward."""
+grouped path) -- out, logit and attn forward, every input / weight gradient backward, with random
+upstream gradients on all three outputs.  The reference's losses read attn_logit only (blocks.py:372-377,
+491-492; attn feeds the matching and eval, blocks.py:96, 243-281), so X2YFn marks attn non-differentiable;
+the C entry point still takes a dattn (fx_x2y_bwd), and this test reaches it through a subclass whose
+attn output is differentiable, so the cores' dP += dattn paths are checked against the oracle too.  The
+opt-in fused f2a backward core (FX_X2Y_F2A_BWD=1; library knobs are read once per process) runs the f2a
+cases in a child process."""
 import math
+import os
+import subprocess
+import sys
 
 import pytest
 import torch
 
-from factmx import functional as fxf
-from oracle import fact_oracle as fo
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for _p in (_ROOT, os.path.join(_ROOT, "fact-clip_amd")):     # (the child process has no conftest)
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+from factmx import functional as fxf  # noqa: E402
+from oracle import fact_oracle as fo  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -33,6 +46,44 @@ def _params(xdim, ydim, outdim, seed):
                                              ("f2a", 64, (64, 1)), ("f2a", 75, (200, 90)),
                                              ("a2f", 32, (1,)), ("f2a", 7, (3000,))])
 def test_x2y_vs_oracle(direction, nq, Ts):
+    check_x2y(direction, nq, Ts)
+
+
+def test_x2y_f2a_fused_backward_vs_oracle():
+    """The f2a cases again with the fused f2a backward core switched on (child process: the knob is
+    read when the library loads)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, FX_X2Y_F2A_BWD="1")
+    p = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), "f2a"], env=env, cwd=root, timeout=240)
+    assert p.returncode == 0, p.returncode
+
+
+class _X2YAttnGrad(fxf.X2YFn):
+    """X2YFn with a differentiable attn output (test only): backward receives dattn."""
+
+    @staticmethod
+    def forward(ctx, *args):
+        outs = fxf.X2YFn.forward(ctx, *args)
+        ctx.non_differentiable = ()
+        return outs
+
+
+def test_x2y_attn_not_differentiable_in_product():
+    x = torch.randn(5, A, device=DEV, requires_grad=True)
+    y = torch.randn(7, D2, device=DEV, requires_grad=True)
+    P = {n: t.float().to(DEV).requires_grad_(True) for n, t in _params(A, D2, 8, seed=1).items()}
+    _, logit, attn = fxf.X2YFn.apply(x, y, None, None, None, P["X_K.weight"], P["X_K.bias"], P["X_V.weight"],
+                                     P["X_V.bias"], P["Y_Q.weight"], P["Y_Q.bias"], P["Y_W.weight"], P["Y_W.bias"],
+                                     0.0, 0)
+    assert logit.requires_grad and not attn.requires_grad
+
+
+CASES = [("a2f", 32, (700, 413)), ("a2f", 40, (300, 257)), ("a2f", 64, (129, 64)), ("a2f", 75, (300, 200)),
+         ("f2a", 32, (700, 413)), ("f2a", 40, (300, 257, 65)), ("f2a", 64, (64, 1)), ("f2a", 75, (200, 90)),
+         ("a2f", 32, (1,)), ("f2a", 7, (3000,))]
+
+
+def check_x2y(direction, nq, Ts):
     g = torch.Generator().manual_seed(7)
     nv = len(Ts)
     tok = [torch.randn(nq, A, generator=g, dtype=torch.float64).float().double() for _ in Ts]
@@ -53,13 +104,15 @@ def test_x2y_vs_oracle(direction, nq, Ts):
     X, Y, Xp, Yp = cat(Xs), cat(Ys), cat(Xps), cat(Yps)
     W = {n: t.float().to(DEV).requires_grad_(True) for n, t in P.items()}
     rows = (xl, yl) if nv > 1 else None
-    out, logit, attn = fxf.X2YFn.apply(X, Y, Xp, Yp, rows, W["X_K.weight"], W["X_K.bias"], W["X_V.weight"],
+    out, logit, attn = _X2YAttnGrad.apply(X, Y, Xp, Yp, rows, W["X_K.weight"], W["X_K.bias"], W["X_V.weight"],
                                        W["X_V.bias"], W["Y_Q.weight"], W["Y_Q.bias"], W["Y_W.weight"],
                                        W["Y_W.bias"], 0.0, 0)
     gen = torch.Generator().manual_seed(9)
     gout = torch.randn(out.shape, generator=gen, dtype=torch.float64)
     glog = torch.randn(logit.shape, generator=gen, dtype=torch.float64)
-    loss = (out.double() * gout.to(DEV)).sum() + (logit.double() * glog.to(DEV)).sum()
+    gatt = torch.randn(attn.shape, generator=gen, dtype=torch.float64)
+    loss = ((out.double() * gout.to(DEV)).sum() + (logit.double() * glog.to(DEV)).sum() +
+            (attn.double() * gatt.to(DEV)).sum())
     loss.backward()
     torch.cuda.synchronize()
     # oracle per video (fp64), same upstream gradients
@@ -72,7 +125,8 @@ def test_x2y_vs_oracle(direction, nq, Ts):
     for v in range(nv):
         o, lg, at = fo.x2y(Pr, "", Xr[v], Yr[v], Xpr[v], Ypr[v])
         n = lg.numel()
-        total = total + (o * gout[yl[v]:yl[v + 1]]).sum() + (lg.reshape(-1) * glog.reshape(-1)[a0:a0 + n]).sum()
+        total = (total + (o * gout[yl[v]:yl[v + 1]]).sum() + (lg.reshape(-1) * glog.reshape(-1)[a0:a0 + n]).sum() +
+                 (at.reshape(-1) * gatt.reshape(-1)[a0:a0 + n]).sum())
         lo.append(lg.reshape(-1))
         ao.append(at.reshape(-1))
         a0 += n
@@ -95,3 +149,10 @@ def test_x2y_vs_oracle(direction, nq, Ts):
     close(Yp.grad, torch.cat([t.grad for t in Ypr]), 1e-4, "dYpos")
     for n in P:
         close(W[n].grad, Pr[n].grad, 2e-4, n)
+
+
+if __name__ == "__main__":      # child of test_x2y_f2a_fused_backward_vs_oracle: python tests/test_gpu_x2y.py f2a
+    for d, nq, Ts in CASES:
+        if d == sys.argv[1]:
+            check_x2y(d, nq, Ts)
+            print("ok", d, nq, Ts, flush=True)

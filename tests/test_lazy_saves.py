@@ -48,3 +48,29 @@ def test_pending_resolved_by_next_forward_and_failure_raises_once():
         vloss.resolve_pending()
     assert p.done and not vloss._PENDING
     vloss.resolve_pending()          # nothing left: no second raise
+
+
+def test_failed_readback_error_persists_on_every_read():
+    p, _ = _pending(fail=True)
+    with pytest.raises(RuntimeError, match="GRU"):
+        p.saves[0]["pred"]
+    for s in p.saves:                 # later reads name the real failure, not KeyError('pred')
+        with pytest.raises(RuntimeError, match="GRU"):
+            s["pred"]
+        with pytest.raises(RuntimeError, match="GRU"):
+            s.get("loss")
+    vloss.resolve_pending()
+
+
+def test_lazy_save_pickles_and_copies_as_plain_dicts():
+    import copy
+    import pickle
+    p, calls = _pending()
+    s = p.saves[1]
+    out = pickle.loads(pickle.dumps(s))
+    assert type(out) is dict and out == {"pred": [1, 1], "loss": {"loss": 2.5}} and calls["fill"] == 1
+    p2, _ = _pending()
+    d = copy.deepcopy(p2.saves[0])
+    assert type(d) is dict and d["pred"] == [0, 0]
+    assert type(copy.copy(p2.saves[1])) is dict
+    vloss.resolve_pending()

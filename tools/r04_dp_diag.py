@@ -50,8 +50,9 @@ def main():
         dp.finish_gradients()
         fin[0] += time.perf_counter() - t0
 
-    def timed(active, k=20):
+    def timed(active, k=20, thread=False):
         dp.active = active
+        dp.issue_thread = thread
         step()
         torch.cuda.synchronize()
         dp.host_issue_s = 0.0
@@ -65,10 +66,11 @@ def main():
     for _ in range(3):
         step()
     freeze_host_heap()
-    res = {"plain": [], "forced": []}
+    res = {"plain": [], "forced": [], "forced_thread": []}
     for _ in range(4):
         res["plain"].append(timed(False))
         res["forced"].append(timed(True))
+        res["forced_thread"].append(timed(True, thread=True))
     for k, v in res.items():
         print(k, "ms/step, host issue ms/step, finish ms/step:", [tuple(round(x, 3) for x in t) for t in v])
         print("  median step", round(statistics.median(t[0] for t in v), 3))
