@@ -41,6 +41,13 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
 
+// tanh through one exp (the recurrence's critical path; tanhf's range reduction is several times
+// longer): tanh|x| = (1 - e) / (1 + e), e = exp(-2|x|) in (0, 1]; absolute error a few ulp of 1
+__device__ __forceinline__ float tanh_fast(float x) {
+  const float e = __expf(-2.f * fabsf(x));
+  return copysignf((1.f - e) / (1.f + e), x);
+}
+
 __device__ __forceinline__ void put_granule(unsigned long long* g, unsigned epoch, float v) {
   __hip_atomic_store((gu64*)g, ((unsigned long long)epoch << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
@@ -110,27 +117,33 @@ __global__ __launch_bounds__(GT) void gru_fwd_kernel(GruArgs args) {
   const int r0 = args.off[sq], S = args.off[sq + 1] - r0;
   unsigned long long* gran = args.gran + (long long)(sq * 2 + dir) * 2 * Hh;
   const int U = (Hh + NW - 1) / NW, u0 = j * U;
-  __shared__ float h[256];
-  __shared__ float gh[3 * MAXU];
+  // Wave wv owns k-chunk wv of the recurrent product: it gathers units [64 wv, 64 wv + 64) of the new
+  // state (the other workgroups' granules, and this one's) and multiplies them into its lanes' rows
+  // (lane o = row o of the workgroup's 3U gate rows) without waiting for the other waves; ONE barrier
+  // per step then joins the four partial sums for the gate threads.  h and the partials are double-
+  // buffered by step parity (a wave may run one step ahead of the gate threads, never two: reaching
+  // step s + 2 takes step s + 1's barrier).
+  __shared__ float h[2][256];
+  __shared__ float part[2][4][64];
   __shared__ int dead;
   if (tid == 0) dead = 0;
-  // this thread's slice of W_hh: row o of the workgroup's 3U rows, k-chunk c
-  const int o = tid >> 2, c = tid & 3;
+  const int wv = tid >> 6;
+  const int o = lane;
   const int g = o / U, ui = o - g * U, unit = u0 + ui;
   const bool act = o < 3 * U && unit < Hh;
   const int row = g * Hh + unit;
   float w[KCH];
 #pragma unroll
   for (int i = 0; i < KCH; ++i) {
-    const int k = c * KCH + i;
+    const int k = wv * KCH + i;
     w[i] = (act && k < Hh) ? a.whh[(long long)row * Hh + k] : 0.f;
   }
-  const float bias = act ? a.bhh[row] : 0.f;
-  for (int k = tid; k < 256; k += GT) h[k] = 0.f;
-  // the input projections of step s are loaded during step s-1 (their latency hides behind the
-  // exchange instead of opening every step)
+  for (int k = tid; k < 512; k += GT) (&h[0][0])[k] = 0.f;
+  // the gate threads (wave 0, lanes < U): their three b_hh entries, and the input projections of step s
+  // loaded during step s-1 (their latency hides behind the exchange instead of opening every step)
   const bool own = tid < U && u0 + tid < Hh;
   const int uo = u0 + (own ? tid : 0);
+  const float br = own ? a.bhh[uo] : 0.f, bz = own ? a.bhh[Hh + uo] : 0.f, bn = own ? a.bhh[2 * Hh + uo] : 0.f;
   float pr = 0.f, pz = 0.f, pn = 0.f;
   if (own && S > 0) {
     const float* gg = a.gi + (long long)(r0 + (a.reverse ? S - 1 : 0)) * a.ldgi;
@@ -138,16 +151,31 @@ __global__ __launch_bounds__(GT) void gru_fwd_kernel(GruArgs args) {
     pz = gg[Hh + uo];
     pn = gg[2 * Hh + uo];
   }
+  const int kc0 = wv * KCH, kcn = max(0, min(KCH, Hh - kc0));   // this wave's chunk of the state
   __syncthreads();
   for (int s = 0; s < S; ++s) {
     const int t = r0 + (a.reverse ? S - 1 - s : s);
-    float acc = 0.f;
+    float* hc = h[s & 1];
+    if (s > 0 && kcn > 0) {   // the state after step s-1: granules of epoch s in slot (s-1) & 1
+      if (!gather_granules(gran + (long long)((s - 1) & 1) * Hh + kc0, kcn, (unsigned)s, hc + kc0, args.tmo,
+                           args.spin_max, lane))
+        dead = 1;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS writes land before its reads
+    }
+    // four independent FMA chains over the wave's 64-deep chunk (broadcast LDS reads)
+    float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
+    const float4* hv = reinterpret_cast<const float4*>(hc + kc0);
 #pragma unroll
-    for (int i = 0; i < KCH; ++i) acc = fmaf(w[i], h[c * KCH + i], acc);
-    acc += __shfl_xor(acc, 1, 64);
-    acc += __shfl_xor(acc, 2, 64);
-    if (act && c == 0) gh[o] = acc + bias;
+    for (int i = 0; i < KCH / 4; ++i) {
+      const float4 x = hv[i];
+      c0 = fmaf(w[4 * i], x.x, c0);
+      c1 = fmaf(w[4 * i + 1], x.y, c1);
+      c2 = fmaf(w[4 * i + 2], x.z, c2);
+      c3 = fmaf(w[4 * i + 3], x.w, c3);
+    }
+    part[s & 1][wv][o] = (c0 + c1) + (c2 + c3);
     __syncthreads();
+    if (dead) break;
     if (own) {
       const int u = uo;
       const float gr = pr, gz = pz, gn = pn;
@@ -157,30 +185,24 @@ __global__ __launch_bounds__(GT) void gru_fwd_kernel(GruArgs args) {
         pz = gg[Hh + u];
         pn = gg[2 * Hh + u];
       }
-      const float r = sigm(gr + gh[tid]);
-      const float z = sigm(gz + gh[U + tid]);
-      const float n = tanhf(gn + r * gh[2 * U + tid]);
-      const float hp = h[u];
+      const float (*pp)[64] = part[s & 1];
+      const float ghr = (pp[0][tid] + pp[1][tid]) + (pp[2][tid] + pp[3][tid]) + br;
+      const float ghz = (pp[0][U + tid] + pp[1][U + tid]) + (pp[2][U + tid] + pp[3][U + tid]) + bz;
+      const float ghn = (pp[0][2 * U + tid] + pp[1][2 * U + tid]) + (pp[2][2 * U + tid] + pp[3][2 * U + tid]) + bn;
+      const float r = sigm(gr + ghr);
+      const float z = sigm(gz + ghz);
+      const float n = tanh_fast(gn + r * ghn);
+      const float hp = hc[u];
       const float hn = (1.f - z) * n + z * hp;
+      if (s + 1 < S) put_granule(gran + (long long)(s & 1) * Hh + u, (unsigned)(s + 1), hn);
       a.out[(long long)t * a.ldo + u] = hn;
       a.hprev[(long long)t * Hh + u] = hp;
       float* gs = a.gates + (long long)t * 4 * Hh;
       gs[u] = r;
       gs[Hh + u] = z;
       gs[2 * Hh + u] = n;
-      gs[3 * Hh + u] = gh[2 * U + tid];
-      put_granule(gran + (long long)(s & 1) * Hh + u, (unsigned)(s + 1), hn);
+      gs[3 * Hh + u] = ghn;
     }
-    __syncthreads();   // every wave is done with the old h
-    if (s + 1 < S) {   // the 4 waves gather a quarter of h each (one round trip instead of several)
-      const int q = (Hh + 4 * 64 - 1) / (4 * 64) * 64, b0 = (tid >> 6) * q;
-      if (b0 < Hh &&
-          !gather_granules(gran + (long long)(s & 1) * Hh + b0, min(q, Hh - b0), (unsigned)(s + 1), h + b0, args.tmo,
-                           args.spin_max, lane))
-        dead = 1;
-    }
-    __syncthreads();
-    if (dead) break;
   }
 }
 
@@ -204,28 +226,38 @@ struct GruBwdArgs {
   int off[MAXSEQ + 1];
 };
 
+// Backward recurrence, row-partitioned like the forward: workgroup j keeps W_hh's rows of its own U
+// units (3U rows x Hh, thread k = column k) and turns its units' gate gradients dgh (3U values) into a
+// partial dh_rec over ALL Hh units, p_j[k] = sum_{its rows r} W[r][k] dgh[r]; each unit's owner then
+// sums the NW partials in source order (deterministic).  Per step a workgroup sends U granules to
+// every workgroup and gathers NW x U = Hh of its own -- one granule per lane, the forward's exchange --
+// instead of gathering all 3Hh gate gradients (3 per lane).  Granule block of destination d, source j:
+// slot + (d * NW + j) * U.
 __global__ __launch_bounds__(GT) void gru_bwd_kernel(GruBwdArgs args) {
   const int sq = blockIdx.x / (2 * NW), rem = blockIdx.x - sq * 2 * NW;
   const int dir = rem / NW, j = rem - dir * NW;
   const GruBwdDirArgs& a = args.d[dir];
   const int Hh = a.Hh, H3 = 3 * Hh, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r0 = args.off[sq], S = args.off[sq + 1] - r0;
-  unsigned long long* gran = args.gran + (long long)(sq * 2 + dir) * 2 * H3;
-  const int U = (Hh + NW - 1) / NW, u0 = j * U;
-  __shared__ float dg[768];
+  const int U = (Hh + NW - 1) / NW, u0 = j * U, NG = NW * U;   // NG granules per destination block
+  unsigned long long* gran = args.gran + (long long)(sq * 2 + dir) * 2 * NW * NG;
+  __shared__ float dgo[3 * MAXU];       // this workgroup's gate gradients of the step (r, z, n*r rows)
+  __shared__ float red[NW * MAXU];      // gathered partials: red[src * U + ui]
   __shared__ float dh[MAXU], dhd[MAXU];
-  __shared__ float part[4][MAXU];
   __shared__ int dead;
   if (tid == 0) dead = 0;
-  // this thread's slice of W_hh^T: unit i of the workgroup, gate rows [c*RCH, c*RCH + RCH)
-  const int i = tid & 15, c = tid >> 4;
-  const bool act = i < U && u0 + i < Hh;
-  float w[RCH];
+  // thread k: column k of the workgroup's 3U rows (row g * Hh + u0 + ui at index g * U + ui)
+  const int k = tid;
+  const bool kact = k < Hh;
+  float w[3 * MAXU];
 #pragma unroll
-  for (int r = 0; r < RCH; ++r) {
-    const int row = c * RCH + r;
-    w[r] = (act && row < H3) ? a.whh[(long long)row * Hh + u0 + i] : 0.f;
+  for (int q = 0; q < 3 * MAXU; ++q) {
+    const int g = q / MAXU, ui = q - g * MAXU;
+    w[q] = (kact && ui < U && u0 + ui < Hh) ? a.whh[(long long)(g * Hh + u0 + ui) * Hh + k] : 0.f;
   }
+  // every k < NW * U puts (zero past Hh), so each workgroup's block is complete whatever Hh % U
+  const bool kput = k < NG;
+  const int kd = kput ? k / U : 0, kl = kput ? k - kd * U : 0;   // owner workgroup of unit k, its index there
   if (tid < MAXU) dh[tid] = 0.f;
   // step s's saved gates, h_{t-1} and output gradient are loaded during step s-1
   const bool own = tid < U && u0 + tid < Hh;
@@ -241,10 +273,11 @@ __global__ __launch_bounds__(GT) void gru_bwd_kernel(GruBwdArgs args) {
     nd = a.dout[(long long)t * a.lddo + uo];
   };
   if (own && S > 0) fetch(r0 + (a.reverse ? 0 : S - 1));
+  if (tid < 3 * MAXU) dgo[tid] = 0.f;
   __syncthreads();
   for (int s = 0; s < S; ++s) {
     const int t = r0 + (a.reverse ? s : S - 1 - s);   // reverse of the forward visiting order
-    unsigned long long* slot = gran + (long long)(s & 1) * H3;
+    unsigned long long* slot = gran + (long long)(s & 1) * NW * NG;
     if (own) {
       const int u = uo;
       const float r = nr, z = nz, n = nn, ghn = ng, hp = nh, dcur = nd;
@@ -253,6 +286,9 @@ __global__ __launch_bounds__(GT) void gru_bwd_kernel(GruBwdArgs args) {
       const float dnp = d * (1.f - z) * (1.f - n * n);
       const float dzp = d * (hp - n) * z * (1.f - z);
       const float drp = dnp * ghn * r * (1.f - r);
+      dgo[tid] = drp;
+      dgo[U + tid] = dzp;
+      dgo[2 * U + tid] = dnp * r;
       float* gi = a.dgi + (long long)t * a.lddgi;
       gi[u] = drp;
       gi[Hh + u] = dzp;
@@ -261,40 +297,49 @@ __global__ __launch_bounds__(GT) void gru_bwd_kernel(GruBwdArgs args) {
       gg[u] = drp;
       gg[Hh + u] = dzp;
       gg[2 * Hh + u] = dnp * r;
-      put_granule(slot + u, (unsigned)(s + 1), drp);
-      put_granule(slot + Hh + u, (unsigned)(s + 1), dzp);
-      put_granule(slot + 2 * Hh + u, (unsigned)(s + 1), dnp * r);
-      dhd[tid] = d * z;   // direct path; W^T dgh added below
+      dhd[tid] = d * z;   // direct path; the NW partials of W^T dgh are added below
     }
     if (s + 1 == S) break;   // the last step's recurrent gradient feeds nothing
-    {   // the 4 waves gather a quarter of the 3Hh gate gradients each
-      const int q = (H3 + 4 * 64 - 1) / (4 * 64) * 64, b0 = wv * q;
-      if (b0 < H3 && !gather_granules(slot + b0, min(q, H3 - b0), (unsigned)(s + 1), dg + b0, args.tmo, args.spin_max,
-                                           lane))
+    __syncthreads();         // dgo of this step visible to every column thread
+    if (kput) {
+      // p_j[k] over the 3U rows (four independent chains; rows past the real units have zero weights)
+      float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
+#pragma unroll
+      for (int q = 0; q < 3 * MAXU; q += 4) {
+        const int g0 = q / MAXU, i0 = q - g0 * MAXU;   // dgo index g * U + ui
+        c0 = fmaf(w[q], dgo[g0 * U + min(i0, U - 1)], c0);
+        c1 = fmaf(w[q + 1], dgo[g0 * U + min(i0 + 1, U - 1)], c1);
+        c2 = fmaf(w[q + 2], dgo[g0 * U + min(i0 + 2, U - 1)], c2);
+        c3 = fmaf(w[q + 3], dgo[g0 * U + min(i0 + 3, U - 1)], c3);
+      }
+      put_granule(slot + (long long)(kd * NW + j) * U + kl, (unsigned)(s + 1), (c0 + c1) + (c2 + c3));
+    }
+    {   // this workgroup's destination block: NW sources x U units, one granule per lane
+      const int b0 = wv * 64;
+      if (b0 < NG && !gather_granules(slot + (long long)j * NG + b0, min(64, NG - b0), (unsigned)(s + 1), red + b0,
+                                      args.tmo, args.spin_max, lane))
         dead = 1;
     }
     __syncthreads();
     if (dead) break;
-    float acc = 0.f;
-#pragma unroll
-    for (int r = 0; r < RCH; ++r) {
-      const int row = c * RCH + r;
-      acc = fmaf(w[r], row < H3 ? dg[row] : 0.f, acc);
+    if (own) {   // sources in order (deterministic); dh[tid] / dhd[tid] are this thread's own
+      float acc = 0.f;
+      for (int src = 0; src < NW; ++src) acc += red[src * U + tid];
+      dh[tid] = dhd[tid] + acc;
     }
-    acc += __shfl_xor(acc, 16, 64);
-    acc += __shfl_xor(acc, 32, 64);
-    if (lane < 16) part[wv][lane] = acc;
-    __syncthreads();
-    if (tid < U) dh[tid] = dhd[tid] + (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
-    __syncthreads();
   }
 }
 
 }  // namespace
 
 // floats of the per-call sync area for nseq sequences: timeout word (padded to 16 B) +
-// per sequence 2 dirs x 2 slots x 3Hh granules (8 B each)
-long long gru_sync_floats(int Hh, int nseq) { return 4 + (long long)std::max(nseq, 1) * 2 * 2 * 3 * Hh * 2; }
+// per sequence 2 dirs x 2 slots x max(3Hh, NW * NW * U) granules (8 B each: the forward uses Hh of them,
+// the backward NW x NW x U)
+long long gru_sync_floats(int Hh, int nseq) {
+  const long long U = (Hh + NW - 1) / NW;
+  const long long per = std::max<long long>(3LL * Hh, (long long)NW * NW * U);   // granules per slot
+  return 4 + (long long)std::max(nseq, 1) * 2 * 2 * per * 2;
+}
 
 int launch_gru_fwd(const float* gi, long long ldgi, int nseq, const int* seq_off, int Hh, const float* const whh[2],
                    const float* const bhh[2], float* out, long long ldo, float* saved, float* ws, unsigned* status,
@@ -346,7 +391,7 @@ int launch_gru_bwd(const float* dout, long long lddo, int nseq, const int* seq_o
     GruBwdArgs args{};
     args.tmo = status ? status : tmo;
     args.spin_max = spin_max > 0 ? (unsigned)spin_max : SPIN_MAX;
-    args.gran = gran + (long long)c0 * 2 * 2 * H3;
+    args.gran = gran + (long long)c0 * 2 * 2 * NW * NW * ((Hh + NW - 1) / NW);
     for (int q = 0; q <= nc; ++q) args.off[q] = seq_off[c0 + q];
     for (int d = 0; d < 2; ++d) {
       GruBwdDirArgs& a = args.d[d];

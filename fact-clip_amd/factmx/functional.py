@@ -521,10 +521,12 @@ class X2YFn(torch.autograd.Function):
         ctx.rows = rows
         ctx.has_pos = (Xpos is not None, Ypos is not None)
         ctx.save_for_backward(X, Y, wk, bk, wv, bv, wq, bq, wy, by, attn, saved)
-        ctx.mark_non_differentiable(attn)
         ctx.set_materialize_grads(False)   # unused logit / attn gradients arrive as None (no zero fill)
         if rows is None:
-            return out, logit.view(Ny, Nx), attn.view(Ny, Nx)
+            logit, attn = logit.view(Ny, Nx), attn.view(Ny, Nx)
+        # the reference differentiates attn_logit only (its losses, blocks.py:372-377); attn feeds the
+        # matching and eval (blocks.py:96, 243-281)
+        ctx.mark_non_differentiable(attn)
         return out, logit, attn
 
     @staticmethod
