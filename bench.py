@@ -51,6 +51,13 @@ SPLIT_PRODUCTS = 6               # FX_PREC_F32S: bf16 piece products per fp32 pr
 SPLIT_KERNEL = "gemm_split_wide8_kernel<1, 0, 3>"
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 HOLDOUT = [51, 53, 61, 67, 56]   # havid_view0_lh_pt_holdout.yaml
+# fx_prof kinds of the X2Y attention cores (capi.cpp fx_x2y_fwd / fx_x2y_bwd); algorithmic bytes per call:
+# query, key and value rows, the logit / probability tiles and the attended features (+ their gradients)
+X2Y_KINDS = {3: "x2y_a2f_fwd", 4: "x2y_a2f_bwd", 5: "x2y_f2a_fwd", 6: "x2y_f2a_bwd"}
+X2Y_NOTES = {"x2y_a2f_fwd": "x2y_a2f_kernel<0> (frames attend to the action tokens: logit, attn, feat in one launch)",
+             "x2y_a2f_bwd": "x2y_a2f_kernel<1> + grouped dxv / dxk GEMM launch",
+             "x2y_f2a_fwd": "x2y_f2a_chunk_kernel + x2y_f2a_merge_kernel (tokens attend to the frames)",
+             "x2y_f2a_bwd": "f2a backward: grouped dP / dxv GEMMs, softmax backward, grouped dyq / dxk GEMMs"}
 D_IN, NCLS, NTOKEN, T_DEFAULT = 2048, 75, 32, 4096
 BF_NCLS, BF_NTOKEN, BF_T = 48, 60, 512   # breakfast.yaml (FACT.ntoken 60, 48 classes)
 
@@ -469,6 +476,8 @@ def main():
     native.check(lib.fx_prof_enable(0, max_ev), "fx_prof_enable")
     for kind in (1, 2):       # attention over T, forward and backward (one launch per SCA decoder layer)
         native.check(lib.fx_prof_enable(kind, psteps * 16 + 64), "fx_prof_enable")
+    for kind in X2Y_KINDS:    # the frame<->action X2Y cores (one call per X2Y map of every update block)
+        native.check(lib.fx_prof_enable(kind, psteps * 8 + 16), "fx_prof_enable")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -481,6 +490,7 @@ def main():
     elapsed = time.perf_counter() - t0
     ms, fl, by, cnt = prof_collect(lib, 0)
     attn_prof = {name: prof_collect(lib, kind) for kind, name in ((1, "fwd"), (2, "bwd"))}
+    x2y_prof = {name: prof_collect(lib, kind) for kind, name in X2Y_KINDS.items()}
     lib.fx_prof_disable()
     S_after = video_segments(net)
     if world > 1:
@@ -565,6 +575,9 @@ def main():
         for name, r in roofline_attention.items():
             if r is not None and default_shape:   # PMC bytes of the main kernel (the merge launch excluded)
                 r["traffic"] = traffic_from_profiles(f"tattn_{name}_kernel", f"r03_pmc_tattn_{name}.json")
+        for name, v in x2y_prof.items():      # the X2Y_map cores (basic.py:373-380), when they ran fused
+            if v[3].value > 0:
+                roofline_attention[name] = attention_roofline(X2Y_NOTES[name], *v)
         line = dict(metric=metric, value=round(value, 1), unit="frames/s", n_gpus=world, steps=args.steps,
                     warmup=args.warmup, ms_per_step=round(1e3 * elapsed / args.steps, 3), higher_is_better=True,
                     scaling="weak", vs_baseline=None, dtype="fp32", data="synthetic",

@@ -29,7 +29,7 @@ struct ProfState {
   std::vector<double> flops, bytes;
   int used = 0;
 };
-constexpr int kProfKinds = 4;
+constexpr int kProfKinds = 8;   // 0 conv GEMM, 1 / 2 attention over T fwd / bwd, 3-6 X2Y cores
 std::mutex g_prof_mu;
 ProfState g_prof[kProfKinds];
 
@@ -288,7 +288,8 @@ struct MstcnLayout {
   // saved
   long long h, z, xh, rs, wbs, wpts, total_saved;
   // workspace
-  long long wf, wb, wpt, buf0, buf1, buf2, buf3, buf4, buf5, split, split2, colsum, dzall, dhall, csb, bsl, total_ws;
+  long long wf, wb, wpt, wk1, wk2, buf0, buf1, buf2, buf3, buf4, buf5, split, split2, colsum, dzall, dhall, csb, bsl,
+      total_ws;
 };
 
 // Split of the deferred batched weight-gradient GEMMs (fx_mstcn_bwd): each workgroup of a batched
@@ -315,7 +316,9 @@ MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
   L.wf = 0;
   L.wb = L.wf + NL * wsz;
   L.wpt = L.wb + NL * wsz;                   // transposed 1x1 weights (fused backward chain)
-  L.buf0 = L.wpt + NL * F * F;
+  L.wk1 = L.wpt + NL * F * F;                // fused layers: conv weights in MFMA fragment order
+  L.wk2 = L.wk1 + (p->fused_layers ? NL * wsz : 0);   // ... and the 1x1 weights
+  L.buf0 = L.wk2 + (p->fused_layers ? NL * F * F : 0);
   L.buf1 = L.buf0 + L.rowsF;
   L.buf2 = L.buf1 + L.rowsF;
   L.buf3 = L.buf2 + L.rowsF;                 // backward: third dH buffer, second dZ buffer (side stream)
@@ -360,6 +363,28 @@ int pack_conv_weights(const fx_mstcn_params* p, float* ws, float* wbdst, float* 
   }
   hipLaunchKernelGGL(pack_conv_kernel, dim3(cdiv(p->F, 32), cdiv(p->F, 32), p->num_layers), dim3(256), 0, s, a);
   FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+// the fused layer kernel's weights: every layer's conv matrix (ld 3F) and 1x1 matrix (ld F) in fragment
+// order; src2[i] may be a per-layer pointer list (the 1x1 weights) or a base with a uniform stride
+int pack_frag_layers(int NL, int F, const float* w1, long long w1_stride, const float* const* w2list,
+                     const float* w2, long long w2_stride, float* dst1, float* dst2, hipStream_t s) {
+  for (int l0 = 0; l0 < NL; l0 += 32) {
+    const int n = std::min(32, NL - l0);
+    const float* s1[32];
+    const float* s2[32];
+    float* d1[32];
+    float* d2[32];
+    for (int i = 0; i < n; ++i) {
+      s1[i] = w1 + (long long)(l0 + i) * w1_stride;
+      s2[i] = w2list ? w2list[l0 + i] : w2 + (long long)(l0 + i) * w2_stride;
+      d1[i] = dst1 + (long long)(l0 + i) * frl_packed_floats(3 * F);
+      d2[i] = dst2 + (long long)(l0 + i) * frl_packed_floats(F);
+    }
+    FX_TRY(launch_pack_frag(s1, d1, n, 3 * F, 3 * F, s));
+    FX_TRY(launch_pack_frag(s2, d2, n, F, F, s));
+  }
   return FX_OK;
 }
 
@@ -462,6 +487,7 @@ const Knobs& knobs() {
     if (const char* p = env("FX_DEFER_SPLIT")) k.defer_split = std::max(1, std::min(16, std::atoi(p)));
     if (const char* p = env("FX_MSTCN_DEFER")) k.mstcn_defer = p[0] != '0';
     if (const char* p = env("FX_SIDE_MAXWG")) k.side_maxwg = std::max(0, std::atoi(p));
+    if (const char* p = env("FX_GEMM_ROWPERM")) k.gemm_row_perm = p[0] != '0';
     if (const char* p = env("FX_X2Y_FUSED")) k.x2y_fused = p[0] != '0';
     if (const char* p = env("FX_SPLIT_VARIANT")) k.split_variant = std::atoi(p);
     if (const char* p = env("FX_MSTCN_TAIL")) k.mstcn_tail = p[0] != '0';
@@ -570,16 +596,21 @@ int fx_mstcn_fwd(const fx_mstcn_params* p, const float* x, long long ldx, int T,
     FX_CHECK_HIP(hipMemcpy2DAsync(h0, F * sizeof(float), x, ldx * sizeof(float), F * sizeof(float), rows,
                                   hipMemcpyDeviceToDevice, s));
   }
-  const bool fused = p->fused_layers && !p->layernorm && !q.off && frl_supported(F, saved, F, F);
+  const bool fused = p->fused_layers && !p->layernorm && frl_supported(F, saved, F, F) &&
+                     (!q.off || q.nvid <= 16);
+  if (fused && p->num_layers > 0)
+    FX_TRY(pack_frag_layers(p->num_layers, F, workspace + L.wf, 3LL * F * F, p->w_pw, nullptr, 0, workspace + L.wk1,
+                            workspace + L.wk2, s));
   for (int i = 0; i < p->num_layers; ++i) {
     const float* hi = saved + L.h + i * L.rowsF;
     float* hn = saved + L.h + (i + 1) * L.rowsF;
     float* zi = saved + L.z + i * L.rowsF;
     if (fused) {   // z = relu(conv(h) + b); h' = h + dropout(z . Wpw^T + b): one kernel (mstcn_fused.hip)
       prof_begin(0, s);
-      FX_TRY(launch_frl(hi, F, rows, T, layer_dilation(p, i), 1, workspace + L.wf + (long long)i * 3 * F * F,
-                        p->b_dil[i], 1, nullptr, 0, zi, F, p->w_pw[i], p->b_pw[i], hi, F, nullptr, 0, hn, F,
-                        p->dropout, fx_drop_subseed(p->seed, i), s));
+      FX_TRY(launch_frl(hi, F, rows, T, layer_dilation(p, i), 1, q.off, q.nvid,
+                        workspace + L.wk1 + (long long)i * 3 * F * F, p->b_dil[i], 1, nullptr, 0, zi, F,
+                        workspace + L.wk2 + (long long)i * F * F, p->b_pw[i], hi, F, nullptr, 0, hn, F, p->dropout,
+                        fx_drop_subseed(p->seed, i), s));
       prof_end(0, s, 2.0 * rows * F * 4.0 * F, 4.0 * (3.0 * rows * F + 4.0 * F * F));
       continue;
     }
@@ -622,11 +653,15 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   FX_REQUIRE(p->dropout >= 0.f && p->dropout < 1.f, "mstcn: dropout must be in [0, 1)");
   const bool drop = p->dropout > 0.f;
   // Fused chain (no LayerNorm, no dropout, uniform videos, FX_MSTCN_FUSED=1): see below
-  const bool fchain =
-      p->fused_layers && !p->layernorm && !drop && !q.off && NL > 0 && frl_supported(F, ws + L.buf0, F, F);
+  const bool fchain = p->fused_layers && !p->layernorm && !drop && NL > 0 && frl_supported(F, ws + L.buf0, F, F) &&
+                      (!q.off || q.nvid <= 16);
   // the dX-packed conv weights come from the forward (saved); the fused chain also needs the
-  // transposed 1x1 weights (repacked here, into the workspace)
-  if (fchain) FX_TRY(pack_conv_weights(p, ws, ws + L.wb, ws + L.wpt, L, s));
+  // transposed 1x1 weights (repacked here, into the workspace), both then in fragment order
+  if (fchain) {
+    FX_TRY(pack_conv_weights(p, ws, ws + L.wb, ws + L.wpt, L, s));
+    FX_TRY(pack_frag_layers(NL, F, ws + L.wb, 3LL * F * F, nullptr, ws + L.wpt, (long long)F * F, ws + L.wk1,
+                            ws + L.wk2, s));
+  }
   const float* wbp = fchain ? ws + L.wb : saved + L.wbs;
   float* spl = ws + L.split;     // split-K partials of the weight-gradient GEMMs (side stream)
   float* spm = ws + L.split2;    // ... of the main stream's GEMMs / LN backward
@@ -728,9 +763,9 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
       float* dZn = Zb[(NL - i) % 3];
       const float* zn = saved + L.z + (i - 1) * L.rowsF;
       prof_begin(0, s);
-      FX_TRY(launch_frl(dZi, F, rows, T, layer_dilation(p, i), -1, ws + L.wb + (long long)i * 3 * F * F, nullptr, 0,
-                        gU, F, dHi, F, ws + L.wpt + (long long)(i - 1) * F * F, nullptr, nullptr, 0, zn, F, dZn, F,
-                        0.f, 0, s));
+      FX_TRY(launch_frl(dZi, F, rows, T, layer_dilation(p, i), -1, q.off, q.nvid,
+                        ws + L.wk1 + (long long)i * 3 * F * F, nullptr, 0, gU, F, dHi, F,
+                        ws + L.wk2 + (long long)(i - 1) * F * F, nullptr, nullptr, 0, zn, F, dZn, F, 0.f, 0, s));
       prof_end(0, s, 2.0 * rows * F * 4.0 * F, 4.0 * (4.0 * rows * F + 4.0 * F * F));
       FX_TRY(fork(1));
       FX_TRY(linear_dwdb(dHi, F, zn, F, rows, F, F, g->w_pw[i - 1], g->b_pw[i - 1], 1, spl, sd));
@@ -1552,14 +1587,22 @@ int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpo
   // a short key side (the a2f map: <= 64 action tokens per video): the whole core in one launch
   const bool al16 =
       ((reinterpret_cast<uintptr_t>(yq) | reinterpret_cast<uintptr_t>(xk) | reinterpret_cast<uintptr_t>(xv)) & 15) == 0;
+  // algorithmic bytes of the attention core (bench roofline_attention): the query / key / value rows, the
+  // logit and probability tiles, the attended features
+  const double na = (double)V.a[V.n];
+  const double core_bytes = 4.0 * ((double)Ny * Hd + 2.0 * Nx * Hd + 2.0 * na + (double)Ny * Hd);
   if (knobs().x2y_fused && x2y_a2f_fusable(V.n, V.x.data(), Hd) && al16) {
+    prof_begin(3, s);
     FX_TRY(launch_x2y_a2f_fwd(yq, xk, xv, Hd, scale, V.n, V.y.data(), V.x.data(), V.a.data(), logit, attn, feat, s));
+    prof_end(3, s, 4.0 * na * Hd, core_bytes);
   } else if (knobs().x2y_fused && x2y_f2a_fusable(V.n, V.x.data(), V.y.data(), Hd) && al16) {
     // the f2a map (frames -> tokens): per-chunk partials after every other region of the workspace
     float* f2a_ws = workspace + x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, V) + (long long)Ny * (ydim + Hd) +
                     x2y_side_ws(Nx, xdim, Ny, ydim, Hd, outdim);
+    prof_begin(5, s);
     FX_TRY(launch_x2y_f2a_fwd(yq, xk, xv, Hd, scale, V.n, V.y.data(), V.x.data(), V.a.data(), logit, attn, feat,
                               f2a_ws, s));
+    prof_end(5, s, 4.0 * na * Hd, core_bytes);
   } else
   // per video: logits = scale yq . xk^T, attn = softmax(logits), feat = attn . xv  (the GEMMs of up to
   // two videos in one grouped launch each)
@@ -1653,6 +1696,13 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
   const bool al16 = ((reinterpret_cast<uintptr_t>(xk) | reinterpret_cast<uintptr_t>(xv) |
                       reinterpret_cast<uintptr_t>(yq) | reinterpret_cast<uintptr_t>(dcat + ydim)) & 15) == 0;
   const bool fused = knobs().x2y_fused && x2y_a2f_fusable(V.n, V.x.data(), Hd) && (cw & 3) == 0 && al16;
+  // algorithmic bytes of the backward core: dfeat, xv, xk, yq, attn (+ dattn / dlogit in), dlogit, dxv,
+  // dxk, dyq out
+  const double na = (double)V.a[V.n];
+  const double core_bytes = 4.0 * (2.0 * Ny * Hd + 4.0 * Nx * Hd + 4.0 * na + (double)Ny * Hd);
+  const bool f2a_shape = x2y_f2a_fusable(V.n, V.x.data(), V.y.data(), Hd);
+  if (fused) prof_begin(4, s);
+  else if (f2a_shape) prof_begin(6, s);
   if (fused) {
     FX_TRY(launch_x2y_a2f_bwd(dcat + ydim, cw, xv, xk, attn, dattn, dlogit, Hd, scale, V.n, V.y.data(), V.x.data(),
                               V.a.data(), dL, dyq, s));
@@ -1729,6 +1779,8 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
     }
     FX_TRY(launch_gemm_group(g2, n2, s));
   }
+  if (fused) prof_end(4, s, 8.0 * na * Hd, core_bytes);
+  else if (f2a_shape) prof_end(6, s, 8.0 * na * Hd, core_bytes);
   // weight gradients (Y_W; projections X_K, X_V, Y_Q): nothing below needs them -> side stream, each
   // frame-level GEMM split defer_split(rows) ways into its own slab region
   {

@@ -125,6 +125,7 @@ struct Knobs {
   int gemm_stagger = 1;
   bool gemm_xcd_planes = true;
   bool gemm_nt_store = false;
+  bool gemm_row_perm = true;  // FX_GEMM_ROWPERM=0: dilated-conv row tiles in plain order on the XCDs (A/B)
   FILE* gemm_log = nullptr; // FX_GEMM_LOG=<file>: one line per GEMM launch (shape census)
   bool gemm_group = true;
   bool side_stream = true;

@@ -74,6 +74,7 @@ struct GemmDev {
   long long c_last_bs;  // c_last of batch b at c_last + b * c_last_bs
   int b_dil_growth;     // > 1: B's conv dilation of batch b is conv_dil * growth^b
   int xcd_planes;       // wide8: whole z-planes (batch x split-K slice) per XCD, see block_tile
+  int row_perm;         // > 1: dilated-conv A shifting by row_perm row tiles: XCD runs follow the taps, see block_tile
   int a_dil_b1;         // > 0: A's conv dilation of batch 1 (two dilated convs of one input in one launch)
   long long bias_bs;    // bias of batch b at bias + b * bias_bs
   int nt_store;         // FX_GEMM_NTSTORE=1 (A/B): the fast epilogue stores non-temporally
@@ -560,6 +561,13 @@ __device__ __forceinline__ void block_tile(const GemmDev& g, int& tx, int& ty, i
   const int nid = (x8 < rr ? x8 * (q + 1) : rr * (q + 1) + (x8 - rr) * q) + i8;
   ty = nid / g.tiles_x;
   tx = nid - ty * g.tiles_x;
+  if (g.row_perm > 1) {
+    // a dilated conv whose taps shift by row_perm whole row tiles: the XCD runs walk the row tiles in
+    // the order 0, p, 2p, ..., 1, 1 + p, ... so the tiles holding a tile's shifted rows sit next to it in
+    // its run (same L2) instead of one or more runs away (HBM / MALL re-reads)
+    const int per = g.tiles_y / g.row_perm;
+    ty = (ty % per) * g.row_perm + ty / per;
+  }
   z = blockIdx.z;
 }
 
@@ -2050,6 +2058,11 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
   const bool planes_on = knobs().gemm_xcd_planes;
   const long long nz = (long long)d.batch * g.split;
   g.xcd_planes = planes_on && wide && wide8() && nz >= 8 && nz % 8 == 0;
+  // FX_GEMM_ROWPERM=0: keep row tiles in order for dilated-conv A operands too (A/B)
+  if (knobs().gemm_row_perm && wide && !g.xcd_planes && d.a.conv_taps > 1 && !d.a.trans && d.a_dil_b1 <= 0) {
+    const int sh = d.a.conv_dil / WBM;
+    if (sh > 1 && g.tiles_y % sh == 0) g.row_perm = sh;
+  }
   g.nt_store = knobs().gemm_nt_store ? 1 : 0;
   P.grid = grid;
   P.block = block;

@@ -8,20 +8,19 @@
 //                        dH_i   = gU_i + conv_d^T(dZ_i)               -> out1
 //                        dZ_i-1 = (dH_i . W_pw,i-1) * (z_i-1 > 0)     -> out2
 //
-// A workgroup owns FR = 32 rows and all F = 256 channels (8 waves x 32 columns, one 32x32 f32
-// MFMA accumulator each): the full-width row tile is what makes the second GEMM row-local, and
-// 8192 rows give 256 workgroups = one per CU.  Both GEMMs stream their weights (conv 256 x 768,
-// 1x1 256 x 256; L2-resident, shared by every CU) through a three-slot LDS ring fed by two
-// register sets (a stage's global loads are issued four stages, and stored two stages, ahead of
-// its use; one stage index runs over both phases); the conv operand is read straight from the
-// row-major activations, each 32-deep k stage lying inside one tap (zero outside the video).
-// (Loading each wave's weight rows straight into MFMA registers instead -- no LDS for B -- was
-// 1.5x slower: 32 rows per lane-group are 32 cache lines per load instruction.)  The 1x1's first
-// weight stages are loaded during the conv's last stages, so the two phases run back to back.
-// Measured against the two tuned GEMM launches it replaces (conv 128x64 tiles + 1x1), it is about
-// even (58 vs 56 us per layer at 8192 rows: every CU streams the whole weight matrix through its
-// LDS, 1.5x the LDS write traffic per flop of a 128x64 tile), so the stack uses it only when
-// FX_MSTCN_FUSED=1 (diagnostic / A-B); the two-GEMM path stays the default.
+// A workgroup owns FR = 32 rows and all F = 256 channels (8 waves x 32 columns, one 32x32 f32 MFMA
+// accumulator each): the full-width row tile is what makes the second GEMM row-local, and 8192 rows
+// give 256 workgroups = one per CU.
+//
+// Operand paths.  The activation rows of a stage (32 rows x 32 k) are shared by the 8 waves: they go
+// through a 3-slot LDS ring (4.6 KB a slot).  The weights are NOT shared inside a workgroup -- wave w
+// multiplies only columns 32 w .. 32 w + 31 -- so each wave loads its own weight fragments straight
+// into registers, three stages ahead, from a copy of the weight matrix packed once per call in MFMA
+// fragment order (launch_pack_frag): the 16 k values a lane needs for one stage sit in 4 float4 that
+// 64 consecutive lanes read as one contiguous 1 KB per load instruction.  (The first version of this
+// kernel staged the whole weight matrix through every CU's LDS: 1.5x the LDS write traffic per FLOP of
+// the 128 x 64 GEMM tile, and about even with the two GEMM launches it replaces; loading the natural
+// [n][k] rows directly was slower still, 32 rows = 32 cache lines per load instruction.)
 #include <cstdlib>
 
 #include "fx_common.h"
@@ -35,26 +34,29 @@ constexpr int FR = 32;           // rows per workgroup
 constexpr int FN = 256;          // channels: N of both GEMMs, K of the second
 constexpr int FBK = 32;          // k per stage
 constexpr int FT = 512;          // threads: 8 waves x 32 columns
-constexpr int AS = FBK + 4;      // LDS row stride of the stage images ([row][k], k contiguous)
+constexpr int AS = FBK + 4;      // LDS row stride of the activation stage images ([row][k], k contiguous)
 constexpr int VS = FN + 4;       // LDS row stride of the phase-1 tile
 constexpr int A_IMG = FR * AS;
-constexpr int B_IMG = FN * AS;
-constexpr int SLOT = A_IMG + B_IMG;
-constexpr int NSL = 3;           // LDS ring depth
-constexpr int LDS_FLOATS = NSL * SLOT + FR * VS;
+constexpr int NSL = 3;           // activation ring depth
+constexpr int PD = 3;            // weight fragments: stages loaded ahead of their use
+constexpr int NB = PD + 1;       // weight register sets
+constexpr int LDS_FLOATS = NSL * A_IMG + FR * VS;
+constexpr int kMaxSeqF = 16;     // ragged videos per launch
 
 struct FrlArgs {
   const float* x;      // phase-1 conv operand rows (M, FN), ld ldx
   long long ldx;
   int dil, dir, T, M;
-  const float* w1;     // (FN, 3 FN) row-major: [n][tap * FN + c]
+  int nsoff;           // > 0: ragged videos, video v owns rows [soff[v], soff[v+1])
+  int soff[kMaxSeqF + 1];
+  const float* w1p;    // packed (launch_pack_frag) conv weights: [n][tap * FN + c], K = 3 FN
   const float* bias1;  // nullable
   int relu1;
   const float* resid1; // nullable (M, FN) ld ldr1
   long long ldr1;
   float* out1;
   long long ldo1;
-  const float* w2;     // (FN, FN) row-major: [n][k]
+  const float* w2p;    // packed 1x1 weights: [n][k], K = FN
   const float* bias2;  // nullable
   const float* resid2; // nullable
   long long ldr2;
@@ -70,51 +72,19 @@ struct FrlArgs {
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
-// One stage's global loads: A (threads 256..511 repeat 0..255: no branch, so the compiler counts
-// the outstanding loads exactly), B = 4 float4 per thread.  The zero select of A rows outside
-// their video is applied at the LDS store (applying it at the load would wait for the load).
-struct Prefetch {
-  float4 a, b[4];
-  bool a_ok;
-};
-
-__device__ __forceinline__ void load_a(const FrlArgs& g, int m0, int st, int tid, Prefetch& p) {
-  const int k0 = st * FBK, tap = k0 / FN, c0 = k0 - tap * FN;
-  const int ar = (tid & 255) >> 3, k4 = (tid & 7) * 4;
-  const int r = m0 + ar;
-  const int sh = (tap - 1) * g.dil * g.dir;
-  const int t = r % g.T + sh;
-  const bool ok = r < g.M && t >= 0 && t < g.T;
-  const long long src = ok ? (long long)(r + sh) : 0;   // clamped, unconditional load
-  p.a = ld4(g.x + src * g.ldx + c0 + k4);
-  p.a_ok = ok;
-}
-
-__device__ __forceinline__ void load_b(const float* w, int ldw, int st, int tid, Prefetch& p) {
-  const int k0 = st * FBK, k4 = (tid & 7) * 4, n = tid >> 3;
+// packed weight fragment of stage st, wave w for this lane: 4 float4 (k = 16 lh + 4 q .. + 3)
+__device__ __forceinline__ void load_b(const float* wp, int st, int w, int lane, float4* b) {
+  const float* base = wp + ((long long)(st * 8 + w) * 4) * 256 + lane * 4;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) p.b[j] = ld4(w + (long long)(n + 64 * j) * ldw + k0 + k4);
+  for (int q = 0; q < 4; ++q) b[q] = ld4(base + q * 256);
 }
 
-__device__ __forceinline__ void store_stage(float* slot, int tid, const Prefetch& p, bool with_a) {
-  const int k4 = (tid & 7) * 4, n = tid >> 3;
-  if (with_a)   // duplicate lanes write equal data
-    st4(slot + ((tid & 255) >> 3) * AS + k4, p.a_ok ? p.a : make_float4(0.f, 0.f, 0.f, 0.f));
-  float* b = slot + A_IMG;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) st4(b + (n + 64 * j) * AS + k4, p.b[j]);
-}
-
-// 16 MFMAs of one 32-deep stage: A rows from `a` (row stride as), B = this wave's 32 columns; the
+// 16 MFMAs of one 32-deep stage: A rows from `a` (row stride as), B = this wave's fragments; the
 // lane pairs A[li][16 lh + s] with B[n][16 lh + s]
-__device__ __forceinline__ void mma_stage(const float* a, int as, const float* b, int w, int li, int lh,
-                                          f32x16& acc) {
-  float4 fa[4], fb[4];
+__device__ __forceinline__ void mma_stage(const float* a, int as, const float4* fb, int li, int lh, f32x16& acc) {
+  float4 fa[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    fa[q] = ld4(a + li * as + lh * 16 + q * 4);
-    fb[q] = ld4(b + (w * 32 + li) * AS + lh * 16 + q * 4);
-  }
+  for (int q = 0; q < 4; ++q) fa[q] = ld4(a + li * as + lh * 16 + q * 4);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, fb[q].x, acc, 0, 0, 0);
@@ -126,87 +96,133 @@ __device__ __forceinline__ void mma_stage(const float* a, int as, const float* b
 
 __global__ __launch_bounds__(FT) void frl_kernel(FrlArgs g) {
   extern __shared__ float lds[];
-  float* V = lds + NSL * SLOT;
+  float* V = lds + NSL * A_IMG;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 31, lh = lane >> 5;
   const int m0 = blockIdx.x * FR;
   constexpr int n1 = 3 * FN / FBK, n2 = FN / FBK, nall = n1 + n2;
+  // this thread's activation row (threads 256..511 repeat 0..255: no branch, the compiler counts the
+  // outstanding loads exactly; duplicate lanes store equal data) and its position inside its video
+  const int ar = (tid & 255) >> 3, k4 = (tid & 7) * 4;
+  const int r = m0 + ar;
+  int rpos, rlen;
+  if (g.nsoff > 0) {
+    int start = 0, end = 0x7fffffff;
+#pragma unroll
+    for (int i = 1; i <= kMaxSeqF; ++i) {
+      if (i <= g.nsoff) {
+        const int o = g.soff[i];
+        if (o <= r) start = o;
+        else end = min(end, o);
+      }
+    }
+    rpos = r - start;
+    rlen = end - start;
+  } else {
+    rpos = r % g.T;
+    rlen = g.T;
+  }
+  const bool rok = r < g.M;
+  const float* xrow = g.x + (long long)min(r, g.M - 1) * g.ldx + k4;
+  auto load_a = [&](int st, float4& v, bool& ok) {
+    const int k0 = st * FBK, tap = k0 / FN, c0 = k0 - tap * FN;
+    const int sh = (tap - 1) * g.dil * g.dir;
+    const int t = rpos + sh;
+    ok = rok && t >= 0 && t < rlen;
+    v = ld4(xrow + (ok ? (long long)sh * g.ldx : 0ll) + c0);   // clamped, unconditional load
+  };
+  auto store_a = [&](float* slot, const float4& v, bool ok) {
+    st4(slot + ar * AS + k4, ok ? v : make_float4(0.f, 0.f, 0.f, 0.f));
+  };
   f32x16 acc;
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-  // one stage index over both phases: [0, n1) the conv (A + B), [n1, nall) the 1x1 (B; A = the
-  // LDS tile V); every loop has constant bounds and is fully unrolled: no stage branches remain
-  auto load = [&](int st, Prefetch& p) {
-    if (st < n1) {
-      load_a(g, m0, st, tid, p);
-      load_b(g.w1, 3 * FN, st, tid, p);
-    } else if (st < nall) {
-      load_b(g.w2, FN, st - n1, tid, p);
-    }
+  float4 pb[NB][4];                    // weight fragments, register set st % NB
+  float4 pa[2];                        // activation rows of stage st + 2 (set st & 1)
+  bool pok[2];
+  auto load_w = [&](int st) {
+    if (st < n1) load_b(g.w1p, st, w, lane, pb[st % NB]);
+    else if (st < nall) load_b(g.w2p, st - n1, w, lane, pb[st % NB]);
   };
-  // two register sets: stage st + 2 (loaded two stages ago) is stored into slot (st + 2) % 3 while
-  // stage st computes from slot st % 3, then stage st + 4 is loaded into the freed set
-  Prefetch pr[2];
-  load(0, pr[0]);
-  load(1, pr[1]);
-  store_stage(lds, tid, pr[0], true);
-  store_stage(lds + SLOT, tid, pr[1], 1 < n1);
-  load(2, pr[0]);
-  load(3, pr[1]);
+#pragma unroll
+  for (int st = 0; st < PD; ++st) load_w(st);
+  load_a(0, pa[0], pok[0]);
+  load_a(1, pa[1], pok[1]);
+  store_a(lds, pa[0], pok[0]);
+  store_a(lds + A_IMG, pa[1], pok[1]);
+  load_a(2, pa[0], pok[0]);
+  load_a(3, pa[1], pok[1]);
   __syncthreads();
-  // (sched_barrier pins the order: left to itself the scheduler hoists a set's select / LDS stores
-  // up to its loads and waits on loads issued a moment earlier)
-  auto step = [&](int st, f32x16& ac, const float* a, int as) {
-    const float* cur = lds + (st % NSL) * SLOT;
-    mma_stage(a ? a : cur, a ? as : AS, cur + A_IMG, w, li, lh, ac);
+  // stage st: multiply slot st % 3 (phase 2: the LDS tile V); store the activation rows of stage st + 2
+  // (loaded two stages ago) into slot (st + 2) % 3; load stage st + 4's rows and stage st + PD's weights
+  auto step = [&](int st, const float* a, int as) {
+    const float* cur = lds + (st % NSL) * A_IMG;
+    mma_stage(a ? a : cur, a ? as : AS, pb[st % NB], li, lh, acc);
     __builtin_amdgcn_sched_barrier(0);
-    if (st + 2 < nall) store_stage(lds + ((st + 2) % NSL) * SLOT, tid, pr[st & 1], st + 2 < n1);
-    __builtin_amdgcn_sched_barrier(0);
-    if (st + 4 < nall) load(st + 4, pr[st & 1]);
+    if (st + 2 < n1) store_a(lds + ((st + 2) % NSL) * A_IMG, pa[st & 1], pok[st & 1]);
+    if (st + 4 < n1) load_a(st + 4, pa[st & 1], pok[st & 1]);
+    load_w(st + PD);
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
   };
 #pragma unroll
-  for (int st = 0; st < n1; ++st) step(st, acc, nullptr, 0);
+  for (int st = 0; st < n1; ++st) step(st, nullptr, 0);
   // ---------------- phase-1 epilogue: out1 and the LDS tile V
   {
     const int col = w * 32 + li;
     const float bv = g.bias1 ? g.bias1[col] : 0.f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+    for (int q = 0; q < 16; ++q) {
+      const int row = (q & 3) + 8 * (q >> 2) + 4 * lh;
       const int gr = m0 + row;
-      float v = acc[r] + bv;
+      float v = acc[q] + bv;
       if (g.relu1) v = fmaxf(v, 0.f);
       if (g.resid1 && gr < g.M) v += g.resid1[(long long)gr * g.ldr1 + col];
       if (gr < g.M) g.out1[(long long)gr * g.ldo1 + col] = v;
       V[row * VS + col] = v;
-      acc[r] = 0.f;
+      acc[q] = 0.f;
     }
   }
   __syncthreads();
   // ---------------- phase 2: 1x1 GEMM from the LDS tile, K = FN
 #pragma unroll
-  for (int j = 0; j < n2; ++j) step(n1 + j, acc, V + j * FBK, VS);
+  for (int j = 0; j < n2; ++j) step(n1 + j, V + j * FBK, VS);
   // ---------------- phase-2 epilogue
   const int col = w * 32 + li;
   const float bv = g.bias2 ? g.bias2[col] : 0.f;
   float res[16], gat[16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int gr = min(m0 + (r & 3) + 8 * (r >> 2) + 4 * lh, g.M - 1);
-    res[r] = g.resid2 ? g.resid2[(long long)gr * g.ldr2 + col] : 0.f;
-    gat[r] = g.gate2 ? g.gate2[(long long)gr * g.ldg2 + col] : 1.f;
+  for (int q = 0; q < 16; ++q) {
+    const int gr = min(m0 + (q & 3) + 8 * (q >> 2) + 4 * lh, g.M - 1);
+    res[q] = g.resid2 ? g.resid2[(long long)gr * g.ldr2 + col] : 0.f;
+    gat[q] = g.gate2 ? g.gate2[(long long)gr * g.ldg2 + col] : 1.f;
   }
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int gr = m0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-    float v = acc[r] + bv;
+  for (int q = 0; q < 16; ++q) {
+    const int gr = m0 + (q & 3) + 8 * (q >> 2) + 4 * lh;
+    float v = acc[q] + bv;
     if (g.drop_thr)
       v = fx_drop_bits(g.drop_seed, (unsigned long long)gr * FN + col) >= g.drop_thr ? v * g.drop_scale : 0.f;
-    v += res[r];
-    if (!(gat[r] > 0.f)) v = 0.f;
+    v += res[q];
+    if (!(gat[q] > 0.f)) v = 0.f;
     if (gr < g.M) g.out2[(long long)gr * g.ldo2 + col] = v;
   }
+}
+
+// Weight matrices [FN][K] (row-major, leading dim ld) -> MFMA fragment order for frl_kernel:
+// dst[((st * 8 + w) * 4 + q) * 64 + lane] = float4(src[n = 32 w + lane % 32][32 st + 16 (lane / 32) + 4 q ..])
+struct PackFragArgs {
+  const float* src[32];
+  float* dst[32];
+  long long ld;
+  int K;
+};
+
+__global__ __launch_bounds__(256) void pack_frag_kernel(PackFragArgs a) {
+  const int st = blockIdx.x, w = blockIdx.y, m = blockIdx.z;
+  const int q = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n = w * 32 + (lane & 31), k = st * FBK + 16 * (lane >> 5) + 4 * q;
+  const float4 v = ld4(a.src[m] + (long long)n * a.ld + k);
+  st4(a.dst[m] + ((long long)((st * 8 + w) * 4 + q) * 64 + lane) * 4, v);
 }
 
 }  // namespace
@@ -215,12 +231,31 @@ bool frl_supported(int F, const void* x, long long ldx, long long ld_other) {
   return F == FN && ldx % 4 == 0 && ((uintptr_t)x & 15) == 0 && ld_other % 4 == 0;
 }
 
-int launch_frl(const float* x, long long ldx, int M, int T, int dil, int dir, const float* w1, const float* bias1,
-               int relu1, const float* resid1, long long ldr1, float* out1, long long ldo1, const float* w2,
-               const float* bias2, const float* resid2, long long ldr2, const float* gate2, long long ldg2, float* out2,
-               long long ldo2, float drop_p, unsigned long long drop_seed, hipStream_t s) {
-  FX_REQUIRE(M > 0 && T > 0 && dil > 0 && (dir == 1 || dir == -1), "frl: bad shape");
-  FX_REQUIRE(frl_supported(FN, x, ldx, ldo1) && ((uintptr_t)w1 & 15) == 0 && ((uintptr_t)w2 & 15) == 0,
+long long frl_packed_floats(int K) { return (long long)FN * K; }
+
+int launch_pack_frag(const float* const* src, float* const* dst, int n, long long ld, int K, hipStream_t s) {
+  FX_REQUIRE(n >= 1 && n <= 32 && K % FBK == 0 && ld % 4 == 0, "pack_frag: 1..32 matrices, K % 32 == 0");
+  PackFragArgs a{};
+  for (int i = 0; i < n; ++i) {
+    a.src[i] = src[i];
+    a.dst[i] = dst[i];
+  }
+  a.ld = ld;
+  a.K = K;
+  hipLaunchKernelGGL(pack_frag_kernel, dim3(K / FBK, FN / 32, n), dim3(256), 0, s, a);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
+int launch_frl(const float* x, long long ldx, int M, int T, int dil, int dir, const int* seq_off, int nseq,
+               const float* w1p, const float* bias1, int relu1, const float* resid1, long long ldr1, float* out1,
+               long long ldo1, const float* w2p, const float* bias2, const float* resid2, long long ldr2,
+               const float* gate2, long long ldg2, float* out2, long long ldo2, float drop_p,
+               unsigned long long drop_seed, hipStream_t s) {
+  FX_REQUIRE(M > 0 && dil > 0 && (dir == 1 || dir == -1), "frl: bad shape");
+  FX_REQUIRE(seq_off ? (nseq >= 1 && nseq <= kMaxSeqF && seq_off[0] == 0 && seq_off[nseq] == M) : T > 0,
+             "frl: uniform videos of T rows, or ragged offsets spanning [0, M) (<= 16 videos)");
+  FX_REQUIRE(frl_supported(FN, x, ldx, ldo1) && ((uintptr_t)w1p & 15) == 0 && ((uintptr_t)w2p & 15) == 0,
              "frl: needs F = 256 and 16-byte aligned rows");
   FX_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "frl: dropout must be in [0, 1)");
   static const bool attr = [] {
@@ -233,16 +268,19 @@ int launch_frl(const float* x, long long ldx, int M, int T, int dil, int dir, co
   a.ldx = ldx;
   a.dil = dil;
   a.dir = dir;
-  a.T = T;
+  a.T = T > 0 ? T : 1;
   a.M = M;
-  a.w1 = w1;
+  a.nsoff = seq_off ? nseq : 0;
+  if (seq_off)
+    for (int v = 0; v <= nseq; ++v) a.soff[v] = seq_off[v];
+  a.w1p = w1p;
   a.bias1 = bias1;
   a.relu1 = relu1;
   a.resid1 = resid1;
   a.ldr1 = ldr1;
   a.out1 = out1;
   a.ldo1 = ldo1;
-  a.w2 = w2;
+  a.w2p = w2p;
   a.bias2 = bias2;
   a.resid2 = resid2;
   a.ldr2 = ldr2;

@@ -137,12 +137,16 @@ int launch_tattn_bwd(const float* q, long long ldq, const float* k, long long ld
                      long long lddk, float* dv, long long lddv, float* ws, hipStream_t s,
                      const TAttnOpts* opt = nullptr);
 
-// fused MS-TCN layer step (mstcn_fused.hip, opt-in per call: fx_mstcn_params.fused_layers): conv GEMM
-// (K = 3F) -> row-local epilogue -> 1x1 GEMM
+// fused MS-TCN layer step (mstcn_fused.hip, per call: fx_mstcn_params.fused_layers): conv GEMM (K = 3F)
+// -> row-local epilogue -> 1x1 GEMM; both weight matrices in the packed fragment order of
+// launch_pack_frag (FN x K floats each)
 bool frl_supported(int F, const void* x, long long ldx, long long ld_other);
-int launch_frl(const float* x, long long ldx, int M, int T, int dil, int dir, const float* w1, const float* bias1,
-               int relu1, const float* resid1, long long ldr1, float* out1, long long ldo1, const float* w2,
-               const float* bias2, const float* resid2, long long ldr2, const float* gate2, long long ldg2, float* out2,
-               long long ldo2, float drop_p, unsigned long long drop_seed, hipStream_t s);
+long long frl_packed_floats(int K);
+int launch_pack_frag(const float* const* src, float* const* dst, int n, long long ld, int K, hipStream_t s);
+int launch_frl(const float* x, long long ldx, int M, int T, int dil, int dir, const int* seq_off, int nseq,
+               const float* w1p, const float* bias1, int relu1, const float* resid1, long long ldr1, float* out1,
+               long long ldo1, const float* w2p, const float* bias2, const float* resid2, long long ldr2,
+               const float* gate2, long long ldg2, float* out2, long long ldo2, float drop_p,
+               unsigned long long drop_seed, hipStream_t s);
 
 }  // namespace fx

@@ -951,13 +951,19 @@ def _queue_backward_status(dev):
     torch.autograd.Variable._execution_engine.queue_callback(copy_status)
 
 
-def resolve_backward_status():
-    """Raise FactmxNativeError if a kernel of an earlier BACKWARD pass set the status word.  (Called
-    between passes: a copy callback an aborted backward never ran must not block later ones.)"""
+def resolve_backward_status(wait=False):
+    """Raise FactmxNativeError if a kernel of an earlier BACKWARD pass set the status word.  Called
+    between passes (a copy callback an aborted backward never ran must not block later ones).  At the
+    start of a forward (wait=False) only copies that have already landed are checked -- waiting for the
+    previous backward here would drain the device queue every step; FusedAdam's device-side guard
+    covers the step in between.  check_device_status() waits (wait=True)."""
     global _bwd_status_queued
     _bwd_status_queued = False
     while _bwd_status:
-        h, ev, dev = _bwd_status.pop(0)
+        h, ev, dev = _bwd_status[0]
+        if not wait and not ev.query():
+            return
+        _bwd_status.pop(0)
         ev.synchronize()
         if int(h[0]):
             _bwd_status.clear()
@@ -972,7 +978,7 @@ def check_device_status(dev=None):
     """Synchronous check of the status word (e.g. after the last backward of a run)."""
     from .models import vloss
     vloss.resolve_pending()
-    resolve_backward_status()
+    resolve_backward_status(wait=True)
     dev = torch.device("cuda", torch.cuda.current_device()) if dev is None else torch.device(dev)
     if dev in _status:
         status_raise(int(_status[dev][0].item()), dev)
