@@ -690,7 +690,7 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   // overlaps the chain instead; measured even (the per-layer split-K GEMMs slow the chain by as much),
   // so it is off by default
   const bool tail = p->in_map && knobs().mstcn_tail;
-  const bool defer = !fchain && !p->layernorm && !drop && NL > 0 && !tail && mstcn_defer_ok(p, g);
+  const bool defer = !p->layernorm && !drop && NL > 0 && !tail && mstcn_defer_ok(p, g);
   // FX_SIDE_MAXWG=n: the side stream's split-K GEMMs keep within n workgroups (A/B diagnostic)
   GridCap gcap(ss ? knobs().side_maxwg : 0);
   auto fork = [&](int e) -> int {   // side stream waits for the main stream's work so far
@@ -737,7 +737,7 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
       return launch_gemm(d, sd);
     });
   };
-  for (int i = NL - 1; fchain && i >= NL - 1; --i) {   // top layer: dZ by the 1x1 backward GEMM
+  for (int i = NL - 1; fchain && !defer && i >= NL - 1; --i) {   // top layer: dZ by the 1x1 backward GEMM
     const float* zi = saved + L.z + i * L.rowsF;
     FX_TRY(fork(1));
     FX_TRY(linear_dwdb(dH, F, zi, F, rows, F, F, g->w_pw[i], g->b_pw[i], 1, spl, sd));
@@ -746,7 +746,7 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
     FX_TRY(conv_dw(i, Zb[0]));
     FX_TRY(side_done(i));
   }
-  for (int i = NL - 1; fchain && i >= 0; --i) {
+  for (int i = NL - 1; fchain && !defer && i >= 0; --i) {
     float* gU = Hb[(NL - 1 - i) % 3];           // dH_{i+1}
     float* dZi = Zb[(NL - 1 - i) % 3];
     float* dHi = Hb[(NL - i) % 3];
@@ -832,12 +832,26 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
     // FX_MSTCN_DW_HALVES=1: the layers above `half` get their weight gradients as soon as the chain has
     // passed them (overlapping the chain's remaining layers), the rest after the chain.  Measured no
     // better than one batched launch after the chain (the early half slows the chain it overlaps): off
-    const int half = knobs().mstcn_dw_halves ? NL / 2 : 0;
-    for (int i = NL - 1; i >= 0; --i) {
+    const int half = (knobs().mstcn_dw_halves && !fchain) ? NL / 2 : 0;
+    if (fchain) {
+      // the fused chain into the per-layer slots: dZ_NL-1 by the 1x1 backward GEMM, then per layer ONE
+      // kernel for dH_i (-> dHall[i-1]) and dZ_i-1 (-> dZall[i-1]); the bottom layer's conv backward
+      // alone; the weight gradients of every layer follow as the batched side-stream GEMMs below
+      FX_TRY(pw_dx(dHall + (NL - 1) * L.rowsF, NL - 1, dZall + (NL - 1) * L.rowsF, saved + L.z + (NL - 1) * L.rowsF));
+      for (int i = NL - 1; i >= 1; --i) {
+        prof_begin(0, s);
+        FX_TRY(launch_frl(dZall + i * L.rowsF, F, rows, T, layer_dilation(p, i), -1, q.off, q.nvid,
+                          ws + L.wk1 + (long long)i * 3 * F * F, nullptr, 0, dHall + i * L.rowsF, F,
+                          dHall + (i - 1) * L.rowsF, F, ws + L.wk2 + (long long)(i - 1) * F * F, nullptr, nullptr, 0,
+                          saved + L.z + (i - 1) * L.rowsF, F, dZall + (i - 1) * L.rowsF, F, 0.f, 0, s));
+        prof_end(0, s, 2.0 * rows * F * 4.0 * F, 4.0 * (4.0 * rows * F + 4.0 * F * F));
+      }
+    }
+    for (int i = fchain ? 0 : NL - 1; i >= 0; --i) {
       const float* zi = saved + L.z + i * L.rowsF;
       const float* gU = dHall + i * L.rowsF;
       float* dZ = dZall + i * L.rowsF;
-      FX_TRY(pw_dx(gU, i, dZ, zi));
+      if (!fchain) FX_TRY(pw_dx(gU, i, dZ, zi));   // (fused chain: dZ_0 came with dH_1)
       float* dHn = i > 0 ? dHall + (i - 1) * L.rowsF : Hb[0];
       fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dZ, F, F, layer_dilation(p, i), -1, q, false),
                                  op_rows(wbp + (long long)i * 3 * F * F, 3 * F), dHn, F);
