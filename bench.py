@@ -467,17 +467,22 @@ def main():
     S = video_segments(net)
     log(f"[rank {rank}] TDU segments per video (per U block): {S}")
 
-    # HIP events around the dominant kernel's launches (and the attention launches) of the FIRST timed
+    # HIP events around the dominant kernel's launches (and the attention / X2Y launches) of the FIRST timed
     # step(s) only: an event pair per launch costs host time (~1 ms per step over all 80 conv launches,
     # A/B in DESIGN.md), so the roofline samples the timed region instead of perturbing all of it
-    # (FX_BENCH_PROF_STEPS: steps to sample; the durations agree with the all-steps sampling)
+    # (FX_BENCH_PROF_STEPS: steps to sample; the durations agree with the all-steps sampling).  The event
+    # capacity of each kind is its launch count in one step, counted on an untimed extra warm-up step,
+    # times the sampled steps -- so no event pair spills into the later timed steps.
     psteps = min(args.steps, int(os.environ.get("FX_BENCH_PROF_STEPS", 1)))
-    max_ev = psteps * nv * 4 * 10 * 2 + 64
-    native.check(lib.fx_prof_enable(0, max_ev), "fx_prof_enable")
-    for kind in (1, 2):       # attention over T, forward and backward (one launch per SCA decoder layer)
-        native.check(lib.fx_prof_enable(kind, psteps * 16 + 64), "fx_prof_enable")
-    for kind in X2Y_KINDS:    # the frame<->action X2Y cores (one call per X2Y map of every update block)
-        native.check(lib.fx_prof_enable(kind, psteps * 8 + 16), "fx_prof_enable")
+    kinds = [0, 1, 2] + list(X2Y_KINDS)
+    for kind in kinds:
+        native.check(lib.fx_prof_enable(kind, 4096), "fx_prof_enable")
+    step()
+    per_step = {kind: prof_collect(lib, kind)[3].value for kind in kinds}
+    lib.fx_prof_disable()
+    for kind in kinds:
+        if per_step[kind] > 0:
+            native.check(lib.fx_prof_enable(kind, per_step[kind] * psteps), "fx_prof_enable")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -488,9 +493,13 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ms, fl, by, cnt = prof_collect(lib, 0)
-    attn_prof = {name: prof_collect(lib, kind) for kind, name in ((1, "fwd"), (2, "bwd"))}
-    x2y_prof = {name: prof_collect(lib, kind) for kind, name in X2Y_KINDS.items()}
+    def collect(kind):
+        if per_step[kind] > 0:
+            return prof_collect(lib, kind)
+        return native.D(), native.D(), native.D(), native.I()
+    ms, fl, by, cnt = collect(0)
+    attn_prof = {name: collect(kind) for kind, name in ((1, "fwd"), (2, "bwd"))}
+    x2y_prof = {name: collect(kind) for kind, name in X2Y_KINDS.items()}
     lib.fx_prof_disable()
     S_after = video_segments(net)
     if world > 1:

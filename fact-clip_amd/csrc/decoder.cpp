@@ -120,7 +120,7 @@ struct DecLayout {
   long long wkv, bkv, wsp, total_ws_fwd;
   // workspace (bwd)
   long long dkv, dwkv, dbkv, dT, dS, dU, dF, dQKV, dO, dq, G, P, lnws, core, dmask, split, gdu, gdf, gdq, gdqkv,
-      total_ws_bwd;
+      gdy, total_ws_bwd;
 };
 
 long long dec_split_ws(const fx_decoder_params* p, int R, int T) {
@@ -234,6 +234,9 @@ DecLayout dec_layout(const fx_decoder_params* p, int R, int T, int has_qpos, int
   L.gdf = o; o += (long long)p->num_layers * R * FF;
   L.gdq = o; o += (long long)p->num_layers * RA;
   L.gdqkv = o; o += 3LL * p->num_layers * RA;
+  // every layer's three LayerNorm input gradients, kept for the batched LN weight / bias gradients
+  // that follow the chain on the side stream (the chain's LN backward computes dx only)
+  L.gdy = o; o += 3LL * p->num_layers * RA;
   L.total_ws_bwd = o;
   (void)FF;
   return L;
@@ -348,18 +351,21 @@ int fx_decoder_fwd(const fx_decoder_params* p, const float* tgt, long long ldt, 
     // --- self-attention over the tokens: q = k = x + qpos, v = x  (basic.py:495-503 / 438-444)
     const float* xq = x;
     long long ldxq = ldx;
-    if (qpos) {
-      FX_TRY(add2(x, ldx, qpos, A, R, A, b + L.xq, A, 0, s));
+    if (qpos) {   // layers >= 1: written by the previous layer's last LayerNorm (y + pos output)
+      if (l == 0) FX_TRY(add2(x, ldx, qpos, A, R, A, b + L.xq, A, 0, s));
       xq = b + L.xq;
       ldxq = A;
     }
     float* qkv = b + L.qkv;   // (R, 3A): [q | k | v]
     if (!qpos) {
       FX_TRY(linear_fwd(x, ldx, R, A, p->sa_in_w[l], p->sa_in_b[l], qkv, 3 * A, 3 * A, 0, s));
-    } else {
-      FX_TRY(linear_fwd(xq, ldxq, R, A, p->sa_in_w[l], p->sa_in_b[l], qkv, 3 * A, 2 * A, 0, s));
-      FX_TRY(linear_fwd(x, ldx, R, A, p->sa_in_w[l] + 2LL * A * A, p->sa_in_b[l] + 2 * A, qkv + 2 * A, 3 * A, A, 0,
-                        s));
+    } else {   // q, k from x + qpos and v from x: two products, one grouped launch
+      fx_gemm_desc d2[2];
+      d2[0] = gemm_desc(R, 2 * A, A, op_rows(xq, ldxq), op_rows(p->sa_in_w[l], A), qkv, 3 * A);
+      d2[0].bias = p->sa_in_b[l];
+      d2[1] = gemm_desc(R, A, A, op_rows(x, ldx), op_rows(p->sa_in_w[l] + 2LL * A * A, A), qkv + 2 * A, 3 * A);
+      d2[1].bias = p->sa_in_b[l] + 2 * A;
+      FX_TRY(launch_gemm_group(d2, 2, s));
     }
     if (Qv <= kSmallTok) {
       FX_TRY(launch_mha_small_fwd(qkv, 3 * A, qkv + A, 3 * A, qkv + 2 * A, 3 * A, Qv, Qv, hd, h, scale, b + L.psa,
@@ -375,16 +381,16 @@ int fx_decoder_fwd(const fx_decoder_params* p, const float* tgt, long long ldt, 
     float* u = spl + (std::max(L.total_ws_fwd - L.wsp, RA) - RA);   // last RA floats of the scratch
     FX_TRY(linear_fwd_res_drop(b + L.osa, A, R, A, p->sa_out_w[l], A, p->sa_out_b[l], x, ldx, u, A, A, pd,
                                dec_seed(p, l, 1), s));
-    FX_TRY(launch_layernorm_fwd(u, A, nullptr, 0, p->ln_sa_w[l], p->ln_sa_b[l], eps, R, A, 0, b + L.t1, A, nullptr,
-                                b + L.rs1, b + L.xh1, A, s));
+    // (cross-attention decoders with query positions: the LayerNorm also writes t1 + qpos, the query
+    // operand below)
+    const bool t1q = p->cross && qpos;
+    FX_TRY(launch_layernorm_fwd_pos(u, A, nullptr, 0, p->ln_sa_w[l], p->ln_sa_b[l], eps, R, A, 0, b + L.t1, A,
+                                    nullptr, b + L.rs1, b + L.xh1, A, t1q ? qpos : nullptr, A,
+                                    t1q ? b + L.t1q : nullptr, A, s));
     const float* t2 = b + L.t1;
     if (p->cross) {
       // --- cross-attention onto the frames: q = t1 + qpos, k = mem + pos, v = mem (basic.py:504-515)
-      const float* tq = b + L.t1;
-      if (qpos) {
-        FX_TRY(add2(b + L.t1, A, qpos, A, R, A, b + L.t1q, A, 0, s));
-        tq = b + L.t1q;
-      }
+      const float* tq = t1q ? b + L.t1q : b + L.t1;
       FX_TRY(linear_fwd(tq, A, R, A, p->ca_q_w[l], p->ca_in_b[l], b + L.qc, A, A, 0, s));
       // every video's tokens over its own frames, all heads, one fused launch (attn_t.hip)
       TAttnOpts o;
@@ -412,8 +418,11 @@ int fx_decoder_fwd(const fx_decoder_params* p, const float* tgt, long long ldt, 
     }
     FX_TRY(linear_fwd_res_drop(b + L.f1, FF, R, FF, p->ff2_w[l], FF, p->ff2_b[l], t2, A, u, A, A, pd,
                                dec_seed(p, l, 5), s));
-    FX_TRY(launch_layernorm_fwd(u, A, nullptr, 0, p->ln_ff_w[l], p->ln_ff_b[l], eps, R, A, 0, b + L.t3, A, nullptr,
-                                b + L.rs3, b + L.xh3, A, s));
+    // (the next layer's query operand t3 + qpos written beside t3)
+    const bool nxq = qpos && l + 1 < NL;
+    FX_TRY(launch_layernorm_fwd_pos(u, A, nullptr, 0, p->ln_ff_w[l], p->ln_ff_b[l], eps, R, A, 0, b + L.t3, A,
+                                    nullptr, b + L.rs3, b + L.xh3, A, nxq ? qpos : nullptr, A,
+                                    nxq ? b + L.per_layer + L.xq : nullptr, A, s));
     x = b + L.t3;
     ldx = A;
   }
@@ -454,6 +463,10 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
   // out_linear and the final LayerNorm
   const float* xl = saved + L.layers + (NL - 1) * L.per_layer + L.t3;   // last layer output
   const float* fin = p->final_norm ? saved + L.fo : xl;
+  // LN input gradient of layer l's LayerNorm k (0 FFN, 1 cross-attention, 2 self-attention): each
+  // producer in the chain writes straight into the slot its consumer reads
+  auto dy_slot = [&](int k, int l) { return ws + L.gdy + ((long long)k * NL + l) * RA; };
+  dT = dy_slot(0, NL - 1);
   FX_TRY(linear_bwd_pair(desc_linear_dwdb(dout, lddo, fin, A, R, A, p->out_dim, g->out_w, g->out_b, 1, spl),
                          desc_linear_dx(dout, lddo, p->out_w, R, A, p->out_dim, p->final_norm ? dS : dT, A, 0, nullptr,
                                         0, spl),
@@ -468,6 +481,7 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
   auto slot_u = [&](int k, int l) { return ws + L.gdu + ((long long)k * NL + l) * RA; };   // k: 0 ff, 1 ca, 2 sa
   for (int l = NL - 1; l >= 0; --l) {
     const float* b = saved + L.layers + l * L.per_layer;
+    dT = dy_slot(0, l);
     float* dU = slot_u(0, l);
     float* dF = ws + L.gdf + (long long)l * R * FF;
     float* dq = ws + L.gdq + (long long)l * RA;
@@ -479,21 +493,22 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
       if (pd <= 0.f) return FX_OK;
       return launch_dropout(dR, A, R, A, A, 0, pd, dec_seed(p, l, site), du, A, s);
     };
-    FX_TRY(launch_layernorm_bwd(dT, A, nullptr, 0, b + L.xh3, A, p->ln_ff_w[l], b + L.rs3, R, A, 0, dR, A,
-                                g->ln_ff_w[l], g->ln_ff_b[l], lnws, s));
+    FX_TRY(launch_layernorm_bwd(dT, A, nullptr, 0, b + L.xh3, A, p->ln_ff_w[l], b + L.rs3, R, A, 0, dR, A, nullptr,
+                                nullptr, lnws, s));
     FX_TRY(branch_mask(dU, 5));
     {
       fx_gemm_desc d = desc_linear_dx(dU, A, p->ff2_w[l], R, FF, A, dF, FF, 0, b + L.f1, FF, spl);
       if (pd > 0.f) d.alpha = 1.f / (1.f - pd);   // f1 > 0 <=> kept and active: the gate is relu' * mask
       FX_TRY(launch_gemm(d, s));
     }
+    dT = dy_slot(p->cross ? 1 : 2, l);
     FX_TRY(launch_gemm(dx_res_desc(dF, FF, p->ff1_w[l], A, R, A, FF, dR, A, dT, A, spl), s));   // dT2 = dR + dF W1
     if (p->cross) {
       // --- cross-attention + LN2
       dU = slot_u(1, l);
       if (pd <= 0.f) dR = dU;
-      FX_TRY(launch_layernorm_bwd(dT, A, nullptr, 0, b + L.xh2, A, p->ln_ca_w[l], b + L.rs2, R, A, 0, dR, A,
-                                  g->ln_ca_w[l], g->ln_ca_b[l], lnws, s));
+      FX_TRY(launch_layernorm_bwd(dT, A, nullptr, 0, b + L.xh2, A, p->ln_ca_w[l], b + L.rs2, R, A, 0, dR, A, nullptr,
+                                  nullptr, lnws, s));
       FX_TRY(branch_mask(dU, 3));
       FX_TRY(launch_gemm(desc_linear_dx(dU, A, p->ca_out_w[l], R, A, A, dO, A, 0, nullptr, 0, spl), s));
       const float* kv = saved + L.kv;
@@ -504,6 +519,7 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
       FX_TRY(launch_tattn_bwd(b + L.qc, A, kv + (long long)l * A, AL2, kv + (long long)(NL + l) * A, AL2, b + L.oca, A,
                               dO, A, b + L.pca, nvid, Qv, Tv, hd, h, scale, dq, A, dkv + (long long)l * A, AL2,
                               dkv + (long long)(NL + l) * A, AL2, ws + L.core, s, &o));
+      dT = dy_slot(2, l);
       if (qpos) {
         FX_TRY(launch_gemm(desc_linear_dx(dq, A, p->ca_q_w[l], R, A, A, P, A, 0, nullptr, 0, spl), s));
         FX_TRY(add_acc(dR, P, dT, G, RA, s));                                     // dT1 = dR + P ; G += P
@@ -514,8 +530,8 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
     // --- self-attention + LN1
     dU = slot_u(2, l);
     if (pd <= 0.f) dR = dU;
-    FX_TRY(launch_layernorm_bwd(dT, A, nullptr, 0, b + L.xh1, A, p->ln_sa_w[l], b + L.rs1, R, A, 0, dR, A,
-                                g->ln_sa_w[l], g->ln_sa_b[l], lnws, s));
+    FX_TRY(launch_layernorm_bwd(dT, A, nullptr, 0, b + L.xh1, A, p->ln_sa_w[l], b + L.rs1, R, A, 0, dR, A, nullptr,
+                                nullptr, lnws, s));
     FX_TRY(branch_mask(dU, 1));
     FX_TRY(launch_gemm(desc_linear_dx(dU, A, p->sa_out_w[l], R, A, A, dO, A, 0, nullptr, 0, spl), s));
     const float* qkv = b + L.qkv;
@@ -530,7 +546,7 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
       FX_TRY(launch_tattn_bwd(qkv, 3 * A, qkv + A, 3 * A, qkv + 2 * A, 3 * A, b + L.osa, A, dO, A, b + L.psa, nvid, Qv,
                               Qv, hd, h, scale, dQKV, 3 * A, dQKV + A, 3 * A, dQKV + 2 * A, 3 * A, ws + L.core, s, &o));
     }
-    float* dX = l == 0 ? nullptr : dT;   // the next (earlier) layer's output gradient, in place
+    float* dX = l == 0 ? nullptr : dy_slot(0, l - 1);   // the next (earlier) layer's output gradient
     if (!qpos) {
       if (l > 0 || dtgt)
         FX_TRY(launch_gemm(dx_res_desc(dQKV, 3 * A, p->sa_in_w[l], A, R, A, 3 * A, dR, A, l > 0 ? dX : dtgt,
@@ -542,6 +558,8 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
         FX_TRY(linear_dx_res(dQKV + 2 * A, 3 * A, p->sa_in_w[l] + 2LL * A * A, A, R, A, A, dR, A, dS, A, spl, s));
         if (l > 0) {
           FX_TRY(add_acc(dS, P, dX, G, RA, s));
+        } else if (lddt == A) {
+          FX_TRY(add_acc(dS, P, dtgt, G, RA, s));
         } else {
           FX_TRY(add_acc(dS, P, dS, G, RA, s));
           FX_CHECK_HIP(hipMemcpy2DAsync(dtgt, lddt * sizeof(float), dS, A * sizeof(float), A * sizeof(float), R,
@@ -606,6 +624,23 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
       FX_TRY(kind(1, NL - 1, dq0 + 3 * RA + 2 * A, 3 * A, 3 * RA, b0 + L.t3, A, PL, A, A, g->sa_in_w, g->sa_in_b,
                   2 * A, 2LL * A * A));
     }
+  }
+  {
+    // every layer's LayerNorm weight / bias gradients in one launch: dw += sum_rows dy * xhat, db += sum_rows dy
+    // (the chain's LN backward computed dx only)
+    LnGradJob jobs[3 * MAXL];
+    int nj = 0;
+    for (int l = 0; l < NL; ++l) {
+      const float* b = saved + L.layers + l * L.per_layer;
+      auto add = [&](int k, long long xh_off, float* const* gw, float* const* gb) {
+        if (!gw[l] && !gb[l]) return;
+        jobs[nj++] = LnGradJob{dy_slot(k, l), b + xh_off, gw[l], gb[l]};
+      };
+      add(0, L.xh3, g->ln_ff_w, g->ln_ff_b);
+      if (p->cross) add(1, L.xh2, g->ln_ca_w, g->ln_ca_b);
+      add(2, L.xh1, g->ln_sa_w, g->ln_sa_b);
+    }
+    FX_TRY(launch_ln_param_grads(jobs, nj, R, A, A, A, sd));
   }
   if (qpos && dqpos) FX_CHECK_HIP(hipMemcpyAsync(dqpos, G, RA * sizeof(float), hipMemcpyDeviceToDevice, s));
   if (p->cross) {

@@ -33,7 +33,6 @@ constexpr int NW = 16;          // workgroups per direction
 constexpr int GT = 256;         // threads per workgroup
 constexpr int MAXU = 16;        // hidden units per workgroup (Hh <= 256)
 constexpr int KCH = 64;         // fwd: k-chunk per thread (4 chunks cover Hh <= 256)
-constexpr int RCH = 48;         // bwd: gate rows per thread (16 chunks cover 3Hh <= 768)
 constexpr unsigned SPIN_MAX = 1u << 20;   // default: ~1 s of polling; a lost peer ends the kernel, never hangs it
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;

@@ -9,7 +9,22 @@ long long colsum_workspace_floats(int M, int N);
 int launch_layernorm_fwd(const float* x, long long ldx, const float* r, long long ldr, const float* w,
                          const float* b, float eps, int rows, int cols, int relu, float* y, long long ldy,
                          float* mean, float* rstd, float* xhat, long long ldxh, hipStream_t s);
+// the same, also writing y2 = y + pos (nullable: pos / y2 both or neither)
+int launch_layernorm_fwd_pos(const float* x, long long ldx, const float* r, long long ldr, const float* w,
+                             const float* b, float eps, int rows, int cols, int relu, float* y, long long ldy,
+                             float* mean, float* rstd, float* xhat, long long ldxh, const float* pos, long long ldp,
+                             float* y2, long long ldy2, hipStream_t s);
 long long layernorm_bwd_ws_floats(int rows, int cols);
+// LayerNorm weight / bias gradients of several LayerNorms in one launch: job j adds sum_rows dy * xhat to
+// dw and sum_rows dy to db (either nullable), rows x cols, fixed row order (deterministic)
+struct LnGradJob {
+  const float* dy;
+  const float* xhat;
+  float* dw;
+  float* db;
+};
+int launch_ln_param_grads(const LnGradJob* jobs, int n, int rows, int cols, long long lddy, long long ldxh,
+                          hipStream_t s);
 int launch_layernorm_bwd(const float* dy, long long lddy, const float* y, long long ldy, const float* xhat,
                          long long ldxh, const float* w, const float* rstd, int rows, int cols, int relu,
                          float* dx, long long lddx, float* dw, float* db, float* ws, hipStream_t s);

@@ -6,6 +6,7 @@
 #include <algorithm>
 
 #include "fx_common.h"
+#include "ops.h"
 
 namespace fx {
 namespace {
@@ -24,11 +25,13 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // ---------------------------------------------------------------- LayerNorm
+// y2 (nullable) = y + pos: the decoders' "LayerNorm output + query position" operand written beside y
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* x, long long ldx, const float* r,
                                                      long long ldr, const float* w, const float* b,
                                                      float eps, int rows, int cols, int relu, float* y,
                                                      long long ldy, float* mean_out, float* rstd_out,
-                                                     float* xhat, long long ldxh) {
+                                                     float* xhat, long long ldxh, const float* pos, long long ldp,
+                                                     float* y2, long long ldy2) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -63,6 +66,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* x, long long l
       float o = h * w[c] + b[c];
       if (relu) o = fmaxf(o, 0.f);
       y[(long long)row * ldy + c] = o;
+      if (y2) y2[(long long)row * ldy2 + c] = o + pos[(long long)row * ldp + c];
     }
   }
   if (lane == 0) {
@@ -430,20 +434,81 @@ __global__ __launch_bounds__(256) void l2n_bwd_kernel(const float* y, long long 
 
 }  // namespace
 
+int launch_layernorm_fwd_pos(const float* x, long long ldx, const float* r, long long ldr, const float* w,
+                             const float* b, float eps, int rows, int cols, int relu, float* y, long long ldy,
+                             float* mean, float* rstd, float* xhat, long long ldxh, const float* pos, long long ldp,
+                             float* y2, long long ldy2, hipStream_t s) {
+  FX_REQUIRE(cols > 0 && cols <= 64 * MAXPL, "layernorm: cols must be in (0, 1024]");
+  FX_REQUIRE(!y2 || pos, "layernorm: y + pos needs pos");
+  if (rows == 0) return FX_OK;
+  hipLaunchKernelGGL(ln_fwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, r, ldr, w, b, eps, rows, cols,
+                     relu, y, ldy, mean, rstd, xhat, ldxh, pos, ldp, y2, ldy2);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
 int launch_layernorm_fwd(const float* x, long long ldx, const float* r, long long ldr, const float* w,
                          const float* b, float eps, int rows, int cols, int relu, float* y, long long ldy,
                          float* mean, float* rstd, float* xhat, long long ldxh, hipStream_t s) {
-  FX_REQUIRE(cols > 0 && cols <= 64 * MAXPL, "layernorm: cols must be in (0, 1024]");
-  if (rows == 0) return FX_OK;
-  hipLaunchKernelGGL(ln_fwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, r, ldr, w, b, eps, rows, cols,
-                     relu, y, ldy, mean, rstd, xhat, ldxh);
-  FX_CHECK_HIP(hipGetLastError());
-  return FX_OK;
+  return launch_layernorm_fwd_pos(x, ldx, r, ldr, w, b, eps, rows, cols, relu, y, ldy, mean, rstd, xhat, ldxh,
+                                  nullptr, 0, nullptr, 0, s);
+}
+
+constexpr int LN_GRAD_MAXJOB = 48;
+struct LnGradBatch {
+  LnGradJob job[LN_GRAD_MAXJOB];
+  int n, rows, cols;
+  long long lddy, ldxh;
+};
+
+// one thread per (job, column): the rows summed in order, loads unrolled 8 deep
+__global__ __launch_bounds__(256) void ln_param_grad_kernel(LnGradBatch b) {
+  const int j = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
+  if (j >= b.n || c >= b.cols) return;
+  const LnGradJob& J = b.job[j];
+  float sw = 0.f, sb = 0.f;
+  int r = 0;
+  for (; r + 8 <= b.rows; r += 8) {
+    float d[8], h[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      d[i] = J.dy[(long long)(r + i) * b.lddy + c];
+      h[i] = J.xhat[(long long)(r + i) * b.ldxh + c];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      sw += d[i] * h[i];
+      sb += d[i];
+    }
+  }
+  for (; r < b.rows; ++r) {
+    const float d = J.dy[(long long)r * b.lddy + c];
+    sw += d * J.xhat[(long long)r * b.ldxh + c];
+    sb += d;
+  }
+  if (J.dw) J.dw[c] += sw;
+  if (J.db) J.db[c] += sb;
 }
 
 // frame-level rows: up to 1024 blocks of 4 waves (a wave's rows run one after another, each a load
 // round trip + two wave reductions: 256 blocks left 8 rows per wave at 8192 rows, 58 us)
 constexpr int LN_BWD_MAXBLK = 1024;
+
+int launch_ln_param_grads(const LnGradJob* jobs, int n, int rows, int cols, long long lddy, long long ldxh,
+                          hipStream_t s) {
+  for (int j0 = 0; j0 < n; j0 += LN_GRAD_MAXJOB) {
+    LnGradBatch b{};
+    b.n = std::min(LN_GRAD_MAXJOB, n - j0);
+    for (int j = 0; j < b.n; ++j) b.job[j] = jobs[j0 + j];
+    b.rows = rows;
+    b.cols = cols;
+    b.lddy = lddy;
+    b.ldxh = ldxh;
+    hipLaunchKernelGGL(ln_param_grad_kernel, dim3(cdiv(cols, 256), b.n), dim3(256), 0, s, b);
+    FX_CHECK_HIP(hipGetLastError());
+  }
+  return FX_OK;
+}
 
 long long layernorm_bwd_ws_floats(int rows, int cols) {
   const int nblk = std::min(cdiv(rows, 4), LN_BWD_MAXBLK);

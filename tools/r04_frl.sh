@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
 mkdir -p gpurun_out/frl
-timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -k "mstcn" -x -q --timeout 250 --timeout-method thread > gpurun_out/frl/t.log 2>&1; rc=$?
+timeout -k 10 500 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_decoder.py tests/test_gpu_decoder_ext.py tests/test_gpu_backward.py -x -q --timeout 250 --timeout-method thread > gpurun_out/frl/t.log 2>&1; rc=$?
 tail -3 gpurun_out/frl/t.log; [ $rc -eq 0 ] || exit 3
 for f in 0 1; do FX_MSTCN_FUSED_LAYERS=$f timeout -k 10 120 python -u tools/frl_bench.py 2>&1 | grep -v amdgpu | sed "s/^/fused=$f /" || exit 4; done
 for r in 1 2; do for f in 0 1; do
