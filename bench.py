@@ -54,6 +54,7 @@ HOLDOUT = [51, 53, 61, 67, 56]   # havid_view0_lh_pt_holdout.yaml
 # fx_prof kinds of the X2Y attention cores (capi.cpp fx_x2y_fwd / fx_x2y_bwd); algorithmic bytes per call:
 # query, key and value rows, the logit / probability tiles and the attended features (+ their gradients)
 X2Y_KINDS = {3: "x2y_a2f_fwd", 4: "x2y_a2f_bwd", 5: "x2y_f2a_fwd", 6: "x2y_f2a_bwd"}
+FRL_KIND = 7   # fx_prof kind of the fused MS-TCN layer kernel (mstcn_fused.hip)
 X2Y_NOTES = {"x2y_a2f_fwd": "x2y_a2f_kernel<0> (frames attend to the action tokens: logit, attn, feat in one launch)",
              "x2y_a2f_bwd": "x2y_a2f_kernel<1> + grouped dxv / dxk GEMM launch",
              "x2y_f2a_fwd": "x2y_f2a_chunk_kernel + x2y_f2a_merge_kernel (tokens attend to the frames)",
@@ -315,6 +316,22 @@ def attention_roofline(kernel, ms, fl, by, cnt):
                 tflops=round(fl.value / n / (avg_ms * 1e-3) / 1e12, 2))
 
 
+def fused_layer_roofline(prof, peak):
+    """The fused MS-TCN layer kernel (mstcn_fused.hip: conv + ReLU + 1x1 + residual in one launch, and
+    the fused dX chain of the backward), MFMA-bound: 2 rows F 4F algorithmic FLOPs per launch (the
+    3-tap conv's 3F and the 1x1's F columns); None when the two-GEMM layers ran."""
+    ms, fl, by, cnt = prof
+    n = cnt.value
+    if n <= 0 or ms.value <= 0:
+        return None
+    avg_ms = ms.value / n
+    tf = fl.value / n / (avg_ms * 1e-3) / 1e12
+    return dict(kernel="frl_kernel (fused MS-TCN layer: conv fwd + 1x1 fwd, or dX chain bwd)", bound="mfma",
+                achieved=round(tf, 2), peak=round(peak, 1), unit="TFLOP/s", frac=round(tf / peak, 4),
+                launches=n, avg_launch_ms=round(avg_ms, 5), flops_per_launch=fl.value / n,
+                bytes_per_launch=by.value / n)
+
+
 def cpu_baseline(wl, Ts, videos_seeds, min_seconds=10.0, min_steps=2):
     """The CPU oracle (fp32 PyTorch restatement pinned to the reference) timed on host cores: one
     video per step, full T, forward + prediction + loss + backward with FIXED weights (the same
@@ -474,7 +491,7 @@ def main():
     # capacity of each kind is its launch count in one step, counted on an untimed extra warm-up step,
     # times the sampled steps -- so no event pair spills into the later timed steps.
     psteps = min(args.steps, int(os.environ.get("FX_BENCH_PROF_STEPS", 1)))
-    kinds = [0, 1, 2] + list(X2Y_KINDS)
+    kinds = [0, 1, 2] + list(X2Y_KINDS) + [FRL_KIND]
     for kind in kinds:
         native.check(lib.fx_prof_enable(kind, 4096), "fx_prof_enable")
     step()
@@ -500,6 +517,7 @@ def main():
     ms, fl, by, cnt = collect(0)
     attn_prof = {name: collect(kind) for kind, name in ((1, "fwd"), (2, "bwd"))}
     x2y_prof = {name: collect(kind) for kind, name in X2Y_KINDS.items()}
+    frl_prof = collect(FRL_KIND)
     lib.fx_prof_disable()
     S_after = video_segments(net)
     if world > 1:
@@ -575,7 +593,8 @@ def main():
                                  if default_shape else None),
                         kernel=(f"{SPLIT_KERNEL} (implicit dilated-conv GEMM in fp32 by 3-piece bf16 split: conv fwd "
                                 f"+ conv dX; peak = bf16 dense peak / {SPLIT_PRODUCTS} products)" if split else
-                                "gemm_f32_wide8_kernel (implicit dilated-conv GEMM: conv fwd + conv dX)"),
+                                "gemm_f32_wide8_kernel (implicit dilated-conv GEMM: conv fwd + conv dX; the layers "
+                                "the fused MS-TCN layer kernel runs are in roofline_fused_layer)"),
                         launches=cnt.value, avg_launch_ms=round(avg_ms, 5),
                         flops_per_launch=flops_per_launch,
                         sample=f"HIP events on the first {cnt.value} conv-GEMM launches of the timed region")
@@ -601,7 +620,8 @@ def main():
                                 videos_per_rank=nv, global_batch=world * nv, seq_len=T,
                                 parallelism=f"dp{world}", weights="fixed (no optimizer update in the timed steps)",
                                 tdu_segments=S, tdu_segments_after_timing=S_after),
-                    roofline=roofline, roofline_attention=roofline_attention, train_step_with_adam=adam,
+                    roofline=roofline, roofline_attention=roofline_attention,
+                    roofline_fused_layer=fused_layer_roofline(frl_prof, peak), train_step_with_adam=adam,
                     bf16_mode=bf16, dp_schedule=dp_sched)
         if other is not None:
             line["fp32_f32mfma_mode" if headline_prec == "fp32s" else "fp32_split_mode"] = other

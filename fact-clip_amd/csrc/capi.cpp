@@ -29,7 +29,7 @@ struct ProfState {
   std::vector<double> flops, bytes;
   int used = 0;
 };
-constexpr int kProfKinds = 8;   // 0 conv GEMM, 1 / 2 attention over T fwd / bwd, 3-6 X2Y cores
+constexpr int kProfKinds = 8;   // 0 conv GEMM, 1 / 2 attention over T fwd / bwd, 3-6 X2Y cores, 7 fused MS-TCN layer
 std::mutex g_prof_mu;
 ProfState g_prof[kProfKinds];
 
@@ -488,6 +488,7 @@ const Knobs& knobs() {
     if (const char* p = env("FX_MSTCN_DEFER")) k.mstcn_defer = p[0] != '0';
     if (const char* p = env("FX_SIDE_MAXWG")) k.side_maxwg = std::max(0, std::atoi(p));
     if (const char* p = env("FX_GEMM_ROWPERM")) k.gemm_row_perm = p[0] != '0';
+    if (const char* p = env("FX_FRL_XCD")) k.frl_xcd = std::atoi(p);
     if (const char* p = env("FX_X2Y_FUSED")) k.x2y_fused = p[0] != '0';
     if (const char* p = env("FX_SPLIT_VARIANT")) k.split_variant = std::atoi(p);
     if (const char* p = env("FX_MSTCN_TAIL")) k.mstcn_tail = p[0] != '0';
@@ -606,12 +607,12 @@ int fx_mstcn_fwd(const fx_mstcn_params* p, const float* x, long long ldx, int T,
     float* hn = saved + L.h + (i + 1) * L.rowsF;
     float* zi = saved + L.z + i * L.rowsF;
     if (fused) {   // z = relu(conv(h) + b); h' = h + dropout(z . Wpw^T + b): one kernel (mstcn_fused.hip)
-      prof_begin(0, s);
+      prof_begin(7, s);
       FX_TRY(launch_frl(hi, F, rows, T, layer_dilation(p, i), 1, q.off, q.nvid,
                         workspace + L.wk1 + (long long)i * 3 * F * F, p->b_dil[i], 1, nullptr, 0, zi, F,
                         workspace + L.wk2 + (long long)i * F * F, p->b_pw[i], hi, F, nullptr, 0, hn, F, p->dropout,
                         fx_drop_subseed(p->seed, i), s));
-      prof_end(0, s, 2.0 * rows * F * 4.0 * F, 4.0 * (3.0 * rows * F + 4.0 * F * F));
+      prof_end(7, s, 2.0 * rows * F * 4.0 * F, 4.0 * (3.0 * rows * F + 4.0 * F * F));
       continue;
     }
     // z = relu(dilated_conv(h) + b)      (basic.py:158)
@@ -762,11 +763,11 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
     } else {
       float* dZn = Zb[(NL - i) % 3];
       const float* zn = saved + L.z + (i - 1) * L.rowsF;
-      prof_begin(0, s);
+      prof_begin(7, s);
       FX_TRY(launch_frl(dZi, F, rows, T, layer_dilation(p, i), -1, q.off, q.nvid,
                         ws + L.wk1 + (long long)i * 3 * F * F, nullptr, 0, gU, F, dHi, F,
                         ws + L.wk2 + (long long)(i - 1) * F * F, nullptr, nullptr, 0, zn, F, dZn, F, 0.f, 0, s));
-      prof_end(0, s, 2.0 * rows * F * 4.0 * F, 4.0 * (4.0 * rows * F + 4.0 * F * F));
+      prof_end(7, s, 2.0 * rows * F * 4.0 * F, 4.0 * (4.0 * rows * F + 4.0 * F * F));
       FX_TRY(fork(1));
       FX_TRY(linear_dwdb(dHi, F, zn, F, rows, F, F, g->w_pw[i - 1], g->b_pw[i - 1], 1, spl, sd));
       FX_TRY(conv_dw(i - 1, dZn));
@@ -839,12 +840,12 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
       // alone; the weight gradients of every layer follow as the batched side-stream GEMMs below
       FX_TRY(pw_dx(dHall + (NL - 1) * L.rowsF, NL - 1, dZall + (NL - 1) * L.rowsF, saved + L.z + (NL - 1) * L.rowsF));
       for (int i = NL - 1; i >= 1; --i) {
-        prof_begin(0, s);
+        prof_begin(7, s);
         FX_TRY(launch_frl(dZall + i * L.rowsF, F, rows, T, layer_dilation(p, i), -1, q.off, q.nvid,
                           ws + L.wk1 + (long long)i * 3 * F * F, nullptr, 0, dHall + i * L.rowsF, F,
                           dHall + (i - 1) * L.rowsF, F, ws + L.wk2 + (long long)(i - 1) * F * F, nullptr, nullptr, 0,
                           saved + L.z + (i - 1) * L.rowsF, F, dZall + (i - 1) * L.rowsF, F, 0.f, 0, s));
-        prof_end(0, s, 2.0 * rows * F * 4.0 * F, 4.0 * (4.0 * rows * F + 4.0 * F * F));
+        prof_end(7, s, 2.0 * rows * F * 4.0 * F, 4.0 * (4.0 * rows * F + 4.0 * F * F));
       }
     }
     for (int i = fchain ? 0 : NL - 1; i >= 0; --i) {

@@ -126,6 +126,8 @@ struct Knobs {
   bool gemm_xcd_planes = true;
   bool gemm_nt_store = false;
   bool gemm_row_perm = true;  // FX_GEMM_ROWPERM=0: dilated-conv row tiles in plain order on the XCDs (A/B)
+  int frl_xcd = 2;             // FX_FRL_XCD: fused MS-TCN layer row tiles on the XCDs -- 0 round robin,
+                              // 1 contiguous runs, 2 runs that follow the conv taps (A/B)
   FILE* gemm_log = nullptr; // FX_GEMM_LOG=<file>: one line per GEMM launch (shape census)
   bool gemm_group = true;
   bool side_stream = true;

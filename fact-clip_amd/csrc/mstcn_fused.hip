@@ -47,6 +47,8 @@ struct FrlArgs {
   const float* x;      // phase-1 conv operand rows (M, FN), ld ldx
   long long ldx;
   int dil, dir, T, M;
+  int xcd_runs;        // 1: consecutive row tiles share an XCD (and its L2), see frl_tile
+  int row_perm;        // > 1: the conv taps shift by row_perm whole row tiles (dilation / FR)
   int nsoff;           // > 0: ragged videos, video v owns rows [soff[v], soff[v+1])
   int soff[kMaxSeqF + 1];
   const float* w1p;    // packed (launch_pack_frag) conv weights: [n][tap * FN + c], K = 3 FN
@@ -94,11 +96,29 @@ __device__ __forceinline__ void mma_stage(const float* a, int as, const float4* 
   }
 }
 
+// Row tile of this workgroup.  Workgroups go to the 8 XCDs round robin by dispatch id, so in plain
+// order a tile's neighbours -- whose rows are its conv halo (dilation < FR) or its shifted taps -- sit
+// on other XCDs and every tile fetches its halo / taps through its own L2 again.  xcd_runs: XCD x gets
+// a contiguous run of tiles; row_perm p > 1 (taps shift by p whole tiles): the runs walk the tiles
+// 0, p, 2p, ..., 1, 1 + p, ... so a tile and its shifted taps share the run (the GEMM's block_tile
+// does the same for the dilated-conv GEMMs).
+__device__ __forceinline__ int frl_tile(const FrlArgs& g) {
+  const int id = blockIdx.x;
+  if (!g.xcd_runs) return id;
+  const int nt = gridDim.x, q = nt / 8, rr = nt % 8, x8 = id % 8, i8 = id / 8;
+  int t = (x8 < rr ? x8 * (q + 1) : rr * (q + 1) + (x8 - rr) * q) + i8;
+  if (g.row_perm > 1) {
+    const int per = nt / g.row_perm;
+    t = (t % per) * g.row_perm + t / per;
+  }
+  return t;
+}
+
 __global__ __launch_bounds__(FT) void frl_kernel(FrlArgs g) {
   extern __shared__ float lds[];
   float* V = lds + NSL * A_IMG;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 31, lh = lane >> 5;
-  const int m0 = blockIdx.x * FR;
+  const int m0 = frl_tile(g) * FR;
   constexpr int n1 = 3 * FN / FBK, n2 = FN / FBK, nall = n1 + n2;
   // this thread's activation row (threads 256..511 repeat 0..255: no branch, the compiler counts the
   // outstanding loads exactly; duplicate lanes store equal data) and its position inside its video
@@ -270,6 +290,9 @@ int launch_frl(const float* x, long long ldx, int M, int T, int dil, int dir, co
   a.dir = dir;
   a.T = T > 0 ? T : 1;
   a.M = M;
+  const int nt = cdiv(M, FR), sh = dil / FR;
+  a.xcd_runs = knobs().frl_xcd >= 1 && nt >= 16;
+  a.row_perm = (knobs().frl_xcd >= 2 && dil % FR == 0 && sh > 1 && nt % sh == 0) ? sh : 1;
   a.nsoff = seq_off ? nseq : 0;
   if (seq_off)
     for (int v = 0; v <= nseq; ++v) a.soff[v] = seq_off[v];

@@ -578,9 +578,10 @@ def x2y(mod, X, Y, Xpos, Ypos, rows=None):
 # MS-TCN stack
 # ---------------------------------------------------------------------------
 
-# fx_mstcn_params.fused_layers: the opt-in one-kernel MS-TCN layer (slower than the two tuned GEMMs at
-# the benchmark shape; kept for A/B and its own tests)
-MSTCN_FUSED_LAYERS = os.environ.get("FX_MSTCN_FUSED_LAYERS", "0") == "1"   # A/B knob
+# fx_mstcn_params.fused_layers: the one-kernel MS-TCN layer (mstcn_fused.hip, weights in MFMA fragment
+# order): on by default since round 4 (whole step 14.9 -> 14.5 ms);
+# FX_MSTCN_FUSED_LAYERS=0 selects the two-GEMM layers (A/B knob)
+MSTCN_FUSED_LAYERS = os.environ.get("FX_MSTCN_FUSED_LAYERS", "1") == "1"
 
 
 def _ptr_array(ts):

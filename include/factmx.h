@@ -699,7 +699,10 @@ int fx_get_default_precision(void);
  * (bench.py roofline).  Kinds are enabled independently:
  *   0 = dilated-conv implicit GEMM (conv forward, conv dX),
  *   1 = attention over T forward (tattn_fwd_kernel + split merge),
- *   2 = attention over T backward (tattn_bwd_kernel + split merge).
+ *   2 = attention over T backward (tattn_bwd_kernel + split merge),
+ *   3-6 = X2Y cores (a2f fwd, a2f bwd, f2a fwd, f2a bwd),
+ *   7 = fused MS-TCN layer (frl_kernel: conv + ReLU + 1x1 + residual forward,
+ *       or the fused dX chain backward).
  * fx_prof_enable resets one kind; fx_prof_disable resets all.
  * ---------------------------------------------------------------------- */
 int fx_prof_enable(int kind, int max_events);

@@ -18,3 +18,4 @@ cat gpurun_out/pmc_dominant.json
 # the same FETCH/WRITE passes, averaged over the attention-over-T kernels
 python tools/pmc_dominant.py $OUT "tattn_fwd_kernel" > gpurun_out/pmc_tattn_fwd.json
 python tools/pmc_dominant.py $OUT "tattn_bwd_kernel" > gpurun_out/pmc_tattn_bwd.json
+python tools/pmc_dominant.py $OUT "frl_kernel" > gpurun_out/pmc_frl.json
