@@ -489,6 +489,9 @@ const Knobs& knobs() {
     if (const char* p = env("FX_SIDE_MAXWG")) k.side_maxwg = std::max(0, std::atoi(p));
     if (const char* p = env("FX_GEMM_ROWPERM")) k.gemm_row_perm = p[0] != '0';
     if (const char* p = env("FX_FRL_XCD")) k.frl_xcd = std::atoi(p);
+    if (const char* p = env("FX_FRL_PAIR")) k.frl_pair = p[0] != '0';
+    if (const char* p = env("FX_FRL_PD")) k.frl_pd = std::atoi(p);
+    if (const char* p = env("FX_FRL_ABLATE")) k.frl_ablate = std::atoi(p);
     if (const char* p = env("FX_X2Y_FUSED")) k.x2y_fused = p[0] != '0';
     if (const char* p = env("FX_SPLIT_VARIANT")) k.split_variant = std::atoi(p);
     if (const char* p = env("FX_MSTCN_TAIL")) k.mstcn_tail = p[0] != '0';

@@ -126,6 +126,9 @@ struct Knobs {
   bool gemm_xcd_planes = true;
   bool gemm_nt_store = false;
   bool gemm_row_perm = true;  // FX_GEMM_ROWPERM=0: dilated-conv row tiles in plain order on the XCDs (A/B)
+  bool frl_pair = true;        // FX_FRL_PAIR=0: the fused MS-TCN layer synchronises per 32-deep stage (A/B)
+  int frl_pd = 3;              // FX_FRL_PD=3|5: fused MS-TCN layer weight prefetch distance in stages (A/B)
+  int frl_ablate = 0;          // FX_FRL_ABLATE: diagnostic timing ablations of the fused layer (wrong results)
   int frl_xcd = 2;             // FX_FRL_XCD: fused MS-TCN layer row tiles on the XCDs -- 0 round robin,
                               // 1 contiguous runs, 2 runs that follow the conv taps (A/B)
   FILE* gemm_log = nullptr; // FX_GEMM_LOG=<file>: one line per GEMM launch (shape census)

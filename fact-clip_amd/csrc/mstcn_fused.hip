@@ -38,15 +38,18 @@ constexpr int AS = FBK + 4;      // LDS row stride of the activation stage image
 constexpr int VS = FN + 4;       // LDS row stride of the phase-1 tile
 constexpr int A_IMG = FR * AS;
 constexpr int NSL = 3;           // activation ring depth
-constexpr int PD = 3;            // weight fragments: stages loaded ahead of their use
-constexpr int NB = PD + 1;       // weight register sets
+// weight fragments are loaded PD stages ahead of their use into NB = PD + 1 register sets (kernel
+// template parameter: 3 or 5, FX_FRL_PD)
 constexpr int LDS_FLOATS = NSL * A_IMG + FR * VS;
+constexpr int LDS_FLOATS_PAIR = 2 * NSL * A_IMG + FR * VS;
 constexpr int kMaxSeqF = 16;     // ragged videos per launch
 
 struct FrlArgs {
   const float* x;      // phase-1 conv operand rows (M, FN), ld ldx
   long long ldx;
   int dil, dir, T, M;
+  int ablate;          // diagnostic (FX_FRL_ABLATE, wrong results): 1 no weight loads after the prologue,
+                       // 2 no activation loads after it, 4 no ring barriers, 8 no epilogue global traffic
   int xcd_runs;        // 1: consecutive row tiles share an XCD (and its L2), see frl_tile
   int row_perm;        // > 1: the conv taps shift by row_perm whole row tiles (dilation / FR)
   int nsoff;           // > 0: ragged videos, video v owns rows [soff[v], soff[v+1])
@@ -79,6 +82,23 @@ __device__ __forceinline__ void load_b(const float* wp, int st, int w, int lane,
   const float* base = wp + ((long long)(st * 8 + w) * 4) * 256 + lane * 4;
 #pragma unroll
   for (int q = 0; q < 4; ++q) b[q] = ld4(base + q * 256);
+}
+
+// A fragments of one 32-deep stage from LDS rows `a` (row stride as): lane (li, lh) takes row li, k 16 lh ..
+__device__ __forceinline__ void lds_frag(const float* a, int as, int li, int lh, float4* fa) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) fa[q] = ld4(a + li * as + lh * 16 + q * 4);
+}
+
+// the 16 MFMAs of one stage from fragments already in registers
+__device__ __forceinline__ void mma_frag(const float4* fa, const float4* fb, f32x16& acc) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, fb[q].x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, fb[q].y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, fb[q].z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, fb[q].w, acc, 0, 0, 0);
+  }
 }
 
 // 16 MFMAs of one 32-deep stage: A rows from `a` (row stride as), B = this wave's fragments; the
@@ -114,15 +134,21 @@ __device__ __forceinline__ int frl_tile(const FrlArgs& g) {
   return t;
 }
 
+// PAIR: the activation ring holds stage PAIRS -- threads 0..255 stage the even stage of a pair, 256..511
+// the odd one, and the workgroup synchronises once per 64 k instead of once per 32 k; the 1x1 phase reads
+// the static LDS tile V without any barrier.  !PAIR: one barrier per 32-deep stage in both phases.
+template <bool PAIR, int PD>
 __global__ __launch_bounds__(FT) void frl_kernel(FrlArgs g) {
+  constexpr int NB = PD + 1;
   extern __shared__ float lds[];
-  float* V = lds + NSL * A_IMG;
+  float* V = lds + (PAIR ? 2 : 1) * NSL * A_IMG;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 31, lh = lane >> 5;
   const int m0 = frl_tile(g) * FR;
   constexpr int n1 = 3 * FN / FBK, n2 = FN / FBK, nall = n1 + n2;
-  // this thread's activation row (threads 256..511 repeat 0..255: no branch, the compiler counts the
-  // outstanding loads exactly; duplicate lanes store equal data) and its position inside its video
-  const int ar = (tid & 255) >> 3, k4 = (tid & 7) * 4;
+  static_assert(n1 % 2 == 0, "stage pairs");
+  // this thread's activation row (!PAIR: threads 256..511 repeat 0..255: no branch, the compiler counts
+  // the outstanding loads exactly; duplicate lanes store equal data) and its position inside its video
+  const int ar = (tid & 255) >> 3, k4 = (tid & 7) * 4, half = PAIR ? tid >> 8 : 0;
   const int r = m0 + ar;
   int rpos, rlen;
   if (g.nsoff > 0) {
@@ -160,18 +186,10 @@ __global__ __launch_bounds__(FT) void frl_kernel(FrlArgs g) {
   float4 pa[2];                        // activation rows of stage st + 2 (set st & 1)
   bool pok[2];
   auto load_w = [&](int st) {
+    if ((g.ablate & 1) && st >= PD) return;
     if (st < n1) load_b(g.w1p, st, w, lane, pb[st % NB]);
     else if (st < nall) load_b(g.w2p, st - n1, w, lane, pb[st % NB]);
   };
-#pragma unroll
-  for (int st = 0; st < PD; ++st) load_w(st);
-  load_a(0, pa[0], pok[0]);
-  load_a(1, pa[1], pok[1]);
-  store_a(lds, pa[0], pok[0]);
-  store_a(lds + A_IMG, pa[1], pok[1]);
-  load_a(2, pa[0], pok[0]);
-  load_a(3, pa[1], pok[1]);
-  __syncthreads();
   // stage st: multiply slot st % 3 (phase 2: the LDS tile V); store the activation rows of stage st + 2
   // (loaded two stages ago) into slot (st + 2) % 3; load stage st + 4's rows and stage st + PD's weights
   auto step = [&](int st, const float* a, int as) {
@@ -184,11 +202,71 @@ __global__ __launch_bounds__(FT) void frl_kernel(FrlArgs g) {
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
   };
+  // epilogue operands (phase-1 residual; phase-2 residual and gate), loaded into registers before the
+  // MFMAs they follow so their latency hides behind them
+  const int ecol = w * 32 + li;
+  float r1[16], res[16], gat[16];
+  auto erow = [&](int q) { return min(m0 + (q & 3) + 8 * (q >> 2) + 4 * lh, g.M - 1); };
+  auto load_r1 = [&]() {
 #pragma unroll
-  for (int st = 0; st < n1; ++st) step(st, nullptr, 0);
+    for (int q = 0; q < 16; ++q) r1[q] = g.resid1 ? g.resid1[(long long)erow(q) * g.ldr1 + ecol] : 0.f;
+  };
+#pragma unroll
+  for (int st = 0; st < PD; ++st) load_w(st);
+  if constexpr (PAIR) {
+    // pair p of stages (2p, 2p + 1) in ring slot p % NSL; this thread's stage 2p + half
+    constexpr int np = n1 / 2;
+    auto slot = [&](int p) { return lds + (p % NSL) * 2 * A_IMG; };
+    load_a(half, pa[0], pok[0]);
+    load_a(2 + half, pa[1], pok[1]);
+    store_a(slot(0) + half * A_IMG, pa[0], pok[0]);
+    store_a(slot(1) + half * A_IMG, pa[1], pok[1]);
+    load_a(4 + half, pa[0], pok[0]);
+    __syncthreads();
+    // A fragments of pair p are read from LDS one pair ahead (during pair p - 1's MFMAs): slot p % NSL
+    // was written before the barrier that ended pair p - 2, so the read needs no extra barrier, and
+    // after each barrier the MFMAs start on fragments already in registers
+    float4 fa[2][2][4];   // [pair parity][stage of the pair][q]
+    lds_frag(slot(0), AS, li, lh, fa[0][0]);
+    lds_frag(slot(0) + A_IMG, AS, li, lh, fa[0][1]);
+#pragma unroll
+    for (int p = 0; p < np; ++p) {
+      if (p + 1 < np) {
+        lds_frag(slot(p + 1), AS, li, lh, fa[(p + 1) & 1][0]);
+        lds_frag(slot(p + 1) + A_IMG, AS, li, lh, fa[(p + 1) & 1][1]);
+      } else {
+        load_r1();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mma_frag(fa[p & 1][0], pb[(2 * p) % NB], acc);
+      __builtin_amdgcn_sched_barrier(0);
+      load_w(2 * p + PD);
+      __builtin_amdgcn_sched_barrier(0);
+      mma_frag(fa[p & 1][1], pb[(2 * p + 1) % NB], acc);
+      __builtin_amdgcn_sched_barrier(0);
+      // pair p + 2 (loaded during the previous pair) into the slot pair p - 1 used (its fragments were
+      // read during pair p - 2); fetch pair p + 3
+      if (p + 2 < np) store_a(slot(p + 2) + half * A_IMG, pa[0], pok[0]);
+      if (p + 3 < np && !(g.ablate & 2)) load_a(2 * (p + 3) + half, pa[0], pok[0]);
+      load_w(2 * p + 1 + PD);
+      __builtin_amdgcn_sched_barrier(0);
+      if (!(g.ablate & 4)) __syncthreads();
+    }
+  } else {
+    load_a(0, pa[0], pok[0]);
+    load_a(1, pa[1], pok[1]);
+    store_a(lds, pa[0], pok[0]);
+    store_a(lds + A_IMG, pa[1], pok[1]);
+    load_a(2, pa[0], pok[0]);
+    load_a(3, pa[1], pok[1]);
+    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < n1; ++st) step(st, nullptr, 0);
+  }
+  if (!PAIR) load_r1();
   // ---------------- phase-1 epilogue: out1 and the LDS tile V
   {
-    const int col = w * 32 + li;
+    const int col = ecol;
     const float bv = g.bias1 ? g.bias1[col] : 0.f;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -196,26 +274,41 @@ __global__ __launch_bounds__(FT) void frl_kernel(FrlArgs g) {
       const int gr = m0 + row;
       float v = acc[q] + bv;
       if (g.relu1) v = fmaxf(v, 0.f);
-      if (g.resid1 && gr < g.M) v += g.resid1[(long long)gr * g.ldr1 + col];
-      if (gr < g.M) g.out1[(long long)gr * g.ldo1 + col] = v;
+      v += r1[q];
+      if (gr < g.M && !(g.ablate & 8)) g.out1[(long long)gr * g.ldo1 + col] = v;
       V[row * VS + col] = v;
       acc[q] = 0.f;
     }
   }
+  auto load_res = [&]() {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      res[q] = (g.resid2 && !(g.ablate & 8)) ? g.resid2[(long long)erow(q) * g.ldr2 + ecol] : 0.f;
+      gat[q] = (g.gate2 && !(g.ablate & 8)) ? g.gate2[(long long)erow(q) * g.ldg2 + ecol] : 1.f;
+    }
+  };
+  load_res();
   __syncthreads();
   // ---------------- phase 2: 1x1 GEMM from the LDS tile, K = FN
+  if constexpr (PAIR) {
+    float4 fv[2][4];      // V fragments one stage ahead
+    lds_frag(V, VS, li, lh, fv[0]);
 #pragma unroll
-  for (int j = 0; j < n2; ++j) step(n1 + j, V + j * FBK, VS);
-  // ---------------- phase-2 epilogue
-  const int col = w * 32 + li;
-  const float bv = g.bias2 ? g.bias2[col] : 0.f;
-  float res[16], gat[16];
+    for (int j = 0; j < n2; ++j) {
+      if (j + 1 < n2) lds_frag(V + (j + 1) * FBK, VS, li, lh, fv[(j + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      mma_frag(fv[j & 1], pb[(n1 + j) % NB], acc);
+      __builtin_amdgcn_sched_barrier(0);
+      load_w(n1 + j + PD);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int gr = min(m0 + (q & 3) + 8 * (q >> 2) + 4 * lh, g.M - 1);
-    res[q] = g.resid2 ? g.resid2[(long long)gr * g.ldr2 + col] : 0.f;
-    gat[q] = g.gate2 ? g.gate2[(long long)gr * g.ldg2 + col] : 1.f;
+    for (int j = 0; j < n2; ++j) step(n1 + j, V + j * FBK, VS);
   }
+  // ---------------- phase-2 epilogue
+  const int col = ecol;
+  const float bv = g.bias2 ? g.bias2[col] : 0.f;
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int gr = m0 + (q & 3) + 8 * (q >> 2) + 4 * lh;
@@ -224,7 +317,7 @@ __global__ __launch_bounds__(FT) void frl_kernel(FrlArgs g) {
       v = fx_drop_bits(g.drop_seed, (unsigned long long)gr * FN + col) >= g.drop_thr ? v * g.drop_scale : 0.f;
     v += res[q];
     if (!(gat[q] > 0.f)) v = 0.f;
-    if (gr < g.M) g.out2[(long long)gr * g.ldo2 + col] = v;
+    if (gr < g.M && (!(g.ablate & 8) || v == 12345.f)) g.out2[(long long)gr * g.ldo2 + col] = v;
   }
 }
 
@@ -279,8 +372,12 @@ int launch_frl(const float* x, long long ldx, int M, int T, int dil, int dir, co
              "frl: needs F = 256 and 16-byte aligned rows");
   FX_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "frl: dropout must be in [0, 1)");
   static const bool attr = [] {
-    return hipFuncSetAttribute((const void*)frl_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               LDS_FLOATS * (int)sizeof(float)) == hipSuccess;
+    return hipFuncSetAttribute((const void*)frl_kernel<false, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               LDS_FLOATS * (int)sizeof(float)) == hipSuccess &&
+           hipFuncSetAttribute((const void*)frl_kernel<true, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               LDS_FLOATS_PAIR * (int)sizeof(float)) == hipSuccess &&
+           hipFuncSetAttribute((const void*)frl_kernel<true, 5>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               LDS_FLOATS_PAIR * (int)sizeof(float)) == hipSuccess;
   }();
   FX_REQUIRE(attr, "frl: cannot raise the LDS limit");
   FrlArgs a{};
@@ -291,6 +388,7 @@ int launch_frl(const float* x, long long ldx, int M, int T, int dil, int dir, co
   a.T = T > 0 ? T : 1;
   a.M = M;
   const int nt = cdiv(M, FR), sh = dil / FR;
+  a.ablate = knobs().frl_ablate;
   a.xcd_runs = knobs().frl_xcd >= 1 && nt >= 16;
   a.row_perm = (knobs().frl_xcd >= 2 && dil % FR == 0 && sh > 1 && nt % sh == 0) ? sh : 1;
   a.nsoff = seq_off ? nseq : 0;
@@ -314,7 +412,12 @@ int launch_frl(const float* x, long long ldx, int M, int T, int dil, int dir, co
   a.drop_thr = drop_p > 0.f ? std::max(fx_drop_thresh(drop_p), 1u) : 0u;
   a.drop_scale = 1.f / (1.f - drop_p);
   a.drop_seed = drop_seed;
-  hipLaunchKernelGGL(frl_kernel, dim3(cdiv(M, FR)), dim3(FT), LDS_FLOATS * sizeof(float), s, a);
+  if (!knobs().frl_pair)
+    hipLaunchKernelGGL((frl_kernel<false, 3>), dim3(nt), dim3(FT), LDS_FLOATS * sizeof(float), s, a);
+  else if (knobs().frl_pd == 5)
+    hipLaunchKernelGGL((frl_kernel<true, 5>), dim3(nt), dim3(FT), LDS_FLOATS_PAIR * sizeof(float), s, a);
+  else
+    hipLaunchKernelGGL((frl_kernel<true, 3>), dim3(nt), dim3(FT), LDS_FLOATS_PAIR * sizeof(float), s, a);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }

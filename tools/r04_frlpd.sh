@@ -1,0 +1,11 @@
+# Round 4: weight prefetch distance of the fused MS-TCN layer kernel (FX_FRL_PD 3/5).
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
+O=gpurun_out/frlpd; rm -rf $O; mkdir -p $O
+FX_FRL_PD=5 timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -k "mstcn" -x -q --timeout 200 --timeout-method thread > $O/t.log 2>&1 || { tail -20 $O/t.log; exit 2; }
+tail -1 $O/t.log
+for x in 3 5 3 5; do FX_FRL_PD=$x timeout -k 10 120 python -u tools/frl_bench.py 2>&1 | grep -v amdgpu | sed "s/^/pd=$x /" || exit 3; done
+for r in 1 2; do for x in 3 5; do
+  FX_FRL_PD=$x timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-bf16 --no-dp-overhead --adam-steps 10 > $O/b$x$r.json 2>/dev/null || exit 5
+  python -c "import json;d=json.loads(open('$O/b$x$r.json').read().splitlines()[-1]);f=d['roofline_fused_layer'];print('pd=$x', d['ms_per_step'], d['train_step_with_adam']['ms_per_step'], f['avg_launch_ms'], f['frac'])"
+done; done
