@@ -39,7 +39,10 @@ sys.path.insert(0, os.path.join(ROOT, "fact-clip_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-DOMINANT_KERNEL = "gemm_f32_wide8_kernel<1, 0, 0>"   # rocprofv3 name: fx::(anonymous namespace)::gemm_f32_wide8_kernel<1, 0, 0>
+# PMC summaries under profiles/ (tools/pmc_dominant.sh): the fused MS-TCN layer kernel (the dominant
+# kernel since round 4) in pmc_dominant.json, the dilated-conv GEMM in pmc_conv_gemm.json
+CONV_KERNEL = "gemm_f32_wide8_kernel<1, 0, 0>"   # rocprofv3 name: fx::(anonymous namespace)::gemm_f32_wide8_kernel<1, 0, 0>
+FRL_KERNEL = "frl_kernel"
 METRIC = "frames/sec FACT_CLIP fwd+bwd, T=4096 D=2048 Nact=32, at 1/2/4/8 GPUs"
 METRIC_BREAKFAST = "frames/sec FACT fwd+bwd, Breakfast dims T=512 D=2048 Nact=60 (BASELINE configs[0])"
 METRIC_SHIPPED = ("frames/sec FACT_CLIP fwd+bwd, havid_view0_lh_pt_holdout.yaml as shipped (ntoken 75, dropout 0.2, "
@@ -587,17 +590,25 @@ def main():
         # split arithmetic: the matrix cores' bound is the bf16 dense peak over the 6 piece products
         # (fp32 FLOPs counted once); f32 MFMA: the f32 matrix peak
         peak = BF16_MFMA_PEAK_TFLOPS / SPLIT_PRODUCTS if split else F32_MFMA_PEAK_TFLOPS
-        roofline = dict(bound="mfma", achieved=round(achieved, 2), peak=round(peak, 1), unit="TFLOP/s",
+        conv_roofline = dict(bound="mfma", achieved=round(achieved, 2), peak=round(peak, 1), unit="TFLOP/s",
                         frac=round(achieved / peak, 4),
-                        traffic=(traffic_from_profiles(SPLIT_KERNEL if split else DOMINANT_KERNEL)
+                        traffic=(traffic_from_profiles(SPLIT_KERNEL if split else CONV_KERNEL,
+                                                       "pmc_split.json" if split else "pmc_conv_gemm.json")
                                  if default_shape else None),
                         kernel=(f"{SPLIT_KERNEL} (implicit dilated-conv GEMM in fp32 by 3-piece bf16 split: conv fwd "
                                 f"+ conv dX; peak = bf16 dense peak / {SPLIT_PRODUCTS} products)" if split else
-                                "gemm_f32_wide8_kernel (implicit dilated-conv GEMM: conv fwd + conv dX; the layers "
-                                "the fused MS-TCN layer kernel runs are in roofline_fused_layer)"),
+                                "gemm_f32_wide8_kernel (implicit dilated-conv GEMM: conv fwd + conv dX of the layers "
+                                "the fused MS-TCN layer kernel does not run)"),
                         launches=cnt.value, avg_launch_ms=round(avg_ms, 5),
                         flops_per_launch=flops_per_launch,
                         sample=f"HIP events on the first {cnt.value} conv-GEMM launches of the timed region")
+        # the dominant kernel by measured time in the sampled step: the fused MS-TCN layer when it ran
+        frl_roofline = fused_layer_roofline(frl_prof, F32_MFMA_PEAK_TFLOPS)
+        if frl_roofline is not None:
+            frl_roofline["traffic"] = traffic_from_profiles(FRL_KERNEL) if default_shape else None
+            frl_roofline["sample"] = (f"HIP events on the first {frl_roofline['launches']} fused-layer launches of "
+                                      "the timed region")
+        roofline = (frl_roofline if frl_roofline is not None and frl_prof[0].value > ms.value else conv_roofline)
         roofline_attention = {name: attention_roofline(f"tattn_{name}_kernel (+ tattn_merge_kernel over T splits)", *v)
                               for name, v in attn_prof.items()}
         for name, r in roofline_attention.items():
@@ -621,7 +632,7 @@ def main():
                                 parallelism=f"dp{world}", weights="fixed (no optimizer update in the timed steps)",
                                 tdu_segments=S, tdu_segments_after_timing=S_after),
                     roofline=roofline, roofline_attention=roofline_attention,
-                    roofline_fused_layer=fused_layer_roofline(frl_prof, peak), train_step_with_adam=adam,
+                    roofline_conv_gemm=conv_roofline, roofline_fused_layer=frl_roofline, train_step_with_adam=adam,
                     bf16_mode=bf16, dp_schedule=dp_sched)
         if other is not None:
             line["fp32_f32mfma_mode" if headline_prec == "fp32s" else "fp32_split_mode"] = other

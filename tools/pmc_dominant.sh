@@ -13,9 +13,10 @@ for set in "FETCH_SIZE" "WRITE_SIZE" \
   timeout -s KILL 240 rocprofv3 --pmc $set -d $OUT/p$i -o p$i --output-format csv -- \
     python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-bf16 > $OUT/p$i.log 2>&1 || { echo "pass $i ($set) failed"; tail -5 $OUT/p$i.log; exit 1; }
 done
-python tools/pmc_dominant.py $OUT "${KERNEL:-gemm_f32_wide8_kernel<1, 0, 0>}" > gpurun_out/pmc_dominant.json
+python tools/pmc_dominant.py $OUT "${KERNEL:-frl_kernel}" > gpurun_out/pmc_dominant.json
+# the dilated-conv GEMM (the dominant kernel before the fused layer became the default)
+python tools/pmc_dominant.py $OUT "gemm_f32_wide8_kernel<1, 0, 0>" > gpurun_out/pmc_conv_gemm.json
 cat gpurun_out/pmc_dominant.json
 # the same FETCH/WRITE passes, averaged over the attention-over-T kernels
 python tools/pmc_dominant.py $OUT "tattn_fwd_kernel" > gpurun_out/pmc_tattn_fwd.json
 python tools/pmc_dominant.py $OUT "tattn_bwd_kernel" > gpurun_out/pmc_tattn_bwd.json
-python tools/pmc_dominant.py $OUT "frl_kernel" > gpurun_out/pmc_frl.json
