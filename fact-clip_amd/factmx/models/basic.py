@@ -351,12 +351,17 @@ def decoder_dropout(dec):
     """(branch p, attention p) of a decoder's layers: the residual-branch / FFN-hidden nn.Dropout p and
     the MultiheadAttention probability dropout (basic.py:398-412, 457-478: every layer is a clone of one
     layer, so one value each); None when the layers disagree."""
-    br, at = set(), set()
-    for lyr in dec.layers:
-        br.update(float(m.p) for m in lyr.modules() if isinstance(m, nn.Dropout))
-        at.add(float(lyr.multihead_attn.dropout))
-        if hasattr(lyr, "self_attn"):
-            at.add(float(lyr.self_attn.dropout))
+    # the Dropout / attention modules of every layer, found once per layer set (the p values are read
+    # on every call: a caller may change them between steps)
+    key = tuple(id(lyr) for lyr in dec.layers)
+    mods = dec.__dict__.get("_fx_drop_mods")
+    if mods is None or mods[0] != key:
+        drops = [m for lyr in dec.layers for m in lyr.modules() if isinstance(m, nn.Dropout)]
+        attns = [a for lyr in dec.layers for a in ((lyr.multihead_attn, lyr.self_attn) if hasattr(lyr, "self_attn")
+                                                   else (lyr.multihead_attn,))]
+        mods = dec.__dict__["_fx_drop_mods"] = (key, drops, attns)
+    br = {float(m.p) for m in mods[1]}
+    at = {float(a.dropout) for a in mods[2]}
     if len(br) > 1 or len(at) > 1:
         return None
     return (br.pop() if br else 0.0), (at.pop() if at else 0.0)

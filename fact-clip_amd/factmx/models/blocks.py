@@ -48,6 +48,15 @@ class FeatureProjection(nn.Module):
         return y.reshape(*shp[:-1], self.clip_dim)
 
 
+def _set_side(blk, rec):
+    """setattr(blk, k, v) for the per-video side-channel values, straight into the instance dict (the
+    lazily evaluated ones under their property's key): nn.Module.__setattr__ costs ~3 us a call and a
+    step restores ~30 of them on the host's critical path."""
+    d = blk.__dict__
+    for k, val in rec.items():
+        d[_LAZY_KEYS.get(k, k)] = val
+
+
 class _Lazy:
     """A side-channel value computed on first read (frame-level gathers of segment attention that
     only evaluation code reads)."""
@@ -57,8 +66,12 @@ class _Lazy:
         self.fn = fn
 
 
+_LAZY_KEYS = {}
+
+
 def _lazy_attr(name):
     key = "_lz_" + name
+    _LAZY_KEYS[name] = key
 
     def get(self):
         d = self.__dict__
@@ -195,7 +208,7 @@ class InputBlock(Block):
         fc, ac, ao = vb.frames(f_cl), vb.tokens(a_cl), vb.tokens(a_out)
         self._vrec = [dict(frame_clogit=fc[v].unsqueeze(1), action_clogit=ac[v].unsqueeze(1),
                            action_feature=ao[v][:, :-n].unsqueeze(1)) for v in range(vb.nvid)]
-        self._bt = dict(f_cl=f_cl, a_cl=a_cl)
+        self.__dict__["_bt"] = dict(f_cl=f_cl, a_cl=a_cl)
         return f_out, a_out
 
     def compute_loss(self, criterion, match=None):
@@ -242,9 +255,11 @@ class UpdateBlock(Block):
         a_out, a_cl = fxf.process_feature(a, self.nclass + 1)
         f, a2f_lg, a2f_at = fxf.x2y(a2f, a_out, f2, apos if a2f.kq_pos else None, fpos if a2f.kq_pos else None,
                                     rows=(vb.a_off, vb.f_off))
-        if vb.on_a2f is not None and vb.last is self:
-            vb.on_a2f(vb, a_cl, a2f_at)         # the loss phase's matching starts here (vloss.EarlyMatch)
         f = _frame_branch_batch(self.frame_branch, f, vb)
+        if vb.on_a2f is not None and vb.last is self:
+            # the loss phase's matching starts here (vloss.EarlyMatch): its host work runs while the
+            # device works through the frame branch just issued, its cost launch queues behind it
+            vb.on_a2f(vb, a_cl, a2f_at)
         f_out, f_cl = fxf.process_feature(f, self.nclass)
         n, Q = self.nclass + 1, vb.Q
         recs = []
@@ -257,8 +272,8 @@ class UpdateBlock(Block):
                              action_feature=ao[v][:, :-n].unsqueeze(1),
                              f2a_attn=fat[v].view(1, Q, T), a2f_attn=aat[v].view(1, T, Q),
                              f2a_attn_logit=flg[v].view(1, Q, T), a2f_attn_logit=alg[v].view(1, T, Q)))
-        self._vrec = recs
-        self._bt = dict(f_cl=f_cl, a_cl=a_cl, f2a_lg=f2a_lg, a2f_lg=a2f_lg, a2f_at=a2f_at)
+        self.__dict__["_vrec"] = recs     # (plain attributes: no nn.Module.__setattr__ walk)
+        self.__dict__["_bt"] = dict(f_cl=f_cl, a_cl=a_cl, f2a_lg=f2a_lg, a2f_lg=a2f_lg, a2f_at=a2f_at)
         return f_out, a_out
 
     def compute_loss(self, criterion, match=None):
@@ -346,11 +361,11 @@ class UpdateBlockTDU(Block):
         a_out, a_cl = fxf.process_feature(a, self.nclass + 1)
         sg, a2f_lg, a2f_at = fxf.x2y(a2f, a_out, seg_out, apos if a2f.kq_pos else None,
                                      seg_pos if a2f.kq_pos else None, rows=(vb.a_off, s_off))
-        if vb.on_a2f is not None and vb.last is self:
-            vb.on_a2f(vb, a_cl, a2f_at, (s_off, local))
         lin = self.sf_merge[0]
         f = fxf.SegMergeFn.apply(sg, f2, gid, gst, gen, lin.weight, lin.bias)
         f = _frame_branch_batch(self.frame_branch, f, vb)
+        if vb.on_a2f is not None and vb.last is self:
+            vb.on_a2f(vb, a_cl, a2f_at, (s_off, local))     # (see UpdateBlock.forward_batch)
         f_out, f_cl = fxf.process_feature(f, self.nclass)
         n, Q = self.nclass + 1, vb.Q
         recs = []
@@ -371,8 +386,8 @@ class UpdateBlockTDU(Block):
                                             .transpose(2, 1)),
                              a2f_attn_logit=alg[v].view(1, Sv, Q),
                              a2f_attn=_Lazy(lambda t=tdu, a=a2f_at_v: t.attn_seg2frame(a[0]))))
-        self._vrec = recs
-        self._bt = dict(f_cl=f_cl, a_cl=a_cl, f2a_lg=f2a_lg, a2f_lg=a2f_lg, a2f_at=a2f_at, seg_cl=seg_cl, S=S,
+        self.__dict__["_vrec"] = recs     # (plain attributes: no nn.Module.__setattr__ walk)
+        self.__dict__["_bt"] = dict(f_cl=f_cl, a_cl=a_cl, f2a_lg=f2a_lg, a2f_lg=a2f_lg, a2f_at=a2f_at, seg_cl=seg_cl, S=S,
                         s_off=s_off, local=local)
         return f_out, a_out
 
@@ -475,8 +490,7 @@ class _FACTBase(nn.Module):
 
         def restore(v):
             for blk in self.block_list:
-                for k, val in blk._vrec[v].items():
-                    setattr(blk, k, val)
+                _set_side(blk, blk._vrec[v])
             if proj_v is not None:
                 self.projected_frame_embeddings = proj_v[v].unsqueeze(1)
         return restore

@@ -392,10 +392,11 @@ def run(net, vb, compute_loss, early=None):
         return [{"pred": host[fo[v]:fo[v + 1]].astype(np.int64)} for v in range(nvid)]
 
     assert early is not None and early.done, "the last block did not run the early matching stage"
-    matches = early.matches(Q)
-    big = [v for v, (ai, _) in enumerate(matches) if len(ai) > nx.LOSS_MAXK]
-    if big:      # e.g. o2m matching (every ground-truth segment paired, loss.py:155-193) past 512 segments
-        raise TableTooLarge(big)
+    # Everything that does not depend on the matching is built first, while the device still works
+    # through the end of the forward: the term table with room for the matched columns (K <= G
+    # segments of the video), the structs, the scratch layout, and the prediction launch.  Only then
+    # does the host wait for the match costs; after the Hungarian it fills the token targets and the
+    # matched columns, sets K and the token-CE normaliser, sends the table and launches the loss.
     labs, gts, G, gt_off, lab_off = early.labs, early.gts, early.G, early.gt_off, early.lab_off
     cw, cw_off, base = early.cw, early.cw_off, early.base
 
@@ -429,24 +430,29 @@ def run(net, vb, compute_loss, early=None):
         con_on.append(bool((y != -1).any()))
         y_con.append(y)
 
+    # the predictions (no matching needed): own small table, launched before the wait
+    pke = _Pack()
+    va_off, va = eval_structs(pke)
+    pke.alloc(dev)
+    pke.send()
+    nx.check(lib.fx_eval_pred(ctypes.addressof(va), pke.base + va_off, nvid, float(cfg.FACT.mwt), nx.ptr(pred),
+                              nx.stream()), "fx_eval_pred")
+
     pk2 = _Pack()
-    va_off, va = eval_structs(pk2)
-    tgt_off, sw_list = [], []
+    # per video: token targets (Q) and the matched columns (capacity G[v] >= K), filled after matching
+    tgt_arr = [np.full(Q, C1 - 1, dtype=np.int32) for _ in range(nvid)]
+    tgt_off = [pk2.array(t, np.int32) for t in tgt_arr]
+    tgt_arr = [pk2.items[-nvid + v][1] for v in range(nvid)]     # the buffers pk2 sends
+    kcap = [max(int(G[v]), 1) for v in range(nvid)]
+    sw_arr, sw_list = [], []
     for v in range(nvid):
-        ai, si = matches[v]
-        tgt = np.full(Q, C1 - 1, dtype=np.int32)
-        tgt[ai] = gts[v][2][si]
-        tgt_off.append((pk2.array(tgt, np.int32), float(cw[tgt].sum())))
-        swn = segment_weights(mc, gts[v][2])
-        K = len(ai)
-        if len(swn) not in (K, 1):
-            raise RuntimeError(f"cross_attn_loss: {K} matched columns vs {len(swn)} segment weights")
-        if K > nx.LOSS_MAXK:
-            raise nx.FactmxNativeError(f"video {v}: {K} matched token/segment pairs > FX_LOSS_MAXK "
-                                       f"({nx.LOSS_MAXK}) of the fused loss table")
-        ksw = np.asarray([float(swn[i if len(swn) == K else 0]) for i in range(K)], dtype=np.float32)
-        sw_list.append((pk2.array(ai, np.int32), pk2.array(gts[v][0][si], np.int32),
-                        pk2.array(gts[v][1][si], np.int32), pk2.array(ksw, np.float32)))
+        arrs = []
+        offs = []
+        for dt in (np.int32, np.int32, np.int32, np.float32):
+            offs.append(pk2.array(np.zeros(kcap[v], dtype=dt), dt))
+            arrs.append(pk2.items[-1][1])
+        sw_arr.append(arrs)
+        sw_list.append(tuple(offs))
     ycon_off = [pk2.array(y, np.int32) if y is not None and con_on[v] else None for v, y in enumerate(y_con)]
 
     inputs, grads, gidx = [], [], {}
@@ -460,6 +466,7 @@ def run(net, vb, compute_loss, early=None):
         return grads[gidx[k]]
 
     specs = []       # (block index or -1 for InfoNCE, video, dict of LossTerm fields, scratch sizes)
+    tok_terms, attn_terms = [], []     # (term index, video): fields set after the matching
     scratch = [0]
 
     def add(k, v, f, n_lse, n_lse2, n_colz):
@@ -468,6 +475,7 @@ def run(net, vb, compute_loss, early=None):
             offs.append(scratch[0])
             scratch[0] += (max(n, 1) + 3) & ~3        # 16-byte aligned slots
         specs.append((k, v, f, offs))
+        return len(specs) - 1
 
     for k, blk in enumerate(blocks):
         bt = blk._bt
@@ -482,15 +490,14 @@ def run(net, vb, compute_loss, early=None):
             add(k, v, dict(kind=nx.TERM_CLASS, R=T, C=C, x=_ptr_rows(f_cl, fo[v], C), sr=C, sc=1,
                            dx=_ptr_rows(gf, fo[v], C), dsr=C, dsc=1, y=("p1", lab_off[v]), w=("p1", cw_off),
                            c_ce=fce / T, c_sm=(sw_coef / ((T - 1) * C) if sw_coef and T > 1 else 0.0)), T, 0, 0)
-            # token CE
-            add(k, v, dict(kind=nx.TERM_CLASS, R=Q, C=C1, x=_ptr_rows(a_cl, v * Q, C1), sr=C1, sc=1,
-                           dx=_ptr_rows(ga, v * Q, C1), dsr=C1, dsc=1, y=("p2", tgt_off[v][0]), w=("p1", cw_off),
-                           c_ce=1.0 / tgt_off[v][1], c_sm=0.0), Q, 0, 0)
+            # token CE (c_ce = 1 / the targets' class-weight sum, after the matching)
+            tok_terms.append((add(k, v, dict(kind=nx.TERM_CLASS, R=Q, C=C1, x=_ptr_rows(a_cl, v * Q, C1), sr=C1, sc=1,
+                                             dx=_ptr_rows(ga, v * Q, C1), dsr=C1, dsc=1, y=("p2", tgt_off[v]),
+                                             w=("p1", cw_off), c_ce=0.0, c_sm=0.0), Q, 0, 0), v))
             if isinstance(blk, InputBlock):
                 continue
-            ai, si = matches[v]
-            K = len(ai)
             ka_o, kgs_o, kge_o, ksw_o = sw_list[v]
+            Kc = kcap[v]
             if is_tdu:
                 Sv, s0 = bt["S"][v], bt["s_off"][v]
                 st, en = bt["local"][v][1], bt["local"][v][2]
@@ -506,13 +513,13 @@ def run(net, vb, compute_loss, early=None):
                 c_xe, c_sm = 1.0 / T, (sw_coef / ((T - 1) * Q) if sw_coef and T > 1 else 0.0)
             f2a, a2f = bt["f2a_lg"], bt["a2f_lg"]
             gfa, gaf = grad_of(f2a), grad_of(a2f)
-            common = dict(kind=nx.TERM_ATTN, R=R, C=Q, rs=ivs[0], re=ivs[1], K=K, ka=("p2", ka_o),
+            common = dict(kind=nx.TERM_ATTN, R=R, C=Q, rs=ivs[0], re=ivs[1], K=0, ka=("p2", ka_o),
                           kgs=("p2", kgs_o), kge=("p2", kge_o), ksw=("p2", ksw_o), c_ce=c_xe, c_sm=c_sm)
             # f2a logits (Q, R) read as (R, Q): log_softmax over rows per matched column (dim=1)
-            add(k, v, dict(common, x=f2a.data_ptr() + 4 * off, sr=1, sc=R, dx=gfa.data_ptr() + 4 * off, dsr=1,
-                           dsc=R, axis=0), R, R + K, K)
-            add(k, v, dict(common, x=a2f.data_ptr() + 4 * off, sr=Q, sc=1, dx=gaf.data_ptr() + 4 * off, dsr=Q,
-                           dsc=1, axis=1), R, R + K, K)
+            attn_terms.append((add(k, v, dict(common, x=f2a.data_ptr() + 4 * off, sr=1, sc=R,
+                                              dx=gfa.data_ptr() + 4 * off, dsr=1, dsc=R, axis=0), R, R + Kc, Kc), v))
+            attn_terms.append((add(k, v, dict(common, x=a2f.data_ptr() + 4 * off, sr=Q, sc=1,
+                                              dx=gaf.data_ptr() + 4 * off, dsr=Q, dsc=1, axis=1), R, R + Kc, Kc), v))
     sims = None
     if any(con_on):
         Cs = text_seen.shape[0]
@@ -564,12 +571,37 @@ def run(net, vb, compute_loss, early=None):
             elif val is not None:
                 setattr(t, name, val)
         t.lse, t.lse2, t.colz = (sbase + 4 * o for o in offs)
-    pk2.send()
-    nx.check(lib.fx_eval_pred(ctypes.addressof(va), base2 + va_off, nvid, float(cfg.FACT.mwt), nx.ptr(pred),
-                              nx.stream()), "fx_eval_pred")
     ws = torch.empty(max(lib.fx_loss_terms_workspace_floats(nterms), 1), device=dev, dtype=torch.float32)
+
+    # ------------------------------------------------------------------ the matching (waits for the costs)
+    matches = early.matches(Q)
+    big = [v for v, (ai, _) in enumerate(matches) if len(ai) > nx.LOSS_MAXK]
+    if big:      # e.g. o2m matching (every ground-truth segment paired, loss.py:155-193) past 512 segments
+        raise TableTooLarge(big)
+    ksum = []
+    for v in range(nvid):
+        ai, si = matches[v]
+        K = len(ai)
+        if K > kcap[v]:
+            raise RuntimeError(f"video {v}: {K} matched columns > {kcap[v]} ground-truth segments")
+        tgt = tgt_arr[v]
+        tgt[ai] = gts[v][2][si]
+        ksum.append(float(cw[tgt].sum()))
+        swn = segment_weights(mc, gts[v][2])
+        if len(swn) not in (K, 1):
+            raise RuntimeError(f"cross_attn_loss: {K} matched columns vs {len(swn)} segment weights")
+        ka, kgs, kge, ksw = sw_arr[v]
+        ka[:K] = ai
+        kgs[:K] = gts[v][0][si]
+        kge[:K] = gts[v][1][si]
+        ksw[:K] = swn if len(swn) == K else swn[0]
+    for i, v in tok_terms:
+        terms[i].c_ce = 1.0 / ksum[v]
+    for i, v in attn_terms:
+        terms[i].K = len(matches[v][0])
+    pk2.send()
     plan = dict(terms_host=terms, terms_dev=base2 + t_off, nterms=nterms, coef_dev=base2 + coef_off, nout=nout,
-                ws=ws, grads=grads, keep=(early, pk2, scr, sims, flog, text_seen))
+                ws=ws, grads=grads, keep=(early, pk2, pke, scr, sims, flog, text_seen))
     out = _LossFn.apply(plan, *inputs)
 
     # the reference's side channels: last video's per-block losses, fact / contrastive terms
