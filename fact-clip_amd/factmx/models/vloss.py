@@ -119,6 +119,13 @@ def _ptr_rows(t, row0, ld):
 
 _PENDING = []          # read-backs not resolved yet (resolved at the next forward at the latest)
 LAZY_READBACK = os.environ.get("FX_LAZY_READBACK", "1") != "0"   # 0: resolve inside the forward (A/B)
+RUN_TIMES = [] if os.environ.get("FX_VLOSS_TIMES") == "1" else None   # diagnostic: host time stamps of run()
+
+
+def _stamp(name):
+    if RUN_TIMES is not None:
+        import time
+        RUN_TIMES.append((name, time.perf_counter()))
 
 
 class LazySave(dict):
@@ -379,6 +386,7 @@ def run(net, vb, compute_loss, early=None):
             a.pred_off = fo[v]
         return off, va
 
+    _stamp("pred")
     pred = torch.empty(fo[-1], dtype=torch.int32, device=dev)
     if not compute_loss:
         pk = _Pack()
@@ -430,6 +438,7 @@ def run(net, vb, compute_loss, early=None):
         con_on.append(bool((y != -1).any()))
         y_con.append(y)
 
+    _stamp("con")
     # the predictions (no matching needed): own small table, launched before the wait
     pke = _Pack()
     va_off, va = eval_structs(pke)
@@ -438,6 +447,7 @@ def run(net, vb, compute_loss, early=None):
     nx.check(lib.fx_eval_pred(ctypes.addressof(va), pke.base + va_off, nvid, float(cfg.FACT.mwt), nx.ptr(pred),
                               nx.stream()), "fx_eval_pred")
 
+    _stamp("eval_pred")
     pk2 = _Pack()
     # per video: token targets (Q) and the matched columns (capacity G[v] >= K), filled after matching
     tgt_arr = [np.full(Q, C1 - 1, dtype=np.int32) for _ in range(nvid)]
@@ -455,15 +465,27 @@ def run(net, vb, compute_loss, early=None):
         sw_list.append(tuple(offs))
     ycon_off = [pk2.array(y, np.int32) if y is not None and con_on[v] else None for v, y in enumerate(y_con)]
 
-    inputs, grads, gidx = [], [], {}
+    _stamp("pk2_arrays")
+    # every differentiated input of the term table, its gradient a view of ONE flat allocation
+    inputs, gidx = [], {}
+
+    def want(t):
+        if id(t) not in gidx:
+            gidx[id(t)] = len(inputs)
+            inputs.append(t)
+    for blk in blocks:
+        bt = blk._bt
+        for key in ("f_cl", "a_cl", "seg_cl", "f2a_lg", "a2f_lg"):
+            if key in bt and not (key.endswith("_lg") and isinstance(blk, InputBlock)):
+                want(bt[key])
+    if any(con_on):
+        want(proj)
+    sizes = [(t.numel() + 63) & ~63 for t in inputs]      # 256-byte aligned slices, as separate tensors
+    gflat = torch.empty(sum(sizes), device=dev, dtype=torch.float32)
+    grads = [g[:t.numel()].view(t.shape) for g, t in zip(torch.split(gflat, sizes), inputs)]
 
     def grad_of(t):
-        k = id(t)
-        if k not in gidx:
-            gidx[k] = len(inputs)
-            inputs.append(t)
-            grads.append(torch.empty_like(t))
-        return grads[gidx[k]]
+        return grads[gidx[id(t)]]
 
     specs = []       # (block index or -1 for InfoNCE, video, dict of LossTerm fields, scratch sizes)
     tok_terms, attn_terms = [], []     # (term index, video): fields set after the matching
@@ -520,6 +542,7 @@ def run(net, vb, compute_loss, early=None):
                                               dx=gfa.data_ptr() + 4 * off, dsr=1, dsc=R, axis=0), R, R + Kc, Kc), v))
             attn_terms.append((add(k, v, dict(common, x=a2f.data_ptr() + 4 * off, sr=Q, sc=1,
                                               dx=gaf.data_ptr() + 4 * off, dsr=Q, dsc=1, axis=1), R, R + Kc, Kc), v))
+    _stamp("specs")
     sims = None
     if any(con_on):
         Cs = text_seen.shape[0]
@@ -539,6 +562,7 @@ def run(net, vb, compute_loss, early=None):
                             inv_temp=1.0 / float(cfg.CLIP.temp), demb=_ptr_rows(gp, fo[v], Dc), ld_demb=Dc,
                             c_ce=0.5), T, Cs, ncolz)
 
+    _stamp("infonce")
     # coefficient matrix: out = [batch loss, per video (loss, fact, contrastive, block values...)]
     nterms = len(specs)
     per = 3 + nb
@@ -557,6 +581,7 @@ def run(net, vb, compute_loss, early=None):
         coef[o, i] = lw
         coef[0, i] = lw / nvid
     coef_off = pk2.array(coef, np.float32)
+    _stamp("coef")
     t_off, terms = pk2.structs(nx.LossTerm, nterms)
     base2 = pk2.alloc(dev)
     scr = torch.empty(max(scratch[0], 1), device=dev, dtype=torch.float32)
@@ -571,10 +596,12 @@ def run(net, vb, compute_loss, early=None):
             elif val is not None:
                 setattr(t, name, val)
         t.lse, t.lse2, t.colz = (sbase + 4 * o for o in offs)
+    _stamp("structs")
     ws = torch.empty(max(lib.fx_loss_terms_workspace_floats(nterms), 1), device=dev, dtype=torch.float32)
 
     # ------------------------------------------------------------------ the matching (waits for the costs)
     matches = early.matches(Q)
+    _stamp("matches")
     big = [v for v, (ai, _) in enumerate(matches) if len(ai) > nx.LOSS_MAXK]
     if big:      # e.g. o2m matching (every ground-truth segment paired, loss.py:155-193) past 512 segments
         raise TableTooLarge(big)
@@ -599,27 +626,34 @@ def run(net, vb, compute_loss, early=None):
         terms[i].c_ce = 1.0 / ksum[v]
     for i, v in attn_terms:
         terms[i].K = len(matches[v][0])
+    _stamp("fill")
     pk2.send()
     plan = dict(terms_host=terms, terms_dev=base2 + t_off, nterms=nterms, coef_dev=base2 + coef_off, nout=nout,
                 ws=ws, grads=grads, keep=(early, pk2, pke, scr, sims, flog, text_seen))
     out = _LossFn.apply(plan, *inputs)
 
+    _stamp("send_lossfn")
     # the reference's side channels: last video's per-block losses, fact / contrastive terms
     # (blocks.py:905-910: a video without a contrastive term reports the attributes an earlier
     # video -- or an earlier call -- left behind, as the reference's hasattr checks do)
     prev = None
     if not all(con_on) and hasattr(net, "fact_loss") and hasattr(net, "contrastive_loss"):
-        prev = (float(net.fact_loss), float(net.contrastive_loss))
+        # read at resolve time: float() of a device value here would drain the stream (the loss
+        # kernels just issued included) before the backward is issued
+        prev = (net.fact_loss, net.contrastive_loss)
     o = 1 + (nvid - 1) * per
-    net.loss_list = [out[o + 3 + k] for k in range(nb)]
+    from .blocks import _OutRef
+    d = net.__dict__              # lazily indexed (blocks._lazy_out_attr), no nn.Module.__setattr__ walk
+    d["_lo_loss_list"] = _OutRef(out, list(range(o + 3, o + 3 + nb)))
     for v in range(nvid):
         if con_on[v]:
             o = 1 + v * per
-            net.fact_loss, net.contrastive_loss = out[o + 1], out[o + 2]
+            d["_lo_fact_loss"], d["_lo_contrastive_loss"] = _OutRef(out, o + 1), _OutRef(out, o + 2)
     # ONE device->host read-back for the predictions and every loss value, enqueued here and resolved
     # later: at the end of the backward pass (autograd callback queued by _LossFn.backward), at the first
     # read of a save entry, or at the next forward -- whichever comes first -- so loss.backward() is
     # issued while the device still finishes the forward instead of after a drain
+    _stamp("side")
     out_h = torch.empty(out.shape, dtype=torch.float32, pin_memory=True)
     pred_h = torch.empty(pred.shape, dtype=torch.int32, pin_memory=True)
     st_h = torch.empty(1, dtype=torch.int32, pin_memory=True)
@@ -629,10 +663,11 @@ def run(net, vb, compute_loss, early=None):
     ready = torch.cuda.Event()
     ready.record()
 
+    _stamp("readback")
     def fill(saves):
         vals = out_h.tolist()
         ph = pred_h.numpy()
-        prev_ = prev
+        prev_ = None if prev is None else tuple(float(x) for x in prev)
         for v in range(nvid):
             o = 1 + v * per
             d = {"loss": vals[o]}

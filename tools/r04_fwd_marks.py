@@ -106,6 +106,10 @@ def main():
         MARKS.clear()
         step()
         torch.cuda.synchronize()
+    if vloss.RUN_TIMES:
+        t = vloss.RUN_TIMES[-14:]
+        for (a, ta), (b, tb) in zip(t, t[1:]):
+            print(f"run: {a:>12s} -> {b:12s} {1e6 * (tb - ta):8.1f} us")
     h0, e0 = MARKS[0][1], MARKS[0][2]
     ph, pg = 0.0, 0.0
     for name, h, e in MARKS:
