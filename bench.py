@@ -613,7 +613,7 @@ def main():
                               for name, v in attn_prof.items()}
         for name, r in roofline_attention.items():
             if r is not None and default_shape:   # PMC bytes of the main kernel (the merge launch excluded)
-                r["traffic"] = traffic_from_profiles(f"tattn_{name}_kernel", f"r03_pmc_tattn_{name}.json")
+                r["traffic"] = traffic_from_profiles(f"tattn_{name}_kernel", f"r04_pmc_tattn_{name}.json")
         for name, v in x2y_prof.items():      # the X2Y_map cores (basic.py:373-380), when they ran fused
             if v[3].value > 0:
                 roofline_attention[name] = attention_roofline(X2Y_NOTES[name], *v)
