@@ -492,6 +492,7 @@ const Knobs& knobs() {
     if (const char* p = env("FX_FRL_PAIR")) k.frl_pair = p[0] != '0';
     if (const char* p = env("FX_FRL_PD")) k.frl_pd = std::atoi(p);
     if (const char* p = env("FX_FRL_ABLATE")) k.frl_ablate = std::atoi(p);
+    if (const char* p = env("FX_FRL_MIN_FILL")) k.frl_min_fill = std::atoi(p);
     if (const char* p = env("FX_X2Y_FUSED")) k.x2y_fused = p[0] != '0';
     if (const char* p = env("FX_SPLIT_VARIANT")) k.split_variant = std::atoi(p);
     if (const char* p = env("FX_MSTCN_TAIL")) k.mstcn_tail = p[0] != '0';
@@ -601,7 +602,7 @@ int fx_mstcn_fwd(const fx_mstcn_params* p, const float* x, long long ldx, int T,
                                   hipMemcpyDeviceToDevice, s));
   }
   const bool fused = p->fused_layers && !p->layernorm && frl_supported(F, saved, F, F) &&
-                     (!q.off || q.nvid <= 16);
+                     (!q.off || q.nvid <= 16) && (p->fused_layers == 2 || frl_fills_device(rows));
   if (fused && p->num_layers > 0)
     FX_TRY(pack_frag_layers(p->num_layers, F, workspace + L.wf, 3LL * F * F, p->w_pw, nullptr, 0, workspace + L.wk1,
                             workspace + L.wk2, s));
@@ -658,7 +659,7 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   const bool drop = p->dropout > 0.f;
   // Fused chain (no LayerNorm, no dropout, uniform videos, FX_MSTCN_FUSED=1): see below
   const bool fchain = p->fused_layers && !p->layernorm && !drop && NL > 0 && frl_supported(F, ws + L.buf0, F, F) &&
-                      (!q.off || q.nvid <= 16);
+                      (!q.off || q.nvid <= 16) && (p->fused_layers == 2 || frl_fills_device(rows));
   // the dX-packed conv weights come from the forward (saved); the fused chain also needs the
   // transposed 1x1 weights (repacked here, into the workspace), both then in fragment order
   if (fchain) {

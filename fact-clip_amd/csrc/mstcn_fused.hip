@@ -22,6 +22,8 @@
 // the 128 x 64 GEMM tile, and about even with the two GEMM launches it replaces; loading the natural
 // [n][k] rows directly was slower still, 32 rows = 32 cache lines per load instruction.)
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include "fx_common.h"
 #include "ops.h"
@@ -339,6 +341,25 @@ __global__ __launch_bounds__(256) void pack_frag_kernel(PackFragArgs a) {
 }
 
 }  // namespace
+
+bool frl_fills_device(long long rows) {
+  static std::mutex mu;
+  static std::map<int, int> cus;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  int n = 0;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cus.find(dev);
+    if (it == cus.end()) {
+      if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 256;
+      cus[dev] = n;
+    } else {
+      n = it->second;
+    }
+  }
+  return (rows + FR - 1) / FR >= (long long)n * knobs().frl_min_fill / 100;
+}
 
 bool frl_supported(int F, const void* x, long long ldx, long long ld_other) {
   return F == FN && ldx % 4 == 0 && ((uintptr_t)x & 15) == 0 && ld_other % 4 == 0;

@@ -581,7 +581,8 @@ def x2y(mod, X, Y, Xpos, Ypos, rows=None):
 # fx_mstcn_params.fused_layers: the one-kernel MS-TCN layer (mstcn_fused.hip, weights in MFMA fragment
 # order): on by default since round 4 (whole step 14.9 -> 14.5 ms);
 # FX_MSTCN_FUSED_LAYERS=0 selects the two-GEMM layers (A/B knob)
-MSTCN_FUSED_LAYERS = os.environ.get("FX_MSTCN_FUSED_LAYERS", "1") == "1"
+# (2: also below one 32-row tile per CU, where the library would pick the two GEMMs -- tests)
+MSTCN_FUSED_LAYERS = int(os.environ.get("FX_MSTCN_FUSED_LAYERS", "1"))
 
 
 def _ptr_array(ts):

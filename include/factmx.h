@@ -293,8 +293,9 @@ typedef struct fx_mstcn_params {
                                  [seq_off[v], seq_off[v+1]), zero padding at its own ends; nvid <= 16;
                                  T ignored); NULL: nvid videos of T rows */
   int fused_layers;           /* 1: the fused one-kernel layer (conv -> epilogue -> 1x1, F = 256, no LN,
-                                 uniform videos) where it applies -- opt-in, measured even with the
-                                 two tuned GEMMs */
+                                 <= 16 videos) where it applies and its 32-row tiles cover every CU
+                                 (fewer rows: the two tuned GEMMs are faster); 2: wherever it applies
+                                 (tests); 0: the two GEMMs per layer */
 } fx_mstcn_params;
 
 typedef struct fx_mstcn_grads {

@@ -238,7 +238,7 @@ def test_mstcn_fused_layers_match_fp64(T, nvid, nl, fused, monkeypatch):
     the conv GEMMs; per-video weight-gradient launches; the fused layer declines ragged videos)."""
     from factmx.dp import FlatGradReducer
     from factmx.models.basic import MSTCN
-    monkeypatch.setattr(fxf, "MSTCN_FUSED_LAYERS", fused == "1")
+    monkeypatch.setattr(fxf, "MSTCN_FUSED_LAYERS", 2 if fused == "1" else 0)   # 2: the fused kernel at any size
     torch.manual_seed(0)
     mod = MSTCN(96, 256, 40, nl, dropout=0.0, ln=False, in_map=True).to(DEV).train()
     Ts = list(T) if isinstance(T, tuple) else [T] * nvid
