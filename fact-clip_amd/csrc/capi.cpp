@@ -254,6 +254,10 @@ struct SideStream {
   hipEvent_t to_side[3] = {};
   hipEvent_t layer_done[4] = {};
   hipEvent_t join = nullptr;
+  // a second, short-lived helper stream for work whose result the caller's stream needs before the
+  // entry point returns (no backlog of deferred weight gradients in front of it)
+  hipStream_t aux = nullptr;
+  hipEvent_t aux_fork = nullptr, aux_done = nullptr;
 };
 
 SideStream* side_stream() {
@@ -274,6 +278,9 @@ SideStream* side_stream() {
   for (auto& e : ss->to_side) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
   for (auto& e : ss->layer_done) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
   ok = ok && hipEventCreateWithFlags(&ss->join, hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipStreamCreateWithPriority(&ss->aux, hipStreamNonBlocking, prio) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&ss->aux_fork, hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&ss->aux_done, hipEventDisableTiming) == hipSuccess;
   if (!ok) {
     delete ss;   // (a partially created set leaks its handles; the caller falls back to one stream)
     return nullptr;
@@ -1233,6 +1240,22 @@ int side_join_into(hipStream_t s) {
   if (!ss) return FX_OK;
   FX_CHECK_HIP(hipEventRecord(ss->join, ss->s));
   FX_CHECK_HIP(hipStreamWaitEvent(s, ss->join, 0));
+  return FX_OK;
+}
+
+hipStream_t aux_fork(hipStream_t s) {
+  SideStream* ss = side_stream();
+  if (!ss) return s;
+  if (hipEventRecord(ss->aux_fork, s) != hipSuccess || hipStreamWaitEvent(ss->aux, ss->aux_fork, 0) != hipSuccess)
+    return s;
+  return ss->aux;
+}
+
+int aux_join_into(hipStream_t s, hipStream_t a) {
+  SideStream* ss = side_stream();
+  if (!ss || a == s) return FX_OK;
+  FX_CHECK_HIP(hipEventRecord(ss->aux_done, ss->aux));
+  FX_CHECK_HIP(hipStreamWaitEvent(s, ss->aux_done, 0));
   return FX_OK;
 }
 

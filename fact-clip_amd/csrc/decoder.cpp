@@ -65,22 +65,6 @@ __global__ void unpack_kv_acc_kernel(UnpackKV p) {
     for (int i = threadIdx.x; i < p.A; i += blockDim.x) p.bdst[blk][i] += p.bsrc[blk * p.A + i];
 }
 
-// o1 = a + b (nullable b -> a);  o2 += b  (pos-path gradient accumulation)
-__global__ void add_acc_kernel(const float* a, const float* b, float* o1, float* o2, long long n) {
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const float bv = b[i];
-    o1[i] = a[i] + bv;
-    if (o2) o2[i] += bv;
-  }
-}
-
-int add_acc(const float* a, const float* b, float* o1, float* o2, long long n, hipStream_t s) {
-  if (n == 0) return FX_OK;
-  hipLaunchKernelGGL(add_acc_kernel, dim3(ew_grid(n)), dim3(256), 0, s, a, b, o1, o2, n);
-  FX_CHECK_HIP(hipGetLastError());
-  return FX_OK;
-}
-
 // y = x . w^T + b + resid   (w (N, K) row stride ldw)
 int linear_fwd_res(const float* x, long long ldx, int M, int K, const float* w, long long ldw, const float* b,
                    const float* resid, long long ldr, float* y, long long ldy, int N, hipStream_t s) {
@@ -119,7 +103,7 @@ struct DecLayout {
   // workspace (fwd)
   long long wkv, bkv, wsp, total_ws_fwd;
   // workspace (bwd)
-  long long dkv, dwkv, dbkv, dT, dS, dU, dF, dQKV, dO, dq, G, P, lnws, core, dmask, split, gdu, gdf, gdq, gdqkv,
+  long long dkv, dwkv, dbkv, dT, dS, dU, dF, dQKV, dO, dq, lnws, core, dmask, split, gdu, gdf, gdq, gdqkv,
       gdy, total_ws_bwd;
 };
 
@@ -222,8 +206,6 @@ DecLayout dec_layout(const fx_decoder_params* p, int R, int T, int has_qpos, int
   L.dQKV = o; o += 3 * RA;
   L.dO = o; o += RA;
   L.dq = o; o += RA;
-  L.G = o; o += RA;
-  L.P = o; o += RA;
   L.lnws = o; o += layernorm_bwd_ws_floats(R, (int)A);
   L.core = o; o += att;
   L.dmask = o; o += (p->dropout > 0.f) ? RA : 0;   // masked branch gradient (training dropout)
@@ -456,10 +438,7 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
   float* dT = ws + L.dT;     // gradient w.r.t. the current layer output
   float* dS = ws + L.dS;
   float* dO = ws + L.dO;
-  float* G = ws + L.G;       // sum of the query-position gradients over layers
-  float* P = ws + L.P;
   float* dkv = ws + L.dkv;
-  if (qpos) FX_CHECK_HIP(hipMemsetAsync(G, 0, RA * sizeof(float), s));
   // out_linear and the final LayerNorm
   const float* xl = saved + L.layers + (NL - 1) * L.per_layer + L.t3;   // last layer output
   const float* fin = p->final_norm ? saved + L.fo : xl;
@@ -520,12 +499,9 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
                               dO, A, b + L.pca, nvid, Qv, Tv, hd, h, scale, dq, A, dkv + (long long)l * A, AL2,
                               dkv + (long long)(NL + l) * A, AL2, ws + L.core, s, &o));
       dT = dy_slot(2, l);
-      if (qpos) {
-        FX_TRY(launch_gemm(desc_linear_dx(dq, A, p->ca_q_w[l], R, A, A, P, A, 0, nullptr, 0, spl), s));
-        FX_TRY(add_acc(dR, P, dT, G, RA, s));                                     // dT1 = dR + P ; G += P
-      } else {
-        FX_TRY(launch_gemm(dx_res_desc(dq, A, p->ca_q_w[l], A, R, A, A, dR, A, dT, A, spl), s));
-      }
+      // dT1 = dR + dq Wq (the query-position gradient's share, dq Wq again, follows the chain on the aux
+      // stream)
+      FX_TRY(launch_gemm(dx_res_desc(dq, A, p->ca_q_w[l], A, R, A, A, dR, A, dT, A, spl), s));
     }
     // --- self-attention + LN1
     dU = slot_u(2, l);
@@ -547,27 +523,30 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
                               Qv, hd, h, scale, dQKV, 3 * A, dQKV + A, 3 * A, dQKV + 2 * A, 3 * A, ws + L.core, s, &o));
     }
     float* dX = l == 0 ? nullptr : dy_slot(0, l - 1);   // the next (earlier) layer's output gradient
-    if (!qpos) {
-      if (l > 0 || dtgt)
-        FX_TRY(launch_gemm(dx_res_desc(dQKV, 3 * A, p->sa_in_w[l], A, R, A, 3 * A, dR, A, l > 0 ? dX : dtgt,
-                                       l > 0 ? A : lddt, spl), s));
-    } else {
-      // P = dq W_q + dk W_k  (the position path);  dX = dR + dv W_v + P ; G += P
-      FX_TRY(linear_dx(dQKV, 3 * A, p->sa_in_w[l], R, A, 2 * A, P, A, 0, nullptr, 0, spl, s));
-      if (l > 0 || dtgt) {
-        FX_TRY(linear_dx_res(dQKV + 2 * A, 3 * A, p->sa_in_w[l] + 2LL * A * A, A, R, A, A, dR, A, dS, A, spl, s));
-        if (l > 0) {
-          FX_TRY(add_acc(dS, P, dX, G, RA, s));
-        } else if (lddt == A) {
-          FX_TRY(add_acc(dS, P, dtgt, G, RA, s));
-        } else {
-          FX_TRY(add_acc(dS, P, dS, G, RA, s));
-          FX_CHECK_HIP(hipMemcpy2DAsync(dtgt, lddt * sizeof(float), dS, A * sizeof(float), A * sizeof(float), R,
-                                        hipMemcpyDeviceToDevice, s));
-        }
-      } else {
-        FX_TRY(add2(P, A, nullptr, 0, R, A, G, A, 1, s));
-      }
+    // dX = dR + [dq | dk | dv] W_in  (q and k see x + qpos: with query positions their share dq W_q + dk W_k
+    // is also the position gradient's, accumulated on the aux stream below)
+    if (l > 0 || dtgt)
+      FX_TRY(launch_gemm(dx_res_desc(dQKV, 3 * A, p->sa_in_w[l], A, R, A, 3 * A, dR, A, l > 0 ? dX : dtgt,
+                                     l > 0 ? A : lddt, spl), s));
+  }
+  // Query-position gradient dqpos = sum over layers of dq_ca W_q,ca + [dq | dk]_sa W_{q,k},sa (the chain
+  // above computed these products inside its dX GEMMs): accumulating GEMMs over the per-layer dq / dQKV
+  // slots on the aux stream, beside the rest of this backward; the caller's stream waits for them
+  // before returning.  (Split 1: the aux stream must not touch `spl`.)
+  hipStream_t sa = s;
+  if (qpos && dqpos) {
+    sa = aux_fork(s);
+    bool first = true;
+    auto acc = [&](const float* dy, long long lddy, const float* w, int N) -> int {
+      fx_gemm_desc d = desc_linear_dx(dy, lddy, w, R, A, N, dqpos, A, first ? 0 : 1, nullptr, 0, nullptr);
+      d.split_k = 1;
+      d.workspace = nullptr;
+      first = false;
+      return launch_gemm(d, sa);
+    };
+    for (int l = NL - 1; l >= 0; --l) {
+      if (p->cross) FX_TRY(acc(ws + L.gdq + (long long)l * RA, A, p->ca_q_w[l], A));
+      FX_TRY(acc(ws + L.gdqkv + (long long)l * 3 * RA, 3 * A, p->sa_in_w[l], 2 * A));
     }
   }
   hipStream_t sd = side_fork(s, 1);
@@ -642,7 +621,6 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
     }
     FX_TRY(launch_ln_param_grads(jobs, nj, R, A, A, A, sd));
   }
-  if (qpos && dqpos) FX_CHECK_HIP(hipMemcpyAsync(dqpos, G, RA * sizeof(float), hipMemcpyDeviceToDevice, s));
   if (p->cross) {
     // frame memory: dmem = dKV . Wkv ; dWkv = dKV^T [mem+pos | mem] ; dbkv = colsum(dKV)
     PackKV pk{};
@@ -699,6 +677,7 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
     FX_CHECK_HIP(hipGetLastError());
   }
   if (sd != s && !p->side_defer) FX_TRY(side_join_into(s));
+  FX_TRY(aux_join_into(s, sa));
   return FX_OK;
 }
 

@@ -68,6 +68,10 @@ struct GridCap {
 // side_join_into: s waits for everything enqueued on the side stream.
 hipStream_t side_fork(hipStream_t s, int event);
 int side_join_into(hipStream_t s);
+// aux_fork: the helper stream (after waiting for everything enqueued on s), or s when there is none;
+// aux_join_into(s, a): s waits for what was enqueued on a since (no-op when a == s)
+hipStream_t aux_fork(hipStream_t s);
+int aux_join_into(hipStream_t s, hipStream_t a);
 // split-K factor for weight-gradient GEMMs deferred to the side stream over `rows` rows (keeps each
 // workgroup's share of K short, so the main stream's kernels find free CUs)
 int defer_split(int rows);
