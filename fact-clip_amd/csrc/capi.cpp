@@ -500,6 +500,7 @@ const Knobs& knobs() {
     if (const char* p = env("FX_FRL_PD")) k.frl_pd = std::atoi(p);
     if (const char* p = env("FX_FRL_ABLATE")) k.frl_ablate = std::atoi(p);
     if (const char* p = env("FX_FRL_MIN_FILL")) k.frl_min_fill = std::atoi(p);
+    if (const char* p = env("FX_AUX_STREAM")) k.aux_stream = p[0] != '0';
     if (const char* p = env("FX_X2Y_FUSED")) k.x2y_fused = p[0] != '0';
     if (const char* p = env("FX_SPLIT_VARIANT")) k.split_variant = std::atoi(p);
     if (const char* p = env("FX_MSTCN_TAIL")) k.mstcn_tail = p[0] != '0';
@@ -1245,7 +1246,7 @@ int side_join_into(hipStream_t s) {
 
 hipStream_t aux_fork(hipStream_t s) {
   SideStream* ss = side_stream();
-  if (!ss) return s;
+  if (!ss || !knobs().aux_stream) return s;   // FX_AUX_STREAM=0: everything on the caller's stream (A/B)
   if (hipEventRecord(ss->aux_fork, s) != hipSuccess || hipStreamWaitEvent(ss->aux, ss->aux_fork, 0) != hipSuccess)
     return s;
   return ss->aux;
