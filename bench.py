@@ -606,8 +606,9 @@ def main():
         frl_roofline = fused_layer_roofline(frl_prof, F32_MFMA_PEAK_TFLOPS)
         if frl_roofline is not None:
             frl_roofline["traffic"] = traffic_from_profiles(FRL_KERNEL) if default_shape else None
-            frl_roofline["sample"] = (f"HIP events on the first {frl_roofline['launches']} fused-layer launches of "
-                                      "the timed region")
+            frl_roofline["sample"] = (f"HIP events around the back-to-back fused-layer chains (one pair per MS-TCN "
+                                      f"stack and direction) of the timed region: {frl_roofline['launches']} "
+                                      "launches, inter-launch gaps included")
         roofline = (frl_roofline if frl_roofline is not None and frl_prof[0].value > ms.value else conv_roofline)
         roofline_attention = {name: attention_roofline(f"tattn_{name}_kernel (+ tattn_merge_kernel over T splits)", *v)
                               for name, v in attn_prof.items()}

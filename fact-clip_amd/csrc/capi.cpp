@@ -27,6 +27,7 @@ struct ProfState {
   int max_events = 0;
   std::vector<hipEvent_t> ev;
   std::vector<double> flops, bytes;
+  std::vector<int> launches;   // launches an event pair brackets (back-to-back chains: one pair)
   int used = 0;
 };
 constexpr int kProfKinds = 8;   // 0 conv GEMM, 1 / 2 attention over T fwd / bwd, 3-6 X2Y cores, 7 fused MS-TCN layer
@@ -47,7 +48,7 @@ void prof_begin(int kind, hipStream_t s) {
   (void)hipEventRecord(p.ev[2 * p.used], s);
 }
 
-void prof_end(int kind, hipStream_t s, double flops, double bytes) {
+void prof_end(int kind, hipStream_t s, double flops, double bytes, int launches) {
   std::lock_guard<std::mutex> lk(g_prof_mu);
   if (kind < 0 || kind >= kProfKinds) return;
   ProfState& p = g_prof[kind];
@@ -55,6 +56,7 @@ void prof_end(int kind, hipStream_t s, double flops, double bytes) {
   (void)hipEventRecord(p.ev[2 * p.used + 1], s);
   p.flops[p.used] = flops;
   p.bytes[p.used] = bytes;
+  p.launches[p.used] = launches;
   p.used++;
 }
 
@@ -619,12 +621,15 @@ int fx_mstcn_fwd(const fx_mstcn_params* p, const float* x, long long ldx, int T,
     float* hn = saved + L.h + (i + 1) * L.rowsF;
     float* zi = saved + L.z + i * L.rowsF;
     if (fused) {   // z = relu(conv(h) + b); h' = h + dropout(z . Wpw^T + b): one kernel (mstcn_fused.hip)
-      prof_begin(7, s);
+      // (timed as one chain: an event pair around every launch would add its own dispatch gap)
+      if (i == 0) prof_begin(7, s);
       FX_TRY(launch_frl(hi, F, rows, T, layer_dilation(p, i), 1, q.off, q.nvid,
                         workspace + L.wk1 + (long long)i * 3 * F * F, p->b_dil[i], 1, nullptr, 0, zi, F,
                         workspace + L.wk2 + (long long)i * F * F, p->b_pw[i], hi, F, nullptr, 0, hn, F, p->dropout,
                         fx_drop_subseed(p->seed, i), s));
-      prof_end(7, s, 2.0 * rows * F * 4.0 * F, 4.0 * (3.0 * rows * F + 4.0 * F * F));
+      if (i == p->num_layers - 1)
+        prof_end(7, s, p->num_layers * 2.0 * rows * F * 4.0 * F, p->num_layers * 4.0 * (3.0 * rows * F + 4.0 * F * F),
+                 p->num_layers);
       continue;
     }
     // z = relu(dilated_conv(h) + b)      (basic.py:158)
@@ -851,14 +856,15 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
       // kernel for dH_i (-> dHall[i-1]) and dZ_i-1 (-> dZall[i-1]); the bottom layer's conv backward
       // alone; the weight gradients of every layer follow as the batched side-stream GEMMs below
       FX_TRY(pw_dx(dHall + (NL - 1) * L.rowsF, NL - 1, dZall + (NL - 1) * L.rowsF, saved + L.z + (NL - 1) * L.rowsF));
+      if (NL > 1) prof_begin(7, s);   // (the chain of NL - 1 back-to-back launches timed as one)
       for (int i = NL - 1; i >= 1; --i) {
-        prof_begin(7, s);
         FX_TRY(launch_frl(dZall + i * L.rowsF, F, rows, T, layer_dilation(p, i), -1, q.off, q.nvid,
                           ws + L.wk1 + (long long)i * 3 * F * F, nullptr, 0, dHall + i * L.rowsF, F,
                           dHall + (i - 1) * L.rowsF, F, ws + L.wk2 + (long long)(i - 1) * F * F, nullptr, nullptr, 0,
                           saved + L.z + (i - 1) * L.rowsF, F, dZall + (i - 1) * L.rowsF, F, 0.f, 0, s));
-        prof_end(7, s, 2.0 * rows * F * 4.0 * F, 4.0 * (4.0 * rows * F + 4.0 * F * F));
       }
+      if (NL > 1)
+        prof_end(7, s, (NL - 1) * 2.0 * rows * F * 4.0 * F, (NL - 1) * 4.0 * (4.0 * rows * F + 4.0 * F * F), NL - 1);
     }
     for (int i = fchain ? 0 : NL - 1; i >= 0; --i) {
       const float* zi = saved + L.z + i * L.rowsF;
@@ -1990,6 +1996,7 @@ int fx_prof_enable(int kind, int max_events) {
   for (auto& e : p.ev) FX_CHECK_HIP(hipEventCreate(&e));
   p.flops.assign(max_events, 0.0);
   p.bytes.assign(max_events, 0.0);
+  p.launches.assign(max_events, 0);
   p.max_events = max_events;
   return FX_OK;
 }
@@ -1999,6 +2006,7 @@ int fx_prof_collect(int kind, double* total_ms, double* total_flops, double* tot
   FX_REQUIRE(kind >= 0 && kind < kProfKinds && g_prof[kind].max_events > 0, "prof: kind not enabled");
   const ProfState& p = g_prof[kind];
   double ms = 0, fl = 0, by = 0;
+  int n = 0;
   for (int i = 0; i < p.used; ++i) {
     FX_CHECK_HIP(hipEventSynchronize(p.ev[2 * i + 1]));
     float t = 0.f;
@@ -2006,11 +2014,12 @@ int fx_prof_collect(int kind, double* total_ms, double* total_flops, double* tot
     ms += t;
     fl += p.flops[i];
     by += p.bytes[i];
+    n += p.launches[i];
   }
   *total_ms = ms;
   *total_flops = fl;
   *total_bytes = by;
-  *count = p.used;
+  *count = n;
   return FX_OK;
 }
 

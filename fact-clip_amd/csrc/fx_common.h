@@ -155,6 +155,6 @@ const Knobs& knobs();
 
 // event-based timing hooks around launches of one kernel class (bench roofline)
 void prof_begin(int kind, hipStream_t s);
-void prof_end(int kind, hipStream_t s, double flops, double bytes);
+void prof_end(int kind, hipStream_t s, double flops, double bytes, int launches = 1);
 
 }  // namespace fx
