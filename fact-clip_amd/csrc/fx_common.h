@@ -136,6 +136,7 @@ struct Knobs {
   int frl_min_fill = 100;       // FX_FRL_MIN_FILL: fused MS-TCN layer only when its row tiles cover this % of the CUs
   bool aux_stream = true;       // FX_AUX_STREAM=0: the decoder's query-position gradient on the caller's stream
   int tattn_tc_max = 256;       // FX_TATTN_TC: largest key chunk per attention-over-T workgroup (32..256, A/B)
+  bool gru_poll2 = true;        // FX_GRU_POLL2=0: one granule poll in flight per lane (A/B)
   int frl_xcd = 2;             // FX_FRL_XCD: fused MS-TCN layer row tiles on the XCDs -- 0 round robin,
                               // 1 contiguous runs, 2 runs that follow the conv taps (A/B)
   FILE* gemm_log = nullptr; // FX_GEMM_LOG=<file>: one line per GEMM launch (shape census)

@@ -54,7 +54,33 @@ __device__ __forceinline__ void put_granule(unsigned long long* g, unsigned epoc
 
 // one wave gathers n granules of `epoch` into LDS dst (bounded spin; on timeout flags *tmo)
 __device__ __forceinline__ bool gather_granules(unsigned long long* g, int n, unsigned epoch, float* dst,
-                                                unsigned* tmo, unsigned spin_max, int lane) {
+                                                unsigned* tmo, unsigned spin_max, int lane, bool poll2) {
+  if (poll2 && n <= 64) {
+    // one granule per lane, two polls in flight, each re-issued right after its check (epochs only move
+    // forward while this wave still needs the slot).  Per recurrent step (tools/r04_gru_bench.py, S = 3400,
+    // 2 sequences): fwd 1.88 -> 1.70-1.80 us, bwd 2.49 -> 2.20-2.36 us; four polls in flight were slower
+    // (the extra L2 / MALL traffic), delaying the second poll by 256-1024 cycles gained nothing
+    const bool mine = lane < n;
+    gu64* p = (gu64*)(g + (mine ? lane : 0));
+    unsigned long long a = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long b = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (unsigned spins = 0;; spins += 2) {
+      if (__all(!mine || (unsigned)(a >> 32) == epoch)) {
+        if (mine) dst[lane] = __uint_as_float((unsigned)a);
+        return true;
+      }
+      a = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__all(!mine || (unsigned)(b >> 32) == epoch)) {
+        if (mine) dst[lane] = __uint_as_float((unsigned)b);
+        return true;
+      }
+      b = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (spins > spin_max) {
+        if (lane == 0) __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+    }
+  }
   for (int base = 0; base < n; base += 64 * 4) {
     unsigned long long x[4];
     bool done[4];
@@ -105,6 +131,7 @@ struct GruArgs {
   unsigned long long* gran;
   unsigned* tmo;        // the caller's status word (fx_gru_bidir_*: FX_STATUS_GRU_TIMEOUT on a lost peer)
   unsigned spin_max;
+  int poll2;            // two granule polls in flight (FX_GRU_POLL2, default on)
   int off[MAXSEQ + 1];
 };
 
@@ -157,7 +184,7 @@ __global__ __launch_bounds__(GT) void gru_fwd_kernel(GruArgs args) {
     float* hc = h[s & 1];
     if (s > 0 && kcn > 0) {   // the state after step s-1: granules of epoch s in slot (s-1) & 1
       if (!gather_granules(gran + (long long)((s - 1) & 1) * Hh + kc0, kcn, (unsigned)s, hc + kc0, args.tmo,
-                           args.spin_max, lane))
+                           args.spin_max, lane, args.poll2 != 0))
         dead = 1;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS writes land before its reads
     }
@@ -222,6 +249,7 @@ struct GruBwdArgs {
   unsigned long long* gran;
   unsigned* tmo;        // the caller's status word (fx_gru_bidir_*: FX_STATUS_GRU_TIMEOUT on a lost peer)
   unsigned spin_max;
+  int poll2;
   int off[MAXSEQ + 1];
 };
 
@@ -316,7 +344,7 @@ __global__ __launch_bounds__(GT) void gru_bwd_kernel(GruBwdArgs args) {
     {   // this workgroup's destination block: NW sources x U units, one granule per lane
       const int b0 = wv * 64;
       if (b0 < NG && !gather_granules(slot + (long long)j * NG + b0, min(64, NG - b0), (unsigned)(s + 1), red + b0,
-                                      args.tmo, args.spin_max, lane))
+                                      args.tmo, args.spin_max, lane, args.poll2 != 0))
         dead = 1;
     }
     __syncthreads();
@@ -354,6 +382,7 @@ int launch_gru_fwd(const float* gi, long long ldgi, int nseq, const int* seq_off
     GruArgs args{};
     args.tmo = status ? status : tmo;
     args.spin_max = spin_max > 0 ? (unsigned)spin_max : SPIN_MAX;
+    args.poll2 = knobs().gru_poll2;
     args.gran = gran + (long long)c0 * 2 * 2 * 3 * Hh;
     for (int q = 0; q <= nc; ++q) args.off[q] = seq_off[c0 + q];
     for (int d = 0; d < 2; ++d) {
@@ -390,6 +419,7 @@ int launch_gru_bwd(const float* dout, long long lddo, int nseq, const int* seq_o
     GruBwdArgs args{};
     args.tmo = status ? status : tmo;
     args.spin_max = spin_max > 0 ? (unsigned)spin_max : SPIN_MAX;
+    args.poll2 = knobs().gru_poll2;
     args.gran = gran + (long long)c0 * 2 * 2 * NW * NW * ((Hh + NW - 1) / NW);
     for (int q = 0; q <= nc; ++q) args.off[q] = seq_off[c0 + q];
     for (int d = 0; d < 2; ++d) {
