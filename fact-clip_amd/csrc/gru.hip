@@ -30,7 +30,8 @@ namespace {
 // still reading.  All 2*NW workgroups are co-resident (32 of 256 CUs); every spin is bounded and
 // sets a timeout word, so the grid always drains.
 constexpr int NW = 16;          // workgroups per direction
-constexpr int GT = 256;         // threads per workgroup
+constexpr int GT = 256;         // threads per workgroup (the backward's; the forward adds a store wave)
+constexpr int GTF = GT + 64;    // forward: 4 compute waves + 1 wave that writes the per-step tables
 constexpr int MAXU = 16;        // hidden units per workgroup (Hh <= 256)
 constexpr int KCH = 64;         // fwd: k-chunk per thread (4 chunks cover Hh <= 256)
 constexpr unsigned SPIN_MAX = 1u << 20;   // default: ~1 s of polling; a lost peer ends the kernel, never hangs it
@@ -132,10 +133,11 @@ struct GruArgs {
   unsigned* tmo;        // the caller's status word (fx_gru_bidir_*: FX_STATUS_GRU_TIMEOUT on a lost peer)
   unsigned spin_max;
   int poll2;            // two granule polls in flight (FX_GRU_POLL2, default on)
+  int store_wave;       // 1: a fifth wave writes the per-step tables (FX_GRU_STORE_WAVE)
   int off[MAXSEQ + 1];
 };
 
-__global__ __launch_bounds__(GT) void gru_fwd_kernel(GruArgs args) {
+__global__ __launch_bounds__(GTF) void gru_fwd_kernel(GruArgs args) {
   const int sq = blockIdx.x / (2 * NW), rem = blockIdx.x - sq * 2 * NW;
   const int dir = rem / NW, j = rem - dir * NW;
   const GruDirArgs& a = args.d[dir];
@@ -151,6 +153,10 @@ __global__ __launch_bounds__(GT) void gru_fwd_kernel(GruArgs args) {
   // step s + 2 takes step s + 1's barrier).
   __shared__ float h[2][256];
   __shared__ float part[2][4][64];
+  // the step's results (h_t, h_t-1, r, z, n, gh_n of the U units) staged for the store wave (wave 4), which
+  // writes them to the output / saved tables one step later: vector stores count in the same in-order
+  // counter as the granule polls, so the polling waves issue no table stores of their own
+  __shared__ float stage[2][6][MAXU];
   __shared__ int dead;
   if (tid == 0) dead = 0;
   const int wv = tid >> 6;
@@ -164,7 +170,23 @@ __global__ __launch_bounds__(GT) void gru_fwd_kernel(GruArgs args) {
     const int k = wv * KCH + i;
     w[i] = (act && k < Hh) ? a.whh[(long long)row * Hh + k] : 0.f;
   }
-  for (int k = tid; k < 512; k += GT) (&h[0][0])[k] = 0.f;
+  for (int k = tid; k < 512; k += blockDim.x) (&h[0][0])[k] = 0.f;
+  const bool storer = wv == 4;   // (launched only with args.store_wave)
+  auto flush = [&](int s_) {   // store wave: step s_'s staged results
+    const int u = lane;
+    if (u < U && u0 + u < Hh) {
+      const int t_ = r0 + (a.reverse ? S - 1 - s_ : s_);
+      const float* st_ = &stage[s_ & 1][0][0];
+      const int uu = u0 + u;
+      a.out[(long long)t_ * a.ldo + uu] = st_[0 * MAXU + u];
+      a.hprev[(long long)t_ * Hh + uu] = st_[1 * MAXU + u];
+      float* gs = a.gates + (long long)t_ * 4 * Hh;
+      gs[uu] = st_[2 * MAXU + u];
+      gs[Hh + uu] = st_[3 * MAXU + u];
+      gs[2 * Hh + uu] = st_[4 * MAXU + u];
+      gs[3 * Hh + uu] = st_[5 * MAXU + u];
+    }
+  };
   // the gate threads (wave 0, lanes < U): their three b_hh entries, and the input projections of step s
   // loaded during step s-1 (their latency hides behind the exchange instead of opening every step)
   const bool own = tid < U && u0 + tid < Hh;
@@ -182,26 +204,29 @@ __global__ __launch_bounds__(GT) void gru_fwd_kernel(GruArgs args) {
   for (int s = 0; s < S; ++s) {
     const int t = r0 + (a.reverse ? S - 1 - s : s);
     float* hc = h[s & 1];
-    if (s > 0 && kcn > 0) {   // the state after step s-1: granules of epoch s in slot (s-1) & 1
+    if (s > 0 && kcn > 0 && !storer) {   // the state after step s-1: granules of epoch s in slot (s-1) & 1
       if (!gather_granules(gran + (long long)((s - 1) & 1) * Hh + kc0, kcn, (unsigned)s, hc + kc0, args.tmo,
                            args.spin_max, lane, args.poll2 != 0))
         dead = 1;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS writes land before its reads
     }
-    // four independent FMA chains over the wave's 64-deep chunk (broadcast LDS reads)
-    float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
-    const float4* hv = reinterpret_cast<const float4*>(hc + kc0);
+    if (!storer) {
+      // four independent FMA chains over the wave's 64-deep chunk (broadcast LDS reads)
+      float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
+      const float4* hv = reinterpret_cast<const float4*>(hc + kc0);
 #pragma unroll
-    for (int i = 0; i < KCH / 4; ++i) {
-      const float4 x = hv[i];
-      c0 = fmaf(w[4 * i], x.x, c0);
-      c1 = fmaf(w[4 * i + 1], x.y, c1);
-      c2 = fmaf(w[4 * i + 2], x.z, c2);
-      c3 = fmaf(w[4 * i + 3], x.w, c3);
+      for (int i = 0; i < KCH / 4; ++i) {
+        const float4 x = hv[i];
+        c0 = fmaf(w[4 * i], x.x, c0);
+        c1 = fmaf(w[4 * i + 1], x.y, c1);
+        c2 = fmaf(w[4 * i + 2], x.z, c2);
+        c3 = fmaf(w[4 * i + 3], x.w, c3);
+      }
+      part[s & 1][wv][o] = (c0 + c1) + (c2 + c3);
     }
-    part[s & 1][wv][o] = (c0 + c1) + (c2 + c3);
     __syncthreads();
     if (dead) break;
+    if (storer && s > 0) flush(s - 1);
     if (own) {
       const int u = uo;
       const float gr = pr, gz = pz, gn = pn;
@@ -221,15 +246,28 @@ __global__ __launch_bounds__(GT) void gru_fwd_kernel(GruArgs args) {
       const float hp = hc[u];
       const float hn = (1.f - z) * n + z * hp;
       if (s + 1 < S) put_granule(gran + (long long)(s & 1) * Hh + u, (unsigned)(s + 1), hn);
-      a.out[(long long)t * a.ldo + u] = hn;
-      a.hprev[(long long)t * Hh + u] = hp;
-      float* gs = a.gates + (long long)t * 4 * Hh;
-      gs[u] = r;
-      gs[Hh + u] = z;
-      gs[2 * Hh + u] = n;
-      gs[3 * Hh + u] = ghn;
+      if (args.store_wave) {
+        float* st_ = &stage[s & 1][0][0];
+        st_[0 * MAXU + tid] = hn;
+        st_[1 * MAXU + tid] = hp;
+        st_[2 * MAXU + tid] = r;
+        st_[3 * MAXU + tid] = z;
+        st_[4 * MAXU + tid] = n;
+        st_[5 * MAXU + tid] = ghn;
+      } else {
+        a.out[(long long)t * a.ldo + u] = hn;
+        a.hprev[(long long)t * Hh + u] = hp;
+        float* gs = a.gates + (long long)t * 4 * Hh;
+        gs[u] = r;
+        gs[Hh + u] = z;
+        gs[2 * Hh + u] = n;
+        gs[3 * Hh + u] = ghn;
+      }
     }
   }
+  // the last step's results (every wave leaves the loop together; none after a lost peer)
+  __syncthreads();
+  if (storer && S > 0 && !dead) flush(S - 1);
 }
 
 struct GruBwdDirArgs {
@@ -382,6 +420,7 @@ int launch_gru_fwd(const float* gi, long long ldgi, int nseq, const int* seq_off
     GruArgs args{};
     args.tmo = status ? status : tmo;
     args.spin_max = spin_max > 0 ? (unsigned)spin_max : SPIN_MAX;
+    args.store_wave = knobs().gru_store_wave;
     args.poll2 = knobs().gru_poll2;
     args.gran = gran + (long long)c0 * 2 * 2 * 3 * Hh;
     for (int q = 0; q <= nc; ++q) args.off[q] = seq_off[c0 + q];
@@ -398,7 +437,7 @@ int launch_gru_fwd(const float* gi, long long ldgi, int nseq, const int* seq_off
       a.Hh = Hh;
       a.reverse = d;
     }
-    hipLaunchKernelGGL(gru_fwd_kernel, dim3(nc * 2 * NW), dim3(GT), 0, s, args);
+    hipLaunchKernelGGL(gru_fwd_kernel, dim3(nc * 2 * NW), dim3(args.store_wave ? GTF : GT), 0, s, args);
     FX_CHECK_HIP(hipGetLastError());
   }
   return FX_OK;
