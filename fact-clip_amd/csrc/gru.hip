@@ -155,7 +155,8 @@ __global__ __launch_bounds__(GTF) void gru_fwd_kernel(GruArgs args) {
   __shared__ float part[2][4][64];
   // the step's results (h_t, h_t-1, r, z, n, gh_n of the U units) staged for the store wave (wave 4), which
   // writes them to the output / saved tables one step later: vector stores count in the same in-order
-  // counter as the granule polls, so the polling waves issue no table stores of their own
+  // counter as the granule polls, so the polling waves issue no table stores of their own (the backward,
+  // with two barriers per step, measured no gain from the same change and keeps its gate-thread stores)
   __shared__ float stage[2][6][MAXU];
   __shared__ int dead;
   if (tid == 0) dead = 0;
