@@ -137,7 +137,7 @@ struct Knobs {
   bool aux_stream = true;       // FX_AUX_STREAM=0: the decoder's query-position gradient on the caller's stream
   int tattn_tc_max = 256;       // FX_TATTN_TC: largest key chunk per attention-over-T workgroup (32..256, A/B)
   bool gru_poll2 = true;        // FX_GRU_POLL2=0: one granule poll in flight per lane (A/B)
-  bool gru_store_wave = true;   // FX_GRU_STORE_WAVE=0: the GRU forward's gate threads write the per-step tables (A/B)
+  int gru_store_wave = 2;        // FX_GRU_STORE_WAVE: GRU forward table stores -- 0 by wave 0's gate threads, 1 staged for a fifth wave, 2 gate threads on the fifth wave (A/B)
   int frl_xcd = 2;             // FX_FRL_XCD: fused MS-TCN layer row tiles on the XCDs -- 0 round robin,
                               // 1 contiguous runs, 2 runs that follow the conv taps (A/B)
   FILE* gemm_log = nullptr; // FX_GEMM_LOG=<file>: one line per GEMM launch (shape census)

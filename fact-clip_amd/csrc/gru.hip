@@ -190,8 +190,11 @@ __global__ __launch_bounds__(GTF) void gru_fwd_kernel(GruArgs args) {
   };
   // the gate threads (wave 0, lanes < U): their three b_hh entries, and the input projections of step s
   // loaded during step s-1 (their latency hides behind the exchange instead of opening every step)
-  const bool own = tid < U && u0 + tid < Hh;
-  const int uo = u0 + (own ? tid : 0);
+  // (store_wave 2: the gate threads are wave 4's lanes < U -- the polling waves then issue no stores at
+  // all, not even the granule's; store_wave 1: wave 0's, their results staged for wave 4)
+  const int gl = args.store_wave == 2 ? (wv == 4 ? lane : GTF) : tid;   // gate-thread index
+  const bool own = gl < U && u0 + gl < Hh;
+  const int uo = u0 + (own ? gl : 0);
   const float br = own ? a.bhh[uo] : 0.f, bz = own ? a.bhh[Hh + uo] : 0.f, bn = own ? a.bhh[2 * Hh + uo] : 0.f;
   float pr = 0.f, pz = 0.f, pn = 0.f;
   if (own && S > 0) {
@@ -227,7 +230,7 @@ __global__ __launch_bounds__(GTF) void gru_fwd_kernel(GruArgs args) {
     }
     __syncthreads();
     if (dead) break;
-    if (storer && s > 0) flush(s - 1);
+    if (storer && s > 0 && args.store_wave == 1) flush(s - 1);
     if (own) {
       const int u = uo;
       const float gr = pr, gz = pz, gn = pn;
@@ -238,16 +241,16 @@ __global__ __launch_bounds__(GTF) void gru_fwd_kernel(GruArgs args) {
         pn = gg[2 * Hh + u];
       }
       const float (*pp)[64] = part[s & 1];
-      const float ghr = (pp[0][tid] + pp[1][tid]) + (pp[2][tid] + pp[3][tid]) + br;
-      const float ghz = (pp[0][U + tid] + pp[1][U + tid]) + (pp[2][U + tid] + pp[3][U + tid]) + bz;
-      const float ghn = (pp[0][2 * U + tid] + pp[1][2 * U + tid]) + (pp[2][2 * U + tid] + pp[3][2 * U + tid]) + bn;
+      const float ghr = (pp[0][gl] + pp[1][gl]) + (pp[2][gl] + pp[3][gl]) + br;
+      const float ghz = (pp[0][U + gl] + pp[1][U + gl]) + (pp[2][U + gl] + pp[3][U + gl]) + bz;
+      const float ghn = (pp[0][2 * U + gl] + pp[1][2 * U + gl]) + (pp[2][2 * U + gl] + pp[3][2 * U + gl]) + bn;
       const float r = sigm(gr + ghr);
       const float z = sigm(gz + ghz);
       const float n = tanh_fast(gn + r * ghn);
       const float hp = hc[u];
       const float hn = (1.f - z) * n + z * hp;
       if (s + 1 < S) put_granule(gran + (long long)(s & 1) * Hh + u, (unsigned)(s + 1), hn);
-      if (args.store_wave) {
+      if (args.store_wave == 1) {
         float* st_ = &stage[s & 1][0][0];
         st_[0 * MAXU + tid] = hn;
         st_[1 * MAXU + tid] = hp;
@@ -268,7 +271,7 @@ __global__ __launch_bounds__(GTF) void gru_fwd_kernel(GruArgs args) {
   }
   // the last step's results (every wave leaves the loop together; none after a lost peer)
   __syncthreads();
-  if (storer && S > 0 && !dead) flush(S - 1);
+  if (storer && S > 0 && !dead && args.store_wave == 1) flush(S - 1);
 }
 
 struct GruBwdDirArgs {
