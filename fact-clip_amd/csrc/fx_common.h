@@ -138,6 +138,7 @@ struct Knobs {
   int tattn_tc_max = 256;       // FX_TATTN_TC: largest key chunk per attention-over-T workgroup (32..256, A/B)
   bool gru_poll2 = true;        // FX_GRU_POLL2=0: one granule poll in flight per lane (A/B)
   int gru_store_wave = 2;        // FX_GRU_STORE_WAVE: GRU forward table stores -- 0 by wave 0's gate threads, 1 staged for a fifth wave, 2 gate threads on the fifth wave (A/B)
+  bool gru_bwd_gate_wave = false; // FX_GRU_BWD_GATE_WAVE=1: the GRU backward's gate threads on a fifth wave (A/B: even, 2.25 vs 2.26 us per step)
   int frl_xcd = 2;             // FX_FRL_XCD: fused MS-TCN layer row tiles on the XCDs -- 0 round robin,
                               // 1 contiguous runs, 2 runs that follow the conv taps (A/B)
   FILE* gemm_log = nullptr; // FX_GEMM_LOG=<file>: one line per GEMM launch (shape census)

@@ -292,6 +292,7 @@ struct GruBwdArgs {
   unsigned* tmo;        // the caller's status word (fx_gru_bidir_*: FX_STATUS_GRU_TIMEOUT on a lost peer)
   unsigned spin_max;
   int poll2;
+  int gate_wave;
   int off[MAXSEQ + 1];
 };
 
@@ -302,7 +303,7 @@ struct GruBwdArgs {
 // every workgroup and gathers NW x U = Hh of its own -- one granule per lane, the forward's exchange --
 // instead of gathering all 3Hh gate gradients (3 per lane).  Granule block of destination d, source j:
 // slot + (d * NW + j) * U.
-__global__ __launch_bounds__(GT) void gru_bwd_kernel(GruBwdArgs args) {
+__global__ __launch_bounds__(GTF) void gru_bwd_kernel(GruBwdArgs args) {
   const int sq = blockIdx.x / (2 * NW), rem = blockIdx.x - sq * 2 * NW;
   const int dir = rem / NW, j = rem - dir * NW;
   const GruBwdDirArgs& a = args.d[dir];
@@ -329,8 +330,11 @@ __global__ __launch_bounds__(GT) void gru_bwd_kernel(GruBwdArgs args) {
   const int kd = kput ? k / U : 0, kl = kput ? k - kd * U : 0;   // owner workgroup of unit k, its index there
   if (tid < MAXU) dh[tid] = 0.f;
   // step s's saved gates, h_{t-1} and output gradient are loaded during step s-1
-  const bool own = tid < U && u0 + tid < Hh;
-  const int uo = u0 + (own ? tid : 0);
+  // gate threads: wave 0's lanes < U, or (args.gate_wave, FX_GRU_BWD_GATE_WAVE) a fifth wave's, so that the
+  // four polling waves issue no gate-gradient stores or table loads
+  const int gl = args.gate_wave ? (wv == 4 ? lane : GTF) : tid;
+  const bool own = gl < U && u0 + gl < Hh;
+  const int uo = u0 + (own ? gl : 0);
   float nr = 0.f, nz = 0.f, nn = 0.f, ng = 0.f, nh = 0.f, nd = 0.f;
   auto fetch = [&](int t) {
     const float* gs = a.gates + (long long)t * 4 * Hh;
@@ -351,13 +355,13 @@ __global__ __launch_bounds__(GT) void gru_bwd_kernel(GruBwdArgs args) {
       const int u = uo;
       const float r = nr, z = nz, n = nn, ghn = ng, hp = nh, dcur = nd;
       if (s + 1 < S) fetch(r0 + (a.reverse ? s + 1 : S - 2 - s));
-      const float d = dcur + dh[tid];
+      const float d = dcur + dh[gl];
       const float dnp = d * (1.f - z) * (1.f - n * n);
       const float dzp = d * (hp - n) * z * (1.f - z);
       const float drp = dnp * ghn * r * (1.f - r);
-      dgo[tid] = drp;
-      dgo[U + tid] = dzp;
-      dgo[2 * U + tid] = dnp * r;
+      dgo[gl] = drp;
+      dgo[U + gl] = dzp;
+      dgo[2 * U + gl] = dnp * r;
       float* gi = a.dgi + (long long)t * a.lddgi;
       gi[u] = drp;
       gi[Hh + u] = dzp;
@@ -366,7 +370,7 @@ __global__ __launch_bounds__(GT) void gru_bwd_kernel(GruBwdArgs args) {
       gg[u] = drp;
       gg[Hh + u] = dzp;
       gg[2 * Hh + u] = dnp * r;
-      dhd[tid] = d * z;   // direct path; the NW partials of W^T dgh are added below
+      dhd[gl] = d * z;   // direct path; the NW partials of W^T dgh are added below
     }
     if (s + 1 == S) break;   // the last step's recurrent gradient feeds nothing
     __syncthreads();         // dgo of this step visible to every column thread
@@ -393,8 +397,8 @@ __global__ __launch_bounds__(GT) void gru_bwd_kernel(GruBwdArgs args) {
     if (dead) break;
     if (own) {   // sources in order (deterministic); dh[tid] / dhd[tid] are this thread's own
       float acc = 0.f;
-      for (int src = 0; src < NW; ++src) acc += red[src * U + tid];
-      dh[tid] = dhd[tid] + acc;
+      for (int src = 0; src < NW; ++src) acc += red[src * U + gl];
+      dh[gl] = dhd[gl] + acc;
     }
   }
 }
@@ -462,6 +466,7 @@ int launch_gru_bwd(const float* dout, long long lddo, int nseq, const int* seq_o
     GruBwdArgs args{};
     args.tmo = status ? status : tmo;
     args.spin_max = spin_max > 0 ? (unsigned)spin_max : SPIN_MAX;
+    args.gate_wave = knobs().gru_bwd_gate_wave;
     args.poll2 = knobs().gru_poll2;
     args.gran = gran + (long long)c0 * 2 * 2 * NW * NW * ((Hh + NW - 1) / NW);
     for (int q = 0; q <= nc; ++q) args.off[q] = seq_off[c0 + q];
@@ -478,7 +483,7 @@ int launch_gru_bwd(const float* dout, long long lddo, int nseq, const int* seq_o
       a.Hh = Hh;
       a.reverse = d;
     }
-    hipLaunchKernelGGL(gru_bwd_kernel, dim3(nc * 2 * NW), dim3(GT), 0, s, args);
+    hipLaunchKernelGGL(gru_bwd_kernel, dim3(nc * 2 * NW), dim3(args.gate_wave ? GTF : GT), 0, s, args);
     FX_CHECK_HIP(hipGetLastError());
   }
   return FX_OK;

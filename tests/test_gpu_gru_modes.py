@@ -22,7 +22,8 @@ pytestmark = pytest.mark.gpu
 
 VARIANTS = [{"FX_GRU_STORE_WAVE": "2", "FX_GRU_POLL2": "1"},
             {"FX_GRU_STORE_WAVE": "1", "FX_GRU_POLL2": "1"},
-            {"FX_GRU_STORE_WAVE": "0", "FX_GRU_POLL2": "0"}]
+            {"FX_GRU_STORE_WAVE": "0", "FX_GRU_POLL2": "0"},
+            {"FX_GRU_BWD_GATE_WAVE": "1"}]
 
 
 def _run(path):
