@@ -133,7 +133,7 @@ struct Knobs {
   bool frl_pair = true;        // FX_FRL_PAIR=0: the fused MS-TCN layer synchronises per 32-deep stage (A/B)
   int frl_pd = 3;              // FX_FRL_PD=3|5: fused MS-TCN layer weight prefetch distance in stages (A/B)
   int frl_ablate = 0;          // FX_FRL_ABLATE: diagnostic timing ablations of the fused layer (wrong results)
-  int frl_min_fill = 100;       // FX_FRL_MIN_FILL: fused MS-TCN layer only when its row tiles cover this % of the CUs
+  int frl_min_fill = 80;        // FX_FRL_MIN_FILL: fused MS-TCN layer only when its row tiles cover this % of the CUs (shipped yaml, 219 tiles: 80 vs 100 -> 54.5-54.8 vs 55.1-55.2 ms)
   bool aux_stream = true;       // FX_AUX_STREAM=0: the decoder's query-position gradient on the caller's stream
   int tattn_tc_max = 256;       // FX_TATTN_TC: largest key chunk per attention-over-T workgroup (32..256, A/B)
   bool gru_poll2 = true;        // FX_GRU_POLL2=0: one granule poll in flight per lane (A/B)

@@ -156,8 +156,9 @@ int launch_tattn_bwd(const float* q, long long ldq, const float* k, long long ld
 // -> row-local epilogue -> 1x1 GEMM; both weight matrices in the packed fragment order of
 // launch_pack_frag (FN x K floats each)
 bool frl_supported(int F, const void* x, long long ldx, long long ld_other);
-// whether rows / 32 row tiles fill every CU of the current device: below that the fused layer leaves CUs idle
-// and the two tuned GEMMs are faster (T = 2048 x 2 videos: 11.6-11.8 vs 12.0 ms per step)
+// whether rows / 32 row tiles cover FX_FRL_MIN_FILL (80) % of the CUs of the current device: below that the
+// fused layer leaves too many CUs idle and the two tuned GEMMs are faster (T = 2048 x 2 videos, 50 %: 11.6-11.8
+// vs 12.0 ms per step; the shipped yaml's 4096 + 2900 rows, 86 %: the fused layer 0.5 ms faster)
 bool frl_fills_device(long long rows);
 long long frl_packed_floats(int K);
 int launch_pack_frag(const float* const* src, float* const* dst, int n, long long ld, int K, hipStream_t s);
