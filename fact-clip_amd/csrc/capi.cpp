@@ -293,11 +293,15 @@ SideStream* side_stream() {
 
 // ---- MS-TCN layout of saved activations / workspace --------------------------------
 struct MstcnLayout {
+  // every per-layer row slot holds rows_pad = rows rounded up to the 64-deep GEMM stage; the pad rows of
+  // the h / z slots (forward) and of the deferred dZ / dH / dB slots (backward) are zero, so the deferred
+  // weight-gradient GEMMs run over K = rows_pad on the FAST loaders (ragged batches included)
+  long long rows_pad;
   long long rowsF;
   // saved
   long long h, z, xh, rs, wbs, wpts, total_saved;
   // workspace
-  long long wf, wb, wpt, wk1, wk2, buf0, buf1, buf2, buf3, buf4, buf5, split, split2, colsum, dzall, dhall, csb, bsl,
+  long long wf, wb, wpt, wk1, wk2, buf0, buf1, buf2, buf3, buf4, buf5, split, split2, colsum, dzall, dhall, dball, csb, bsl,
       total_ws;
 };
 
@@ -313,7 +317,8 @@ MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
   MstcnLayout L{};
   const long long F = p->F;
   const int NL = p->num_layers;
-  L.rowsF = (long long)rows * F;
+  L.rows_pad = (long long)cdiv(rows, 64) * 64;
+  L.rowsF = L.rows_pad * F;
   L.h = 0;                                   // h_0 .. h_NL
   L.z = L.h + (NL + 1) * L.rowsF;            // z_0 .. z_{NL-1}
   L.xh = L.z + NL * L.rowsF;                 // LN xhat_i
@@ -350,7 +355,8 @@ MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
   // dW GEMMs, and the batched conv-bias column sums
   L.dzall = L.colsum + cs;
   L.dhall = L.dzall + NL * L.rowsF;
-  L.csb = L.dhall + NL * L.rowsF;
+  L.dball = L.dhall + NL * L.rowsF;          // training dropout: dB_i = dropout_i(dH_i+1), the 1x1 branch's gradient
+  L.csb = L.dball + (p->dropout > 0.f ? NL * L.rowsF : 0);
   L.bsl = L.csb + (long long)NL * colsum_workspace_floats(rows, p->F);
   const int dsp = defer_split_impl(rows);
   L.total_ws = L.bsl + std::max(split_ws(p->F, p->F + 1, rows, std::max(NL, 1)),
@@ -441,14 +447,15 @@ int check_seqs(const Seqs& q) {
 }
 
 // dilated-conv operand over the call's videos (zero outside each video).  The column-major (weight-
-// gradient) form needs uniform videos: ragged calls run their weight gradients video by video.
+// gradient) form of a ragged call needs K padded to whole 64-deep stages (gemm_f32.hip COLS_CONVR): the
+// per-layer weight gradients (K = rows) run video by video instead.
 fx_operand conv_operand(const float* h, long long ld, int cin, int dil, int dir, const Seqs& q, bool trans) {
   fx_operand o = trans ? op_cols(h, ld) : op_rows(h, ld);
   o.conv_taps = 3;
   o.conv_cin = cin;
   o.conv_dil = dil;
   o.conv_dir = dir;
-  if (q.off && !trans) {
+  if (q.off) {   // (column-major: FAST loaders only, K padded to whole stages -- the deferred dW GEMMs)
     o.seq_off = q.off;
     o.nseq = q.nvid;
   } else {
@@ -608,6 +615,9 @@ int fx_mstcn_fwd(const fx_mstcn_params* p, const float* x, long long ldx, int T,
   const int F = p->F;
   const MstcnLayout L = mstcn_layout(p, rows);
   FX_TRY(pack_conv_weights(p, workspace, saved + L.wbs, saved + L.wpts, L, s));
+  if (L.rows_pad > rows && p->num_layers > 0)   // pad rows of h_0 .. h_NL, z_0 .. z_NL-1 (adjacent slots)
+    FX_CHECK_HIP(hipMemset2DAsync(saved + L.h + (long long)rows * F, L.rowsF * sizeof(float), 0,
+                                  (L.rows_pad - rows) * F * sizeof(float), 2 * p->num_layers + 1, s));
   float* h0 = saved + L.h;
   if (p->in_map) {
     FX_TRY(linear_fwd(x, ldx, rows, p->cin, p->w_in, p->b_in, h0, F, F, 0, s));
@@ -674,9 +684,19 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   float* ws = workspace;
   FX_REQUIRE(p->dropout >= 0.f && p->dropout < 1.f, "mstcn: dropout must be in [0, 1)");
   const bool drop = p->dropout > 0.f;
-  // Fused chain (no LayerNorm, no dropout, uniform videos, FX_MSTCN_FUSED=1): see below
-  const bool fchain = p->fused_layers && !p->layernorm && !drop && NL > 0 && frl_supported(F, ws + L.buf0, F, F) &&
-                      (!q.off || q.nvid <= 16) && (p->fused_layers == 2 || frl_fills_device(rows));
+  // the input block's stack (in_map) is the LAST work of the backward pass: its batched deferred weight
+  // gradients run after the chain with nothing left to overlap (a ~0.7 ms side-stream tail that the
+  // end-of-backward join waits for).  FX_MSTCN_TAIL=1 gives that stack the per-layer schedule that
+  // overlaps the chain instead; measured even (the per-layer split-K GEMMs slow the chain by as much),
+  // so it is off by default
+  const bool tail = p->in_map && knobs().mstcn_tail;
+  // deferred batched weight gradients (below); with training dropout the chain also keeps every layer's
+  // masked dB_i for the 1x1 weight gradient
+  const bool defer = !p->layernorm && NL > 0 && !tail && mstcn_defer_ok(p, g);
+  // Fused chain (no LayerNorm, <= 16 ragged videos, FX_MSTCN_FUSED=1; dropout on the deferred schedule): see below
+  const bool fchain = p->fused_layers && !p->layernorm && (!drop || defer) && NL > 0 &&
+                      frl_supported(F, ws + L.buf0, F, F) && (!q.off || q.nvid <= 16) &&
+                      (p->fused_layers == 2 || frl_fills_device(rows));
   // the dX-packed conv weights come from the forward (saved); the fused chain also needs the
   // transposed 1x1 weights (repacked here, into the workspace), both then in fragment order
   if (fchain) {
@@ -704,15 +724,12 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   // barriers and epilogue).  Without LayerNorm the chain's buffers rotate (dH over 3, dZ over 2)
   // so the side stream reads a layer's gU / dZ while the main stream computes the next layer;
   // a main-stream write waits for the side stream's layer that last read that buffer.
-  SideStream* ss = (p->layernorm || drop) ? nullptr : side_stream();
+  SideStream* ss = (p->layernorm || (drop && !defer)) ? nullptr : side_stream();
   hipStream_t sd = ss ? ss->s : s;
-  // the input block's stack (in_map) is the LAST work of the backward pass: its batched deferred weight
-  // gradients run after the chain with nothing left to overlap (a ~0.7 ms side-stream tail that the
-  // end-of-backward join waits for).  FX_MSTCN_TAIL=1 gives that stack the per-layer schedule that
-  // overlaps the chain instead; measured even (the per-layer split-K GEMMs slow the chain by as much),
-  // so it is off by default
-  const bool tail = p->in_map && knobs().mstcn_tail;
-  const bool defer = !p->layernorm && !drop && NL > 0 && !tail && mstcn_defer_ok(p, g);
+  // deferred: the pad rows of the dZ / dH (/ dB) slots are zero, so the batched dW GEMMs run over K = rows_pad
+  if (defer && L.rows_pad > rows)
+    FX_CHECK_HIP(hipMemset2DAsync(ws + L.dzall + (long long)rows * F, L.rowsF * sizeof(float), 0,
+                                  (L.rows_pad - rows) * F * sizeof(float), (drop ? 3 : 2) * NL, s));
   // FX_SIDE_MAXWG=n: the side stream's split-K GEMMs keep within n workgroups (A/B diagnostic)
   GridCap gcap(ss ? knobs().side_maxwg : 0);
   auto fork = [&](int e) -> int {   // side stream waits for the main stream's work so far
@@ -806,6 +823,9 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   if (defer) {
     float* dZall = ws + L.dzall;
     float* dHall = ws + L.dhall;   // dHall[i] = dH_{i+1} (gradient at layer i's output)
+    // the 1x1 branch's gradient: dB_i = dropout_i(dH_i+1) with the forward's mask (basic.py:160), else dH_i+1
+    float* dBall = drop ? ws + L.dball : dHall;
+    const int Kp = (int)L.rows_pad;
     // the batched weight gradients of layers [base, base + nb) on the side stream
     auto batched_dw = [&](int base, int nb) -> int {
       if (nb <= 0) return FX_OK;
@@ -814,9 +834,9 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
         fx_operand b = op_cols(saved + L.z + (long long)base * L.rowsF, F);
         b.batch_stride = L.rowsF;
         b.ones_col = F + 1;
-        fx_operand a = op_cols(dHall + (long long)base * L.rowsF, F);
+        fx_operand a = op_cols(dBall + (long long)base * L.rowsF, F);
         a.batch_stride = L.rowsF;
-        fx_gemm_desc d = gemm_desc(F, F + 1, rows, a, b, g->w_pw[base], F);
+        fx_gemm_desc d = gemm_desc(F, F + 1, Kp, a, b, g->w_pw[base], F);
         d.batch = nb;
         d.c_batch_stride = NL > 1 ? g->w_pw[1] - g->w_pw[0] : 0;
         d.c_last_col = g->b_pw[base];
@@ -828,24 +848,21 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
         FX_TRY(launch_gemm(d, sd));
       }
       {   // dilated conv: dW_i += dZ_i^T taps(h_i) stored straight into (F, F, 3)   (batched over layers;
-          // ragged videos: one such launch per video, accumulating)
+          // ragged videos in the same launch: the B loader finds each frame's video, gemm_f32.hip COLS_CONVR)
         WsBound wbb(ws + L.bsl, L.total_ws - L.bsl);
-        FX_TRY(per_video(q, [&](int r0, int nr, const Seqs& qv) -> int {
-          fx_operand b = conv_operand(saved + L.h + (long long)base * L.rowsF + (long long)r0 * F, F, F,
-                                      layer_dilation(p, base), 1, qv, true);
-          b.batch_stride = L.rowsF;
-          fx_operand a = op_cols(dZall + (long long)base * L.rowsF + (long long)r0 * F, F);
-          a.batch_stride = L.rowsF;
-          fx_gemm_desc d = gemm_desc(F, 3 * F, nr, a, b, g->w_dil[base], 3 * F);
-          d.batch = nb;
-          d.c_batch_stride = NL > 1 ? g->w_dil[1] - g->w_dil[0] : 0;
-          d.b_dil_growth = p->dil_factor > 0 ? p->dil_factor : 2;
-          d.c_tap_cin = F;
-          d.beta = 1.f;
-          d.split_k = defer_split_impl(nr);
-          d.workspace = ws + L.bsl;
-          return launch_gemm(d, sd);
-        }));
+        fx_operand b = conv_operand(saved + L.h + (long long)base * L.rowsF, F, F, layer_dilation(p, base), 1, q, true);
+        b.batch_stride = L.rowsF;
+        fx_operand a = op_cols(dZall + (long long)base * L.rowsF, F);
+        a.batch_stride = L.rowsF;
+        fx_gemm_desc d = gemm_desc(F, 3 * F, Kp, a, b, g->w_dil[base], 3 * F);
+        d.batch = nb;
+        d.c_batch_stride = NL > 1 ? g->w_dil[1] - g->w_dil[0] : 0;
+        d.b_dil_growth = p->dil_factor > 0 ? p->dil_factor : 2;
+        d.c_tap_cin = F;
+        d.beta = 1.f;
+        d.split_k = defer_split_impl(rows);
+        d.workspace = ws + L.bsl;
+        FX_TRY(launch_gemm(d, sd));
         FX_TRY(launch_colsum_batched(dZall + (long long)base * L.rowsF, F, L.rowsF, rows, F, nb, g->b_dil[base],
                                      NL > 1 ? g->b_dil[1] - g->b_dil[0] : 0, 1, ws + L.csb, sd));
       }
@@ -859,13 +876,18 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
       // the fused chain into the per-layer slots: dZ_NL-1 by the 1x1 backward GEMM, then per layer ONE
       // kernel for dH_i (-> dHall[i-1]) and dZ_i-1 (-> dZall[i-1]); the bottom layer's conv backward
       // alone; the weight gradients of every layer follow as the batched side-stream GEMMs below
-      FX_TRY(pw_dx(dHall + (NL - 1) * L.rowsF, NL - 1, dZall + (NL - 1) * L.rowsF, saved + L.z + (NL - 1) * L.rowsF));
+      if (drop)
+        FX_TRY(launch_dropout(dHall + (NL - 1) * L.rowsF, F, rows, F, F, 0, p->dropout,
+                              fx_drop_subseed(p->seed, NL - 1), dBall + (NL - 1) * L.rowsF, F, s));
+      FX_TRY(pw_dx(dBall + (NL - 1) * L.rowsF, NL - 1, dZall + (NL - 1) * L.rowsF, saved + L.z + (NL - 1) * L.rowsF));
       if (NL > 1) prof_begin(7, s);   // (the chain of NL - 1 back-to-back launches timed as one)
       for (int i = NL - 1; i >= 1; --i) {
         FX_TRY(launch_frl(dZall + i * L.rowsF, F, rows, T, layer_dilation(p, i), -1, q.off, q.nvid,
                           ws + L.wk1 + (long long)i * 3 * F * F, nullptr, 0, dHall + i * L.rowsF, F,
                           dHall + (i - 1) * L.rowsF, F, ws + L.wk2 + (long long)(i - 1) * F * F, nullptr, nullptr, 0,
-                          saved + L.z + (i - 1) * L.rowsF, F, dZall + (i - 1) * L.rowsF, F, 0.f, 0, s));
+                          saved + L.z + (i - 1) * L.rowsF, F, dZall + (i - 1) * L.rowsF, F, 0.f, 0, s,
+                          drop ? p->dropout : 0.f, fx_drop_subseed(p->seed, i - 1),
+                          drop ? dBall + (i - 1) * L.rowsF : nullptr, F));
       }
       if (NL > 1)
         prof_end(7, s, (NL - 1) * 2.0 * rows * F * 4.0 * F, (NL - 1) * 4.0 * (4.0 * rows * F + 4.0 * F * F), NL - 1);
@@ -874,7 +896,12 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
       const float* zi = saved + L.z + i * L.rowsF;
       const float* gU = dHall + i * L.rowsF;
       float* dZ = dZall + i * L.rowsF;
-      if (!fchain) FX_TRY(pw_dx(gU, i, dZ, zi));   // (fused chain: dZ_0 came with dH_1)
+      if (!fchain) {   // (fused chain: dZ_0 came with dH_1)
+        if (drop)
+          FX_TRY(launch_dropout(gU, F, rows, F, F, 0, p->dropout, fx_drop_subseed(p->seed, i), dBall + i * L.rowsF,
+                                F, s));
+        FX_TRY(pw_dx(dBall + i * L.rowsF, i, dZ, zi));
+      }
       float* dHn = i > 0 ? dHall + (i - 1) * L.rowsF : Hb[0];
       fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dZ, F, F, layer_dilation(p, i), -1, q, false),
                                  op_rows(wbp + (long long)i * 3 * F * F, 3 * F), dHn, F);
@@ -1753,9 +1780,12 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
   // dxk, dyq out
   const double na = (double)V.a[V.n];
   const double core_bytes = 4.0 * (2.0 * Ny * Hd + 4.0 * Nx * Hd + 4.0 * na + (double)Ny * Hd);
-  const bool f2a_shape = x2y_f2a_fusable(V.n, V.x.data(), V.y.data(), Hd);
+  // the fused f2a core (bracketed as fx_prof kind 6 only when it runs: the per-video GEMM fallback below
+  // is not the kernel whose algorithmic bytes kind 6 reports)
+  const bool f2a_fused = !fused && knobs().x2y_fused && knobs().x2y_f2a_bwd &&
+                         x2y_f2a_fusable(V.n, V.x.data(), V.y.data(), Hd) && (cw & 3) == 0 && al16;
   if (fused) prof_begin(4, s);
-  else if (f2a_shape) prof_begin(6, s);
+  else if (f2a_fused) prof_begin(6, s);
   if (fused) {
     FX_TRY(launch_x2y_a2f_bwd(dcat + ydim, cw, xv, xk, attn, dattn, dlogit, Hd, scale, V.n, V.y.data(), V.x.data(),
                               V.a.data(), dL, dyq, s));
@@ -1780,8 +1810,7 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
       }
       FX_TRY(launch_gemm_group(g2, n2, s));
     }
-  } else if (knobs().x2y_fused && knobs().x2y_f2a_bwd && x2y_f2a_fusable(V.n, V.x.data(), V.y.data(), Hd) &&
-             (cw & 3) == 0 && al16) {
+  } else if (f2a_fused) {
     // the f2a map: dP / dxv, then dlogit / dxk / dyq partials per 64-key chunk, then the ordered dyq merge
     float* f2a_ws = workspace + x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, V) + (long long)Ny * cw +
                     x2y_side_ws(Nx, xdim, Ny, ydim, Hd, outdim);
@@ -1833,7 +1862,7 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
     FX_TRY(launch_gemm_group(g2, n2, s));
   }
   if (fused) prof_end(4, s, 8.0 * na * Hd, core_bytes);
-  else if (f2a_shape) prof_end(6, s, 8.0 * na * Hd, core_bytes);
+  else if (f2a_fused) prof_end(6, s, 8.0 * na * Hd, core_bytes);
   // weight gradients (Y_W; projections X_K, X_V, Y_Q): nothing below needs them -> side stream, each
   // frame-level GEMM split defer_split(rows) ways into its own slab region
   {

@@ -9,6 +9,8 @@
 //   ROWS_GEN  concatenated inputs / row gathers / positional adds (generic)
 //   COLS      element (r,k) = p[k*ld + r]            dY^T for dW, W^T for dX
 //   COLS_CONV conv input for dW, tap from r; optional all-ones row (bias grad)
+//   COLS_CONVR the same over ragged videos (host row offsets): weight gradients of a ragged batch in
+//             one launch, K padded to whole stages (rows past the last video read as zero)
 //
 // Tiled kernel: 64x64 output tile per 256-thread workgroup, one wave per SIMD, each wave a
 // 32x32 sub-tile over the block's whole K range (32 MFMAs = 2048 matrix-core cycles per
@@ -48,7 +50,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 //           either gather optional -- the FAST form of the concatenation / gather operands
 constexpr int kMaxSeq = 16;        // ragged videos per conv operand
 
-enum Kind { ROWS = 0, ROWS_CONV = 1, ROWS_GEN = 2, COLS = 3, COLS_CONV = 4, ROWS_CAT = 5 };
+enum Kind { ROWS = 0, ROWS_CONV = 1, ROWS_GEN = 2, COLS = 3, COLS_CONV = 4, ROWS_CAT = 5, COLS_CONVR = 6 };
 
 struct GemmDev {
   int M, N, K;
@@ -79,7 +81,7 @@ struct GemmDev {
   long long bias_bs;    // bias of batch b at bias + b * bias_bs
   int nt_store;         // FX_GEMM_NTSTORE=1 (A/B): the fast epilogue stores non-temporally
   int nsoff;            // > 0: the conv operand's videos are ragged: video v owns rows [soff[v], soff[v+1])
-  int soff[kMaxSeq + 1];
+  int soff[kMaxSeq + 1];   // (COLS_CONVR: entries past nsoff are INT_MAX)
 };
 
 // Position of row r inside its video and the video's length (the conv operand's zero padding):
@@ -166,6 +168,20 @@ __device__ __forceinline__ float fetch_rm(const fx_operand& o, const float* p0, 
   return v;
 }
 
+// COLS_CONVR: does frame k + s lie in frame k's video?  Branch-free over the 16 offsets (entries past
+// the last video are INT_MAX, so frames past the last video -- the K padding -- are never valid).
+__device__ __forceinline__ bool seq_same(const SeqOff& soff, int k, int s) {
+  int start = 0, end = 0x7fffffff;
+#pragma unroll
+  for (int i = 1; i <= kMaxSeq; ++i) {
+    const int o = soff[i];
+    start = o <= k ? o : start;
+    end = o > k ? min(end, o) : end;
+  }
+  const int t = k + s;
+  return end != 0x7fffffff && t >= start && t < end;
+}
+
 __device__ __forceinline__ float fetch_cm(const fx_operand& o, const float* p0, int r, int k) {
   if (o.ones_col && r == o.ones_col - 1) return 1.f;
   if (o.conv_taps) {   // uniform videos only (ragged weight gradients run per video)
@@ -222,8 +238,8 @@ struct Loader {
                                        const SeqOff& soff_, int nsoff_) {
     o = op;
     base = p0;
-    nsoff = (KIND == ROWS_CONV || KIND == ROWS_GEN) ? nsoff_ : 0;
-    if (KIND == ROWS_GEN) {   // the generic element fetch (edge shapes) looks rows up per element
+    nsoff = (KIND == ROWS_CONV || KIND == ROWS_GEN || KIND == COLS_CONVR) ? nsoff_ : 0;
+    if (KIND == ROWS_GEN || KIND == COLS_CONVR) {   // the generic element fetch (edge shapes) looks rows up per element
 #pragma unroll
       for (int i = 0; i <= kMaxSeq; ++i) soff[i] = soff_[i];
     }
@@ -266,7 +282,7 @@ struct Loader {
       }
       rc = min(r, ((stored - 1) / 4) * 4);
       pcol = p0 + (long long)ta * op.ld + rc;
-      if (KIND == COLS_CONV) {
+      if (KIND == COLS_CONV || KIND == COLS_CONVR) {
         const int j = rc / op.conv_cin;
         tapc = rc - j * op.conv_cin;
         tap_s = conv_shift(op, j);
@@ -324,6 +340,15 @@ struct Loader {
         vm |= (ok ? 1u : 0u) << j;
         v[j] = ldg4(base + (long long)(ok ? k + tap_s : k) * o.ld + tapc);
       }
+    } else if (KIND == COLS_CONVR) {
+      vm = 0;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int k = k0 + ta + RSTEP * j;
+        const bool ok = seq_same(soff, k, tap_s);
+        vm |= (ok ? 1u : 0u) << j;
+        v[j] = ldg4(base + (long long)(ok ? k + tap_s : k) * o.ld + tapc);
+      }
     }
   }
 
@@ -362,7 +387,7 @@ struct Loader {
       for (int j = 0; j < NJ; ++j) {
         float e[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
         if (FAST) {
-          const bool tok = KIND != COLS_CONV || ((vm >> j) & 1u);
+          const bool tok = (KIND != COLS_CONV && KIND != COLS_CONVR) || ((vm >> j) & 1u);
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const float one = ((omask >> q) & 1u) ? 1.f : 0.f;
@@ -1682,7 +1707,7 @@ bool operand_vec_ok(const fx_operand& o) {
 }
 
 int kind_of(const fx_operand& o, bool vec) {
-  if (o.trans) return o.conv_taps ? COLS_CONV : COLS;
+  if (o.trans) return o.conv_taps ? (o.nseq > 0 ? COLS_CONVR : COLS_CONV) : COLS;
   if (o.conv_taps) return (vec && o.conv_cin % BK == 0) ? ROWS_CONV : ROWS_GEN;   // a stage stays in one tap
   if (o.pos) return ROWS_GEN;
   if (o.ptr1 || o.rows0 || o.rows1) return (vec && (!o.ptr1 || o.k_split % BK == 0)) ? ROWS_CAT : ROWS_GEN;
@@ -1705,6 +1730,12 @@ int launch_wide_b(int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
     case COLS_CONV:
       hipLaunchKernelGGL((gemm_f32_wide_kernel<AK, COLS_CONV>), grid, dim3(NTHREADS), 0, s, g);
       return FX_OK;
+    case COLS_CONVR:
+      if constexpr (AK == COLS) {
+        hipLaunchKernelGGL((gemm_f32_wide_kernel<AK, COLS_CONVR>), grid, dim3(NTHREADS), 0, s, g);
+        return FX_OK;
+      }
+      break;
     default: break;
   }
   set_error("gemm(wide): unsupported B operand kind");
@@ -1719,6 +1750,12 @@ int launch_wide8_b(int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
     case COLS_CONV:
       hipLaunchKernelGGL((gemm_f32_wide8_kernel<AK, COLS_CONV>), grid, dim3(W8T), 0, s, g);
       return FX_OK;
+    case COLS_CONVR:
+      if constexpr (AK == COLS) {
+        hipLaunchKernelGGL((gemm_f32_wide8_kernel<AK, COLS_CONVR>), grid, dim3(W8T), 0, s, g);
+        return FX_OK;
+      }
+      break;
     default: break;
   }
   set_error("gemm(wide8): unsupported B operand kind");
@@ -1755,6 +1792,13 @@ int launch_b(int bk, dim3 grid, hipStream_t s, const GemmDev& g, bool fast) {
     case ROWS: launch_t<AK, ROWS>(grid, s, g, fast); return FX_OK;
     case COLS: launch_t<AK, COLS>(grid, s, g, fast); return FX_OK;
     case COLS_CONV: launch_t<AK, COLS_CONV>(grid, s, g, fast); return FX_OK;
+    case COLS_CONVR:   // FAST only (plan_gemm checks): the ragged frame lookup lives in the FAST loader
+      if constexpr (AK == COLS) {
+        if (!fast) break;
+        hipLaunchKernelGGL((gemm_f32_kernel<AK, COLS_CONVR, true>), grid, dim3(NTHREADS), 0, s, g);
+        return FX_OK;
+      }
+      break;
     case ROWS_GEN:
     case ROWS_CAT: launch_t<AK, ROWS_GEN>(grid, s, g, false); return FX_OK;
     default: break;
@@ -1837,7 +1881,7 @@ bool use_wide(const GemmDev& g, int ak, int bk, int batch) {
   const int force = knobs().gemm_wide;
   const bool fast = g.a_vec && g.b_vec && (g.K % BK) == 0;
   const bool ok = fast && (ak == ROWS || ak == ROWS_CONV || ak == ROWS_CAT || ak == COLS) &&
-                  (bk == ROWS || bk == COLS || bk == COLS_CONV);
+                  (bk == ROWS || bk == COLS || bk == COLS_CONV || bk == COLS_CONVR);
   if (!ok || force == 0) return false;
   if (force == 1) return true;
   return (long long)cdiv(g.M, WBM) * g.tiles_x * batch * g.split >= 192;
@@ -1937,8 +1981,9 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
   FX_REQUIRE(!(d.a.conv_taps && d.a.seq_len <= 0 && d.a.nseq <= 0) &&
                  !(d.b.conv_taps && d.b.seq_len <= 0 && d.b.nseq <= 0),
              "gemm: conv operand needs seq_len or seq_off");
-  FX_REQUIRE(d.b.nseq <= 0 && (d.a.nseq <= 0 || !d.a.trans),
-             "gemm: ragged conv offsets only on a row-major A operand (weight gradients run per video)");
+  FX_REQUIRE(d.a.nseq <= 0 || !d.a.trans, "gemm: ragged conv offsets on a row-major A or a column-major B operand");
+  FX_REQUIRE(d.b.nseq <= 0 || (d.b.trans && d.b.conv_taps && d.a.nseq <= 0),
+             "gemm: ragged column-major conv B needs a plain A operand");
   FX_REQUIRE(!(d.a.conv_taps && d.K != d.a.conv_taps * d.a.conv_cin), "gemm: conv A needs K == taps*cin");
   FX_REQUIRE(!(d.b.conv_taps && d.b.trans && d.N != d.b.conv_taps * d.b.conv_cin + (d.b.ones_col ? 1 : 0)),
              "gemm: conv B needs N == taps*cin (+1 with a ones column)");
@@ -1960,6 +2005,21 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
       for (int v = 0; v <= o.nseq; ++v) {
         FX_REQUIRE(v == 0 || o.seq_off[v] > o.seq_off[v - 1], "gemm: seq_off must increase");
         g.soff[v] = o.seq_off[v];
+      }
+      g.nsoff = o.nseq;
+    }
+  }
+  {   // ragged column-major conv B (weight gradients of a ragged batch, K = frames): K may pad the last
+      // video to whole 64-deep stages; those frames read as zero
+    const fx_operand& o = d.b;
+    if (o.nseq > 0) {
+      FX_REQUIRE(o.seq_off && o.nseq <= kMaxSeq && o.seq_off[0] == 0 && o.seq_off[o.nseq] <= d.K,
+                 "gemm: ragged B offsets must start at 0 and end within K, <= 16 videos");
+      FX_REQUIRE(operand_vec_ok(d.a) && operand_vec_ok(d.b) && d.K % BK == 0,
+                 "gemm: ragged B needs 16-B operands and K a multiple of 64 (pad the frames)");
+      for (int v = 0; v <= kMaxSeq; ++v) {
+        FX_REQUIRE(v == 0 || v > o.nseq || o.seq_off[v] > o.seq_off[v - 1], "gemm: seq_off must increase");
+        g.soff[v] = v <= o.nseq ? o.seq_off[v] : 0x7fffffff;
       }
       g.nsoff = o.nseq;
     }
@@ -2076,8 +2136,9 @@ void log_gemm(const fx_gemm_desc& d, const GemmPlan& P, int member = 0) {
   // FX_GEMM_LOG=<file>: append one line per launch (diagnostic shape census, tools/gemm_census.py)
   FILE* glog = knobs().gemm_log;
   if (glog)
-    std::fprintf(glog, "%d %d %d %d %d %d %d %d %d %d %d %d\n", d.M, d.N, d.K, d.batch, P.ak, P.bk, P.g.split,
-                 d.a.conv_taps, d.b.conv_taps, d.relu, P.direct ? (int)P.block.x / 64 : (P.wide ? -1 : 0), member);
+    std::fprintf(glog, "%d %d %d %d %d %d %d %d %d %d %d %d %d %d\n", d.M, d.N, d.K, d.batch, P.ak, P.bk, P.g.split,
+                 d.a.conv_taps, d.b.conv_taps, d.relu, P.direct ? (int)P.block.x / 64 : (P.wide ? -1 : 0), member,
+                 P.g.a_vec + 2 * P.g.b_vec, d.K % BK == 0);
 }
 
 int launch_reduce(const fx_gemm_desc& d, const GemmPlan& P, hipStream_t s) {

@@ -158,6 +158,10 @@ __global__ __launch_bounds__(GTF) void gru_fwd_kernel(GruArgs args) {
   // counter as the granule polls, so the polling waves issue no table stores of their own (the backward,
   // with two barriers per step, measured no gain from the same change and keeps its gate-thread stores)
   __shared__ float stage[2][6][MAXU];
+  // lost peer: 1 + the step whose gather gave up.  A step number, not a flag, because with one barrier
+  // per step a fast wave may already be in step s + 1's gather while a slow one still reads the word
+  // after barrier s: a failure of step s + 1 must not make the slow wave leave at step s (the waves
+  // would then run different numbers of barriers)
   __shared__ int dead;
   if (tid == 0) dead = 0;
   const int wv = tid >> 6;
@@ -211,7 +215,7 @@ __global__ __launch_bounds__(GTF) void gru_fwd_kernel(GruArgs args) {
     if (s > 0 && kcn > 0 && !storer) {   // the state after step s-1: granules of epoch s in slot (s-1) & 1
       if (!gather_granules(gran + (long long)((s - 1) & 1) * Hh + kc0, kcn, (unsigned)s, hc + kc0, args.tmo,
                            args.spin_max, lane, args.poll2 != 0))
-        dead = 1;
+        dead = s + 1;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS writes land before its reads
     }
     if (!storer) {
@@ -229,7 +233,10 @@ __global__ __launch_bounds__(GTF) void gru_fwd_kernel(GruArgs args) {
       part[s & 1][wv][o] = (c0 + c1) + (c2 + c3);
     }
     __syncthreads();
-    if (dead) break;
+    {
+      const int ds = dead;
+      if (ds != 0 && ds <= s + 1) break;
+    }
     if (storer && s > 0 && args.store_wave == 1) flush(s - 1);
     if (own) {
       const int u = uo;

@@ -6,7 +6,10 @@
 //                        h_i+1 = h_i + dropout(z . W_pw^T + b_pw)      -> out2
 //   backward (layers i, i-1 of the dX chain):
 //                        dH_i   = gU_i + conv_d^T(dZ_i)               -> out1
-//                        dZ_i-1 = (dH_i . W_pw,i-1) * (z_i-1 > 0)     -> out2
+//                        dB_i-1 = dropout_i-1(dH_i)                   -> out3 (training dropout only)
+//                        dZ_i-1 = (dB_i-1 . W_pw,i-1) * (z_i-1 > 0)   -> out2
+// (with dropout the 1x1 branch of layer i-1 saw mask m: its gradient is dH_i masked the same way --
+// the phase-1 tile is masked on its way into LDS, the unmasked dH_i goes to out1 for the residual)
 //
 // A workgroup owns FR = 32 rows and all F = 256 channels (8 waves x 32 columns, one 32x32 f32 MFMA
 // accumulator each): the full-width row tile is what makes the second GEMM row-local, and 8192 rows
@@ -74,6 +77,11 @@ struct FrlArgs {
   unsigned drop_thr;   // dropout on (acc2 + bias2) before resid2; 0 = off
   float drop_scale;
   unsigned long long drop_seed;
+  unsigned vdrop_thr;  // dropout on the phase-1 tile as phase 2 reads it (out1 keeps it unmasked); 0 = off
+  float vdrop_scale;
+  unsigned long long vdrop_seed;
+  float* out3;         // nullable: the masked phase-1 tile (vdrop only)
+  long long ldo3;
 };
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -278,6 +286,10 @@ __global__ __launch_bounds__(FT) void frl_kernel(FrlArgs g) {
       if (g.relu1) v = fmaxf(v, 0.f);
       v += r1[q];
       if (gr < g.M && !(g.ablate & 8)) g.out1[(long long)gr * g.ldo1 + col] = v;
+      if (g.vdrop_thr) {
+        v = fx_drop_bits(g.vdrop_seed, (unsigned long long)gr * FN + col) >= g.vdrop_thr ? v * g.vdrop_scale : 0.f;
+        if (g.out3 && gr < g.M) g.out3[(long long)gr * g.ldo3 + col] = v;
+      }
       V[row * VS + col] = v;
       acc[q] = 0.f;
     }
@@ -385,13 +397,15 @@ int launch_frl(const float* x, long long ldx, int M, int T, int dil, int dir, co
                const float* w1p, const float* bias1, int relu1, const float* resid1, long long ldr1, float* out1,
                long long ldo1, const float* w2p, const float* bias2, const float* resid2, long long ldr2,
                const float* gate2, long long ldg2, float* out2, long long ldo2, float drop_p,
-               unsigned long long drop_seed, hipStream_t s) {
+               unsigned long long drop_seed, hipStream_t s, float vdrop_p, unsigned long long vdrop_seed, float* out3,
+               long long ldo3) {
   FX_REQUIRE(M > 0 && dil > 0 && (dir == 1 || dir == -1), "frl: bad shape");
   FX_REQUIRE(seq_off ? (nseq >= 1 && nseq <= kMaxSeqF && seq_off[0] == 0 && seq_off[nseq] == M) : T > 0,
              "frl: uniform videos of T rows, or ragged offsets spanning [0, M) (<= 16 videos)");
   FX_REQUIRE(frl_supported(FN, x, ldx, ldo1) && ((uintptr_t)w1p & 15) == 0 && ((uintptr_t)w2p & 15) == 0,
              "frl: needs F = 256 and 16-byte aligned rows");
-  FX_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "frl: dropout must be in [0, 1)");
+  FX_REQUIRE(drop_p >= 0.f && drop_p < 1.f && vdrop_p >= 0.f && vdrop_p < 1.f, "frl: dropout must be in [0, 1)");
+  FX_REQUIRE(!out3 || (vdrop_p > 0.f && ldo3 % 4 == 0), "frl: out3 holds the masked tile of a dropout layer");
   static const bool attr = [] {
     return hipFuncSetAttribute((const void*)frl_kernel<false, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                LDS_FLOATS * (int)sizeof(float)) == hipSuccess &&
@@ -433,6 +447,11 @@ int launch_frl(const float* x, long long ldx, int M, int T, int dil, int dir, co
   a.drop_thr = drop_p > 0.f ? std::max(fx_drop_thresh(drop_p), 1u) : 0u;
   a.drop_scale = 1.f / (1.f - drop_p);
   a.drop_seed = drop_seed;
+  a.vdrop_thr = vdrop_p > 0.f ? std::max(fx_drop_thresh(vdrop_p), 1u) : 0u;
+  a.vdrop_scale = 1.f / (1.f - vdrop_p);
+  a.vdrop_seed = vdrop_seed;
+  a.out3 = out3;
+  a.ldo3 = ldo3;
   if (!knobs().frl_pair)
     hipLaunchKernelGGL((frl_kernel<false, 3>), dim3(nt), dim3(FT), LDS_FLOATS * sizeof(float), s, a);
   else if (knobs().frl_pd == 5)

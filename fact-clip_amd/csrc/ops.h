@@ -166,6 +166,7 @@ int launch_frl(const float* x, long long ldx, int M, int T, int dil, int dir, co
                const float* w1p, const float* bias1, int relu1, const float* resid1, long long ldr1, float* out1,
                long long ldo1, const float* w2p, const float* bias2, const float* resid2, long long ldr2,
                const float* gate2, long long ldg2, float* out2, long long ldo2, float drop_p,
-               unsigned long long drop_seed, hipStream_t s);
+               unsigned long long drop_seed, hipStream_t s, float vdrop_p = 0.f, unsigned long long vdrop_seed = 0,
+               float* out3 = nullptr, long long ldo3 = 0);
 
 }  // namespace fx

@@ -281,6 +281,22 @@ class DataParallel:
             self._thread.start()
         return self._q
 
+    def _issue_status(self):
+        """All-reduce (MAX) the device status word behind the gradient buckets, on the device: a rank
+        whose BiGRU timed out in this backward (invalid gradients, already summed into the buckets) makes
+        EVERY rank's FusedAdam skip the update (fx_adam_step_checked reads the word) and every rank raise
+        at its next read-back, so the replicas neither apply corrupted averages nor diverge."""
+        if self.world <= 1:
+            return
+        st = fxf.device_status(self.flat.device)[:1]
+        cs = self._cstream
+        if cs is None:
+            self._pending.append((dist.all_reduce(st, op=dist.ReduceOp.MAX, group=self.group, async_op=True), False))
+            return
+        cs.wait_stream(torch.cuda.current_stream(cs.device))
+        with torch.cuda.stream(cs):
+            self._pending.append((dist.all_reduce(st, op=dist.ReduceOp.MAX, group=self.group, async_op=True), False))
+
     def _launch_block(self, k, from_hook=False):
         if not self.active or k in self._launched:
             return
@@ -300,6 +316,7 @@ class DataParallel:
         self._launched.update(self.block_buckets)
         fxf.side_join()           # (the backward's end-of-pass callback has normally joined already)
         self._issue(_merge_adjacent(left + list(self.rest_buckets)))
+        self._issue_status()
         if self._q is not None:
             self._q.join()        # every collective has been issued (the helper thread is idle)
             if self._worker_error is not None:

@@ -293,9 +293,12 @@ typedef struct fx_mstcn_params {
                                  [seq_off[v], seq_off[v+1]), zero padding at its own ends; nvid <= 16;
                                  T ignored); NULL: nvid videos of T rows */
   int fused_layers;           /* 1: the fused one-kernel layer (conv -> epilogue -> 1x1, F = 256, no LN,
-                                 <= 16 videos) where it applies and its 32-row tiles cover every CU
-                                 (fewer rows: the two tuned GEMMs are faster); 2: wherever it applies
-                                 (tests); 0: the two GEMMs per layer */
+                                 <= 16 ragged or uniform videos, training dropout included) where it
+                                 applies and its 32-row tiles cover FX_FRL_MIN_FILL (default 80) % of
+                                 the CUs (fewer rows: the two tuned GEMMs are faster); 2: wherever it
+                                 applies (tests); 0: the two GEMMs per layer.  The backward's fused dX
+                                 chain needs the deferred weight gradients (uniformly strided gradient
+                                 buffers) when dropout is on: it keeps the masked 1x1 gradient dB_i */
 } fx_mstcn_params;
 
 typedef struct fx_mstcn_grads {

@@ -169,6 +169,38 @@ def test_data_parallel_refuses_gradient_accumulation(tmp_path):
     assert torch.load(out, weights_only=True).tolist() == [True]
 
 
+def _status_worker(rank, world, port, out_path):
+    from factmx import functional as fxf
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        net = _ToyBlocks(seed=0)
+        dp = DataParallel(net, bucket_mb=0.0002)
+        st = fxf.device_status("cpu")
+        got = []
+        for fail in (True, False):
+            st.zero_()
+            dp.zero_grad()
+            net(_videos()[rank]).pow(2).mean().backward()
+            if fail and rank == 1:
+                st[0] = 2                    # this rank's BiGRU backward timed out (FX_STATUS_GRU_TIMEOUT)
+            dp.finish_gradients()
+            got.append(int(st[0]))
+        torch.save(torch.tensor(got), out_path + f".{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_spreads_a_failed_backward_to_every_rank(tmp_path):
+    """A rank whose kernels set the device status word in the backward (invalid gradients, already in
+    the all-reduced buckets) makes every rank see it after finish_gradients (MAX all-reduce of the word):
+    every rank's FusedAdam then skips the update on the device and raises at its next read-back."""
+    out = str(tmp_path / "st.pt")
+    mp.spawn(_status_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        assert torch.load(out + f".{r}", weights_only=True).tolist() == [2, 0]
+
+
 def test_bench_refuses_more_gpus_than_visible():
     """bench.py --gpus N must start N ranks or refuse: never time one rank for an N-GPU request."""
     import subprocess

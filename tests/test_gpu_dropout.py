@@ -225,3 +225,68 @@ def test_fact_clip_trains_with_havid_dropout():
     assert math.isfinite(l1) and torch.isfinite(g1).all()
     assert l1 == l2 and torch.equal(g1, g2)
     assert l1 != l3
+
+
+def _prof_count(lib, kind):
+    import ctypes
+    ms, fl, by, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+    assert lib.fx_prof_collect(kind, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(by), ctypes.byref(n)) == 0
+    return n.value
+
+
+@pytest.mark.parametrize("fused,flat", [(1, True), (2, True), (0, True), (1, False)])
+def test_mstcn_dropout_ragged_shipped_rows(fused, flat, fixed_seeds, monkeypatch):
+    """The shipped yaml's frame branch shape in training (havid_view0_lh_pt_holdout.yaml: F = 256, 10
+    layers, dropout 0.2, basic.py:154-171) on its ragged 4096 + 2900 batch (219 row tiles: the fused
+    layer under the default 80 % fill rule).  fused: 1 = the library's fill rule, 2 = forced, 0 = the
+    two-GEMM layers; flat: gradients as views of one flat buffer (the deferred batched weight gradients
+    over K = rows rounded up to the 64-deep stage, the masked 1x1 gradient dB kept by the fused dX
+    chain) or separate buffers (the per-layer single-stream path).  Output, input gradient and every
+    weight gradient vs the float64 restatement with the SAME masks (index row * F + col of the stacked
+    rows, sub-seed per layer) and the GPU's own ReLU decisions; fx_prof kind 7 proves which kernel ran."""
+    from factmx import native as nx
+    from factmx.dp import FlatGradReducer
+    from factmx.models.basic import MSTCN
+    monkeypatch.setattr(fxf, "MSTCN_FUSED_LAYERS", fused)
+    lib = nx.load()
+    p, nl, F = 0.2, 10, 256
+    off = [0, 4096, 6996]
+    rows = off[-1]
+    torch.manual_seed(0)
+    mod = MSTCN(64, F, 40, nl, dropout=p, ln=False, in_map=True).to(DEV).train()
+    if flat:
+        FlatGradReducer(mod.parameters())
+    x = _r(rows, 64, seed=31)
+    g = _r(rows, 40, seed=32)
+    xd = x.float().to(DEV).requires_grad_(True)
+    assert lib.fx_prof_enable(7, 64) == 0
+    try:
+        y = fxf.mstcn(mod, xd, T=0, nvid=2, seq_off=off)
+        n_fwd = _prof_count(lib, 7)
+        saved = y.grad_fn.saved_tensors[1].detach().double().cpu()
+        assert lib.fx_prof_enable(7, 64) == 0
+        (y * g.float().to(DEV)).sum().backward()
+        torch.cuda.synchronize()
+        n_bwd = _prof_count(lib, 7)
+    finally:
+        lib.fx_prof_disable()
+    assert n_fwd == (nl if fused else 0), n_fwd
+    assert n_bwd == (nl - 1 if fused and flat else 0), n_bwd
+    seed = fixed_seeds[-1]
+    n = -(-rows // 64) * 64 * F
+    gates = [(saved[(nl + 1 + i) * n:(nl + 1 + i) * n + rows * F].view(rows, F) > 0).double() for i in range(nl)]
+    masks = [_mask(drop_subseed(seed, i), (rows, F), p) / (1.0 - float(np.float32(p))) for i in range(nl)]
+    P = {k: t.detach().double().cpu().requires_grad_(True) for k, t in mod.named_parameters()}
+    xr = x.clone().requires_grad_(True)
+    h = fo.linear(xr, P["conv_1x1.weight"], P["conv_1x1.bias"])
+    for i in range(nl):
+        q = f"layers.{i}."
+        z = torch.cat([fo.dilated_conv3(h[off[v]:off[v + 1]], P[q + "conv_dilated.weight"],
+                                        P[q + "conv_dilated.bias"], 2 ** i) for v in range(2)], 0) * gates[i]
+        h = h + fo.linear(z, P[q + "conv_1x1.weight"], P[q + "conv_1x1.bias"]) * masks[i]
+    yr = fo.linear(h, P["conv_out.weight"], P["conv_out.bias"])
+    (yr * g).sum().backward()
+    _close(y, yr, rtol=2e-4, atol=2e-4, what="y")
+    _close(xd.grad, xr.grad, rtol=2e-4, atol=2e-4, what="dx")
+    for k, t in mod.named_parameters():
+        _close(t.grad, P[k].grad, rtol=2e-4, atol=2e-4, what=f"d{k}")

@@ -235,7 +235,9 @@ def test_mstcn_fused_layers_match_fp64(T, nvid, nl, fused, monkeypatch):
     layer kernel (mstcn_fused.hip) forward + fused dX chain backward: output, input gradient and every
     weight gradient vs the float64 MS-TCN restatement (odd row counts, dilations up to 2^(nl-1),
     several videos: no leakage across video edges).  A tuple T is a ragged batch (row offsets through
-    the conv GEMMs; per-video weight-gradient launches; the fused layer declines ragged videos)."""
+    the conv GEMMs and the fused layer's tap gather, up to 16 videos; the deferred weight gradients in
+    one launch per weight kind, the ragged frame lookup in the GEMM's B loader over K = rows rounded up
+    to the 64-deep stage)."""
     from factmx.dp import FlatGradReducer
     from factmx.models.basic import MSTCN
     monkeypatch.setattr(fxf, "MSTCN_FUSED_LAYERS", 2 if fused == "1" else 0)   # 2: the fused kernel at any size
@@ -260,8 +262,8 @@ def test_mstcn_fused_layers_match_fp64(T, nvid, nl, fused, monkeypatch):
     # a pre-activation within ~1e-6 of 0 may land on the other side in fp32 (either summation order
     # is valid), which would move single dZ entries -- whole conv-weight-gradient rows -- by O(1)
     # (the GRU kink of tests/helpers.GruKinks); with the same gates everything agrees at fp32 noise
-    n = rows * 256
-    gates = [(saved[(nl + 1 + i) * n:(nl + 2 + i) * n].view(rows, 256) > 0).double() for i in range(nl)]
+    n = -(-rows // 64) * 64 * 256         # per-layer slot: rows rounded up to the 64-deep GEMM stage
+    gates = [(saved[(nl + 1 + i) * n:(nl + 1 + i) * n + rows * 256].view(rows, 256) > 0).double() for i in range(nl)]
     P = {n_: t.detach().double().cpu().requires_grad_(True) for n_, t in mod.named_parameters()}
     xr = x.clone().requires_grad_(True)
     outs = []
