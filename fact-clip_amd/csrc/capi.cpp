@@ -498,6 +498,7 @@ const Knobs& knobs() {
     if (const char* p = env("FX_GEMM_NTSTORE")) k.gemm_nt_store = p[0] == '1';
     if (const char* p = env("FX_GEMM_LOG")) k.gemm_log = std::fopen(p, "a");
     if (const char* p = env("FX_GEMM_GROUP")) k.gemm_group = p[0] != '0';
+    if (const char* p = env("FX_GEMM_KTAIL")) k.gemm_ktail = p[0] != '0';
     if (const char* p = env("FX_SIDE_STREAM")) k.side_stream = p[0] != '0';
     if (const char* p = env("FX_SIDE_PRIORITY")) k.side_priority = std::string(p) == "low" ? -1 : std::string(p) == "high" ? 1 : 0;
     if (const char* p = env("FX_DEFER_SPLIT")) k.defer_split = std::max(1, std::min(16, std::atoi(p)));
@@ -1524,12 +1525,12 @@ struct X2YLayout {
 X2YLayout x2y_layout(int Nx, int xdim, int Ny, int ydim, int Hd) {
   X2YLayout L{};
   L.xin = 0;
-  L.yin = L.xin + (long long)Nx * xdim;
-  L.xk = L.yin + (long long)Ny * ydim;
-  L.xv = L.xk + (long long)Nx * Hd;
-  L.yq = L.xv + (long long)Nx * Hd;
-  L.feat = L.yq + (long long)Ny * Hd;
-  L.total = L.feat + (long long)Ny * Hd;
+  L.yin = L.xin + al64((long long)Nx * xdim);
+  L.xk = L.yin + al64((long long)Ny * ydim);
+  L.xv = L.xk + al64((long long)Nx * Hd);
+  L.yq = L.xv + al64((long long)Nx * Hd);
+  L.feat = L.yq + al64((long long)Ny * Hd);
+  L.total = L.feat + al64((long long)Ny * Hd);
   return L;
 }
 struct VidRows {
@@ -1597,15 +1598,17 @@ static long long x2y_side_ws(int Nx, int xdim, int Ny, int ydim, int Hd, int out
 }
 
 static long long x2y_ws_nocatd(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim, const VidRows& v) {
-  long long w = (long long)Ny * (ydim + Hd) + v.a[v.n] + 2LL * Nx * Hd + (long long)Ny * Hd +
-                (long long)Nx * xdim + (long long)Ny * ydim;
-  return w + x2y_split_ws(v, xdim, ydim, Hd, outdim) + colsum_workspace_floats(std::max(Nx, Ny), std::max(Hd, outdim));
+  // dcat, dL, dxv, dxk, dyq, dXk, dYq (fx_x2y_bwd), each region 64-float aligned
+  long long w = al64((long long)Ny * (ydim + Hd)) + al64(v.a[v.n]) + 2 * al64((long long)Nx * Hd) +
+                al64((long long)Ny * Hd) + al64((long long)Nx * xdim) + al64((long long)Ny * ydim);
+  return w + al64(x2y_split_ws(v, xdim, ydim, Hd, outdim)) +
+         al64(colsum_workspace_floats(std::max(Nx, Ny), std::max(Hd, outdim)));
 }
 
 long long fx_x2y_workspace_floats(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim, int nvid,
                                   const int* x_off, const int* y_off) {
   const VidRows v = vid_rows(Nx, Ny, nvid, x_off, y_off);
-  return x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, v) + (long long)Ny * (ydim + Hd) +
+  return x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, v) + al64((long long)Ny * (ydim + Hd)) +
          x2y_side_ws(Nx, xdim, Ny, ydim, Hd, outdim) + x2y_f2a_ws_floats(v.n, v.x.data(), Hd);
 }
 
@@ -1677,7 +1680,7 @@ int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpo
     prof_end(3, s, 4.0 * na * Hd, core_bytes);
   } else if (knobs().x2y_fused && x2y_f2a_fusable(V.n, V.x.data(), V.y.data(), Hd) && al16) {
     // the f2a map (frames -> tokens): per-chunk partials after every other region of the workspace
-    float* f2a_ws = workspace + x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, V) + (long long)Ny * (ydim + Hd) +
+    float* f2a_ws = workspace + x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, V) + al64((long long)Ny * (ydim + Hd)) +
                     x2y_side_ws(Nx, xdim, Ny, ydim, Hd, outdim);
     prof_begin(5, s);
     FX_TRY(launch_x2y_f2a_fwd(yq, xk, xv, Hd, scale, V.n, V.y.data(), V.x.data(), V.a.data(), logit, attn, feat,
@@ -1749,13 +1752,13 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
   const long long ldyin = has_ypos ? ydim : ldy;
   const int cw = ydim + Hd;
   float* dcat = workspace;
-  float* dL = dcat + (long long)Ny * cw;
-  float* dxv = dL + V.a[V.n];
-  float* dxk = dxv + (long long)Nx * Hd;
-  float* dyq = dxk + (long long)Nx * Hd;
-  float* dXk = dyq + (long long)Ny * Hd;
-  float* dYq = dXk + (long long)Nx * xdim;
-  float* spl = dYq + (long long)Ny * ydim;
+  float* dL = dcat + al64((long long)Ny * cw);
+  float* dxv = dL + al64(V.a[V.n]);
+  float* dxk = dxv + al64((long long)Nx * Hd);
+  float* dyq = dxk + al64((long long)Nx * Hd);
+  float* dXk = dyq + al64((long long)Ny * Hd);
+  float* dYq = dXk + al64((long long)Nx * xdim);
+  float* spl = dYq + al64((long long)Ny * ydim);
   WsBound wb(spl, x2y_split_ws(V, xdim, ydim, Hd, outdim));
   const float scale = 1.0f / std::sqrt((float)Hd);
   // Y_W: dcat = dout . Wy, dWy = dout^T [Y, feat], dby  (dropout: the dropped concatenation and
@@ -1812,7 +1815,7 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
     }
   } else if (f2a_fused) {
     // the f2a map: dP / dxv, then dlogit / dxk / dyq partials per 64-key chunk, then the ordered dyq merge
-    float* f2a_ws = workspace + x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, V) + (long long)Ny * cw +
+    float* f2a_ws = workspace + x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, V) + al64((long long)Ny * cw) +
                     x2y_side_ws(Nx, xdim, Ny, ydim, Hd, outdim);
     FX_TRY(launch_x2y_f2a_bwd(dcat + ydim, cw, xv, xk, yq, attn, dattn, dlogit, Hd, scale, V.n, V.y.data(), V.x.data(),
                               V.a.data(), dL, dxv, dxk, dyq, f2a_ws, s));
@@ -1867,7 +1870,7 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
   // frame-level GEMM split defer_split(rows) ways into its own slab region
   {
     hipStream_t sd = side_fork(s, 1);
-    float* sps = workspace + x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, V) + (long long)Ny * cw;
+    float* sps = workspace + x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, V) + al64((long long)Ny * cw);
     WsBound wbs(sps, x2y_side_ws(Nx, xdim, Ny, ydim, Hd, outdim));
     auto dw = [&](const float* dy, long long lddy, const float* x, long long ldx_, int rows, int K, int N, float* w,
                   float* b, long long ldw) -> int {

@@ -156,69 +156,69 @@ DecLayout dec_layout(const fx_decoder_params* p, int R, int T, int has_qpos, int
   const long long A = p->A, FF = p->FF, h = p->nhead, RA = (long long)R * A;
   const long long Qv = R / nvid, Tv = dec_tmax(p, T, nvid);   // tokens / frames (longest video) per video
   long long o = 0;
-  L.xq = o; o += has_qpos ? RA : 0;
-  L.qkv = o; o += 3 * RA;
-  L.psa = o; o += nvid * h * Qv * Qv;
-  L.osa = o; o += RA;
-  L.xh1 = o; o += RA;
-  L.rs1 = o; o += R;
-  L.t1 = o; o += RA;
+  L.xq = o; o += al64(has_qpos ? RA : 0);
+  L.qkv = o; o += al64(3 * RA);
+  L.psa = o; o += al64(nvid * h * Qv * Qv);
+  L.osa = o; o += al64(RA);
+  L.xh1 = o; o += al64(RA);
+  L.rs1 = o; o += al64(R);
+  L.t1 = o; o += al64(RA);
   if (p->cross) {
-    L.t1q = o; o += has_qpos ? RA : 0;
-    L.qc = o; o += RA;
-    L.pca = o; o += nvid * h * Qv;            // cross-attention log-sum-exp per (video, head, token)
-    L.oca = o; o += RA;
-    L.xh2 = o; o += RA;
-    L.rs2 = o; o += R;
-    L.t2 = o; o += RA;
+    L.t1q = o; o += al64(has_qpos ? RA : 0);
+    L.qc = o; o += al64(RA);
+    L.pca = o; o += al64(nvid * h * Qv);            // cross-attention log-sum-exp per (video, head, token)
+    L.oca = o; o += al64(RA);
+    L.xh2 = o; o += al64(RA);
+    L.rs2 = o; o += al64(R);
+    L.t2 = o; o += al64(RA);
   }
-  L.f1 = o; o += (long long)R * FF;
-  L.xh3 = o; o += RA;
-  L.rs3 = o; o += R;
-  L.t3 = o; o += RA;
+  L.f1 = o; o += al64((long long)R * FF);
+  L.xh3 = o; o += al64(RA);
+  L.rs3 = o; o += al64(R);
+  L.t3 = o; o += al64(RA);
   L.per_layer = o;
   L.layers = 0;
   o = L.layers + L.per_layer * p->num_layers;
-  L.fxh = o; o += p->final_norm ? RA : 0;
-  L.frs = o; o += p->final_norm ? R : 0;
-  L.fo = o; o += p->final_norm ? RA : 0;
+  L.fxh = o; o += al64(p->final_norm ? RA : 0);
+  L.frs = o; o += al64(p->final_norm ? R : 0);
+  L.fo = o; o += al64(p->final_norm ? RA : 0);
   const long long AL2 = 2 * A * p->num_layers;
-  L.kv = o; o += p->cross ? (long long)T * AL2 : 0;
-  L.mpos = o; o += (p->cross && has_mpos) ? (long long)T * p->Hm : 0;
+  L.kv = o; o += al64(p->cross ? (long long)T * AL2 : 0);
+  L.mpos = o; o += al64((p->cross && has_mpos) ? (long long)T * p->Hm : 0);
   L.total_saved = o;
   const long long sp = dec_split_ws(p, R, T);
   // forward workspace
   o = 0;
-  L.wkv = o; o += p->cross ? AL2 * p->Hm : 0;
-  L.bkv = o; o += p->cross ? AL2 : 0;
+  L.wkv = o; o += al64(p->cross ? AL2 * p->Hm : 0);
+  L.bkv = o; o += al64(p->cross ? AL2 : 0);
   const long long att = dec_attn_ws(p, nvid, (int)Qv, (int)Tv);
-  L.wsp = o; o += std::max(sp, att) + RA;
+  L.wsp = o; o += al64(std::max(sp, att) + RA);
   L.total_ws_fwd = o;
   // backward workspace
   o = 0;
-  L.dkv = o; o += p->cross ? (long long)T * AL2 : 0;
-  L.dwkv = o; o += p->cross ? AL2 * p->Hm : 0;
-  L.dbkv = o; o += p->cross ? AL2 : 0;
-  L.dT = o; o += RA;
-  L.dS = o; o += RA;
-  L.dU = o; o += RA;
-  L.dF = o; o += (long long)R * FF;
-  L.dQKV = o; o += 3 * RA;
-  L.dO = o; o += RA;
-  L.dq = o; o += RA;
-  L.lnws = o; o += layernorm_bwd_ws_floats(R, (int)A);
-  L.core = o; o += att;
-  L.dmask = o; o += (p->dropout > 0.f) ? RA : 0;   // masked branch gradient (training dropout)
-  L.split = o; o += sp;
+  L.dkv = o; o += al64(p->cross ? (long long)T * AL2 : 0);
+  L.dwkv = o; o += al64(p->cross ? AL2 * p->Hm : 0);
+  L.dbkv = o; o += al64(p->cross ? AL2 : 0);
+  L.dT = o; o += al64(RA);
+  L.dS = o; o += al64(RA);
+  L.dU = o; o += al64(RA);
+  L.dF = o; o += al64((long long)R * FF);
+  L.dQKV = o; o += al64(3 * RA);
+  L.dO = o; o += al64(RA);
+  L.dq = o; o += al64(RA);
+  L.lnws = o; o += al64(layernorm_bwd_ws_floats(R, (int)A));
+  L.core = o; o += al64(att);
+  L.dmask = o; o += al64((p->dropout > 0.f) ? RA : 0);   // masked branch gradient (training dropout)
+  L.split = o; o += al64(sp);
   // every layer's output gradients of its token linears, kept for the weight-gradient GEMMs that run
   // after the chain (side stream): dU of the three LayerNorms, dF, dq, dQKV
-  L.gdu = o; o += 3LL * p->num_layers * RA;
-  L.gdf = o; o += (long long)p->num_layers * R * FF;
-  L.gdq = o; o += (long long)p->num_layers * RA;
-  L.gdqkv = o; o += 3LL * p->num_layers * RA;
+  L.gdu = o; o += al64(3LL * p->num_layers * RA);
+  L.gdf = o; o += al64((long long)p->num_layers * R * FF);
+  L.gdq = o; o += al64((long long)p->num_layers * RA);
+  L.gdqkv = o; o += al64(3LL * p->num_layers * RA);
   // every layer's three LayerNorm input gradients, kept for the batched LN weight / bias gradients
   // that follow the chain on the side stream (the chain's LN backward computes dx only)
-  L.gdy = o; o += 3LL * p->num_layers * RA;
+  L.gdy = o; o += al64(3LL * p->num_layers * RA);
   L.total_ws_bwd = o;
   (void)FF;
   return L;

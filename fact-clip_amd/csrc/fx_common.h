@@ -37,6 +37,10 @@ void set_error(const std::string& msg);
   } while (0)
 
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+// workspace / saved-buffer region sizes rounded up to 64 floats: every region then starts 256-B aligned
+// (the GEMM's FAST loaders need 16-B aligned operands; a region after R = 75 token rows of a scalar
+// per row would otherwise leave everything behind it misaligned)
+inline long long al64(long long n) { return (n + 63) & ~63LL; }
 
 // ------------------------------------------------------------------------
 // GEMM (internal C++ view of fx_gemm_desc; see include/factmx.h)
@@ -143,6 +147,7 @@ struct Knobs {
                               // 1 contiguous runs, 2 runs that follow the conv taps (A/B)
   FILE* gemm_log = nullptr; // FX_GEMM_LOG=<file>: one line per GEMM launch (shape census)
   bool gemm_group = true;
+  bool gemm_ktail = true;    // FX_GEMM_KTAIL=0: column-major operands with a K tail take the generic kernel (A/B)
   bool side_stream = true;
   int side_priority = 0;    // -1 low, 0 normal, 1 high
   int defer_split = 16;     // FX_DEFER_SPLIT: split-K of the deferred (side-stream) weight-gradient GEMMs (16 vs 8: 15.78 vs 15.95 ms median of 6 pairs)

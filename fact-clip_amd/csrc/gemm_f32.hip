@@ -11,6 +11,8 @@
 //   COLS_CONV conv input for dW, tap from r; optional all-ones row (bias grad)
 //   COLS_CONVR the same over ragged videos (host row offsets): weight gradients of a ragged batch in
 //             one launch, K padded to whole stages (rows past the last video read as zero)
+//   COLS_KT   COLS with K not a whole number of 64-deep stages (frame-level weight gradients over a
+//             ragged frame count): rows past K read as zero from a clamped address, both operands
 //
 // Tiled kernel: 64x64 output tile per 256-thread workgroup, one wave per SIMD, each wave a
 // 32x32 sub-tile over the block's whole K range (32 MFMAs = 2048 matrix-core cycles per
@@ -50,7 +52,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 //           either gather optional -- the FAST form of the concatenation / gather operands
 constexpr int kMaxSeq = 16;        // ragged videos per conv operand
 
-enum Kind { ROWS = 0, ROWS_CONV = 1, ROWS_GEN = 2, COLS = 3, COLS_CONV = 4, ROWS_CAT = 5, COLS_CONVR = 6 };
+enum Kind { ROWS = 0, ROWS_CONV = 1, ROWS_GEN = 2, COLS = 3, COLS_CONV = 4, ROWS_CAT = 5, COLS_CONVR = 6, COLS_KT = 7 };
 
 struct GemmDev {
   int M, N, K;
@@ -330,6 +332,15 @@ struct Loader {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) v[j] = ldg4(pcol + (long long)(k0 + RSTEP * j) * o.ld);
       vm = 0xFu;
+    } else if (KIND == COLS_KT) {
+      vm = 0;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int k = k0 + ta + RSTEP * j;
+        const bool ok = k < K;
+        vm |= (ok ? 1u : 0u) << j;
+        v[j] = ldg4(pcol + (long long)((ok ? k : K - 1) - ta) * o.ld);
+      }
     } else if (KIND == COLS_CONV) {
       vm = 0;
 #pragma unroll
@@ -387,10 +398,11 @@ struct Loader {
       for (int j = 0; j < NJ; ++j) {
         float e[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
         if (FAST) {
-          const bool tok = (KIND != COLS_CONV && KIND != COLS_CONVR) || ((vm >> j) & 1u);
+          const bool tok = (KIND != COLS_CONV && KIND != COLS_CONVR && KIND != COLS_KT) || ((vm >> j) & 1u);
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const float one = ((omask >> q) & 1u) ? 1.f : 0.f;
+            // (COLS_KT: rows past K are zero, the ones row included)
+            const float one = (((omask >> q) & 1u) && (KIND != COLS_KT || tok)) ? 1.f : 0.f;
             e[q] = (tok && ((emask >> q) & 1u)) ? e[q] : one;
           }
         }
@@ -1736,6 +1748,12 @@ int launch_wide_b(int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
         return FX_OK;
       }
       break;
+    case COLS_KT:
+      if constexpr (AK == COLS_KT) {
+        hipLaunchKernelGGL((gemm_f32_wide_kernel<AK, COLS_KT>), grid, dim3(NTHREADS), 0, s, g);
+        return FX_OK;
+      }
+      break;
     default: break;
   }
   set_error("gemm(wide): unsupported B operand kind");
@@ -1756,6 +1774,12 @@ int launch_wide8_b(int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
         return FX_OK;
       }
       break;
+    case COLS_KT:
+      if constexpr (AK == COLS_KT) {
+        hipLaunchKernelGGL((gemm_f32_wide8_kernel<AK, COLS_KT>), grid, dim3(W8T), 0, s, g);
+        return FX_OK;
+      }
+      break;
     default: break;
   }
   set_error("gemm(wide8): unsupported B operand kind");
@@ -1768,6 +1792,7 @@ int launch_wide8(int ak, int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
     case ROWS_CONV: return launch_wide8_b<ROWS_CONV>(bk, grid, s, g);
     case ROWS_CAT: return launch_wide8_b<ROWS_CAT>(bk, grid, s, g);
     case COLS: return launch_wide8_b<COLS>(bk, grid, s, g);
+    case COLS_KT: return launch_wide8_b<COLS_KT>(bk, grid, s, g);
     default: break;
   }
   set_error("gemm(wide8): unsupported A operand kind");
@@ -1780,6 +1805,7 @@ int launch_wide(int ak, int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
     case ROWS_CONV: return launch_wide_b<ROWS_CONV>(bk, grid, s, g);
     case ROWS_CAT: return launch_wide_b<ROWS_CAT>(bk, grid, s, g);
     case COLS: return launch_wide_b<COLS>(bk, grid, s, g);
+    case COLS_KT: return launch_wide_b<COLS_KT>(bk, grid, s, g);
     default: break;
   }
   set_error("gemm(wide): unsupported A operand kind");
@@ -1799,6 +1825,13 @@ int launch_b(int bk, dim3 grid, hipStream_t s, const GemmDev& g, bool fast) {
         return FX_OK;
       }
       break;
+    case COLS_KT:   // FAST only (plan_gemm picks it for vectorisable operands)
+      if constexpr (AK == COLS_KT) {
+        if (!fast) break;
+        hipLaunchKernelGGL((gemm_f32_kernel<AK, COLS_KT, true>), grid, dim3(NTHREADS), 0, s, g);
+        return FX_OK;
+      }
+      break;
     case ROWS_GEN:
     case ROWS_CAT: launch_t<AK, ROWS_GEN>(grid, s, g, false); return FX_OK;
     default: break;
@@ -1809,13 +1842,14 @@ int launch_b(int bk, dim3 grid, hipStream_t s, const GemmDev& g, bool fast) {
 
 // FAST loop: both operands 16-B vector-loadable, K a multiple of the 64-deep stage, no gathers
 int launch_tiled(int ak, int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
-  const bool fast = g.a_vec && g.b_vec && (g.K % BK) == 0 && ak != ROWS_GEN && bk != ROWS_GEN;
+  const bool fast = g.a_vec && g.b_vec && ((g.K % BK) == 0 || ak == COLS_KT) && ak != ROWS_GEN && bk != ROWS_GEN;
   switch (ak) {
     case ROWS: return launch_b<ROWS>(bk, grid, s, g, fast);
     case ROWS_CONV: return launch_b<ROWS_CONV>(bk, grid, s, g, fast);
     case ROWS_GEN: return launch_b<ROWS_GEN>(bk, grid, s, g, false);
     case ROWS_CAT: return launch_b<ROWS_CAT>(bk, grid, s, g, fast);
     case COLS: return launch_b<COLS>(bk, grid, s, g, fast);
+    case COLS_KT: return launch_b<COLS_KT>(bk, grid, s, g, fast);
     default: break;
   }
   set_error("gemm: unsupported A operand kind");
@@ -1879,9 +1913,9 @@ bool wide8() {
 
 bool use_wide(const GemmDev& g, int ak, int bk, int batch) {
   const int force = knobs().gemm_wide;
-  const bool fast = g.a_vec && g.b_vec && (g.K % BK) == 0;
-  const bool ok = fast && (ak == ROWS || ak == ROWS_CONV || ak == ROWS_CAT || ak == COLS) &&
-                  (bk == ROWS || bk == COLS || bk == COLS_CONV || bk == COLS_CONVR);
+  const bool fast = g.a_vec && g.b_vec && ((g.K % BK) == 0 || ak == COLS_KT);
+  const bool ok = fast && (ak == ROWS || ak == ROWS_CONV || ak == ROWS_CAT || ak == COLS || ak == COLS_KT) &&
+                  (bk == ROWS || bk == COLS || bk == COLS_CONV || bk == COLS_CONVR || bk == COLS_KT);
   if (!ok || force == 0) return false;
   if (force == 1) return true;
   return (long long)cdiv(g.M, WBM) * g.tiles_x * batch * g.split >= 192;
@@ -2056,10 +2090,13 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
   g.b_vec = operand_vec_ok(d.b);
   g.ws = d.workspace;
   g.w8_stagger = knobs().gemm_stagger;
-  const int ak = kind_of(d.a, g.a_vec), bk = kind_of(d.b, g.b_vec);
+  int ak = kind_of(d.a, g.a_vec), bk = kind_of(d.b, g.b_vec);
+  const bool direct = d.b_dil_growth <= 1 && d.a_dil_b1 <= 0 && use_direct(d, ak, bk);   // (the direct kernel: one dilation)
+  // weight gradients over a frame count that is not a whole number of 64-deep stages (ragged batches):
+  // the K-tail loaders keep them on the FAST tiled / wide kernels instead of the element-wise generic one
+  if (!direct && ak == COLS && bk == COLS && g.a_vec && g.b_vec && d.K % BK != 0 && knobs().gemm_ktail) ak = bk = COLS_KT;
   P.ak = ak;
   P.bk = bk;
-  const bool direct = d.b_dil_growth <= 1 && d.a_dil_b1 <= 0 && use_direct(d, ak, bk);   // (the direct kernel: one dilation)
   bool wide = false;
   const int cap = (d.split_k > 1 && d.workspace) ? d.split_k : 1;   // workspace holds `cap` slabs
   FX_REQUIRE(!(d.split_k > 1 && !d.workspace), "gemm: split-K needs a workspace");

@@ -40,6 +40,9 @@ CASES = [
     (600, 520, 300, 1, False, False, 1),    # tiled
     (600, 520, 3000, 1, True, False, 6),    # tiled split-K, fused reduction
     (1000, 700, 77, 2, False, True, 1),     # tiled, batched, ragged
+    (600, 520, 3001, 1, True, True, 6),     # weight gradient, K tail (COLS_KT: rows past K read as zero)
+    (512, 513, 6996, 1, True, True, 13),    # the shipped yaml's ragged 4096 + 2900 rows (K tail, wide tile)
+    (640, 256, 1000, 2, True, True, 1),     # K tail, batched
 ]
 
 
@@ -72,7 +75,7 @@ def test_gemm(M, N, K, batch, at, bt, split, epi):
     assert err <= 1e-5 * (1 + ref.abs().max().item()) + 1e-6 * K ** 0.5, err
 
 
-@pytest.mark.parametrize("M,K,split", [(256, 32, 1), (256, 4096, 13), (512, 4096, 5)])
+@pytest.mark.parametrize("M,K,split", [(256, 32, 1), (256, 4096, 13), (512, 4096, 5), (512, 6996, 13), (256, 2900, 1)])
 def test_gemm_fused_bias_column(M, K, split):
     """dW|db in one GEMM: the B operand's last column is a virtual ones column (c_last gets row sums)."""
     N1 = 200

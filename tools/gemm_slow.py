@@ -4,7 +4,7 @@ calls and why (A / B not 16-B vectorisable, K not a whole number of 64-deep stag
 import collections
 import sys
 
-KIND = ["rows", "rconv", "rgen", "cols", "cconv", "rcat", "cconvr"]
+KIND = ["rows", "rconv", "rgen", "cols", "cconv", "rcat", "cconvr", "ckt"]
 agg = collections.Counter()
 for ln in open(sys.argv[1]):
     f = [int(v) for v in ln.split()]
@@ -12,7 +12,7 @@ for ln in open(sys.argv[1]):
         continue
     M, N, K, b, ak, bk, sp, ca, cb, relu, path, mem, vec, kok = f
     direct = path > 0
-    slow = not direct and not ((vec == 3) and kok and ak != 2 and bk != 2)
+    slow = not direct and not ((vec == 3) and (kok or ak == 7) and ak != 2 and bk != 2)
     if slow:
         why = ("A" if not vec & 1 else "") + ("B" if not vec & 2 else "") + ("K" if not kok else "") + \
               ("G" if 2 in (ak, bk) else "")
