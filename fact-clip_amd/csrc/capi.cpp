@@ -30,7 +30,8 @@ struct ProfState {
   std::vector<int> launches;   // launches an event pair brackets (back-to-back chains: one pair)
   int used = 0;
 };
-constexpr int kProfKinds = 8;   // 0 conv GEMM, 1 / 2 attention over T fwd / bwd, 3-6 X2Y cores, 7 fused MS-TCN layer
+constexpr int kProfKinds = 9;   // 0 conv GEMM, 1 / 2 attention over T fwd / bwd, 3-6 X2Y cores, 7 fused MS-TCN layer,
+                                // 8 persistent token-kernel launches (tokdec.hip)
 std::mutex g_prof_mu;
 ProfState g_prof[kProfKinds];
 
@@ -499,6 +500,8 @@ const Knobs& knobs() {
     if (const char* p = env("FX_GEMM_LOG")) k.gemm_log = std::fopen(p, "a");
     if (const char* p = env("FX_GEMM_GROUP")) k.gemm_group = p[0] != '0';
     if (const char* p = env("FX_GEMM_KTAIL")) k.gemm_ktail = p[0] != '0';
+    if (const char* p = env("FX_DEC_TOK")) k.dec_tok = p[0] != '0';
+    if (const char* p = env("FX_TOK_SPIN")) k.tok_spin = std::max(0, std::atoi(p));
     if (const char* p = env("FX_SIDE_STREAM")) k.side_stream = p[0] != '0';
     if (const char* p = env("FX_SIDE_PRIORITY")) k.side_priority = std::string(p) == "low" ? -1 : std::string(p) == "high" ? 1 : 0;
     if (const char* p = env("FX_DEFER_SPLIT")) k.defer_split = std::max(1, std::min(16, std::atoi(p)));

@@ -19,6 +19,7 @@
 
 #include "fx_common.h"
 #include "ops.h"
+#include "tokdec.h"
 
 namespace fx {
 namespace {
@@ -263,12 +264,397 @@ int linear_fwd_res_drop(const float* x, long long ldx, int M, int K, const float
   return launch_gemm(d, s);
 }
 
+
+// ---------------------------------------------------------------- persistent token kernel (tokdec.hip)
+// The token rows of the whole decoder as a few launches of tok_kernel: one program per stretch between
+// two attention-over-T launches (forward: [ca-out, FFN1, FFN2] of layer l - 1 + [self-attention,
+// sa-out, q-proj] of layer l; backward the same stretch reversed), every phase writing exactly the
+// saved / workspace slots the separate-launch path writes, so the deferred weight-gradient GEMMs, the
+// LayerNorm parameter gradients and the query-position gradient read the same buffers either way.
+// Shapes it covers: <= 32 tokens per video, head dim 32, A <= 256, FF and out_dim <= 768 (the
+// benchmark's SCADecoder / SADecoders); other decoders keep the separate launches.
+bool dec_tok_ok(const fx_decoder_params* p, int R, int nvid, const void* const* ptrs, int nptr,
+                const long long* lds, int nld) {
+  if (!knobs().dec_tok) return false;
+  const int Qv = R / nvid, A = p->A;
+  bool ok = Qv >= 1 && Qv <= 32 && p->nhead * 32 == A && A <= TOK_MAXSA && p->FF % 32 == 0 && p->FF >= A &&
+            p->FF <= TOK_MAXK && 3 * A <= TOK_MAXK && p->out_dim >= 4 && p->out_dim % 4 == 0 && p->out_dim <= TOK_MAXK;
+  for (int i = 0; i < nptr && ok; ++i) ok = ptrs[i] == nullptr || ((uintptr_t)ptrs[i] & 15) == 0;
+  // weights and LayerNorm parameters are read as float4 (a flat parameter buffer may misalign them)
+  auto al = [](const void* q) { return q == nullptr || ((uintptr_t)q & 15) == 0; };
+  for (int l = 0; l < p->num_layers && ok; ++l) {
+    ok = al(p->sa_in_w[l]) && al(p->sa_out_w[l]) && al(p->ff1_w[l]) && al(p->ff2_w[l]) && al(p->ln_sa_w[l]) &&
+         al(p->ln_sa_b[l]) && al(p->ln_ff_w[l]) && al(p->ln_ff_b[l]);
+    if (ok && p->cross)
+      ok = al(p->ca_q_w[l]) && al(p->ca_out_w[l]) && al(p->ln_ca_w[l]) && al(p->ln_ca_b[l]);
+  }
+  ok = ok && al(p->out_w) && (!p->final_norm || (al(p->fn_w) && al(p->fn_b)));
+  for (int i = 0; i < nld && ok; ++i) ok = lds[i] % 4 == 0;
+  return ok;
+}
+
+struct TokBuild {
+  TokProgram prog{};
+  hipStream_t s;
+  int* status;
+  explicit TokBuild(hipStream_t st, int* stat) : s(st), status(stat) {}
+  static int items(const TokPhase& P) {
+    if (P.op == TOK_SAFWD || P.op == TOK_MHABWD) return P.nvid * P.nh;
+    if (P.op == TOK_LNROWS) return (P.M + 31) / 32;
+    return ((P.M + 31) / 32) * ((P.N + 31) / 32);
+  }
+  int flush() {
+    if (prog.nphase == 0) return FX_OK;
+    int G = 1;
+    for (int i = 0; i < prog.nphase; ++i) G = std::max(G, items(prog.ph[i]));
+    prog.G = std::min(G, 256);
+    prog.status = reinterpret_cast<unsigned*>(status);
+    prog.spin_max = knobs().tok_spin > 0 ? (unsigned)knobs().tok_spin : (1u << 20);
+    FX_REQUIRE(status, "decoder: the persistent token kernel needs the caller's status word (fx_decoder_params.status)");
+    prof_begin(8, s);
+    FX_TRY(launch_tok(prog, s));
+    prof_end(8, s, 0.0, 0.0, 1);
+    prog = TokProgram{};
+    return FX_OK;
+  }
+  // a new phase (the program launches when full)
+  TokPhase* add(int op, int amode, int M, int N, int K) {
+    if (prog.nphase == TOK_MAXPH && flush() != FX_OK) return nullptr;
+    TokPhase& P = prog.ph[prog.nphase++];
+    P = TokPhase{};
+    P.op = op;
+    P.amode = amode;
+    P.M = M;
+    P.N = N;
+    P.K = K;
+    P.Kp = (K + 31) / 32 * 32;
+    P.alpha = 1.f;
+    return &P;
+  }
+};
+
+void tok_drop(unsigned& thr, float& scale, unsigned long long& seed, float p, unsigned long long sd) {
+  thr = p > 0.f ? std::max(fx_drop_thresh(p), 1u) : 0u;
+  scale = 1.f / (1.f - p);
+  seed = sd;
+}
+
+// y = x W^T (+ b) (+ relu) (+ dropout) (+ resid) into c
+TokPhase* tok_gemm(TokBuild& tb, int amode, int M, int N, int K, const float* a, long long lda, const float* w,
+                   long long ldw, int btrans, const float* bias, float* c, long long ldc) {
+  TokPhase* P = tb.add(TOK_GEMM, amode, M, N, K);
+  if (!P) return nullptr;
+  P->a = a;
+  P->lda = lda;
+  P->w = w;
+  P->ldw = ldw;
+  P->btrans = btrans;
+  P->bias = bias;
+  P->c = c;
+  P->ldc = ldc;
+  return P;
+}
+
+int dec_fwd_tok(const fx_decoder_params* p, const float* tgt, long long ldt, int R, const float* qpos, int nvid,
+                int Qv, int Tv, const float* kv, float* out, long long ldo, float* saved, const DecLayout& L,
+                float* u, float* spl, hipStream_t s) {
+  const int A = p->A, FF = p->FF, h = p->nhead, hd = A / h, NL = p->num_layers, AL2 = 2 * A * NL;
+  const float eps = p->eps > 0.f ? p->eps : 1e-5f;
+  const float pd = p->dropout, pa = p->attn_dropout;
+  const float scale = 1.0f / std::sqrt((float)hd);
+  TokBuild tb(s, p->status);
+  auto blk = [&](int l) { return saved + L.layers + (long long)l * L.per_layer; };
+  auto lnp = [&](TokPhase* P, const float* w, const float* b) {
+    P->ln.w = w;
+    P->ln.b = b;
+    P->ln.eps = eps;
+  };
+  // self-attention of layer l from x (layer 0: tgt) or LN3(u) of layer l - 1, then sa-out -> u, then the
+  // next operand: cross decoders q-proj (LN1(u) + qpos), else FFN of the SALayer (below)
+  auto self_attn = [&](int l) -> int {
+    float* b = blk(l);
+    TokPhase* P = tb.add(TOK_SAFWD, l == 0 ? TOK_A_PLAIN : TOK_A_LN, R, 3 * A, A);
+    FX_REQUIRE(P, "decoder: token program");
+    if (l == 0) {
+      P->a = tgt;
+      P->lda = ldt;
+      if (qpos) {   // the saved q / k input x + qpos of layer 0 (basic.py:438)
+        P->ln.pos = qpos;
+        P->ln.y2 = b + L.xq;
+      }
+    } else {
+      float* pb = blk(l - 1);
+      P->a = u;
+      P->lda = A;
+      lnp(P, p->ln_ff_w[l - 1], p->ln_ff_b[l - 1]);
+      P->ln.y = pb + L.t3;
+      P->ln.xh = pb + L.xh3;
+      P->ln.rs = pb + L.rs3;
+      if (qpos) {
+        P->ln.pos = qpos;
+        P->ln.y2 = b + L.xq;
+      }
+    }
+    P->apos = qpos;
+    P->ldpos = A;
+    P->w = p->sa_in_w[l];
+    P->ldw = A;
+    P->bias = p->sa_in_b[l];
+    P->c = b + L.osa;
+    P->ldc = A;
+    P->nvid = nvid;
+    P->Qv = Qv;
+    P->nh = h;
+    P->scale = scale;
+    P->qkv = b + L.qkv;
+    P->probs = b + L.psa;
+    tok_drop(P->attn_thr, P->attn_scale, P->attn_seed, pa, dec_seed(p, l, 0));
+    // t1 (pre-LN) = x + dropout1(out_proj(o))
+    const float* x = l == 0 ? tgt : blk(l - 1) + L.t3;
+    const long long ldx = l == 0 ? ldt : A;
+    P = tok_gemm(tb, TOK_A_PLAIN, R, A, A, b + L.osa, A, p->sa_out_w[l], A, 0, p->sa_out_b[l], u, A);
+    FX_REQUIRE(P, "decoder: token program");
+    P->resid = x;
+    P->ldr = ldx;
+    tok_drop(P->drop_thr, P->drop_scale, P->drop_seed, pd, dec_seed(p, l, 1));
+    return FX_OK;
+  };
+  // FFN of layer l on LN(u) (LN2 for cross decoders, LN1 for SALayers): f1 = relu(W1 t + b1) -> u = t + W2 f1 + b2
+  auto ffn = [&](int l) -> int {
+    float* b = blk(l);
+    const bool cr = p->cross != 0;
+    TokPhase* P = tok_gemm(tb, TOK_A_LN, R, FF, A, u, A, p->ff1_w[l], A, 0, p->ff1_b[l], b + L.f1, FF);
+    FX_REQUIRE(P, "decoder: token program");
+    lnp(P, cr ? p->ln_ca_w[l] : p->ln_sa_w[l], cr ? p->ln_ca_b[l] : p->ln_sa_b[l]);
+    P->ln.y = b + (cr ? L.t2 : L.t1);
+    P->ln.xh = b + (cr ? L.xh2 : L.xh1);
+    P->ln.rs = b + (cr ? L.rs2 : L.rs1);
+    P->relu = pd > 0.f ? 2 : 1;
+    tok_drop(P->drop_thr, P->drop_scale, P->drop_seed, pd, dec_seed(p, l, 4));
+    P = tok_gemm(tb, TOK_A_PLAIN, R, A, FF, b + L.f1, FF, p->ff2_w[l], FF, 0, p->ff2_b[l], u, A);
+    FX_REQUIRE(P, "decoder: token program");
+    P->resid = b + (cr ? L.t2 : L.t1);
+    P->ldr = A;
+    tok_drop(P->drop_thr, P->drop_scale, P->drop_seed, pd, dec_seed(p, l, 5));
+    return FX_OK;
+  };
+  for (int l = 0; l < NL; ++l) {
+    float* b = blk(l);
+    if (p->cross) {
+      if (l > 0) {   // layer l - 1 after its attention over T: ca-out (+ t1) -> u, FFN
+        float* pb = blk(l - 1);
+        TokPhase* P = tok_gemm(tb, TOK_A_PLAIN, R, A, A, pb + L.oca, A, p->ca_out_w[l - 1], A, 0, p->ca_out_b[l - 1], u, A);
+        FX_REQUIRE(P, "decoder: token program");
+        P->resid = pb + L.t1;
+        P->ldr = A;
+        tok_drop(P->drop_thr, P->drop_scale, P->drop_seed, pd, dec_seed(p, l - 1, 3));
+        FX_TRY(ffn(l - 1));
+      }
+      FX_TRY(self_attn(l));
+      // q = (LN1(u) + qpos) W_q^T + b_q, with t1 / x-hat / rstd / t1 + qpos written
+      TokPhase* P = tok_gemm(tb, TOK_A_LN, R, A, A, u, A, p->ca_q_w[l], A, 0, p->ca_in_b[l], b + L.qc, A);
+      FX_REQUIRE(P, "decoder: token program");
+      lnp(P, p->ln_sa_w[l], p->ln_sa_b[l]);
+      P->ln.y = b + L.t1;
+      P->ln.xh = b + L.xh1;
+      P->ln.rs = b + L.rs1;
+      if (qpos) {
+        P->ln.pos = qpos;
+        P->ln.y2 = b + L.t1q;
+        P->apos = qpos;
+        P->ldpos = A;
+        P->apos_ncols = A;
+      }
+      FX_TRY(tb.flush());
+      TAttnOpts o;
+      o.koff = p->mem_off;
+      o.drop_p = pa;
+      o.drop_seed = dec_seed(p, l, 2);
+      FX_TRY(launch_tattn_fwd(b + L.qc, A, kv + (long long)l * A, AL2, kv + (long long)(NL + l) * A, AL2, nvid, Qv, Tv,
+                              hd, h, scale, b + L.oca, A, b + L.pca, spl, s, &o));
+    } else {
+      FX_TRY(self_attn(l));
+      FX_TRY(ffn(l));
+    }
+  }
+  float* lb = blk(NL - 1);
+  if (p->cross) {
+    TokPhase* P = tok_gemm(tb, TOK_A_PLAIN, R, A, A, lb + L.oca, A, p->ca_out_w[NL - 1], A, 0, p->ca_out_b[NL - 1], u, A);
+    FX_REQUIRE(P, "decoder: token program");
+    P->resid = lb + L.t1;
+    P->ldr = A;
+    tok_drop(P->drop_thr, P->drop_scale, P->drop_seed, pd, dec_seed(p, NL - 1, 3));
+    FX_TRY(ffn(NL - 1));
+  }
+  // last LayerNorm (t3), the final norm, the output linear
+  TokPhase* P = tb.add(TOK_LNROWS, TOK_A_LN, R, A, A);
+  FX_REQUIRE(P, "decoder: token program");
+  P->a = u;
+  P->lda = A;
+  lnp(P, p->ln_ff_w[NL - 1], p->ln_ff_b[NL - 1]);
+  P->ln.y = lb + L.t3;
+  P->ln.xh = lb + L.xh3;
+  P->ln.rs = lb + L.rs3;
+  const float* fin = lb + L.t3;
+  if (p->final_norm) {
+    P = tb.add(TOK_LNROWS, TOK_A_LN, R, A, A);
+    FX_REQUIRE(P, "decoder: token program");
+    P->a = lb + L.t3;
+    P->lda = A;
+    lnp(P, p->fn_w, p->fn_b);
+    P->ln.y = saved + L.fo;
+    P->ln.xh = saved + L.fxh;
+    P->ln.rs = saved + L.frs;
+    fin = saved + L.fo;
+  }
+  P = tok_gemm(tb, TOK_A_PLAIN, R, p->out_dim, A, fin, A, p->out_w, A, 0, p->out_b, out, ldo);
+  FX_REQUIRE(P, "decoder: token program");
+  return tb.flush();
+}
+
+// The backward chain (fx_decoder_bwd's separate-launch loop, same slots): per layer, the LN3 backward staged
+// into the FFN2 dX product, FFN1 dX + residual, the LN2 backward staged into the ca-out dX product,
+// (attention over T), dq W_q + residual, the LN1 backward staged into the sa-out dX product, the self-
+// attention backward per (video, head), [dq | dk | dv] W_in + residual.
+int dec_bwd_tok(const fx_decoder_params* p, int R, int nvid, int Qv, int Tv, const float* dout, long long lddo,
+                float* dtgt, long long lddt, const float* saved, float* ws, const DecLayout& L, float* dkv,
+                hipStream_t s) {
+  const int A = p->A, FF = p->FF, h = p->nhead, hd = A / h, NL = p->num_layers, AL2 = 2 * A * NL;
+  const long long RA = (long long)R * A;
+  const float pd = p->dropout, pa = p->attn_dropout;
+  const float scale = 1.0f / std::sqrt((float)hd);
+  TokBuild tb(s, p->status);
+  auto blk = [&](int l) { return saved + L.layers + (long long)l * L.per_layer; };
+  auto dy_slot = [&](int k, int l) { return ws + L.gdy + ((long long)k * NL + l) * RA; };
+  auto slot_u = [&](int k, int l) { return ws + L.gdu + ((long long)k * NL + l) * RA; };
+  float* dO = ws + L.dO;
+  float* dmask = ws + L.dmask;
+  const float* xl = blk(NL - 1) + L.t3;
+  (void)xl;
+  // LN backward staged into a product: dR (un-masked, residual path) and dU (masked branch) written
+  auto lnb = [&](TokPhase* P, const float* w, const float* xh, const float* rs, int k, int l, int site) {
+    P->ln.w = w;
+    P->ln.xhat = xh;
+    P->ln.rstd = rs;
+    P->ln.du = slot_u(k, l);
+    P->ln.dr = pd > 0.f ? dmask : nullptr;
+    tok_drop(P->ln.drop_thr, P->ln.drop_scale, P->ln.drop_seed, pd, dec_seed(p, l, site));
+  };
+  auto dres = [&](int k, int l) -> const float* { return pd > 0.f ? dmask : slot_u(k, l); };
+  // top: dfin = dout W_out (+ the final norm's backward) -> dT of the last layer
+  {
+    float* dT = dy_slot(0, NL - 1);
+    TokPhase* P = tok_gemm(tb, TOK_A_PLAIN, R, A, p->out_dim, dout, lddo, p->out_w, A, 1, nullptr,
+                           p->final_norm ? ws + L.dS : dT, A);
+    FX_REQUIRE(P, "decoder: token program");
+    if (p->final_norm) {
+      P = tb.add(TOK_LNROWS, TOK_A_LNBWD, R, A, A);
+      FX_REQUIRE(P, "decoder: token program");
+      P->a = ws + L.dS;
+      P->lda = A;
+      P->ln.w = p->fn_w;
+      P->ln.xhat = saved + L.fxh;
+      P->ln.rstd = saved + L.frs;
+      P->ln.dr = dT;
+    }
+  }
+  // FFN (+ its LN) of layer l: dF = (LNbwd(dT) masked) W2 * (f1 > 0) [/ (1 - p)]; dT2 = dR + dF W1
+  auto ffn_bwd = [&](int l) -> int {
+    const float* b = blk(l);
+    const bool cr = p->cross != 0;
+    float* dF = ws + L.gdf + (long long)l * R * FF;
+    TokPhase* P = tok_gemm(tb, TOK_A_LNBWD, R, FF, A, dy_slot(0, l), A, p->ff2_w[l], FF, 1, nullptr, dF, FF);
+    FX_REQUIRE(P, "decoder: token program");
+    lnb(P, p->ln_ff_w[l], b + L.xh3, b + L.rs3, 0, l, 5);
+    P->gate = b + L.f1;
+    P->ldg = FF;
+    if (pd > 0.f) P->alpha = 1.f / (1.f - pd);
+    P = tok_gemm(tb, TOK_A_PLAIN, R, A, FF, dF, FF, p->ff1_w[l], A, 1, nullptr, dy_slot(cr ? 1 : 2, l), A);
+    FX_REQUIRE(P, "decoder: token program");
+    P->resid = dres(0, l);
+    P->ldr = A;
+    return FX_OK;
+  };
+  // self-attention (+ its LN) of layer l: dO = LNbwd1(dT1) W_o ; [dq|dk|dv] ; dX = dR1 + dQKV W_in
+  auto sa_bwd = [&](int l) -> int {
+    const float* b = blk(l);
+    TokPhase* P = tok_gemm(tb, TOK_A_LNBWD, R, A, A, dy_slot(2, l), A, p->sa_out_w[l], A, 1, nullptr, dO, A);
+    FX_REQUIRE(P, "decoder: token program");
+    lnb(P, p->ln_sa_w[l], b + L.xh1, b + L.rs1, 2, l, 1);
+    float* dQKV = ws + L.gdqkv + (long long)l * 3 * RA;
+    P = tb.add(TOK_MHABWD, TOK_A_PLAIN, R, 3 * A, A);
+    FX_REQUIRE(P, "decoder: token program");
+    P->a = dO;
+    P->lda = A;
+    P->c = dQKV;
+    P->ldc = 3 * A;
+    P->nvid = nvid;
+    P->Qv = Qv;
+    P->nh = h;
+    P->scale = scale;
+    P->qkv = const_cast<float*>(b + L.qkv);
+    P->probs = const_cast<float*>(b + L.psa);
+    tok_drop(P->attn_thr, P->attn_scale, P->attn_seed, pa, dec_seed(p, l, 0));
+    if (l > 0 || dtgt) {
+      P = tok_gemm(tb, TOK_A_PLAIN, R, A, 3 * A, dQKV, 3 * A, p->sa_in_w[l], A, 1, nullptr, l > 0 ? dy_slot(0, l - 1) : dtgt,
+                   l > 0 ? A : lddt);
+      FX_REQUIRE(P, "decoder: token program");
+      P->resid = dres(2, l);
+      P->ldr = A;
+    }
+    return FX_OK;
+  };
+  for (int l = NL - 1; l >= 0; --l) {
+    const float* b = blk(l);
+    FX_TRY(ffn_bwd(l));
+    if (p->cross) {
+      TokPhase* P = tok_gemm(tb, TOK_A_LNBWD, R, A, A, dy_slot(1, l), A, p->ca_out_w[l], A, 1, nullptr, dO, A);
+      FX_REQUIRE(P, "decoder: token program");
+      lnb(P, p->ln_ca_w[l], b + L.xh2, b + L.rs2, 1, l, 3);
+      FX_TRY(tb.flush());
+      float* dq = ws + L.gdq + (long long)l * RA;
+      const float* kv = saved + L.kv;
+      TAttnOpts o;
+      o.koff = p->mem_off;
+      o.drop_p = pa;
+      o.drop_seed = dec_seed(p, l, 2);
+      FX_TRY(launch_tattn_bwd(b + L.qc, A, kv + (long long)l * A, AL2, kv + (long long)(NL + l) * A, AL2, b + L.oca, A,
+                              dO, A, b + L.pca, nvid, Qv, Tv, hd, h, scale, dq, A, dkv + (long long)l * A, AL2,
+                              dkv + (long long)(NL + l) * A, AL2, ws + L.core, s, &o));
+      P = tok_gemm(tb, TOK_A_PLAIN, R, A, A, dq, A, p->ca_q_w[l], A, 1, nullptr, dy_slot(2, l), A);
+      FX_REQUIRE(P, "decoder: token program");
+      P->resid = dres(1, l);
+      P->ldr = A;
+    }
+    FX_TRY(sa_bwd(l));
+  }
+  return tb.flush();
+}
+
 }  // namespace
 }  // namespace fx
 
 using namespace fx;
 
 extern "C" {
+
+int fx_tok_gemm(const float* a, long long lda, int M, int N, int K, int amode, const float* ln_w, const float* ln_b,
+                const float* w, long long ldw, int btrans, const float* bias, const float* resid, long long ldr,
+                float* c, long long ldc, int* status, void* stream) {
+  FX_REQUIRE(a && w && c && M > 0 && N > 0 && (amode == TOK_A_PLAIN || (amode == TOK_A_LN && ln_w && ln_b)),
+             "tok gemm: bad arguments");
+  TokBuild tb((hipStream_t)stream, status);
+  TokPhase* P = tok_gemm(tb, amode, M, N, K, a, lda, w, ldw, btrans, bias, c, ldc);
+  FX_REQUIRE(P, "tok gemm: program");
+  P->resid = resid;
+  P->ldr = ldr;
+  if (amode == TOK_A_LN) {
+    P->ln.w = ln_w;
+    P->ln.b = ln_b;
+    P->ln.eps = 1e-5f;
+  }
+  return tb.flush();
+}
 
 long long fx_decoder_saved_floats(const fx_decoder_params* p, int R, int T, int nvid, int has_qpos, int has_mpos) {
   return dec_layout(p, R, T, has_qpos, has_mpos, std::max(nvid, 1)).total_saved;
@@ -324,6 +710,14 @@ int fx_decoder_fwd(const fx_decoder_params* p, const float* tgt, long long ldt, 
                         kv + AL, AL2, AL, 0, s));
       // keep mem + pos for the key weight gradient
       FX_TRY(add2(mem, ldm, mpos, ldmp, T, p->Hm, saved + L.mpos, p->Hm, 0, s));
+    }
+  }
+  {
+    const void* ptrs[3] = {tgt, qpos, out};
+    const long long lds_[2] = {ldt, ldo};
+    if (dec_tok_ok(p, R, nvid, ptrs, 3, lds_, 2)) {
+      float* u = spl + (std::max(L.total_ws_fwd - L.wsp, RA) - RA);
+      return dec_fwd_tok(p, tgt, ldt, R, qpos, nvid, Qv, Tv, kv, out, ldo, saved, L, u, spl, s);
     }
   }
   const float* x = tgt;
@@ -445,12 +839,16 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
   // LN input gradient of layer l's LayerNorm k (0 FFN, 1 cross-attention, 2 self-attention): each
   // producer in the chain writes straight into the slot its consumer reads
   auto dy_slot = [&](int k, int l) { return ws + L.gdy + ((long long)k * NL + l) * RA; };
+  const void* tptrs[3] = {dout, dtgt, qpos};
+  const long long tlds[2] = {lddo, dtgt ? lddt : 4};
+  const bool tok = dec_tok_ok(p, R, nvid, tptrs, 3, tlds, 2);
+  if (tok) FX_TRY(dec_bwd_tok(p, R, nvid, Qv, Tv, dout, lddo, dtgt, lddt, saved, ws, L, dkv, s));
   dT = dy_slot(0, NL - 1);
-  FX_TRY(linear_bwd_pair(desc_linear_dwdb(dout, lddo, fin, A, R, A, p->out_dim, g->out_w, g->out_b, 1, spl),
+  if (!tok) FX_TRY(linear_bwd_pair(desc_linear_dwdb(dout, lddo, fin, A, R, A, p->out_dim, g->out_w, g->out_b, 1, spl),
                          desc_linear_dx(dout, lddo, p->out_w, R, A, p->out_dim, p->final_norm ? dS : dT, A, 0, nullptr,
                                         0, spl),
                          s));
-  if (p->final_norm)
+  if (p->final_norm && !tok)
     FX_TRY(launch_layernorm_bwd(dS, A, nullptr, 0, saved + L.fxh, A, p->fn_w, saved + L.frs, R, A, 0, dT, A, g->fn_w,
                                 g->fn_b, lnws, s));
   // Weight gradients of the token linears: the chain below writes each layer's dU (three LayerNorm
@@ -458,7 +856,7 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
   // GEMMs of every layer follow the chain on the side stream, batched over the layers where the
   // gradient buffers are uniformly strided (~35 one-wave launches per step left the main stream).
   auto slot_u = [&](int k, int l) { return ws + L.gdu + ((long long)k * NL + l) * RA; };   // k: 0 ff, 1 ca, 2 sa
-  for (int l = NL - 1; l >= 0; --l) {
+  for (int l = NL - 1; l >= 0 && !tok; --l) {
     const float* b = saved + L.layers + l * L.per_layer;
     dT = dy_slot(0, l);
     float* dU = slot_u(0, l);
@@ -583,6 +981,12 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
     };
     const long long PL = L.per_layer;
     const float* b0 = saved + L.layers;
+    if (tok && (g->out_w || g->out_b)) {   // the output linear's weight gradient (the separate-launch path pairs it with its dX)
+      fx_gemm_desc d = desc_linear_dwdb(dout, lddo, fin, A, R, A, p->out_dim, g->out_w, g->out_b, 1, nullptr);
+      d.split_k = 1;
+      d.workspace = nullptr;
+      FX_TRY(launch_gemm(d, sd));
+    }
     FX_TRY(kind(0, NL, slot_u(0, 0), A, RA, b0 + L.f1, FF, PL, FF, A, g->ff2_w, g->ff2_b, 0, 0));
     FX_TRY(kind(0, NL, ws + L.gdf, FF, (long long)R * FF, b0 + (p->cross ? L.t2 : L.t1), A, PL, A, FF, g->ff1_w,
                 g->ff1_b, 0, 0));
@@ -607,8 +1011,9 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
   {
     // every layer's LayerNorm weight / bias gradients in one launch: dw += sum_rows dy * xhat, db += sum_rows dy
     // (the chain's LN backward computed dx only)
-    LnGradJob jobs[3 * MAXL];
+    LnGradJob jobs[3 * MAXL + 1];
     int nj = 0;
+    if (tok && p->final_norm && (g->fn_w || g->fn_b)) jobs[nj++] = LnGradJob{dS, saved + L.fxh, g->fn_w, g->fn_b};
     for (int l = 0; l < NL; ++l) {
       const float* b = saved + L.layers + l * L.per_layer;
       auto add = [&](int k, long long xh_off, float* const* gw, float* const* gb) {

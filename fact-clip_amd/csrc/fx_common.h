@@ -148,6 +148,9 @@ struct Knobs {
   FILE* gemm_log = nullptr; // FX_GEMM_LOG=<file>: one line per GEMM launch (shape census)
   bool gemm_group = true;
   bool gemm_ktail = true;    // FX_GEMM_KTAIL=0: column-major operands with a K tail take the generic kernel (A/B)
+  bool dec_tok = true;       // FX_DEC_TOK=0: the decoders' token rows as separate launches instead of the persistent
+                             // token kernel (tokdec.hip) (A/B, and the fallback the tests compare with)
+  int tok_spin = 0;          // FX_TOK_SPIN: grid-barrier polls before a token-kernel workgroup gives up (0: ~1 s)
   bool side_stream = true;
   int side_priority = 0;    // -1 low, 0 normal, 1 high
   int defer_split = 16;     // FX_DEFER_SPLIT: split-K of the deferred (side-stream) weight-gradient GEMMs (16 vs 8: 15.78 vs 15.95 ms median of 6 pairs)

@@ -920,8 +920,17 @@ def status_raise(value, dev):
     if value:
         device_status(dev).zero_()
         _bwd_status.clear()       # (the same failure, possibly also seen by a backward-pass copy)
-        raise nx.FactmxNativeError(f"device status {value}: a BiGRU workgroup timed out waiting for its peers "
-                                   "(FX_STATUS_GRU_TIMEOUT) -- the GRU outputs of this step are invalid")
+        raise nx.FactmxNativeError(f"device status {value}: {_status_text(value)} -- the outputs of this step "
+                                   "are invalid")
+
+
+def _status_text(value):
+    parts = []
+    if value & nx.STATUS_GRU_TIMEOUT:
+        parts.append("a BiGRU workgroup timed out waiting for its peers (FX_STATUS_GRU_TIMEOUT)")
+    if value & nx.STATUS_TOK_TIMEOUT:
+        parts.append("a persistent token-kernel workgroup timed out at a grid barrier (FX_STATUS_TOK_TIMEOUT)")
+    return "; ".join(parts) or "unknown failure"
 
 
 # Backward-pass status read-backs: a BiGRU backward writes the same status word as the forward, but
@@ -1283,6 +1292,7 @@ class DecoderFn(torch.autograd.Function):
             _fill_decoder_struct(prm, slots, gl, params, keep)
             cache.update(prm=prm, key=key, keep=keep)
         DecoderFn._set_call(prm, call)
+        prm.status = nx.ptr(device_status(tgt.device))
         ctx.call = call
         R = tgt.shape[0]
         T = mem.shape[0] if mem is not None else 0
@@ -1320,6 +1330,7 @@ class DecoderFn(torch.autograd.Function):
             cache.update(grads=g, gkey=gkey, gkeep=keep)
         prm = cache["prm"]
         DecoderFn._set_call(prm, ctx.call)        # the module may have run again since this forward
+        prm.status = nx.ptr(device_status(dev))
         A = meta["A"]
         dtgt = _empty(R, A, device=dev) if nd[0] else None
         dqpos = _empty(R, A, device=dev) if (hq and nd[1]) else None
@@ -1335,8 +1346,8 @@ class DecoderFn(torch.autograd.Function):
                                   nx.ld(dout),
                                   nx.ptr(dtgt), nx.ld(dtgt), nx.ptr(dqpos), nx.ptr(dmem), nx.ld(dmem), nx.ptr(dmpos),
                                   nx.ld(dmpos), nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_decoder_bwd")
-        if defer:
-            _defer_to_side(tgt, mem, mpos, saved, ws)
+        if defer:   # (dout too: the output linear's weight gradient reads it on the side stream)
+            _defer_to_side(tgt, mem, mpos, saved, ws, dout)
         return (dtgt, dqpos, dmem, dmpos, None, None, None) + tuple(t[1] for t in tg)
 
 

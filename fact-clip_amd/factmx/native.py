@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FACTMX_LIB", os.path.join(_HERE, "_lib", "libfactmx.so"))
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -76,7 +76,7 @@ DECODER_GLOBAL_FIELDS = ["fn_w", "fn_b", "out_w", "out_b"]
 class DecoderParams(ctypes.Structure):
     _fields_ = ([("A", I), ("FF", I), ("nhead", I), ("num_layers", I), ("cross", I), ("Hm", I), ("out_dim", I),
                  ("final_norm", I), ("eps", F)] + [(n, P) for n in _DEC_PTRS] + [(n, P) for n in DECODER_GLOBAL_FIELDS]
-                + [("side_defer", I), ("dropout", F), ("attn_dropout", F), ("seed", U), ("mem_off", P)])
+                + [("side_defer", I), ("dropout", F), ("attn_dropout", F), ("seed", U), ("mem_off", P), ("status", P)])
 
 
 class DecoderGrads(ctypes.Structure):
@@ -84,6 +84,7 @@ class DecoderGrads(ctypes.Structure):
 
 
 STATUS_GRU_TIMEOUT = 1   # FX_STATUS_GRU_TIMEOUT: a BiGRU workgroup gave up waiting for a peer
+STATUS_TOK_TIMEOUT = 2   # FX_STATUS_TOK_TIMEOUT: a persistent token-kernel barrier wait gave up
 LOSS_MAXK = 512        # FX_LOSS_MAXK: matched columns of an attention loss term
 LOSS_NB = 128          # FX_LOSS_NB: row blocks per loss term
 TERM_CLASS, TERM_ATTN, TERM_INFONCE = 0, 1, 2
@@ -124,6 +125,7 @@ SIGNATURES = {
                        P, P, P, P, P, P, P, P, I, I, P, I, P]),
     "fx_decoder_saved_floats": (L, [ctypes.POINTER(DecoderParams), I, I, I, I, I]),
     "fx_decoder_workspace_floats": (L, [ctypes.POINTER(DecoderParams), I, I, I, I, I]),
+    "fx_tok_gemm": (I, [P, L, I, I, I, I, P, P, P, L, I, P, P, L, P, L, P, P]),
     "fx_decoder_fwd": (I, [ctypes.POINTER(DecoderParams), P, L, I, P, L, P, L, I, I, P, L, P, L, P, P, P]),
     "fx_decoder_bwd": (I, [ctypes.POINTER(DecoderParams), ctypes.POINTER(DecoderGrads), P, L, I, P, P, L, I, I, P, L,
                            P, L, P, L, P, P, L, P, L, P, P, P]),

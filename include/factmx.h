@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FX_ABI_VERSION 17
+#define FX_ABI_VERSION 18
 
 enum {
   FX_OK = 0,
@@ -233,6 +233,9 @@ typedef struct fx_decoder_params {
                                  (query_row * nhead + head) * key_rows_total + key_row */
   const int* mem_off;         /* host (nvid + 1) frame-memory row offsets of ragged videos; NULL: video v
                                  owns memory rows [v T/nvid, (v+1) T/nvid) */
+  int* status;                /* caller-owned device int32 status word (nullable): the persistent token
+                                 kernel (tokdec.hip) ORs FX_STATUS_TOK_TIMEOUT into it when a grid-barrier
+                                 wait gives up (outputs then wrong; never cleared by the library) */
 } fx_decoder_params;
 
 typedef struct fx_decoder_grads {
@@ -252,6 +255,13 @@ typedef struct fx_decoder_grads {
 
 long long fx_decoder_saved_floats(const fx_decoder_params* p, int R, int T, int nvid, int has_qpos,
                                   int has_mpos);
+/* One product through the persistent token kernel's GEMM phase (tokdec.hip; kernel-level tests):
+ * c = epilogue(A' W^T) with A' = a (amode 0) or LayerNorm(a; ln_w, ln_b, eps 1e-5) (amode 1, K <= 256),
+ * W (N, K) row-major, or with btrans W (K, N) (c = A' W); + bias, + resid (nullable).  M, N any; K a
+ * multiple of 4, <= 768.  status: device int32 word (FX_STATUS_TOK_TIMEOUT). */
+int fx_tok_gemm(const float* a, long long lda, int M, int N, int K, int amode, const float* ln_w, const float* ln_b,
+                const float* w, long long ldw, int btrans, const float* bias, const float* resid, long long ldr,
+                float* c, long long ldc, int* status, void* stream);
 long long fx_decoder_workspace_floats(const fx_decoder_params* p, int R, int T, int nvid, int has_qpos,
                                       int has_mpos);
 int fx_decoder_fwd(const fx_decoder_params* p, const float* tgt, long long ldt, int R, const float* qpos,
@@ -494,6 +504,7 @@ int fx_seg_sum_rows(const float* dx, long long lddx, const int32_t* seg_start, c
  *   fails (factmx raises FactmxNativeError).
  * ---------------------------------------------------------------------- */
 #define FX_STATUS_GRU_TIMEOUT 1
+#define FX_STATUS_TOK_TIMEOUT 2   /* fx_decoder_*: a persistent token-kernel barrier wait gave up */
 long long fx_gru_saved_floats(int S, int Hh);
 long long fx_gru_workspace_floats(int S, int nseq, int In, int Hh);
 int fx_gru_bidir_fwd(const float* x, long long ldx, int S, int nseq, const int* seq_off, int In,
@@ -706,7 +717,8 @@ int fx_get_default_precision(void);
  *   2 = attention over T backward (tattn_bwd_kernel + split merge),
  *   3-6 = X2Y cores (a2f fwd, a2f bwd, f2a fwd, f2a bwd),
  *   7 = fused MS-TCN layer (frl_kernel: conv + ReLU + 1x1 + residual forward,
- *       or the fused dX chain backward).
+ *       or the fused dX chain backward),
+ *   8 = persistent token-kernel launches of the decoders (tokdec.hip programs).
  * fx_prof_enable resets one kind; fx_prof_disable resets all.
  * ---------------------------------------------------------------------- */
 int fx_prof_enable(int kind, int max_events);

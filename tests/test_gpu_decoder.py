@@ -100,3 +100,29 @@ def test_fused_path_is_taken():
     assert basic._fused_decoder_ok(dec)
     dec(torch.randn(8, 1, 32, device=DEV), torch.randn(8, 1, 32, device=DEV))
     assert hasattr(dec, "_fx_spec")
+
+
+@pytest.mark.parametrize("M,N,K,amode,btrans", [(64, 256, 256, 0, 0), (64, 512, 256, 1, 0), (32, 256, 768, 0, 1),
+                                                 (37, 80, 256, 1, 0), (64, 256, 76, 0, 1)])
+def test_token_kernel_gemm_phase(M, N, K, amode, btrans):
+    """One GEMM phase of the persistent token kernel (tokdec.hip) vs float64 torch: plain or LayerNorm-staged
+    A rows, W or W^T, bias + residual epilogue."""
+    from factmx import functional as fxf
+    from factmx import native as nx
+    g = torch.Generator().manual_seed(5)
+    a = torch.randn(M, K, generator=g, dtype=torch.float64)
+    w = torch.randn(K, N, generator=g, dtype=torch.float64) if btrans else torch.randn(N, K, generator=g, dtype=torch.float64)
+    w = w / K ** 0.5
+    lw, lb = 1 + 0.3 * torch.randn(K, generator=g, dtype=torch.float64), 0.2 * torch.randn(K, generator=g, dtype=torch.float64)
+    bias, res = torch.randn(N, generator=g, dtype=torch.float64), torch.randn(M, N, generator=g, dtype=torch.float64)
+    d = [t.float().to(DEV).contiguous() for t in (a, w, lw, lb, bias, res)]
+    c = torch.empty(M, N, device=DEV)
+    st = fxf.device_status(c.device)
+    lib = nx.load()
+    assert lib.fx_tok_gemm(nx.ptr(d[0]), K, M, N, K, amode, nx.ptr(d[2]), nx.ptr(d[3]), nx.ptr(d[1]), N if btrans else K,
+                           btrans, nx.ptr(d[4]), nx.ptr(d[5]), N, nx.ptr(c), N, nx.ptr(st), nx.stream()) == 0
+    torch.cuda.synchronize()
+    assert int(st[0]) == 0
+    x = fo.layer_norm(a, lw, lb) if amode else a
+    ref = x @ (w if btrans else w.t()) + bias + res
+    _close(c, ref, 2e-5, "c")

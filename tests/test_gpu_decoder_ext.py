@@ -151,15 +151,45 @@ CASES = [
 ]
 
 
+def _tok_launches(lib):
+    import ctypes
+    ms, fl, by, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+    assert lib.fx_prof_collect(8, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(by), ctypes.byref(n)) == 0
+    return n.value
+
+
 @pytest.mark.parametrize("cross,Q,T,p", CASES)
 def test_fused_decoder_tokens_dropout_ragged(cross, Q, T, p, monkeypatch):
+    _decoder_case(cross, Q, T, p, monkeypatch, 64, 4, 96, expect_tok=False)
+
+
+# shapes of the persistent token kernel (tokdec.hip): head dim 32, <= 32 tokens per video
+TOK_CASES = [
+    (True, 32, (300, 220), 0.2),
+    (True, 20, (257, 257), 0.0),
+    (True, 7, (64, 90), 0.2),
+    (False, 32, None, 0.2),
+    (False, 17, None, 0.0),
+]
+
+
+@pytest.mark.parametrize("cross,Q,T,p", TOK_CASES)
+def test_token_kernel_decoder_dropout_ragged(cross, Q, T, p, monkeypatch):
+    """The persistent token kernel's programs (forward and backward, LayerNorm staged into the products,
+    in-projection + self-attention items, dropout at every site, ragged frame memory) vs the float64
+    masked restatement, and fx_prof kind 8 proves the kernel ran."""
+    _decoder_case(cross, Q, T, p, monkeypatch, 128, 4, 192, expect_tok=True)
+
+
+def _decoder_case(cross, Q, T, p, monkeypatch, A, nh, FF, expect_tok):
+    from factmx import native as nx
     seeds = []
 
     def nxt():
         seeds.append(0x5DEECE66D * (len(seeds) + 3) % 2 ** 62)
         return seeds[-1]
     monkeypatch.setattr(fxf, "dropout_seed", nxt)
-    A, nh, FF, nl, Hm, out_dim, nvid = 64, 4, 96, 2, 96, 80, 2
+    nl, Hm, out_dim, nvid = 2, 96, 80, 2
     dec = _build(cross, A, nh, FF, nl, Hm, out_dim, p).train()
     R = nvid * Q
     moff = [0] + [int(x) for x in np.cumsum(T)] if cross else None
@@ -169,10 +199,18 @@ def test_fused_decoder_tokens_dropout_ragged(cross, Q, T, p, monkeypatch):
     dt = [t.float().to(DEV).requires_grad_(True) for t in (tgt, qpos)]
     dm = [t.float().to(DEV).requires_grad_(True) for t in (mem, mpos)] if cross else [None, None]
     ragged = cross and T[0] != T[1]
-    y = fxf.decoder(dec, dt[0], dm[0], pos=dm[1], query_pos=dt[1], nvid=nvid, mem_off=moff if ragged else None)
-    (y * g.float().to(DEV)).sum().backward()
-    fxf.side_join()
-    torch.cuda.synchronize()
+    lib = nx.load()
+    assert lib.fx_prof_enable(8, 64) == 0
+    try:
+        y = fxf.decoder(dec, dt[0], dm[0], pos=dm[1], query_pos=dt[1], nvid=nvid, mem_off=moff if ragged else None)
+        (y * g.float().to(DEV)).sum().backward()
+        fxf.side_join()
+        torch.cuda.synchronize()
+        ntok = _tok_launches(lib)
+    finally:
+        lib.fx_prof_disable()
+    assert (ntok > 0) == expect_tok, ntok
+    fxf.check_device_status()
     assert len(seeds) == (1 if p > 0 else 0)
     M = _Masks(seeds[-1] if seeds else 0, p, p, R, nh)
     P = {n: t.detach().double().cpu().requires_grad_(True) for n, t in dec.named_parameters()}
