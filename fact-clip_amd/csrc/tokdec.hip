@@ -100,7 +100,13 @@ __device__ __forceinline__ float keepf(unsigned long long seed, unsigned thr, fl
 // accumulator element r of a lane: row (r & 3) + 8 (r >> 2) + 4 (lane >> 5), column lane & 31
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
-// diagnostic stamps (FX_TOK_DEBUG): the current phase's 8 slots of this workgroup, or null
+// workgroup barrier for LDS hand-offs only: waits for this wave's LDS accesses, not for its global
+// stores (__syncthreads() also waits for every outstanding global store -- with write-through stores,
+// their write acknowledgements -- before the barrier; the phases' global hand-offs are ordered by the
+// grid barrier's own wait instead)
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// diagnostic stamps (FX_TOK_DEBUG): the current phase's 8 LDS slots of this workgroup, or null
 __device__ __forceinline__ void tstamp(unsigned long long* st, int k) {
   if (st && threadIdx.x == 0) st[k] = __builtin_amdgcn_s_memrealtime();
 }
@@ -117,7 +123,7 @@ struct BarState {
   int G;
 };
 
-__device__ bool grid_sync(BarState& b, int* dead) {
+__device__ __forceinline__ bool grid_sync(BarState& b, int* dead) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has left (sc1: written through)
   __syncthreads();
   b.target += (unsigned long long)b.G;
@@ -137,7 +143,7 @@ __device__ bool grid_sync(BarState& b, int* dead) {
   return !*dead;
 }
 
-__device__ void grid_exit(BarState& b, int dead) {
+__device__ __forceinline__ void grid_exit(BarState& b, int dead) {
   if (threadIdx.x == 0 && !dead) {
     unsigned long long* ex = b.cnt + 16;
     const unsigned long long prev = __hip_atomic_fetch_add(ex, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -162,38 +168,50 @@ constexpr int DUTY_ALL = -2;
 
 __device__ __forceinline__ bool duty_col(int wd, int k) { return wd == DUTY_ALL || (wd >= 0 && (k >> 5) == (wd >> 5)); }
 
-// BWD: LayerNorm backward rows (x-hat, 1/std read); else forward; ADDPOS: + apos on the staged rows
-template <bool BWD, bool ADDPOS>
-__device__ __forceinline__ void stage_ln(const TokPhase& P, int r0, int rlim, float* As, int as, int wd) {
+// keep mask of up to 32 dropout draws idx0 + off(e) (one bit each): the hash in a loop that is not
+// unrolled (its 64-bit multiplies are long; unrolled per element they were a large share of the code)
+__device__ __forceinline__ unsigned keep_bits(unsigned long long seed, unsigned thr, unsigned long long idx0, int n,
+                                              int stride4) {
+  unsigned km = 0;
+#pragma unroll 1
+  for (int e = 0; e < n; ++e)
+    km |= (fx_drop_bits(seed, idx0 + (unsigned long long)((e >> 2) * stride4 + (e & 3))) >= thr ? 1u : 0u) << e;
+  return km;
+}
+__device__ __forceinline__ float kbit(unsigned km, int e, float scale) { return (km >> e) & 1u ? scale : 0.f; }
+
+// LayerNorm rows, forward (bwd false: the stored rows are the pre-LN sum) or backward (the stored rows
+// are dL/d(LN output); x-hat and 1/std read).  addpos: the staged rows get + apos.
+__device__ __forceinline__ void stage_ln(const TokPhase& P, bool bwd, int r0, int rlim, float* As, int as, int wd,
+                                         bool addpos) {
   const int tid = threadIdx.x, row = tid >> 3, sub = tid & 7;
   const int m = r0 + row, K = P.K;
   const bool mok = m < rlim;
   const int ng = (K + 31) / 32;
-  constexpr bool bwd = BWD, addpos = ADDPOS;
-  constexpr int NH = BWD ? NGL : 1, NB = BWD ? 1 : NGL, NP = ADDPOS ? NGL : 1;
-  float4 v[NGL], h[NH], gw[NGL], gb[NB], pp[NP];
+  float4 v[NGL], x[NGL], gw[NGL], pp[NGL];
   // unconditional loads from clamped in-range addresses, zeroed by selects after every load has been
-  // issued: no branch around a load, so no wait between them
+  // issued: no branch around a load, so no wait between them.  x: beta (forward) or x-hat (backward);
+  // tensors written before the launch (x-hat, 1/std, gamma, beta, positions) take plain loads
   const int mc = min(m, rlim - 1);
+  const float* xs = bwd ? P.ln.xhat + (long long)mc * K : P.ln.b;
+  const float* ps = addpos ? P.apos + (long long)mc * P.ldpos : P.ln.w;
 #pragma unroll
   for (int i = 0; i < NGL; ++i) {
     const int kc = min(4 * sub + 32 * i, K - 4);
     v[i] = ldc4(P.a, (long long)mc * P.lda + kc);
-    if (BWD) h[i % NH] = ldc4(P.ln.xhat, (long long)mc * K + kc);
+    x[i] = ld4(xs + kc);
     gw[i] = ld4(P.ln.w + kc);
-    if (!BWD) gb[i % NB] = ld4(P.ln.b + kc);
-    if (ADDPOS) pp[i % NP] = ld4(P.apos + (long long)mc * P.ldpos + kc);
+    pp[i] = ld4(ps + kc);
   }
-  const float rsb = BWD ? ldc1(P.ln.rstd, mc) : 0.f;
+  const float rsb = bwd ? P.ln.rstd[mc] : 0.f;
 #pragma unroll
   for (int i = 0; i < NGL; ++i) {
     const int k = 4 * sub + 32 * i;
     const bool kok = i < ng && k < K, ok = kok && mok;
     v[i] = ok ? v[i] : zero4();
-    if (BWD) h[i % NH] = ok ? h[i % NH] : zero4();
+    x[i] = (bwd ? ok : kok) ? x[i] : zero4();
     gw[i] = kok ? gw[i] : zero4();
-    if (!BWD) gb[i % NB] = kok ? gb[i % NB] : zero4();
-    if (ADDPOS) pp[i % NP] = ok ? pp[i % NP] : zero4();
+    pp[i] = (ok && addpos) ? pp[i] : zero4();
   }
   if (!bwd) {
     float s = 0.f;
@@ -204,26 +222,25 @@ __device__ __forceinline__ void stage_ln(const TokPhase& P, int r0, int rlim, fl
 #pragma unroll
     for (int i = 0; i < NGL; ++i) {
       const int k = 4 * sub + 32 * i;
-      if (i < ng && k < K) {
-        const float a = v[i].x - mu, b = v[i].y - mu, c = v[i].z - mu, d = v[i].w - mu;
-        q += (a * a + b * b) + (c * c + d * d);
-      }
+      const bool kok = i < ng && k < K;
+      const float a = v[i].x - mu, b = v[i].y - mu, c = v[i].z - mu, d = v[i].w - mu;
+      q += kok ? (a * a + b * b) + (c * c + d * d) : 0.f;
     }
     const float rs = rsqrtf(rsum8(q) / K + P.ln.eps);
 #pragma unroll
     for (int i = 0; i < NGL; ++i) {
       const int k = 4 * sub + 32 * i;
       if (i < ng && k < K) {
-        const float4 g = gw[i], bb = gb[i % NB];
+        const float4 g = gw[i], bb = x[i];
         const float4 hh = make_float4((v[i].x - mu) * rs, (v[i].y - mu) * rs, (v[i].z - mu) * rs, (v[i].w - mu) * rs);
         const float4 y = make_float4(hh.x * g.x + bb.x, hh.y * g.y + bb.y, hh.z * g.z + bb.z, hh.w * g.w + bb.w);
         if (mok && duty_col(wd, k)) {
           const long long o = (long long)m * K + k;
           if (P.ln.xh) stc4(P.ln.xh, o, hh);
           if (P.ln.y) stc4(P.ln.y, o, y);
-          if (P.ln.y2) stc4(P.ln.y2, o, add4(y, (addpos && P.ln.pos == P.apos) ? pp[i % NP] : ld4(P.ln.pos + o)));
+          if (P.ln.y2) stc4(P.ln.y2, o, add4(y, (addpos && P.ln.pos == P.apos) ? pp[i] : ld4(P.ln.pos + o)));
         }
-        v[i] = addpos ? add4(y, pp[i % NP]) : y;
+        v[i] = add4(y, pp[i]);
       }
     }
     if (mok && (wd == 0 || wd == DUTY_ALL) && sub == 0 && P.ln.rs) stc1(P.ln.rs, m, rs);
@@ -235,28 +252,29 @@ __device__ __forceinline__ void stage_ln(const TokPhase& P, int r0, int rlim, fl
       const float4 g = gw[i];
       v[i] = make_float4(v[i].x * g.x, v[i].y * g.y, v[i].z * g.z, v[i].w * g.w);
       s1 += (v[i].x + v[i].y) + (v[i].z + v[i].w);
-      s2 += (v[i].x * h[i % NH].x + v[i].y * h[i % NH].y) + (v[i].z * h[i % NH].z + v[i].w * h[i % NH].w);
+      s2 += (v[i].x * x[i].x + v[i].y * x[i].y) + (v[i].z * x[i].z + v[i].w * x[i].w);
     }
     s1 = rsum8(s1) / K;
     s2 = rsum8(s2) / K;
+    const bool drop = P.ln.drop_thr != 0;
+    const unsigned km = drop ? keep_bits(P.ln.drop_seed, P.ln.drop_thr, (unsigned long long)m * K + 4 * sub,
+                                         4 * min(ng, NGL), 32)
+                             : ~0u;
+    const float dsc = drop ? P.ln.drop_scale : 1.f;
 #pragma unroll
     for (int i = 0; i < NGL; ++i) {
       const int k = 4 * sub + 32 * i;
       if (i < ng && k < K) {
-        const float4 hh = h[i % NH];
+        const float4 hh = x[i];
         float4 d = make_float4(rsb * (v[i].x - s1 - hh.x * s2), rsb * (v[i].y - s1 - hh.y * s2),
                                rsb * (v[i].z - s1 - hh.z * s2), rsb * (v[i].w - s1 - hh.w * s2));
         const long long o = (long long)m * K + k;
         const bool duty = mok && duty_col(wd, k);
         if (duty && P.ln.dr) stc4(P.ln.dr, o, d);
-        if (P.ln.drop_thr) {
-          d.x *= keepf(P.ln.drop_seed, P.ln.drop_thr, P.ln.drop_scale, (unsigned long long)o);
-          d.y *= keepf(P.ln.drop_seed, P.ln.drop_thr, P.ln.drop_scale, (unsigned long long)o + 1);
-          d.z *= keepf(P.ln.drop_seed, P.ln.drop_thr, P.ln.drop_scale, (unsigned long long)o + 2);
-          d.w *= keepf(P.ln.drop_seed, P.ln.drop_thr, P.ln.drop_scale, (unsigned long long)o + 3);
-        }
+        d = make_float4(d.x * kbit(km, 4 * i, dsc), d.y * kbit(km, 4 * i + 1, dsc), d.z * kbit(km, 4 * i + 2, dsc),
+                        d.w * kbit(km, 4 * i + 3, dsc));
         if (duty && P.ln.du) stc4(P.ln.du, o, d);
-        v[i] = addpos ? add4(d, pp[i % NP]) : d;
+        v[i] = add4(d, pp[i]);
       }
     }
   }
@@ -306,9 +324,7 @@ __device__ __forceinline__ void stage_plain(const TokPhase& P, int r0, int rlim,
 
 __device__ __forceinline__ void stage_rows(const TokPhase& P, int r0, int rlim, float* As, int as, int wd, bool addpos) {
   if (P.amode == TOK_A_PLAIN) stage_plain(P, r0, rlim, As, as, wd, addpos);
-  else if (P.amode == TOK_A_LNBWD) stage_ln<true, false>(P, r0, rlim, As, as, wd);
-  else if (addpos) stage_ln<false, true>(P, r0, rlim, As, as, wd);
-  else stage_ln<false, false>(P, r0, rlim, As, as, wd);
+  else stage_ln(P, P.amode == TOK_A_LNBWD, r0, rlim, As, as, wd, addpos);
 }
 
 // ------------------------------------------------------------------ 32 x 32 products
@@ -332,8 +348,8 @@ __device__ __forceinline__ void load_b(const float* W, long long ldw, int n, boo
                          W[(long long)(kc + 3) * ldw + n]);
     }
   }
-#pragma unroll
-  for (int g = 0; g < NGB; ++g) b[g] = (g < ng && nok && kb + 4 * g < K) ? b[g] : zero4();
+  // no zeroing: a clamped k >= K re-reads an in-range weight that meets a zero A column (As is zero for
+  // K <= k < Kp), and a clamped column n >= N is never stored; so nothing here waits for the loads
 }
 
 __device__ __forceinline__ void mma_groups(const float* arow, int kb, int ng, const float4* b, f32x16& acc) {
@@ -376,6 +392,7 @@ __device__ __forceinline__ float red_sum(const float* red, int r, int lane) {
 // Per item: the B loads, the epilogue operands (bias, residual, gate of this thread's 4 outputs) and the
 // staging loads all go out before the first product, so an item costs about one memory round trip.
 __device__ __forceinline__ void gemm_phase(const TokPhase& P, float* lds, int G, unsigned long long* st) {
+  const int sit = (int)blockIdx.x + (st && st[7] == 3 ? G : 0);   // diagnostic: FX_TOK_DEBUG=3 stamps the second item
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nrt = (P.M + 31) / 32, nct = (P.N + 31) / 32, nitems = nrt * nct;
   const int as = P.Kp + 4;
@@ -384,6 +401,9 @@ __device__ __forceinline__ void gemm_phase(const TokPhase& P, float* lds, int G,
   const int kw = P.Kp / 4, kh = kw / 2, ngb = kh / 4;   // each wave's k range; per lane half; float4 groups
   const bool duty = P.amode != TOK_A_PLAIN || P.ln.y2;
   for (int it = blockIdx.x; it < nitems; it += G) {
+    lds_sync();   // As / red of the previous item are free: before any load of this item, so the B
+                       // loads, the epilogue operands and the staging loads are one round trip
+    tstamp(it == sit ? st : nullptr, 4);
     const int rt = it / nct, ct = it - rt * nct;
     const int r0 = rt * 32, n0 = ct * 32;
     const int n = n0 + (lane & 31), nc = min(n, P.N - 1);
@@ -405,41 +425,42 @@ __device__ __forceinline__ void gemm_phase(const TokPhase& P, float* lds, int G,
       eres[j] = ldc1(rp, (long long)mc * rld + nc);
       egate[j] = ldc1(gp, (long long)mc * gld + nc);
     }
-    tstamp(it == (int)blockIdx.x ? st : nullptr, 2);
-    ebias = P.bias ? ebias : 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      eres[j] = P.resid ? eres[j] : 0.f;
-      egate[j] = P.gate ? egate[j] : 1.f;
-    }
-    __syncthreads();   // As / red of the previous item are free
+    tstamp(it == sit ? st : nullptr, 2);
     stage_rows(P, r0, P.M, As, as, duty && n0 < P.K ? n0 : -1, P.apos && n0 < P.apos_ncols);
-    tstamp(it == (int)blockIdx.x ? st : nullptr, 3);
-    __syncthreads();
-    tstamp(it == (int)blockIdx.x ? st : nullptr, 4);
+    tstamp(it == sit ? st : nullptr, 3);
+    lds_sync();
     f32x16 acc;
     zero16(acc);
     if (P.btrans) mma_range<true>(As + (lane & 31) * as, P.w, P.ldw, nc, nok, P.K, kb, ngb, b, acc);
     else mma_range<false>(As + (lane & 31) * as, P.w, P.ldw, nc, nok, P.K, kb, ngb, b, acc);
     red_store(red, acc, w, lane);
-    tstamp(it == (int)blockIdx.x ? st : nullptr, 5);
-    __syncthreads();
-    tstamp(it == (int)blockIdx.x ? st : nullptr, 6);
+    tstamp(it == sit ? st : nullptr, 5);
+    lds_sync();
+    tstamp(it == sit ? st : nullptr, 6);
+    // this thread's 4 rows are consecutive: m0 + j (acc_row(4 w + j, lane))
+    const int m0 = r0 + acc_row(4 * w, lane);
+    unsigned km = ~0u;
+    if (P.drop_thr) {
+      km = 0;
+#pragma unroll 1
+      for (int j = 0; j < 4; ++j)
+        km |= (fx_drop_bits(P.drop_seed, (unsigned long long)(m0 + j) * P.N + n) >= P.drop_thr ? 1u : 0u) << j;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int r = 4 * w + j;
       float v = red_sum(red, r, lane);
       const int m = r0 + acc_row(r, lane);
       if (m >= P.M || !nok) continue;
-      v = v * P.alpha + ebias;
+      v = v * P.alpha + (P.bias ? ebias : 0.f);
       if (P.relu == 2) v = fmaxf(v, 0.f);
-      if (P.drop_thr) v *= keepf(P.drop_seed, P.drop_thr, P.drop_scale, (unsigned long long)m * P.N + n);
-      v += eres[j];
-      if (!(egate[j] > 0.f)) v = 0.f;
+      if (P.drop_thr) v *= kbit(km, j, P.drop_scale);
+      if (P.resid) v += eres[j];
+      if (P.gate && !(egate[j] > 0.f)) v = 0.f;
       if (P.relu == 1) v = fmaxf(v, 0.f);
       stc1(P.c, (long long)m * P.ldc + n, v);
     }
-    tstamp(it == (int)blockIdx.x ? st : nullptr, 7);
+    tstamp(it == sit ? st : nullptr, 7);
   }
 }
 
@@ -449,10 +470,7 @@ __device__ __forceinline__ void ln_phase(const TokPhase& P, int G) {
   for (int it = blockIdx.x; it < nrt; it += G) stage_rows(P, it * 32, P.M, nullptr, 0, DUTY_ALL, false);
 }
 
-// ------------------------------------------------------------------ 32 x 32 x 32 products in LDS
-// acc += A (32 x 32) B (32 x 32): A element (r, k) = ATR ? a[k * lda + r] : a[r * lda + k], B element (k, c) =
-// BTR ? b[c * ldb + k] : b[k * ldb + c]; lane half h takes k in [16 h, 16 h + 16) (any k order works as long
-// as A and B agree)
+// LDS 32 x 32 x 32 product on the matrix cores (wave-level): acc += A B, A / B row-major or transposed
 template <bool ATR, bool BTR>
 __device__ __forceinline__ void mm32s(const float* a, int lda, const float* b, int ldb, f32x16& acc, int lane) {
   const int li = lane & 31, kh = (lane >> 5) * 16;
@@ -471,7 +489,8 @@ __device__ __forceinline__ void mm32s(const float* a, int lda, const float* b, i
 // position, added in place: (x + p) computed once, as a staged x + p would be) for q_h and k_h; each
 // product K-split over the 4 waves with every B load issued up front; then S = scale q k^T and
 // O = P_d V on the matrix cores, the row softmax (probabilities saved before the dropout) in between.
-__device__ __forceinline__ void safwd_phase(const TokPhase& P, float* lds, int G) {
+__device__ __forceinline__ void safwd_phase(const TokPhase& P, float* lds, int G, unsigned long long* st) {
+  const int sit = (int)blockIdx.x + (st && st[7] == 3 ? G : 0);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nh = P.nh, Qv = P.Qv, A = P.K, nitems = P.nvid * nh;
   const int as = P.Kp + 4;
@@ -492,14 +511,20 @@ __device__ __forceinline__ void safwd_phase(const TokPhase& P, float* lds, int G
     // (v weights and the position fragments before the staging, q / k weights after it: registers)
     float4 bq[8], bk[8], bv[8], pq[8];
     const int prow = R0 + min(c, Qv - 1);
+    lds_sync();   // LDS of the previous item is free (before this item's loads)
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
       const long long k = min(kb + 4 * g, A - 4);
       bv[g] = ld4(P.w + (long long)(2 * A + h * 32 + c) * P.ldw + k);
       pq[g] = ld4((qpos ? P.apos + (long long)prow * P.ldpos : P.w) + k);
     }
-    __syncthreads();
+    const float* bp = P.bias ? P.bias : P.w;
+    float bb3[3];
+#pragma unroll
+    for (int mat = 0; mat < 3; ++mat) bb3[mat] = bp[mat * A + h * 32 + c];
+    tstamp(it == sit ? st : nullptr, 2);
     stage_rows(P, R0, R0 + Qv, As, as, P.amode == TOK_A_PLAIN && !P.ln.y2 ? -1 : h * 32, false);
+    tstamp(it == sit ? st : nullptr, 3);
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
       const long long k = min(kb + 4 * g, A - 4);
@@ -514,7 +539,7 @@ __device__ __forceinline__ void safwd_phase(const TokPhase& P, float* lds, int G
       bv[g] = ok ? bv[g] : zero4();
       pq[g] = (ok && qpos && c < Qv) ? pq[g] : zero4();
     }
-    __syncthreads();
+    lds_sync();
     f32x16 av, aq, ak;
     zero16(av);
     zero16(aq);
@@ -544,12 +569,13 @@ __device__ __forceinline__ void safwd_phase(const TokPhase& P, float* lds, int G
     red_store(red, aq, w, lane);
     red_store(red + 4096, ak, w, lane);
     red_store(red + 8192, av, w, lane);
-    __syncthreads();
+    tstamp(it == sit ? st : nullptr, 4);
+    lds_sync();
 #pragma unroll
     for (int mat = 0; mat < 3; ++mat) {
       float* dst = mat == 0 ? Qs : mat == 1 ? Ks : Vs;
       const int n = mat * A + h * 32 + c;
-      const float bb = P.bias ? P.bias[n] : 0.f;
+      const float bb = P.bias ? bb3[mat] : 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int r = 4 * w + j, row = acc_row(r, lane);
@@ -558,7 +584,7 @@ __device__ __forceinline__ void safwd_phase(const TokPhase& P, float* lds, int G
         if (row < Qv) P.qkv[(long long)(R0 + row) * 3 * A + n] = x;   // saved for the backward
       }
     }
-    __syncthreads();
+    lds_sync();
     if (w == 0) {   // S = scale q k^T
       f32x16 sacc;
       zero16(sacc);
@@ -566,8 +592,10 @@ __device__ __forceinline__ void safwd_phase(const TokPhase& P, float* lds, int G
 #pragma unroll
       for (int r = 0; r < 16; ++r) Ps[acc_row(r, lane) * HS + c] = sacc[r] * P.scale;
     }
-    __syncthreads();
+    lds_sync();
+    tstamp(it == sit ? st : nullptr, 5);
     float* probs = P.probs + (long long)v * nh * Qv * Qv;
+#pragma unroll 1
     for (int i = w; i < 32; i += 4) {
       const float x = (lane < Qv && i < Qv) ? Ps[i * HS + lane] : -INFINITY;
       const float mx = wmax(x);
@@ -584,7 +612,8 @@ __device__ __forceinline__ void safwd_phase(const TokPhase& P, float* lds, int G
       }
       if (lane < 32) Ps[i * HS + lane] = pd;
     }
-    __syncthreads();
+    lds_sync();
+    tstamp(it == sit ? st : nullptr, 6);
     if (w == 0) {   // O = P_d V
       f32x16 o;
       zero16(o);
@@ -595,6 +624,7 @@ __device__ __forceinline__ void safwd_phase(const TokPhase& P, float* lds, int G
         if (i < Qv) stc1(P.c, (long long)(R0 + i) * P.ldc + h * 32 + c, o[r]);
       }
     }
+    tstamp(it == sit ? st : nullptr, 7);
   }
 }
 
@@ -619,7 +649,7 @@ __device__ __forceinline__ void mhabwd_phase(const TokPhase& P, float* lds, int 
     const int v = it / nh, h = it - v * nh;
     const int R0 = v * Qv;
     const float* probs = P.probs + ((long long)v * nh + h) * Qv * Qv;
-    __syncthreads();
+    lds_sync();
     {   // the head's q, k, v, dO and P tiles: 4 elements per thread each, every load issued first (clamped)
       float q4[4], k4[4], v4[4], d4[4], p4[4];
 #pragma unroll
@@ -650,7 +680,7 @@ __device__ __forceinline__ void mhabwd_phase(const TokPhase& P, float* lds, int 
         Ms[i * HS + d] = kp;
       }
     }
-    __syncthreads();
+    lds_sync();
     if (w == 0) {   // dP = dO V^T (masked)
       f32x16 acc;
       zero16(acc);
@@ -675,7 +705,7 @@ __device__ __forceinline__ void mhabwd_phase(const TokPhase& P, float* lds, int 
         if (j < Qv) stc1(P.c, (long long)(R0 + j) * P.ldc + 2 * A + h * 32 + c, acc[r]);
       }
     }
-    __syncthreads();
+    lds_sync();
     // dS = P (dP - rowsum(P dP)) with the un-dropped P (Us: wave 1 turned Ps into P_d)
     for (int i = w; i < 32; i += 4) {
       const float p = lane < 32 ? Us[i * HS + lane] : 0.f;
@@ -683,7 +713,7 @@ __device__ __forceinline__ void mhabwd_phase(const TokPhase& P, float* lds, int 
       const float r = wsum(p * g);
       if (lane < 32) Gs[i * HS + lane] = p * (g - r);
     }
-    __syncthreads();
+    lds_sync();
     if (w < 2) {   // dq = scale dS K ; dk = scale dS^T q
       f32x16 acc;
       zero16(acc);
@@ -711,29 +741,46 @@ __global__ __launch_bounds__(TT) void tok_kernel(TokProgram prog) {
 #else
   const TokProgram* pk = &prog;
 #endif
+  // The phases go to LDS once (vector loads by the whole workgroup, one round trip), and each phase from
+  // there into registers, made wave-uniform (readfirstlane).  Read in place, the fields are scalar loads
+  // from the argument segment that the compiler re-issues wherever it runs short of scalar registers
+  // (rather than spilling them), and those reads are slow: chains of them cost microseconds per item.
+  static_assert(sizeof(TokPhase) % 4 == 0, "phase copy by words");
+  constexpr int kPW = (int)(sizeof(TokPhase) / 4);
+  __shared__ unsigned sph[TOK_MAXPH * kPW];
+  {
+    const unsigned* src = reinterpret_cast<const unsigned*>(pk->ph);
+    for (int i = threadIdx.x; i < prog.nphase * kPW; i += TT) sph[i] = src[i];
+  }
+  // diagnostic stamps (FX_TOK_DEBUG): kept in LDS (a global store at a phase start would put its
+  // write acknowledgement in front of the phase's first wait), written out at the end
+  __shared__ unsigned long long tst[TOK_MAXPH * 8];
+  if (prog.debug && threadIdx.x < TOK_MAXPH * 8) tst[threadIdx.x] = 0;
+  __syncthreads();
   for (int p = 0; p < prog.nphase; ++p) {
-    const TokPhase& P = pk->ph[p];
-    if (prog.debug && threadIdx.x == 0) {   // diagnostic (FX_TOK_DEBUG): phases entered, and the op seen
-      __hip_atomic_fetch_add(prog.status + 1 + (P.op & 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      prog.stamps[(blockIdx.x * TOK_MAXPH + p) * 8] = __builtin_amdgcn_s_memrealtime();
+    TokPhase P;
+    {
+      unsigned* dst = reinterpret_cast<unsigned*>(&P);
+#pragma unroll
+      for (int i = 0; i < kPW; ++i) dst[i] = __builtin_amdgcn_readfirstlane(sph[p * kPW + i]);
     }
-    if (prog.debug == 2) {   // diagnostic: run the phase once more first (warm instruction cache), timed in slot 7
-      if (P.op == TOK_GEMM) gemm_phase(P, lds, prog.G, nullptr);
-      else if (P.op == TOK_SAFWD) safwd_phase(P, lds, prog.G);
-      else if (P.op == TOK_MHABWD) mhabwd_phase(P, lds, prog.G);
-      else if (P.op == TOK_LNROWS) ln_phase(P, prog.G);
-      __syncthreads();
-      if (threadIdx.x == 0) prog.stamps[(blockIdx.x * TOK_MAXPH + p) * 8 + 2] = __builtin_amdgcn_s_memrealtime();
-    }
-    if (P.op == TOK_GEMM) gemm_phase(P, lds, prog.G, prog.debug == 1 ? prog.stamps + (blockIdx.x * TOK_MAXPH + p) * 8 : nullptr);
-    else if (P.op == TOK_SAFWD) safwd_phase(P, lds, prog.G);
+    unsigned long long* st = prog.debug ? tst + p * 8 : nullptr;
+    if (st && threadIdx.x == 0) st[7] = prog.debug;
+    __syncthreads();
+    tstamp(st, 0);
+    if (P.op == TOK_GEMM) gemm_phase(P, lds, prog.G, st);
+    else if (P.op == TOK_SAFWD) safwd_phase(P, lds, prog.G, st);
     else if (P.op == TOK_MHABWD) mhabwd_phase(P, lds, prog.G);
     else if (P.op == TOK_LNROWS) ln_phase(P, prog.G);
     if (prog.debug) {
       __syncthreads();
-      if (threadIdx.x == 0) prog.stamps[(blockIdx.x * TOK_MAXPH + p) * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+      tstamp(st, 1);
     }
     if (p + 1 < prog.nphase && !grid_sync(b, &dead)) return;
+  }
+  if (prog.debug) {
+    __syncthreads();
+    if (threadIdx.x < prog.nphase * 8) prog.stamps[blockIdx.x * TOK_MAXPH * 8 + threadIdx.x] = tst[threadIdx.x];
   }
   grid_exit(b, dead);
 }

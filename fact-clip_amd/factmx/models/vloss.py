@@ -104,8 +104,10 @@ def segment_weights(mc, transcript):
 def supported(net):
     """The fused phase covers FACT / FACT_CLIP without transcripts whose last block has token->frame
     attention (every reference config: the matching reads it).  A batch in which some video's matching
-    pairs more than FX_LOSS_MAXK columns makes run() raise TableTooLarge before any of its work is
-    enqueued, and the caller computes that batch's losses per video (loss.py's methods)."""
+    pairs more than FX_LOSS_MAXK columns makes run() raise TableTooLarge once the matching is known:
+    the per-frame predictions (fx_eval_pred) are already enqueued by then (they only read the network's
+    outputs and are recomputed by the fallback), but none of the loss launches is; the caller computes
+    that batch's losses per video (loss.py's methods)."""
     from .blocks import UpdateBlock, UpdateBlockTDU
     mc = getattr(net, "mcriterion", None)
     if mc is None or net.cfg.FACT.trans or net.cfg.Loss.match not in ("o2o", "o2m", "seq"):
