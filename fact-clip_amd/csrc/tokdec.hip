@@ -69,7 +69,19 @@ __device__ __forceinline__ void stc4(float* base, long long idx, float4 v) {
   v4f x = {v.x, v.y, v.z, v.w};
   __builtin_amdgcn_raw_buffer_store_b128(x, rsrc(base), (int)(idx * 4), 0, 16);
 }
-__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+// plain accesses to tensors written before the launch, as global-memory instructions (the phase fields
+// come through LDS, so the compiler cannot tell that their pointers are global and would emit flat ones)
+// (through the native vector type: float4's copy constructor would take the operand back to a generic
+// reference)
+typedef __attribute__((address_space(1))) const v4f gcf4;
+typedef __attribute__((address_space(1))) const float gcf1;
+typedef __attribute__((address_space(1))) float gf1;
+__device__ __forceinline__ float4 ld4(const float* p) {
+  const v4f v = *(gcf4*)(p);
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ float ld1(const float* p) { return *(gcf1*)(p); }
+__device__ __forceinline__ void st1(float* p, float v) { *(gf1*)(p) = v; }
 __device__ __forceinline__ float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
 __device__ __forceinline__ float4 zero4() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
@@ -203,7 +215,7 @@ __device__ __forceinline__ void stage_ln(const TokPhase& P, bool bwd, int r0, in
     gw[i] = ld4(P.ln.w + kc);
     pp[i] = ld4(ps + kc);
   }
-  const float rsb = bwd ? P.ln.rstd[mc] : 0.f;
+  const float rsb = bwd ? ld1(P.ln.rstd + mc) : 0.f;
 #pragma unroll
   for (int i = 0; i < NGL; ++i) {
     const int k = 4 * sub + 32 * i;
@@ -344,8 +356,8 @@ __device__ __forceinline__ void load_b(const float* W, long long ldw, int n, boo
     if (!BT) {
       b[g] = ld4(W + (long long)n * ldw + kc);
     } else {
-      b[g] = make_float4(W[(long long)kc * ldw + n], W[(long long)(kc + 1) * ldw + n], W[(long long)(kc + 2) * ldw + n],
-                         W[(long long)(kc + 3) * ldw + n]);
+      b[g] = make_float4(ld1(W + (long long)kc * ldw + n), ld1(W + (long long)(kc + 1) * ldw + n),
+                         ld1(W + (long long)(kc + 2) * ldw + n), ld1(W + (long long)(kc + 3) * ldw + n));
     }
   }
   // no zeroing: a clamped k >= K re-reads an in-range weight that meets a zero A column (As is zero for
@@ -412,13 +424,14 @@ __device__ __forceinline__ void gemm_phase(const TokPhase& P, float* lds, int G,
     float4 b[NGB];
     if (P.btrans) load_b<true>(P.w, P.ldw, nc, nok, P.K, kb, ngb, b);
     else load_b<false>(P.w, P.ldw, nc, nok, P.K, kb, ngb, b);
+    tstamp(it == sit ? st : nullptr, 6);
     // this thread's outputs: rows r0 + acc_row(4 w + j, lane), column n; their epilogue operands loaded
     // unconditionally (clamped; stand-ins for absent operands) beside the B loads
     const float* rp = P.resid ? P.resid : P.c;
     const long long rld = P.resid ? P.ldr : P.ldc;
     const float* gp = P.gate ? P.gate : P.c;
     const long long gld = P.gate ? P.ldg : P.ldc;
-    float ebias = (P.bias ? P.bias : P.w)[nc], eres[4], egate[4];
+    float ebias = ld1((P.bias ? P.bias : P.w) + nc), eres[4], egate[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int mc = min(r0 + acc_row(4 * w + j, lane), P.M - 1);
@@ -436,7 +449,6 @@ __device__ __forceinline__ void gemm_phase(const TokPhase& P, float* lds, int G,
     red_store(red, acc, w, lane);
     tstamp(it == sit ? st : nullptr, 5);
     lds_sync();
-    tstamp(it == sit ? st : nullptr, 6);
     // this thread's 4 rows are consecutive: m0 + j (acc_row(4 w + j, lane))
     const int m0 = r0 + acc_row(4 * w, lane);
     unsigned km = ~0u;
@@ -521,7 +533,7 @@ __device__ __forceinline__ void safwd_phase(const TokPhase& P, float* lds, int G
     const float* bp = P.bias ? P.bias : P.w;
     float bb3[3];
 #pragma unroll
-    for (int mat = 0; mat < 3; ++mat) bb3[mat] = bp[mat * A + h * 32 + c];
+    for (int mat = 0; mat < 3; ++mat) bb3[mat] = ld1(bp + mat * A + h * 32 + c);
     tstamp(it == sit ? st : nullptr, 2);
     stage_rows(P, R0, R0 + Qv, As, as, P.amode == TOK_A_PLAIN && !P.ln.y2 ? -1 : h * 32, false);
     tstamp(it == sit ? st : nullptr, 3);
@@ -581,7 +593,7 @@ __device__ __forceinline__ void safwd_phase(const TokPhase& P, float* lds, int G
         const int r = 4 * w + j, row = acc_row(r, lane);
         const float x = red_sum(red + mat * 4096, r, lane) + bb;
         dst[row * HS + c] = row < Qv ? x : 0.f;
-        if (row < Qv) P.qkv[(long long)(R0 + row) * 3 * A + n] = x;   // saved for the backward
+        if (row < Qv) st1(P.qkv + (long long)(R0 + row) * 3 * A + n, x);   // saved for the backward
       }
     }
     lds_sync();
@@ -603,7 +615,7 @@ __device__ __forceinline__ void safwd_phase(const TokPhase& P, float* lds, int G
       const float p = ex / wsum(ex);
       float pd = 0.f;
       if (lane < Qv && i < Qv) {
-        probs[((long long)h * Qv + i) * Qv + lane] = p;   // saved before the dropout (the backward redraws it)
+        st1(probs + ((long long)h * Qv + i) * Qv + lane, p);   // saved before the dropout (the backward redraws it)
         pd = p;
         if (P.attn_thr) {   // mha_small's mask: index (query_row * nh + h) * (nvid Qv) + key_row
           const unsigned long long qg = (unsigned long long)v * Qv + i, kg = (unsigned long long)v * Qv + lane;
@@ -657,11 +669,11 @@ __device__ __forceinline__ void mhabwd_phase(const TokPhase& P, float* lds, int 
         const int e = tid + u * TT, i = e >> 5, d = e & 31;
         const int ic = min(i, Qv - 1), dc = min(d, Qv - 1);
         const long long row = (long long)(R0 + ic) * 3 * A + h * 32 + d;
-        q4[u] = P.qkv[row];
-        k4[u] = P.qkv[row + A];
-        v4[u] = P.qkv[row + 2 * A];
+        q4[u] = ld1(P.qkv + row);
+        k4[u] = ld1(P.qkv + row + A);
+        v4[u] = ld1(P.qkv + row + 2 * A);
         d4[u] = ldc1(P.a, (long long)(R0 + ic) * P.lda + h * 32 + d);   // dO of the head
-        p4[u] = probs[ic * Qv + dc];
+        p4[u] = ld1(probs + ic * Qv + dc);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
