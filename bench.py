@@ -58,6 +58,15 @@ HOLDOUT = [51, 53, 61, 67, 56]   # havid_view0_lh_pt_holdout.yaml
 # query, key and value rows, the logit / probability tiles and the attended features (+ their gradients)
 X2Y_KINDS = {3: "x2y_a2f_fwd", 4: "x2y_a2f_bwd", 5: "x2y_f2a_fwd", 6: "x2y_f2a_bwd"}
 FRL_KIND = 7   # fx_prof kind of the fused MS-TCN layer kernel (mstcn_fused.hip)
+# fx_prof kinds of the cross-attention projection GEMMs (north-star measurement set)
+XATTN_KINDS = {9: "sca_kv_projection", 10: "x2y_projections"}
+XATTN_NOTES = {
+    "sca_kv_projection": ("SCA frame-memory K/V projection: every decoder layer's keys and values in one frame-level "
+                          "GEMM (basic.py:508-516 in-projection of the memory), gemm_f32 wide kernel",
+                          "r05_pmc_kvproj.json"),
+    "x2y_projections": ("X2Y_map input projections k, v (X rows) and q (Y rows) (basic.py:357-369), three GEMMs "
+                        "per call", "r05_pmc_x2yproj.json"),
+}
 X2Y_NOTES = {"x2y_a2f_fwd": "x2y_a2f_kernel<0> (frames attend to the action tokens: logit, attn, feat in one launch)",
              "x2y_a2f_bwd": "x2y_a2f_kernel<1> + grouped dxv / dxk GEMM launch",
              "x2y_f2a_fwd": "x2y_f2a_chunk_kernel + x2y_f2a_merge_kernel (tokens attend to the frames)",
@@ -335,6 +344,29 @@ def fused_layer_roofline(prof, peak):
                 bytes_per_launch=by.value / n)
 
 
+def gemm_roofline(name, ms, fl, by, cnt, peak):
+    """A cross-attention projection GEMM kind, MFMA-bound: algorithmic FLOPs over the HIP-event time of
+    its launches in the sampled step(s); `traffic` from a committed standalone PMC pass of the same shape."""
+    n = cnt.value
+    if n <= 0 or ms.value <= 0:
+        return None
+    note, pmc = XATTN_NOTES[name]
+    tf = fl.value / (ms.value * 1e-3) / 1e12
+    out = dict(kernel=note, bound="mfma", achieved=round(tf, 2), peak=round(peak, 1), unit="TFLOP/s",
+               frac=round(tf / peak, 4), launches=n, avg_launch_ms=round(ms.value / n, 5),
+               flops_per_launch=fl.value / n, bytes_per_launch=by.value / n,
+               hbm_gbs_algorithmic=round(by.value / (ms.value * 1e-3) / 1e9, 1))
+    path = os.path.join(ROOT, "profiles", pmc)
+    out["traffic"] = None
+    if os.path.exists(path):
+        try:
+            with open(path) as f:
+                out["traffic"] = json.load(f).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+    return out
+
+
 def cpu_baseline(wl, Ts, videos_seeds, min_seconds=10.0, min_steps=2):
     """The CPU oracle (fp32 PyTorch restatement pinned to the reference) timed on host cores: one
     video per step, full T, forward + prediction + loss + backward with FIXED weights (the same
@@ -494,7 +526,7 @@ def main():
     # capacity of each kind is its launch count in one step, counted on an untimed extra warm-up step,
     # times the sampled steps -- so no event pair spills into the later timed steps.
     psteps = min(args.steps, int(os.environ.get("FX_BENCH_PROF_STEPS", 1)))
-    kinds = [0, 1, 2] + list(X2Y_KINDS) + [FRL_KIND]
+    kinds = [0, 1, 2] + list(X2Y_KINDS) + [FRL_KIND] + list(XATTN_KINDS)
     for kind in kinds:
         native.check(lib.fx_prof_enable(kind, 4096), "fx_prof_enable")
     step()
@@ -521,6 +553,7 @@ def main():
     attn_prof = {name: collect(kind) for kind, name in ((1, "fwd"), (2, "bwd"))}
     x2y_prof = {name: collect(kind) for kind, name in X2Y_KINDS.items()}
     frl_prof = collect(FRL_KIND)
+    xattn_prof = {name: collect(kind) for kind, name in XATTN_KINDS.items()}
     lib.fx_prof_disable()
     S_after = video_segments(net)
     if world > 1:
@@ -633,6 +666,8 @@ def main():
                                 parallelism=f"dp{world}", weights="fixed (no optimizer update in the timed steps)",
                                 tdu_segments=S, tdu_segments_after_timing=S_after),
                     roofline=roofline, roofline_attention=roofline_attention,
+                    roofline_xattn_gemm={name: gemm_roofline(name, *v, F32_MFMA_PEAK_TFLOPS)
+                                         for name, v in xattn_prof.items()},
                     roofline_conv_gemm=conv_roofline, roofline_fused_layer=frl_roofline, train_step_with_adam=adam,
                     bf16_mode=bf16, dp_schedule=dp_sched)
         if other is not None:

@@ -30,8 +30,9 @@ struct ProfState {
   std::vector<int> launches;   // launches an event pair brackets (back-to-back chains: one pair)
   int used = 0;
 };
-constexpr int kProfKinds = 9;   // 0 conv GEMM, 1 / 2 attention over T fwd / bwd, 3-6 X2Y cores, 7 fused MS-TCN layer,
-                                // 8 persistent token-kernel launches (tokdec.hip)
+constexpr int kProfKinds = 11;  // 0 conv GEMM, 1 / 2 attention over T fwd / bwd, 3-6 X2Y cores, 7 fused MS-TCN layer,
+                                // 8 persistent token-kernel launches (tokdec.hip), 9 SCA frame-memory K/V projection
+                                // GEMM, 10 X2Y input projections (k, v, q)
 std::mutex g_prof_mu;
 ProfState g_prof[kProfKinds];
 
@@ -1666,9 +1667,13 @@ int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpo
     yin = saved + L.yin;
     ldyin = ydim;
   }
+  prof_begin(10, s);
   FX_TRY(linear_fwd(xin, ldxin, Nx, xdim, wk, bk, xk, Hd, Hd, 0, s));
   FX_TRY(linear_fwd(X, ldx, Nx, xdim, wv, bv, xv, Hd, Hd, 0, s));
   FX_TRY(linear_fwd(yin, ldyin, Ny, ydim, wq, bq, yq, Hd, Hd, 0, s));
+  // algorithmic: the input rows, weights and outputs of the three products once
+  prof_end(10, s, 2.0 * Hd * (2.0 * Nx * xdim + (double)Ny * ydim),
+           4.0 * (2.0 * Nx * xdim + (double)Ny * ydim + Hd * (2.0 * xdim + ydim) + Hd * (2.0 * Nx + Ny)), 3);
   const float scale = 1.0f / std::sqrt((float)Hd);
   // a short key side (the a2f map: <= 64 action tokens per video): the whole core in one launch
   const bool al16 =

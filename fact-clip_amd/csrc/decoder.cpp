@@ -701,14 +701,18 @@ int fx_decoder_fwd(const fx_decoder_params* p, const float* tgt, long long ldt, 
     hipLaunchKernelGGL(pack_kv_kernel, dim3(std::min(cdiv((long long)A * p->Hm, 256), 256), 2 * NL), dim3(256), 0, s,
                        pk);
     FX_CHECK_HIP(hipGetLastError());
+    // (profiling kind 9: the frame-level GEMM(s); algorithmic bytes = mem rows, packed weights, K/V rows)
+    prof_begin(9, s);
     if (!mpos) {
       FX_TRY(linear_fwd(mem, ldm, T, p->Hm, workspace + L.wkv, workspace + L.bkv, kv, AL2, AL2, 0, s));
+      prof_end(9, s, 2.0 * T * AL2 * p->Hm, 4.0 * ((double)T * p->Hm + (double)AL2 * p->Hm + (double)T * AL2));
     } else {
       const int AL = A * NL;
       FX_TRY(linear_fwd(mem, ldm, T, p->Hm, workspace + L.wkv, workspace + L.bkv, kv, AL2, AL, 0, s, -1, mpos, ldmp,
                         p->Hm));
       FX_TRY(linear_fwd(mem, ldm, T, p->Hm, workspace + L.wkv + (long long)AL * p->Hm, workspace + L.bkv + AL,
                         kv + AL, AL2, AL, 0, s));
+      prof_end(9, s, 2.0 * T * AL2 * p->Hm, 4.0 * (2.0 * T * p->Hm + (double)AL2 * p->Hm + (double)T * AL2), 2);
       // keep mem + pos for the key weight gradient
       FX_TRY(add2(mem, ldm, mpos, ldmp, T, p->Hm, saved + L.mpos, p->Hm, 0, s));
     }

@@ -718,7 +718,10 @@ int fx_get_default_precision(void);
  *   3-6 = X2Y cores (a2f fwd, a2f bwd, f2a fwd, f2a bwd),
  *   7 = fused MS-TCN layer (frl_kernel: conv + ReLU + 1x1 + residual forward,
  *       or the fused dX chain backward),
- *   8 = persistent token-kernel launches of the decoders (tokdec.hip programs).
+ *   8 = persistent token-kernel launches of the decoders (tokdec.hip programs),
+ *   9 = SCA frame-memory K/V projection GEMM (every layer's keys and values in one
+ *       frame-level product, M = frames, N = 2 d_model layers, K = memory width),
+ *   10 = X2Y input projections (k, v from X, q from Y: three products per call).
  * fx_prof_enable resets one kind; fx_prof_disable resets all.
  * ---------------------------------------------------------------------- */
 int fx_prof_enable(int kind, int max_events);
