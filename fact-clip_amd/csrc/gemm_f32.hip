@@ -79,6 +79,7 @@ struct GemmDev {
   int b_dil_growth;     // > 1: B's conv dilation of batch b is conv_dil * growth^b
   int xcd_planes;       // wide8: whole z-planes (batch x split-K slice) per XCD, see block_tile
   int row_perm;         // > 1: dilated-conv A shifting by row_perm row tiles: XCD runs follow the taps, see block_tile
+  int group_m;          // > 1: tiles in groups of group_m row tiles, column-major inside a group, see block_tile
   int a_dil_b1;         // > 0: A's conv dilation of batch 1 (two dilated convs of one input in one launch)
   long long bias_bs;    // bias of batch b at bias + b * bias_bs
   int nt_store;         // FX_GEMM_NTSTORE=1 (A/B): the fast epilogue stores non-temporally
@@ -598,6 +599,16 @@ __device__ __forceinline__ void block_tile(const GemmDev& g, int& tx, int& ty, i
   const int nid = (x8 < rr ? x8 * (q + 1) : rr * (q + 1) + (x8 - rr) * q) + i8;
   ty = nid / g.tiles_x;
   tx = nid - ty * g.tiles_x;
+  if (g.group_m > 1) {
+    // a large B: in row-major order the 32 tiles an XCD runs at once span one row tile and every column
+    // tile, so each row tile re-streams all of B through the XCD's L2.  Groups of group_m row tiles (one
+    // XCD run), walked column by column: the tiles in flight share a few B columns and the group's A rows
+    // (both L2-resident), so B is fetched about once per XCD
+    const int gsz = g.group_m * g.tiles_x, grp = nid / gsz, r = nid - grp * gsz;
+    const int rows = min(g.group_m, g.tiles_y - grp * g.group_m);
+    ty = grp * g.group_m + r % rows;
+    tx = r / rows;
+  }
   if (g.row_perm > 1) {
     // a dilated conv whose taps shift by row_perm whole row tiles: the XCD runs walk the row tiles in
     // the order 0, p, 2p, ..., 1, 1 + p, ... so the tiles holding a tile's shifted rows sit next to it in
@@ -2159,6 +2170,15 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
   if (knobs().gemm_row_perm && wide && !g.xcd_planes && d.a.conv_taps > 1 && !d.a.trans && d.a_dil_b1 <= 0) {
     const int sh = d.a.conv_dil / WBM;
     if (sh > 1 && g.tiles_y % sh == 0) g.row_perm = sh;
+  }
+  // FX_GEMM_GROUPM=0: plain row-major tile runs (A/B).  Grouped order when B does not fit an XCD's L2
+  // share (> 2 MB) but one XCD run of A rows does (<= 2 MB), plain operands only
+  g.group_m = 0;
+  if (knobs().gemm_group_m && !g.xcd_planes && g.row_perm <= 1 && d.a.conv_taps <= 1 && d.b.conv_taps <= 1 &&
+      g.tiles_y >= 16 && g.tiles_x >= 8) {
+    const int gm = g.tiles_y / 8, tm = wide ? WBM : BM;
+    const double b_bytes = 4.0 * d.N * d.K, a_run = 4.0 * gm * tm * d.K;
+    if (b_bytes > 2.0 * (1 << 20) && a_run <= 2.0 * (1 << 20)) g.group_m = gm;
   }
   g.nt_store = knobs().gemm_nt_store ? 1 : 0;
   P.grid = grid;
