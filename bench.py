@@ -294,12 +294,14 @@ def dp_schedule_overhead(net, seqs, labels, steps, rounds=3):
         for _ in range(rounds):
             plain.append(timed(False))
             forced.append(timed(True))
-        early = list(dp.hook_launched)
+        early = [k if isinstance(k, int) else f"{k[0]}.{k[1]}" for k in dp.hook_launched]
         pm, fm = statistics.median(plain), statistics.median(forced)
         return dict(dp_schedule_overhead_ms=round(fm - pm, 3), plain_ms_per_step=[round(v, 3) for v in plain],
                     forced_ms_per_step=[round(v, 3) for v in forced], backend=dist.get_backend(),
                     buckets_per_step=sum(len(b) for b in dp.block_buckets.values()) + len(dp.rest_buckets),
                     hook_launched_blocks=early,
+                    dp_tail_mb=round(dp.tail_bytes / 2 ** 20, 2),
+                    dp_total_mb=round(dp.flat.numel() * dp.flat.element_size() / 2 ** 20, 2),
                     note="world-size-1 nccl (RCCL) group, DataParallel(force_buckets=True): every block's bucket "
                          "all-reduced (AVG) from its backward hook; median of alternating rounds")
     finally:

@@ -119,6 +119,19 @@ def mark_block_input(net, k, x):
     dp._arm(k, x)
 
 
+def mark_block_part(net, k, name, x):
+    """Called by block k's forward with a tensor x that only sub-module `name` of the block (and what
+    follows it) consumes -- e.g. the input block's frame-branch output, read by its action branch: once
+    autograd has produced x's gradient, every kernel of `name`'s backward has been enqueued, so that
+    part of block k's bucket launches right there instead of with the rest of the block.  Needed where
+    the block's own input has no gradient (the first block reads the data), so its bucket would
+    otherwise wait for the end of the backward."""
+    dp = getattr(net, "_fx_dp", None)
+    if dp is None or not dp.active or not torch.is_grad_enabled() or not torch.is_tensor(x) or not x.requires_grad:
+        return
+    dp._arm_part(k, name, x)
+
+
 class DataParallel:
     """Whole-video data parallelism for FACT / FACT_CLIP (or any module with a ``block_list``).
 
@@ -156,14 +169,52 @@ class DataParallel:
                 ranges[k] = (lo, off + p.numel())
             off += p.numel()
         per = max(1, int(bucket_mb * (1 << 20) // 4))
-        self.block_buckets = {k: [self.flat[i:min(i + per, hi)] for i in range(lo, hi, per)]
-                              for k, (lo, hi) in ranges.items()}
-        # everything outside the blocks (action queries, CLIP projection head): the tail buckets
+
+        def cut(lo, hi):
+            return [self.flat[i:min(i + per, hi)] for i in range(lo, hi, per)]
+
+        def span(prefix):
+            """[lo, hi) of the parameters named prefix.* (contiguous in parameter order), or None."""
+            lo = hi = None
+            off = 0
+            for n, p in named:
+                if n.startswith(prefix + "."):
+                    if lo is None:
+                        lo = off
+                    elif hi != off:
+                        raise RuntimeError(f"{prefix} parameters are not contiguous in parameter order")
+                    hi = off + p.numel()
+                off += p.numel()
+            return None if lo is None else (lo, hi)
+
+        # parts of a block launched by their own hook (mark_block_part): the sub-modules the block lists
+        # in dp_parts; the block's bucket keeps the rest of its range
+        blocks = list(getattr(net, "block_list", []))
+        self.part_buckets = {}
+        self.block_buckets = {}
+        for k, (lo, hi) in ranges.items():
+            cuts = []
+            for name in getattr(blocks[k], "dp_parts", ()) if k < len(blocks) else ():
+                sp = span(f"block_list.{k}.{name}")
+                if sp is not None:
+                    self.part_buckets[(k, name)] = cut(*sp)
+                    cuts.append(sp)
+            rem, cur = [], lo
+            for a, b in sorted(cuts) + [(hi, hi)]:
+                rem += cut(cur, a)
+                cur = b
+            self.block_buckets[k] = rem
+        # everything outside the blocks (action queries, CLIP projection head): the tail buckets, except
+        # the modules the model lists in dp_head_modules -- used only after the last block, so their
+        # gradients are final once the backward is under way: they go with the first hook that fires
+        heads = [sp for sp in (span(n) for n in getattr(net, "dp_head_modules", ())) if sp is not None]
         rest, cur = [], 0
-        for lo, hi in sorted(ranges.values()) + [(self.flat.numel(), self.flat.numel())]:
-            rest += [self.flat[a:min(a + per, lo)] for a in range(cur, lo, per)]
+        for lo, hi in sorted(list(ranges.values()) + heads) + [(self.flat.numel(), self.flat.numel())]:
+            rest += cut(cur, lo)
             cur = hi
         self.rest_buckets = rest
+        self.head_buckets = [b for sp in heads for b in cut(*sp)]
+        self.tail_bytes = 0          # bytes finish_gradients reduced (after the backward), last step
         self.nblk = nblk
         self._pending = []
         self._launched = set()
@@ -202,6 +253,7 @@ class DataParallel:
         self._launched = set()
         self.hook_launched = []
         self._armed = {}
+        self._heads_out = False
         self._calls += 1
         if self._calls % 64 == 0:
             _check_views(self.params, self.flat)
@@ -218,10 +270,25 @@ class DataParallel:
             self._armed[k] = self._armed.get(k, 0) + 1
             x.register_hook(lambda g, k=k: self._fired(k))
 
+    def _arm_part(self, k, name, x):
+        key = (k, name)
+        if key in self._launched:
+            raise RuntimeError("factmx DataParallel: each step must be zero_grad(), one forward + backward, "
+                               "finish_gradients()")
+        if key in self.part_buckets:
+            self._armed[key] = self._armed.get(key, 0) + 1
+            x.register_hook(lambda g, key=key: self._fired(key))
+
     def _fired(self, k):
         self._armed[k] -= 1
         if self._armed[k] == 0:
+            self._launch_heads()
             self._launch_block(k, True)
+
+    def _launch_heads(self):
+        if not getattr(self, "_heads_out", False):
+            self._heads_out = True
+            self._issue(self.head_buckets)
 
     def _issue(self, buckets):
         """All-reduce `buckets` from the collective stream once everything enqueued so far on the
@@ -298,12 +365,13 @@ class DataParallel:
             self._pending.append((dist.all_reduce(st, op=dist.ReduceOp.MAX, group=self.group, async_op=True), False))
 
     def _launch_block(self, k, from_hook=False):
+        """k: a block index (its bucket less its parts) or a (block, part) key."""
         if not self.active or k in self._launched:
             return
         self._launched.add(k)
         if from_hook:
             self.hook_launched.append(k)
-        self._issue(self.block_buckets.get(k, []))
+        self._issue(self.part_buckets.get(k, []) if isinstance(k, tuple) else self.block_buckets.get(k, []))
 
     def finish_gradients(self):
         """Launch the buckets no hook has launched and make the current stream wait for all of them."""
@@ -313,9 +381,17 @@ class DataParallel:
         # CLIP head): adjacent slices of the flat buffer are merged into one collective
         left = [b for k in sorted(self.block_buckets, reverse=True) if k not in self._launched
                 for b in self.block_buckets[k]]
+        left += [b for key in sorted(self.part_buckets, reverse=True) if key not in self._launched
+                 for b in self.part_buckets[key]]
+        if not getattr(self, "_heads_out", False):
+            left += self.head_buckets
+            self._heads_out = True
         self._launched.update(self.block_buckets)
+        self._launched.update(self.part_buckets)
         fxf.side_join()           # (the backward's end-of-pass callback has normally joined already)
-        self._issue(_merge_adjacent(left + list(self.rest_buckets)))
+        tail = _merge_adjacent(left + list(self.rest_buckets))
+        self.tail_bytes = sum(b.numel() * b.element_size() for b in tail)
+        self._issue(tail)
         self._issue_status()
         if self._q is not None:
             self._q.join()        # every collective has been issued (the helper thread is idle)

@@ -12,7 +12,7 @@ import torch.nn as nn
 
 from .. import functional as fxf
 from ..configs.utils import update_from
-from ..dp import mark_block_input
+from ..dp import mark_block_input, mark_block_part
 from ..utils import utils
 from . import basic
 from . import loss as loss_mod
@@ -178,6 +178,15 @@ def _frame_branch_batch(branch, f, vb):
 class InputBlock(Block):
     """blocks.py:284-320."""
 
+    # data parallelism: the action branch's gradient bucket launches from a hook on the frame-branch
+    # output (the block's own input is the data: no gradient, no block hook), factmx.dp.mark_block_part
+    dp_parts = ("action_branch",)
+
+    def _dp_mark(self, f):
+        ctx = self.__dict__.get("_dp_ctx")
+        if ctx is not None:
+            mark_block_part(ctx[0], ctx[1], "action_branch", f)
+
     def __init__(self, cfg, in_dim, nclass):
         super().__init__()
         self.cfg = cfg
@@ -188,6 +197,7 @@ class InputBlock(Block):
 
     def forward(self, frame_feature, action_feature, frame_pos, action_pos, action_clogit=None):
         frame_feature = self.frame_branch(frame_feature)
+        self._dp_mark(frame_feature)
         frame_feature, frame_clogit = self.process_feature(frame_feature, self.nclass)
         action_feature = self.action_branch(action_feature, frame_feature, pos=frame_pos, query_pos=action_pos)
         action_feature, action_clogit = self.process_feature(action_feature, self.nclass + 1)
@@ -200,6 +210,7 @@ class InputBlock(Block):
         """``forward`` over vb.nvid stacked videos (frames (nvid*T, C), tokens (nvid*Q, A));
         per-video side-channel attributes go to ``self._vrec``."""
         f = _frame_branch_batch(self.frame_branch, f2, vb)
+        self._dp_mark(f)
         f_out, f_cl = fxf.process_feature(f, self.nclass)
         a = fxf.decoder(self.action_branch, a2, f_out, pos=fpos, query_pos=apos, nvid=vb.nvid,
                         mem_off=vb.f_off if vb.ragged else None)
@@ -486,6 +497,7 @@ class _FACTBase(nn.Module):
         block_output = []
         for k, block in enumerate(self.block_list):
             mark_block_input(self, k, frame_feature)
+            block.__dict__["_dp_ctx"] = (self, k)      # (not a submodule registration)
             frame_feature, action_feature = block(frame_feature, action_feature, frame_pe, action_pe)
             block_output.append([frame_feature, action_feature])
         return block_output
@@ -513,6 +525,7 @@ class _FACTBase(nn.Module):
         a2 = torch.zeros_like(apos)
         for k, blk in enumerate(self.block_list):
             mark_block_input(self, k, f2)       # DP: block k's gradient bucket launches once f2 has its grad
+            blk.__dict__["_dp_ctx"] = (self, k)
             f2, a2 = blk.forward_batch(f2, a2, fpos, apos, vb)
         proj = None
         if isinstance(self, FACT_CLIP):
@@ -563,6 +576,10 @@ class FACT(_FACTBase):
 
 class FACT_CLIP(_FACTBase):
     """blocks.py:504-920: FACT + CLIP projection head + InfoNCE; zero-shot eval via text similarity."""
+
+    # data parallelism: the projection head reads only the last block's output, so its gradients are
+    # final once the backward is under way -- reduced with the first block bucket (factmx.dp)
+    dp_head_modules = ("frame_projection",)
 
     def __init__(self, cfg, in_dim, n_classes, text_embeddings=None):
         super().__init__()

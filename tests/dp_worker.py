@@ -48,11 +48,13 @@ def main():
         dp.zero_grad()
         loss, _ = net(seqs, labs, compute_loss=True)
         loss.backward()
-        early = list(dp.hook_launched)
+        # a block part (k, name) as -1 - k
+        early = [k if isinstance(k, int) else -1 - k[0] for k in dp.hook_launched]
         dp.finish_gradients()
         torch.cuda.synchronize()
         np.savez(os.path.join(args.out, f"rank{rank}.npz"), flat=dp.flat.detach().cpu().numpy(),
                  early=np.asarray(early, dtype=np.int64), nblk=np.int64(len(net.block_list)),
+                 tail=np.int64(dp.tail_bytes),
                  wsum=np.asarray([float(wsum.sum()), float((wsum * wsum).sum())]),
                  loss=np.float64(loss.item()), S=np.asarray(bench.video_segments(net), dtype=np.int64))
     finally:

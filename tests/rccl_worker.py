@@ -65,7 +65,9 @@ def main():
             dp.active = active
             loss = step()
             torch.cuda.synchronize()
-            return dp.flat.detach().cpu().numpy().copy(), float(loss.item()), list(dp.hook_launched)
+            # (a block part (k, name) as -1 - k)
+            return (dp.flat.detach().cpu().numpy().copy(), float(loss.item()),
+                    [k if isinstance(k, int) else -1 - k[0] for k in dp.hook_launched])
 
         run(False)                         # warm-up (allocator, matching caches)
         plain1, loss1, _ = run(False)
@@ -87,6 +89,7 @@ def main():
             forced_ms.append(timed(True, args.time_steps))
         np.savez(os.path.join(args.out, "rccl.npz"), plain1=plain1, plain2=plain2, forced=forced,
                  early=np.asarray(early, dtype=np.int64), nblk=np.int64(len(net.block_list)),
+                 tail=np.int64(dp.tail_bytes),
                  loss=np.asarray([loss1, loss2, loss3]))
         with open(os.path.join(args.out, "rccl.json"), "w") as f:
             json.dump(dict(plain_ms=plain_ms, forced_ms=forced_ms, backend=dist.get_backend(),

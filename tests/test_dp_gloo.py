@@ -15,7 +15,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from factmx.dp import DataParallel, FlatGradReducer, mark_block_input
+from factmx.dp import DataParallel, FlatGradReducer, mark_block_input, mark_block_part
 
 
 def _free_port():
@@ -138,6 +138,87 @@ def test_data_parallel_hooks_broadcast_and_mean(tmp_path):
     vids = _videos()
     loss = sum(net(x).pow(2).mean() for x in vids) / len(vids)
     loss.backward()
+    for n, p in net.named_parameters():
+        torch.testing.assert_close(got["grads"][n], p.grad, rtol=1e-5, atol=1e-7)
+
+
+class _ToyInputBlock(torch.nn.Module):
+    """A first block whose input is the data: part `b` reads only the output of part `a`
+    (InputBlock: the action branch reads the frame branch's output)."""
+    dp_parts = ("b",)
+
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Linear(12, 12)
+        self.b = torch.nn.Linear(12, 12)
+
+    def forward(self, h):
+        f = torch.tanh(self.a(h))
+        ctx = self.__dict__.get("_dp_ctx")
+        if ctx is not None:
+            mark_block_part(ctx[0], ctx[1], "b", f)
+        return torch.tanh(self.b(f)) + f
+
+
+class _ToyParts(torch.nn.Module):
+    """_ToyBlocks with a first block split in two parts and a head applied after the last block (the
+    CLIP projection), registered BEFORE the blocks so its slice is not adjacent to theirs."""
+    dp_head_modules = ("head",)
+
+    def __init__(self, seed=0):
+        super().__init__()
+        torch.manual_seed(seed)
+        self.q = torch.nn.Parameter(torch.randn(12) * 0.1)
+        self.head = torch.nn.Linear(5, 3)
+        self.block_list = torch.nn.ModuleList([_ToyInputBlock(), torch.nn.Linear(12, 12), torch.nn.Linear(12, 5)])
+
+    def forward(self, x):
+        h = x
+        for k, b in enumerate(self.block_list):
+            mark_block_input(self, k, h)
+            b.__dict__["_dp_ctx"] = (self, k)
+            h = torch.tanh(b(h + (self.q if h.shape[-1] == 12 else 0)))
+        return self.head(h)
+
+
+def _parts_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        net = _ToyParts(seed=rank)
+        dp = DataParallel(net, bucket_mb=0.0002)
+        mine = _videos()[rank::world]
+        for step in range(2):
+            dp.zero_grad()
+            loss = sum(net(x).pow(2).mean() for x in mine) / len(mine)
+            issued = []
+            orig = dp._issue
+            dp._issue = lambda bs, orig=orig: (issued.append(sum(b.numel() for b in bs)), orig(bs))[1]
+            loss.backward()
+            early = [str(k) for k in dp.hook_launched]
+            dp.finish_gradients()
+            dp._issue = orig
+        if rank == 0:
+            torch.save({"grads": {n: p.grad.clone() for n, p in net.named_parameters()}, "early": early,
+                        "issued": issued, "tail": dp.tail_bytes}, out_path)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_part_and_head_buckets(tmp_path):
+    out = str(tmp_path / "dpp.pt")
+    mp.spawn(_parts_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    # hooks in backward order: block 2, block 1, then block 0's part b from the hook on part a's output
+    assert got["early"] == ["2", "1", "(0, 'b')"]
+    # the head (5x3 + 3) goes out with the first hook, before block 2's bucket
+    assert got["issued"][0] == 5 * 3 + 3 and got["issued"][1] == 12 * 5 + 5
+    # left for finish_gradients: block 0's part a and the shared queries only (+ the status word: none
+    # on gloo/CPU)
+    assert got["tail"] == 4 * ((12 * 12 + 12) + 12)
+    net = _ToyParts(seed=0)
+    vids = _videos()
+    (sum(net(x).pow(2).mean() for x in vids) / len(vids)).backward()
     for n, p in net.named_parameters():
         torch.testing.assert_close(got["grads"][n], p.grad, rtol=1e-5, atol=1e-7)
 

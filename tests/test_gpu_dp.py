@@ -58,10 +58,14 @@ def test_dp_two_ranks_equal_single_process_lockstep(tmp_path):
     np.testing.assert_array_equal(rk[0]["wsum"], rk[1]["wsum"])
     # all-reduce: identical gradients on both ranks
     np.testing.assert_array_equal(rk[0]["flat"], rk[1]["flat"])
-    # buckets from hooks, in backward order (block 0's input is the data: launched at finish)
+    # buckets from hooks, in backward order: blocks nblk-1 .. 1 from their input hooks, then block 0's
+    # action branch (-1) from the hook on its frame-branch output; block 0's frame branch (its input is
+    # the data) and the action queries at finish: the un-overlapped tail stays under 16 MB (the whole
+    # gradient is ~100 MB)
     nblk = int(rk[0]["nblk"])
     for r in rk:
-        assert r["early"].tolist() == list(range(nblk - 1, 0, -1)), r["early"]
+        assert r["early"].tolist() == list(range(nblk - 1, 0, -1)) + [-1], r["early"]
+        assert 0 < int(r["tail"]) <= 16 * 2 ** 20, int(r["tail"])
     # single process, the same 4 videos in one lockstep batch, seed-0 weights (= rank 0's)
     dev = torch.device("cuda", 0)
     cfg = bench.make_cfg()

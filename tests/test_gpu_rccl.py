@@ -36,5 +36,7 @@ def test_rccl_world1_bucket_schedule_bitwise(tmp_path):
     np.testing.assert_array_equal(r["forced"], r["plain1"])          # AVG over one rank == identity
     assert r["loss"][0] == r["loss"][1] == r["loss"][2]
     nblk = int(r["nblk"])
-    # block buckets from the hooks, last block first (block 0's input is the data: launched at finish)
-    assert r["early"].tolist() == list(range(nblk - 1, 0, -1)), r["early"]
+    # block buckets from the hooks, last block first, then block 0's action branch (-1) from the hook on
+    # its frame-branch output; block 0's frame branch (its input is the data) at finish: <= 16 MB
+    assert r["early"].tolist() == list(range(nblk - 1, 0, -1)) + [-1], r["early"]
+    assert 0 < int(r["tail"]) <= 16 * 2 ** 20, int(r["tail"])
