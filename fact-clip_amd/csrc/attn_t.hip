@@ -139,6 +139,8 @@ struct TAttnArgs {
   unsigned drop_thr;
   unsigned long long drop_seed;
   long long ktot;                       // key rows over all videos (mask index stride)
+  unsigned* cnt;                        // register-resident kernels: arrival counters per (video, head) for the
+                                        // in-launch merge (null: partials for tattn_merge_kernel)
   int koff[MAXV + 1];                   // key / value rows of video v: [koff[v], koff[v+1])
 };
 
@@ -540,6 +542,358 @@ __global__ __launch_bounds__(AT) void tattn_bwd_kernel(TAttnArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ register-resident kernels (hd 32)
+// For head dim 32 and <= 32 queries per video (the benchmark's SCA decoder: 8 heads of 32, 32 tokens)
+// every operand goes straight from memory into MFMA registers, no LDS staging:
+//   * S^T (keys x queries) = K q^T: lane (li, lh) feeds K[key li][16 lh .. 16 lh + 15] and
+//     q[query li][16 lh ..] as A / B (4 float4 each; the d order inside the sum is free as long as A and
+//     B agree);
+//   * the S^T accumulators hold, per lane, 16 keys of ONE query (keys acc_row(r)): the softmax statistics
+//     are in-register reductions plus one exchange with the other lane half;
+//   * O^T (d x queries) = V^T P^T takes the probabilities straight from those accumulators as the B
+//     operand, the key of MFMA step j being acc_row(j) -- V[key acc_row(j)][d li] as the A operand (32
+//     lanes read one 128-B row slice);
+//   * each wave owns 32 KT keys of the chunk; the 4 waves' (m, l, O) are combined through LDS once.
+// Backward: S^T and dP^T = V dO^T the same way, dq = dS K with dS^T from the accumulators as the A
+// operand; dV = P_d^T dO and dK = scale dS^T q need the probabilities with the key as the ROW index, so
+// P_d^T and dS^T go through a wave-private LDS tile (no workgroup barrier).
+__device__ __forceinline__ float4 ld4g(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// write-through (sc1) accesses of the in-launch merge: L1 bypassed, stores written through (the b32
+// buffer forms move the float's bits)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ float ldc1(const float* base, long long idx) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc(base), (int)(idx * 4), 0, 16));
+}
+__device__ __forceinline__ void stc1(float* base, long long idx, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc(base), (int)(idx * 4), 0, 16);
+}
+constexpr int FOLD_MAX = 16;   // chunks per video merged inside the launch (more: tattn_merge_kernel)
+
+// The chunk partials of (video, head) merged by the LAST workgroup to finish one (the microarch guide's
+// write-through hand-off, valid form 1): every workgroup stored its 32 x 32 partial (and forward: row
+// max / sum) with sc1 stores and waited for their acknowledgement before its arrival on the counter; the
+// last arriver re-arms the counter and reads the partials with sc1 loads, in chunk order (deterministic,
+// the same order as tattn_merge).  Forward (stats): o = sum_s e^(m_s - M) O_s / L, lse = M + log L;
+// backward: dq = mul sum_s dq_s.  Returns after the merge (or at once for the other workgroups).
+__device__ __forceinline__ void fold_merge(const TAttnArgs& a, int vid, int h, int ns, bool stats, float mul,
+                                           long long qrow, float (*wm)[32], float (*wl)[32], int* last) {
+  const int tid = threadIdx.x;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's partial stores acknowledged
+  __syncthreads();
+  if (tid == 0) {
+    unsigned* c = a.cnt + (long long)vid * a.nh + h;
+    const unsigned prev = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *last = prev == (unsigned)ns - 1;
+    if (*last) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!*last) return;
+  const long long pbase = ((long long)vid * a.nh + h) * a.nsplit;
+  const float* part = a.ws;
+  const float* pm = a.ws + (long long)gridDim.z * a.nh * a.nsplit * 32 * 32;
+  const float* pl = pm + (long long)gridDim.z * a.nh * a.nsplit * 32;
+  // every load of the merge at once: this thread's 4 (query, d) elements of every partial, and (forward)
+  // the row statistics of (partial, query) pairs tid, tid + 256
+  float x[4][FOLD_MAX];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = tid + i * AT;
+#pragma unroll
+    for (int sp = 0; sp < FOLD_MAX; ++sp) x[i][sp] = ldc1(part, (pbase + min(sp, ns - 1)) * 1024 + e);
+  }
+  if (stats) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + i * AT, sp = e >> 5, q = e & 31;
+      const float m = ldc1(pm, (pbase + min(sp, ns - 1)) * 32 + q), l = ldc1(pl, (pbase + min(sp, ns - 1)) * 32 + q);
+      if (sp < ns) {
+        wm[sp][q] = m;
+        wl[sp][q] = l;
+      }
+    }
+    __syncthreads();
+    if (tid < 32) {
+      float M = -INFINITY;
+      for (int sp = 0; sp < ns; ++sp) M = fmaxf(M, wm[sp][tid]);
+      float L = 0.f;
+      for (int sp = 0; sp < ns; ++sp) L += __expf(wm[sp][tid] - M) * wl[sp][tid];
+      const float inv = 1.f / L;
+      for (int sp = 0; sp < ns; ++sp) wm[sp][tid] = __expf(wm[sp][tid] - M) * inv;
+      if (tid < a.Qv) a.lse[((long long)vid * a.nh + h) * a.qs + a.q0 + tid] = M + __logf(L);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = tid + i * AT, q = e >> 5, d = e & 31;
+    float acc = 0.f;
+#pragma unroll
+    for (int sp = 0; sp < FOLD_MAX; ++sp)
+      if (sp < ns) acc += (stats ? wm[sp][q] : 1.f) * x[i][sp];
+    if (q < a.Qv) a.out[(qrow + q) * a.ld_out + h * 32 + d] = acc * mul;
+  }
+}
+
+template <int KT>
+__global__ __launch_bounds__(AT) void tattn_fwd32_kernel(TAttnArgs a) {
+  __shared__ float xo[4][32][33];   // per-wave O^T partial [d][query]
+  __shared__ float xm[4][32], xl[4][32];
+  const int c = blockIdx.x, h = blockIdx.y, vid = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 31, lh = lane >> 5;
+  const int Tv = a.koff[vid + 1] - a.koff[vid];
+  const int t0 = c * a.Tc, nk = min(a.Tc, Tv - t0);
+  if (nk <= 0) return;
+  const long long qrow = (long long)vid * a.qs + a.q0, krow = (long long)a.koff[vid] + t0;
+  const int kw0 = w * 32 * KT;
+  // every load first: q and K fragments, V columns
+  float4 qf[4], kf[KT][4];
+  float vf[KT][16];
+  {
+    const float* qp = a.q + (qrow + min(li, a.Qv - 1)) * a.ldq + h * 32 + 16 * lh;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) qf[q] = ld4g(qp + 4 * q);
+#pragma unroll
+    for (int u = 0; u < KT; ++u) {
+      const float* kp = a.k + (krow + min(kw0 + 32 * u + li, nk - 1)) * a.ldk + h * 32 + 16 * lh;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) kf[u][q] = ld4g(kp + 4 * q);
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        vf[u][j] = a.v[(krow + min(kw0 + 32 * u + acc_row(j, lane), nk - 1)) * a.ldv + h * 32 + li];
+    }
+  }
+  f32x16 st[KT];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < KT; ++u) {
+    zero16(st[u]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      st[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[u][q].x, qf[q].x, st[u], 0, 0, 0);
+      st[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[u][q].y, qf[q].y, st[u], 0, 0, 0);
+      st[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[u][q].z, qf[q].z, st[u], 0, 0, 0);
+      st[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[u][q].w, qf[q].w, st[u], 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kw0 + 32 * u + acc_row(r, lane);
+      st[u][r] = key < nk ? st[u][r] * a.scale : -INFINITY;
+      mx = fmaxf(mx, st[u][r]);
+    }
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float l = 0.f;
+  f32x16 ou[KT];   // one P V accumulator per key tile: independent MFMA chains, summed after
+#pragma unroll
+  for (int u = 0; u < KT; ++u) {
+    zero16(ou[u]);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = mx == -INFINITY ? 0.f : __expf(st[u][r] - mx);   // (a wave past the video's keys)
+      l += p;                                                         // the normaliser sees every key
+      float kp = 1.f;
+      if (a.drop_p > 0.f && p != 0.f) kp = drop_keep(a, qrow + li, h, krow + kw0 + 32 * u + acc_row(r, lane));
+      st[u][r] = p * kp;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) ou[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(vf[u][j], st[u][j], ou[u], 0, 0, 0);
+  }
+  f32x16 o = ou[0];
+#pragma unroll
+  for (int u = 1; u < KT; ++u) o += ou[u];
+  l += __shfl_xor(l, 32, 64);
+  if (lane < 32) {
+    xm[w][li] = mx;
+    xl[w][li] = l;
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) xo[w][acc_row(r, lane)][li] = o[r];
+  __syncthreads();
+  // the 4 waves' partials, in wave order; thread -> (query q, d) pairs
+  const long long pid = ((long long)vid * a.nh + h) * a.nsplit + c;
+  float* pm = a.ws + (long long)gridDim.z * a.nh * a.nsplit * 32 * 32;
+  float* pl = pm + (long long)gridDim.z * a.nh * a.nsplit * 32;
+  const int ns = (Tv + a.Tc - 1) / a.Tc;   // this video's chunks
+  const bool fold = a.cnt != nullptr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = tid + i * AT, q = e >> 5, d = e & 31;
+    float M = -INFINITY;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, xm[ww][q]);
+    float O = 0.f, L = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) {
+      const float f = xm[ww][q] == -INFINITY ? 0.f : __expf(xm[ww][q] - M);
+      O += f * xo[ww][d][q];
+      L += f * xl[ww][q];
+    }
+    if (ns == 1) {
+      if (q < a.Qv) {
+        a.out[(qrow + q) * a.ld_out + h * 32 + d] = O / L;
+        if (d == 0) a.lse[((long long)vid * a.nh + h) * a.qs + a.q0 + q] = M + __logf(L);
+      }
+    } else if (fold) {
+      stc1(a.ws, (pid * 32 + q) * 32 + d, O);
+      if (d == 0) {
+        stc1(pm, pid * 32 + q, M);
+        stc1(pl, pid * 32 + q, L);
+      }
+    } else {
+      a.ws[(pid * 32 + q) * 32 + d] = O;
+      if (d == 0) {
+        pm[pid * 32 + q] = M;
+        pl[pid * 32 + q] = L;
+      }
+    }
+  }
+  if (ns > 1 && fold) {
+    __shared__ int last;
+    // (the wave partial images are free now: the merge's weights reuse them)
+    fold_merge(a, vid, h, ns, true, 1.f, qrow, reinterpret_cast<float(*)[32]>(&xo[0][0][0]),
+               reinterpret_cast<float(*)[32]>(&xo[2][0][0]), &last);
+  }
+}
+
+template <int KT>
+__global__ __launch_bounds__(AT) void tattn_bwd32_kernel(TAttnArgs a) {
+  __shared__ float tp[4][32][33];    // wave-private: P_d^T of the current key tile [key][query]
+  __shared__ float tds[4][32][33];   // dS^T [key][query]
+  __shared__ float xq[4][32][33];    // per-wave dq partial [query][d]
+  const int c = blockIdx.x, h = blockIdx.y, vid = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 31, lh = lane >> 5;
+  const int Tv = a.koff[vid + 1] - a.koff[vid];
+  const int t0 = c * a.Tc, nk = min(a.Tc, Tv - t0);
+  if (nk <= 0) return;
+  const long long qrow = (long long)vid * a.qs + a.q0, krow = (long long)a.koff[vid] + t0;
+  const int kw0 = w * 32 * KT;
+  const int Qv = a.Qv;
+  // every load first.  Query-side fragments (query li, d 16 lh ..): q, dO, o; query-side columns (query
+  // acc_row(j), d li): q, dO (the B operands of dK and dV); key side: K and V fragments (key li, d 16 lh ..)
+  // and K columns (key acc_row(j), d li) for dq
+  float4 qf[4], df[4], of[4], kf[KT][4], vf[KT][4];
+  float qt[16], dt[16], kt[KT][16];
+  const int qi = min(li, Qv - 1);
+  {
+    const float* qp = a.q + (qrow + qi) * a.ldq + h * 32 + 16 * lh;
+    const float* dp = a.dout + (qrow + qi) * a.lddo + h * 32 + 16 * lh;
+    const float* op = a.o + (qrow + qi) * a.ldo + h * 32 + 16 * lh;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      qf[q] = ld4g(qp + 4 * q);
+      df[q] = ld4g(dp + 4 * q);
+      of[q] = ld4g(op + 4 * q);
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const long long qr = qrow + min(acc_row(j, lane), Qv - 1);
+      qt[j] = a.q[qr * a.ldq + h * 32 + li];
+      dt[j] = a.dout[qr * a.lddo + h * 32 + li];
+    }
+#pragma unroll
+    for (int u = 0; u < KT; ++u) {
+      const long long kr = krow + min(kw0 + 32 * u + li, nk - 1);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        kf[u][q] = ld4g(a.k + kr * a.ldk + h * 32 + 16 * lh + 4 * q);
+        vf[u][q] = ld4g(a.v + kr * a.ldv + h * 32 + 16 * lh + 4 * q);
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        kt[u][j] = a.k[(krow + min(kw0 + 32 * u + acc_row(j, lane), nk - 1)) * a.ldk + h * 32 + li];
+    }
+  }
+  const float lse = li < Qv ? a.lse[((long long)vid * a.nh + h) * a.qs + a.q0 + li] : 0.f;
+  // D = rowsum(dO o) of this lane's query
+  float D = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) D += (df[q].x * of[q].x + df[q].y * of[q].y) + (df[q].z * of[q].z + df[q].w * of[q].w);
+  D += __shfl_xor(D, 32, 64);
+  f32x16 dqu[KT];   // one dq accumulator per key tile (independent chains), summed after
+#pragma unroll
+  for (int u = 0; u < KT; ++u) {
+    zero16(dqu[u]);
+    f32x16 s, dp;
+    zero16(s);
+    zero16(dp);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[u][q].x, qf[q].x, s, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x2f32(vf[u][q].x, df[q].x, dp, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[u][q].y, qf[q].y, s, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x2f32(vf[u][q].y, df[q].y, dp, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[u][q].z, qf[q].z, s, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x2f32(vf[u][q].z, df[q].z, dp, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[u][q].w, qf[q].w, s, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x2f32(vf[u][q].w, df[q].w, dp, 0, 0, 0);
+    }
+    // P^T, P_d^T, dS^T = P (dP keep - D) (dropout: P_d = P keep multiplied V, dP = (dO V^T) keep)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int kl = acc_row(r, lane), key = kw0 + 32 * u + kl;
+      const float p = (key < nk && li < Qv) ? __expf(s[r] * a.scale - lse) : 0.f;
+      const float kp = (a.drop_p > 0.f && p != 0.f) ? drop_keep(a, qrow + li, h, krow + key) : 1.f;
+      const float ds = p * (dp[r] * kp - D);
+      tp[w][kl][li] = p * kp;
+      tds[w][kl][li] = ds;
+      s[r] = ds;
+    }
+    // dq += dS K: A = dS (query li, key acc_row(j)) from the accumulators, B = K (key acc_row(j), d li)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dqu[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(s[j], kt[u][j], dqu[u], 0, 0, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's tile writes are visible to its lanes
+    // dV = P_d^T dO and dK = dS^T q over the queries: A = the LDS tile (key li, query acc_row(j))
+    f32x16 dv, dk;
+    zero16(dv);
+    zero16(dk);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int qj = acc_row(j, lane);
+      dv = __builtin_amdgcn_mfma_f32_32x32x2f32(tp[w][li][qj], dt[j], dv, 0, 0, 0);
+      dk = __builtin_amdgcn_mfma_f32_32x32x2f32(tds[w][li][qj], qt[j], dk, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kw0 + 32 * u + acc_row(r, lane);
+      if (key < nk) {
+        float* pv = a.dv + (krow + key) * a.lddv + h * 32 + li;
+        float* pk = a.dk + (krow + key) * a.lddk + h * 32 + li;
+        *pv = a.acc_kv ? *pv + dv[r] : dv[r];
+        *pk = a.acc_kv ? *pk + dk[r] * a.scale : dk[r] * a.scale;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // tile reads done before the next tile's writes
+  }
+  f32x16 dq = dqu[0];
+#pragma unroll
+  for (int u = 1; u < KT; ++u) dq += dqu[u];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) xq[w][acc_row(r, lane)][li] = dq[r];
+  __syncthreads();
+  const long long pid = ((long long)vid * a.nh + h) * a.nsplit + c;
+  const int ns = (Tv + a.Tc - 1) / a.Tc;
+  const bool fold = a.cnt != nullptr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = tid + i * AT, q = e >> 5, d = e & 31;
+    const float v = (xq[0][q][d] + xq[1][q][d]) + (xq[2][q][d] + xq[3][q][d]);
+    if (ns == 1) {
+      if (q < Qv) a.out[(qrow + q) * a.ld_out + h * 32 + d] = v * a.scale;
+    } else if (fold) {
+      stc1(a.ws, (pid * 32 + q) * 32 + d, v);
+    } else {
+      a.ws[(pid * 32 + q) * 32 + d] = v;
+    }
+  }
+  if (ns > 1 && fold) {
+    __shared__ int last;
+    fold_merge(a, vid, h, ns, false, a.scale, qrow, nullptr, nullptr, &last);
+  }
+}
+
 struct TAttnGeom {
   int Qp, Hp, Tc, nsplit;
   size_t lds;
@@ -577,8 +931,25 @@ extern "C" int fx_dbg_tattn_stamps(long long* p) {
 }
 #endif
 
+// the register-resident kernels' chunk: 32 KT keys per wave, KT = 2 (256-key chunks) unless that leaves
+// fewer than one workgroup per CU, then KT = 1 (128-key chunks)
+static int tattn_rr_tc(int nvid, int Tv, int nh) {
+  return (long long)nvid * nh * ((Tv + 255) / 256) >= 256 ? 256 : 128;
+}
+static bool tattn_rr_ok(int Qv, int hd, bool aligned) { return knobs().tattn_rr && hd == 32 && Qv <= 32 && aligned; }
+// the register-resident kernels merge in the launch (fold_merge) when every video has <= FOLD_MAX chunks:
+// the stream's arrival counters, one per (video, head); else null (tattn_merge_kernel after the launch)
+static unsigned* tattn_fold_counters(int nsplit, int nvid, int nh, hipStream_t s) {
+  if (!knobs().tattn_fold || nsplit <= 1 || nsplit > FOLD_MAX || (long long)nvid * nh > kArrivalCounters) return nullptr;
+  return arrival_counters(s);
+}
+
 long long tattn_ws_floats(int nvid, int Qv, int Tv, int hd, int nh) {
   long long w = 0;
+  if (hd == 32 && Qv <= 32) {   // (the register-resident geometry: 32 x 32 partials)
+    const long long np = (long long)nvid * nh * ((Tv + tattn_rr_tc(nvid, Tv, nh) - 1) / tattn_rr_tc(nvid, Tv, nh));
+    w = np * 32 * 32 + 2 * np * 32;
+  }
   for (int bwd = 0; bwd < 2; ++bwd) {
     const TAttnGeom g = tattn_geom(nvid, Qv, Tv, hd, nh, bwd);
     const long long np = (long long)nvid * nh * g.nsplit;
@@ -643,6 +1014,26 @@ int launch_tattn_fwd(const float* q, long long ldq, const float* k, long long ld
   // algorithmic traffic: K and V rows read once per query block, q read, o and lse written
   const int nqb = (Qv + QB - 1) / QB;
   const double kv = (double)ktot * nh * hd * nqb, qo = (double)nvid * Qv * nh * hd;
+  if (tattn_rr_ok(Qv, hd, a.vec)) {
+    a.Tc = tattn_rr_tc(nvid, Tmax, nh);
+    a.nsplit = (Tmax + a.Tc - 1) / a.Tc;
+    a.Qp = a.Hp = 32;
+    a.q0 = 0;
+    a.Qv = Qv;
+    FX_REQUIRE(ws || a.nsplit == 1, "attention over T: workspace required");
+    a.cnt = tattn_fold_counters(a.nsplit, nvid, nh, s);
+    prof_begin(1, s);
+    if (a.Tc == 256) hipLaunchKernelGGL(tattn_fwd32_kernel<2>, dim3(a.nsplit, nh, nvid), dim3(AT), 0, s, a);
+    else hipLaunchKernelGGL(tattn_fwd32_kernel<1>, dim3(a.nsplit, nh, nvid), dim3(AT), 0, s, a);
+    FX_CHECK_HIP(hipGetLastError());
+    if (a.nsplit > 1 && !a.cnt) {
+      hipLaunchKernelGGL(tattn_merge_kernel, dim3(nh, nvid), dim3(AT), sizeof(float) * 2 * a.nsplit * 32, s, a, 1,
+                         1.f);
+      FX_CHECK_HIP(hipGetLastError());
+    }
+    prof_end(1, s, 4.0 * qo * (double)ktot / nvid, 4.0 * (2.0 * kv + 2.0 * qo + (double)nvid * nh * Qv));
+    return FX_OK;
+  }
   prof_begin(1, s);
   for (int q0 = 0; q0 < Qv; q0 += QB) {
     a.q0 = q0;
@@ -682,6 +1073,26 @@ int launch_tattn_bwd(const float* q, long long ldq, const float* k, long long ld
   // flops: S = qK^T recomputed, dP = dO V^T, dV = P^T dO, dK = dS^T q, dq = dS K
   const int nqb = (Qv + QB - 1) / QB;
   const double kv = (double)ktot * nh * hd * nqb, qo = (double)nvid * Qv * nh * hd;
+  if (tattn_rr_ok(Qv, hd, a.vec)) {
+    a.Tc = tattn_rr_tc(nvid, Tmax, nh);
+    a.nsplit = (Tmax + a.Tc - 1) / a.Tc;
+    a.Qp = a.Hp = 32;
+    a.q0 = 0;
+    a.Qv = Qv;
+    a.acc_kv = opt && opt->acc_kv;
+    FX_REQUIRE(ws || a.nsplit == 1, "attention over T: workspace required");
+    a.cnt = tattn_fold_counters(a.nsplit, nvid, nh, s);
+    prof_begin(2, s);
+    if (a.Tc == 256) hipLaunchKernelGGL(tattn_bwd32_kernel<2>, dim3(a.nsplit, nh, nvid), dim3(AT), 0, s, a);
+    else hipLaunchKernelGGL(tattn_bwd32_kernel<1>, dim3(a.nsplit, nh, nvid), dim3(AT), 0, s, a);
+    FX_CHECK_HIP(hipGetLastError());
+    if (a.nsplit > 1 && !a.cnt) {
+      hipLaunchKernelGGL(tattn_merge_kernel, dim3(nh, nvid), dim3(AT), 0, s, a, 0, scale);
+      FX_CHECK_HIP(hipGetLastError());
+    }
+    prof_end(2, s, 10.0 * qo * (double)ktot / nvid, 4.0 * (4.0 * kv + 4.0 * qo + (double)nvid * nh * Qv));
+    return FX_OK;
+  }
   prof_begin(2, s);
   // query blocks one after another: a later block ADDS its dK / dV to the earlier blocks' (same key rows)
   for (int q0 = 0; q0 < Qv; q0 += QB) {

@@ -519,6 +519,8 @@ const Knobs& knobs() {
     if (const char* p = env("FX_GRU_POLL2")) k.gru_poll2 = p[0] != '0';
     if (const char* p = env("FX_GRU_BWD_GATE_WAVE")) k.gru_bwd_gate_wave = p[0] != '0';
     if (const char* p = env("FX_GRU_STORE_WAVE")) k.gru_store_wave = std::max(0, std::min(2, std::atoi(p)));
+    if (const char* p = env("FX_TATTN_RR")) k.tattn_rr = p[0] != '0';
+    if (const char* p = env("FX_TATTN_FOLD")) k.tattn_fold = p[0] != '0';
     if (const char* p = env("FX_TATTN_TC")) k.tattn_tc_max = std::max(32, std::min(256, std::atoi(p)));
     if (const char* p = env("FX_X2Y_FUSED")) k.x2y_fused = p[0] != '0';
     if (const char* p = env("FX_SPLIT_VARIANT")) k.split_variant = std::atoi(p);

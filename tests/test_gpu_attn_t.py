@@ -2,7 +2,8 @@
 float64 torch restatement of nn.MultiheadAttention's core (basic.py:508-516): o, log-sum-exp and
 the dq / dk / dv gradients, on the benchmark shape (2 videos x 32 tokens x 4096 frames, 8 heads of
 32, K and V as column ranges of one packed (T, 2 A L) projection like fx_decoder), the Breakfast
-shape (60 tokens, head dim 64) and ragged sizes (T not a multiple of the chunk, 3 videos)."""
+shape (60 tokens, head dim 64) and ragged sizes (T not a multiple of the chunk, 3 videos, fewer
+queries than a 32-row tile)."""
 import ctypes
 import math
 
@@ -33,8 +34,12 @@ def _ref(q, k, v, nvid, Lq, T, hd, nh, scale, dout):
     return o.detach(), torch.stack(lses, 0).detach(), q.grad, k.grad, v.grad
 
 
+# head dim 32 with <= 32 queries runs the register-resident kernels (256- or 128-key chunks merged inside
+# the launch by the last workgroup of each (video, head); one chunk: no merge; > 16 chunks (T = 5000): the
+# merge launch); the others the LDS-staged ones
 @pytest.mark.parametrize("nvid,Lq,T,hd,nh", [(2, 32, 4096, 32, 8), (1, 60, 512, 64, 8), (3, 8, 200, 16, 2),
-                                             (2, 64, 1000, 64, 4)])
+                                             (2, 64, 1000, 64, 4), (3, 20, 1000, 32, 4), (1, 32, 100, 32, 8),
+                                             (2, 32, 300, 32, 8), (16, 32, 512, 32, 8), (2, 32, 5000, 32, 8)])
 def test_mha_over_t_matches_fp64(nvid, Lq, T, hd, nh):
     lib = nx.load()
     A = hd * nh
