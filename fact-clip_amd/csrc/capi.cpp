@@ -510,6 +510,7 @@ const Knobs& knobs() {
     if (const char* p = env("FX_SIDE_MAXWG")) k.side_maxwg = std::max(0, std::atoi(p));
     if (const char* p = env("FX_GEMM_ROWPERM")) k.gemm_row_perm = p[0] != '0';
     if (const char* p = env("FX_GEMM_GROUPM")) k.gemm_group_m = p[0] != '0';
+    if (const char* p = env("FX_GEMM_PERSIST")) k.gemm_persist = p[0] != '0';
     if (const char* p = env("FX_FRL_XCD")) k.frl_xcd = std::atoi(p);
     if (const char* p = env("FX_FRL_PAIR")) k.frl_pair = p[0] != '0';
     if (const char* p = env("FX_FRL_PD")) k.frl_pd = std::atoi(p);

@@ -133,6 +133,7 @@ struct Knobs {
   int gemm_stagger = 1;
   bool gemm_xcd_planes = true;
   bool gemm_nt_store = false;
+  bool gemm_persist = true;  // FX_GEMM_PERSIST=0: one workgroup per wide8 tile (A/B)
   bool gemm_group_m = true;  // FX_GEMM_GROUPM=0: no grouped tile order for large-B GEMMs (A/B)
   bool gemm_row_perm = true;  // FX_GEMM_ROWPERM=0: dilated-conv row tiles in plain order on the XCDs (A/B)
   bool frl_pair = true;        // FX_FRL_PAIR=0: the fused MS-TCN layer synchronises per 32-deep stage (A/B)

@@ -80,6 +80,8 @@ struct GemmDev {
   int xcd_planes;       // wide8: whole z-planes (batch x split-K slice) per XCD, see block_tile
   int row_perm;         // > 1: dilated-conv A shifting by row_perm row tiles: XCD runs follow the taps, see block_tile
   int group_m;          // > 1: tiles in groups of group_m row tiles, column-major inside a group, see block_tile
+  int persist;          // wide8 only, > 0: tiles per launch; a grid of gridDim.x workgroups walks them (see
+                        // gemm_f32_wide8_kernel)
   int a_dil_b1;         // > 0: A's conv dilation of batch 1 (two dilated convs of one input in one launch)
   long long bias_bs;    // bias of batch b at bias + b * bias_bs
   int nt_store;         // FX_GEMM_NTSTORE=1 (A/B): the fast epilogue stores non-temporally
@@ -583,6 +585,7 @@ __device__ __forceinline__ void kloop(const Loader<AK, FAST>& la, const Loader<B
 // multiple of 8, e.g. the batched / split weight-gradient GEMMs, K = 8192 rows): plane p runs whole
 // on XCD p % 8, so every tile reading the plane's A rows and B rows hits one L2 instead of all eight
 // XCDs fetching them from MALL / HBM.
+__device__ __forceinline__ void block_tile_id(const GemmDev& g, int id, int& tx, int& ty);
 __device__ __forceinline__ void block_tile(const GemmDev& g, int& tx, int& ty, int& z) {
   const int nt = g.tiles_x * g.tiles_y;
   if (g.xcd_planes) {
@@ -594,7 +597,12 @@ __device__ __forceinline__ void block_tile(const GemmDev& g, int& tx, int& ty, i
     tx = t - ty * g.tiles_x;
     return;
   }
-  const int id = blockIdx.y * g.tiles_x + blockIdx.x;
+  block_tile_id(g, blockIdx.y * g.tiles_x + blockIdx.x, tx, ty);
+  z = blockIdx.z;
+}
+// the (x, y) tile of linear workgroup id `id` (XCD id % 8): XCD runs, then the group / row-permutation orders
+__device__ __forceinline__ void block_tile_id(const GemmDev& g, int id, int& tx, int& ty) {
+  const int nt = g.tiles_x * g.tiles_y;
   const int q = nt / 8, rr = nt % 8, x8 = id % 8, i8 = id / 8;
   const int nid = (x8 < rr ? x8 * (q + 1) : rr * (q + 1) + (x8 - rr) * q) + i8;
   ty = nid / g.tiles_x;
@@ -616,7 +624,6 @@ __device__ __forceinline__ void block_tile(const GemmDev& g, int& tx, int& ty, i
     const int per = g.tiles_y / g.row_perm;
     ty = (ty % per) * g.row_perm + ty / per;
   }
-  z = blockIdx.z;
 }
 
 template <int AK, int BKIND, bool FAST>
@@ -1072,8 +1079,17 @@ __global__ __launch_bounds__(W8T) void gemm_f32_wide8_kernel(GemmDev g) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, li = lane & 31, lh = lane >> 5;
   const int ai = wm >> 1, wr = (wm & 1) * 32;   // A image (rows m0 / m0 + 64) and row offset in it
+  // persist: gridDim.x (a multiple of 8) workgroups walk the tiles as virtual workgroup ids blockIdx.x +
+  // i gridDim.x -- same XCD as the physical one -- saving a dispatch and teardown per tile
+  for (int vb = blockIdx.x;; vb += gridDim.x) {
   int tx, ty, z;
-  block_tile(g, tx, ty, z);
+  if (g.persist) {
+    if (vb >= g.persist) break;
+    block_tile_id(g, vb, tx, ty);
+    z = 0;
+  } else {
+    block_tile(g, tx, ty, z);
+  }
   const int n0 = tx * BN, m0 = ty * WBM;
   const int bidx = z / g.split, sk = z - bidx * g.split;
   const int nkt = (g.K + BK - 1) / BK;
@@ -1113,6 +1129,9 @@ __global__ __launch_bounds__(W8T) void gemm_f32_wide8_kernel(GemmDev g) {
     return;
   }
   tile_epilogue(g, bidx, rbase, col, acc);
+  if (!g.persist) break;
+  __syncthreads();   // the next tile's prologue refills the LDS ring
+  }
 }
 
 // ---------------------------------------------------------------- bf16 arithmetic (FX_PREC_BF16)
@@ -2181,6 +2200,7 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
     if (b_bytes > 2.0 * (1 << 20) && a_run <= 2.0 * (1 << 20)) g.group_m = gm;
   }
   g.nt_store = knobs().gemm_nt_store ? 1 : 0;
+  g.persist = 0;
   P.grid = grid;
   P.block = block;
   P.direct = direct;
@@ -2302,8 +2322,19 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
   GemmPlan P;
   FX_TRY(plan_gemm(d, s, P));
   log_gemm(d, P);
-  const GemmDev& g = P.g;
   const int np = split_pieces_for(P, s);
+  // FX_GEMM_PERSIST=0: one workgroup per tile (A/B).  A persistent grid for the f32 wide8 kernel on
+  // single, unsplit products with at least two tiles per CU (the kernel loops over virtual workgroups)
+  if (knobs().gemm_persist && !np && !bf16_eligible(P, s) && P.wide && wide8() && P.g.split == 1 && d.batch == 1 &&
+      !P.g.xcd_planes) {
+    const long long nt = (long long)P.g.tiles_x * P.g.tiles_y;
+    constexpr int G = 256;   // (a multiple of 8: a virtual workgroup keeps its physical one's XCD)
+    if (nt >= 2 * G) {
+      P.g.persist = (int)nt;
+      P.grid = dim3(G, 1, 1);
+    }
+  }
+  const GemmDev& g = P.g;
   int st = np ? launch_split(P, np, s)
          : bf16_eligible(P, s) ? launch_bf16(P, s)
          : P.direct ? launch_direct(P.ak, P.bk, P.grid, P.block, s, g)
