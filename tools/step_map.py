@@ -13,6 +13,7 @@ import sys
 
 CATS = [  # (category, substrings of the kernel name), first match wins
     ("frl (fused MS-TCN layer)", ["frl_kernel"]),
+    ("token decoder kernel", ["tok_kernel"]),
     ("gru", ["gru_fwd", "gru_bwd"]),
     ("attention over T", ["tattn_"]),
     ("x2y cores", ["x2y_"]),
