@@ -650,9 +650,18 @@ def main():
         for name, r in roofline_attention.items():
             if r is not None and default_shape:   # PMC bytes of the main kernel (the merge launch excluded)
                 r["traffic"] = traffic_from_profiles(f"tattn_{name}_kernel", f"r04_pmc_tattn_{name}.json")
+        x2y_pmc = {}
+        if default_shape and os.path.exists(os.path.join(ROOT, "profiles", "r05_pmc_x2y.json")):
+            try:
+                with open(os.path.join(ROOT, "profiles", "r05_pmc_x2y.json")) as f:
+                    x2y_pmc = json.load(f)
+            except (OSError, ValueError):
+                x2y_pmc = {}
         for name, v in x2y_prof.items():      # the X2Y_map cores (basic.py:373-380), when they ran fused
             if v[3].value > 0:
                 roofline_attention[name] = attention_roofline(X2Y_NOTES[name], *v)
+                if roofline_attention[name] is not None:   # (standalone PMC passes, tools/r05_x2y_pmc.sh)
+                    roofline_attention[name]["traffic"] = x2y_pmc.get(name)
         line = dict(metric=metric, value=round(value, 1), unit="frames/s", n_gpus=world, steps=args.steps,
                     warmup=args.warmup, ms_per_step=round(1e3 * elapsed / args.steps, 3), higher_is_better=True,
                     scaling="weak", vs_baseline=None, dtype="fp32", data="synthetic",
