@@ -521,6 +521,7 @@ const Knobs& knobs() {
     if (const char* p = env("FX_GRU_BWD_GATE_WAVE")) k.gru_bwd_gate_wave = p[0] != '0';
     if (const char* p = env("FX_GRU_STORE_WAVE")) k.gru_store_wave = std::max(0, std::min(2, std::atoi(p)));
     if (const char* p = env("FX_TATTN_RR")) k.tattn_rr = p[0] != '0';
+    if (const char* p = env("FX_X2Y_A2F_DW")) k.x2y_a2f_dw = p[0] != '0';
     if (const char* p = env("FX_TATTN_FOLD")) k.tattn_fold = p[0] != '0';
     if (const char* p = env("FX_TATTN_TC")) k.tattn_tc_max = std::max(32, std::min(256, std::atoi(p)));
     if (const char* p = env("FX_X2Y_FUSED")) k.x2y_fused = p[0] != '0';
@@ -1578,6 +1579,7 @@ long long x2y_split_ws1(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim) 
 }
 long long x2y_split_ws(const VidRows& v, int xdim, int ydim, int Hd, int outdim) {
   long long sp = x2y_split_ws1(v.x[v.n], xdim, v.y[v.n], ydim, Hd, outdim);
+  if (Hd % 32 == 0) sp = std::max(sp, x2y_a2f_dw_ws_floats(v.n, Hd));   // (the a2f dW kernel's partials)
   for (int i = 0; i < v.n; ++i)
     sp = std::max(sp, x2y_split_ws1(v.x[i + 1] - v.x[i], xdim, v.y[i + 1] - v.y[i], ydim, Hd, outdim));
   return sp;
@@ -1804,7 +1806,12 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
   if (fused) {
     FX_TRY(launch_x2y_a2f_bwd(dcat + ydim, cw, xv, xk, attn, dattn, dlogit, Hd, scale, V.n, V.y.data(), V.x.data(),
                               V.a.data(), dL, dyq, s));
-    // dxv = attn^T dfeat and dxk = scale dlogit^T yq of up to two videos in one grouped launch
+    // dxv = attn^T dfeat and dxk = scale dlogit^T yq: one launch over every video (x2y_a2f_dw_kernel), or
+    // (FX_X2Y_A2F_DW=0) grouped split-K GEMMs of up to two videos per launch
+    if (knobs().x2y_a2f_dw && x2y_a2f_dw_ok(V.n, V.y.data())) {
+      FX_TRY(launch_x2y_a2f_dw(attn, dL, dcat + ydim, cw, yq, Hd, scale, V.n, V.y.data(), V.x.data(), V.a.data(), dxv,
+                               dxk, spl, s));
+    } else
     for (int v0 = 0; v0 < V.n; v0 += GMAX_GROUP / 2) {
       fx_gemm_desc g2[GMAX_GROUP];
       int n2 = 0;

@@ -141,6 +141,7 @@ struct Knobs {
   int frl_ablate = 0;          // FX_FRL_ABLATE: diagnostic timing ablations of the fused layer (wrong results)
   int frl_min_fill = 80;        // FX_FRL_MIN_FILL: fused MS-TCN layer only when its row tiles cover this % of the CUs (shipped yaml, 219 tiles: 80 vs 100 -> 54.5-54.8 vs 55.1-55.2 ms)
   bool aux_stream = true;       // FX_AUX_STREAM=0: the decoder's query-position gradient on the caller's stream
+  bool x2y_a2f_dw = true;        // FX_X2Y_A2F_DW=0: the a2f backward's dxv / dxk as grouped split-K GEMMs (A/B)
   bool tattn_fold = true;        // FX_TATTN_FOLD=0: the register-resident kernels' merge as a second launch (A/B)
   bool tattn_rr = true;          // FX_TATTN_RR=0: the LDS-staged attention-over-T kernels for head dim 32 too (A/B)
   int tattn_tc_max = 256;       // FX_TATTN_TC: largest key chunk per attention-over-T workgroup (32..256, A/B)

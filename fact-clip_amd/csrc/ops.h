@@ -82,6 +82,13 @@ int launch_x2y_f2a_bwd(const float* dfeat, long long ldf, const float* xv, const
                        float* dyq, float* ws, hipStream_t s);
 // backward, input-gradient side: dP = dfeat . xv^T (+ dattn), dlogit = attn (dP - rowsum(attn dP)) (+ dlogit_in),
 // dyq = scale dlogit . xk;  dfeat rows ld ldf (16-B aligned)
+// the a2f backward's weight-side products dxv = attn^T dfeat, dxk = scale dlogit^T yq in one launch
+// (x2y_a2f_dw_kernel); ws: x2y_a2f_dw_ws_floats(nvid, Hd) floats
+long long x2y_a2f_dw_ws_floats(int nvid, int Hd);
+bool x2y_a2f_dw_ok(int nvid, const int* yoff);   // every video within the kernel's row chunks
+int launch_x2y_a2f_dw(const float* attn, const float* dl, const float* dfeat, long long ldf, const float* yq, int Hd,
+                      float scale, int nvid, const int* yoff, const int* xoff, const long long* aoff, float* dxv,
+                      float* dxk, float* ws, hipStream_t s);
 int launch_x2y_a2f_bwd(const float* dfeat, long long ldf, const float* xv, const float* xk, const float* attn,
                        const float* dattn, const float* dlogit_in, int Hd, float scale, int nvid, const int* yoff,
                        const int* xoff, const long long* aoff, float* dlogit, float* dyq, hipStream_t s);

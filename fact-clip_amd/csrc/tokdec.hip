@@ -141,8 +141,17 @@ __device__ __forceinline__ bool grid_sync(BarState& b, int* dead) {
   b.target += (unsigned long long)b.G;
   if (threadIdx.x == 0) {
     __hip_atomic_fetch_add(b.cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // two polls in flight, half a round trip apart: the last arrival is seen up to half a memory round
+    // trip sooner than with one poll at a time
+    unsigned long long x0 = __hip_atomic_load(b.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_s_sleep(4);
+    unsigned long long x1 = __hip_atomic_load(b.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned n = 0;
-    while ((long long)(__hip_atomic_load(b.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - b.target) < 0) {
+    while (true) {
+      if ((long long)(x0 - b.target) >= 0) break;
+      x0 = __hip_atomic_load(b.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((long long)(x1 - b.target) >= 0) break;
+      x1 = __hip_atomic_load(b.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_s_sleep(1);
       if (++n > b.spin_max) {
         __hip_atomic_fetch_or(b.status, (unsigned)FX_STATUS_TOK_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -742,6 +742,193 @@ int launch_x2y_a2f_bwd(const float* dfeat, long long ldf, const float* xv, const
   return launch_a2f(a, 1, yoff, xoff, aoff, s);
 }
 
+// ---------------------------------------------------------------- a2f weight-side products
+// dxv = attn^T dfeat and dxk = scale dlogit^T yq of every video (the products of the a2f backward that
+// reduce over the query rows) in ONE launch, instead of grouped split-K GEMMs + their reduce launches:
+// grid (row chunk, 32-column block of Hd, video x {dxv, dxk}); a workgroup's 4 waves each take a quarter
+// of the chunk's rows (sub-chunks of 32: the P values of a row as the A operand with the key as the row
+// index -- lane li reads P[r][li], 32 lanes one 128-B row slice --, the B rows likewise), summed through
+// LDS in wave order; the chunks of a (video, matrix, column block) are summed in chunk order by the last
+// workgroup to finish one (write-through hand-off: partials stored sc1 and acknowledged before the
+// arrival, read back sc1 by the last arriver, which re-arms the counter) -- deterministic.
+constexpr int DWT = 256;          // threads
+constexpr int DW_MAXC = 8;        // row chunks per video
+struct A2fDwArgs {
+  const float* attn;              // per video (ny x nx) at aoff[v]
+  const float* dl;                // dlogit, same layout
+  const float* dfeat;             // (Ny, Hd) rows, ld ldf
+  long long ldf;
+  const float* yq;                // (Ny, Hd) rows, ld Hd
+  float* dxv;                     // (Nx, Hd) rows
+  float* dxk;
+  float scale;
+  int Hd, nvid, nchunk, crows;    // chunks per video (grid x), rows per chunk (a multiple of 128)
+  float* ws;                      // partials [vid][mat][col block][chunk][64 x][32 d]
+  unsigned* cnt;                  // arrival counters [vid][mat][col block]
+  int yoff[FX_X2Y_MAXV + 1], xoff[FX_X2Y_MAXV + 1];
+  long long aoff[FX_X2Y_MAXV + 1];
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t dw_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
+}
+
+__global__ __launch_bounds__(DWT) void x2y_a2f_dw_kernel(A2fDwArgs a) {
+  __shared__ float red[4][2][16][64];
+  __shared__ int last;
+  const int c = blockIdx.x, cb = blockIdx.y, vid = blockIdx.z >> 1, mat = blockIdx.z & 1;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 31, lh = lane >> 5;
+  int y0 = 0, ny = 0, x0 = 0, nx = 0;
+  long long ao = 0;
+#pragma unroll
+  for (int i = 0; i < FX_X2Y_MAXV; ++i)
+    if (i == vid) {
+      y0 = a.yoff[i];
+      ny = a.yoff[i + 1] - a.yoff[i];
+      x0 = a.xoff[i];
+      nx = a.xoff[i + 1] - a.xoff[i];
+      ao = a.aoff[i];
+    }
+  if (nx <= 0 || ny <= 0) return;                     // (uniform: the whole workgroup)
+  const int nch = (ny + a.crows - 1) / a.crows;       // this video's chunks
+  if (c >= nch) return;
+  const float* P = (mat == 0 ? a.attn : a.dl) + ao;   // (ny x nx)
+  const float* B = mat == 0 ? a.dfeat : a.yq;
+  const long long ldb = mat == 0 ? a.ldf : a.Hd;
+  const int d0 = cb * 32;
+  const int nxt = nx > 32 ? 2 : 1;
+  f32x16 acc[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+  // this wave's rows: [c crows + w crows/4, + crows/4) in sub-chunks of 32 (lane half lh: rows 16 lh ..
+  // + 15): the P values of a row as the A operand with the key as the row index (lane li reads P[r][li],
+  // 32 lanes one 128-B row slice), the B rows likewise.  (Staging the chunk through LDS first, and a
+  // register double buffer over the sub-chunks, both measured slower.)
+  const int wr0 = c * a.crows + w * (a.crows >> 2), wr1 = min(ny, wr0 + (a.crows >> 2));
+  for (int r0 = wr0; r0 < wr1; r0 += 32) {
+    float pv[2][16], bv[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int r = r0 + 16 * lh + s, rc = min(r, ny - 1);
+      bv[s] = B[(long long)(y0 + rc) * ldb + d0 + li];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        if (t < nxt) pv[t][s] = P[(long long)rc * nx + min(32 * t + li, nx - 1)];
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const bool rok = r0 + 16 * lh + s < wr1;
+      const float b = rok ? bv[s] : 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        if (t < nxt) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(32 * t + li < nx ? pv[t][s] : 0.f, b, acc[t], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[w][t][r][lane] = acc[t][r];
+  __syncthreads();
+  // the workgroup's tile (64 x, 32 d) summed over the waves in order; thread -> 8 elements (t, r, lane)
+  const float mul = mat == 0 ? 1.f : a.scale;
+  float* out = mat == 0 ? a.dxv : a.dxk;
+  const long long grp = ((long long)vid * 2 + mat) * gridDim.y + cb;
+  float* part = a.ws + (grp * a.nchunk + c) * 2048;
+  const bool direct = nch == 1 || a.cnt == nullptr;
+  float v8[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int e = tid + i * DWT, t = e >> 10, r = (e >> 6) & 15, l = e & 63;
+    v8[i] = (red[0][t][r][l] + red[1][t][r][l]) + (red[2][t][r][l] + red[3][t][r][l]);
+    const int x = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), d = d0 + (l & 31);
+    if (direct) {
+      if (x < nx && t < nxt) out[(long long)(x0 + x) * a.Hd + d] = v8[i] * mul;
+    } else {
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v8[i]), dw_rsrc(part), e * 4, 0, 16);
+    }
+  }
+  if (direct) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's partial stores acknowledged
+  __syncthreads();
+  if (tid == 0) {
+    unsigned* cp = a.cnt + grp;
+    const unsigned prev = __hip_atomic_fetch_add(cp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == (unsigned)nch - 1;
+    if (last) __hip_atomic_store(cp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!last) return;
+  const float* pbase = a.ws + grp * a.nchunk * 2048;
+  float x8[DW_MAXC][8];
+#pragma unroll
+  for (int q = 0; q < DW_MAXC; ++q)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      x8[q][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          dw_rsrc(pbase), ((long long)min(q, nch - 1) * 2048 + tid + i * DWT) * 4, 0, 16));
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int e = tid + i * DWT, t = e >> 10, r = (e >> 6) & 15, l = e & 63;
+    float sum = 0.f;
+#pragma unroll
+    for (int q = 0; q < DW_MAXC; ++q)
+      if (q < nch) sum += x8[q][i];
+    const int x = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), d = d0 + (l & 31);
+    if (x < nx && t < nxt) out[(long long)(x0 + x) * a.Hd + d] = sum * mul;
+  }
+}
+
+bool x2y_a2f_dw_ok(int nvid, const int* yoff) {
+  (void)yoff;   // (any row count: the chunks grow with the video)
+  return nvid >= 1 && nvid <= FX_X2Y_MAXV;
+}
+long long x2y_a2f_dw_ws_floats(int nvid, int Hd) { return (long long)nvid * 2 * (Hd / 32) * DW_MAXC * 2048; }
+
+int launch_x2y_a2f_dw(const float* attn, const float* dl, const float* dfeat, long long ldf, const float* yq, int Hd,
+                      float scale, int nvid, const int* yoff, const int* xoff, const long long* aoff, float* dxv,
+                      float* dxk, float* ws, hipStream_t s) {
+  FX_REQUIRE(nvid >= 1 && nvid <= FX_X2Y_MAXV && Hd % 32 == 0, "x2y a2f dW: <= 16 videos, Hd % 32 == 0");
+  A2fDwArgs a{};
+  a.attn = attn;
+  a.dl = dl;
+  a.dfeat = dfeat;
+  a.ldf = ldf;
+  a.yq = yq;
+  a.dxv = dxv;
+  a.dxk = dxk;
+  a.scale = scale;
+  a.Hd = Hd;
+  a.nvid = nvid;
+  int nymax = 0;
+  for (int v = 0; v <= nvid; ++v) {
+    a.yoff[v] = yoff[v];
+    a.xoff[v] = xoff[v];
+    a.aoff[v] = aoff[v];
+    if (v < nvid) {
+      FX_REQUIRE(xoff[v + 1] - xoff[v] <= 64, "x2y a2f dW: <= 64 keys per video");
+      nymax = std::max(nymax, yoff[v + 1] - yoff[v]);
+    }
+  }
+  if (nymax == 0) return FX_OK;
+  // about one workgroup per CU: chunks of a multiple of 128 rows (32 per wave), at most DW_MAXC per video
+  const int ncb = Hd / 32;
+  const long long groups = (long long)nvid * 2 * ncb;
+  int nchunk = (int)std::max<long long>(1, std::min<long long>(DW_MAXC, (256 + groups - 1) / groups));
+  int crows = (nymax + nchunk - 1) / nchunk;
+  crows = (crows + 127) / 128 * 128;
+  nchunk = (nymax + crows - 1) / crows;
+  a.nchunk = nchunk;
+  a.crows = crows;
+  a.ws = ws;
+  a.cnt = (nchunk > 1 && groups <= kArrivalCounters) ? arrival_counters(s) : nullptr;
+  FX_REQUIRE(nchunk == 1 || (a.cnt && ws), "x2y a2f dW: workspace / counters required");
+  hipLaunchKernelGGL(x2y_a2f_dw_kernel, dim3(nchunk, ncb, 2 * nvid), dim3(DWT), 0, s, a);
+  FX_CHECK_HIP(hipGetLastError());
+  return FX_OK;
+}
+
 bool x2y_f2a_fusable(int nvid, const int* xoff, const int* yoff, int Hd) {
   if (nvid < 1 || nvid > FX_X2Y_MAXV || Hd % 256 != 0 || Hd > XT) return false;
   long long nch = 0;
