@@ -718,6 +718,9 @@ __global__ __launch_bounds__(AT) void tattn_fwd32_kernel(TAttnArgs a) {
   float* pl = pm + (long long)gridDim.z * a.nh * a.nsplit * 32;
   const int ns = (Tv + a.Tc - 1) / a.Tc;   // this video's chunks
   const bool fold = a.cnt != nullptr;
+  // a one-chunk video writes its rows directly, except when a merge launch follows (no fold, more than
+  // one chunk in the launch): that launch merges every video, so every video leaves partials
+  const bool direct = ns == 1 && (fold || a.nsplit == 1);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int e = tid + i * AT, q = e >> 5, d = e & 31;
@@ -731,7 +734,7 @@ __global__ __launch_bounds__(AT) void tattn_fwd32_kernel(TAttnArgs a) {
       O += f * xo[ww][d][q];
       L += f * xl[ww][q];
     }
-    if (ns == 1) {
+    if (direct) {
       if (q < a.Qv) {
         a.out[(qrow + q) * a.ld_out + h * 32 + d] = O / L;
         if (d == 0) a.lse[((long long)vid * a.nh + h) * a.qs + a.q0 + q] = M + __logf(L);
@@ -876,11 +879,12 @@ __global__ __launch_bounds__(AT) void tattn_bwd32_kernel(TAttnArgs a) {
   const long long pid = ((long long)vid * a.nh + h) * a.nsplit + c;
   const int ns = (Tv + a.Tc - 1) / a.Tc;
   const bool fold = a.cnt != nullptr;
+  const bool direct = ns == 1 && (fold || a.nsplit == 1);   // (see the forward)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int e = tid + i * AT, q = e >> 5, d = e & 31;
     const float v = (xq[0][q][d] + xq[1][q][d]) + (xq[2][q][d] + xq[3][q][d]);
-    if (ns == 1) {
+    if (direct) {
       if (q < Qv) a.out[(qrow + q) * a.ld_out + h * 32 + d] = v * a.scale;
     } else if (fold) {
       stc1(a.ws, (pid * 32 + q) * 32 + d, v);

@@ -166,6 +166,9 @@ def test_fused_decoder_tokens_dropout_ragged(cross, Q, T, p, monkeypatch):
 # shapes of the persistent token kernel (tokdec.hip): head dim 32, <= 32 tokens per video
 TOK_CASES = [
     (True, 32, (300, 220), 0.2),
+    # a one-chunk frame memory beside a 5000-frame one: more key chunks than the attention's in-launch
+    # merge takes, so the merge launch runs over both videos
+    (True, 32, (33, 5000), 0.0),
     (True, 20, (257, 257), 0.0),
     (True, 7, (64, 90), 0.2),
     (False, 32, None, 0.2),
