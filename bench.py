@@ -649,7 +649,7 @@ def main():
                               for name, v in attn_prof.items()}
         for name, r in roofline_attention.items():
             if r is not None and default_shape:   # PMC bytes of the main kernel (the merge launch excluded)
-                r["traffic"] = traffic_from_profiles(f"tattn_{name}_kernel", f"r04_pmc_tattn_{name}.json")
+                r["traffic"] = traffic_from_profiles(f"tattn_{name}32_kernel", f"r05_pmc_tattn_{name}.json")
         x2y_pmc = {}
         if default_shape and os.path.exists(os.path.join(ROOT, "profiles", "r05_pmc_x2y.json")):
             try:

@@ -343,6 +343,12 @@ class EarlyMatch:
                 ai = si = np.arange(Gv)
             else:
                 c = cost[v, :, :Gv].astype(np.float64)
+                if not np.isfinite(c).all():
+                    # costs from a step whose kernels reported a failure (e.g. a BiGRU timeout): raise that
+                    # failure (the status word is final: the costs' event has completed) rather than the
+                    # matching's own error on the garbage it produced
+                    st = fxf.device_status(self.cost_dev.device)
+                    fxf.status_raise(int(st[0].item()), self.cost_dev.device)
                 ai, si = linear_sum_assignment(c) if kind == "o2o" else one_to_many_match(c, self.gts[v][2])
             out.append((np.asarray(ai, dtype=np.int64), np.asarray(si, dtype=np.int64)))
         return out

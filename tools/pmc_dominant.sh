@@ -18,5 +18,6 @@ python tools/pmc_dominant.py $OUT "${KERNEL:-frl_kernel}" > gpurun_out/pmc_domin
 python tools/pmc_dominant.py $OUT "gemm_f32_wide8_kernel<1, 0, 0>" > gpurun_out/pmc_conv_gemm.json
 cat gpurun_out/pmc_dominant.json
 # the same FETCH/WRITE passes, averaged over the attention-over-T kernels
-python tools/pmc_dominant.py $OUT "tattn_fwd_kernel" > gpurun_out/pmc_tattn_fwd.json
-python tools/pmc_dominant.py $OUT "tattn_bwd_kernel" > gpurun_out/pmc_tattn_bwd.json
+# (head dim 32: the register-resident kernels, round 5)
+python tools/pmc_dominant.py $OUT "tattn_fwd32_kernel" > gpurun_out/r05_pmc_tattn_fwd.json
+python tools/pmc_dominant.py $OUT "tattn_bwd32_kernel" > gpurun_out/r05_pmc_tattn_bwd.json
