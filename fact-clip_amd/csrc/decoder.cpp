@@ -957,7 +957,9 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
     // one weight-gradient kind over all layers: dW_l (+)= dy_l^T x_l (+ db_l), layer l's operands at layer
     // 0's plus l times a stride; batched when the parameter gradients are uniformly strided (views of
     // one flat buffer), else one launch per layer.  Split 1: the side stream must not touch `spl`,
-    // which the main stream's remaining GEMMs use.
+    // which the main stream's remaining GEMMs use.  The products are collected and launched up to four
+    // per grouped launch (launch_gemm_group: independent direct-kernel problems in one launch)
+    std::vector<fx_gemm_desc> pend;
     auto kind = [&](int l0, int nl, const float* dy, long long lddy, long long dy_bs, const float* xx, long long ldxx,
                     long long x_bs, int K, int N, float* const* gw, float* const* gb, long long b_off,
                     long long w_off) -> int {
@@ -980,7 +982,7 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
           d.c_batch_stride = gw[l0 + 1] - gw[l0];
           d.c_last_batch_stride = gb ? gb[l0 + 1] - gb[l0] : 0;
         }
-        FX_TRY(launch_gemm(d, sd));
+        pend.push_back(d);
       }
       return FX_OK;
     };
@@ -990,7 +992,7 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
       fx_gemm_desc d = desc_linear_dwdb(dout, lddo, fin, A, R, A, p->out_dim, g->out_w, g->out_b, 1, nullptr);
       d.split_k = 1;
       d.workspace = nullptr;
-      FX_TRY(launch_gemm(d, sd));
+      pend.push_back(d);
     }
     FX_TRY(kind(0, NL, slot_u(0, 0), A, RA, b0 + L.f1, FF, PL, FF, A, g->ff2_w, g->ff2_b, 0, 0));
     FX_TRY(kind(0, NL, ws + L.gdf, FF, (long long)R * FF, b0 + (p->cross ? L.t2 : L.t1), A, PL, A, FF, g->ff1_w,
@@ -1012,6 +1014,8 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
       FX_TRY(kind(1, NL - 1, dq0 + 3 * RA + 2 * A, 3 * A, 3 * RA, b0 + L.t3, A, PL, A, A, g->sa_in_w, g->sa_in_b,
                   2 * A, 2LL * A * A));
     }
+    for (size_t i = 0; i < pend.size(); i += 4)   // 4: members per grouped launch (gemm_f32.hip GMAX)
+      FX_TRY(launch_gemm_group(pend.data() + i, (int)std::min<size_t>(4, pend.size() - i), sd));
   }
   {
     // every layer's LayerNorm weight / bias gradients in one launch: dw += sum_rows dy * xhat, db += sum_rows dy
