@@ -75,11 +75,11 @@ __global__ void relu_bwd_kernel(const float* dy, long long lddy, const float* y,
 }
 
 __global__ void add2_kernel(const float* a, long long lda, const float* b, long long ldb, int rows, int cols,
-                            float* o, long long ldo, int accumulate) {
+                            float* o, long long ldo, int accumulate, int bcols) {
   const long long total = (long long)rows * cols;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
     const long long r = i / cols, c = i % cols;
-    const float v = a[r * lda + c] + (b ? b[r * ldb + c] : 0.f);
+    const float v = a[r * lda + c] + (b && c < bcols ? b[r * ldb + c] : 0.f);
     o[r * ldo + c] = accumulate ? o[r * ldo + c] + v : v;
   }
 }
@@ -148,10 +148,10 @@ int relu_bwd(const float* dy, long long lddy, const float* y, long long ldy, int
 }
 
 int add2(const float* a, long long lda, const float* b, long long ldb, int rows, int cols, float* o, long long ldo,
-         int accumulate, hipStream_t s) {
+         int accumulate, hipStream_t s, int bcols) {
   if ((long long)rows * cols == 0) return FX_OK;
   hipLaunchKernelGGL(add2_kernel, dim3(ew_grid((long long)rows * cols)), dim3(256), 0, s, a, lda, b, ldb, rows, cols,
-                     o, ldo, accumulate);
+                     o, ldo, accumulate, bcols < 0 ? cols : bcols);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }
@@ -1646,30 +1646,19 @@ int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpo
   float* xv = saved + L.xv;
   float* yq = saved + L.yq;
   float* feat = saved + L.feat;
-  // keep X+Xpos / Y+Ypos for the weight gradients (basic.py:357-369)
+  // keep X+Xpos / Y+Ypos for the weight gradients (basic.py:357-369); the position covers the first
+  // *pos_cols channels (one launch either way)
   const float* xin = X;
   long long ldxin = ldx;
-  if (Xpos && xpos_cols == xdim) {
-    FX_TRY(add2(X, ldx, Xpos, ldxp, Nx, xdim, saved + L.xin, xdim, 0, s));
-    xin = saved + L.xin;
-    ldxin = xdim;
-  } else if (Xpos) {
-    FX_CHECK_HIP(hipMemcpy2DAsync(saved + L.xin, xdim * sizeof(float), X, ldx * sizeof(float), xdim * sizeof(float), Nx,
-                                  hipMemcpyDeviceToDevice, s));
-    FX_TRY(add2(Xpos, ldxp, nullptr, 0, Nx, xpos_cols, saved + L.xin, xdim, 1, s));
+  if (Xpos) {
+    FX_TRY(add2(X, ldx, Xpos, ldxp, Nx, xdim, saved + L.xin, xdim, 0, s, xpos_cols));
     xin = saved + L.xin;
     ldxin = xdim;
   }
   const float* yin = Y;
   long long ldyin = ldy;
-  if (Ypos && ypos_cols == ydim) {
-    FX_TRY(add2(Y, ldy, Ypos, ldyp, Ny, ydim, saved + L.yin, ydim, 0, s));
-    yin = saved + L.yin;
-    ldyin = ydim;
-  } else if (Ypos) {
-    FX_CHECK_HIP(hipMemcpy2DAsync(saved + L.yin, ydim * sizeof(float), Y, ldy * sizeof(float), ydim * sizeof(float), Ny,
-                                  hipMemcpyDeviceToDevice, s));
-    FX_TRY(add2(Ypos, ldyp, nullptr, 0, Ny, ypos_cols, saved + L.yin, ydim, 1, s));
+  if (Ypos) {
+    FX_TRY(add2(Y, ldy, Ypos, ldyp, Ny, ydim, saved + L.yin, ydim, 0, s, ypos_cols));
     yin = saved + L.yin;
     ldyin = ydim;
   }
@@ -1910,9 +1899,7 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
   }
   if (dX || dXpos) {
     FX_TRY(linear_dx(dxk, Hd, wk, Nx, xdim, Hd, dXk, xdim, 0, nullptr, 0, spl, s));
-    if (dXpos)
-      FX_CHECK_HIP(hipMemcpy2DAsync(dXpos, xpos_cols * sizeof(float), dXk, xdim * sizeof(float),
-                                    xpos_cols * sizeof(float), Nx, hipMemcpyDeviceToDevice, s));
+    if (dXpos) FX_TRY(add2(dXk, xdim, nullptr, 0, Nx, xpos_cols, dXpos, xpos_cols, (has_xpos >> 1) & 1, s));
     if (dX) {
       fx_gemm_desc d = gemm_desc(Nx, xdim, Hd, op_rows(dxv, Hd), op_cols(wv, xdim), dX, xdim);
       d.resid = dXk;
@@ -1924,9 +1911,7 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
   }
   if (dY || dYpos) {
     FX_TRY(linear_dx(dyq, Hd, wq, Ny, ydim, Hd, dYq, ydim, 0, nullptr, 0, spl, s));
-    if (dYpos)
-      FX_CHECK_HIP(hipMemcpy2DAsync(dYpos, ypos_cols * sizeof(float), dYq, ydim * sizeof(float),
-                                    ypos_cols * sizeof(float), Ny, hipMemcpyDeviceToDevice, s));
+    if (dYpos) FX_TRY(add2(dYq, ydim, nullptr, 0, Ny, ypos_cols, dYpos, ypos_cols, (has_ypos >> 1) & 1, s));
     if (dY) FX_TRY(add2(dYq, ydim, dcat, cw, Ny, ydim, dY, ydim, 0, s));
   }
   return FX_OK;

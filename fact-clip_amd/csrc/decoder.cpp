@@ -939,7 +939,7 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
   hipStream_t sa = s;
   if (qpos && dqpos) {
     sa = aux_fork(s);
-    bool first = true;
+    bool first = !p->dqpos_accumulate;
     auto acc = [&](const float* dy, long long lddy, const float* w, int N) -> int {
       fx_gemm_desc d = desc_linear_dx(dy, lddy, w, R, A, N, dqpos, A, first ? 0 : 1, nullptr, 0, nullptr);
       d.split_k = 1;

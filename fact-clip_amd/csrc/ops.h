@@ -97,8 +97,9 @@ int launch_x2y_a2f_bwd(const float* dfeat, long long ldf, const float* xv, const
 int ew_grid(long long total);
 int relu_bwd(const float* dy, long long lddy, const float* y, long long ldy, int rows, int cols, float* dz,
              long long lddz, hipStream_t s);
+// o (+)= a + b, b added on the first bcols columns only (bcols < 0: all)
 int add2(const float* a, long long lda, const float* b, long long ldb, int rows, int cols, float* o, long long ldo,
-         int accumulate, hipStream_t s);
+         int accumulate, hipStream_t s, int bcols = -1);
 // split-K factor / workspace floats for a (M x N, depth K) product
 int pick_split(int M, int N, int K, int batch = 1);
 long long split_ws(int M, int N, int K, int batch = 1);

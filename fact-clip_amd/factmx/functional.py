@@ -167,6 +167,64 @@ def grad_target(p, needed=True):
     return buf, buf
 
 
+class PosGradSink:
+    """One gradient buffer for a position table that several fused ops read (the action queries
+    repeated per video: every block's decoder query_pos and both cross-attention maps, blocks.py
+    _forward_batch).  Each op's backward ACCUMULATES its position gradient into ``buf`` (the first one
+    writes it) and returns None for it; ``PosSinkFn``'s backward -- which autograd runs only after every
+    op reading its output has run its own -- hands the sum on.  Without it the engine adds the per-op
+    position gradients pairwise (one add launch per extra reader, ~10 per headline step)."""
+
+    def __init__(self):
+        self.buf = None
+
+    def target(self, shape, dev):
+        """(buffer, accumulate flag) for one reader's position gradient."""
+        if self.buf is None:
+            self.buf = _empty(*shape, device=dev)
+            return self.buf, 0
+        assert tuple(self.buf.shape) == tuple(shape), (self.buf.shape, shape)
+        return self.buf, 1
+
+
+class PosSinkFn(torch.autograd.Function):
+    """Identity on a position table whose readers accumulate into one PosGradSink (see there)."""
+
+    @staticmethod
+    def forward(ctx, pos, sink):
+        ctx.sink = sink
+        ctx.set_materialize_grads(False)
+        return pos.view_as(pos)
+
+    @staticmethod
+    def backward(ctx, g):
+        buf, ctx.sink.buf = ctx.sink.buf, None
+        if buf is None:
+            return g, None
+        if g is not None:        # readers outside the fused ops (plain torch) returned theirs
+            buf.add_(g)
+        return buf, None
+
+
+# FX_POS_SINK=0: every reader returns its own position gradient (autograd adds them; A/B knob)
+POS_SINK = int(os.environ.get("FX_POS_SINK", "1"))
+
+
+def pos_sink(pos):
+    """``pos`` wrapped so that the fused ops reading it share one gradient buffer (PosGradSink);
+    ``pos`` itself when it needs no gradient."""
+    if pos is None or not (POS_SINK and pos.requires_grad and torch.is_grad_enabled()):
+        return pos
+    sink = PosGradSink()
+    out = PosSinkFn.apply(pos, sink)
+    out._fx_pos_sink = sink
+    return out
+
+
+def _sink_of(t):
+    return None if t is None else getattr(t, "_fx_pos_sink", None)
+
+
 # ---------------------------------------------------------------------------
 # raw launch helpers (no autograd)
 # ---------------------------------------------------------------------------
@@ -490,7 +548,7 @@ class X2YFn(torch.autograd.Function):
     each video's (ny_v, nx_v) block in video order."""
 
     @staticmethod
-    def forward(ctx, X, Y, Xpos, Ypos, rows, wk, bk, wv, bv, wq, bq, wy, by, drop_p=0.0, seed=0):
+    def forward(ctx, X, Y, Xpos, Ypos, rows, wk, bk, wv, bv, wq, bq, wy, by, drop_p=0.0, seed=0, sinks=(None, None)):
         lib = nx.load()
         dev = X.device
         Nx, xdim = X.shape
@@ -520,6 +578,7 @@ class X2YFn(torch.autograd.Function):
         ctx.drop = (float(drop_p), int(seed))
         ctx.rows = rows
         ctx.has_pos = (Xpos is not None, Ypos is not None)
+        ctx.sinks = sinks
         ctx.save_for_backward(X, Y, wk, bk, wv, bv, wq, bq, wy, by, attn, saved)
         ctx.set_materialize_grads(False)   # unused logit / attn gradients arrive as None (no zero fill)
         if rows is None:
@@ -548,8 +607,22 @@ class X2YFn(torch.autograd.Function):
         dattn = None if dattn is None else dattn.contiguous()
         dX = _empty(Nx, xdim, device=dev) if nd[0] else None
         dY = _empty(Ny, ydim, device=dev) if nd[1] else None
-        dXp = _empty(Nx, xpc, device=dev) if (hx and nd[2]) else None
-        dYp = _empty(Ny, ypc, device=dev) if (hy and nd[3]) else None
+        # position gradients: fresh buffers, or accumulated into a shared PosGradSink (returned as None)
+        dXp = dYp = None
+        fx, fy = int(hx), int(hy)
+        sx, sy = ctx.sinks
+        if hx and nd[2]:
+            if sx is not None:
+                dXp, acc = sx.target((Nx, xpc), dev)
+                fx |= 2 * acc
+            else:
+                dXp = _empty(Nx, xpc, device=dev)
+        if hy and nd[3]:
+            if sy is not None:
+                dYp, acc = sy.target((Ny, ypc), dev)
+                fy |= 2 * acc
+            else:
+                dYp = _empty(Ny, ypc, device=dev)
         tg = [grad_target(p, nd[5 + i]) for i, p in enumerate((wk, bk, wv, bv, wq, bq, wy, by))]
         bufs = [t[0] for t in tg]
         # the kernel needs every weight-gradient target; absent ones go to scratch
@@ -560,18 +633,26 @@ class X2YFn(torch.autograd.Function):
                               nx.ptr(wk), nx.ptr(wv), nx.ptr(wq), nx.ptr(wy), Hd, outdim, nvid, xo, yo,
                               ctx.drop[0], ctx.drop[1], nx.ptr(attn),
                               nx.ptr(saved), nx.ptr(dout), outdim, nx.ptr(dlogit), nx.ptr(dattn), nx.ptr(dX),
-                              nx.ptr(dXp), nx.ptr(dY), nx.ptr(dYp), *[nx.ptr(t) for t in bufs], int(hx), int(hy),
+                              nx.ptr(dXp), nx.ptr(dY), nx.ptr(dYp), *[nx.ptr(t) for t in bufs], fx, fy,
                               nx.ptr(ws), int(defer), nx.stream()), "fx_x2y_bwd")
         if defer:
             _defer_to_side(X, Y, saved, dout, ws, *bufs)
-        return (dX, dY, dXp, dYp, None) + tuple(t[1] for t in tg) + (None, None)
+        if sx is not None:
+            dXp = None
+        if sy is not None:
+            dYp = None
+        return (dX, dY, dXp, dYp, None) + tuple(t[1] for t in tg) + (None, None, None)
 
 
 def x2y(mod, X, Y, Xpos, Ypos, rows=None):
     p = float(mod.dropout.p) if mod.training else 0.0
-    return X2YFn.apply(_2d(X), _2d(Y), None if Xpos is None else _2d(Xpos), None if Ypos is None else _2d(Ypos),
-                       rows, mod.X_K.weight, mod.X_K.bias, mod.X_V.weight, mod.X_V.bias, mod.Y_Q.weight,
-                       mod.Y_Q.bias, mod.Y_W.weight, mod.Y_W.bias, p, dropout_seed() if p > 0 else 0)
+    xp = None if Xpos is None else _2d(Xpos)
+    yp = None if Ypos is None else _2d(Ypos)
+    # a shared position-gradient buffer only when the op reads the sink's own output (not a view of it)
+    sinks = (_sink_of(Xpos) if xp is Xpos else None, _sink_of(Ypos) if yp is Ypos else None)
+    return X2YFn.apply(_2d(X), _2d(Y), xp, yp, rows, mod.X_K.weight, mod.X_K.bias, mod.X_V.weight, mod.X_V.bias,
+                       mod.Y_Q.weight, mod.Y_Q.bias, mod.Y_W.weight, mod.Y_W.bias, p,
+                       dropout_seed() if p > 0 else 0, sinks)
 
 
 # ---------------------------------------------------------------------------
@@ -1276,7 +1357,7 @@ class DecoderFn(torch.autograd.Function):
     @staticmethod
     def _set_call(prm, call):
         """Per-call fields (dropout p's and seed, ragged memory offsets) of the cached param struct."""
-        pd, pa, seed, mem_off = call
+        pd, pa, seed, mem_off = call[:4]
         prm.dropout, prm.attn_dropout, prm.seed = pd, pa, seed
         prm.mem_off = None if mem_off is None else ctypes.addressof(mem_off)
 
@@ -1333,7 +1414,13 @@ class DecoderFn(torch.autograd.Function):
         prm.status = nx.ptr(device_status(dev))
         A = meta["A"]
         dtgt = _empty(R, A, device=dev) if nd[0] else None
-        dqpos = _empty(R, A, device=dev) if (hq and nd[1]) else None
+        dqpos, sink = None, ctx.call[4]
+        prm.dqpos_accumulate = 0
+        if hq and nd[1]:
+            if sink is not None:     # accumulated into the table's shared buffer (PosGradSink)
+                dqpos, prm.dqpos_accumulate = sink.target((R, A), dev)
+            else:
+                dqpos = _empty(R, A, device=dev)
         dmem = _empty(*mem.shape, device=dev) if (mem is not None and nd[2]) else None
         dmpos = _empty(*mpos.shape, device=dev) if (hm and nd[3]) else None
         ws = _ws(lib.fx_decoder_workspace_floats(ctypes.byref(prm), R, T, nvid, hq, hm), dev)
@@ -1348,6 +1435,8 @@ class DecoderFn(torch.autograd.Function):
                                   nx.ld(dmpos), nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_decoder_bwd")
         if defer:   # (dout too: the output linear's weight gradient reads it on the side stream)
             _defer_to_side(tgt, mem, mpos, saved, ws, dout)
+        if sink is not None:
+            dqpos = None
         return (dtgt, dqpos, dmem, dmpos, None, None, None) + tuple(t[1] for t in tg)
 
 
@@ -1371,7 +1460,8 @@ def decoder(mod, tgt, memory=None, pos=None, query_pos=None, nvid=1, mem_off=Non
     pd, pa = decoder_dropout(mod) if mod.training else (0.0, 0.0)
     seed = dropout_seed() if (pd > 0 or pa > 0) else 0
     off = None if (mem_off is None or memory is None) else nx.int_array(mem_off)
-    return DecoderFn.apply(t2, qp, mem, mp, spec, int(nvid), (float(pd), float(pa), seed, off), *params)
+    sink = _sink_of(query_pos) if qp is query_pos else None
+    return DecoderFn.apply(t2, qp, mem, mp, spec, int(nvid), (float(pd), float(pa), seed, off, sink), *params)
 
 
 # ---------------------------------------------------------------------------

@@ -521,7 +521,8 @@ class _FACTBase(nn.Module):
         f2 = torch.cat(frames, 0)
         fpe = [_frame_pos(self.frame_pe, s.unsqueeze(1)) for s in seq_list]
         fpos = None if fpe[0] is None else torch.cat([p.squeeze(1) for p in fpe], 0)
-        apos = self.action_query.squeeze(1).repeat(nvid, 1)
+        # one shared gradient buffer for the query table's readers (fxf.PosGradSink: no pairwise adds)
+        apos = fxf.pos_sink(self.action_query.squeeze(1).repeat(nvid, 1))
         a2 = torch.zeros_like(apos)
         for k, blk in enumerate(self.block_list):
             mark_block_input(self, k, f2)       # DP: block k's gradient bucket launches once f2 has its grad

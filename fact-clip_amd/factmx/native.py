@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FACTMX_LIB", os.path.join(_HERE, "_lib", "libfactmx.so"))
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -76,7 +76,8 @@ DECODER_GLOBAL_FIELDS = ["fn_w", "fn_b", "out_w", "out_b"]
 class DecoderParams(ctypes.Structure):
     _fields_ = ([("A", I), ("FF", I), ("nhead", I), ("num_layers", I), ("cross", I), ("Hm", I), ("out_dim", I),
                  ("final_norm", I), ("eps", F)] + [(n, P) for n in _DEC_PTRS] + [(n, P) for n in DECODER_GLOBAL_FIELDS]
-                + [("side_defer", I), ("dropout", F), ("attn_dropout", F), ("seed", U), ("mem_off", P), ("status", P)])
+                + [("side_defer", I), ("dropout", F), ("attn_dropout", F), ("seed", U), ("mem_off", P), ("status", P),
+                   ("dqpos_accumulate", I)])
 
 
 class DecoderGrads(ctypes.Structure):

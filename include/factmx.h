@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FX_ABI_VERSION 18
+#define FX_ABI_VERSION 19
 
 enum {
   FX_OK = 0,
@@ -163,6 +163,9 @@ int fx_linear_bwd(const float* dy, long long lddy, const float* x, long long ldx
  * index r (ydim + Hd) + c over the concatenated row, regenerated by the backward.
  * bwd: the four weight-gradient GEMMs run on the library's side stream after the attention
  * gradients exist; side_defer = 1 leaves them running there (fx_side_join), 0 joins before return.
+ * has_xpos / has_ypos: bit 0 = the forward had the position input; bit 1 = ACCUMULATE (+=) the
+ * position gradient into dXpos / dYpos instead of writing it (one buffer shared by every op that
+ * reads the same position table, so autograd does not add the per-op gradients pairwise).
  * ---------------------------------------------------------------------- */
 long long fx_x2y_saved_floats(int Nx, int xdim, int Ny, int ydim, int Hd);
 long long fx_x2y_workspace_floats(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim, int nvid,
@@ -203,7 +206,7 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
  * [v*R/nvid, (v+1)*R/nvid) and memory rows [v*T/nvid, (v+1)*T/nvid) (or mem_off); attention
  * never crosses videos, every projection runs over all rows at once.
  * bwd: every weight gradient ACCUMULATES (+=) into g; dtgt, dqpos (dense (R,A)),
- * dmem, dmpos are written (each nullable).
+ * dmem, dmpos are written (each nullable; dqpos accumulated when dqpos_accumulate).
  * ---------------------------------------------------------------------- */
 typedef struct fx_decoder_params {
   int A, FF, nhead, num_layers, cross, Hm, out_dim, final_norm;
@@ -236,6 +239,8 @@ typedef struct fx_decoder_params {
   int* status;                /* caller-owned device int32 status word (nullable): the persistent token
                                  kernel (tokdec.hip) ORs FX_STATUS_TOK_TIMEOUT into it when a grid-barrier
                                  wait gives up (outputs then wrong; never cleared by the library) */
+  int dqpos_accumulate;       /* bwd: dqpos += instead of = (a position gradient shared with other ops,
+                                 as fx_x2y_bwd has_xpos bit 1) */
 } fx_decoder_params;
 
 typedef struct fx_decoder_grads {

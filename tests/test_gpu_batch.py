@@ -124,3 +124,28 @@ def test_lockstep_north_star_vs_oracle():
                     np.testing.assert_array_equal(blk.tdu.end32.cpu().numpy(), rec["tdu"].ends)
                 err = (blk.frame_clogit[:, 0].double().cpu() - rec["frame_clogit"]).abs().max().item()
                 assert err < 1e-3, f"block {i}: per-frame logits differ by {err}"
+
+
+@pytest.mark.parametrize("name", ["tiny_clip", "tiny_clip_iid"])
+def test_pos_sink_matches_autograd_adds(name, monkeypatch):
+    """The action-query table's readers accumulating into one shared buffer (fxf.PosGradSink) give the
+    same parameter gradients as autograd adding their returned position gradients (FX_POS_SINK=0),
+    up to the summation order."""
+    from factmx import functional as fxf
+    fx = load_fixture(name)
+    meta = tiny_meta(fx)
+    cfg = cfg_from_meta(meta)
+    feats, label, _ = tiny_inputs(meta)
+    T, D = feats.shape
+    f2, l2 = pg.segmented_video(T + 9, D, sorted(set(label.tolist())), 5, seed=12, noise=0.4)
+    seqs = [torch.from_numpy(feats).float().to(DEV), torch.from_numpy(f2).float().to(DEV)]
+    labs = [torch.from_numpy(label).to(DEV), torch.from_numpy(l2).to(DEV)]
+    monkeypatch.setattr(fxf, "POS_SINK", 0)
+    ref = _run(_model(meta, cfg), seqs, labs, True, monkeypatch)
+    monkeypatch.setattr(fxf, "POS_SINK", 1)
+    got = _run(_model(meta, cfg), seqs, labs, True, monkeypatch)
+    assert got[0] == pytest.approx(ref[0], rel=1e-6)
+    assert ref[3]["action_query"].abs().max().item() > 0
+    for n, g in ref[3].items():
+        err = (got[3][n] - g).abs().max().item()
+        assert err <= 1e-5 * g.abs().max().item() + 1e-7, (n, err)
