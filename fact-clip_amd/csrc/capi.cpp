@@ -301,9 +301,9 @@ struct MstcnLayout {
   long long rows_pad;
   long long rowsF;
   // saved
-  long long h, z, xh, rs, wbs, wpts, total_saved;
+  long long h, z, xh, rs, wbs, wpts, wk1b, wk2b, total_saved;
   // workspace
-  long long wf, wb, wpt, wk1, wk2, buf0, buf1, buf2, buf3, buf4, buf5, split, split2, colsum, dzall, dhall, dball, csb, bsl,
+  long long wf, wk1, wk2, buf0, buf1, buf2, buf3, buf4, buf5, split, split2, colsum, dzall, dhall, dball, csb, bsl,
       total_ws;
 };
 
@@ -328,11 +328,11 @@ MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
   L.wbs = L.rs + (p->layernorm ? (long long)NL * rows : 0);   // dX-packed conv weights (fwd packs, bwd reads)
   const long long wsz = 3 * F * F;
   L.wpts = L.wbs + NL * wsz;                 // transposed 1x1 weights (fwd packs, bwd dZ GEMM reads)
-  L.total_saved = L.wpts + NL * F * F;
+  L.wk1b = L.wpts + NL * F * F;              // fused layers: the backward chain's weights (the two above) in
+  L.wk2b = L.wk1b + (p->fused_layers ? NL * wsz : 0);   // MFMA fragment order, packed by the forward
+  L.total_saved = L.wk2b + (p->fused_layers ? NL * F * F : 0);
   L.wf = 0;
-  L.wb = L.wf + NL * wsz;
-  L.wpt = L.wb + NL * wsz;                   // transposed 1x1 weights (fused backward chain)
-  L.wk1 = L.wpt + NL * F * F;                // fused layers: conv weights in MFMA fragment order
+  L.wk1 = L.wf + NL * wsz;                   // fused layers: conv weights in MFMA fragment order
   L.wk2 = L.wk1 + (p->fused_layers ? NL * wsz : 0);   // ... and the 1x1 weights
   L.buf0 = L.wk2 + (p->fused_layers ? NL * F * F : 0);
   L.buf1 = L.buf0 + L.rowsF;
@@ -384,25 +384,26 @@ int pack_conv_weights(const fx_mstcn_params* p, float* ws, float* wbdst, float* 
 }
 
 // the fused layer kernel's weights: every layer's conv matrix (ld 3F) and 1x1 matrix (ld F) in fragment
-// order; src2[i] may be a per-layer pointer list (the 1x1 weights) or a base with a uniform stride
-int pack_frag_layers(int NL, int F, const float* w1, long long w1_stride, const float* const* w2list,
-                     const float* w2, long long w2_stride, float* dst1, float* dst2, hipStream_t s) {
-  for (int l0 = 0; l0 < NL; l0 += 32) {
-    const int n = std::min(32, NL - l0);
-    const float* s1[32];
-    const float* s2[32];
-    float* d1[32];
-    float* d2[32];
-    for (int i = 0; i < n; ++i) {
-      s1[i] = w1 + (long long)(l0 + i) * w1_stride;
-      s2[i] = w2list ? w2list[l0 + i] : w2 + (long long)(l0 + i) * w2_stride;
-      d1[i] = dst1 + (long long)(l0 + i) * frl_packed_floats(3 * F);
-      d2[i] = dst2 + (long long)(l0 + i) * frl_packed_floats(F);
-    }
-    FX_TRY(launch_pack_frag(s1, d1, n, 3 * F, 3 * F, s));
-    FX_TRY(launch_pack_frag(s2, d2, n, F, F, s));
+// order, appended to a job list; the 1x1 sources are a per-layer pointer list or a base with a uniform
+// stride
+void frag_layer_jobs(std::vector<FragJob>& J, int NL, int F, const float* w1, long long w1_stride,
+                     const float* const* w2list, const float* w2, long long w2_stride, float* dst1, float* dst2) {
+  for (int l = 0; l < NL; ++l) {
+    J.push_back({w1 + (long long)l * w1_stride, dst1 + (long long)l * frl_packed_floats(3 * F), 3 * F, 3 * F});
+    J.push_back({w2list ? w2list[l] : w2 + (long long)l * w2_stride, dst2 + (long long)l * frl_packed_floats(F), F, F});
   }
+}
+
+int launch_frag_jobs(const std::vector<FragJob>& J, hipStream_t s) {
+  for (size_t i = 0; i < J.size(); i += FRAG_JOBS)
+    FX_TRY(launch_pack_frag(J.data() + i, (int)std::min<size_t>(FRAG_JOBS, J.size() - i), s));
   return FX_OK;
+}
+
+// whether fx_mstcn_fwd ran the fused layers (and so packed the backward chain's weights into `saved`)
+bool mstcn_fwd_fused(const fx_mstcn_params* p, int nvid, bool ragged, int rows, const float* saved) {
+  return p->fused_layers && !p->layernorm && frl_supported(p->F, saved, p->F, p->F) && (!ragged || nvid <= 16) &&
+         (p->fused_layers == 2 || frl_fills_device(rows));
 }
 
 int layer_dilation(const fx_mstcn_params* p, int i) {
@@ -635,11 +636,17 @@ int fx_mstcn_fwd(const fx_mstcn_params* p, const float* x, long long ldx, int T,
     FX_CHECK_HIP(hipMemcpy2DAsync(h0, F * sizeof(float), x, ldx * sizeof(float), F * sizeof(float), rows,
                                   hipMemcpyDeviceToDevice, s));
   }
-  const bool fused = p->fused_layers && !p->layernorm && frl_supported(F, saved, F, F) &&
-                     (!q.off || q.nvid <= 16) && (p->fused_layers == 2 || frl_fills_device(rows));
-  if (fused && p->num_layers > 0)
-    FX_TRY(pack_frag_layers(p->num_layers, F, workspace + L.wf, 3LL * F * F, p->w_pw, nullptr, 0, workspace + L.wk1,
-                            workspace + L.wk2, s));
+  const bool fused = mstcn_fwd_fused(p, q.nvid, q.off != nullptr, rows, saved);
+  if (fused && p->num_layers > 0) {
+    // one launch: this pass's weights (conv from the pack above, 1x1 as given) and the backward chain's
+    // (the dX-packed conv and transposed 1x1 weights packed above into `saved`), so the backward packs none
+    std::vector<FragJob> J;
+    frag_layer_jobs(J, p->num_layers, F, workspace + L.wf, 3LL * F * F, p->w_pw, nullptr, 0, workspace + L.wk1,
+                    workspace + L.wk2);
+    frag_layer_jobs(J, p->num_layers, F, saved + L.wbs, 3LL * F * F, nullptr, saved + L.wpts, (long long)F * F,
+                    saved + L.wk1b, saved + L.wk2b);
+    FX_TRY(launch_frag_jobs(J, s));
+  }
   for (int i = 0; i < p->num_layers; ++i) {
     const float* hi = saved + L.h + i * L.rowsF;
     float* hn = saved + L.h + (i + 1) * L.rowsF;
@@ -707,14 +714,19 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   const bool fchain = p->fused_layers && !p->layernorm && (!drop || defer) && NL > 0 &&
                       frl_supported(F, ws + L.buf0, F, F) && (!q.off || q.nvid <= 16) &&
                       (p->fused_layers == 2 || frl_fills_device(rows));
-  // the dX-packed conv weights come from the forward (saved); the fused chain also needs the
-  // transposed 1x1 weights (repacked here, into the workspace), both then in fragment order
-  if (fchain) {
-    FX_TRY(pack_conv_weights(p, ws, ws + L.wb, ws + L.wpt, L, s));
-    FX_TRY(pack_frag_layers(NL, F, ws + L.wb, 3LL * F * F, nullptr, ws + L.wpt, (long long)F * F, ws + L.wk1,
-                            ws + L.wk2, s));
+  // the dX-packed conv weights and the transposed 1x1 weights come from the forward (saved); the fused
+  // chain reads both in fragment order, which the fused forward packed too (else packed here)
+  const float* wk1 = saved + L.wk1b;
+  const float* wk2 = saved + L.wk2b;
+  if (fchain && !mstcn_fwd_fused(p, q.nvid, q.off != nullptr, rows, saved)) {
+    std::vector<FragJob> J;
+    frag_layer_jobs(J, NL, F, saved + L.wbs, 3LL * F * F, nullptr, saved + L.wpts, (long long)F * F, ws + L.wk1,
+                    ws + L.wk2);
+    FX_TRY(launch_frag_jobs(J, s));
+    wk1 = ws + L.wk1;
+    wk2 = ws + L.wk2;
   }
-  const float* wbp = fchain ? ws + L.wb : saved + L.wbs;
+  const float* wbp = saved + L.wbs;
   float* spl = ws + L.split;     // split-K partials of the weight-gradient GEMMs (side stream)
   float* spm = ws + L.split2;    // ... of the main stream's GEMMs / LN backward
   // dZ_i = (g . W_pw,i) * (z_i > 0) with W_pw,i^T packed row-major by the forward: the B operand
@@ -802,7 +814,7 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
     FX_TRY(wait_side(i + 2));
     if (i == 0) {   // the bottom layer: conv backward only
       fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dZi, F, F, layer_dilation(p, 0), -1, q, false),
-                                 op_rows(ws + L.wb, 3 * F), dHi, F);
+                                 op_rows(wbp, 3 * F), dHi, F);
       d.resid = gU;
       d.ld_resid = F;
       prof_begin(0, s);
@@ -813,8 +825,8 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
       const float* zn = saved + L.z + (i - 1) * L.rowsF;
       prof_begin(7, s);
       FX_TRY(launch_frl(dZi, F, rows, T, layer_dilation(p, i), -1, q.off, q.nvid,
-                        ws + L.wk1 + (long long)i * 3 * F * F, nullptr, 0, gU, F, dHi, F,
-                        ws + L.wk2 + (long long)(i - 1) * F * F, nullptr, nullptr, 0, zn, F, dZn, F, 0.f, 0, s));
+                        wk1 + (long long)i * 3 * F * F, nullptr, 0, gU, F, dHi, F,
+                        wk2 + (long long)(i - 1) * F * F, nullptr, nullptr, 0, zn, F, dZn, F, 0.f, 0, s));
       prof_end(7, s, 2.0 * rows * F * 4.0 * F, 4.0 * (4.0 * rows * F + 4.0 * F * F));
       FX_TRY(fork(1));
       FX_TRY(linear_dwdb(dHi, F, zn, F, rows, F, F, g->w_pw[i - 1], g->b_pw[i - 1], 1, spl, sd));
@@ -893,8 +905,8 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
       if (NL > 1) prof_begin(7, s);   // (the chain of NL - 1 back-to-back launches timed as one)
       for (int i = NL - 1; i >= 1; --i) {
         FX_TRY(launch_frl(dZall + i * L.rowsF, F, rows, T, layer_dilation(p, i), -1, q.off, q.nvid,
-                          ws + L.wk1 + (long long)i * 3 * F * F, nullptr, 0, dHall + i * L.rowsF, F,
-                          dHall + (i - 1) * L.rowsF, F, ws + L.wk2 + (long long)(i - 1) * F * F, nullptr, nullptr, 0,
+                          wk1 + (long long)i * 3 * F * F, nullptr, 0, dHall + i * L.rowsF, F,
+                          dHall + (i - 1) * L.rowsF, F, wk2 + (long long)(i - 1) * F * F, nullptr, nullptr, 0,
                           saved + L.z + (i - 1) * L.rowsF, F, dZall + (i - 1) * L.rowsF, F, 0.f, 0, s,
                           drop ? p->dropout : 0.f, fx_drop_subseed(p->seed, i - 1),
                           drop ? dBall + (i - 1) * L.rowsF : nullptr, F));

@@ -337,18 +337,21 @@ __global__ __launch_bounds__(FT) void frl_kernel(FrlArgs g) {
 
 // Weight matrices [FN][K] (row-major, leading dim ld) -> MFMA fragment order for frl_kernel:
 // dst[((st * 8 + w) * 4 + q) * 64 + lane] = float4(src[n = 32 w + lane % 32][32 st + 16 (lane / 32) + 4 q ..])
+// Up to FRAG_JOBS matrices per launch, each with its own K and leading dim (a layer stack's conv and 1x1
+// weights, forward and backward orientations, in one launch); blocks past a matrix's K stages exit.
 struct PackFragArgs {
-  const float* src[32];
-  float* dst[32];
-  long long ld;
-  int K;
+  const float* src[FRAG_JOBS];
+  float* dst[FRAG_JOBS];
+  int ld[FRAG_JOBS];
+  int K[FRAG_JOBS];
 };
 
 __global__ __launch_bounds__(256) void pack_frag_kernel(PackFragArgs a) {
   const int st = blockIdx.x, w = blockIdx.y, m = blockIdx.z;
+  if (st * FBK >= a.K[m]) return;
   const int q = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int n = w * 32 + (lane & 31), k = st * FBK + 16 * (lane >> 5) + 4 * q;
-  const float4 v = ld4(a.src[m] + (long long)n * a.ld + k);
+  const float4 v = ld4(a.src[m] + (long long)n * a.ld[m] + k);
   st4(a.dst[m] + ((long long)((st * 8 + w) * 4 + q) * 64 + lane) * 4, v);
 }
 
@@ -379,16 +382,19 @@ bool frl_supported(int F, const void* x, long long ldx, long long ld_other) {
 
 long long frl_packed_floats(int K) { return (long long)FN * K; }
 
-int launch_pack_frag(const float* const* src, float* const* dst, int n, long long ld, int K, hipStream_t s) {
-  FX_REQUIRE(n >= 1 && n <= 32 && K % FBK == 0 && ld % 4 == 0, "pack_frag: 1..32 matrices, K % 32 == 0");
+int launch_pack_frag(const FragJob* jobs, int n, hipStream_t s) {
+  FX_REQUIRE(n >= 1 && n <= FRAG_JOBS, "pack_frag: 1..48 matrices per launch");
   PackFragArgs a{};
+  int kmax = 0;
   for (int i = 0; i < n; ++i) {
-    a.src[i] = src[i];
-    a.dst[i] = dst[i];
+    FX_REQUIRE(jobs[i].K % FBK == 0 && jobs[i].ld % 4 == 0 && jobs[i].ld >= jobs[i].K, "pack_frag: K % 32 == 0");
+    a.src[i] = jobs[i].src;
+    a.dst[i] = jobs[i].dst;
+    a.ld[i] = jobs[i].ld;
+    a.K[i] = jobs[i].K;
+    kmax = std::max(kmax, jobs[i].K);
   }
-  a.ld = ld;
-  a.K = K;
-  hipLaunchKernelGGL(pack_frag_kernel, dim3(K / FBK, FN / 32, n), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(pack_frag_kernel, dim3(kmax / FBK, FN / 32, n), dim3(256), 0, s, a);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }

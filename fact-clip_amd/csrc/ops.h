@@ -169,7 +169,14 @@ bool frl_supported(int F, const void* x, long long ldx, long long ld_other);
 // vs 12.0 ms per step; the shipped yaml's 4096 + 2900 rows, 86 %: the fused layer 0.5 ms faster)
 bool frl_fills_device(long long rows);
 long long frl_packed_floats(int K);
-int launch_pack_frag(const float* const* src, float* const* dst, int n, long long ld, int K, hipStream_t s);
+// one matrix [FN][K] (leading dim ld) -> fragment order at dst (frl_packed_floats(K) floats)
+struct FragJob {
+  const float* src;
+  float* dst;
+  int ld, K;
+};
+constexpr int FRAG_JOBS = 48;   // matrices per pack launch
+int launch_pack_frag(const FragJob* jobs, int n, hipStream_t s);
 int launch_frl(const float* x, long long ldx, int M, int T, int dil, int dir, const int* seq_off, int nseq,
                const float* w1p, const float* bias1, int relu1, const float* resid1, long long ldr1, float* out1,
                long long ldo1, const float* w2p, const float* bias2, const float* resid2, long long ldr2,
