@@ -529,6 +529,7 @@ const Knobs& knobs() {
     if (const char* p = env("FX_SPLIT_VARIANT")) k.split_variant = std::atoi(p);
     if (const char* p = env("FX_MSTCN_TAIL")) k.mstcn_tail = p[0] != '0';
     if (const char* p = env("FX_MSTCN_DW_HALVES")) k.mstcn_dw_halves = p[0] != '0';
+    if (const char* p = env("FX_MSTCN_TAIL_SPLIT")) k.mstcn_tail_split = std::atoi(p);
     if (const char* p = env("FX_DIRECT_CPW")) k.direct_cpw = std::max(1, std::min(8, std::atoi(p)));
     if (const char* p = env("FX_X2Y_F2A_BWD")) k.x2y_f2a_bwd = p[0] != '0';
   });
@@ -893,7 +894,15 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
     // FX_MSTCN_DW_HALVES=1: the layers above `half` get their weight gradients as soon as the chain has
     // passed them (overlapping the chain's remaining layers), the rest after the chain.  Measured no
     // better than one batched launch after the chain (the early half slows the chain it overlaps): off
-    const int half = (knobs().mstcn_dw_halves && !fchain) ? NL / 2 : 0;
+    // The input block's stack (in_map) is the last work of the backward pass: after its chain the side
+    // stream's batched dW runs alone on the device (~0.7 ms at T = 4096 x 2).  FX_MSTCN_TAIL_SPLIT=k has
+    // the fused chain launch the dW of the layers >= k as soon as it has passed them, overlapping its own
+    // remaining layers and the input map's dX (measured no faster: off by default)
+    int half = (knobs().mstcn_dw_halves && !fchain) ? NL / 2 : 0;
+    if (fchain && p->in_map && NL > 1) {
+      const int k = knobs().mstcn_tail_split;
+      half = k < 0 ? NL / 2 : std::min(k, NL - 1);
+    }
     if (fchain) {
       // the fused chain into the per-layer slots: dZ_NL-1 by the 1x1 backward GEMM, then per layer ONE
       // kernel for dH_i (-> dHall[i-1]) and dZ_i-1 (-> dZall[i-1]); the bottom layer's conv backward
@@ -910,6 +919,8 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
                           saved + L.z + (i - 1) * L.rowsF, F, dZall + (i - 1) * L.rowsF, F, 0.f, 0, s,
                           drop ? p->dropout : 0.f, fx_drop_subseed(p->seed, i - 1),
                           drop ? dBall + (i - 1) * L.rowsF : nullptr, F));
+        // (dZ_j, dH_j+1 of every layer j >= i - 1 exist now)
+        if (half > 0 && i == half) FX_TRY(batched_dw(half, NL - half));
       }
       if (NL > 1)
         prof_end(7, s, (NL - 1) * 2.0 * rows * F * 4.0 * F, (NL - 1) * 4.0 * (4.0 * rows * F + 4.0 * F * F), NL - 1);
@@ -924,17 +935,19 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
                                 F, s));
         FX_TRY(pw_dx(dBall + i * L.rowsF, i, dZ, zi));
       }
-      float* dHn = i > 0 ? dHall + (i - 1) * L.rowsF : Hb[0];
+      // the bottom layer's dH is the stack's input gradient: straight into dx when there is no input map
+      const bool to_dx = i == 0 && !p->in_map && dx;
+      float* dHn = i > 0 ? dHall + (i - 1) * L.rowsF : (to_dx ? dx : Hb[0]);
       fx_gemm_desc d = gemm_desc(rows, F, 3 * F, conv_operand(dZ, F, F, layer_dilation(p, i), -1, q, false),
-                                 op_rows(wbp + (long long)i * 3 * F * F, 3 * F), dHn, F);
+                                 op_rows(wbp + (long long)i * 3 * F * F, 3 * F), dHn, to_dx ? lddx : F);
       d.resid = gU;
       d.ld_resid = F;
       prof_begin(0, s);
       FX_TRY(launch_gemm(d, s));
       prof_end(0, s, 2.0 * rows * F * 3.0 * F, 4.0 * (3.0 * rows * F + 3.0 * F * F));
-      if (half > 0 && i == half) FX_TRY(batched_dw(half, NL - half));
+      if (!fchain && half > 0 && i == half) FX_TRY(batched_dw(half, NL - half));
     }
-    dH = Hb[0];
+    dH = (!p->in_map && dx) ? nullptr : Hb[0];   // (nullptr: already in dx)
     FX_TRY(batched_dw(0, half > 0 ? half : NL));
   }
   for (int i = NL - 1; !fchain && !defer && i >= 0; --i) {
@@ -993,7 +1006,7 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
       FX_TRY(linear_dwdb(dH, F, x, ldx, rows, p->cin, F, g->w_in, g->b_in, 1, spl, sd));
     }
     if (dx) FX_TRY(linear_dx(dH, F, p->w_in, rows, p->cin, F, dx, lddx, 0, nullptr, 0, spm, s));
-  } else if (dx) {
+  } else if (dx && dH) {
     FX_CHECK_HIP(hipMemcpy2DAsync(dx, lddx * sizeof(float), dH, F * sizeof(float), F * sizeof(float), rows,
                                   hipMemcpyDeviceToDevice, s));
   }

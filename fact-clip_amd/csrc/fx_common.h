@@ -167,6 +167,10 @@ struct Knobs {
   int direct_cpw = 1;       // FX_DIRECT_CPW: 32-deep k chunks per wave of the direct (small) GEMM kernel (1 vs 2: direct-kernel time 2.74 -> 2.61 ms/step)
   bool mstcn_dw_halves = false; // FX_MSTCN_DW_HALVES=1: upper half of the batched MS-TCN dW mid-chain (A/B: no gain)
   bool mstcn_tail = false;  // FX_MSTCN_TAIL=1: the input block's MS-TCN keeps per-layer side dW (A/B: even)
+  int mstcn_tail_split = 0;  // FX_MSTCN_TAIL_SPLIT=k: the input block's fused chain launches the batched dW of
+                             // layers >= k once it has passed them (-1: NL / 2; 0: all after the chain).
+                             // A/B at T = 4096 x 2 (4 alternating rounds of 40 steps): k = 5 no faster, and
+                             // the overlapped dW slows the chain (fused-layer 0.525 -> 0.508): off
 };
 const Knobs& knobs();
 
