@@ -636,6 +636,7 @@ def run(net, vb, compute_loss, early=None):
         terms[i].K = len(matches[v][0])
     _stamp("fill")
     pk2.send()
+    _stamp("send")
     plan = dict(terms_host=terms, terms_dev=base2 + t_off, nterms=nterms, coef_dev=base2 + coef_off, nout=nout,
                 ws=ws, grads=grads, keep=(early, pk2, pke, scr, sims, flog, text_seen))
     out = _LossFn.apply(plan, *inputs)

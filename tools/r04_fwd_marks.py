@@ -107,7 +107,7 @@ def main():
         step()
         torch.cuda.synchronize()
     if vloss.RUN_TIMES:
-        t = vloss.RUN_TIMES[-14:]
+        t = vloss.RUN_TIMES[-15:]
         for (a, ta), (b, tb) in zip(t, t[1:]):
             print(f"run: {a:>12s} -> {b:12s} {1e6 * (tb - ta):8.1f} us")
     h0, e0 = MARKS[0][1], MARKS[0][2]
