@@ -531,7 +531,7 @@ const Knobs& knobs() {
     if (const char* p = env("FX_MSTCN_DW_HALVES")) k.mstcn_dw_halves = p[0] != '0';
     if (const char* p = env("FX_MSTCN_TAIL_SPLIT")) k.mstcn_tail_split = std::atoi(p);
     if (const char* p = env("FX_DIRECT_CPW")) k.direct_cpw = std::max(1, std::min(8, std::atoi(p)));
-    if (const char* p = env("FX_X2Y_F2A_BWD")) k.x2y_f2a_bwd = p[0] != '0';
+    if (const char* p = env("FX_X2Y_F2A_BWD")) k.x2y_f2a_bwd = std::atoi(p);
   });
   return k;
 }
@@ -1813,7 +1813,9 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
   const double core_bytes = 4.0 * (2.0 * Ny * Hd + 4.0 * Nx * Hd + 4.0 * na + (double)Ny * Hd);
   // the fused f2a core (bracketed as fx_prof kind 6 only when it runs: the per-video GEMM fallback below
   // is not the kernel whose algorithmic bytes kind 6 reports)
-  const bool f2a_fused = !fused && knobs().x2y_fused && knobs().x2y_f2a_bwd &&
+  const int f2a_mode = knobs().x2y_f2a_bwd;
+  const bool f2a_fused = !fused && knobs().x2y_fused &&
+                         (f2a_mode == 1 || (f2a_mode == 2 && x2y_f2a_chunks(V.n, V.x.data()) >= 64)) &&
                          x2y_f2a_fusable(V.n, V.x.data(), V.y.data(), Hd) && (cw & 3) == 0 && al16;
   if (fused) prof_begin(4, s);
   else if (f2a_fused) prof_begin(6, s);

@@ -162,7 +162,9 @@ struct Knobs {
   bool mstcn_defer = true;
   int side_maxwg = 0;
   bool x2y_fused = true;    // FX_X2Y_FUSED=0: the X2Y attention core as grouped GEMM + softmax launches
-  bool x2y_f2a_bwd = false; // FX_X2Y_F2A_BWD=1: the fused f2a backward core (correct vs the oracle, measured no faster than the grouped GEMMs)
+  int x2y_f2a_bwd = 2;      // FX_X2Y_F2A_BWD: the fused f2a backward core (one workgroup per 64-key chunk) 1 always,
+                            // 0 never (grouped GEMMs), 2 when the call has >= 64 chunks: at 8192 frames 145 vs
+                            // ~180 us for the grouped GEMMs; with a few hundred segments (3-4 chunks) 80 vs ~56 us
   int split_variant = 0;    // FX_SPLIT_VARIANT=1: the LDS-image split kernel for every FX_PREC_F32S GEMM
   int direct_cpw = 1;       // FX_DIRECT_CPW: 32-deep k chunks per wave of the direct (small) GEMM kernel (1 vs 2: direct-kernel time 2.74 -> 2.61 ms/step)
   bool mstcn_dw_halves = false; // FX_MSTCN_DW_HALVES=1: upper half of the batched MS-TCN dW mid-chain (A/B: no gain)

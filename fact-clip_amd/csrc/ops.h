@@ -71,6 +71,8 @@ int launch_x2y_a2f_fwd(const float* yq, const float* xk, const float* xv, int Hd
 // long key side (f2a: <= 64 queries per video over up to T keys): chunk kernel + ordered merge; ws holds
 // x2y_f2a_ws_floats(...) floats of per-chunk partials
 bool x2y_f2a_fusable(int nvid, const int* xoff, const int* yoff, int Hd);
+// 64-key chunks (= workgroups of the fused f2a backward passes) of a call
+long long x2y_f2a_chunks(int nvid, const int* xoff);
 long long x2y_f2a_ws_floats(int nvid, const int* xoff, int Hd);
 int launch_x2y_f2a_fwd(const float* yq, const float* xk, const float* xv, int Hd, float scale, int nvid,
                        const int* yoff, const int* xoff, const long long* aoff, float* logit, float* attn,

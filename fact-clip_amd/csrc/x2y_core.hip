@@ -941,6 +941,12 @@ bool x2y_f2a_fusable(int nvid, const int* xoff, const int* yoff, int Hd) {
   return nch > 0;
 }
 
+long long x2y_f2a_chunks(int nvid, const int* xoff) {
+  long long nch = 0;
+  for (int v = 0; v < nvid; ++v) nch += (xoff[v + 1] - xoff[v] + FC - 1) / FC;
+  return nch;
+}
+
 long long x2y_f2a_ws_floats(int nvid, const int* xoff, int Hd) {
   long long nch = 0;
   for (int v = 0; v < nvid; ++v) nch += (xoff[v + 1] - xoff[v] + FC - 1) / FC;

@@ -7,8 +7,9 @@ upstream gradients on all three outputs.  The reference's losses read attn_logit
 491-492; attn feeds the matching and eval, blocks.py:96, 243-281), so X2YFn marks attn non-differentiable;
 the C entry point still takes a dattn (fx_x2y_bwd), and this test reaches it through a subclass whose
 attn output is differentiable, so the cores' dP += dattn paths are checked against the oracle too.  The
-opt-in fused f2a backward core (FX_X2Y_F2A_BWD=1; library knobs are read once per process) runs the f2a
-cases in a child process."""
+fused f2a backward core runs by default for calls of >= 64 key chunks (the 4096 + 300 frame case); every
+f2a case runs again through it in a child process (FX_X2Y_F2A_BWD=1; library knobs are read once per
+process)."""
 import math
 import os
 import subprocess
@@ -44,7 +45,8 @@ def _params(xdim, ydim, outdim, seed):
                                              ("a2f", 64, (129, 64)), ("a2f", 75, (300, 200)),
                                              ("f2a", 32, (700, 413)), ("f2a", 40, (300, 257, 65)),
                                              ("f2a", 64, (64, 1)), ("f2a", 75, (200, 90)),
-                                             ("a2f", 32, (1,)), ("f2a", 7, (3000,))])
+                                             ("a2f", 32, (1,)), ("f2a", 7, (3000,)),
+                                             ("f2a", 32, (4096, 300))])
 def test_x2y_vs_oracle(direction, nq, Ts):
     check_x2y(direction, nq, Ts)
 
