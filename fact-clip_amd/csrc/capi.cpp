@@ -532,6 +532,7 @@ const Knobs& knobs() {
     if (const char* p = env("FX_MSTCN_TAIL_SPLIT")) k.mstcn_tail_split = std::atoi(p);
     if (const char* p = env("FX_DIRECT_CPW")) k.direct_cpw = std::max(1, std::min(8, std::atoi(p)));
     if (const char* p = env("FX_X2Y_F2A_BWD")) k.x2y_f2a_bwd = std::atoi(p);
+    if (const char* p = env("FX_X2Y_F2A_ONE")) k.x2y_f2a_one = p[0] != '0';
   });
   return k;
 }

@@ -162,6 +162,7 @@ struct Knobs {
   bool mstcn_defer = true;
   int side_maxwg = 0;
   bool x2y_fused = true;    // FX_X2Y_FUSED=0: the X2Y attention core as grouped GEMM + softmax launches
+  bool x2y_f2a_one = true;  // FX_X2Y_F2A_ONE=0: the fused f2a backward as two launches (dP pass, dlogit pass)
   int x2y_f2a_bwd = 2;      // FX_X2Y_F2A_BWD: the fused f2a backward core (one workgroup per 64-key chunk) 1 always,
                             // 0 never (grouped GEMMs), 2 when the call has >= 64 chunks: at 8192 frames 145 vs
                             // ~180 us for the grouped GEMMs; with a few hundred segments (3-4 chunks) 80 vs ~56 us

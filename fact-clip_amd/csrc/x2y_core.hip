@@ -478,12 +478,39 @@ struct F2aBwdArgs {
   float* dyq;           // (Ny, Hd)
   float* part;          // (chunks, FMAXQ, Hd)
   float* stats;         // (chunks, FMAXQ, 2)
+  unsigned* bar;        // one-launch form: {arrivals, ..., exits at +32} of the stream's counter pool
   int Hd, nvid;
   float scale;
   int yoff[FX_X2Y_MAXV + 1], xoff[FX_X2Y_MAXV + 1];
   long long aoff[FX_X2Y_MAXV + 1];
   int ch_off[FX_X2Y_MAXV + 1];
 };
+
+// write-through (sc1) buffer access for the one-launch form's hand-off of the row-dot partials
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t f2a_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
+}
+
+// Grid barrier of the one-launch form (every workgroup co-resident: grid <= 256): each workgroup's
+// write-through stores acknowledged (vmcnt 0) before its arrival; the last workgroup past the barrier
+// re-arms the slot.  Bounded spin (~1 s): on timeout the workgroup goes on (results wrong, never a hang)
+__device__ __forceinline__ void f2a_grid_sync(unsigned* bar) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned G = gridDim.x;
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned n = 0;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < G && ++n < (1u << 22))
+      __builtin_amdgcn_s_sleep(1);
+    const unsigned prev = __hip_atomic_fetch_add(bar + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == G - 1) {   // every workgroup is past the barrier
+      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(bar + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+}
 
 __device__ __forceinline__ void f2ab_video(const F2aBwdArgs& a, int v, int& y0, int& ny, int& x0, int& nx, long long& ao,
                                            int& c0) {
@@ -532,6 +559,8 @@ __device__ __forceinline__ void keys_out(const float (*L)[FC + 1], const float* 
   }
 }
 
+// PASS 1: dP, its row-dot partials, dxv; PASS 2: dlogit, dxk, the dyq partials (reading dP back);
+// PASS 3: both in one launch, dP kept in LDS, a grid barrier for the row dots in between
 template <int PASS>
 __global__ __launch_bounds__(XT) void x2y_f2a_bwd_kernel(F2aBwdArgs a) {
   __shared__ float red[8][16][64];
@@ -567,7 +596,7 @@ __global__ __launch_bounds__(XT) void x2y_f2a_bwd_kernel(F2aBwdArgs a) {
   }
   __syncthreads();
 
-  if (PASS == 1) {
+  if (PASS != 2) {
     // ---- dP = dfeat . xv_c^T (+ dattn): blocks (query block rb, key block cb), waves split Hd ----
     const int nrb = ny > 32 ? 2 : 1, nblk = 2 * nrb, wpb = 8 / nblk;
     const int blk = w % nblk, kpart = w / nblk, rb = blk >> 1, cb = blk & 1;
@@ -619,18 +648,37 @@ __global__ __launch_bounds__(XT) void x2y_f2a_bwd_kernel(F2aBwdArgs a) {
       for (int j = 0; j < 8; ++j) {
         const int col = c8 + 8 * j;
         if (row < ny && col < keys) {
-          a.dL[ao + (long long)row * nx + k0c + col] = S[row][col];
+          if (PASS == 1) a.dL[ao + (long long)row * nx + k0c + col] = S[row][col];
           part += Pa[row][col] * S[row][col];
         }
       }
 #pragma unroll
       for (int o = 4; o >= 1; o >>= 1) part += __shfl_xor(part, o, 8);
-      if (c8 == 0 && row < ny) a.stats[((long long)chunk * FMAXQ + row) * 2] = part;
+      if (c8 == 0 && row < ny) {
+        const long long si = ((long long)chunk * FMAXQ + row) * 2;
+        if (PASS == 3) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(part), f2a_rsrc(a.stats), (int)(si * 4), 0, 16);
+        else a.stats[si] = part;
+      }
     }
     // dxv_c = attn_c^T . dfeat
     keys_out(Pa, a.dfeat + (long long)y0 * a.ldf, a.ldf, ny, keys, Hd, 1.f, a.dxv + (long long)(x0 + k0c) * Hd, w, li,
              lh);
-  } else {
+  }
+  if (PASS == 3) {
+    // every chunk's row-dot partial written through: the row sums of this video's chunks
+    f2a_grid_sync(a.bar);
+    if (tid < FMAXQ) {
+      const int nch = (nx + FC - 1) / FC;
+      float sum = 0.f;
+      if (tid < ny)
+        for (int c = 0; c < nch; ++c)
+          sum += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+              f2a_rsrc(a.stats), (int)(((long long)(c0 + c) * FMAXQ + tid) * 2 * 4), 0, 16));
+      rdot[tid] = sum;
+    }
+    __syncthreads();
+  }
+  if (PASS != 1) {
     // ---- dlogit = attn (dP - rowdot) (+ direct) -> dL and LDS ----
     for (int e = tid; e < FMAXQ * FC; e += XT) {
       const int y = e / FC, x = e - y * FC;
@@ -1025,8 +1073,15 @@ int launch_x2y_f2a_bwd(const float* dfeat, long long ldf, const float* xv, const
   a.part = ws;
   a.stats = ws + (long long)nch * FMAXQ * Hd;
   if (nch == 0 || maxq == 0) return FX_OK;
-  hipLaunchKernelGGL(x2y_f2a_bwd_kernel<1>, dim3(nch), dim3(XT), 0, s, a);
-  hipLaunchKernelGGL(x2y_f2a_bwd_kernel<2>, dim3(nch), dim3(XT), 0, s, a);
+  // one launch when every chunk's workgroup can be resident at once (the grid barrier waits for all of
+  // them): <= 256 chunks; FX_X2Y_F2A_ONE=0 keeps the two launches (A/B)
+  a.bar = (knobs().x2y_f2a_one && nch <= 256) ? arrival_counters(s) : nullptr;
+  if (a.bar) {
+    hipLaunchKernelGGL(x2y_f2a_bwd_kernel<3>, dim3(nch), dim3(XT), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(x2y_f2a_bwd_kernel<1>, dim3(nch), dim3(XT), 0, s, a);
+    hipLaunchKernelGGL(x2y_f2a_bwd_kernel<2>, dim3(nch), dim3(XT), 0, s, a);
+  }
   hipLaunchKernelGGL(x2y_f2a_bwd_merge_kernel, dim3(maxq, nvid), dim3(XT), 0, s, a);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;

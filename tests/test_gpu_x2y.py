@@ -51,11 +51,13 @@ def test_x2y_vs_oracle(direction, nq, Ts):
     check_x2y(direction, nq, Ts)
 
 
-def test_x2y_f2a_fused_backward_vs_oracle():
-    """The f2a cases again with the fused f2a backward core switched on (child process: the knob is
-    read when the library loads)."""
+@pytest.mark.parametrize("one_launch", ["1", "0"])
+def test_x2y_f2a_fused_backward_vs_oracle(one_launch):
+    """The f2a cases again with the fused f2a backward core switched on for every call, as one launch
+    with a grid barrier between the dP and dlogit passes (default) and as two launches
+    (FX_X2Y_F2A_ONE=0); child processes: the knobs are read when the library loads."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, FX_X2Y_F2A_BWD="1")
+    env = dict(os.environ, FX_X2Y_F2A_BWD="1", FX_X2Y_F2A_ONE=one_launch)
     p = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), "f2a"], env=env, cwd=root, timeout=240)
     assert p.returncode == 0, p.returncode
 
