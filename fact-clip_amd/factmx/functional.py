@@ -1126,10 +1126,14 @@ class GRUFn(torch.autograd.Function):
 
 
 def gru(mod, x, seq_off=None):
-    """Run an ``nn.GRU(bidirectional=True)`` module's parameters layer by layer through GRUFn."""
+    """Run an ``nn.GRU(bidirectional=True)`` module's parameters layer by layer through GRUFn; in
+    training, ``mod.dropout`` on every layer's output but the last (nn.GRU's inter-layer dropout)."""
     assert mod.bidirectional and not mod.batch_first
     h = _2d(x)
+    p_drop = float(mod.dropout) if (mod.training and mod.num_layers > 1) else 0.0
     for layer in range(mod.num_layers):
+        if layer and p_drop:
+            h = torch.nn.functional.dropout(h, p_drop, True)
         p = [getattr(mod, f"{n}_l{layer}{s}") for s in ("", "_reverse")
              for n in ("weight_ih", "weight_hh", "bias_ih", "bias_hh")]
         h = GRUFn.apply(h, seq_off, *p)

@@ -215,7 +215,9 @@ class MSTCN2(nn.Module):
 
 
 class ActionUpdate_GRU(nn.Module):
-    """basic.py:283-308 (transcript-conditioned action branch; not on the FACT_CLIP path)."""
+    """basic.py:283-308 (transcript-conditioned action branch; not on the FACT_CLIP path).  The
+    bidirectional GRU runs through the library's BiGRU (``fxf.gru``: every layer one GRUFn, the
+    tokens as one sequence), the LayerNorm and output map through fxf as well."""
 
     def __init__(self, in_dim, hid_dim, out_dim, n_layers, dropout=0.5, layer_norm_eps=1e-5, out_map=False):
         super().__init__()
@@ -229,7 +231,7 @@ class ActionUpdate_GRU(nn.Module):
             self.out_map = nn.Identity()
 
     def forward(self, tgt, memory, pos=None, query_pos=None):
-        out, _ = self.gru(tgt)
+        out = fxf.gru(self.gru, tgt)
         out = _as3d(fxf.layer_norm(out, self.layernorm.weight, self.layernorm.bias, self.layernorm.eps))
         if isinstance(self.out_map, nn.Linear):
             out = _as3d(fxf.linear(out, self.out_map.weight, self.out_map.bias))
