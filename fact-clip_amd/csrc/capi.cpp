@@ -519,6 +519,7 @@ const Knobs& knobs() {
     if (const char* p = env("FX_FRL_MIN_FILL")) k.frl_min_fill = std::atoi(p);
     if (const char* p = env("FX_AUX_STREAM")) k.aux_stream = p[0] != '0';
     if (const char* p = env("FX_GRU_POLL2")) k.gru_poll2 = p[0] != '0';
+    if (const char* p = env("FX_GRU_XCD")) k.gru_xcd = p[0] != '0';
     if (const char* p = env("FX_GRU_BWD_GATE_WAVE")) k.gru_bwd_gate_wave = p[0] != '0';
     if (const char* p = env("FX_GRU_STORE_WAVE")) k.gru_store_wave = std::max(0, std::min(2, std::atoi(p)));
     if (const char* p = env("FX_TATTN_RR")) k.tattn_rr = p[0] != '0';

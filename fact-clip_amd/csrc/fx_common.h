@@ -145,6 +145,7 @@ struct Knobs {
   bool tattn_fold = true;        // FX_TATTN_FOLD=0: the register-resident kernels' merge as a second launch (A/B)
   bool tattn_rr = true;          // FX_TATTN_RR=0: the LDS-staged attention-over-T kernels for head dim 32 too (A/B)
   int tattn_tc_max = 256;       // FX_TATTN_TC: largest key chunk per attention-over-T workgroup (32..256, A/B)
+  bool gru_xcd = false;         // FX_GRU_XCD=1: a GRU direction's workgroups on one XCD (A/B: fwd 1.88-1.95 vs 1.86 us, bwd 2.27-2.28 vs 2.19-2.20 us per step spread; off)
   bool gru_poll2 = true;        // FX_GRU_POLL2=0: one granule poll in flight per lane (A/B)
   int gru_store_wave = 2;        // FX_GRU_STORE_WAVE: GRU forward table stores -- 0 by wave 0's gate threads, 1 staged for a fifth wave, 2 gate threads on the fifth wave (A/B)
   bool gru_bwd_gate_wave = false; // FX_GRU_BWD_GATE_WAVE=1: the GRU backward's gate threads on a fifth wave (A/B: even, 2.25 vs 2.26 us per step)
