@@ -68,9 +68,11 @@ XATTN_NOTES = {
                         "per call", "r05_pmc_x2yproj.json"),
 }
 X2Y_NOTES = {"x2y_a2f_fwd": "x2y_a2f_kernel<0> (frames attend to the action tokens: logit, attn, feat in one launch)",
-             "x2y_a2f_bwd": "x2y_a2f_kernel<1> + grouped dxv / dxk GEMM launch",
+             "x2y_a2f_bwd": "x2y_a2f_kernel<1> + x2y_a2f_dw_kernel (weight-side dxv / dxk in one launch)",
              "x2y_f2a_fwd": "x2y_f2a_chunk_kernel + x2y_f2a_merge_kernel (tokens attend to the frames)",
-             "x2y_f2a_bwd": "f2a backward: grouped dP / dxv GEMMs, softmax backward, grouped dyq / dxk GEMMs"}
+             "x2y_f2a_bwd": "x2y_f2a_bwd_kernel (one launch: dP in LDS across a grid barrier, softmax backward, "
+                            "dxv / dxk / dyq partials) + x2y_f2a_bwd_merge_kernel; at the 8192-frame map only (>= 64 "
+                            "key chunks), the segment-level maps run grouped GEMMs"}
 D_IN, NCLS, NTOKEN, T_DEFAULT = 2048, 75, 32, 4096
 BF_NCLS, BF_NTOKEN, BF_T = 48, 60, 512   # breakfast.yaml (FACT.ntoken 60, 48 classes)
 

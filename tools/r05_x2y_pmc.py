@@ -1,7 +1,7 @@
 """Per-launch HBM bytes of the X2Y core kernels from tools/r05_x2y_pmc.sh's PMC passes, summed per
 bench bracket (fx_prof kinds 3-6): a2f fwd = x2y_a2f_kernel<0>; a2f bwd = x2y_a2f_kernel<1> +
-x2y_a2f_dw_kernel; f2a fwd = x2y_f2a_chunk_kernel + x2y_f2a_merge_kernel; f2a bwd (grouped GEMMs and a
-softmax backward, no single kernel family): not reported.  fetch = 2 x FETCH_SIZE (gfx950 wide-read
+x2y_a2f_dw_kernel; f2a fwd = x2y_f2a_chunk_kernel + x2y_f2a_merge_kernel; f2a bwd = x2y_f2a_bwd_kernel (the
+one-launch fused core, the default for calls of >= 64 key chunks) + x2y_f2a_bwd_merge_kernel.  fetch = 2 x FETCH_SIZE (gfx950 wide-read
 correction, MI355X_MICROARCH.md), write = WRITE_SIZE; KB -> B."""
 import collections
 import csv
@@ -38,7 +38,8 @@ out = {
                                                                       bytes_of(a2f, "x2y_a2f_dw_kernel")),
     "x2y_f2a_fwd": (lambda a, b: None if a is None else a + (b or 0.0))(bytes_of(f2a, "x2y_f2a_chunk_kernel"),
                                                                       bytes_of(f2a, "x2y_f2a_merge_kernel")),
-    "x2y_f2a_bwd": None,
+    "x2y_f2a_bwd": (lambda a, b: None if a is None else a + (b or 0.0))(bytes_of(f2a, "x2y_f2a_bwd_kernel"),
+                                                                      bytes_of(f2a, "x2y_f2a_bwd_merge_kernel")),
     "note": "HBM bytes per launch (fetch = 2 x FETCH_SIZE, write = WRITE_SIZE), kernels of each bench bracket "
             "summed; tools/r05_x2y_bench.py shapes (2 videos x 4096 frames, 32 tokens, head 512)",
 }
