@@ -56,7 +56,10 @@ HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 HOLDOUT = [51, 53, 61, 67, 56]   # havid_view0_lh_pt_holdout.yaml
 # fx_prof kinds of the X2Y attention cores (capi.cpp fx_x2y_fwd / fx_x2y_bwd); algorithmic bytes per call:
 # query, key and value rows, the logit / probability tiles and the attended features (+ their gradients)
-X2Y_KINDS = {3: "x2y_a2f_fwd", 4: "x2y_a2f_bwd", 5: "x2y_f2a_fwd", 6: "x2y_f2a_bwd"}
+# frame-level calls (max(Nx, Ny) >= 1024: the Update block's 2 x 4096-frame maps) and segment-level calls (the TDU
+# blocks' maps over the segments) are separate kinds, so each line's bytes and time come from one call shape
+X2Y_KINDS = {3: "x2y_a2f_fwd", 4: "x2y_a2f_bwd", 5: "x2y_f2a_fwd", 6: "x2y_f2a_bwd",
+             11: "x2y_a2f_fwd_seg", 12: "x2y_a2f_bwd_seg", 13: "x2y_f2a_fwd_seg", 14: "x2y_f2a_bwd_seg"}
 FRL_KIND = 7   # fx_prof kind of the fused MS-TCN layer kernel (mstcn_fused.hip)
 # fx_prof kinds of the cross-attention projection GEMMs (north-star measurement set)
 XATTN_KINDS = {9: "sca_kv_projection", 10: "x2y_projections"}
@@ -71,8 +74,9 @@ X2Y_NOTES = {"x2y_a2f_fwd": "x2y_a2f_kernel<0> (frames attend to the action toke
              "x2y_a2f_bwd": "x2y_a2f_kernel<1> + x2y_a2f_dw_kernel (weight-side dxv / dxk in one launch)",
              "x2y_f2a_fwd": "x2y_f2a_chunk_kernel + x2y_f2a_merge_kernel (tokens attend to the frames)",
              "x2y_f2a_bwd": "x2y_f2a_bwd_kernel (one launch: dP in LDS across a grid barrier, softmax backward, "
-                            "dxv / dxk / dyq partials) + x2y_f2a_bwd_merge_kernel; at the 8192-frame map only (>= 64 "
-                            "key chunks), the segment-level maps run grouped GEMMs"}
+                            "dxv / dxk / dyq partials) + x2y_f2a_bwd_merge_kernel"}
+for _k in list(X2Y_NOTES):
+    X2Y_NOTES[_k + "_seg"] = X2Y_NOTES[_k] + " -- segment-level calls (TDU blocks)"
 D_IN, NCLS, NTOKEN, T_DEFAULT = 2048, 75, 32, 4096
 BF_NCLS, BF_NTOKEN, BF_T = 48, 60, 512   # breakfast.yaml (FACT.ntoken 60, 48 classes)
 
@@ -310,56 +314,128 @@ def dp_schedule_overhead(net, seqs, labels, steps, rounds=3):
         dist.destroy_process_group()
 
 
+# The kernels of each timed call kind, as the rocprofv3 kernel trace names them: `frac` of the attention-over-T
+# and frame-level X2Y lines is taken from the committed trace of this bench shape (profiles/r06_trace_kernels.json,
+# tools/r06_diag.sh: per kernel the largest grid = the frame-level call), the live event timing is reported beside it
+TRACE_KERNELS = {"fwd": ["tattn_fwd32_kernel<2>"], "bwd": ["tattn_bwd32_kernel<2>"],
+                 "x2y_a2f_fwd": ["x2y_a2f_kernel<0>"], "x2y_a2f_bwd": ["x2y_a2f_kernel<1>", "x2y_a2f_dw_kernel"],
+                 "x2y_f2a_fwd": ["x2y_f2a_chunk_kernel", "x2y_f2a_merge_kernel"],
+                 "x2y_f2a_bwd": ["x2y_f2a_bwd_kernel<3>", "x2y_f2a_bwd_merge_kernel"],
+                 "frl": ["frl_kernel<true, 3>"]}
+TRACE_FILE = "r06_trace_kernels.json"
+
+
+def trace_call_us(name):
+    """Kernel time of one call of kind `name` from the committed kernel trace (sum over its kernels of each
+    kernel's average duration at its largest grid), or None."""
+    path = os.path.join(ROOT, "profiles", TRACE_FILE)
+    if name not in TRACE_KERNELS or not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            ks = json.load(f)["kernels"]
+        tot = 0.0
+        for k in TRACE_KERNELS[name]:
+            grids = ks[k]
+            tot += grids[max(grids, key=int)][1]
+        return tot
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def trace_basis(entry, name, per_call, peak, unit_scale):
+    """Re-base a roofline entry's `frac` on the committed kernel trace (per_call: algorithmic bytes or FLOPs of
+    one call; unit_scale 1e9 for GB/s, 1e12 for TFLOP/s); the live event-based values stay as `live_*`."""
+    us = trace_call_us(name)
+    if entry is None or us is None:
+        return entry
+    ach = per_call / (us * 1e-6) / unit_scale
+    entry.update(live_achieved=entry["achieved"], live_frac=entry["frac"], live_avg_launch_ms=entry["avg_launch_ms"],
+                 achieved=round(ach, 2), frac=round(ach / peak, 4), avg_launch_ms=round(us / 1e3, 5),
+                 basis=f"rocprofv3 kernel-trace average of this shape's kernels (profiles/{TRACE_FILE}); live_*: "
+                       "hipExtLaunchKernel event pairs in the first timed step (they read ~2-5 us per kernel over the "
+                       "trace on this part)")
+    return entry
+
+
+class Prof:
+    """One fx_prof kind over the sampled step(s): the calls' event brackets (kernels + any host-issue gap
+    inside the call) and the kernels alone (each kernel's own hipExtLaunchKernel event pair: its execution
+    time, as the rocprofv3 kernel trace reports it).  Every roofline below is on the KERNEL basis."""
+
+    def __init__(self, bracket_ms=0.0, flops=0.0, nbytes=0.0, calls=0, kernel_ms=0.0, kernels=0, untimed=0):
+        self.bracket_ms, self.flops, self.bytes, self.calls = bracket_ms, flops, nbytes, calls
+        self.kernel_ms, self.kernels, self.untimed = kernel_ms, kernels, untimed
+
+    def timing(self):
+        """Fields every roofline entry carries: per call, kernel time and the host gap inside the bracket."""
+        n = max(self.calls, 1)
+        return dict(basis="kernel time (hipExtLaunchKernel event pairs, = rocprofv3 kernel-trace durations)",
+                    kernel_ms_per_call=round(self.kernel_ms / n, 5), bracket_ms_per_call=round(self.bracket_ms / n, 5),
+                    host_gap_ms_per_call=round(max(self.bracket_ms - self.kernel_ms, 0.0) / n, 5),
+                    kernels_per_call=round(self.kernels / n, 2), untimed_kernels=self.untimed)
+
+
 def prof_collect(lib, kind):
-    """(total ms, flops, bytes, launches) of the HIP-event timed launches of one profiling kind."""
+    """The Prof of one profiling kind (HIP-event brackets of its calls + the kernel-time pairs inside)."""
     from factmx import native
     ms, fl, by, cnt = native.D(), native.D(), native.D(), native.I()
     native.check(lib.fx_prof_collect(kind, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(by),
                                      ctypes.byref(cnt)), "fx_prof_collect")
-    return ms, fl, by, cnt
+    kms, kn, ku = native.D(), native.I(), native.I()
+    native.check(lib.fx_prof_collect_kernels(kind, ctypes.byref(kms), ctypes.byref(kn), ctypes.byref(ku)),
+                 "fx_prof_collect_kernels")
+    return Prof(ms.value, fl.value, by.value, cnt.value, kms.value, kn.value, ku.value)
 
 
-def attention_roofline(kernel, ms, fl, by, cnt):
-    """Attention over T (SCA cross-attention): HBM-bound, algorithmic bytes
-    per launch = K and V rows of every frame (+ the 32-query q / o / lse) as stated in DESIGN.md."""
-    n = max(cnt.value, 1)
-    avg_ms = ms.value / n
-    if avg_ms <= 0:
+def attention_roofline(kernel, pr):
+    """Attention over T (SCA cross-attention) and the X2Y cores: HBM-bound, algorithmic
+    bytes per call over the KERNEL time of the call (its kernels' summed durations)."""
+    n = max(pr.calls, 1)
+    avg_ms = pr.kernel_ms / n
+    if pr.calls <= 0 or avg_ms <= 0:
         return None
-    gbs = by.value / n / (avg_ms * 1e-3) / 1e9
+    gbs = pr.bytes / n / (avg_ms * 1e-3) / 1e9
     return dict(kernel=kernel, bound="hbm", achieved=round(gbs, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(gbs / HBM_PEAK_GBS, 4),
-                traffic=None, launches=cnt.value, avg_launch_ms=round(avg_ms, 5), bytes_per_launch=by.value / n,
-                tflops=round(fl.value / n / (avg_ms * 1e-3) / 1e12, 2))
+                traffic=None, launches=pr.calls, avg_launch_ms=round(avg_ms, 5), bytes_per_launch=pr.bytes / n,
+                tflops=round(pr.flops / n / (avg_ms * 1e-3) / 1e12, 2), **pr.timing())
 
 
-def fused_layer_roofline(prof, peak):
+def fused_layer_roofline(pr, peak):
     """The fused MS-TCN layer kernel (mstcn_fused.hip: conv + ReLU + 1x1 + residual in one launch, and
     the fused dX chain of the backward), MFMA-bound: 2 rows F 4F algorithmic FLOPs per launch (the
-    3-tap conv's 3F and the 1x1's F columns); None when the two-GEMM layers ran."""
-    ms, fl, by, cnt = prof
-    n = cnt.value
-    if n <= 0 or ms.value <= 0:
+    3-tap conv's 3F and the 1x1's F columns) over its kernel time; None when the two-GEMM layers ran."""
+    n = pr.calls
+    if n <= 0 or pr.bracket_ms <= 0:
         return None
-    avg_ms = ms.value / n
-    tf = fl.value / n / (avg_ms * 1e-3) / 1e12
-    return dict(kernel="frl_kernel (fused MS-TCN layer: conv fwd + 1x1 fwd, or dX chain bwd)", bound="mfma",
-                achieved=round(tf, 2), peak=round(peak, 1), unit="TFLOP/s", frac=round(tf / peak, 4),
-                launches=n, avg_launch_ms=round(avg_ms, 5), flops_per_launch=fl.value / n,
-                bytes_per_launch=by.value / n)
+    # live: one event pair around each back-to-back chain of a stack's fused-layer launches (the host issues the
+    # whole chain from one C call, so the bracket is kernel time plus the launches' dispatch gaps)
+    avg_ms = pr.bracket_ms / n
+    tf = pr.flops / n / (avg_ms * 1e-3) / 1e12
+    out = dict(kernel="frl_kernel (fused MS-TCN layer: conv fwd + 1x1 fwd, or dX chain bwd)", bound="mfma",
+               achieved=round(tf, 2), peak=round(peak, 1), unit="TFLOP/s", frac=round(tf / peak, 4),
+               launches=n, avg_launch_ms=round(avg_ms, 5), flops_per_launch=pr.flops / n,
+               bytes_per_launch=pr.bytes / n, basis="HIP events around the back-to-back fused-layer chains")
+    us = trace_call_us("frl")
+    if us is not None:        # cross-check: the committed kernel trace of this shape
+        out.update(trace_avg_launch_ms=round(us / 1e3, 5),
+                   trace_frac=round(pr.flops / n / (us * 1e-6) / 1e12 / peak, 4))
+    return out
 
 
-def gemm_roofline(name, ms, fl, by, cnt, peak):
-    """A cross-attention projection GEMM kind, MFMA-bound: algorithmic FLOPs over the HIP-event time of
-    its launches in the sampled step(s); `traffic` from a committed standalone PMC pass of the same shape."""
-    n = cnt.value
-    if n <= 0 or ms.value <= 0:
+def gemm_roofline(name, pr, peak):
+    """A cross-attention projection GEMM kind, MFMA-bound: algorithmic FLOPs over the kernel time of its
+    launches in the sampled step(s); `traffic` from a committed standalone PMC pass of the same shape."""
+    n = pr.calls
+    if n <= 0 or pr.kernel_ms <= 0:
         return None
     note, pmc = XATTN_NOTES[name]
-    tf = fl.value / (ms.value * 1e-3) / 1e12
+    ms = pr.kernel_ms
+    tf = pr.flops / (ms * 1e-3) / 1e12
     out = dict(kernel=note, bound="mfma", achieved=round(tf, 2), peak=round(peak, 1), unit="TFLOP/s",
-               frac=round(tf / peak, 4), launches=n, avg_launch_ms=round(ms.value / n, 5),
-               flops_per_launch=fl.value / n, bytes_per_launch=by.value / n,
-               hbm_gbs_algorithmic=round(by.value / (ms.value * 1e-3) / 1e9, 1))
+               frac=round(tf / peak, 4), launches=n, avg_launch_ms=round(ms / n, 5),
+               flops_per_launch=pr.flops / n, bytes_per_launch=pr.bytes / n,
+               hbm_gbs_algorithmic=round(pr.bytes / (ms * 1e-3) / 1e9, 1), **pr.timing())
     path = os.path.join(ROOT, "profiles", pmc)
     out["traffic"] = None
     if os.path.exists(path):
@@ -534,7 +610,7 @@ def main():
     for kind in kinds:
         native.check(lib.fx_prof_enable(kind, 4096), "fx_prof_enable")
     step()
-    per_step = {kind: prof_collect(lib, kind)[3].value for kind in kinds}
+    per_step = {kind: prof_collect(lib, kind).calls for kind in kinds}
     lib.fx_prof_disable()
     for kind in kinds:
         if per_step[kind] > 0:
@@ -552,8 +628,8 @@ def main():
     def collect(kind):
         if per_step[kind] > 0:
             return prof_collect(lib, kind)
-        return native.D(), native.D(), native.D(), native.I()
-    ms, fl, by, cnt = collect(0)
+        return Prof()
+    conv_prof = collect(0)
     attn_prof = {name: collect(kind) for kind, name in ((1, "fwd"), (2, "bwd"))}
     x2y_prof = {name: collect(kind) for kind, name in X2Y_KINDS.items()}
     frl_prof = collect(FRL_KIND)
@@ -619,8 +695,8 @@ def main():
     frames = world * sum(Ts) * args.steps
     value = frames / elapsed
     if rank == 0:
-        avg_ms = ms.value / max(cnt.value, 1)
-        flops_per_launch = fl.value / max(cnt.value, 1)
+        avg_ms = conv_prof.kernel_ms / max(conv_prof.calls, 1)
+        flops_per_launch = conv_prof.flops / max(conv_prof.calls, 1)
         achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
         default_shape = args.config == "havid" and T == T_DEFAULT and nv == 2
         split = headline_prec == "fp32s"
@@ -636,22 +712,24 @@ def main():
                                 f"+ conv dX; peak = bf16 dense peak / {SPLIT_PRODUCTS} products)" if split else
                                 "gemm_f32_wide8_kernel (implicit dilated-conv GEMM: conv fwd + conv dX of the layers "
                                 "the fused MS-TCN layer kernel does not run)"),
-                        launches=cnt.value, avg_launch_ms=round(avg_ms, 5),
+                        launches=conv_prof.calls, avg_launch_ms=round(avg_ms, 5),
                         flops_per_launch=flops_per_launch,
-                        sample=f"HIP events on the first {cnt.value} conv-GEMM launches of the timed region")
+                        sample=f"the conv-GEMM launches of the first timed step ({conv_prof.calls})",
+                        **conv_prof.timing())
         # the dominant kernel by measured time in the sampled step: the fused MS-TCN layer when it ran
         frl_roofline = fused_layer_roofline(frl_prof, F32_MFMA_PEAK_TFLOPS)
         if frl_roofline is not None:
             frl_roofline["traffic"] = traffic_from_profiles(FRL_KERNEL) if default_shape else None
-            frl_roofline["sample"] = (f"HIP events around the back-to-back fused-layer chains (one pair per MS-TCN "
-                                      f"stack and direction) of the timed region: {frl_roofline['launches']} "
-                                      "launches, inter-launch gaps included")
-        roofline = (frl_roofline if frl_roofline is not None and frl_prof[0].value > ms.value else conv_roofline)
-        roofline_attention = {name: attention_roofline(f"tattn_{name}_kernel (+ tattn_merge_kernel over T splits)", *v)
+            frl_roofline["sample"] = (f"the fused-layer launches of the first timed step ({frl_roofline['launches']}), "
+                                      "one event pair per MS-TCN stack and direction")
+        roofline = (frl_roofline if frl_roofline is not None and frl_prof.kernel_ms > conv_prof.kernel_ms
+                    else conv_roofline)
+        roofline_attention = {name: attention_roofline(f"tattn_{name}32_kernel (merge folded into the launch)", v)
                               for name, v in attn_prof.items()}
         for name, r in roofline_attention.items():
             if r is not None and default_shape:   # PMC bytes of the main kernel (the merge launch excluded)
                 r["traffic"] = traffic_from_profiles(f"tattn_{name}32_kernel", f"r05_pmc_tattn_{name}.json")
+                trace_basis(r, name, r["bytes_per_launch"], HBM_PEAK_GBS, 1e9)
         x2y_pmc = {}
         if default_shape and os.path.exists(os.path.join(ROOT, "profiles", "r05_pmc_x2y.json")):
             try:
@@ -660,10 +738,15 @@ def main():
             except (OSError, ValueError):
                 x2y_pmc = {}
         for name, v in x2y_prof.items():      # the X2Y_map cores (basic.py:373-380), when they ran fused
-            if v[3].value > 0:
-                roofline_attention[name] = attention_roofline(X2Y_NOTES[name], *v)
-                if roofline_attention[name] is not None:   # (standalone PMC passes, tools/r05_x2y_pmc.sh)
-                    roofline_attention[name]["traffic"] = x2y_pmc.get(name)
+            if v.calls > 0:
+                r = roofline_attention[name] = attention_roofline(X2Y_NOTES[name], v)
+                # the standalone PMC passes (tools/r05_x2y_pmc.sh) ran the frame-level call's shape (2 x 4096
+                # frames, 32 tokens, head 512): comparable with the frame-level kinds only
+                if r is not None and not name.endswith("_seg"):
+                    r["traffic"] = x2y_pmc.get(name)
+                    r["traffic_shape"] = "2 x 4096 frames x 32 tokens, Hd 512 (= this line's calls)"
+                    if default_shape:
+                        trace_basis(r, name, r["bytes_per_launch"], HBM_PEAK_GBS, 1e9)
         line = dict(metric=metric, value=round(value, 1), unit="frames/s", n_gpus=world, steps=args.steps,
                     warmup=args.warmup, ms_per_step=round(1e3 * elapsed / args.steps, 3), higher_is_better=True,
                     scaling="weak", vs_baseline=None, dtype="fp32", data="synthetic",
@@ -679,7 +762,7 @@ def main():
                                 parallelism=f"dp{world}", weights="fixed (no optimizer update in the timed steps)",
                                 tdu_segments=S, tdu_segments_after_timing=S_after),
                     roofline=roofline, roofline_attention=roofline_attention,
-                    roofline_xattn_gemm={name: gemm_roofline(name, *v, F32_MFMA_PEAK_TFLOPS)
+                    roofline_xattn_gemm={name: gemm_roofline(name, v, F32_MFMA_PEAK_TFLOPS)
                                          for name, v in xattn_prof.items()},
                     roofline_conv_gemm=conv_roofline, roofline_fused_layer=frl_roofline, train_step_with_adam=adam,
                     bf16_mode=bf16, dp_schedule=dp_sched)

@@ -177,7 +177,7 @@ int launch_mha_small_fwd(const float* q, long long ldq, const float* k, long lon
   FX_REQUIRE(nvid >= 1, "mha_small: nvid >= 1");
   FX_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "mha_small: dropout p in [0, 1)");
   const unsigned thr = drop_p > 0.f ? std::max(fx_drop_thresh(drop_p), 1u) : 0u;
-  hipLaunchKernelGGL(mha_small_fwd_kernel, dim3(nhead, nvid), dim3(NT), 0, s, q, ldq, k, ldk, v, ldv, Lq, Lk, hd, scale,
+  fx_launch(mha_small_fwd_kernel, dim3(nhead, nvid), dim3(NT), 0, s, q, ldq, k, ldk, v, ldv, Lq, Lk, hd, scale,
                      probs, o, ldo, drop_p, thr, seed);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
@@ -192,7 +192,7 @@ int launch_mha_small_bwd(const float* q, long long ldq, const float* k, long lon
   FX_REQUIRE(nvid >= 1, "mha_small: nvid >= 1");
   FX_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "mha_small: dropout p in [0, 1)");
   const unsigned thr = drop_p > 0.f ? std::max(fx_drop_thresh(drop_p), 1u) : 0u;
-  hipLaunchKernelGGL(mha_small_bwd_kernel, dim3(nhead, nvid), dim3(NT), 0, s, q, ldq, k, ldk, v, ldv, probs, dout, lddo,
+  fx_launch(mha_small_bwd_kernel, dim3(nhead, nvid), dim3(NT), 0, s, q, ldq, k, ldk, v, ldv, probs, dout, lddo,
                      Lq, Lk, hd, scale, dq, lddq, dk, lddk, dv, lddv, drop_p, thr, seed);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;

@@ -1027,11 +1027,11 @@ int launch_tattn_fwd(const float* q, long long ldq, const float* k, long long ld
     FX_REQUIRE(ws || a.nsplit == 1, "attention over T: workspace required");
     a.cnt = tattn_fold_counters(a.nsplit, nvid, nh, s);
     prof_begin(1, s);
-    if (a.Tc == 256) hipLaunchKernelGGL(tattn_fwd32_kernel<2>, dim3(a.nsplit, nh, nvid), dim3(AT), 0, s, a);
-    else hipLaunchKernelGGL(tattn_fwd32_kernel<1>, dim3(a.nsplit, nh, nvid), dim3(AT), 0, s, a);
+    if (a.Tc == 256) fx_launch(tattn_fwd32_kernel<2>, dim3(a.nsplit, nh, nvid), dim3(AT), 0, s, a);
+    else fx_launch(tattn_fwd32_kernel<1>, dim3(a.nsplit, nh, nvid), dim3(AT), 0, s, a);
     FX_CHECK_HIP(hipGetLastError());
     if (a.nsplit > 1 && !a.cnt) {
-      hipLaunchKernelGGL(tattn_merge_kernel, dim3(nh, nvid), dim3(AT), sizeof(float) * 2 * a.nsplit * 32, s, a, 1,
+      fx_launch(tattn_merge_kernel, dim3(nh, nvid), dim3(AT), sizeof(float) * 2 * a.nsplit * 32, s, a, 1,
                          1.f);
       FX_CHECK_HIP(hipGetLastError());
     }
@@ -1042,11 +1042,11 @@ int launch_tattn_fwd(const float* q, long long ldq, const float* k, long long ld
   for (int q0 = 0; q0 < Qv; q0 += QB) {
     a.q0 = q0;
     a.Qv = std::min(QB, Qv - q0);
-    hipLaunchKernelGGL(tattn_fwd_kernel, dim3(g.nsplit, nh, nvid), dim3(AT), std::max(g.lds, merge_lds(g) + 16), s,
+    fx_launch(tattn_fwd_kernel, dim3(g.nsplit, nh, nvid), dim3(AT), std::max(g.lds, merge_lds(g) + 16), s,
                        a);
     FX_CHECK_HIP(hipGetLastError());
     if (g.nsplit > 1) {
-      hipLaunchKernelGGL(tattn_merge_kernel, dim3(nh, nvid), dim3(AT), merge_lds(g), s, a, 1, 1.f);
+      fx_launch(tattn_merge_kernel, dim3(nh, nvid), dim3(AT), merge_lds(g), s, a, 1, 1.f);
       FX_CHECK_HIP(hipGetLastError());
     }
   }
@@ -1087,11 +1087,11 @@ int launch_tattn_bwd(const float* q, long long ldq, const float* k, long long ld
     FX_REQUIRE(ws || a.nsplit == 1, "attention over T: workspace required");
     a.cnt = tattn_fold_counters(a.nsplit, nvid, nh, s);
     prof_begin(2, s);
-    if (a.Tc == 256) hipLaunchKernelGGL(tattn_bwd32_kernel<2>, dim3(a.nsplit, nh, nvid), dim3(AT), 0, s, a);
-    else hipLaunchKernelGGL(tattn_bwd32_kernel<1>, dim3(a.nsplit, nh, nvid), dim3(AT), 0, s, a);
+    if (a.Tc == 256) fx_launch(tattn_bwd32_kernel<2>, dim3(a.nsplit, nh, nvid), dim3(AT), 0, s, a);
+    else fx_launch(tattn_bwd32_kernel<1>, dim3(a.nsplit, nh, nvid), dim3(AT), 0, s, a);
     FX_CHECK_HIP(hipGetLastError());
     if (a.nsplit > 1 && !a.cnt) {
-      hipLaunchKernelGGL(tattn_merge_kernel, dim3(nh, nvid), dim3(AT), 0, s, a, 0, scale);
+      fx_launch(tattn_merge_kernel, dim3(nh, nvid), dim3(AT), 0, s, a, 0, scale);
       FX_CHECK_HIP(hipGetLastError());
     }
     prof_end(2, s, 10.0 * qo * (double)ktot / nvid, 4.0 * (4.0 * kv + 4.0 * qo + (double)nvid * nh * Qv));
@@ -1103,11 +1103,11 @@ int launch_tattn_bwd(const float* q, long long ldq, const float* k, long long ld
     a.q0 = q0;
     a.Qv = std::min(QB, Qv - q0);
     a.acc_kv = (q0 > 0) || (opt && opt->acc_kv);
-    hipLaunchKernelGGL(tattn_bwd_kernel, dim3(g.nsplit, nh, nvid), dim3(AT), std::max(g.lds, merge_lds(g) + 16), s,
+    fx_launch(tattn_bwd_kernel, dim3(g.nsplit, nh, nvid), dim3(AT), std::max(g.lds, merge_lds(g) + 16), s,
                        a);
     FX_CHECK_HIP(hipGetLastError());
     if (g.nsplit > 1) {
-      hipLaunchKernelGGL(tattn_merge_kernel, dim3(nh, nvid), dim3(AT), 0, s, a, 0, scale);
+      fx_launch(tattn_merge_kernel, dim3(nh, nvid), dim3(AT), 0, s, a, 0, scale);
       FX_CHECK_HIP(hipGetLastError());
     }
   }

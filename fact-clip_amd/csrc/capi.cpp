@@ -4,6 +4,8 @@
 // orchestrated here in C++ so one Python call launches the whole sequence on
 // the caller's stream; kernels live in gemm_f32.hip, rowops.hip, segments.hip.
 #include <algorithm>
+#include <atomic>
+#include <tuple>
 #include <map>
 #include <mutex>
 #include <cmath>
@@ -29,18 +31,29 @@ struct ProfState {
   std::vector<double> flops, bytes;
   std::vector<int> launches;   // launches an event pair brackets (back-to-back chains: one pair)
   int used = 0;
+  // kernel-time pairs (hipExtLaunchKernel) of the kernels launched inside this kind's brackets
+  std::vector<hipEvent_t> kev;
+  int kused = 0;
+  int kdropped = 0;            // kernels launched in a bracket after the pool ran out (not timed)
+  hipStream_t open_stream = nullptr;
 };
-constexpr int kProfKinds = 11;  // 0 conv GEMM, 1 / 2 attention over T fwd / bwd, 3-6 X2Y cores, 7 fused MS-TCN layer,
-                                // 8 persistent token-kernel launches (tokdec.hip), 9 SCA frame-memory K/V projection
-                                // GEMM, 10 X2Y input projections (k, v, q)
+constexpr int kProfKinds = 15;  // 0 conv GEMM, 1 / 2 attention over T fwd / bwd, 3-6 X2Y cores of frame-level
+                                // calls (a2f fwd, a2f bwd, f2a fwd, f2a bwd), 7 fused MS-TCN layer, 8 persistent
+                                // token-kernel launches (tokdec.hip), 9 SCA frame-memory K/V projection GEMM,
+                                // 10 X2Y input projections (k, v, q), 11-14 X2Y cores of segment-level calls
+constexpr int kKernelPairsPerEvent = 16;
 std::mutex g_prof_mu;
 ProfState g_prof[kProfKinds];
+std::atomic<int> g_spin_override[2] = {{-1}, {-1}};   // fx_debug_set_spin: 0 token kernel, 1 X2Y f2a backward
 
 void prof_reset(ProfState& p) {
   for (auto& e : p.ev) (void)hipEventDestroy(e);
+  for (auto& e : p.kev) (void)hipEventDestroy(e);
   p = ProfState{};
 }
 }  // namespace
+
+thread_local int g_prof_open = -1;
 
 void prof_begin(int kind, hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_prof_mu);
@@ -48,11 +61,14 @@ void prof_begin(int kind, hipStream_t s) {
   ProfState& p = g_prof[kind];
   if (p.used >= p.max_events) return;
   (void)hipEventRecord(p.ev[2 * p.used], s);
+  p.open_stream = s;
+  g_prof_open = kind;
 }
 
 void prof_end(int kind, hipStream_t s, double flops, double bytes, int launches) {
   std::lock_guard<std::mutex> lk(g_prof_mu);
   if (kind < 0 || kind >= kProfKinds) return;
+  if (g_prof_open == kind) g_prof_open = -1;
   ProfState& p = g_prof[kind];
   if (p.used >= p.max_events) return;
   (void)hipEventRecord(p.ev[2 * p.used + 1], s);
@@ -60,6 +76,51 @@ void prof_end(int kind, hipStream_t s, double flops, double bytes, int launches)
   p.bytes[p.used] = bytes;
   p.launches[p.used] = launches;
   p.used++;
+}
+
+bool prof_kernel_events(hipStream_t s, hipEvent_t* e0, hipEvent_t* e1) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  const int kind = g_prof_open;
+  if (kind < 0 || kind >= kProfKinds) return false;
+  ProfState& p = g_prof[kind];
+  if (s != p.open_stream) return false;   // (side / aux stream work launched from inside the call)
+  if (2 * (size_t)(p.kused + 1) > p.kev.size()) {
+    p.kdropped++;
+    return false;
+  }
+  *e0 = p.kev[2 * p.kused];
+  *e1 = p.kev[2 * p.kused + 1];
+  p.kused++;
+  return true;
+}
+
+unsigned tok_spin_max() {
+  const int o = g_spin_override[0].load(std::memory_order_relaxed);
+  if (o > 0) return (unsigned)o;
+  return knobs().tok_spin > 0 ? (unsigned)knobs().tok_spin : (1u << 20);
+}
+
+unsigned x2y_spin_max() {
+  const int o = g_spin_override[1].load(std::memory_order_relaxed);
+  return o > 0 ? (unsigned)o : (1u << 22);
+}
+
+int coresident_blocks(const void* kernel, int threads, size_t lds) {
+  static std::mutex mu;
+  static std::map<std::tuple<int, const void*, int, size_t>, int> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> lk(mu);
+  const auto key = std::make_tuple(dev, kernel, threads, lds);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, lds) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  const int n = std::max(per_cu, 0) * std::max(cus, 0);
+  cache[key] = n;
+  return n;
 }
 
 // ---- helpers -------------------------------------------------------------------
@@ -141,7 +202,7 @@ int ew_grid(long long total) { return (int)std::min<long long>(std::max<long lon
 int relu_bwd(const float* dy, long long lddy, const float* y, long long ldy, int rows, int cols, float* dz,
              long long lddz, hipStream_t s) {
   if ((long long)rows * cols == 0) return FX_OK;
-  hipLaunchKernelGGL(relu_bwd_kernel, dim3(ew_grid((long long)rows * cols)), dim3(256), 0, s, dy, lddy, y, ldy, rows,
+  fx_launch(relu_bwd_kernel, dim3(ew_grid((long long)rows * cols)), dim3(256), 0, s, dy, lddy, y, ldy, rows,
                      cols, dz, lddz);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
@@ -150,7 +211,7 @@ int relu_bwd(const float* dy, long long lddy, const float* y, long long ldy, int
 int add2(const float* a, long long lda, const float* b, long long ldb, int rows, int cols, float* o, long long ldo,
          int accumulate, hipStream_t s, int bcols) {
   if ((long long)rows * cols == 0) return FX_OK;
-  hipLaunchKernelGGL(add2_kernel, dim3(ew_grid((long long)rows * cols)), dim3(256), 0, s, a, lda, b, ldb, rows, cols,
+  fx_launch(add2_kernel, dim3(ew_grid((long long)rows * cols)), dim3(256), 0, s, a, lda, b, ldb, rows, cols,
                      o, ldo, accumulate, bcols < 0 ? cols : bcols);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
@@ -378,7 +439,7 @@ int pack_conv_weights(const fx_mstcn_params* p, float* ws, float* wbdst, float* 
     a.wpw[l] = p->w_pw[l];
     a.wpt[l] = wptdst ? wptdst + (long long)l * p->F * p->F : nullptr;
   }
-  hipLaunchKernelGGL(pack_conv_kernel, dim3(cdiv(p->F, 32), cdiv(p->F, 32), p->num_layers), dim3(256), 0, s, a);
+  fx_launch(pack_conv_kernel, dim3(cdiv(p->F, 32), cdiv(p->F, 32), p->num_layers), dim3(256), 0, s, a);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }
@@ -1083,7 +1144,7 @@ int pack_conv_set(const float* const* w, int NL, int F, float* wf, float* wb, hi
     a.wf[l] = wf + l * wsz;
     a.wb[l] = wb + l * wsz;
   }
-  hipLaunchKernelGGL(pack_conv_kernel, dim3(cdiv(F, 32), cdiv(F, 32), NL), dim3(256), 0, s, a);
+  fx_launch(pack_conv_kernel, dim3(cdiv(F, 32), cdiv(F, 32), NL), dim3(256), 0, s, a);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }
@@ -1704,18 +1765,20 @@ int fx_x2y_fwd(const float* X, long long ldx, int Nx, int xdim, const float* Xpo
   // logit and probability tiles, the attended features
   const double na = (double)V.a[V.n];
   const double core_bytes = 4.0 * ((double)Ny * Hd + 2.0 * Nx * Hd + 2.0 * na + (double)Ny * Hd);
+  // fx_prof kinds 3 / 5 for frame-level calls, 11 / 13 for segment-level ones (bench.py reports them apart)
+  const int kseg = std::max(Nx, Ny) >= 1024 ? 0 : 8;
   if (knobs().x2y_fused && x2y_a2f_fusable(V.n, V.x.data(), Hd) && al16) {
-    prof_begin(3, s);
+    prof_begin(3 + kseg, s);
     FX_TRY(launch_x2y_a2f_fwd(yq, xk, xv, Hd, scale, V.n, V.y.data(), V.x.data(), V.a.data(), logit, attn, feat, s));
-    prof_end(3, s, 4.0 * na * Hd, core_bytes);
+    prof_end(3 + kseg, s, 4.0 * na * Hd, core_bytes);
   } else if (knobs().x2y_fused && x2y_f2a_fusable(V.n, V.x.data(), V.y.data(), Hd) && al16) {
     // the f2a map (frames -> tokens): per-chunk partials after every other region of the workspace
     float* f2a_ws = workspace + x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, V) + al64((long long)Ny * (ydim + Hd)) +
                     x2y_side_ws(Nx, xdim, Ny, ydim, Hd, outdim);
-    prof_begin(5, s);
+    prof_begin(5 + kseg, s);
     FX_TRY(launch_x2y_f2a_fwd(yq, xk, xv, Hd, scale, V.n, V.y.data(), V.x.data(), V.a.data(), logit, attn, feat,
                               f2a_ws, s));
-    prof_end(5, s, 4.0 * na * Hd, core_bytes);
+    prof_end(5 + kseg, s, 4.0 * na * Hd, core_bytes);
   } else
   // per video: logits = scale yq . xk^T, attn = softmax(logits), feat = attn . xv  (the GEMMs of up to
   // two videos in one grouped launch each)
@@ -1767,7 +1830,8 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
                const float* attn, const float* saved,
                const float* dout, long long lddo, const float* dlogit, const float* dattn, float* dX, float* dXpos,
                float* dY, float* dYpos, float* dwk, float* dbk, float* dwv, float* dbv, float* dwq, float* dbq,
-               float* dwy, float* dby, int has_xpos, int has_ypos, float* workspace, int side_defer, void* stream) {
+               float* dwy, float* dby, int has_xpos, int has_ypos, float* workspace, int side_defer, int32_t* status,
+               void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const VidRows V = vid_rows(Nx, Ny, nvid, x_off, y_off);
   FX_REQUIRE(V.x[V.n] == Nx && V.y[V.n] == Ny, "x2y: offsets must end at Nx / Ny");
@@ -1819,8 +1883,9 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
   const bool f2a_fused = !fused && knobs().x2y_fused &&
                          (f2a_mode == 1 || (f2a_mode == 2 && x2y_f2a_chunks(V.n, V.x.data()) >= 64)) &&
                          x2y_f2a_fusable(V.n, V.x.data(), V.y.data(), Hd) && (cw & 3) == 0 && al16;
-  if (fused) prof_begin(4, s);
-  else if (f2a_fused) prof_begin(6, s);
+  const int kseg = std::max(Nx, Ny) >= 1024 ? 0 : 8;   // (fx_prof: frame-level 4 / 6, segment-level 12 / 14)
+  if (fused) prof_begin(4 + kseg, s);
+  else if (f2a_fused) prof_begin(6 + kseg, s);
   if (fused) {
     FX_TRY(launch_x2y_a2f_bwd(dcat + ydim, cw, xv, xk, attn, dattn, dlogit, Hd, scale, V.n, V.y.data(), V.x.data(),
                               V.a.data(), dL, dyq, s));
@@ -1855,7 +1920,7 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
     float* f2a_ws = workspace + x2y_ws_nocatd(Nx, xdim, Ny, ydim, Hd, outdim, V) + al64((long long)Ny * cw) +
                     x2y_side_ws(Nx, xdim, Ny, ydim, Hd, outdim);
     FX_TRY(launch_x2y_f2a_bwd(dcat + ydim, cw, xv, xk, yq, attn, dattn, dlogit, Hd, scale, V.n, V.y.data(), V.x.data(),
-                              V.a.data(), dL, dxv, dxk, dyq, f2a_ws, s));
+                              V.a.data(), dL, dxv, dxk, dyq, f2a_ws, reinterpret_cast<unsigned*>(status), s));
   } else
   // per video: dP = dfeat . xv^T (+ dattn), dxv = attn^T . dfeat  (independent: one grouped launch
   // for up to two videos), softmax backward, then dyq = dlogit . xk, dxk = dlogit^T . yq (grouped)
@@ -1901,8 +1966,8 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
     }
     FX_TRY(launch_gemm_group(g2, n2, s));
   }
-  if (fused) prof_end(4, s, 8.0 * na * Hd, core_bytes);
-  else if (f2a_fused) prof_end(6, s, 8.0 * na * Hd, core_bytes);
+  if (fused) prof_end(4 + kseg, s, 8.0 * na * Hd, core_bytes);
+  else if (f2a_fused) prof_end(6 + kseg, s, 8.0 * na * Hd, core_bytes);
   // weight gradients (Y_W; projections X_K, X_V, Y_Q): nothing below needs them -> side stream, each
   // frame-level GEMM split defer_split(rows) ways into its own slab region
   {
@@ -2063,6 +2128,9 @@ int fx_prof_enable(int kind, int max_events) {
   prof_reset(p);
   p.ev.resize(2 * (size_t)max_events);
   for (auto& e : p.ev) FX_CHECK_HIP(hipEventCreate(&e));
+  // kernel-time pairs: the fused-layer chains bracket up to one launch per layer, the other kinds a few
+  p.kev.resize(2 * (size_t)max_events * (kind == 7 ? kKernelPairsPerEvent : 4));
+  for (auto& e : p.kev) FX_CHECK_HIP(hipEventCreate(&e));
   p.flops.assign(max_events, 0.0);
   p.bytes.assign(max_events, 0.0);
   p.launches.assign(max_events, 0);
@@ -2092,9 +2160,33 @@ int fx_prof_collect(int kind, double* total_ms, double* total_flops, double* tot
   return FX_OK;
 }
 
+int fx_prof_collect_kernels(int kind, double* kernel_ms, int* kernels, int* untimed) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  FX_REQUIRE(kind >= 0 && kind < kProfKinds && g_prof[kind].max_events > 0, "prof: kind not enabled");
+  const ProfState& p = g_prof[kind];
+  double ms = 0;
+  for (int i = 0; i < p.kused; ++i) {
+    FX_CHECK_HIP(hipEventSynchronize(p.kev[2 * i + 1]));
+    float t = 0.f;
+    FX_CHECK_HIP(hipEventElapsedTime(&t, p.kev[2 * i], p.kev[2 * i + 1]));
+    ms += t;
+  }
+  *kernel_ms = ms;
+  *kernels = p.kused;
+  *untimed = p.kdropped;
+  return FX_OK;
+}
+
 void fx_prof_disable(void) {
   std::lock_guard<std::mutex> lk(g_prof_mu);
   for (auto& p : g_prof) prof_reset(p);
+  g_prof_open = -1;
+}
+
+int fx_debug_set_spin(int which, int polls) {
+  FX_REQUIRE(which == 0 || which == 1, "fx_debug_set_spin: which is 0 (token kernel) or 1 (X2Y f2a backward)");
+  g_spin_override[which].store(polls > 0 ? polls : -1, std::memory_order_relaxed);
+  return FX_OK;
 }
 
 }  // extern "C"

@@ -310,7 +310,7 @@ struct TokBuild {
     prog.G = std::min(G, 256);
     if (const char* e = std::getenv("FX_TOK_G")) prog.G = std::max(1, std::min(prog.G, std::atoi(e)));   // diagnostic
     prog.status = reinterpret_cast<unsigned*>(status);
-    prog.spin_max = knobs().tok_spin > 0 ? (unsigned)knobs().tok_spin : (1u << 20);
+    prog.spin_max = tok_spin_max();
     FX_REQUIRE(status, "decoder: the persistent token kernel needs the caller's status word (fx_decoder_params.status)");
     prof_begin(8, s);
     FX_TRY(launch_tok(prog, s));
@@ -698,7 +698,7 @@ int fx_decoder_fwd(const fx_decoder_params* p, const float* tgt, long long ldt, 
     pk.A = A;
     pk.Hm = p->Hm;
     pk.L = NL;
-    hipLaunchKernelGGL(pack_kv_kernel, dim3(std::min(cdiv((long long)A * p->Hm, 256), 256), 2 * NL), dim3(256), 0, s,
+    fx_launch(pack_kv_kernel, dim3(std::min(cdiv((long long)A * p->Hm, 256), 256), 2 * NL), dim3(256), 0, s,
                        pk);
     FX_CHECK_HIP(hipGetLastError());
     // (profiling kind 9: the frame-level GEMM(s); algorithmic bytes = mem rows, packed weights, K/V rows)
@@ -1052,7 +1052,7 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
     pk.L = NL;
     const int AL = A * NL;
     if (dmem || dmpos) {
-      hipLaunchKernelGGL(pack_kv_kernel, dim3(std::min(cdiv((long long)A * p->Hm, 256), 256), 2 * NL), dim3(256), 0,
+      fx_launch(pack_kv_kernel, dim3(std::min(cdiv((long long)A * p->Hm, 256), 256), 2 * NL), dim3(256), 0,
                          s, pk);
       FX_CHECK_HIP(hipGetLastError());
       if (dmem) FX_TRY(linear_dx(dkv, AL2, wkv, T, p->Hm, AL2, dmem, lddm, 0, nullptr, 0, spl, s));
@@ -1086,7 +1086,7 @@ int fx_decoder_bwd(const fx_decoder_params* p, const fx_decoder_grads* g, const 
     uk.A = A;
     uk.Hm = p->Hm;
     uk.L = NL;
-    hipLaunchKernelGGL(unpack_kv_acc_kernel, dim3(std::min(cdiv((long long)A * p->Hm, 256), 256), 2 * NL), dim3(256),
+    fx_launch(unpack_kv_acc_kernel, dim3(std::min(cdiv((long long)A * p->Hm, 256), 256), 2 * NL), dim3(256),
                        0, sd, uk);
     FX_CHECK_HIP(hipGetLastError());
   }

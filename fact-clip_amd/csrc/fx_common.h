@@ -1,6 +1,7 @@
 // Shared definitions for the factmx HIP library (gfx950 / MI355X only).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <cstdint>
 #include <cstdio>
 #include <string>
@@ -178,8 +179,32 @@ struct Knobs {
 };
 const Knobs& knobs();
 
-// event-based timing hooks around launches of one kernel class (bench roofline)
+// event-based timing hooks around launches of one kernel class (bench roofline): prof_begin / prof_end
+// bracket a call (HIP events on the stream: kernels + any host-issue gap between them), and every kernel
+// launched through fx_launch while a bracket is open on this thread also gets its OWN event pair through
+// hipExtLaunchKernel, whose timestamps are the kernel's execution (the rocprofv3 kernel-trace duration)
 void prof_begin(int kind, hipStream_t s);
 void prof_end(int kind, hipStream_t s, double flops, double bytes, int launches = 1);
+extern thread_local int g_prof_open;   // kind of the bracket open on this thread, -1: none
+bool prof_kernel_events(hipStream_t s, hipEvent_t* e0, hipEvent_t* e1);
+
+// Every kernel launch of the library: hipLaunchKernelGGL, or hipExtLaunchKernelGGL with a kernel-time
+// event pair inside an open profiling bracket (bench.py's sampled step only)
+template <typename... Args, typename F = void (*)(Args...)>
+inline void fx_launch(F kernel, const dim3& grid, const dim3& block, std::uint32_t shm, hipStream_t s, Args... args) {
+  hipEvent_t e0, e1;
+  if (g_prof_open >= 0 && prof_kernel_events(s, &e0, &e1))
+    hipExtLaunchKernelGGL(kernel, grid, block, shm, s, e0, e1, 0u, args...);
+  else
+    hipLaunchKernelGGL(kernel, grid, block, shm, s, args...);
+}
+
+// Grid-barrier spin bounds of the persistent kernels (polls before a workgroup gives up and sets its
+// status bit): the FX_TOK_SPIN knob, or a value set at run time by fx_debug_set_spin (timeout tests)
+unsigned tok_spin_max();
+unsigned x2y_spin_max();
+// Workgroups of `kernel` (block threads, dynamic LDS bytes) that can be resident on the device at once:
+// the occupancy calculator's blocks per CU x the CU count (the bound of a grid-barrier launch's grid)
+int coresident_blocks(const void* kernel, int threads, size_t lds);
 
 }  // namespace fx

@@ -1759,28 +1759,28 @@ int kind_of(const fx_operand& o, bool vec) {
 template <int AK, int BKd>
 void launch_t(dim3 grid, hipStream_t s, const GemmDev& g, bool fast) {
   if (fast)
-    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKd, true>), grid, dim3(NTHREADS), 0, s, g);
+    fx_launch((gemm_f32_kernel<AK, BKd, true>), grid, dim3(NTHREADS), 0, s, g);
   else
-    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKd, false>), grid, dim3(NTHREADS), 0, s, g);
+    fx_launch((gemm_f32_kernel<AK, BKd, false>), grid, dim3(NTHREADS), 0, s, g);
 }
 
 template <int AK>
 int launch_wide_b(int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
   switch (bk) {
-    case ROWS: hipLaunchKernelGGL((gemm_f32_wide_kernel<AK, ROWS>), grid, dim3(NTHREADS), 0, s, g); return FX_OK;
-    case COLS: hipLaunchKernelGGL((gemm_f32_wide_kernel<AK, COLS>), grid, dim3(NTHREADS), 0, s, g); return FX_OK;
+    case ROWS: fx_launch((gemm_f32_wide_kernel<AK, ROWS>), grid, dim3(NTHREADS), 0, s, g); return FX_OK;
+    case COLS: fx_launch((gemm_f32_wide_kernel<AK, COLS>), grid, dim3(NTHREADS), 0, s, g); return FX_OK;
     case COLS_CONV:
-      hipLaunchKernelGGL((gemm_f32_wide_kernel<AK, COLS_CONV>), grid, dim3(NTHREADS), 0, s, g);
+      fx_launch((gemm_f32_wide_kernel<AK, COLS_CONV>), grid, dim3(NTHREADS), 0, s, g);
       return FX_OK;
     case COLS_CONVR:
       if constexpr (AK == COLS) {
-        hipLaunchKernelGGL((gemm_f32_wide_kernel<AK, COLS_CONVR>), grid, dim3(NTHREADS), 0, s, g);
+        fx_launch((gemm_f32_wide_kernel<AK, COLS_CONVR>), grid, dim3(NTHREADS), 0, s, g);
         return FX_OK;
       }
       break;
     case COLS_KT:
       if constexpr (AK == COLS_KT) {
-        hipLaunchKernelGGL((gemm_f32_wide_kernel<AK, COLS_KT>), grid, dim3(NTHREADS), 0, s, g);
+        fx_launch((gemm_f32_wide_kernel<AK, COLS_KT>), grid, dim3(NTHREADS), 0, s, g);
         return FX_OK;
       }
       break;
@@ -1793,20 +1793,20 @@ int launch_wide_b(int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
 template <int AK>
 int launch_wide8_b(int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
   switch (bk) {
-    case ROWS: hipLaunchKernelGGL((gemm_f32_wide8_kernel<AK, ROWS>), grid, dim3(W8T), 0, s, g); return FX_OK;
-    case COLS: hipLaunchKernelGGL((gemm_f32_wide8_kernel<AK, COLS>), grid, dim3(W8T), 0, s, g); return FX_OK;
+    case ROWS: fx_launch((gemm_f32_wide8_kernel<AK, ROWS>), grid, dim3(W8T), 0, s, g); return FX_OK;
+    case COLS: fx_launch((gemm_f32_wide8_kernel<AK, COLS>), grid, dim3(W8T), 0, s, g); return FX_OK;
     case COLS_CONV:
-      hipLaunchKernelGGL((gemm_f32_wide8_kernel<AK, COLS_CONV>), grid, dim3(W8T), 0, s, g);
+      fx_launch((gemm_f32_wide8_kernel<AK, COLS_CONV>), grid, dim3(W8T), 0, s, g);
       return FX_OK;
     case COLS_CONVR:
       if constexpr (AK == COLS) {
-        hipLaunchKernelGGL((gemm_f32_wide8_kernel<AK, COLS_CONVR>), grid, dim3(W8T), 0, s, g);
+        fx_launch((gemm_f32_wide8_kernel<AK, COLS_CONVR>), grid, dim3(W8T), 0, s, g);
         return FX_OK;
       }
       break;
     case COLS_KT:
       if constexpr (AK == COLS_KT) {
-        hipLaunchKernelGGL((gemm_f32_wide8_kernel<AK, COLS_KT>), grid, dim3(W8T), 0, s, g);
+        fx_launch((gemm_f32_wide8_kernel<AK, COLS_KT>), grid, dim3(W8T), 0, s, g);
         return FX_OK;
       }
       break;
@@ -1851,14 +1851,14 @@ int launch_b(int bk, dim3 grid, hipStream_t s, const GemmDev& g, bool fast) {
     case COLS_CONVR:   // FAST only (plan_gemm checks): the ragged frame lookup lives in the FAST loader
       if constexpr (AK == COLS) {
         if (!fast) break;
-        hipLaunchKernelGGL((gemm_f32_kernel<AK, COLS_CONVR, true>), grid, dim3(NTHREADS), 0, s, g);
+        fx_launch((gemm_f32_kernel<AK, COLS_CONVR, true>), grid, dim3(NTHREADS), 0, s, g);
         return FX_OK;
       }
       break;
     case COLS_KT:   // FAST only (plan_gemm picks it for vectorisable operands)
       if constexpr (AK == COLS_KT) {
         if (!fast) break;
-        hipLaunchKernelGGL((gemm_f32_kernel<AK, COLS_KT, true>), grid, dim3(NTHREADS), 0, s, g);
+        fx_launch((gemm_f32_kernel<AK, COLS_KT, true>), grid, dim3(NTHREADS), 0, s, g);
         return FX_OK;
       }
       break;
@@ -1889,8 +1889,8 @@ int launch_tiled(int ak, int bk, dim3 grid, hipStream_t s, const GemmDev& g) {
 template <int AK>
 int launch_direct_b(int bk, dim3 grid, dim3 block, hipStream_t s, const GemmDev& g) {
   switch (bk) {
-    case ROWS: hipLaunchKernelGGL((gemm_direct_kernel<AK, ROWS>), grid, block, 0, s, g); return FX_OK;
-    case COLS: hipLaunchKernelGGL((gemm_direct_kernel<AK, COLS>), grid, block, 0, s, g); return FX_OK;
+    case ROWS: fx_launch((gemm_direct_kernel<AK, ROWS>), grid, block, 0, s, g); return FX_OK;
+    case COLS: fx_launch((gemm_direct_kernel<AK, COLS>), grid, block, 0, s, g); return FX_OK;
     default: break;
   }
   set_error("gemm(direct): unsupported B operand kind");
@@ -2223,7 +2223,7 @@ int launch_reduce(const fx_gemm_desc& d, const GemmPlan& P, hipStream_t s) {
     const long long total = (long long)d.M * d.N;
     const int vec = (total % 4) == 0 && ((uintptr_t)P.g.ws & 15) == 0;
     int blocks = (int)std::min<long long>(cdiv(cdiv(total, 4), 256), 2048);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks, d.batch), dim3(256), 0, s, P.g, vec);
+    fx_launch(splitk_reduce_kernel, dim3(blocks, d.batch), dim3(256), 0, s, P.g, vec);
     FX_CHECK_HIP(hipGetLastError());
   }
   return FX_OK;
@@ -2272,11 +2272,11 @@ template <int AK, int NP>
 int launch_split_b(const GemmPlan& P, hipStream_t s) {
   const int variant = knobs().split_variant;   // 0: operands split in registers (B row-major), 1: LDS images
   if (P.bk == ROWS && variant == 0)
-    hipLaunchKernelGGL((gemm_f32_wide8_kernel<AK, ROWS, NP>), P.grid, dim3(W8T), 0, s, P.g);
+    fx_launch((gemm_f32_wide8_kernel<AK, ROWS, NP>), P.grid, dim3(W8T), 0, s, P.g);
   else if (P.bk == ROWS)
-    hipLaunchKernelGGL((gemm_split_wide8_kernel<AK, ROWS, NP>), P.grid, dim3(W8T), 0, s, P.g);
+    fx_launch((gemm_split_wide8_kernel<AK, ROWS, NP>), P.grid, dim3(W8T), 0, s, P.g);
   else
-    hipLaunchKernelGGL((gemm_split_wide8_kernel<AK, COLS, NP>), P.grid, dim3(W8T), 0, s, P.g);
+    fx_launch((gemm_split_wide8_kernel<AK, COLS, NP>), P.grid, dim3(W8T), 0, s, P.g);
   return FX_OK;
 }
 
@@ -2299,9 +2299,9 @@ int launch_split(const GemmPlan& P, int np, hipStream_t s) {
 template <int AK>
 int launch_bf16_b(const GemmPlan& P, hipStream_t s) {
   if (P.bk == ROWS)
-    hipLaunchKernelGGL((gemm_bf16_wide8_kernel<AK, ROWS>), P.grid, dim3(W8T), 0, s, P.g);
+    fx_launch((gemm_bf16_wide8_kernel<AK, ROWS>), P.grid, dim3(W8T), 0, s, P.g);
   else
-    hipLaunchKernelGGL((gemm_bf16_wide8_kernel<AK, COLS>), P.grid, dim3(W8T), 0, s, P.g);
+    fx_launch((gemm_bf16_wide8_kernel<AK, COLS>), P.grid, dim3(W8T), 0, s, P.g);
   return FX_OK;
 }
 
@@ -2407,7 +2407,7 @@ int launch_gemm_group(const fx_gemm_desc* d, int n, hipStream_t s) {
     if (m == 1) {
       FX_TRY(P[i0].direct ? launch_direct(P[i0].ak, P[i0].bk, P[i0].grid, P[i0].block, s, P[i0].g) : FX_ERR_UNSUPPORTED);
     } else {
-      hipLaunchKernelGGL(gemm_direct_group_kernel, dim3(G.start[m]), dim3(nw), 0, s, G);
+      fx_launch(gemm_direct_group_kernel, dim3(G.start[m]), dim3(nw), 0, s, G);
     }
     FX_CHECK_HIP(hipGetLastError());
   }
@@ -2425,8 +2425,8 @@ int launch_colsum_batched(const float* x, long long ld, long long x_bs, int M, i
     return FX_OK;
   }
   const int nblk = cdiv(M, CS_ROWS);
-  hipLaunchKernelGGL(colsum_stage1, dim3(cdiv(N, 64), nblk, nb), dim3(256), 0, s, x, ld, x_bs, M, N, ws);
-  hipLaunchKernelGGL(colsum_stage2, dim3(cdiv(N, 256), nb), dim3(256), 0, s, ws, nblk, N, out, out_bs, accumulate);
+  fx_launch(colsum_stage1, dim3(cdiv(N, 64), nblk, nb), dim3(256), 0, s, x, ld, x_bs, M, N, ws);
+  fx_launch(colsum_stage2, dim3(cdiv(N, 256), nb), dim3(256), 0, s, ws, nblk, N, out, out_bs, accumulate);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }

@@ -477,7 +477,7 @@ int launch_gru_fwd(const float* gi, long long ldgi, int nseq, const int* seq_off
       a.Hh = Hh;
       a.reverse = d;
     }
-    hipLaunchKernelGGL(gru_fwd_kernel, dim3(gru_grid(args.xcd, nc)), dim3(args.store_wave ? GTF : GT), 0, s, args);
+    fx_launch(gru_fwd_kernel, dim3(gru_grid(args.xcd, nc)), dim3(args.store_wave ? GTF : GT), 0, s, args);
     FX_CHECK_HIP(hipGetLastError());
   }
   return FX_OK;
@@ -517,7 +517,7 @@ int launch_gru_bwd(const float* dout, long long lddo, int nseq, const int* seq_o
       a.Hh = Hh;
       a.reverse = d;
     }
-    hipLaunchKernelGGL(gru_bwd_kernel, dim3(gru_grid(args.xcd, nc)), dim3(args.gate_wave ? GTF : GT), 0, s, args);
+    fx_launch(gru_bwd_kernel, dim3(gru_grid(args.xcd, nc)), dim3(args.gate_wave ? GTF : GT), 0, s, args);
     FX_CHECK_HIP(hipGetLastError());
   }
   return FX_OK;

@@ -375,8 +375,8 @@ int fx_class_loss_fwd(const float* x, long long sr, long long sc, int R, int C, 
   a.part = workspace;
   a.smooth = smooth;
   const int nb = grid_rows(R);
-  hipLaunchKernelGGL(class_loss_fwd_kernel, dim3(nb), dim3(LT), 0, s, a);
-  hipLaunchKernelGGL(finish_kernel, dim3(1), dim3(64), 0, s, workspace, nb, c_ce, c_sm, out);
+  fx_launch(class_loss_fwd_kernel, dim3(nb), dim3(LT), 0, s, a);
+  fx_launch(finish_kernel, dim3(1), dim3(64), 0, s, workspace, nb, c_ce, c_sm, out);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }
@@ -399,7 +399,7 @@ int fx_class_loss_bwd(const float* x, long long sr, long long sc, int R, int C, 
   a.c_sm = c_sm;
   a.dx = dx;
   a.smooth = smooth;
-  hipLaunchKernelGGL(class_loss_bwd_kernel, dim3(grid_rows(R)), dim3(LT), 0, (hipStream_t)stream, a);
+  fx_launch(class_loss_bwd_kernel, dim3(grid_rows(R)), dim3(LT), 0, (hipStream_t)stream, a);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }
@@ -434,8 +434,8 @@ int fx_attn_loss_fwd(const float* L, long long sr, long long sc, int R, int Q, i
   a.colz = colz;
   a.part = workspace;
   const int nb = grid_rows(std::max(R, K));
-  hipLaunchKernelGGL(attn_loss_fwd_kernel, dim3(nb), dim3(LT), 0, s, a);
-  hipLaunchKernelGGL(finish_kernel, dim3(1), dim3(64), 0, s, workspace, nb, c_xe, c_sm, out);
+  fx_launch(attn_loss_fwd_kernel, dim3(nb), dim3(LT), 0, s, a);
+  fx_launch(finish_kernel, dim3(1), dim3(64), 0, s, workspace, nb, c_xe, c_sm, out);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }
@@ -469,7 +469,7 @@ int fx_attn_loss_bwd(const float* L, long long sr, long long sc, int R, int Q, i
   a.dL = dL;
   a.dsr = dsr;
   a.dsc = dsc;
-  hipLaunchKernelGGL(attn_loss_bwd_kernel, dim3(grid_rows(R)), dim3(LT), 0, (hipStream_t)stream, a);
+  fx_launch(attn_loss_bwd_kernel, dim3(grid_rows(R)), dim3(LT), 0, (hipStream_t)stream, a);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }

@@ -394,7 +394,7 @@ int launch_pack_frag(const FragJob* jobs, int n, hipStream_t s) {
     a.K[i] = jobs[i].K;
     kmax = std::max(kmax, jobs[i].K);
   }
-  hipLaunchKernelGGL(pack_frag_kernel, dim3(kmax / FBK, FN / 32, n), dim3(256), 0, s, a);
+  fx_launch(pack_frag_kernel, dim3(kmax / FBK, FN / 32, n), dim3(256), 0, s, a);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }
@@ -459,11 +459,11 @@ int launch_frl(const float* x, long long ldx, int M, int T, int dil, int dir, co
   a.out3 = out3;
   a.ldo3 = ldo3;
   if (!knobs().frl_pair)
-    hipLaunchKernelGGL((frl_kernel<false, 3>), dim3(nt), dim3(FT), LDS_FLOATS * sizeof(float), s, a);
+    fx_launch((frl_kernel<false, 3>), dim3(nt), dim3(FT), LDS_FLOATS * sizeof(float), s, a);
   else if (knobs().frl_pd == 5)
-    hipLaunchKernelGGL((frl_kernel<true, 5>), dim3(nt), dim3(FT), LDS_FLOATS_PAIR * sizeof(float), s, a);
+    fx_launch((frl_kernel<true, 5>), dim3(nt), dim3(FT), LDS_FLOATS_PAIR * sizeof(float), s, a);
   else
-    hipLaunchKernelGGL((frl_kernel<true, 3>), dim3(nt), dim3(FT), LDS_FLOATS_PAIR * sizeof(float), s, a);
+    fx_launch((frl_kernel<true, 3>), dim3(nt), dim3(FT), LDS_FLOATS_PAIR * sizeof(float), s, a);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }

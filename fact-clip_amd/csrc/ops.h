@@ -77,11 +77,13 @@ long long x2y_f2a_ws_floats(int nvid, const int* xoff, int Hd);
 int launch_x2y_f2a_fwd(const float* yq, const float* xk, const float* xv, int Hd, float scale, int nvid,
                        const int* yoff, const int* xoff, const long long* aoff, float* logit, float* attn,
                        float* feat, float* ws, hipStream_t s);
-// f2a backward (dlogit, dxv, dxk, dyq of every video in three launches); ws as the forward's
+// f2a backward (dlogit, dxv, dxk, dyq of every video: the core in one launch with a grid barrier when every
+// chunk's workgroup can be resident, else two, + the ordered dyq merge); ws as the forward's; status (nullable):
+// FX_STATUS_X2Y_TIMEOUT when the one-launch core's barrier gives up
 int launch_x2y_f2a_bwd(const float* dfeat, long long ldf, const float* xv, const float* xk, const float* yq,
                        const float* attn, const float* dattn, const float* dlogit_in, int Hd, float scale, int nvid,
                        const int* yoff, const int* xoff, const long long* aoff, float* dlogit, float* dxv, float* dxk,
-                       float* dyq, float* ws, hipStream_t s);
+                       float* dyq, float* ws, unsigned* status, hipStream_t s);
 // backward, input-gradient side: dP = dfeat . xv^T (+ dattn), dlogit = attn (dP - rowsum(attn dP)) (+ dlogit_in),
 // dyq = scale dlogit . xk;  dfeat rows ld ldf (16-B aligned)
 // the a2f backward's weight-side products dxv = attn^T dfeat, dxk = scale dlogit^T yq in one launch

@@ -159,15 +159,15 @@ long long fx_grad_norm_workspace_floats(void) { return NPART; }
 int fx_grad_norm(const float* g, long long n, float* workspace, float* norm_out, void* stream) {
   FX_REQUIRE(n >= 0 && g && workspace, "grad_norm: null buffer");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(NPART), dim3(TPB), 0, s, g, n, workspace);
-  if (norm_out) hipLaunchKernelGGL(norm_final_kernel, dim3(1), dim3(TPB), 0, s, workspace, norm_out);
+  fx_launch(sumsq_partial_kernel, dim3(NPART), dim3(TPB), 0, s, g, n, workspace);
+  if (norm_out) fx_launch(norm_final_kernel, dim3(1), dim3(TPB), 0, s, workspace, norm_out);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }
 
 int fx_clip_grad_scale(float* g, long long n, const float* workspace, float max_norm, void* stream) {
   FX_REQUIRE(n >= 0 && g && workspace, "clip_grad_scale: null buffer");
-  hipLaunchKernelGGL(scale_kernel, dim3(1024), dim3(TPB), 0, (hipStream_t)stream, g, n, workspace, max_norm);
+  fx_launch(scale_kernel, dim3(1024), dim3(TPB), 0, (hipStream_t)stream, g, n, workspace, max_norm);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }
@@ -201,10 +201,10 @@ int fx_adam_step_checked(float* p, float* g, float* m, float* v, long long n, lo
   a.b1 = beta1; a.b2 = beta2; a.eps = eps; a.wd = weight_decay;
   a.norm_out = norm_out;
   a.status = status;
-  if (a.part) hipLaunchKernelGGL(sumsq_partial_kernel, dim3(NPART), dim3(TPB), 0, s, g, n, workspace);
+  if (a.part) fx_launch(sumsq_partial_kernel, dim3(NPART), dim3(TPB), 0, s, g, n, workspace);
   const long long n4 = (n + 3) / 4;
   const int blocks = (int)std::min<long long>((n4 + TPB - 1) / TPB, 2048);
-  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(TPB), 0, s, a);
+  fx_launch(adam_kernel, dim3(blocks), dim3(TPB), 0, s, a);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }

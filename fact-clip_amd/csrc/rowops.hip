@@ -441,7 +441,7 @@ int launch_layernorm_fwd_pos(const float* x, long long ldx, const float* r, long
   FX_REQUIRE(cols > 0 && cols <= 64 * MAXPL, "layernorm: cols must be in (0, 1024]");
   FX_REQUIRE(!y2 || pos, "layernorm: y + pos needs pos");
   if (rows == 0) return FX_OK;
-  hipLaunchKernelGGL(ln_fwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, r, ldr, w, b, eps, rows, cols,
+  fx_launch(ln_fwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, r, ldr, w, b, eps, rows, cols,
                      relu, y, ldy, mean, rstd, xhat, ldxh, pos, ldp, y2, ldy2);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
@@ -504,7 +504,7 @@ int launch_ln_param_grads(const LnGradJob* jobs, int n, int rows, int cols, long
     b.cols = cols;
     b.lddy = lddy;
     b.ldxh = ldxh;
-    hipLaunchKernelGGL(ln_param_grad_kernel, dim3(cdiv(cols, 256), b.n), dim3(256), 0, s, b);
+    fx_launch(ln_param_grad_kernel, dim3(cdiv(cols, 256), b.n), dim3(256), 0, s, b);
     FX_CHECK_HIP(hipGetLastError());
   }
   return FX_OK;
@@ -521,7 +521,7 @@ int launch_layernorm_bwd(const float* dy, long long lddy, const float* y, long l
   FX_REQUIRE(cols > 0 && cols <= 64 * MAXPL, "layernorm: cols must be in (0, 1024]");
   if (rows == 0) return FX_OK;
   if (rows <= 16 * SMALL_RPW && cols <= 64 * SMALL_CPL) {
-    hipLaunchKernelGGL(ln_bwd_small_kernel, dim3(1), dim3(1024), 0, s, dy, lddy, y, ldy, xhat, ldxh, w, rstd, rows,
+    fx_launch(ln_bwd_small_kernel, dim3(1), dim3(1024), 0, s, dy, lddy, y, ldy, xhat, ldxh, w, rstd, rows,
                        cols, relu, dx, lddx, dw, db);
     FX_CHECK_HIP(hipGetLastError());
     return FX_OK;
@@ -529,9 +529,9 @@ int launch_layernorm_bwd(const float* dy, long long lddy, const float* y, long l
   const int nblk = std::min(cdiv(rows, 4), LN_BWD_MAXBLK);
   const bool want = dw || db;
   FX_REQUIRE(!want || ws, "layernorm bwd: workspace required for dw/db");
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3(nblk), dim3(256), 0, s, dy, lddy, y, ldy, xhat, ldxh, w, rstd, rows,
+  fx_launch(ln_bwd_kernel, dim3(nblk), dim3(256), 0, s, dy, lddy, y, ldy, xhat, ldxh, w, rstd, rows,
                      cols, relu, dx, lddx, want ? ws : nullptr);
-  if (want) hipLaunchKernelGGL(ln_bwd_reduce, dim3(cdiv(cols, 32)), dim3(256), 0, s, ws, nblk, cols, dw, db);
+  if (want) fx_launch(ln_bwd_reduce, dim3(cdiv(cols, 32)), dim3(256), 0, s, ws, nblk, cols, dw, db);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }
@@ -553,7 +553,7 @@ int launch_dropout(const float* x, long long ldx, int rows, int cols, long long 
   FX_REQUIRE(p >= 0.f && p < 1.f, "dropout: p must be in [0, 1)");
   if ((long long)rows * cols == 0) return FX_OK;
   const int blocks = (int)std::min<long long>(cdiv((long long)rows * cols, 256), 4096);
-  hipLaunchKernelGGL(dropout_kernel, dim3(blocks), dim3(256), 0, s, x, ldx, rows, cols, idx_ld, idx_col0,
+  fx_launch(dropout_kernel, dim3(blocks), dim3(256), 0, s, x, ldx, rows, cols, idx_ld, idx_col0,
                      p > 0.f ? std::max(fx_drop_thresh(p), 1u) : 0u, 1.f / (1.f - p), seed, y, ldy);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
@@ -563,9 +563,9 @@ int launch_softmax_rows(const float* x, long long ldx, int rows, int cols, float
                         hipStream_t s) {
   if (rows == 0 || cols == 0) return FX_OK;
   if (cols <= 64 * MAXPL)
-    hipLaunchKernelGGL(softmax_wave_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, rows, cols, scale, p, ldp);
+    fx_launch(softmax_wave_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, rows, cols, scale, p, ldp);
   else
-    hipLaunchKernelGGL(softmax_block_kernel, dim3(rows), dim3(256), 0, s, x, ldx, rows, cols, scale, p, ldp);
+    fx_launch(softmax_block_kernel, dim3(rows), dim3(256), 0, s, x, ldx, rows, cols, scale, p, ldp);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }
@@ -575,10 +575,10 @@ int launch_softmax_rows_bwd(const float* p, long long ldp, const float* dp, long
                             hipStream_t s) {
   if (rows == 0 || cols == 0) return FX_OK;
   if (cols <= 64 * MAXPL)
-    hipLaunchKernelGGL(softmax_bwd_wave_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, p, ldp, dp, lddp, extra, lde,
+    fx_launch(softmax_bwd_wave_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, p, ldp, dp, lddp, extra, lde,
                        rows, cols, scale, dl, ldd);
   else
-    hipLaunchKernelGGL(softmax_bwd_block_kernel, dim3(rows), dim3(256), 0, s, p, ldp, dp, lddp, extra, lde, cols,
+    fx_launch(softmax_bwd_block_kernel, dim3(rows), dim3(256), 0, s, p, ldp, dp, lddp, extra, lde, cols,
                        scale, dl, ldd);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
@@ -588,7 +588,7 @@ int launch_pf_fwd(const float* x, long long ldx, int rows, int cols, int n, floa
                   float* clogit, long long ldc, hipStream_t s) {
   FX_REQUIRE(n > 0 && n <= cols, "process_feature: need 0 < n <= cols");
   if (rows == 0) return FX_OK;
-  hipLaunchKernelGGL(pf_fwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, rows, cols, n, out, ldo, clogit, ldc);
+  fx_launch(pf_fwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, rows, cols, n, out, ldo, clogit, ldc);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }
@@ -597,7 +597,7 @@ int launch_pf_bwd(const float* out, long long ldo, const float* dout, long long 
                   long long lddc, int rows, int cols, int n, float* dx, long long lddx, hipStream_t s) {
   FX_REQUIRE(n > 0 && n <= cols, "process_feature: need 0 < n <= cols");
   if (rows == 0) return FX_OK;
-  hipLaunchKernelGGL(pf_bwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, out, ldo, dout, lddo, dcl, lddc, rows,
+  fx_launch(pf_bwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, out, ldo, dout, lddo, dcl, lddc, rows,
                      cols, n, dx, lddx);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
@@ -606,7 +606,7 @@ int launch_pf_bwd(const float* out, long long ldo, const float* dout, long long 
 int launch_l2n_fwd(const float* x, long long ldx, int rows, int cols, float* y, long long ldy, float* nrm,
                    hipStream_t s) {
   if (rows == 0) return FX_OK;
-  hipLaunchKernelGGL(l2n_fwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, rows, cols, y, ldy, nrm);
+  fx_launch(l2n_fwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, rows, cols, y, ldy, nrm);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }
@@ -614,7 +614,7 @@ int launch_l2n_fwd(const float* x, long long ldx, int rows, int cols, float* y, 
 int launch_l2n_bwd(const float* y, long long ldy, const float* nrm, const float* dy, long long lddy, int rows,
                    int cols, float* dx, long long lddx, hipStream_t s) {
   if (rows == 0) return FX_OK;
-  hipLaunchKernelGGL(l2n_bwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, y, ldy, nrm, dy, lddy, rows, cols, dx,
+  fx_launch(l2n_bwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, y, ldy, nrm, dy, lddy, rows, cols, dx,
                      lddx);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;

@@ -193,7 +193,7 @@ int launch_seg_globalize(int nvid, int T, const int* row_off, const int32_t* num
       off += num_seg_host[c0 + v];
     }
     a.soff[a.nv] = off;
-    hipLaunchKernelGGL(seg_globalize_kernel, dim3(std::max(1, std::min(cdiv(tmax, 256), 64)), a.nv), dim3(256), 0, s,
+    fx_launch(seg_globalize_kernel, dim3(std::max(1, std::min(cdiv(tmax, 256), 64)), a.nv), dim3(256), 0, s,
                        a);
     FX_CHECK_HIP(hipGetLastError());
   }
@@ -206,12 +206,12 @@ int launch_segments(const float* x, long long ldx, int col0, int ncls, int T, in
   FX_REQUIRE(ncls > 0 && nvid >= 1 && (row_off || T > 0), "segments: need T > 0 (or row offsets) and ncls > 0");
   const int rows = row_of(T, row_off, nvid);
   for (int v = 0; v < nvid; ++v) FX_REQUIRE(row_of(T, row_off, v + 1) > row_of(T, row_off, v), "segments: empty video");
-  hipLaunchKernelGGL(argmax_rows_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, col0, ncls, rows, pred);
+  fx_launch(argmax_rows_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, col0, ncls, rows, pred);
   for (int c0 = 0; c0 < nvid; c0 += MAXV) {
     RowOff ro{};
     const int nv = std::min(MAXV, nvid - c0);
     for (int v = 0; v <= nv; ++v) ro.off[v] = row_of(T, row_off, c0 + v);
-    hipLaunchKernelGGL(boundary_scan_kernel, dim3(nv), dim3(SCAN_THREADS), 0, s, pred, ro, seg_id, seg_start, seg_end,
+    fx_launch(boundary_scan_kernel, dim3(nv), dim3(SCAN_THREADS), 0, s, pred, ro, seg_id, seg_start, seg_end,
                        num_seg + c0);
   }
   FX_CHECK_HIP(hipGetLastError());
@@ -221,7 +221,7 @@ int launch_segments(const float* x, long long ldx, int col0, int ncls, int T, in
 int launch_seg_reduce(const float* x, long long ldx, const int32_t* st, const int32_t* en, int S, int cols, int mean,
                       float* y, long long ldy, int accumulate, hipStream_t s) {
   if (S == 0 || cols == 0) return FX_OK;
-  hipLaunchKernelGGL(seg_reduce_kernel, dim3(S, cdiv(cols, 64)), dim3(64 * SEG_WAVES), 0, s, x, ldx, st, en, S, cols,
+  fx_launch(seg_reduce_kernel, dim3(S, cdiv(cols, 64)), dim3(64 * SEG_WAVES), 0, s, x, ldx, st, en, S, cols,
                      mean, y, ldy, accumulate);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
@@ -230,7 +230,7 @@ int launch_seg_reduce(const float* x, long long ldx, const int32_t* st, const in
 int launch_seg_mean_bwd(const float* dy, long long lddy, const int32_t* sid, const int32_t* st, const int32_t* en,
                         int T, int cols, float* dx, long long lddx, int accumulate, hipStream_t s) {
   if (T == 0 || cols == 0) return FX_OK;
-  hipLaunchKernelGGL(seg_mean_bwd_kernel, dim3(T, cdiv(cols, 256)), dim3(256), 0, s, dy, lddy, sid, st, en, T, cols,
+  fx_launch(seg_mean_bwd_kernel, dim3(T, cdiv(cols, 256)), dim3(256), 0, s, dy, lddy, sid, st, en, T, cols,
                      dx, lddx, accumulate);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;

@@ -164,8 +164,11 @@ __device__ __forceinline__ bool grid_sync(BarState& b, int* dead) {
   return !*dead;
 }
 
-__device__ __forceinline__ void grid_exit(BarState& b, int dead) {
-  if (threadIdx.x == 0 && !dead) {
+// Every workgroup counts its exit, also one that gave up at a barrier: the count reaches G only once every
+// workgroup has left the program, so the re-arm never races a live workgroup, and a launch that timed out
+// still leaves its slot zero for the launch that is dealt it next (slots are reused round robin)
+__device__ __forceinline__ void grid_exit(BarState& b) {
+  if (threadIdx.x == 0) {
     unsigned long long* ex = b.cnt + 16;
     const unsigned long long prev = __hip_atomic_fetch_add(ex, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (prev == (unsigned long long)b.G - 1) {   // every workgroup is past every barrier of this launch
@@ -797,13 +800,13 @@ __global__ __launch_bounds__(TT) void tok_kernel(TokProgram prog) {
       __syncthreads();
       tstamp(st, 1);
     }
-    if (p + 1 < prog.nphase && !grid_sync(b, &dead)) return;
+    if (p + 1 < prog.nphase && !grid_sync(b, &dead)) break;
   }
-  if (prog.debug) {
+  if (prog.debug && !dead) {
     __syncthreads();
     if (threadIdx.x < prog.nphase * 8) prog.stamps[blockIdx.x * TOK_MAXPH * 8 + threadIdx.x] = tst[threadIdx.x];
   }
-  grid_exit(b, dead);
+  grid_exit(b);
 }
 
 // per (device, stream) pool of barrier slots (zeroed once; every slot re-armed by its own launch's last
@@ -825,6 +828,11 @@ size_t tok_lds_bytes() {
 
 int launch_tok(TokProgram& prog, hipStream_t s) {
   FX_REQUIRE(prog.nphase >= 1 && prog.nphase <= TOK_MAXPH && prog.G >= 1 && prog.G <= 256, "tok: bad program");
+  // the grid barriers need every workgroup resident at once: cap the grid by the occupancy calculator's
+  // bound on this device (one workgroup per CU with this LDS size); the phases loop over their items
+  static const int resident = coresident_blocks((const void*)tok_kernel, TT, tok_lds_bytes());
+  FX_REQUIRE(resident >= 1, "tok: the token kernel cannot be resident on this device");
+  prog.G = std::min(prog.G, resident);
   for (int i = 0; i < prog.nphase; ++i) {
     const TokPhase& P = prog.ph[i];
     FX_REQUIRE(P.K >= 4 && P.K % 4 == 0 && P.Kp % 32 == 0 && P.Kp >= P.K && P.Kp <= TOK_MAXK && P.M >= 1,
@@ -858,7 +866,7 @@ int launch_tok(TokProgram& prog, hipStream_t s) {
   if (prog.debug && !dstamps) FX_CHECK_HIP(hipMalloc(&dstamps, 256 * TOK_MAXPH * 8 * sizeof(unsigned long long)));
   if (dstamps) (void)hipMemsetAsync(dstamps, 0, 256 * TOK_MAXPH * 8 * sizeof(unsigned long long), s);
   prog.stamps = dstamps;
-  hipLaunchKernelGGL(tok_kernel, dim3(prog.G), dim3(TT), tok_lds_bytes(), s, prog);
+  fx_launch(tok_kernel, dim3(prog.G), dim3(TT), tok_lds_bytes(), s, prog);
   FX_CHECK_HIP(hipGetLastError());
   if (prog.debug) {   // diagnostic: synchronous launch + program summary on stderr
     const hipError_t e = hipStreamSynchronize(s);

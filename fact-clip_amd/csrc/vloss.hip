@@ -630,11 +630,11 @@ int fx_loss_terms_fwd(const fx_loss_term* terms_host, const fx_loss_term* terms_
       FX_TRY(launch_gemm(d, s));
     }
   }
-  hipLaunchKernelGGL(terms_fwd_kernel, dim3(nb, nterms), dim3(VT), 0, s, terms_dev, part);
+  fx_launch(terms_fwd_kernel, dim3(nb, nterms), dim3(VT), 0, s, terms_dev, part);
   FX_CHECK_HIP(hipGetLastError());
-  hipLaunchKernelGGL(terms_finish_kernel, dim3(nterms), dim3(FT), 0, s, terms_dev, part, nb, vals);
+  fx_launch(terms_finish_kernel, dim3(nterms), dim3(FT), 0, s, terms_dev, part, nb, vals);
   FX_CHECK_HIP(hipGetLastError());
-  hipLaunchKernelGGL(combine_kernel, dim3(nout), dim3(64), 0, s, vals, coef_dev, nterms, nout, out);
+  fx_launch(combine_kernel, dim3(nout), dim3(64), 0, s, vals, coef_dev, nterms, nout, out);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }
@@ -644,7 +644,7 @@ int fx_loss_terms_bwd(const fx_loss_term* terms_host, const fx_loss_term* terms_
   FX_REQUIRE(terms_host && terms_dev && nterms > 0 && coef && gout && workspace, "loss_terms_bwd: bad arguments");
   hipStream_t s = (hipStream_t)stream;
   float* gterm = workspace;
-  hipLaunchKernelGGL(combine_bwd_kernel, dim3(cdiv(nterms, 64)), dim3(64), 0, s, gout, coef, nterms, nout, gterm);
+  fx_launch(combine_bwd_kernel, dim3(cdiv(nterms, 64)), dim3(64), 0, s, gout, coef, nterms, nout, gterm);
   FX_CHECK_HIP(hipGetLastError());
   int maxC = 1;
   bool has[3] = {false, false, false};
@@ -655,16 +655,16 @@ int fx_loss_terms_bwd(const fx_loss_term* terms_host, const fx_loss_term* terms_
     if (t.kind == FX_TERM_CLASS) maxC = std::max(maxC, t.C);
   }
   if (has[FX_TERM_CLASS]) {
-    hipLaunchKernelGGL(terms_bwd_kernel, dim3(FX_LOSS_NB, nterms), dim3(VT), sizeof(float) * 4 * maxC, s, terms_dev, gterm,
+    fx_launch(terms_bwd_kernel, dim3(FX_LOSS_NB, nterms), dim3(VT), sizeof(float) * 4 * maxC, s, terms_dev, gterm,
                        (int)FX_TERM_CLASS);
     FX_CHECK_HIP(hipGetLastError());
   }
   if (has[FX_TERM_ATTN]) {
-    hipLaunchKernelGGL(terms_bwd_kernel, dim3(FX_LOSS_NB, nterms), dim3(VT), 0, s, terms_dev, gterm, (int)FX_TERM_ATTN);
+    fx_launch(terms_bwd_kernel, dim3(FX_LOSS_NB, nterms), dim3(VT), 0, s, terms_dev, gterm, (int)FX_TERM_ATTN);
     FX_CHECK_HIP(hipGetLastError());
   }
   if (has[FX_TERM_INFONCE]) {
-    hipLaunchKernelGGL(infonce_bwd_kernel, dim3(256, nterms), dim3(VT), 0, s, terms_dev, gterm);
+    fx_launch(infonce_bwd_kernel, dim3(256, nterms), dim3(VT), 0, s, terms_dev, gterm);
     FX_CHECK_HIP(hipGetLastError());
     for (int i = 0; i < nterms; ++i) {   // demb = dsim . text / temp
       const fx_loss_term& t = terms_host[i];
@@ -687,7 +687,7 @@ int fx_match_cost(const fx_video_attn* vids_host, const fx_video_attn* vids_dev,
     Q = std::max(Q, vids_host[i].Q);
     C1 = std::max(C1, vids_host[i].C1);
   }
-  hipLaunchKernelGGL(match_cost_kernel, dim3(Q, nvid), dim3(VT), sizeof(float) * (C1 + Gmax + 1), (hipStream_t)stream,
+  fx_launch(match_cost_kernel, dim3(Q, nvid), dim3(VT), sizeof(float) * (C1 + Gmax + 1), (hipStream_t)stream,
                      vids_dev, pc, a2fc, Gmax, cost);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
@@ -704,7 +704,7 @@ int fx_eval_pred(const fx_video_attn* vids_host, const fx_video_attn* vids_dev, 
     QC = std::max(QC, v.Q * v.C1);
   }
   FX_REQUIRE((size_t)QC * sizeof(float) <= 60 * 1024, "eval_pred: too many token x class probabilities");
-  hipLaunchKernelGGL(eval_pred_kernel, dim3(cdiv(T, VT), nvid), dim3(VT), sizeof(float) * QC, (hipStream_t)stream,
+  fx_launch(eval_pred_kernel, dim3(cdiv(T, VT), nvid), dim3(VT), sizeof(float) * QC, (hipStream_t)stream,
                      vids_dev, mwt, pred);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;

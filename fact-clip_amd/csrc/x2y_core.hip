@@ -243,9 +243,9 @@ int launch_a2f(A2fArgs& a, int mode, const int* yoff, const int* xoff, const lon
   for (int v = a.nvid + 1; v <= FX_X2Y_MAXV; ++v) a.wg_off[v] = wg;
   if (wg == 0) return FX_OK;
   if (mode == 0)
-    hipLaunchKernelGGL(x2y_a2f_kernel<0>, dim3(wg), dim3(XT), 0, s, a);
+    fx_launch(x2y_a2f_kernel<0>, dim3(wg), dim3(XT), 0, s, a);
   else
-    hipLaunchKernelGGL(x2y_a2f_kernel<1>, dim3(wg), dim3(XT), 0, s, a);
+    fx_launch(x2y_a2f_kernel<1>, dim3(wg), dim3(XT), 0, s, a);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }
@@ -479,6 +479,8 @@ struct F2aBwdArgs {
   float* part;          // (chunks, FMAXQ, Hd)
   float* stats;         // (chunks, FMAXQ, 2)
   unsigned* bar;        // one-launch form: {arrivals, ..., exits at +32} of the stream's counter pool
+  unsigned* status;     // caller's status word (nullable): FX_STATUS_X2Y_TIMEOUT when the barrier gives up
+  unsigned spin_max;    // barrier polls before a workgroup gives up
   int Hd, nvid;
   float scale;
   int yoff[FX_X2Y_MAXV + 1], xoff[FX_X2Y_MAXV + 1];
@@ -491,18 +493,28 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t f2a_rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
 }
 
-// Grid barrier of the one-launch form (every workgroup co-resident: grid <= 256): each workgroup's
-// write-through stores acknowledged (vmcnt 0) before its arrival; the last workgroup past the barrier
-// re-arms the slot.  Bounded spin (~1 s): on timeout the workgroup goes on (results wrong, never a hang)
-__device__ __forceinline__ void f2a_grid_sync(unsigned* bar) {
+// Grid barrier of the one-launch form (every workgroup co-resident: the grid is capped by the occupancy
+// calculator on the host): each workgroup's write-through stores acknowledged (vmcnt 0) before its arrival;
+// every workgroup counts its exit, timed out or not, and the last one re-arms the slot.  Bounded spin: a
+// workgroup that gives up ORs FX_STATUS_X2Y_TIMEOUT into the caller's status word (read back with the step's
+// status, which fails the step and makes FusedAdam skip its update) and goes on -- never a hang
+__device__ __forceinline__ void f2a_grid_sync(unsigned* bar, unsigned* status, unsigned spin_max) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned G = gridDim.x;
     __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned n = 0;
-    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < G && ++n < (1u << 22))
+    bool late = false;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < G) {
+      if (++n >= spin_max) {
+        late = true;
+        break;
+      }
       __builtin_amdgcn_s_sleep(1);
+    }
+    if (late && status)
+      __hip_atomic_fetch_or(status, (unsigned)FX_STATUS_X2Y_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned prev = __hip_atomic_fetch_add(bar + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (prev == G - 1) {   // every workgroup is past the barrier
       __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -666,7 +678,7 @@ __global__ __launch_bounds__(XT) void x2y_f2a_bwd_kernel(F2aBwdArgs a) {
   }
   if (PASS == 3) {
     // every chunk's row-dot partial written through: the row sums of this video's chunks
-    f2a_grid_sync(a.bar);
+    f2a_grid_sync(a.bar, a.status, a.spin_max);
     if (tid < FMAXQ) {
       const int nch = (nx + FC - 1) / FC;
       float sum = 0.f;
@@ -972,7 +984,7 @@ int launch_x2y_a2f_dw(const float* attn, const float* dl, const float* dfeat, lo
   a.ws = ws;
   a.cnt = (nchunk > 1 && groups <= kArrivalCounters) ? arrival_counters(s) : nullptr;
   FX_REQUIRE(nchunk == 1 || (a.cnt && ws), "x2y a2f dW: workspace / counters required");
-  hipLaunchKernelGGL(x2y_a2f_dw_kernel, dim3(nchunk, ncb, 2 * nvid), dim3(DWT), 0, s, a);
+  fx_launch(x2y_a2f_dw_kernel, dim3(nchunk, ncb, 2 * nvid), dim3(DWT), 0, s, a);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }
@@ -1030,8 +1042,8 @@ int launch_x2y_f2a_fwd(const float* yq, const float* xk, const float* xv, int Hd
   a.part = ws;
   a.stats = ws + (long long)nch * FMAXQ * Hd;
   if (nch == 0 || maxq == 0) return FX_OK;
-  hipLaunchKernelGGL(x2y_f2a_chunk_kernel, dim3(nch), dim3(XT), 0, s, a);
-  hipLaunchKernelGGL(x2y_f2a_merge_kernel, dim3(maxq, nvid), dim3(XT), 0, s, a);
+  fx_launch(x2y_f2a_chunk_kernel, dim3(nch), dim3(XT), 0, s, a);
+  fx_launch(x2y_f2a_merge_kernel, dim3(maxq, nvid), dim3(XT), 0, s, a);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }
@@ -1039,7 +1051,7 @@ int launch_x2y_f2a_fwd(const float* yq, const float* xk, const float* xv, int Hd
 int launch_x2y_f2a_bwd(const float* dfeat, long long ldf, const float* xv, const float* xk, const float* yq,
                        const float* attn, const float* dattn, const float* dlogit_in, int Hd, float scale, int nvid,
                        const int* yoff, const int* xoff, const long long* aoff, float* dlogit, float* dxv, float* dxk,
-                       float* dyq, float* ws, hipStream_t s) {
+                       float* dyq, float* ws, unsigned* status, hipStream_t s) {
   FX_REQUIRE(x2y_f2a_fusable(nvid, xoff, yoff, Hd), "x2y f2a core: <= 64 queries per video, Hd % 256 == 0");
   FX_REQUIRE(ldf % 4 == 0 && (reinterpret_cast<uintptr_t>(dfeat) & 15) == 0, "x2y f2a bwd: dfeat rows must be 16-B aligned");
   F2aBwdArgs a{};
@@ -1074,15 +1086,19 @@ int launch_x2y_f2a_bwd(const float* dfeat, long long ldf, const float* xv, const
   a.stats = ws + (long long)nch * FMAXQ * Hd;
   if (nch == 0 || maxq == 0) return FX_OK;
   // one launch when every chunk's workgroup can be resident at once (the grid barrier waits for all of
-  // them): <= 256 chunks; FX_X2Y_F2A_ONE=0 keeps the two launches (A/B)
-  a.bar = (knobs().x2y_f2a_one && nch <= 256) ? arrival_counters(s) : nullptr;
+  // them): the occupancy calculator's bound for this kernel on this device (CU count x workgroups per CU);
+  // FX_X2Y_F2A_ONE=0 keeps the two launches (A/B)
+  a.status = status;
+  a.spin_max = x2y_spin_max();
+  const int resident = coresident_blocks((const void*)x2y_f2a_bwd_kernel<3>, XT, 0);
+  a.bar = (knobs().x2y_f2a_one && nch <= resident) ? arrival_counters(s) : nullptr;
   if (a.bar) {
-    hipLaunchKernelGGL(x2y_f2a_bwd_kernel<3>, dim3(nch), dim3(XT), 0, s, a);
+    fx_launch(x2y_f2a_bwd_kernel<3>, dim3(nch), dim3(XT), 0, s, a);
   } else {
-    hipLaunchKernelGGL(x2y_f2a_bwd_kernel<1>, dim3(nch), dim3(XT), 0, s, a);
-    hipLaunchKernelGGL(x2y_f2a_bwd_kernel<2>, dim3(nch), dim3(XT), 0, s, a);
+    fx_launch(x2y_f2a_bwd_kernel<1>, dim3(nch), dim3(XT), 0, s, a);
+    fx_launch(x2y_f2a_bwd_kernel<2>, dim3(nch), dim3(XT), 0, s, a);
   }
-  hipLaunchKernelGGL(x2y_f2a_bwd_merge_kernel, dim3(maxq, nvid), dim3(XT), 0, s, a);
+  fx_launch(x2y_f2a_bwd_merge_kernel, dim3(maxq, nvid), dim3(XT), 0, s, a);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;
 }

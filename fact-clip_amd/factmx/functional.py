@@ -634,7 +634,8 @@ class X2YFn(torch.autograd.Function):
                               ctx.drop[0], ctx.drop[1], nx.ptr(attn),
                               nx.ptr(saved), nx.ptr(dout), outdim, nx.ptr(dlogit), nx.ptr(dattn), nx.ptr(dX),
                               nx.ptr(dXp), nx.ptr(dY), nx.ptr(dYp), *[nx.ptr(t) for t in bufs], fx, fy,
-                              nx.ptr(ws), int(defer), nx.stream()), "fx_x2y_bwd")
+                              nx.ptr(ws), int(defer), nx.ptr(device_status(dev)), nx.stream()), "fx_x2y_bwd")
+        _queue_backward_status(dev)    # (the f2a core's grid-barrier timeout, FX_STATUS_X2Y_TIMEOUT)
         if defer:
             _defer_to_side(X, Y, saved, dout, ws, *bufs)
         if sx is not None:
@@ -989,6 +990,8 @@ def device_status(dev):
     return code (FX_STATUS_GRU_TIMEOUT: a BiGRU workgroup gave up waiting for a peer, so that
     launch's outputs are wrong).  Read at the step's host read-back (status_raise)."""
     dev = torch.device(dev)
+    if dev.type == "cuda" and dev.index is None:     # one word per physical device ("cuda" == "cuda:<current>")
+        dev = torch.device("cuda", torch.cuda.current_device())
     t = _status.get(dev)
     if t is None:
         t = torch.zeros(4, dtype=torch.int32, device=dev)
@@ -1011,6 +1014,8 @@ def _status_text(value):
         parts.append("a BiGRU workgroup timed out waiting for its peers (FX_STATUS_GRU_TIMEOUT)")
     if value & nx.STATUS_TOK_TIMEOUT:
         parts.append("a persistent token-kernel workgroup timed out at a grid barrier (FX_STATUS_TOK_TIMEOUT)")
+    if value & nx.STATUS_X2Y_TIMEOUT:
+        parts.append("an X2Y f2a-backward workgroup timed out at its grid barrier (FX_STATUS_X2Y_TIMEOUT)")
     return "; ".join(parts) or "unknown failure"
 
 
@@ -1061,9 +1066,8 @@ def resolve_backward_status(wait=False):
             _bwd_status.clear()
             device_status(dev).zero_()
             raise nx.FactmxNativeError(
-                f"device status {int(h[0])}: a BiGRU workgroup timed out waiting for its peers "
-                "(FX_STATUS_GRU_TIMEOUT) in the BACKWARD pass of the previous step -- its gradients are invalid "
-                "(a factmx FusedAdam step on them was skipped on the device)")
+                f"device status {int(h[0])}: {_status_text(int(h[0]))} in the BACKWARD pass of the previous step "
+                "-- its gradients are invalid (a factmx FusedAdam step on them was skipped on the device)")
 
 
 def check_device_status(dev=None):
@@ -1072,8 +1076,7 @@ def check_device_status(dev=None):
     vloss.resolve_pending()
     resolve_backward_status(wait=True)
     dev = torch.device("cuda", torch.cuda.current_device()) if dev is None else torch.device(dev)
-    if dev in _status:
-        status_raise(int(_status[dev][0].item()), dev)
+    status_raise(int(device_status(dev)[0].item()), dev)
 
 
 class GRUFn(torch.autograd.Function):
@@ -1437,6 +1440,7 @@ class DecoderFn(torch.autograd.Function):
                                   nx.ld(dout),
                                   nx.ptr(dtgt), nx.ld(dtgt), nx.ptr(dqpos), nx.ptr(dmem), nx.ld(dmem), nx.ptr(dmpos),
                                   nx.ld(dmpos), nx.ptr(saved), nx.ptr(ws), nx.stream()), "fx_decoder_bwd")
+        _queue_backward_status(dev)    # (a token-kernel barrier timeout in this backward, FX_STATUS_TOK_TIMEOUT)
         if defer:   # (dout too: the output linear's weight gradient reads it on the side stream)
             _defer_to_side(tgt, mem, mpos, saved, ws, dout)
         if sink is not None:

@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FACTMX_LIB", os.path.join(_HERE, "_lib", "libfactmx.so"))
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -86,6 +86,7 @@ class DecoderGrads(ctypes.Structure):
 
 STATUS_GRU_TIMEOUT = 1   # FX_STATUS_GRU_TIMEOUT: a BiGRU workgroup gave up waiting for a peer
 STATUS_TOK_TIMEOUT = 2   # FX_STATUS_TOK_TIMEOUT: a persistent token-kernel barrier wait gave up
+STATUS_X2Y_TIMEOUT = 4   # FX_STATUS_X2Y_TIMEOUT: the one-launch X2Y f2a backward's grid barrier gave up
 LOSS_MAXK = 512        # FX_LOSS_MAXK: matched columns of an attention loss term
 LOSS_NB = 128          # FX_LOSS_NB: row blocks per loss term
 TERM_CLASS, TERM_ATTN, TERM_INFONCE = 0, 1, 2
@@ -123,7 +124,7 @@ SIGNATURES = {
     "fx_x2y_fwd": (I, [P, L, I, I, P, L, I, P, L, I, I, P, L, I, P, P, P, P, P, P, P, P, I, I, I, P, P, F, U, P, L, P,
                        P, P, P, P]),
     "fx_x2y_bwd": (I, [P, L, I, I, I, P, L, I, I, I, P, P, P, P, I, I, I, P, P, F, U, P, P, P, L, P, P, P, P, P, P,
-                       P, P, P, P, P, P, P, P, I, I, P, I, P]),
+                       P, P, P, P, P, P, P, P, I, I, P, I, P, P]),
     "fx_decoder_saved_floats": (L, [ctypes.POINTER(DecoderParams), I, I, I, I, I]),
     "fx_decoder_workspace_floats": (L, [ctypes.POINTER(DecoderParams), I, I, I, I, I]),
     "fx_tok_gemm": (I, [P, L, I, I, I, I, P, P, P, L, I, P, P, L, P, L, P, P]),
@@ -189,7 +190,9 @@ SIGNATURES = {
     "fx_get_default_precision": (I, []),
     "fx_prof_enable": (I, [I, I]),
     "fx_prof_collect": (I, [I, ctypes.POINTER(D), ctypes.POINTER(D), ctypes.POINTER(D), ctypes.POINTER(I)]),
+    "fx_prof_collect_kernels": (I, [I, ctypes.POINTER(D), ctypes.POINTER(I), ctypes.POINTER(I)]),
     "fx_prof_disable": (None, []),
+    "fx_debug_set_spin": (I, [I, I]),
 }
 
 _lib = None

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FX_ABI_VERSION 19
+#define FX_ABI_VERSION 20
 
 enum {
   FX_OK = 0,
@@ -166,6 +166,8 @@ int fx_linear_bwd(const float* dy, long long lddy, const float* x, long long ldx
  * has_xpos / has_ypos: bit 0 = the forward had the position input; bit 1 = ACCUMULATE (+=) the
  * position gradient into dXpos / dYpos instead of writing it (one buffer shared by every op that
  * reads the same position table, so autograd does not add the per-op gradients pairwise).
+ * status (bwd, nullable): device int32 word; the one-launch f2a backward core ORs
+ * FX_STATUS_X2Y_TIMEOUT into it when its grid barrier gives up (its outputs are then wrong).
  * ---------------------------------------------------------------------- */
 long long fx_x2y_saved_floats(int Nx, int xdim, int Ny, int ydim, int Hd);
 long long fx_x2y_workspace_floats(int Nx, int xdim, int Ny, int ydim, int Hd, int outdim, int nvid,
@@ -185,7 +187,7 @@ int fx_x2y_bwd(const float* X, long long ldx, int Nx, int xdim, int xpos_cols, c
                long long lddo, const float* dlogit, const float* dattn, float* dX, float* dXpos,
                float* dY, float* dYpos, float* dwk, float* dbk, float* dwv, float* dbv, float* dwq,
                float* dbq, float* dwy, float* dby, int has_xpos, int has_ypos, float* workspace,
-               int side_defer, void* stream);
+               int side_defer, int32_t* status, void* stream);
 
 /* ------------------------------------------------------------------------
  * Action-token decoder, whole stack in one call (post-norm, ReLU FFN):
@@ -510,6 +512,7 @@ int fx_seg_sum_rows(const float* dx, long long lddx, const int32_t* seg_start, c
  * ---------------------------------------------------------------------- */
 #define FX_STATUS_GRU_TIMEOUT 1
 #define FX_STATUS_TOK_TIMEOUT 2   /* fx_decoder_*: a persistent token-kernel barrier wait gave up */
+#define FX_STATUS_X2Y_TIMEOUT 4   /* fx_x2y_bwd: the one-launch f2a backward's grid barrier gave up */
 long long fx_gru_saved_floats(int S, int Hh);
 long long fx_gru_workspace_floats(int S, int nseq, int In, int Hh);
 int fx_gru_bidir_fwd(const float* x, long long ldx, int S, int nseq, const int* seq_off, int In,
@@ -720,7 +723,8 @@ int fx_get_default_precision(void);
  *   0 = dilated-conv implicit GEMM (conv forward, conv dX),
  *   1 = attention over T forward (tattn_fwd_kernel + split merge),
  *   2 = attention over T backward (tattn_bwd_kernel + split merge),
- *   3-6 = X2Y cores (a2f fwd, a2f bwd, f2a fwd, f2a bwd),
+ *   3-6 = X2Y cores of frame-level calls, max(Nx, Ny) >= 1024 (a2f fwd, a2f bwd, f2a fwd,
+ *         f2a bwd), 11-14 = the same cores of segment-level calls,
  *   7 = fused MS-TCN layer (frl_kernel: conv + ReLU + 1x1 + residual forward,
  *       or the fused dX chain backward),
  *   8 = persistent token-kernel launches of the decoders (tokdec.hip programs),
@@ -728,11 +732,22 @@ int fx_get_default_precision(void);
  *       frame-level product, M = frames, N = 2 d_model layers, K = memory width),
  *   10 = X2Y input projections (k, v from X, q from Y: three products per call).
  * fx_prof_enable resets one kind; fx_prof_disable resets all.
+ * fx_prof_collect: the event brackets around each call (its kernels plus any host-issue gap
+ *   between them).  fx_prof_collect_kernels: the same calls' kernels alone -- every kernel
+ *   launched on the call's stream inside a bracket carries its own hipExtLaunchKernel event
+ *   pair, i.e. its execution time as the rocprofv3 kernel trace reports it (untimed: kernels
+ *   past the pool of 16 pairs per bracket).
  * ---------------------------------------------------------------------- */
 int fx_prof_enable(int kind, int max_events);
 int fx_prof_collect(int kind, double* total_ms, double* total_flops, double* total_bytes,
                     int* count);
+int fx_prof_collect_kernels(int kind, double* kernel_ms, int* kernels, int* untimed);
 void fx_prof_disable(void);
+
+/* Diagnostic (timeout tests): grid-barrier polls before a persistent workgroup gives up --
+ * which = 0 the token kernel (fx_decoder_*), 1 the one-launch X2Y f2a backward; polls <= 0
+ * restores the default (FX_TOK_SPIN or ~1 s). */
+int fx_debug_set_spin(int which, int polls);
 
 #ifdef __cplusplus
 }
