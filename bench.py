@@ -424,18 +424,18 @@ def fused_layer_roofline(pr, peak):
 
 
 def gemm_roofline(name, pr, peak):
-    """A cross-attention projection GEMM kind, MFMA-bound: algorithmic FLOPs over the kernel time of its
+    """A cross-attention projection GEMM kind, MFMA-bound: algorithmic FLOPs over the HIP-event time of its
     launches in the sampled step(s); `traffic` from a committed standalone PMC pass of the same shape."""
     n = pr.calls
-    if n <= 0 or pr.kernel_ms <= 0:
+    if n <= 0 or pr.bracket_ms <= 0:
         return None
     note, pmc = XATTN_NOTES[name]
-    ms = pr.kernel_ms
+    ms = pr.bracket_ms
     tf = pr.flops / (ms * 1e-3) / 1e12
     out = dict(kernel=note, bound="mfma", achieved=round(tf, 2), peak=round(peak, 1), unit="TFLOP/s",
                frac=round(tf / peak, 4), launches=n, avg_launch_ms=round(ms / n, 5),
                flops_per_launch=pr.flops / n, bytes_per_launch=pr.bytes / n,
-               hbm_gbs_algorithmic=round(pr.bytes / (ms * 1e-3) / 1e9, 1), **pr.timing())
+               hbm_gbs_algorithmic=round(pr.bytes / (ms * 1e-3) / 1e9, 1))
     path = os.path.join(ROOT, "profiles", pmc)
     out["traffic"] = None
     if os.path.exists(path):
@@ -695,7 +695,7 @@ def main():
     frames = world * sum(Ts) * args.steps
     value = frames / elapsed
     if rank == 0:
-        avg_ms = conv_prof.kernel_ms / max(conv_prof.calls, 1)
+        avg_ms = conv_prof.bracket_ms / max(conv_prof.calls, 1)
         flops_per_launch = conv_prof.flops / max(conv_prof.calls, 1)
         achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
         default_shape = args.config == "havid" and T == T_DEFAULT and nv == 2
@@ -714,15 +714,14 @@ def main():
                                 "the fused MS-TCN layer kernel does not run)"),
                         launches=conv_prof.calls, avg_launch_ms=round(avg_ms, 5),
                         flops_per_launch=flops_per_launch,
-                        sample=f"the conv-GEMM launches of the first timed step ({conv_prof.calls})",
-                        **conv_prof.timing())
+                        sample=f"HIP events around the conv-GEMM launches of the first timed step ({conv_prof.calls})")
         # the dominant kernel by measured time in the sampled step: the fused MS-TCN layer when it ran
         frl_roofline = fused_layer_roofline(frl_prof, F32_MFMA_PEAK_TFLOPS)
         if frl_roofline is not None:
             frl_roofline["traffic"] = traffic_from_profiles(FRL_KERNEL) if default_shape else None
             frl_roofline["sample"] = (f"the fused-layer launches of the first timed step ({frl_roofline['launches']}), "
                                       "one event pair per MS-TCN stack and direction")
-        roofline = (frl_roofline if frl_roofline is not None and frl_prof.kernel_ms > conv_prof.kernel_ms
+        roofline = (frl_roofline if frl_roofline is not None and frl_prof.bracket_ms > conv_prof.bracket_ms
                     else conv_roofline)
         roofline_attention = {name: attention_roofline(f"tattn_{name}32_kernel (merge folded into the launch)", v)
                               for name, v in attn_prof.items()}

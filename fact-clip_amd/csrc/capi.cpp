@@ -41,7 +41,6 @@ constexpr int kProfKinds = 15;  // 0 conv GEMM, 1 / 2 attention over T fwd / bwd
                                 // calls (a2f fwd, a2f bwd, f2a fwd, f2a bwd), 7 fused MS-TCN layer, 8 persistent
                                 // token-kernel launches (tokdec.hip), 9 SCA frame-memory K/V projection GEMM,
                                 // 10 X2Y input projections (k, v, q), 11-14 X2Y cores of segment-level calls
-constexpr int kKernelPairsPerEvent = 16;
 std::mutex g_prof_mu;
 ProfState g_prof[kProfKinds];
 std::atomic<int> g_spin_override[2] = {{-1}, {-1}};   // fx_debug_set_spin: 0 token kernel, 1 X2Y f2a backward
@@ -2128,8 +2127,11 @@ int fx_prof_enable(int kind, int max_events) {
   prof_reset(p);
   p.ev.resize(2 * (size_t)max_events);
   for (auto& e : p.ev) FX_CHECK_HIP(hipEventCreate(&e));
-  // kernel-time pairs: the fused-layer chains bracket up to one launch per layer, the other kinds a few
-  p.kev.resize(2 * (size_t)max_events * (kind == 7 ? kKernelPairsPerEvent : 4));
+  // kernel-time pairs for the attention-over-T and X2Y kinds (a few kernels per call); the MFMA-bound kinds
+  // (conv GEMM, fused layer chains, projection GEMMs) are timed by their brackets alone: their kernels run
+  // back to back inside one C call, and an event pair per kernel would add its own dispatch gap to the chain
+  const bool kpairs = (kind >= 1 && kind <= 6) || kind >= 11;
+  p.kev.resize(kpairs ? 2 * (size_t)max_events * 4 : 0);
   for (auto& e : p.kev) FX_CHECK_HIP(hipEventCreate(&e));
   p.flops.assign(max_events, 0.0);
   p.bytes.assign(max_events, 0.0);

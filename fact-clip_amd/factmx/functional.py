@@ -1161,11 +1161,15 @@ def segments_from_probs(x2d, col0, ncls):
     return S, seg_id, st[:S], en[:S]
 
 
-def segments_from_probs_batched(x2d, col0, ncls, f_off):
+_NS_HOST = {}
+
+
+def segments_from_probs_batched(x2d, col0, ncls, f_off, while_waiting=None):
     """``segments_from_probs`` for the videos stacked in x2d (host frame-row prefix list f_off, ragged
     lengths allowed), with ONE host read of all segment counts.  Returns (S list, per-video local
     (seg_id, start, end) views, global (seg_id, start, end) over the stacked frame rows /
-    concatenated segments)."""
+    concatenated segments).  ``while_waiting``: host work that does not need S, run after the counts'
+    copy is enqueued and before the host waits for it (the device is still working up to this block)."""
     lib = nx.load()
     dev = x2d.device
     nvid = len(f_off) - 1
@@ -1176,7 +1180,16 @@ def segments_from_probs_batched(x2d, col0, ncls, f_off):
     ns = buf[4 * n:]
     _check(lib.fx_segments_from_probs(nx.ptr(x2d), nx.ld(x2d), col0, ncls, 0, nvid, ro, nx.ptr(pred), nx.ptr(seg_id),
                                       nx.ptr(st), nx.ptr(en), nx.ptr(ns), nx.stream()), "fx_segments_from_probs")
-    S = [int(v) for v in ns.tolist()]
+    nh = _NS_HOST.get(nvid)
+    if nh is None:
+        nh = _NS_HOST[nvid] = torch.empty(nvid, dtype=torch.int32, pin_memory=True)
+    nh.copy_(ns, non_blocking=True)
+    ready = torch.cuda.Event()
+    ready.record()
+    if while_waiting is not None:
+        while_waiting()
+    ready.synchronize()
+    S = nh.tolist()
     tot = sum(S)
     g = torch.empty(n + 2 * tot, device=dev, dtype=torch.int32)
     gid, gst, gen = g[:n], g[n:n + tot], g[n + tot:]

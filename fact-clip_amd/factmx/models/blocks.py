@@ -352,8 +352,10 @@ class UpdateBlockTDU(Block):
 
     def forward_batch(self, f2, a2, fpos, apos, vb):
         # temporal downsample: one segmentation launch + ONE host read of every video's S
+        # (the first TDU block: the loss phase's label-only host work runs while the host waits for S)
+        hook, vb.while_waiting = vb.while_waiting, None
         S, local, (gid, gst, gen) = fxf.segments_from_probs_batched(f2, f2.shape[1] - self.nclass, self.nclass,
-                                                                     vb.f_off)
+                                                                     vb.f_off, hook)
         s_off = [0]
         for n_ in S:
             s_off.append(s_off[-1] + n_)
@@ -510,6 +512,9 @@ class _FACTBase(nn.Module):
         Q = self.cfg.FACT.ntoken
         vb = _VideoBatch(nvid, [int(s.shape[0]) for s in seq_list], Q)
         vb.on_a2f, vb.last = on_a2f, self.block_list[-1]
+        if on_a2f is not None:
+            dev = seq_list[0].device
+            vb.while_waiting = lambda: on_a2f.prepare(dev)
         frames = []
         for seq in seq_list:
             x = seq.unsqueeze(1)
@@ -689,7 +694,7 @@ class _VideoBatch:
         for T in self.Ts:
             self.f_off.append(self.f_off[-1] + T)
         self.a_off = [v * Q for v in range(nvid + 1)]
-        self.on_a2f = self.last = None
+        self.on_a2f = self.last = self.while_waiting = None
 
     def fr(self, v):
         return slice(self.f_off[v], self.f_off[v + 1])

@@ -270,6 +270,75 @@ class _LossFn(torch.autograd.Function):
         return (None,) + tuple(plan["grads"])
 
 
+def _stage2_labels(net, labs, G):
+    """Stage 2's tables that depend on the labels only (EarlyMatch.prepare): the holdout remap and the
+    per-video InfoNCE targets (blocks.py:677-747), and the term table's host arrays -- token targets and
+    matched-column slots (capacity G[v] >= K), filled after the matching -- in the pack sent with it."""
+    from .blocks import FACT_CLIP
+    cfg = net.cfg
+    nvid = len(labs)
+    Q = cfg.FACT.ntoken
+    C1 = net.num_classes + 1
+    text = getattr(net, "text_embeddings", None) if isinstance(net, FACT_CLIP) else None
+    use_clip = text is not None
+    con_on = []
+    remap = None
+    text_seen = text
+    if use_clip:
+        hold = list(getattr(cfg, "holdout_classes", []) or [])
+        if hold:
+            n = text.shape[0]
+            key = (n, tuple(hold), text.data_ptr(), text._version)
+            if getattr(net, "_vloss_text_key", None) != key:
+                seen = [i for i in range(n) if i not in set(hold)]
+                rm = np.full(n, -1, dtype=np.int64)
+                rm[seen] = np.arange(len(seen))
+                net._vloss_text = (text[torch.tensor(seen, device=text.device)].contiguous(), rm)
+                net._vloss_text_key = key
+            text_seen, remap = net._vloss_text
+        else:
+            text_seen = text.contiguous()
+    y_con = []
+    for v in range(nvid):
+        if not use_clip:
+            con_on.append(False)
+            y_con.append(None)
+            continue
+        y = remap[labs[v]] if remap is not None else labs[v]
+        con_on.append(bool((y != -1).any()))
+        y_con.append(y)
+    pk2 = _Pack()
+    # per video: token targets (Q) and the matched columns (capacity G[v] >= K), filled after matching
+    tgt_arr = [np.full(Q, C1 - 1, dtype=np.int32) for _ in range(nvid)]
+    tgt_off = [pk2.array(t, np.int32) for t in tgt_arr]
+    tgt_arr = [pk2.items[-nvid + v][1] for v in range(nvid)]     # the buffers pk2 sends
+    kcap = [max(int(G[v]), 1) for v in range(nvid)]
+    sw_arr, sw_list = [], []
+    for v in range(nvid):
+        arrs = []
+        offs = []
+        for dt in (np.int32, np.int32, np.int32, np.float32):
+            offs.append(pk2.array(np.zeros(kcap[v], dtype=dt), dt))
+            arrs.append(pk2.items[-1][1])
+        sw_arr.append(arrs)
+        sw_list.append(tuple(offs))
+    ycon_off = [pk2.array(y, np.int32) if y is not None and con_on[v] else None for v, y in enumerate(y_con)]
+    return dict(use_clip=use_clip, con_on=con_on, y_con=y_con, text_seen=text_seen, pk2=pk2, tgt_off=tgt_off,
+                tgt_arr=tgt_arr, kcap=kcap, sw_arr=sw_arr, sw_list=sw_list, ycon_off=ycon_off)
+
+
+_PINNED = {}
+
+
+def _pinned(key, shape, dtype):
+    """A pinned host buffer reused step after step for one read-back (its previous contents have been read:
+    the step's read-back resolves before the next forward's loss phase enqueues the next copy)."""
+    t = _PINNED.get(key)
+    if t is None or t.shape != torch.Size(shape) or t.dtype != dtype:
+        t = _PINNED[key] = torch.empty(shape, dtype=dtype, pin_memory=True)
+    return t
+
+
 class EarlyMatch:
     """Stage 1, called by the LAST block's forward_batch as soon as its token logits and token->frame
     attention exist (before its frame branch and the CLIP head run): ground truth from the host
@@ -279,13 +348,18 @@ class EarlyMatch:
     def __init__(self, net, hosts):
         self.net, self.hosts = net, hosts
         self.done = False
+        self.prepared = False
 
-    def __call__(self, vb, a_cl, a2f_at, seg=None):
-        net, cfg = self.net, self.net.cfg
-        lib = nx.load()
-        nvid, Q, fo = vb.nvid, vb.Q, vb.f_off
+    def prepare(self, dev):
+        """The label-only host work of the loss phase: ground-truth segments, class weights, their upload,
+        and the holdout / InfoNCE label tables of stage 2.  The first TDU block runs it while the host
+        waits for that block's segment counts (the device is still working through the previous step's
+        backward and the first blocks), so none of it is on the host path after the last block, where the
+        device would idle behind it; without a TDU block the last block's stage 1 runs it."""
+        if self.prepared:
+            return
+        net = self.net
         C1 = net.num_classes + 1
-        dev = a_cl.device
         gts, labs = [], []
         for lh, ev in self.hosts:
             if ev is not None:
@@ -294,14 +368,29 @@ class EarlyMatch:
             labs.append(lab)
             gts.append(gt_segments(lab))
         G = [len(g[0]) for g in gts]
-        Gmax = max(G)
         pk = _Pack()
         gt_off = [(pk.array(g[0], np.int32), pk.array(g[1], np.int32), pk.array(g[2], np.int32)) for g in gts]
         lab_off = [pk.array(lab, np.int32) for lab in labs]
         cw = class_weights(net.mcriterion, C1)
         cw_off = pk.array(cw, np.float32)
-        va_off, va = pk.structs(nx.VideoAttn, nvid)
         base = pk.alloc(dev)
+        pk.send()
+        self.__dict__.update(labs=labs, gts=gts, G=G, Gmax=max(G), gt_off=gt_off, lab_off=lab_off, cw=cw,
+                             cw_off=cw_off, pk=pk, base=base)
+        self.stage2 = _stage2_labels(net, labs, G)
+        self.prepared = True
+
+    def __call__(self, vb, a_cl, a2f_at, seg=None):
+        net, cfg = self.net, self.net.cfg
+        lib = nx.load()
+        nvid, Q, fo = vb.nvid, vb.Q, vb.f_off
+        C1 = net.num_classes + 1
+        dev = a_cl.device
+        self.prepare(dev)
+        G, Gmax, gt_off, base = self.G, self.Gmax, self.gt_off, self.base
+        pkv = _Pack()
+        va_off, va = pkv.structs(nx.VideoAttn, nvid)
+        vbase = pkv.alloc(dev)
         for v in range(nvid):
             a = va[v]
             a.Q, a.C1, a.T, a.G = Q, C1, vb.Ts[v], G[v]
@@ -314,19 +403,18 @@ class EarlyMatch:
                 a.attn, a.lda = a2f_at.data_ptr() + 4 * Q * fo[v], Q
             a.gs, a.ge, a.gl = (base + o for o in gt_off[v])
             a.pred_off = fo[v]
-        pk.send()
+        pkv.send()
         self.cost_host = None
         if cfg.Loss.match != "seq":
             cost = torch.empty(nvid * Q * Gmax, dtype=torch.float32, device=dev)
-            nx.check(lib.fx_match_cost(ctypes.addressof(va), base + va_off, nvid, float(cfg.Loss.pc),
+            nx.check(lib.fx_match_cost(ctypes.addressof(va), vbase + va_off, nvid, float(cfg.Loss.pc),
                                        float(cfg.Loss.a2fc), Gmax, nx.ptr(cost), nx.stream()), "fx_match_cost")
-            self.cost_host = torch.empty(cost.shape, dtype=torch.float32, pin_memory=True)
+            self.cost_host = _pinned("cost", cost.shape, torch.float32)
             self.cost_host.copy_(cost, non_blocking=True)
             self.cost_ready = torch.cuda.Event()
             self.cost_ready.record()
             self.cost_dev = cost
-        self.__dict__.update(labs=labs, gts=gts, G=G, Gmax=Gmax, gt_off=gt_off, lab_off=lab_off, cw=cw,
-                             cw_off=cw_off, pk=pk, base=base)
+        self.pkv = pkv
         self.done = True
 
     def matches(self, Q):
@@ -419,32 +507,14 @@ def run(net, vb, compute_loss, early=None):
     # ------------------------------------------------------------------ stage 2: the term table
     sw_coef = float(cfg.Loss.sw)
     nb = len(blocks)
-    con_on = []
-    remap = None
-    text_seen = text
-    if use_clip:
-        hold = list(getattr(cfg, "holdout_classes", []) or [])
-        if hold:
-            n = text.shape[0]
-            key = (n, tuple(hold), text.data_ptr(), text._version)
-            if getattr(net, "_vloss_text_key", None) != key:
-                seen = [i for i in range(n) if i not in set(hold)]
-                rm = np.full(n, -1, dtype=np.int64)
-                rm[seen] = np.arange(len(seen))
-                net._vloss_text = (text[torch.tensor(seen, device=text.device)].contiguous(), rm)
-                net._vloss_text_key = key
-            text_seen, remap = net._vloss_text
-        else:
-            text_seen = text.contiguous()
-    y_con = []
-    for v in range(nvid):
-        if not use_clip:
-            con_on.append(False)
-            y_con.append(None)
-            continue
-        y = remap[labs[v]] if remap is not None else labs[v]
-        con_on.append(bool((y != -1).any()))
-        y_con.append(y)
+    if not early.prepared:
+        early.prepare(dev)
+    st2 = early.stage2
+    con_on, y_con, text_seen = st2["con_on"], st2["y_con"], st2["text_seen"]
+    pk2, tgt_off, tgt_arr, kcap = st2["pk2"], st2["tgt_off"], st2["tgt_arr"], st2["kcap"]
+    sw_arr, sw_list, ycon_off = st2["sw_arr"], st2["sw_list"], st2["ycon_off"]
+    if use_clip != st2["use_clip"]:
+        raise RuntimeError("vloss: the CLIP head ran differently from the prepared label tables")
 
     _stamp("con")
     # the predictions (no matching needed): own small table, launched before the wait
@@ -456,23 +526,6 @@ def run(net, vb, compute_loss, early=None):
                               nx.stream()), "fx_eval_pred")
 
     _stamp("eval_pred")
-    pk2 = _Pack()
-    # per video: token targets (Q) and the matched columns (capacity G[v] >= K), filled after matching
-    tgt_arr = [np.full(Q, C1 - 1, dtype=np.int32) for _ in range(nvid)]
-    tgt_off = [pk2.array(t, np.int32) for t in tgt_arr]
-    tgt_arr = [pk2.items[-nvid + v][1] for v in range(nvid)]     # the buffers pk2 sends
-    kcap = [max(int(G[v]), 1) for v in range(nvid)]
-    sw_arr, sw_list = [], []
-    for v in range(nvid):
-        arrs = []
-        offs = []
-        for dt in (np.int32, np.int32, np.int32, np.float32):
-            offs.append(pk2.array(np.zeros(kcap[v], dtype=dt), dt))
-            arrs.append(pk2.items[-1][1])
-        sw_arr.append(arrs)
-        sw_list.append(tuple(offs))
-    ycon_off = [pk2.array(y, np.int32) if y is not None and con_on[v] else None for v, y in enumerate(y_con)]
-
     _stamp("pk2_arrays")
     # every differentiated input of the term table, its gradient a view of ONE flat allocation
     inputs, gidx = [], {}
@@ -663,9 +716,9 @@ def run(net, vb, compute_loss, early=None):
     # read of a save entry, or at the next forward -- whichever comes first -- so loss.backward() is
     # issued while the device still finishes the forward instead of after a drain
     _stamp("side")
-    out_h = torch.empty(out.shape, dtype=torch.float32, pin_memory=True)
-    pred_h = torch.empty(pred.shape, dtype=torch.int32, pin_memory=True)
-    st_h = torch.empty(1, dtype=torch.int32, pin_memory=True)
+    out_h = _pinned("out", out.shape, torch.float32)
+    pred_h = _pinned("pred", pred.shape, torch.int32)
+    st_h = _pinned("status", (1,), torch.int32)
     out_h.copy_(out.detach(), non_blocking=True)
     pred_h.copy_(pred, non_blocking=True)
     st_h.copy_(fxf.device_status(dev)[:1], non_blocking=True)   # kernel-side failures (GRU timeout)

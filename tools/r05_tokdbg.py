@@ -10,7 +10,7 @@ from factmx.models import basic  # noqa: E402
 from factmx import functional as fxf  # noqa: E402
 
 DEV = "cuda"
-R, A, h, FF, Hm, L, T = 32, 256, 8, 512, 512, int(os.environ.get("NL", "6")), 1024
+R, A, h, FF, Hm, L, T = int(os.environ.get("R", "32")), 256, 8, 512, 512, int(os.environ.get("NL", "6")), 1024
 layer = basic.SCALayer(A, Hm, h, FF, dropout=0.0, attn_dropout=0.0)
 dec = basic.SCADecoder(A, A, 2 * A, layer, L, norm=torch.nn.LayerNorm(A), in_map=False)
 g = torch.Generator().manual_seed(1)

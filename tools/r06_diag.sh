@@ -23,4 +23,8 @@ if [ "${PROF:-1}" = "1" ]; then
   python tools/r06_trace_groups.py $(find $O/prof -name "*kernel_trace.csv") $O/prof.json $O/trace_kernels.json > $O/trace_groups.txt
   head -3 $O/step_map.txt
 fi
+if [ "${STAMPS:-0}" = "1" ]; then
+  timeout -k 10 300 python tools/r06_vloss_stamps.py > $O/vloss_stamps.txt 2>&1 || exit 5
+  timeout -k 10 300 python tools/r06_host_ops.py > $O/host_ops.txt 2>&1 || exit 6
+fi
 echo done
