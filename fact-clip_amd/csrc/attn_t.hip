@@ -916,7 +916,7 @@ TAttnGeom tattn_geom(int nvid, int Qv, int Tv, int hd, int nh, bool bwd) {
     return sizeof(float) * (q * g.Qp * (g.Hp + 4) + 2 * (size_t)Tc * (g.Hp + 4) + p * g.Qp * (Tc + 4) + 4 * 1024 +
                             2 * g.Qp + 4);
   };
-  int Tc = knobs().tattn_tc_max;   // FX_TATTN_TC (A/B): the largest chunk tried, default 256
+  int Tc = 256;   // the largest key chunk (smaller chunks, more workgroups per CU, measured slower: round 4)
   // (forward: at most 8 score tiles, two per wave, in registers)
   while (Tc > 32 && (lds_b(Tc) > 150 * 1024 || Tc * g.Hp > NVK * 4 * AT || Tc * g.Qp > 8 * 1024)) Tc >>= 1;
   constexpr int kMinWorkgroups = 256;   // one per CU

@@ -334,10 +334,8 @@ SideStream* side_stream() {
   auto it = pool.find(dev);
   if (it != pool.end()) return it->second;
   SideStream* ss = new SideStream();
-  // FX_SIDE_PRIORITY=low|normal|high: the side stream's queue priority (A/B diagnostic; default normal)
-  int prio = 0, least = 0, greatest = 0;
-  if (knobs().side_priority != 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
-    prio = knobs().side_priority < 0 ? least : greatest;
+  // normal priority (the side stream at low priority measured slower: round 3)
+  const int prio = 0;
   bool ok = hipStreamCreateWithPriority(&ss->s, hipStreamNonBlocking, prio) == hipSuccess;
   for (auto& e : ss->to_side) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
   for (auto& e : ss->layer_done) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
@@ -369,11 +367,9 @@ struct MstcnLayout {
 
 // Split of the deferred batched weight-gradient GEMMs (fx_mstcn_bwd): each workgroup of a batched
 // launch otherwise walks all K = rows and holds its CU for the whole launch, so the main stream's
-// next kernels wait for CUs; FX_DEFER_SPLIT=n caps a workgroup's share at K / n (A/B knob).
-int defer_split_impl(int rows) {
-  const int sp = knobs().defer_split;
-  return std::max(1, std::min(sp, rows / 512));
-}
+// next kernels wait for CUs; 16 caps a workgroup's share at K / 16 (16 vs 8: 15.78 vs 15.95 ms, median
+// of 6 pairs, round 3)
+int defer_split_impl(int rows) { return std::max(1, std::min(16, rows / 512)); }
 
 MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
   MstcnLayout L{};
@@ -556,42 +552,26 @@ const Knobs& knobs() {
     if (const char* p = env("FX_GEMM_PATH")) k.gemm_path = std::string(p) == "tiled" ? 1 : std::string(p) == "direct" ? 2 : 0;
     if (const char* p = env("FX_GEMM_W8")) k.gemm_w8 = p[0] == '1';
     if (const char* p = env("FX_GEMM_WIDE")) k.gemm_wide = p[0] == '1' ? 1 : 0;
-    if (const char* p = env("FX_GEMM_STAGGER")) k.gemm_stagger = p[0] == '1' ? 1 : 0;
     if (const char* p = env("FX_GEMM_XCDPLANES")) k.gemm_xcd_planes = p[0] != '0';
-    if (const char* p = env("FX_GEMM_NTSTORE")) k.gemm_nt_store = p[0] == '1';
-    if (const char* p = env("FX_GEMM_LOG")) k.gemm_log = std::fopen(p, "a");
     if (const char* p = env("FX_GEMM_GROUP")) k.gemm_group = p[0] != '0';
     if (const char* p = env("FX_GEMM_KTAIL")) k.gemm_ktail = p[0] != '0';
     if (const char* p = env("FX_DEC_TOK")) k.dec_tok = p[0] != '0';
     if (const char* p = env("FX_TOK_SPIN")) k.tok_spin = std::max(0, std::atoi(p));
     if (const char* p = env("FX_SIDE_STREAM")) k.side_stream = p[0] != '0';
-    if (const char* p = env("FX_SIDE_PRIORITY")) k.side_priority = std::string(p) == "low" ? -1 : std::string(p) == "high" ? 1 : 0;
-    if (const char* p = env("FX_DEFER_SPLIT")) k.defer_split = std::max(1, std::min(16, std::atoi(p)));
     if (const char* p = env("FX_MSTCN_DEFER")) k.mstcn_defer = p[0] != '0';
-    if (const char* p = env("FX_SIDE_MAXWG")) k.side_maxwg = std::max(0, std::atoi(p));
     if (const char* p = env("FX_GEMM_ROWPERM")) k.gemm_row_perm = p[0] != '0';
     if (const char* p = env("FX_GEMM_GROUPM")) k.gemm_group_m = p[0] != '0';
     if (const char* p = env("FX_GEMM_PERSIST")) k.gemm_persist = p[0] != '0';
     if (const char* p = env("FX_FRL_XCD")) k.frl_xcd = std::atoi(p);
     if (const char* p = env("FX_FRL_PAIR")) k.frl_pair = p[0] != '0';
-    if (const char* p = env("FX_FRL_PD")) k.frl_pd = std::atoi(p);
-    if (const char* p = env("FX_FRL_ABLATE")) k.frl_ablate = std::atoi(p);
     if (const char* p = env("FX_FRL_MIN_FILL")) k.frl_min_fill = std::atoi(p);
     if (const char* p = env("FX_AUX_STREAM")) k.aux_stream = p[0] != '0';
     if (const char* p = env("FX_GRU_POLL2")) k.gru_poll2 = p[0] != '0';
-    if (const char* p = env("FX_GRU_XCD")) k.gru_xcd = p[0] != '0';
-    if (const char* p = env("FX_GRU_BWD_GATE_WAVE")) k.gru_bwd_gate_wave = p[0] != '0';
     if (const char* p = env("FX_GRU_STORE_WAVE")) k.gru_store_wave = std::max(0, std::min(2, std::atoi(p)));
     if (const char* p = env("FX_TATTN_RR")) k.tattn_rr = p[0] != '0';
     if (const char* p = env("FX_X2Y_A2F_DW")) k.x2y_a2f_dw = p[0] != '0';
     if (const char* p = env("FX_TATTN_FOLD")) k.tattn_fold = p[0] != '0';
-    if (const char* p = env("FX_TATTN_TC")) k.tattn_tc_max = std::max(32, std::min(256, std::atoi(p)));
     if (const char* p = env("FX_X2Y_FUSED")) k.x2y_fused = p[0] != '0';
-    if (const char* p = env("FX_SPLIT_VARIANT")) k.split_variant = std::atoi(p);
-    if (const char* p = env("FX_MSTCN_TAIL")) k.mstcn_tail = p[0] != '0';
-    if (const char* p = env("FX_MSTCN_DW_HALVES")) k.mstcn_dw_halves = p[0] != '0';
-    if (const char* p = env("FX_MSTCN_TAIL_SPLIT")) k.mstcn_tail_split = std::atoi(p);
-    if (const char* p = env("FX_DIRECT_CPW")) k.direct_cpw = std::max(1, std::min(8, std::atoi(p)));
     if (const char* p = env("FX_X2Y_F2A_BWD")) k.x2y_f2a_bwd = std::atoi(p);
     if (const char* p = env("FX_X2Y_F2A_ONE")) k.x2y_f2a_one = p[0] != '0';
   });
@@ -764,15 +744,12 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   float* ws = workspace;
   FX_REQUIRE(p->dropout >= 0.f && p->dropout < 1.f, "mstcn: dropout must be in [0, 1)");
   const bool drop = p->dropout > 0.f;
-  // the input block's stack (in_map) is the LAST work of the backward pass: its batched deferred weight
-  // gradients run after the chain with nothing left to overlap (a ~0.7 ms side-stream tail that the
-  // end-of-backward join waits for).  FX_MSTCN_TAIL=1 gives that stack the per-layer schedule that
-  // overlaps the chain instead; measured even (the per-layer split-K GEMMs slow the chain by as much),
-  // so it is off by default
-  const bool tail = p->in_map && knobs().mstcn_tail;
   // deferred batched weight gradients (below); with training dropout the chain also keeps every layer's
-  // masked dB_i for the 1x1 weight gradient
-  const bool defer = !p->layernorm && NL > 0 && !tail && mstcn_defer_ok(p, g);
+  // masked dB_i for the 1x1 weight gradient.  (The input block's stack is the LAST work of the backward
+  // pass, so its batched dW runs after the chain with nothing left to overlap, a ~0.7 ms side-stream tail;
+  // giving it the per-layer schedule, or launching the upper layers' dW mid-chain, measured even: the
+  // overlapped GEMMs slow the chain by as much, rounds 3 and 5)
+  const bool defer = !p->layernorm && NL > 0 && mstcn_defer_ok(p, g);
   // Fused chain (no LayerNorm, <= 16 ragged videos, FX_MSTCN_FUSED=1; dropout on the deferred schedule): see below
   const bool fchain = p->fused_layers && !p->layernorm && (!drop || defer) && NL > 0 &&
                       frl_supported(F, ws + L.buf0, F, F) && (!q.off || q.nvid <= 16) &&
@@ -815,8 +792,6 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
   if (defer && L.rows_pad > rows)
     FX_CHECK_HIP(hipMemset2DAsync(ws + L.dzall + (long long)rows * F, L.rowsF * sizeof(float), 0,
                                   (L.rows_pad - rows) * F * sizeof(float), (drop ? 3 : 2) * NL, s));
-  // FX_SIDE_MAXWG=n: the side stream's split-K GEMMs keep within n workgroups (A/B diagnostic)
-  GridCap gcap(ss ? knobs().side_maxwg : 0);
   auto fork = [&](int e) -> int {   // side stream waits for the main stream's work so far
     if (!ss) return FX_OK;
     FX_CHECK_HIP(hipEventRecord(ss->to_side[e], s));
@@ -953,18 +928,6 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
       }
       return FX_OK;
     };
-    // FX_MSTCN_DW_HALVES=1: the layers above `half` get their weight gradients as soon as the chain has
-    // passed them (overlapping the chain's remaining layers), the rest after the chain.  Measured no
-    // better than one batched launch after the chain (the early half slows the chain it overlaps): off
-    // The input block's stack (in_map) is the last work of the backward pass: after its chain the side
-    // stream's batched dW runs alone on the device (~0.7 ms at T = 4096 x 2).  FX_MSTCN_TAIL_SPLIT=k has
-    // the fused chain launch the dW of the layers >= k as soon as it has passed them, overlapping its own
-    // remaining layers and the input map's dX (measured no faster: off by default)
-    int half = (knobs().mstcn_dw_halves && !fchain) ? NL / 2 : 0;
-    if (fchain && p->in_map && NL > 1) {
-      const int k = knobs().mstcn_tail_split;
-      half = k < 0 ? NL / 2 : std::min(k, NL - 1);
-    }
     if (fchain) {
       // the fused chain into the per-layer slots: dZ_NL-1 by the 1x1 backward GEMM, then per layer ONE
       // kernel for dH_i (-> dHall[i-1]) and dZ_i-1 (-> dZall[i-1]); the bottom layer's conv backward
@@ -982,7 +945,6 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
                           drop ? p->dropout : 0.f, fx_drop_subseed(p->seed, i - 1),
                           drop ? dBall + (i - 1) * L.rowsF : nullptr, F));
         // (dZ_j, dH_j+1 of every layer j >= i - 1 exist now)
-        if (half > 0 && i == half) FX_TRY(batched_dw(half, NL - half));
       }
       if (NL > 1)
         prof_end(7, s, (NL - 1) * 2.0 * rows * F * 4.0 * F, (NL - 1) * 4.0 * (4.0 * rows * F + 4.0 * F * F), NL - 1);
@@ -1007,10 +969,9 @@ int fx_mstcn_bwd(const fx_mstcn_params* p, const fx_mstcn_grads* g, const float*
       prof_begin(0, s);
       FX_TRY(launch_gemm(d, s));
       prof_end(0, s, 2.0 * rows * F * 3.0 * F, 4.0 * (3.0 * rows * F + 3.0 * F * F));
-      if (!fchain && half > 0 && i == half) FX_TRY(batched_dw(half, NL - half));
     }
     dH = (!p->in_map && dx) ? nullptr : Hb[0];   // (nullptr: already in dx)
-    FX_TRY(batched_dw(0, half > 0 ? half : NL));
+    FX_TRY(batched_dw(0, NL));   // every layer's weight gradients, after the chain
   }
   for (int i = NL - 1; !fchain && !defer && i >= 0; --i) {
     const int step = NL - 1 - i;

@@ -308,7 +308,6 @@ struct TokBuild {
     int G = 1;
     for (int i = 0; i < prog.nphase; ++i) G = std::max(G, items(prog.ph[i]));
     prog.G = std::min(G, 256);
-    if (const char* e = std::getenv("FX_TOK_G")) prog.G = std::max(1, std::min(prog.G, std::atoi(e)));   // diagnostic
     prog.status = reinterpret_cast<unsigned*>(status);
     prog.spin_max = tok_spin_max();
     FX_REQUIRE(status, "decoder: the persistent token kernel needs the caller's status word (fx_decoder_params.status)");

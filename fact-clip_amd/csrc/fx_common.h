@@ -60,14 +60,6 @@ struct WsBound {
   const float* prev_lo;
   const float* prev_hi;
 };
-// While alive, split-K launches planned on this thread keep tiles x split within `blocks` workgroups
-// (0: no cap) -- for the side stream's weight-gradient GEMMs, so that they leave CUs to the main
-// stream's latency-bound kernels instead of filling every CU's LDS.
-struct GridCap {
-  explicit GridCap(int blocks);
-  ~GridCap();
-  int prev;
-};
 // The library's side stream (one per device; FX_SIDE_STREAM=0: none).  side_fork: the side stream
 // (after making it wait for everything enqueued on s so far), or s itself when there is none;
 // side_join_into: s waits for everything enqueued on the side stream.
@@ -123,59 +115,40 @@ inline unsigned long long fx_drop_subseed(unsigned long long seed, int i) {
 int launch_dropout(const float* x, long long ldx, int rows, int cols, long long idx_ld, long long idx_col0, float p,
                    unsigned long long seed, float* y, long long ldy, hipStream_t s);
 
-// Diagnostic A/B switches (FX_GEMM_PATH, FX_GEMM_W8, FX_GEMM_WIDE, FX_GEMM_STAGGER, FX_GEMM_XCDPLANES,
-// FX_GEMM_NTSTORE, FX_GEMM_LOG, FX_GEMM_GROUP, FX_SIDE_STREAM, FX_SIDE_PRIORITY, FX_DEFER_SPLIT,
-// FX_MSTCN_DEFER, FX_SIDE_MAXWG): read from the environment ONCE, at the library's first use, into this
+// A/B switches of the default paths (FX_GEMM_PATH, FX_GEMM_W8, FX_GEMM_WIDE, FX_GEMM_XCDPLANES, FX_GEMM_GROUP,
+// FX_SIDE_STREAM, FX_MSTCN_DEFER, the fused-kernel switches below): read from the environment ONCE, at the
+// library's first use, into this
 // table (std::call_once); no entry point reads the environment itself.  Defaults are the tuned paths.
 struct Knobs {
   int gemm_path = 0;        // 1 tiled, 2 direct (0: the planner's choice)
   bool gemm_w8 = true;      // 8-wave 128x64 tiles
   int gemm_wide = -1;       // 0 / 1 force the 128x64 tiles off / on (-1: the planner's choice)
-  int gemm_stagger = 1;
   bool gemm_xcd_planes = true;
-  bool gemm_nt_store = false;
   bool gemm_persist = true;  // FX_GEMM_PERSIST=0: one workgroup per wide8 tile (A/B)
   bool gemm_group_m = true;  // FX_GEMM_GROUPM=0: no grouped tile order for large-B GEMMs (A/B)
   bool gemm_row_perm = true;  // FX_GEMM_ROWPERM=0: dilated-conv row tiles in plain order on the XCDs (A/B)
   bool frl_pair = true;        // FX_FRL_PAIR=0: the fused MS-TCN layer synchronises per 32-deep stage (A/B)
-  int frl_pd = 3;              // FX_FRL_PD=3|5: fused MS-TCN layer weight prefetch distance in stages (A/B)
-  int frl_ablate = 0;          // FX_FRL_ABLATE: diagnostic timing ablations of the fused layer (wrong results)
   int frl_min_fill = 80;        // FX_FRL_MIN_FILL: fused MS-TCN layer only when its row tiles cover this % of the CUs (shipped yaml, 219 tiles: 80 vs 100 -> 54.5-54.8 vs 55.1-55.2 ms)
   bool aux_stream = true;       // FX_AUX_STREAM=0: the decoder's query-position gradient on the caller's stream
   bool x2y_a2f_dw = true;        // FX_X2Y_A2F_DW=0: the a2f backward's dxv / dxk as grouped split-K GEMMs (A/B)
   bool tattn_fold = true;        // FX_TATTN_FOLD=0: the register-resident kernels' merge as a second launch (A/B)
   bool tattn_rr = true;          // FX_TATTN_RR=0: the LDS-staged attention-over-T kernels for head dim 32 too (A/B)
-  int tattn_tc_max = 256;       // FX_TATTN_TC: largest key chunk per attention-over-T workgroup (32..256, A/B)
-  bool gru_xcd = false;         // FX_GRU_XCD=1: a GRU direction's workgroups on one XCD (A/B: fwd 1.88-1.95 vs 1.86 us, bwd 2.27-2.28 vs 2.19-2.20 us per step spread; off)
   bool gru_poll2 = true;        // FX_GRU_POLL2=0: one granule poll in flight per lane (A/B)
   int gru_store_wave = 2;        // FX_GRU_STORE_WAVE: GRU forward table stores -- 0 by wave 0's gate threads, 1 staged for a fifth wave, 2 gate threads on the fifth wave (A/B)
-  bool gru_bwd_gate_wave = false; // FX_GRU_BWD_GATE_WAVE=1: the GRU backward's gate threads on a fifth wave (A/B: even, 2.25 vs 2.26 us per step)
   int frl_xcd = 2;             // FX_FRL_XCD: fused MS-TCN layer row tiles on the XCDs -- 0 round robin,
                               // 1 contiguous runs, 2 runs that follow the conv taps (A/B)
-  FILE* gemm_log = nullptr; // FX_GEMM_LOG=<file>: one line per GEMM launch (shape census)
   bool gemm_group = true;
   bool gemm_ktail = true;    // FX_GEMM_KTAIL=0: column-major operands with a K tail take the generic kernel (A/B)
   bool dec_tok = true;       // FX_DEC_TOK=0: the decoders' token rows as separate launches instead of the persistent
                              // token kernel (tokdec.hip) (A/B, and the fallback the tests compare with)
   int tok_spin = 0;          // FX_TOK_SPIN: grid-barrier polls before a token-kernel workgroup gives up (0: ~1 s)
   bool side_stream = true;
-  int side_priority = 0;    // -1 low, 0 normal, 1 high
-  int defer_split = 16;     // FX_DEFER_SPLIT: split-K of the deferred (side-stream) weight-gradient GEMMs (16 vs 8: 15.78 vs 15.95 ms median of 6 pairs)
   bool mstcn_defer = true;
-  int side_maxwg = 0;
   bool x2y_fused = true;    // FX_X2Y_FUSED=0: the X2Y attention core as grouped GEMM + softmax launches
   bool x2y_f2a_one = true;  // FX_X2Y_F2A_ONE=0: the fused f2a backward as two launches (dP pass, dlogit pass)
   int x2y_f2a_bwd = 2;      // FX_X2Y_F2A_BWD: the fused f2a backward core (one workgroup per 64-key chunk) 1 always,
                             // 0 never (grouped GEMMs), 2 when the call has >= 64 chunks: at 8192 frames 145 vs
                             // ~180 us for the grouped GEMMs; with a few hundred segments (3-4 chunks) 80 vs ~56 us
-  int split_variant = 0;    // FX_SPLIT_VARIANT=1: the LDS-image split kernel for every FX_PREC_F32S GEMM
-  int direct_cpw = 1;       // FX_DIRECT_CPW: 32-deep k chunks per wave of the direct (small) GEMM kernel (1 vs 2: direct-kernel time 2.74 -> 2.61 ms/step)
-  bool mstcn_dw_halves = false; // FX_MSTCN_DW_HALVES=1: upper half of the batched MS-TCN dW mid-chain (A/B: no gain)
-  bool mstcn_tail = false;  // FX_MSTCN_TAIL=1: the input block's MS-TCN keeps per-layer side dW (A/B: even)
-  int mstcn_tail_split = 0;  // FX_MSTCN_TAIL_SPLIT=k: the input block's fused chain launches the batched dW of
-                             // layers >= k once it has passed them (-1: NL / 2; 0: all after the chain).
-                             // A/B at T = 4096 x 2 (4 alternating rounds of 40 steps): k = 5 no faster, and
-                             // the overlapped dW slows the chain (fused-layer 0.525 -> 0.508): off
 };
 const Knobs& knobs();
 

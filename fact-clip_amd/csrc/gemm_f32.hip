@@ -71,7 +71,6 @@ struct GemmDev {
   int tiles_x, tiles_y;
   long long* stamps;
   unsigned* tile_cnt;   // split-K arrival counters (one per output tile), NULL -> separate reduce kernel
-  int w8_stagger;       // wide8: waves 4-7 run the staggered stage schedule
   unsigned drop_thr;    // dropout (fx_drop_bits >= drop_thr keeps); 0 = off
   float drop_scale;
   unsigned long long drop_seed;
@@ -84,7 +83,6 @@ struct GemmDev {
                         // gemm_f32_wide8_kernel)
   int a_dil_b1;         // > 0: A's conv dilation of batch 1 (two dilated convs of one input in one launch)
   long long bias_bs;    // bias of batch b at bias + b * bias_bs
-  int nt_store;         // FX_GEMM_NTSTORE=1 (A/B): the fast epilogue stores non-temporally
   int nsoff;            // > 0: the conv operand's videos are ragged: video v owns rows [soff[v], soff[v+1])
   int soff[kMaxSeq + 1];   // (COLS_CONVR: entries past nsoff are INT_MAX)
 };
@@ -832,12 +830,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmDev& g, int bidx, int rb
       if (g.relu == 2) v = fmaxf(v, 0.f);
       v += res[r];
       if (g.relu == 1) v = fmaxf(v, 0.f);
-      if (row < g.M) {
-        if (g.nt_store)
-          __builtin_nontemporal_store(v, cb + (long long)row * g.ldc);
-        else
-          cb[(long long)row * g.ldc] = v;
-      }
+      if (row < g.M) cb[(long long)row * g.ldc] = v;   // (non-temporal stores measured even: round 2)
     }
   } else {   // (a preloaded-C variant here costs the 128x64 kernel 416 B of scratch)
 #pragma unroll
@@ -1107,7 +1100,7 @@ __global__ __launch_bounds__(W8T) void gemm_f32_wide8_kernel(GemmDev g) {
     acc0[i] = 0.f;
     acc1[i] = 0.f;
   }
-  if (g.w8_stagger && wave >= 4)
+  if (wave >= 4)   // the second wave of each SIMD runs the staggered stage schedule
     wide8_kloop<AK, BKIND, 1, NP>(la0, la1, lb, lds, kt0, kt1, ai, wr, wn, li, lh, acc0, acc1);
   else
     wide8_kloop<AK, BKIND, 0, NP>(la0, la1, lb, lds, kt0, kt1, ai, wr, wn, li, lh, acc0, acc1);
@@ -1977,9 +1970,6 @@ unsigned* tile_counters(hipStream_t s) {
 
 unsigned* arrival_counters(hipStream_t s) { return tile_counters(s); }
 
-thread_local int t_max_blocks = 0;
-GridCap::GridCap(int blocks) : prev(t_max_blocks) { t_max_blocks = blocks; }
-GridCap::~GridCap() { t_max_blocks = prev; }
 
 thread_local const float* t_ws_lo = nullptr;
 thread_local const float* t_ws_hi = nullptr;
@@ -2119,7 +2109,6 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
   g.a_vec = operand_vec_ok(d.a);
   g.b_vec = operand_vec_ok(d.b);
   g.ws = d.workspace;
-  g.w8_stagger = knobs().gemm_stagger;
   int ak = kind_of(d.a, g.a_vec), bk = kind_of(d.b, g.b_vec);
   const bool direct = d.b_dil_growth <= 1 && d.a_dil_b1 <= 0 && use_direct(d, ak, bk);   // (the direct kernel: one dilation)
   // weight gradients over a frame count that is not a whole number of 64-deep stages (ragged batches):
@@ -2134,9 +2123,8 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
   if (direct) {
     const int nch = cdiv(d.K, DCH);
     const long long t32 = (long long)cdiv(d.M, 32) * cdiv(d.N, 32) * d.batch;
-    // k chunks per wave (FX_DIRECT_CPW, default 1: up to 8 waves per tile, one 32-deep chunk each; 2 = the
-    // double-buffered loop over two chunks per wave)
-    const int cpw = knobs().direct_cpw;
+    // one 32-deep k chunk per wave, up to 8 waves per tile (two chunks per wave measured slower: round 3)
+    const int cpw = 1;
     const int nw = std::min(DMAXW, std::max(1, nch / cpw));
     int split = 1;
     if (cap > 1) {
@@ -2157,12 +2145,6 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
     g.tiles_x = cdiv(d.N, BN);
     wide = use_wide(g, ak, bk, d.batch);
     g.tiles_y = cdiv(d.M, wide ? WBM : BM);
-    if (t_max_blocks > 0 && g.split > 1) {
-      const long long tiles = (long long)g.tiles_x * g.tiles_y * d.batch;
-      const int sp = (int)std::max<long long>(1, std::min<long long>(g.split, t_max_blocks / std::max(tiles, 1LL)));
-      g.kt_per_split = cdiv(nkt, sp);   // (the tile shape chosen above stays)
-      g.split = cdiv(nkt, g.kt_per_split);
-    }
     grid = dim3(g.tiles_x, g.tiles_y, d.batch * g.split);
     block = dim3(NTHREADS);
   }
@@ -2199,23 +2181,12 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
     const double b_bytes = 4.0 * d.N * d.K, a_run = 4.0 * gm * tm * d.K;
     if (b_bytes > 2.0 * (1 << 20) && a_run <= 2.0 * (1 << 20)) g.group_m = gm;
   }
-  g.nt_store = knobs().gemm_nt_store ? 1 : 0;
   g.persist = 0;
   P.grid = grid;
   P.block = block;
   P.direct = direct;
   P.wide = wide;
   return FX_OK;
-}
-
-// member: index inside a grouped launch (members > 0 share the kernel of member 0)
-void log_gemm(const fx_gemm_desc& d, const GemmPlan& P, int member = 0) {
-  // FX_GEMM_LOG=<file>: append one line per launch (diagnostic shape census, tools/gemm_census.py)
-  FILE* glog = knobs().gemm_log;
-  if (glog)
-    std::fprintf(glog, "%d %d %d %d %d %d %d %d %d %d %d %d %d %d\n", d.M, d.N, d.K, d.batch, P.ak, P.bk, P.g.split,
-                 d.a.conv_taps, d.b.conv_taps, d.relu, P.direct ? (int)P.block.x / 64 : (P.wide ? -1 : 0), member,
-                 P.g.a_vec + 2 * P.g.b_vec, d.K % BK == 0);
 }
 
 int launch_reduce(const fx_gemm_desc& d, const GemmPlan& P, hipStream_t s) {
@@ -2270,11 +2241,9 @@ int split_pieces_for(const GemmPlan& P, hipStream_t s) {
 
 template <int AK, int NP>
 int launch_split_b(const GemmPlan& P, hipStream_t s) {
-  const int variant = knobs().split_variant;   // 0: operands split in registers (B row-major), 1: LDS images
-  if (P.bk == ROWS && variant == 0)
+  // B row-major: the operands split in registers (wide8 kernel); B column-major: the LDS-image split kernel
+  if (P.bk == ROWS)
     fx_launch((gemm_f32_wide8_kernel<AK, ROWS, NP>), P.grid, dim3(W8T), 0, s, P.g);
-  else if (P.bk == ROWS)
-    fx_launch((gemm_split_wide8_kernel<AK, ROWS, NP>), P.grid, dim3(W8T), 0, s, P.g);
   else
     fx_launch((gemm_split_wide8_kernel<AK, COLS, NP>), P.grid, dim3(W8T), 0, s, P.g);
   return FX_OK;
@@ -2321,7 +2290,6 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
   if (d.M == 0 || d.N == 0) return FX_OK;
   GemmPlan P;
   FX_TRY(plan_gemm(d, s, P));
-  log_gemm(d, P);
   const int np = split_pieces_for(P, s);
   // FX_GEMM_PERSIST=0: one workgroup per tile (A/B).  A persistent grid for the f32 wide8 kernel on
   // single, unsplit products with at least two tiles per CU (the kernel loops over virtual workgroups)
@@ -2395,7 +2363,6 @@ int launch_gemm_group(const fx_gemm_desc* d, int n, hipStream_t s) {
     for (int i = i0; i < n; ++i) {
       if (done[i] || d[i].M == 0 || d[i].N == 0 || P[i].block.x != nw) continue;
       done[i] = true;
-      log_gemm(d[i], P[i], m);
       G.g[m] = P[i].g;
       const int ak = P[i].ak == ROWS_CAT ? ROWS_GEN : P[i].ak;
       G.kinds[m] = ak * 8 + P[i].bk;

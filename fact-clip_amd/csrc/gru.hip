@@ -134,27 +134,12 @@ struct GruArgs {
   unsigned spin_max;
   int poll2;            // two granule polls in flight (FX_GRU_POLL2, default on)
   int store_wave;       // 1: a fifth wave writes the per-step tables (FX_GRU_STORE_WAVE)
-  int xcd, ngroups;     // FX_GRU_XCD: a direction's NW workgroups on one XCD (see logical_block)
   int off[MAXSEQ + 1];
 };
 
-// The workgroup's logical index (sequence * 2 + direction) * NW + j.  With xcd set, the NW workgroups of
-// one (sequence, direction) group share blockIdx % 8, i.e. one XCD under the round-robin placement of
-// workgroups over the XCDs, so the per-step hand-offs stay between CUs of one XCD (a speed choice only:
-// the granule exchange is correct at any placement).  Group g's workgroup j is block
-// (g % 8) + 8 (NW (g / 8) + j); the grid is rounded up to whole groups of 8, the blocks past the last
-// group return at once (-1).
-__device__ __forceinline__ int logical_block(int xcd, int ngroups) {
-  const int b = (int)blockIdx.x;
-  if (!xcd) return b;
-  const int m = b >> 3;
-  const int g = (b & 7) + 8 * (m / NW);
-  return g < ngroups ? g * NW + m % NW : -1;
-}
-
 __global__ __launch_bounds__(GTF) void gru_fwd_kernel(GruArgs args) {
-  const int lb = logical_block(args.xcd, args.ngroups);
-  if (lb < 0) return;
+  // workgroup (sequence * 2 + direction) * NW + j
+  const int lb = (int)blockIdx.x;
   const int sq = lb / (2 * NW), rem = lb - sq * 2 * NW;
   const int dir = rem / NW, j = rem - dir * NW;
   const GruDirArgs& a = args.d[dir];
@@ -316,8 +301,6 @@ struct GruBwdArgs {
   unsigned* tmo;        // the caller's status word (fx_gru_bidir_*: FX_STATUS_GRU_TIMEOUT on a lost peer)
   unsigned spin_max;
   int poll2;
-  int gate_wave;
-  int xcd, ngroups;
   int off[MAXSEQ + 1];
 };
 
@@ -328,9 +311,8 @@ struct GruBwdArgs {
 // every workgroup and gathers NW x U = Hh of its own -- one granule per lane, the forward's exchange --
 // instead of gathering all 3Hh gate gradients (3 per lane).  Granule block of destination d, source j:
 // slot + (d * NW + j) * U.
-__global__ __launch_bounds__(GTF) void gru_bwd_kernel(GruBwdArgs args) {
-  const int lb = logical_block(args.xcd, args.ngroups);
-  if (lb < 0) return;
+__global__ __launch_bounds__(GT) void gru_bwd_kernel(GruBwdArgs args) {
+  const int lb = (int)blockIdx.x;
   const int sq = lb / (2 * NW), rem = lb - sq * 2 * NW;
   const int dir = rem / NW, j = rem - dir * NW;
   const GruBwdDirArgs& a = args.d[dir];
@@ -357,9 +339,9 @@ __global__ __launch_bounds__(GTF) void gru_bwd_kernel(GruBwdArgs args) {
   const int kd = kput ? k / U : 0, kl = kput ? k - kd * U : 0;   // owner workgroup of unit k, its index there
   if (tid < MAXU) dh[tid] = 0.f;
   // step s's saved gates, h_{t-1} and output gradient are loaded during step s-1
-  // gate threads: wave 0's lanes < U, or (args.gate_wave, FX_GRU_BWD_GATE_WAVE) a fifth wave's, so that the
-  // four polling waves issue no gate-gradient stores or table loads
-  const int gl = args.gate_wave ? (wv == 4 ? lane : GTF) : tid;
+  // gate threads: wave 0's lanes < U (a fifth wave holding them, as the forward's tables, measured even:
+  // 2.25 vs 2.26 us per recurrent step, round 5)
+  const int gl = tid;
   const bool own = gl < U && u0 + gl < Hh;
   const int uo = u0 + (own ? gl : 0);
   float nr = 0.f, nz = 0.f, nn = 0.f, ng = 0.f, nh = 0.f, nd = 0.f;
@@ -435,8 +417,9 @@ __global__ __launch_bounds__(GTF) void gru_bwd_kernel(GruBwdArgs args) {
 // floats of the per-call sync area for nseq sequences: timeout word (padded to 16 B) +
 // per sequence 2 dirs x 2 slots x max(3Hh, NW * NW * U) granules (8 B each: the forward uses Hh of them,
 // the backward NW x NW x U)
-// workgroups of a launch over nc sequences (2 nc groups of NW; with xcd rounded up to 8 groups)
-static int gru_grid(int xcd, int nc) { return xcd ? 8 * NW * ((2 * nc + 7) / 8) : 2 * nc * NW; }
+// workgroups of a launch over nc sequences: 2 nc groups of NW (placing a group on one XCD measured no gain,
+// round 5: its granules are agent-scope stores, which a same-XCD reader sees at the cross-XCD rate)
+static int gru_grid(int nc) { return 2 * nc * NW; }
 
 long long gru_sync_floats(int Hh, int nseq) {
   const long long U = (Hh + NW - 1) / NW;
@@ -460,8 +443,6 @@ int launch_gru_fwd(const float* gi, long long ldgi, int nseq, const int* seq_off
     args.spin_max = spin_max > 0 ? (unsigned)spin_max : SPIN_MAX;
     args.store_wave = knobs().gru_store_wave;
     args.poll2 = knobs().gru_poll2;
-    args.xcd = knobs().gru_xcd;
-    args.ngroups = 2 * nc;
     args.gran = gran + (long long)c0 * 2 * 2 * 3 * Hh;
     for (int q = 0; q <= nc; ++q) args.off[q] = seq_off[c0 + q];
     for (int d = 0; d < 2; ++d) {
@@ -477,7 +458,7 @@ int launch_gru_fwd(const float* gi, long long ldgi, int nseq, const int* seq_off
       a.Hh = Hh;
       a.reverse = d;
     }
-    fx_launch(gru_fwd_kernel, dim3(gru_grid(args.xcd, nc)), dim3(args.store_wave ? GTF : GT), 0, s, args);
+    fx_launch(gru_fwd_kernel, dim3(gru_grid(nc)), dim3(args.store_wave ? GTF : GT), 0, s, args);
     FX_CHECK_HIP(hipGetLastError());
   }
   return FX_OK;
@@ -498,10 +479,7 @@ int launch_gru_bwd(const float* dout, long long lddo, int nseq, const int* seq_o
     GruBwdArgs args{};
     args.tmo = status ? status : tmo;
     args.spin_max = spin_max > 0 ? (unsigned)spin_max : SPIN_MAX;
-    args.gate_wave = knobs().gru_bwd_gate_wave;
     args.poll2 = knobs().gru_poll2;
-    args.xcd = knobs().gru_xcd;
-    args.ngroups = 2 * nc;
     args.gran = gran + (long long)c0 * 2 * 2 * NW * NW * ((Hh + NW - 1) / NW);
     for (int q = 0; q <= nc; ++q) args.off[q] = seq_off[c0 + q];
     for (int d = 0; d < 2; ++d) {
@@ -517,7 +495,7 @@ int launch_gru_bwd(const float* dout, long long lddo, int nseq, const int* seq_o
       a.Hh = Hh;
       a.reverse = d;
     }
-    fx_launch(gru_bwd_kernel, dim3(gru_grid(args.xcd, nc)), dim3(args.gate_wave ? GTF : GT), 0, s, args);
+    fx_launch(gru_bwd_kernel, dim3(gru_grid(nc)), dim3(GT), 0, s, args);
     FX_CHECK_HIP(hipGetLastError());
   }
   return FX_OK;

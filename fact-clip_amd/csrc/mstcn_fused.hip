@@ -43,8 +43,8 @@ constexpr int AS = FBK + 4;      // LDS row stride of the activation stage image
 constexpr int VS = FN + 4;       // LDS row stride of the phase-1 tile
 constexpr int A_IMG = FR * AS;
 constexpr int NSL = 3;           // activation ring depth
-// weight fragments are loaded PD stages ahead of their use into NB = PD + 1 register sets (kernel
-// template parameter: 3 or 5, FX_FRL_PD)
+// weight fragments are loaded PD = 3 stages ahead of their use into NB = PD + 1 register sets (kernel
+// template parameter; 5 measured no faster)
 constexpr int LDS_FLOATS = NSL * A_IMG + FR * VS;
 constexpr int LDS_FLOATS_PAIR = 2 * NSL * A_IMG + FR * VS;
 constexpr int kMaxSeqF = 16;     // ragged videos per launch
@@ -53,8 +53,6 @@ struct FrlArgs {
   const float* x;      // phase-1 conv operand rows (M, FN), ld ldx
   long long ldx;
   int dil, dir, T, M;
-  int ablate;          // diagnostic (FX_FRL_ABLATE, wrong results): 1 no weight loads after the prologue,
-                       // 2 no activation loads after it, 4 no ring barriers, 8 no epilogue global traffic
   int xcd_runs;        // 1: consecutive row tiles share an XCD (and its L2), see frl_tile
   int row_perm;        // > 1: the conv taps shift by row_perm whole row tiles (dilation / FR)
   int nsoff;           // > 0: ragged videos, video v owns rows [soff[v], soff[v+1])
@@ -196,7 +194,6 @@ __global__ __launch_bounds__(FT) void frl_kernel(FrlArgs g) {
   float4 pa[2];                        // activation rows of stage st + 2 (set st & 1)
   bool pok[2];
   auto load_w = [&](int st) {
-    if ((g.ablate & 1) && st >= PD) return;
     if (st < n1) load_b(g.w1p, st, w, lane, pb[st % NB]);
     else if (st < nall) load_b(g.w2p, st - n1, w, lane, pb[st % NB]);
   };
@@ -257,10 +254,10 @@ __global__ __launch_bounds__(FT) void frl_kernel(FrlArgs g) {
       // pair p + 2 (loaded during the previous pair) into the slot pair p - 1 used (its fragments were
       // read during pair p - 2); fetch pair p + 3
       if (p + 2 < np) store_a(slot(p + 2) + half * A_IMG, pa[0], pok[0]);
-      if (p + 3 < np && !(g.ablate & 2)) load_a(2 * (p + 3) + half, pa[0], pok[0]);
+      if (p + 3 < np) load_a(2 * (p + 3) + half, pa[0], pok[0]);
       load_w(2 * p + 1 + PD);
       __builtin_amdgcn_sched_barrier(0);
-      if (!(g.ablate & 4)) __syncthreads();
+      __syncthreads();
     }
   } else {
     load_a(0, pa[0], pok[0]);
@@ -285,7 +282,7 @@ __global__ __launch_bounds__(FT) void frl_kernel(FrlArgs g) {
       float v = acc[q] + bv;
       if (g.relu1) v = fmaxf(v, 0.f);
       v += r1[q];
-      if (gr < g.M && !(g.ablate & 8)) g.out1[(long long)gr * g.ldo1 + col] = v;
+      if (gr < g.M) g.out1[(long long)gr * g.ldo1 + col] = v;
       if (g.vdrop_thr) {
         v = fx_drop_bits(g.vdrop_seed, (unsigned long long)gr * FN + col) >= g.vdrop_thr ? v * g.vdrop_scale : 0.f;
         if (g.out3 && gr < g.M) g.out3[(long long)gr * g.ldo3 + col] = v;
@@ -297,8 +294,8 @@ __global__ __launch_bounds__(FT) void frl_kernel(FrlArgs g) {
   auto load_res = [&]() {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      res[q] = (g.resid2 && !(g.ablate & 8)) ? g.resid2[(long long)erow(q) * g.ldr2 + ecol] : 0.f;
-      gat[q] = (g.gate2 && !(g.ablate & 8)) ? g.gate2[(long long)erow(q) * g.ldg2 + ecol] : 1.f;
+      res[q] = g.resid2 ? g.resid2[(long long)erow(q) * g.ldr2 + ecol] : 0.f;
+      gat[q] = g.gate2 ? g.gate2[(long long)erow(q) * g.ldg2 + ecol] : 1.f;
     }
   };
   load_res();
@@ -331,7 +328,7 @@ __global__ __launch_bounds__(FT) void frl_kernel(FrlArgs g) {
       v = fx_drop_bits(g.drop_seed, (unsigned long long)gr * FN + col) >= g.drop_thr ? v * g.drop_scale : 0.f;
     v += res[q];
     if (!(gat[q] > 0.f)) v = 0.f;
-    if (gr < g.M && (!(g.ablate & 8) || v == 12345.f)) g.out2[(long long)gr * g.ldo2 + col] = v;
+    if (gr < g.M) g.out2[(long long)gr * g.ldo2 + col] = v;
   }
 }
 
@@ -416,8 +413,6 @@ int launch_frl(const float* x, long long ldx, int M, int T, int dil, int dir, co
     return hipFuncSetAttribute((const void*)frl_kernel<false, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                LDS_FLOATS * (int)sizeof(float)) == hipSuccess &&
            hipFuncSetAttribute((const void*)frl_kernel<true, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               LDS_FLOATS_PAIR * (int)sizeof(float)) == hipSuccess &&
-           hipFuncSetAttribute((const void*)frl_kernel<true, 5>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                LDS_FLOATS_PAIR * (int)sizeof(float)) == hipSuccess;
   }();
   FX_REQUIRE(attr, "frl: cannot raise the LDS limit");
@@ -429,7 +424,6 @@ int launch_frl(const float* x, long long ldx, int M, int T, int dil, int dir, co
   a.T = T > 0 ? T : 1;
   a.M = M;
   const int nt = cdiv(M, FR), sh = dil / FR;
-  a.ablate = knobs().frl_ablate;
   a.xcd_runs = knobs().frl_xcd >= 1 && nt >= 16;
   a.row_perm = (knobs().frl_xcd >= 2 && dil % FR == 0 && sh > 1 && nt % sh == 0) ? sh : 1;
   a.nsoff = seq_off ? nseq : 0;
@@ -460,9 +454,7 @@ int launch_frl(const float* x, long long ldx, int M, int T, int dil, int dir, co
   a.ldo3 = ldo3;
   if (!knobs().frl_pair)
     fx_launch((frl_kernel<false, 3>), dim3(nt), dim3(FT), LDS_FLOATS * sizeof(float), s, a);
-  else if (knobs().frl_pd == 5)
-    fx_launch((frl_kernel<true, 5>), dim3(nt), dim3(FT), LDS_FLOATS_PAIR * sizeof(float), s, a);
-  else
+  else   // (weight prefetch 5 stages ahead instead of 3 measured no faster, round 6: 15.07 / 14.59 vs 14.85 / 14.53 ms)
     fx_launch((frl_kernel<true, 3>), dim3(nt), dim3(FT), LDS_FLOATS_PAIR * sizeof(float), s, a);
   FX_CHECK_HIP(hipGetLastError());
   return FX_OK;

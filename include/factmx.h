@@ -736,7 +736,7 @@ int fx_get_default_precision(void);
  *   between them).  fx_prof_collect_kernels: the same calls' kernels alone -- every kernel
  *   launched on the call's stream inside a bracket carries its own hipExtLaunchKernel event
  *   pair, i.e. its execution time as the rocprofv3 kernel trace reports it (untimed: kernels
- *   past the pool of 16 pairs per bracket).
+ *   past the pool of 4 pairs per bracket; the attention and X2Y kinds only).
  * ---------------------------------------------------------------------- */
 int fx_prof_enable(int kind, int max_events);
 int fx_prof_collect(int kind, double* total_ms, double* total_flops, double* total_bytes,

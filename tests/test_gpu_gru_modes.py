@@ -2,8 +2,7 @@
 
 The forward's gate threads may sit on wave 0 writing their own tables (FX_GRU_STORE_WAVE=0), stage their
 results for a fifth wave (1), or run on that fifth wave (2, the default); the granule gather may keep one
-or two polls in flight per lane (FX_GRU_POLL2); a direction's workgroups may share one XCD or spread over all
-(FX_GRU_XCD).  None of this changes an operation or its order, so the
+or two polls in flight per lane (FX_GRU_POLL2).  None of this changes an operation or its order, so the
 outputs and every gradient must agree BITWISE across the variants (and with the fp64 reference of the
 GRU within fp32 tolerance, which tests/test_gpu_kernels.py and test_gpu_long.py cover).  Library knobs
 are read once per process: each variant runs in a child process that writes its tensors to a file."""
@@ -23,9 +22,7 @@ pytestmark = pytest.mark.gpu
 
 VARIANTS = [{"FX_GRU_STORE_WAVE": "2", "FX_GRU_POLL2": "1"},
             {"FX_GRU_STORE_WAVE": "1", "FX_GRU_POLL2": "1"},
-            {"FX_GRU_STORE_WAVE": "0", "FX_GRU_POLL2": "0"},
-            {"FX_GRU_BWD_GATE_WAVE": "1"},
-            {"FX_GRU_XCD": "1"}]
+            {"FX_GRU_STORE_WAVE": "0", "FX_GRU_POLL2": "0"}]
 
 
 def _run(path):
