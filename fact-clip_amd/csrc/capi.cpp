@@ -1996,7 +1996,8 @@ static std::vector<int> seq_offsets(int S, int nseq, const int* seq_off) {
 int fx_gru_bidir_fwd(const float* x, long long ldx, int S, int nseq, const int* seq_off, int In, int Hh,
                      const float* w_ih_f, const float* w_hh_f, const float* b_ih_f, const float* b_hh_f,
                      const float* w_ih_r, const float* w_hh_r, const float* b_ih_r, const float* b_hh_r, float* out,
-                     long long ldo, float* saved, float* workspace, int32_t* status, int spin_max, void* stream) {
+                     long long ldo, int relu_out, float* saved, float* workspace, int32_t* status, int spin_max,
+                     void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int H3 = 3 * Hh;
   const std::vector<int> off = seq_offsets(S, nseq, seq_off);
@@ -2008,13 +2009,14 @@ int fx_gru_bidir_fwd(const float* x, long long ldx, int S, int nseq, const int* 
   FX_TRY(linear_fwd(x, ldx, S, In, w_ih_r, b_ih_r, gi + H3, 2 * H3, H3, 0, s));
   const float* whh[2] = {w_hh_f, w_hh_r};
   const float* bhh[2] = {b_hh_f, b_hh_r};
-  return launch_gru_fwd(gi, 2 * H3, nq, off.data(), Hh, whh, bhh, out, ldo, saved, workspace, (unsigned*)status,
-                        spin_max, s);
+  return launch_gru_fwd(gi, 2 * H3, nq, off.data(), Hh, whh, bhh, out, ldo, relu_out, saved, workspace,
+                        (unsigned*)status, spin_max, s);
 }
 
 int fx_gru_bidir_bwd(const float* x, long long ldx, int S, int nseq, const int* seq_off, int In, int Hh,
                      const float* w_ih_f, const float* w_hh_f, const float* w_ih_r, const float* w_hh_r,
-                     const float* saved, const float* dout, long long lddo, float* dx, long long lddx, float* dw_ih_f,
+                     const float* saved, const float* dout, long long lddo, const float* relu_y, long long ldy,
+                     float* dx, long long lddx, float* dw_ih_f,
                      float* dw_hh_f, float* db_ih_f, float* db_hh_f, float* dw_ih_r, float* dw_hh_r, float* db_ih_r,
                      float* db_hh_r, float* workspace, int32_t* status, int spin_max, void* stream) {
   hipStream_t s = (hipStream_t)stream;
@@ -2029,8 +2031,8 @@ int fx_gru_bidir_bwd(const float* x, long long ldx, int S, int nseq, const int* 
   WsBound wb(spl, gru_split_ws(S, In, Hh));
   float* sync_ws = csw + colsum_workspace_floats(S, 3 * Hh);
   const float* whh[2] = {w_hh_f, w_hh_r};
-  FX_TRY(launch_gru_bwd(dout, lddo, nq, off.data(), Hh, whh, saved, dgi, 2 * H3, dgh, sync_ws, (unsigned*)status,
-                        spin_max, s));
+  FX_TRY(launch_gru_bwd(dout, lddo, relu_y, ldy, nq, off.data(), Hh, whh, saved, dgi, 2 * H3, dgh, sync_ws,
+                        (unsigned*)status, spin_max, s));
   const float* wih[2] = {w_ih_f, w_ih_r};
   float* dwih[2] = {dw_ih_f, dw_ih_r};
   float* dwhh[2] = {dw_hh_f, dw_hh_r};

@@ -118,8 +118,9 @@ struct GruDirArgs {
   long long ldgi;
   const float* whh;    // (3Hh, Hh) natural layout [row][k]
   const float* bhh;    // (3Hh)
-  float* out;          // (S, ldo) h_t written at column offset
+  float* out;          // (S, ldo) h_t written at column offset (relu(h_t) with relu_out)
   long long ldo;
+  int relu_out;
   float* hprev;        // (S, Hh) h_{t-1} per step
   float* gates;        // (S, 4Hh): r, z, n, gh_n
   int Hh, reverse;
@@ -185,7 +186,7 @@ __global__ __launch_bounds__(GTF) void gru_fwd_kernel(GruArgs args) {
       const int t_ = r0 + (a.reverse ? S - 1 - s_ : s_);
       const float* st_ = &stage[s_ & 1][0][0];
       const int uu = u0 + u;
-      a.out[(long long)t_ * a.ldo + uu] = st_[0 * MAXU + u];
+      a.out[(long long)t_ * a.ldo + uu] = a.relu_out ? fmaxf(st_[0 * MAXU + u], 0.f) : st_[0 * MAXU + u];
       a.hprev[(long long)t_ * Hh + uu] = st_[1 * MAXU + u];
       float* gs = a.gates + (long long)t_ * 4 * Hh;
       gs[uu] = st_[2 * MAXU + u];
@@ -268,7 +269,7 @@ __global__ __launch_bounds__(GTF) void gru_fwd_kernel(GruArgs args) {
         st_[4 * MAXU + tid] = n;
         st_[5 * MAXU + tid] = ghn;
       } else {
-        a.out[(long long)t * a.ldo + u] = hn;
+        a.out[(long long)t * a.ldo + u] = a.relu_out ? fmaxf(hn, 0.f) : hn;
         a.hprev[(long long)t * Hh + u] = hp;
         float* gs = a.gates + (long long)t * 4 * Hh;
         gs[u] = r;
@@ -284,8 +285,10 @@ __global__ __launch_bounds__(GTF) void gru_fwd_kernel(GruArgs args) {
 }
 
 struct GruBwdDirArgs {
-  const float* dout;   // (S, lddo) gradient of h_t at column offset
+  const float* dout;   // (S, lddo) gradient of h_t at column offset (of relu(h_t) with relu_y)
   long long lddo;
+  const float* relu_y; // nullable: the forward's relu(h_t) output (ld ldy), the ReLU's backward gate
+  long long ldy;
   const float* whh;    // (3Hh, Hh) natural layout [row][k]
   const float* hprev;  // (S, Hh)
   const float* gates;  // (S, 4Hh)
@@ -353,6 +356,7 @@ __global__ __launch_bounds__(GT) void gru_bwd_kernel(GruBwdArgs args) {
     ng = gs[3 * Hh + uo];
     nh = a.hprev[(long long)t * Hh + uo];
     nd = a.dout[(long long)t * a.lddo + uo];
+    if (a.relu_y && !(a.relu_y[(long long)t * a.ldy + uo] > 0.f)) nd = 0.f;
   };
   if (own && S > 0) fetch(r0 + (a.reverse ? 0 : S - 1));
   if (tid < 3 * MAXU) dgo[tid] = 0.f;
@@ -428,8 +432,8 @@ long long gru_sync_floats(int Hh, int nseq) {
 }
 
 int launch_gru_fwd(const float* gi, long long ldgi, int nseq, const int* seq_off, int Hh, const float* const whh[2],
-                   const float* const bhh[2], float* out, long long ldo, float* saved, float* ws, unsigned* status,
-                   int spin_max, hipStream_t s) {
+                   const float* const bhh[2], float* out, long long ldo, int relu_out, float* saved, float* ws,
+                   unsigned* status, int spin_max, hipStream_t s) {
   FX_REQUIRE(Hh > 0 && Hh <= NW * MAXU, "gru: hidden size per direction must be <= 256");
   const int Stot = seq_off[nseq];
   if (Stot == 0) return FX_OK;
@@ -453,6 +457,7 @@ int launch_gru_fwd(const float* gi, long long ldgi, int nseq, const int* seq_off
       a.bhh = bhh[d];
       a.out = out + d * Hh;
       a.ldo = ldo;
+      a.relu_out = relu_out;
       a.hprev = saved + (long long)d * Stot * Hh;
       a.gates = saved + 2LL * Stot * Hh + (long long)d * Stot * 4 * Hh;
       a.Hh = Hh;
@@ -464,9 +469,9 @@ int launch_gru_fwd(const float* gi, long long ldgi, int nseq, const int* seq_off
   return FX_OK;
 }
 
-int launch_gru_bwd(const float* dout, long long lddo, int nseq, const int* seq_off, int Hh, const float* const whh[2],
-                   const float* saved, float* dgi, long long lddgi, float* dgh, float* sync_ws, unsigned* status,
-                   int spin_max, hipStream_t s) {
+int launch_gru_bwd(const float* dout, long long lddo, const float* relu_y, long long ldy, int nseq, const int* seq_off,
+                   int Hh, const float* const whh[2], const float* saved, float* dgi, long long lddgi, float* dgh,
+                   float* sync_ws, unsigned* status, int spin_max, hipStream_t s) {
   FX_REQUIRE(Hh > 0 && Hh <= NW * MAXU, "gru: hidden size per direction must be <= 256");
   const int Stot = seq_off[nseq];
   if (Stot == 0) return FX_OK;
@@ -486,6 +491,8 @@ int launch_gru_bwd(const float* dout, long long lddo, int nseq, const int* seq_o
       GruBwdDirArgs& a = args.d[d];
       a.dout = dout + d * Hh;
       a.lddo = lddo;
+      a.relu_y = relu_y ? relu_y + d * Hh : nullptr;
+      a.ldy = ldy;
       a.whh = whh[d];
       a.hprev = saved + (long long)d * Stot * Hh;
       a.gates = saved + 2LL * Stot * Hh + (long long)d * Stot * 4 * Hh;

@@ -55,12 +55,12 @@ int launch_seg_mean_bwd(const float* dy, long long lddy, const int32_t* sid, con
                         int T, int cols, float* dx, long long lddx, int accumulate, hipStream_t s);
 // nseq independent sequences stacked by rows: sequence q owns rows [seq_off[q], seq_off[q+1]) (host)
 int launch_gru_fwd(const float* gi, long long ldgi, int nseq, const int* seq_off, int Hh, const float* const whh[2],
-                   const float* const bhh[2], float* out, long long ldo, float* saved, float* ws, unsigned* status,
-                   int spin_max, hipStream_t s);
+                   const float* const bhh[2], float* out, long long ldo, int relu_out, float* saved, float* ws,
+                   unsigned* status, int spin_max, hipStream_t s);
 long long gru_sync_floats(int Hh, int nseq);
-int launch_gru_bwd(const float* dout, long long lddo, int nseq, const int* seq_off, int Hh, const float* const whh[2],
-                   const float* saved, float* dgi, long long lddgi, float* dgh, float* sync_ws, unsigned* status,
-                   int spin_max, hipStream_t s);
+int launch_gru_bwd(const float* dout, long long lddo, const float* relu_y, long long ldy, int nseq, const int* seq_off,
+                   int Hh, const float* const whh[2], const float* saved, float* dgi, long long lddgi, float* dgh,
+                   float* sync_ws, unsigned* status, int spin_max, hipStream_t s);
 
 // X2Y attention core with <= 64 keys per video (x2y_core.hip): logit, attn, feat in one launch;
 // yoff / xoff: (nvid + 1) host row offsets, aoff: attention block offsets (ny_v * nx_v row-major each)

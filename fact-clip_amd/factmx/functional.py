@@ -1082,10 +1082,12 @@ def check_device_status(dev=None):
 class GRUFn(torch.autograd.Function):
     """One bidirectional ``nn.GRU`` layer (blocks.py:401,432) on (S, In) rows -> (S, 2Hh).
     ``seq_off`` = None (one sequence) or the host prefix list of several sequences stacked by
-    rows (one per video), run concurrently by the kernel."""
+    rows (one per video), run concurrently by the kernel.  ``relu``: the output is relu(GRU(x)) (the
+    UpdateBlockTDU's torch.relu, blocks.py:432, written by the recurrence kernel, its backward gate applied
+    to dout by the backward kernel: no separate launch or autograd node either way)."""
 
     @staticmethod
-    def forward(ctx, x, seq_off, w_ih, w_hh, b_ih, b_hh, w_ih_r, w_hh_r, b_ih_r, b_hh_r):
+    def forward(ctx, x, seq_off, relu, w_ih, w_hh, b_ih, b_hh, w_ih_r, w_hh_r, b_ih_r, b_hh_r):
         lib = nx.load()
         S, In = x.shape
         Hh = w_hh.shape[1]
@@ -1097,16 +1099,18 @@ class GRUFn(torch.autograd.Function):
         ws = _ws(lib.fx_gru_workspace_floats(S, nq, In, Hh), dev)
         _check(lib.fx_gru_bidir_fwd(nx.ptr(x), nx.ld(x), S, nq, so, In, Hh, nx.ptr(w_ih), nx.ptr(w_hh), nx.ptr(b_ih),
                                     nx.ptr(b_hh), nx.ptr(w_ih_r), nx.ptr(w_hh_r), nx.ptr(b_ih_r), nx.ptr(b_hh_r),
-                                    nx.ptr(out), 2 * Hh, nx.ptr(saved), nx.ptr(ws), nx.ptr(device_status(dev)),
-                                    GRU_SPIN_MAX, nx.stream()), "fx_gru_bidir_fwd")
+                                    nx.ptr(out), 2 * Hh, int(bool(relu)), nx.ptr(saved), nx.ptr(ws),
+                                    nx.ptr(device_status(dev)), GRU_SPIN_MAX, nx.stream()), "fx_gru_bidir_fwd")
         ctx.seq_off = seq_off
-        ctx.save_for_backward(x, w_ih, w_hh, b_ih, b_hh, w_ih_r, w_hh_r, b_ih_r, b_hh_r, saved)
+        ctx.relu = bool(relu)
+        ctx.save_for_backward(x, w_ih, w_hh, b_ih, b_hh, w_ih_r, w_hh_r, b_ih_r, b_hh_r, saved,
+                              out if relu else None)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         lib = nx.load()
-        x, *w, saved = ctx.saved_tensors
+        x, *w, saved, y = ctx.saved_tensors
         w_ih, w_hh, _, _, w_ih_r, w_hh_r, _, _ = w
         dout = dout.contiguous()
         S, In = x.shape
@@ -1117,20 +1121,22 @@ class GRUFn(torch.autograd.Function):
         nq = 1 if seq_off is None else len(seq_off) - 1
         so = None if seq_off is None else nx.int_array(seq_off)
         dx = _empty(S, In, device=dev) if nd[0] else None
-        tg = [grad_target(p, nd[2 + i]) for i, p in enumerate(w)]
+        tg = [grad_target(p, nd[3 + i]) for i, p in enumerate(w)]
         bufs = [t[0] for t in tg]
         ws = _ws(lib.fx_gru_workspace_floats(S, nq, In, Hh), dev)
         _check(lib.fx_gru_bidir_bwd(nx.ptr(x), nx.ld(x), S, nq, so, In, Hh, nx.ptr(w_ih), nx.ptr(w_hh), nx.ptr(w_ih_r),
-                                    nx.ptr(w_hh_r), nx.ptr(saved), nx.ptr(dout), 2 * Hh, nx.ptr(dx), nx.ld(dx),
+                                    nx.ptr(w_hh_r), nx.ptr(saved), nx.ptr(dout), 2 * Hh, nx.ptr(y), 2 * Hh,
+                                    nx.ptr(dx), nx.ld(dx),
                                     *[nx.ptr(t) for t in bufs], nx.ptr(ws), nx.ptr(device_status(dev)), GRU_SPIN_MAX,
                                     nx.stream()), "fx_gru_bidir_bwd")
         _queue_backward_status(dev)
-        return (dx, None) + tuple(t[1] for t in tg)
+        return (dx, None, None) + tuple(t[1] for t in tg)
 
 
-def gru(mod, x, seq_off=None):
+def gru(mod, x, seq_off=None, relu=False):
     """Run an ``nn.GRU(bidirectional=True)`` module's parameters layer by layer through GRUFn; in
-    training, ``mod.dropout`` on every layer's output but the last (nn.GRU's inter-layer dropout)."""
+    training, ``mod.dropout`` on every layer's output but the last (nn.GRU's inter-layer dropout).
+    ``relu``: relu of the last layer's output, in the kernel (see GRUFn)."""
     assert mod.bidirectional and not mod.batch_first
     h = _2d(x)
     p_drop = float(mod.dropout) if (mod.training and mod.num_layers > 1) else 0.0
@@ -1139,7 +1145,7 @@ def gru(mod, x, seq_off=None):
             h = torch.nn.functional.dropout(h, p_drop, True)
         p = [getattr(mod, f"{n}_l{layer}{s}") for s in ("", "_reverse")
              for n in ("weight_ih", "weight_hh", "bias_ih", "bias_hh")]
-        h = GRUFn.apply(h, seq_off, *p)
+        h = GRUFn.apply(h, seq_off, relu and layer == mod.num_layers - 1, *p)
     return h
 
 

@@ -318,7 +318,7 @@ class UpdateBlockTDU(Block):
         f2 = fxf._2d(frame_feature)
         tdu = basic.TemporalDownsampleUpsample.from_probs(f2, f2.shape[1] - self.nclass, self.nclass)
         seg = tdu.feature_frame2seg(frame_feature)
-        seg = torch.relu(fxf.gru(self.seg_update, seg))
+        seg = fxf.gru(self.seg_update, seg, relu=True)      # relu(seg_update(seg)) (blocks.py:432)
         seg = fxf.linear(seg, self.seg_combine.weight, self.seg_combine.bias).unsqueeze(1)
         seg, seg_clogit = self.process_feature(seg, self.nclass)
         return tdu, seg, seg_clogit
@@ -361,7 +361,7 @@ class UpdateBlockTDU(Block):
             s_off.append(s_off[-1] + n_)
         tdus = [basic.TemporalDownsampleUpsample(*local[v]) for v in range(vb.nvid)]
         seg = fxf.SegMeanFn.apply(f2, gid, gst, gen)
-        seg = torch.relu(fxf.gru(self.seg_update, seg, seq_off=s_off))
+        seg = fxf.gru(self.seg_update, seg, seq_off=s_off, relu=True)     # relu folded into the kernel
         seg = fxf.linear(seg, self.seg_combine.weight, self.seg_combine.bias)
         seg_out, seg_cl = fxf.process_feature(seg, self.nclass)
         seg_pos = None

@@ -161,8 +161,9 @@ SIGNATURES = {
     "fx_dropout": (I, [P, L, I, I, L, L, F, U, P, L, P]),
     "fx_gru_saved_floats": (L, [I, I]),
     "fx_gru_workspace_floats": (L, [I, I, I, I]),
-    "fx_gru_bidir_fwd": (I, [P, L, I, I, P, I, I, P, P, P, P, P, P, P, P, P, L, P, P, P, I, P]),
-    "fx_gru_bidir_bwd": (I, [P, L, I, I, P, I, I, P, P, P, P, P, P, L, P, L, P, P, P, P, P, P, P, P, P, P, I, P]),
+    "fx_gru_bidir_fwd": (I, [P, L, I, I, P, I, I, P, P, P, P, P, P, P, P, P, L, I, P, P, P, I, P]),
+    "fx_gru_bidir_bwd": (I, [P, L, I, I, P, I, I, P, P, P, P, P, P, L, P, L, P, L, P, P, P, P, P, P, P, P, P, P, I,
+                             P]),
     "fx_segments_from_probs": (I, [P, L, I, I, I, I, P, P, P, P, P, P, P]),
     "fx_segments_globalize": (I, [I, I, P, P, P, P, P, P, P, P, P]),
     "fx_seg_mean_fwd": (I, [P, L, P, P, I, I, P, L, P]),

@@ -501,8 +501,11 @@ int fx_seg_sum_rows(const float* dx, long long lddx, const int32_t* seg_start, c
  *   nseq independent sequences stacked by rows (one per video): sequence q owns rows
  *   [seq_off[q], seq_off[q+1]) (host prefix array, NULL when nseq == 1); they run concurrently.
  *   saved (fx_gru_saved_floats): per-step h_{t-1} and gates for backward.
+ * relu_out != 0: out = relu([h_t fwd, h_t bwd]) (the ReLU UpdateBlockTDU applies to the GRU output,
+ *   blocks.py:432, written by the recurrence kernel; the state itself stays un-rectified).
  * bwd: dout (S, 2Hh) -> dx (nullable) and every weight/bias gradient
- *   (accumulated +=; each pointer nullable).
+ *   (accumulated +=; each pointer nullable); relu_y (nullable, ld ldy): the forward's rectified output,
+ *   dout then flows back through the ReLU first (dout where relu_y > 0, else 0).
  * The 2 x 16 workgroups of a sequence exchange the hidden state / gate gradients
  *   through L2 with bounded spins; a peer that does not arrive within spin_max polls
  *   (0: the default, ~1 s) ends the kernel early and sets *status = FX_STATUS_GRU_TIMEOUT
@@ -518,12 +521,12 @@ long long fx_gru_workspace_floats(int S, int nseq, int In, int Hh);
 int fx_gru_bidir_fwd(const float* x, long long ldx, int S, int nseq, const int* seq_off, int In,
                      int Hh, const float* w_ih_f, const float* w_hh_f, const float* b_ih_f,
                      const float* b_hh_f, const float* w_ih_r, const float* w_hh_r, const float* b_ih_r,
-                     const float* b_hh_r, float* out, long long ldo, float* saved, float* workspace,
-                     int32_t* status, int spin_max, void* stream);
+                     const float* b_hh_r, float* out, long long ldo, int relu_out, float* saved,
+                     float* workspace, int32_t* status, int spin_max, void* stream);
 int fx_gru_bidir_bwd(const float* x, long long ldx, int S, int nseq, const int* seq_off, int In,
                      int Hh, const float* w_ih_f, const float* w_hh_f, const float* w_ih_r,
                      const float* w_hh_r, const float* saved, const float* dout, long long lddo,
-                     float* dx, long long lddx, float* dw_ih_f, float* dw_hh_f, float* db_ih_f,
+                     const float* relu_y, long long ldy, float* dx, long long lddx, float* dw_ih_f, float* dw_hh_f, float* db_ih_f,
                      float* db_hh_f, float* dw_ih_r, float* dw_hh_r, float* db_ih_r, float* db_hh_r,
                      float* workspace, int32_t* status, int spin_max, void* stream);
 

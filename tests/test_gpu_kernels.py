@@ -160,19 +160,25 @@ def test_mha(Lq, Lk, E, nh):
         _close(p.grad, P[n].grad, rtol=1e-4, atol=1e-4, what=f"mha d{n}")
 
 
-@pytest.mark.parametrize("S,In,Hh", [(1, 512, 256), (40, 512, 256), (300, 64, 32), (7, 48, 24)])
-def test_gru_bidirectional(S, In, Hh):
+@pytest.mark.parametrize("S,In,Hh,relu", [(1, 512, 256, False), (40, 512, 256, False), (300, 64, 32, False),
+                                           (7, 48, 24, False), (40, 512, 256, True), (300, 64, 32, True)])
+def test_gru_bidirectional(S, In, Hh, relu):
+    """fxf.gru against the fp64 oracle; relu: the UpdateBlockTDU's relu(seg_update(x)) (blocks.py:432) folded
+    into the recurrence kernels (forward output and backward gate) against torch.relu of the oracle."""
     mod = torch.nn.GRU(In, Hh, 1, bidirectional=True).double()
     x = _r(S, In, seed=28)
     g = _r(S, 2 * Hh, seed=29)
     modd = torch.nn.GRU(In, Hh, 1, bidirectional=True).to(DEV)
     modd.load_state_dict({k: v.float() for k, v in mod.state_dict().items()})
     xd = x.float().to(DEV).requires_grad_(True)
-    y = fxf.gru(modd, xd)
+    y = fxf.gru(modd, xd, relu=relu)
     (y * g.float().to(DEV)).sum().backward()
     xr = x.clone().requires_grad_(True)
     P = dict(mod.named_parameters())
     yr = fo.gru(P, "", xr, 1)
+    if relu:
+        yr = torch.relu(yr)
+        assert (yr == 0).any() and (yr > 0).any()
     (yr * g).sum().backward()
     _close(y, yr, what="gru y")
     _close(xd.grad, xr.grad, rtol=1e-4, atol=1e-4, what="gru dx")
