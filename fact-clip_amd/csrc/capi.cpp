@@ -334,8 +334,14 @@ SideStream* side_stream() {
   auto it = pool.find(dev);
   if (it != pool.end()) return it->second;
   SideStream* ss = new SideStream();
-  // normal priority (the side stream at low priority measured slower: round 3)
-  const int prio = 0;
+  // normal priority (the side stream at low priority measured slower: round 3).  FX_SIDE_PRIO_BUILD (a
+  // diagnostic build define, -1 low / 1 high) builds the other priorities for A/B runs
+#ifndef FX_SIDE_PRIO_BUILD
+#define FX_SIDE_PRIO_BUILD 0
+#endif
+  int prio = 0, least = 0, greatest = 0;
+  if (FX_SIDE_PRIO_BUILD != 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+    prio = FX_SIDE_PRIO_BUILD < 0 ? least : greatest;
   bool ok = hipStreamCreateWithPriority(&ss->s, hipStreamNonBlocking, prio) == hipSuccess;
   for (auto& e : ss->to_side) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
   for (auto& e : ss->layer_done) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;

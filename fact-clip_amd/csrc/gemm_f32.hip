@@ -2303,6 +2303,11 @@ int launch_gemm(const fx_gemm_desc& d, hipStream_t s) {
     }
   }
   const GemmDev& g = P.g;
+#ifdef FX_GEMM_CENSUS
+  // diagnostic build only (tools/r06_gemm_census.sh): one line per GEMM kernel launch, in launch order
+  std::fprintf(stderr, "GEMM %p %d %d %d %d %d %d %d %d %d %d %d\n", (void*)s, d.M, d.N, d.K, d.batch, P.ak, P.bk,
+               P.g.split, P.direct ? 1 : P.wide ? 2 : 0, P.g.persist, d.a.conv_taps, (int)(P.g.split > 1 && !P.g.tile_cnt));
+#endif
   int st = np ? launch_split(P, np, s)
          : bf16_eligible(P, s) ? launch_bf16(P, s)
          : P.direct ? launch_direct(P.ak, P.bk, P.grid, P.block, s, g)
@@ -2372,6 +2377,10 @@ int launch_gemm_group(const fx_gemm_desc* d, int n, hipStream_t s) {
     for (int i = m + 1; i <= GMAX; ++i) G.start[i] = G.start[m];
     G.n = m;
     if (m == 1) {
+#ifdef FX_GEMM_CENSUS
+      std::fprintf(stderr, "GEMM %p %d %d %d %d %d %d %d 1 0 0 %d\n", (void*)s, d[i0].M, d[i0].N, d[i0].K, d[i0].batch,
+                   P[i0].ak, P[i0].bk, P[i0].g.split, (int)(P[i0].g.split > 1 && !P[i0].g.tile_cnt));
+#endif
       FX_TRY(P[i0].direct ? launch_direct(P[i0].ak, P[i0].bk, P[i0].grid, P[i0].block, s, P[i0].g) : FX_ERR_UNSUPPORTED);
     } else {
       fx_launch(gemm_direct_group_kernel, dim3(G.start[m]), dim3(nw), 0, s, G);

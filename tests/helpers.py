@@ -132,8 +132,9 @@ class GruKinks:
         self.gpu, self.ref = [], []
         g0, r0 = fxf.gru, fo.gru
 
-        def gpu(mod, x, seq_off=None):
-            y = g0(mod, x, seq_off=seq_off)
+        def gpu(mod, x, seq_off=None, relu=False):
+            # (relu(y) > 0 exactly where y > 0: the sign test below reads either)
+            y = g0(mod, x, seq_off=seq_off, relu=relu)
             self.gpu.append((y.detach(), seq_off))
             return y
 
