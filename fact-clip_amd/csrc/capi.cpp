@@ -375,7 +375,10 @@ struct MstcnLayout {
 // launch otherwise walks all K = rows and holds its CU for the whole launch, so the main stream's
 // next kernels wait for CUs; 16 caps a workgroup's share at K / 16 (16 vs 8: 15.78 vs 15.95 ms, median
 // of 6 pairs, round 3)
-int defer_split_impl(int rows) { return std::max(1, std::min(16, rows / 512)); }
+#ifndef FX_DEFER_SPLIT_BUILD
+#define FX_DEFER_SPLIT_BUILD 16   // (a diagnostic build define for A/B runs)
+#endif
+int defer_split_impl(int rows) { return std::max(1, std::min(FX_DEFER_SPLIT_BUILD, rows / 512)); }
 
 MstcnLayout mstcn_layout(const fx_mstcn_params* p, int rows) {
   MstcnLayout L{};

@@ -244,30 +244,47 @@ def resolve_pending():
 
 
 class _LossFn(torch.autograd.Function):
-    """out = fx_loss_terms_fwd(term table); backward writes every input's gradient whole."""
+    """(out, loss) = fx_loss_terms_fwd(term table): out = [batch loss, per video (loss, fact, contrastive,
+    per-block)], loss = out[0] as its own 0-dim output (the step's loss.backward() then enters this node
+    directly: no select node, whose backward would zero-fill an nout vector and copy the scalar into it);
+    backward writes every input's gradient whole."""
 
     @staticmethod
     def forward(ctx, plan, *inputs):
         lib = nx.load()
-        out = torch.empty(plan["nout"], device=inputs[0].device, dtype=torch.float32)
+        dev = inputs[0].device
+        out = torch.empty(plan["nout"], device=dev, dtype=torch.float32)
         nx.check(lib.fx_loss_terms_fwd(ctypes.addressof(plan["terms_host"]), plan["terms_dev"], plan["nterms"],
                                        plan["coef_dev"], plan["nout"], nx.ptr(out), nx.ptr(plan["ws"]), nx.stream()),
                  "fx_loss_terms_fwd")
+        loss = out[0].clone()
         ctx.plan = plan
-        return out
+        ctx.set_materialize_grads(False)
+        return out, loss
 
     @staticmethod
-    def backward(ctx, gout):
+    def backward(ctx, gout, gloss):
         plan = ctx.plan
         lib = nx.load()
-        gout = gout.contiguous()
+        nout = plan["nout"]
+        gflat, goff, shapes = plan["grads"]
+        if gout is None and gloss is None:
+            return (None,) + tuple(None for _ in shapes)
+        if gout is None:           # only the batch loss was differentiated: row 0 of the coefficients alone
+            gout, nout = gloss.reshape(1).contiguous(), 1
+        else:
+            gout = gout.contiguous()
+            if gloss is not None:
+                gout = gout.clone()
+                gout[0] += gloss
         nx.check(lib.fx_loss_terms_bwd(ctypes.addressof(plan["terms_host"]), plan["terms_dev"], plan["nterms"],
-                                       plan["coef_dev"], plan["nout"], nx.ptr(gout), nx.ptr(plan["ws"]), nx.stream()),
+                                       plan["coef_dev"], nout, nx.ptr(gout), nx.ptr(plan["ws"]), nx.stream()),
                  "fx_loss_terms_bwd")
         rb = plan.get("readback")
         if rb is not None and not rb.done:       # the step's read-back resolves when the backward pass ends
             torch.autograd.Variable._execution_engine.queue_callback(rb.resolve)
-        return (None,) + tuple(plan["grads"])
+        # every input's gradient: its slice of the flat buffer, laid out as the input (contiguous)
+        return (None,) + tuple(gflat.as_strided(shp, st, o) for o, (shp, st) in zip(goff, shapes))
 
 
 def _stage2_labels(net, labs, G):
@@ -325,6 +342,14 @@ def _stage2_labels(net, labs, G):
     ycon_off = [pk2.array(y, np.int32) if y is not None and con_on[v] else None for v, y in enumerate(y_con)]
     return dict(use_clip=use_clip, con_on=con_on, y_con=y_con, text_seen=text_seen, pk2=pk2, tgt_off=tgt_off,
                 tgt_arr=tgt_arr, kcap=kcap, sw_arr=sw_arr, sw_list=sw_list, ycon_off=ycon_off)
+
+
+def _contig_strides(shape):
+    st, acc = [], 1
+    for n in reversed(tuple(shape)):
+        st.append(acc)
+        acc *= int(n)
+    return tuple(reversed(st))
 
 
 _PINNED = {}
@@ -541,68 +566,113 @@ def run(net, vb, compute_loss, early=None):
                 want(bt[key])
     if any(con_on):
         want(proj)
-    sizes = [(t.numel() + 63) & ~63 for t in inputs]      # 256-byte aligned slices, as separate tensors
+    sizes = [(t.numel() + 63) & ~63 for t in inputs]      # 256-byte aligned slices
     gflat = torch.empty(sum(sizes), device=dev, dtype=torch.float32)
-    grads = [g[:t.numel()].view(t.shape) for g, t in zip(torch.split(gflat, sizes), inputs)]
+    goff, o_ = [], 0
+    for n_ in sizes:
+        goff.append(o_)
+        o_ += n_
+    gb = gflat.data_ptr()
+
+    class _G:       # an input's gradient slice by address only; the tensors are made in the backward
+        __slots__ = ("p",)
+
+        def __init__(self, p):
+            self.p = p
+
+        def data_ptr(self):
+            return self.p
 
     def grad_of(t):
-        return grads[gidx[id(t)]]
+        return _G(gb + 4 * goff[gidx[id(t)]])
 
-    specs = []       # (block index or -1 for InfoNCE, video, dict of LossTerm fields, scratch sizes)
+    # The term table in ONE pass straight into the ABI structs (their count is known from the block types:
+    # frame CE + token CE per block and video, + the segment CE for a TDU block, + the f2a / a2f cross-
+    # attention CE for an update block, + one InfoNCE term per video with a contrastive target); the
+    # pointers into the two packs resolve at once (both are allocated before the structs are filled)
+    nper = [2 if isinstance(blk, InputBlock) else 5 if isinstance(blk, UpdateBlockTDU) else 4 for blk in blocks]
+    nterms = nvid * sum(nper) + sum(1 for c in con_on if c)
+    per = 3 + nb
+    nout = 1 + nvid * per
+    coef_off = pk2.array(np.zeros((nout, nterms), dtype=np.float32), np.float32)
+    coef = pk2.items[-1][1].reshape(nout, nterms)          # (the buffer pk2 sends)
+    t_off, terms = pk2.structs(nx.LossTerm, nterms)
+    base2 = pk2.alloc(dev)
+    fw, cwt = float(getattr(cfg.CLIP, "fact_loss_weight", 1.0)), float(getattr(cfg.CLIP, "contrastive_weight", 0.0))
     tok_terms, attn_terms = [], []     # (term index, video): fields set after the matching
-    scratch = [0]
+    slots = []                         # scratch sizes (lse, lse2, colz) per term
+    # coefficient matrix: out = [batch loss, per video (loss, fact, contrastive, block values...)]
+    lw_blk = [fw / nb if con_on[v] else 1.0 / nb for v in range(nvid)]
+    nxt = [0]
 
-    def add(k, v, f, n_lse, n_lse2, n_colz):
-        offs = []
-        for n in (n_lse, n_lse2, n_colz):
-            offs.append(scratch[0])
-            scratch[0] += (max(n, 1) + 3) & ~3        # 16-byte aligned slots
-        specs.append((k, v, f, offs))
-        return len(specs) - 1
+    def term(k, v, kind, R, Cc, x, sr, sc, dx, dsr, dsc, c_ce, c_sm, n_lse, n_lse2, n_colz):
+        i = nxt[0]
+        nxt[0] = i + 1
+        t = terms[i]
+        t.slot, t.kind, t.R, t.C, t.x, t.sr, t.sc = i, kind, R, Cc, x, sr, sc
+        t.dx, t.dsr, t.dsc, t.c_ce, t.c_sm = dx, dsr, dsc, c_ce, c_sm
+        slots.append((n_lse, n_lse2, n_colz))
+        o = 1 + v * per
+        if k >= 0:
+            coef[o + 3 + k, i] = 1.0
+            coef[o + 1, i] = 1.0 / nb
+            lw = lw_blk[v]
+        else:
+            coef[o + 2, i] = 1.0
+            lw = cwt
+        coef[o, i] = lw
+        coef[0, i] = lw / nvid
+        return i, t
 
+    cw_p = base + cw_off
     for k, blk in enumerate(blocks):
         bt = blk._bt
         is_tdu = isinstance(blk, UpdateBlockTDU)
         f_cl, a_cl = bt["f_cl"], bt["a_cl"]
-        gf, ga = grad_of(f_cl), grad_of(a_cl)
+        pf, pa = f_cl.data_ptr(), a_cl.data_ptr()
+        gf, ga = grad_of(f_cl).data_ptr(), grad_of(a_cl).data_ptr()
         fce = 0.5 if is_tdu else 1.0
+        if not isinstance(blk, InputBlock):
+            f2a, a2f = bt["f2a_lg"], bt["a2f_lg"]
+            pfa, paf = f2a.data_ptr(), a2f.data_ptr()
+            gfa, gaf = grad_of(f2a).data_ptr(), grad_of(a2f).data_ptr()
+            if is_tdu:
+                seg_cl = bt["seg_cl"]
+                psg, gsg = seg_cl.data_ptr(), grad_of(seg_cl).data_ptr()
         for v in range(nvid):
             gs, ge, gl = gt_off[v]
             T = Ts[v]
             # frame CE (+ smooth) on the block's frame logits
-            add(k, v, dict(kind=nx.TERM_CLASS, R=T, C=C, x=_ptr_rows(f_cl, fo[v], C), sr=C, sc=1,
-                           dx=_ptr_rows(gf, fo[v], C), dsr=C, dsc=1, y=("p1", lab_off[v]), w=("p1", cw_off),
-                           c_ce=fce / T, c_sm=(sw_coef / ((T - 1) * C) if sw_coef and T > 1 else 0.0)), T, 0, 0)
+            _, t = term(k, v, nx.TERM_CLASS, T, C, pf + 4 * fo[v] * C, C, 1, gf + 4 * fo[v] * C, C, 1, fce / T,
+                        (sw_coef / ((T - 1) * C) if sw_coef and T > 1 else 0.0), T, 0, 0)
+            t.y, t.w = base + lab_off[v], cw_p
             # token CE (c_ce = 1 / the targets' class-weight sum, after the matching)
-            tok_terms.append((add(k, v, dict(kind=nx.TERM_CLASS, R=Q, C=C1, x=_ptr_rows(a_cl, v * Q, C1), sr=C1, sc=1,
-                                             dx=_ptr_rows(ga, v * Q, C1), dsr=C1, dsc=1, y=("p2", tgt_off[v]),
-                                             w=("p1", cw_off), c_ce=0.0, c_sm=0.0), Q, 0, 0), v))
+            i, t = term(k, v, nx.TERM_CLASS, Q, C1, pa + 4 * v * Q * C1, C1, 1, ga + 4 * v * Q * C1, C1, 1, 0.0, 0.0,
+                        Q, 0, 0)
+            t.y, t.w = base2 + tgt_off[v], cw_p
+            tok_terms.append((i, v))
             if isinstance(blk, InputBlock):
                 continue
             ka_o, kgs_o, kge_o, ksw_o = sw_list[v]
             Kc = kcap[v]
             if is_tdu:
                 Sv, s0 = bt["S"][v], bt["s_off"][v]
-                st, en = bt["local"][v][1], bt["local"][v][2]
-                seg_cl = bt["seg_cl"]
-                gsg = grad_of(seg_cl)
-                add(k, v, dict(kind=nx.TERM_CLASS, R=Sv, C=C, x=_ptr_rows(seg_cl, s0, C), sr=C, sc=1,
-                               dx=_ptr_rows(gsg, s0, C), dsr=C, dsc=1, rs=st.data_ptr(), re=en.data_ptr(),
-                               gs=("p1", gs), ge=("p1", ge), gl=("p1", gl), G=G[v], w=("p1", cw_off),
-                               c_ce=0.5 / Sv, c_sm=0.0), Sv, 0, 0)
-                R, off, ivs, c_xe, c_sm = Sv, Q * s0, (st.data_ptr(), en.data_ptr()), 1.0 / Sv, 0.0
+                rs, re = bt["local"][v][1].data_ptr(), bt["local"][v][2].data_ptr()
+                _, t = term(k, v, nx.TERM_CLASS, Sv, C, psg + 4 * s0 * C, C, 1, gsg + 4 * s0 * C, C, 1, 0.5 / Sv, 0.0,
+                            Sv, 0, 0)
+                t.rs, t.re, t.gs, t.ge, t.gl, t.G, t.w = rs, re, base + gs, base + ge, base + gl, G[v], cw_p
+                R, off, c_xe, c_sm = Sv, Q * s0, 1.0 / Sv, 0.0
             else:
-                R, off, ivs = T, Q * fo[v], (None, None)
+                rs = re = None
+                R, off = T, Q * fo[v]
                 c_xe, c_sm = 1.0 / T, (sw_coef / ((T - 1) * Q) if sw_coef and T > 1 else 0.0)
-            f2a, a2f = bt["f2a_lg"], bt["a2f_lg"]
-            gfa, gaf = grad_of(f2a), grad_of(a2f)
-            common = dict(kind=nx.TERM_ATTN, R=R, C=Q, rs=ivs[0], re=ivs[1], K=0, ka=("p2", ka_o),
-                          kgs=("p2", kgs_o), kge=("p2", kge_o), ksw=("p2", ksw_o), c_ce=c_xe, c_sm=c_sm)
             # f2a logits (Q, R) read as (R, Q): log_softmax over rows per matched column (dim=1)
-            attn_terms.append((add(k, v, dict(common, x=f2a.data_ptr() + 4 * off, sr=1, sc=R,
-                                              dx=gfa.data_ptr() + 4 * off, dsr=1, dsc=R, axis=0), R, R + Kc, Kc), v))
-            attn_terms.append((add(k, v, dict(common, x=a2f.data_ptr() + 4 * off, sr=Q, sc=1,
-                                              dx=gaf.data_ptr() + 4 * off, dsr=Q, dsc=1, axis=1), R, R + Kc, Kc), v))
+            for x, dx, sr, sc, axis in ((pfa, gfa, 1, R, 0), (paf, gaf, Q, 1, 1)):
+                i, t = term(k, v, nx.TERM_ATTN, R, Q, x + 4 * off, sr, sc, dx + 4 * off, sr, sc, c_xe, c_sm,
+                            R, R + Kc, Kc)
+                t.rs, t.re, t.axis = rs, re, axis
+                t.ka, t.kgs, t.kge, t.ksw = base2 + ka_o, base2 + kgs_o, base2 + kge_o, base2 + ksw_o
+                attn_terms.append((i, v))
     _stamp("specs")
     sims = None
     if any(con_on):
@@ -611,52 +681,35 @@ def run(net, vb, compute_loss, early=None):
         sims = torch.empty(2, fo[-1], Cs, device=dev)
         ncolz = ((Cs + 4) & ~3) + 4 * nx.LOSS_NB * Cs
         gp = grad_of(proj)
-        if not all(con_on):
-            gp.zero_()
+        if not all(con_on):     # (videos without a contrastive target leave their projection rows at zero)
+            i_ = gidx[id(proj)]
+            gflat.narrow(0, goff[i_], proj.numel()).zero_()
+        p0, p1, pe, pg = sims[0].data_ptr(), sims[1].data_ptr(), proj.data_ptr(), gp.data_ptr()
+        inv_temp = 1.0 / float(cfg.CLIP.temp)
         for v in range(nvid):
             if not con_on[v]:
                 continue
             T = Ts[v]
-            add(-1, v, dict(kind=nx.TERM_INFONCE, R=T, C=Cs, x=_ptr_rows(sims[0], fo[v], Cs), sr=Cs, sc=1,
-                            dx=_ptr_rows(sims[1], fo[v], Cs), dsr=Cs, dsc=1, y=("p2", ycon_off[v]),
-                            emb=_ptr_rows(proj, fo[v], Dc), ld_emb=Dc, text=text_seen.data_ptr(), D=Dc,
-                            inv_temp=1.0 / float(cfg.CLIP.temp), demb=_ptr_rows(gp, fo[v], Dc), ld_demb=Dc,
-                            c_ce=0.5), T, Cs, ncolz)
-
+            _, t = term(-1, v, nx.TERM_INFONCE, T, Cs, p0 + 4 * fo[v] * Cs, Cs, 1, p1 + 4 * fo[v] * Cs, Cs, 1, 0.5, 0.0,
+                        T, Cs, ncolz)
+            t.y, t.emb, t.ld_emb, t.text, t.D = base2 + ycon_off[v], pe + 4 * fo[v] * Dc, Dc, text_seen.data_ptr(), Dc
+            t.inv_temp, t.demb, t.ld_demb = inv_temp, pg + 4 * fo[v] * Dc, Dc
+    assert nxt[0] == nterms, (nxt[0], nterms)
     _stamp("infonce")
-    # coefficient matrix: out = [batch loss, per video (loss, fact, contrastive, block values...)]
-    nterms = len(specs)
-    per = 3 + nb
-    nout = 1 + nvid * per
-    coef = np.zeros((nout, nterms), dtype=np.float32)
-    fw, cwt = float(getattr(cfg.CLIP, "fact_loss_weight", 1.0)), float(getattr(cfg.CLIP, "contrastive_weight", 0.0))
-    for i, (k, v, _, _) in enumerate(specs):
-        o = 1 + v * per
-        if k >= 0:
-            coef[o + 3 + k, i] = 1.0
-            coef[o + 1, i] = 1.0 / nb
-            lw = fw / nb if con_on[v] else 1.0 / nb
-        else:
-            coef[o + 2, i] = 1.0
-            lw = cwt
-        coef[o, i] = lw
-        coef[0, i] = lw / nvid
-    coef_off = pk2.array(coef, np.float32)
     _stamp("coef")
-    t_off, terms = pk2.structs(nx.LossTerm, nterms)
-    base2 = pk2.alloc(dev)
-    scr = torch.empty(max(scratch[0], 1), device=dev, dtype=torch.float32)
+    # per-term scratch: lse, lse2, colz slots (16-byte aligned)
+    offs, sc_ = [], 0
+    for sz in slots:
+        o3 = []
+        for n in sz:
+            o3.append(sc_)
+            sc_ += (max(n, 1) + 3) & ~3
+        offs.append(o3)
+    scr = torch.empty(max(sc_, 1), device=dev, dtype=torch.float32)
     sbase = scr.data_ptr()
-    bases = {"p1": base, "p2": base2}
-    for i, (k, v, f, offs) in enumerate(specs):
+    for i, o3 in enumerate(offs):
         t = terms[i]
-        t.slot = i
-        for name, val in f.items():
-            if isinstance(val, tuple):
-                setattr(t, name, bases[val[0]] + val[1])
-            elif val is not None:
-                setattr(t, name, val)
-        t.lse, t.lse2, t.colz = (sbase + 4 * o for o in offs)
+        t.lse, t.lse2, t.colz = sbase + 4 * o3[0], sbase + 4 * o3[1], sbase + 4 * o3[2]
     _stamp("structs")
     ws = torch.empty(max(lib.fx_loss_terms_workspace_floats(nterms), 1), device=dev, dtype=torch.float32)
 
@@ -691,8 +744,9 @@ def run(net, vb, compute_loss, early=None):
     pk2.send()
     _stamp("send")
     plan = dict(terms_host=terms, terms_dev=base2 + t_off, nterms=nterms, coef_dev=base2 + coef_off, nout=nout,
-                ws=ws, grads=grads, keep=(early, pk2, pke, scr, sims, flog, text_seen))
-    out = _LossFn.apply(plan, *inputs)
+                ws=ws, grads=(gflat, goff, [(t.shape, _contig_strides(t.shape)) for t in inputs]),
+                keep=(early, pk2, pke, scr, sims, flog, text_seen))
+    out, loss = _LossFn.apply(plan, *inputs)
 
     _stamp("send_lossfn")
     # the reference's side channels: last video's per-block losses, fact / contrastive terms
@@ -743,4 +797,4 @@ def run(net, vb, compute_loss, early=None):
     plan["readback"] = pending
     if not LAZY_READBACK:
         pending.resolve()
-    return out[0], pending.saves
+    return loss, pending.saves
