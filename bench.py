@@ -719,8 +719,9 @@ def main():
         frl_roofline = fused_layer_roofline(frl_prof, F32_MFMA_PEAK_TFLOPS)
         if frl_roofline is not None:
             frl_roofline["traffic"] = traffic_from_profiles(FRL_KERNEL) if default_shape else None
-            frl_roofline["sample"] = (f"the fused-layer launches of the first timed step ({frl_roofline['launches']}), "
-                                      "one event pair per MS-TCN stack and direction")
+            frl_roofline["sample"] = (f"{frl_roofline['launches']} fused-layer launches from the start of the timed region "
+                                      "(one event pair per MS-TCN stack and direction; the pair capacity is one "
+                                      "step's launch count, so the pairs cover the first ~9 timed steps)")
         roofline = (frl_roofline if frl_roofline is not None and frl_prof.bracket_ms > conv_prof.bracket_ms
                     else conv_roofline)
         roofline_attention = {name: attention_roofline(f"tattn_{name}32_kernel (merge folded into the launch)", v)

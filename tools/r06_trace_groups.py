@@ -48,9 +48,14 @@ def main(trace, bench, out=None):
     ent = dict(line.get("roofline_attention") or {})
     ent["frl"] = line.get("roofline_fused_layer")
     for k, v in ent.items():
-        if v:
+        if not v:
+            continue
+        if "kernel_ms_per_call" in v:
             print(f"  {k:20s} kernel {1e3 * v['kernel_ms_per_call']:8.2f}  bracket {1e3 * v['bracket_ms_per_call']:8.2f}"
                   f"  kernels/call {v['kernels_per_call']:5.2f}  frac {v['frac']:.4f}  bytes/call {v.get('bytes_per_launch', 0):.4g}")
+        else:     # the fused MS-TCN layer: chain-bracket basis, trace cross-check
+            print(f"  {k:20s} bracket/launch {1e3 * v['avg_launch_ms']:8.2f}  trace/launch "
+                  f"{1e3 * (v.get('trace_avg_launch_ms') or 0):8.2f}  frac {v['frac']:.4f}  trace_frac {v.get('trace_frac')}")
 
 
 if __name__ == "__main__":
