@@ -136,9 +136,11 @@ def make_cfg_breakfast():
     return cfg
 
 
-def make_video(T, D, C, cfg, seed, nseg=10):
+def make_video(T, D, C, cfg, seed, nseg=10, data="seg10"):
     """seg10 synthetic video: 10 segments with sorted random cut points,
-    one randn(D) prototype per segment, labels seen[(7i+3) % |seen|]."""
+    one randn(D) prototype per segment, labels seen[(7i+3) % |seen|].  data="iid": the stress input of
+    the same section -- features ~ N(0, 1) i.i.d. (a fresh generator on the same seed), the same labels
+    (thousands of TDU segments per block: the BiGRU over segments dominates)."""
     g = torch.Generator().manual_seed(seed)
     hold = set(getattr(cfg, "holdout_classes", []) or [])
     seen = [c for c in range(C) if c not in hold]
@@ -150,6 +152,8 @@ def make_video(T, D, C, cfg, seed, nseg=10):
     for i in range(nseg):
         feats[bounds[i]:bounds[i + 1]] = protos[i]
         label[bounds[i]:bounds[i + 1]] = seen[(7 * i + 3) % len(seen)]
+    if data == "iid":
+        feats = torch.randn(T, D, generator=torch.Generator().manual_seed(seed))
     return feats.numpy(), label.numpy()
 
 
@@ -447,7 +451,7 @@ def gemm_roofline(name, pr, peak):
     return out
 
 
-def cpu_baseline(wl, Ts, videos_seeds, min_seconds=10.0, min_steps=2):
+def cpu_baseline(wl, Ts, videos_seeds, min_seconds=10.0, min_steps=2, data="seg10"):
     """The CPU oracle (fp32 PyTorch restatement pinned to the reference) timed on host cores: one
     video per step, full T, forward + prediction + loss + backward with FIXED weights (the same
     unit as the GPU step), repeated until >= min_seconds of CPU work (a bounded sample).  Also
@@ -460,7 +464,7 @@ def cpu_baseline(wl, Ts, videos_seeds, min_seconds=10.0, min_steps=2):
     spec = fo.resolve_spec(cfg, D, C, clip=clip)
     P = {n: p.detach().clone().float().requires_grad_(True) for n, p in net.named_parameters()}
     txt = text if clip else None
-    vids = [make_video(Tv, D, C, cfg, seed=s) for Tv, s in zip(Ts, videos_seeds)]
+    vids = [make_video(Tv, D, C, cfg, seed=s, data=data) for Tv, s in zip(Ts, videos_seeds)]
 
     def step(v=0):
         for p in P.values():
@@ -491,7 +495,7 @@ def cpu_baseline(wl, Ts, videos_seeds, min_seconds=10.0, min_steps=2):
     stoch = " (the oracle has no dropout / channel masking / time mask: those stay off in the CPU sample)" \
         if wl == "shipped" else ""
     return dict(value=round(frames / dt, 1), unit="frames/s", cores=torch.get_num_threads(), kind="port",
-                sample=f"{n} steps x 1 video (T={'/'.join(str(t) for t in sorted(set(Ts)))}, seg10, the bench videos "
+                sample=f"{n} steps x 1 video (T={'/'.join(str(t) for t in sorted(set(Ts)))}, {data}, the bench videos "
                        f"in turn) fwd+loss+bwd, fixed weights, oracle fp32 (1 untimed warm-up step, {dt:.1f} s "
                        f"timed){stoch}"), flops, S
 
@@ -532,6 +536,9 @@ def main():
                          "ntoken 75), ragged T=4096+2900")
     ap.add_argument("--videos", type=int, default=None, help="videos per rank per step (yaml batch_size)")
     ap.add_argument("--T", type=int, default=None)
+    ap.add_argument("--data", choices=["seg10", "iid"], default="seg10",
+                    help="seg10: the headline's synthetic videos; iid: the stress input (features i.i.d. N(0, 1), "
+                         "thousands of TDU segments, BiGRU-bound)")
     ap.add_argument("--adam-steps", type=int, default=None,
                     help="extra timed steps with clip_grad_norm_ + Adam after the fixed-weight steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -578,7 +585,7 @@ def main():
     Ts = video_lengths(args.config, T, nv)
     seqs, labels = [], []
     for s, Tv in zip(seeds, Ts):
-        f, l_ = make_video(Tv, D, C, cfg, seed=s)
+        f, l_ = make_video(Tv, D, C, cfg, seed=s, data=args.data)
         seqs.append(torch.from_numpy(f).to(dev))
         labels.append(torch.from_numpy(l_).to(dev))
 
@@ -698,7 +705,7 @@ def main():
         avg_ms = conv_prof.bracket_ms / max(conv_prof.calls, 1)
         flops_per_launch = conv_prof.flops / max(conv_prof.calls, 1)
         achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
-        default_shape = args.config == "havid" and T == T_DEFAULT and nv == 2
+        default_shape = args.config == "havid" and T == T_DEFAULT and nv == 2 and args.data == "seg10"
         split = headline_prec == "fp32s"
         # split arithmetic: the matrix cores' bound is the bf16 dense peak over the 6 piece products
         # (fp32 FLOPs counted once); f32 MFMA: the f32 matrix peak
@@ -752,10 +759,10 @@ def main():
                     scaling="weak", vs_baseline=None, dtype="fp32", data="synthetic",
                     gemm_arithmetic=PREC_NOTES[headline_prec][0],
                     config=dict(workload=(f"FACT_CLIP havid_view0_lh_pt_holdout.yaml as shipped (training mode: "
-                                          f"dropout 0.2, cmr 0.3, time mask, ntoken 75), seg10 synthetic, "
+                                          f"dropout 0.2, cmr 0.3, time mask, ntoken 75), {args.data} synthetic, "
                                           f"ragged T={'+'.join(map(str, Ts))}" if args.config == "shipped" else
-                                          f"FACT_CLIP HAViD-holdout dims, seg10 synthetic, T={T}" if clip else
-                                          f"FACT (vanilla) Breakfast dims, seg10 synthetic, T={T}"),
+                                          f"FACT_CLIP HAViD-holdout dims, {args.data} synthetic, T={T}" if clip else
+                                          f"FACT (vanilla) Breakfast dims, {args.data} synthetic, T={T}"),
                                 model="FACT_CLIP" if clip else "FACT", T=T, video_lengths=Ts, D=D,
                                 Nact=cfg.FACT.ntoken, C=C,
                                 videos_per_rank=nv, global_batch=world * nv, seq_len=T,
@@ -769,7 +776,7 @@ def main():
         if other is not None:
             line["fp32_f32mfma_mode" if headline_prec == "fp32s" else "fp32_split_mode"] = other
         if world == 1 and not args.no_cpu_baseline:
-            cb, step_flops, S_oracle = cpu_baseline(args.config, Ts, seeds)
+            cb, step_flops, S_oracle = cpu_baseline(args.config, Ts, seeds, data=args.data)
             line["cpu_baseline"] = cb
             line["tdu_segments_oracle"] = S_oracle
             # dropout / channel masking / time mask (shipped config) draw new masks every step: S is then

@@ -1924,7 +1924,15 @@ bool use_direct(const fx_gemm_desc& d, int ak, int bk) {
   // a shallow K that is not a whole number of 64-deep stages would take the generic tiled kernel
   // (InfoNCE dF: 4096 x 512 x 70, 80 us there; Breakfast's token dW over 4 x 60 = 240 token rows,
   // 512 x 513 x 240: 61 us there); one pass of the direct kernel per tile is ~10x faster
-  return d.M <= lim || d.N <= lim || d.K <= 64 || (d.K <= 512 && d.K % 64 != 0);
+  if (d.M <= lim || d.N <= lim || d.K <= 64 || (d.K <= 512 && d.K % 64 != 0)) return true;
+  // few output tiles (the TDU blocks' segment-level products: S ~ 50-250 segment rows per launch): the
+  // tiled kernel's fixed cost -- a 64-deep stage pipeline filled per block, one 64 x 64 block per ~4 tiles
+  // of 32 x 32 -- is most of its time there; the direct kernel runs every 32 x 32 tile's K chunks on
+  // their own waves.  Measured (tools/r06_seg_gemm.py, SWEEP=1): 192 x 512 x 512 7.9 vs 16.0 us (tiled,
+  // 12.8 with split 4), 1024 x 256 x 512 7.9 vs 16.1, 1024 x 512 x 512 14.0 vs 16.4, 192 x 512 x 2048
+  // 19.5 vs 20.2 (split 4); past ~512 tiles the tiled kernel wins (1536 x 512 x 512: 20.1 vs 16.7)
+  const long long t32 = (long long)cdiv(d.M, 32) * cdiv(d.N, 32) * d.batch;
+  return (ak == ROWS || ak == COLS) && t32 <= 512 && d.K <= 2048;
 }
 
 // 128x64 tiles where the launch still has ~3/4 of a block per CU: FAST operands only.
@@ -2127,7 +2135,9 @@ int plan_gemm(const fx_gemm_desc& d, hipStream_t s, GemmPlan& P, long long tile_
     const int cpw = 1;
     const int nw = std::min(DMAXW, std::max(1, nch / cpw));
     int split = 1;
-    if (cap > 1) {
+    // split K only for launches of few tiles (the token rows): from 64 tiles up the extra slabs and the
+    // last arriver's reduction cost more than they spread (102 x 512 x 512: 7.8 us unsplit, 9.7 in 4)
+    if (cap > 1 && t32 < 64) {
       const long long want = std::min<long long>(nch / (cpw * nw), cdiv(2048, t32 * nw));
       split = (int)std::max<long long>(1, std::min<long long>(cap, want));
     }
