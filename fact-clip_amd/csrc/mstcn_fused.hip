@@ -82,6 +82,20 @@ struct FrlArgs {
   long long ldo3;
 };
 
+// Diagnostic builds only (-DFRL_STAMPS, tools/frl_stamps.py): s_memrealtime stamps of thread 0 of every
+// workgroup at 8 points of the last launch (fx_debug_frl_stamps); never in the shipped library
+#ifdef FRL_STAMPS
+__device__ unsigned long long g_frl_st[1024 * 8];
+#define FRL_ST(k)                                                                                                  \
+  do {                                                                                                             \
+    if (threadIdx.x == 0 && blockIdx.x < 1024) g_frl_st[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define FRL_ST(k) \
+  do {            \
+  } while (0)
+#endif
+
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
@@ -151,6 +165,7 @@ __global__ __launch_bounds__(FT) void frl_kernel(FrlArgs g) {
   extern __shared__ float lds[];
   float* V = lds + (PAIR ? 2 : 1) * NSL * A_IMG;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 31, lh = lane >> 5;
+  FRL_ST(0);
   const int m0 = frl_tile(g) * FR;
   constexpr int n1 = 3 * FN / FBK, n2 = FN / FBK, nall = n1 + n2;
   static_assert(n1 % 2 == 0, "stage pairs");
@@ -229,7 +244,9 @@ __global__ __launch_bounds__(FT) void frl_kernel(FrlArgs g) {
     store_a(slot(0) + half * A_IMG, pa[0], pok[0]);
     store_a(slot(1) + half * A_IMG, pa[1], pok[1]);
     load_a(4 + half, pa[0], pok[0]);
+    FRL_ST(1);
     __syncthreads();
+    FRL_ST(2);
     // A fragments of pair p are read from LDS one pair ahead (during pair p - 1's MFMAs): slot p % NSL
     // was written before the barrier that ended pair p - 2, so the read needs no extra barrier, and
     // after each barrier the MFMAs start on fragments already in registers
@@ -271,6 +288,7 @@ __global__ __launch_bounds__(FT) void frl_kernel(FrlArgs g) {
     for (int st = 0; st < n1; ++st) step(st, nullptr, 0);
   }
   if (!PAIR) load_r1();
+  FRL_ST(3);
   // ---------------- phase-1 epilogue: out1 and the LDS tile V
   {
     const int col = ecol;
@@ -299,7 +317,9 @@ __global__ __launch_bounds__(FT) void frl_kernel(FrlArgs g) {
     }
   };
   load_res();
+  FRL_ST(4);
   __syncthreads();
+  FRL_ST(5);
   // ---------------- phase 2: 1x1 GEMM from the LDS tile, K = FN
   if constexpr (PAIR) {
     float4 fv[2][4];      // V fragments one stage ahead
@@ -317,6 +337,7 @@ __global__ __launch_bounds__(FT) void frl_kernel(FrlArgs g) {
 #pragma unroll
     for (int j = 0; j < n2; ++j) step(n1 + j, V + j * FBK, VS);
   }
+  FRL_ST(6);
   // ---------------- phase-2 epilogue
   const int col = ecol;
   const float bv = g.bias2 ? g.bias2[col] : 0.f;
@@ -330,6 +351,7 @@ __global__ __launch_bounds__(FT) void frl_kernel(FrlArgs g) {
     if (!(gat[q] > 0.f)) v = 0.f;
     if (gr < g.M) g.out2[(long long)gr * g.ldo2 + col] = v;
   }
+  FRL_ST(7);
 }
 
 // Weight matrices [FN][K] (row-major, leading dim ld) -> MFMA fragment order for frl_kernel:
@@ -353,6 +375,12 @@ __global__ __launch_bounds__(256) void pack_frag_kernel(PackFragArgs a) {
 }
 
 }  // namespace
+
+#ifdef FRL_STAMPS
+extern "C" int fx_debug_frl_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_frl_st), sizeof(g_frl_st)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 bool frl_fills_device(long long rows) {
   static std::mutex mu;
