@@ -558,17 +558,40 @@ __global__ __launch_bounds__(AT) void tattn_bwd_kernel(TAttnArgs a) {
 // operand; dV = P_d^T dO and dK = scale dS^T q need the probabilities with the key as the ROW index, so
 // P_d^T and dS^T go through a wave-private LDS tile (no workgroup barrier).
 __device__ __forceinline__ float4 ld4g(const float* p) { return *reinterpret_cast<const float4*>(p); }
+// Diagnostic builds only (-DTATTN_STAMPS, tools/tattn_stamps.py): s_memrealtime stamps of thread 0 of every
+// workgroup of the last tattn_fwd32_kernel launch (fx_debug_tattn_stamps); never in the shipped library
+#ifdef TATTN_STAMPS
+__device__ unsigned long long g_ta_st[1024 * 8];
+#define TA_ST(k)                                                                                        \
+  do {                                                                                                  \
+    const int b_ = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);                      \
+    if (threadIdx.x == 0 && b_ < 1024) g_ta_st[b_ * 8 + (k)] = __builtin_amdgcn_s_memrealtime();        \
+  } while (0)
+#else
+#define TA_ST(k) \
+  do {           \
+  } while (0)
+#endif
 
 // write-through (sc1) accesses of the in-launch merge: L1 bypassed, stores written through (the b32
 // buffer forms move the float's bits)
+typedef float v4f __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
 }
 __device__ __forceinline__ float ldc1(const float* base, long long idx) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc(base), (int)(idx * 4), 0, 16));
 }
+__device__ __forceinline__ float4 ldc4(const float* base, long long idx) {
+  const v4f v = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base), (int)(idx * 4), 0, 16);
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
 __device__ __forceinline__ void stc1(float* base, long long idx, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc(base), (int)(idx * 4), 0, 16);
+}
+__device__ __forceinline__ void stc4(float* base, long long idx, float4 v) {
+  v4f x = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(x, rsrc(base), (int)(idx * 4), 0, 16);
 }
 constexpr int FOLD_MAX = 16;   // chunks per video merged inside the launch (more: tattn_merge_kernel)
 
@@ -583,6 +606,7 @@ __device__ __forceinline__ void fold_merge(const TAttnArgs& a, int vid, int h, i
   const int tid = threadIdx.x;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's partial stores acknowledged
   __syncthreads();
+  if (stats) TA_ST(4);
   if (tid == 0) {
     unsigned* c = a.cnt + (long long)vid * a.nh + h;
     const unsigned prev = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -590,20 +614,19 @@ __device__ __forceinline__ void fold_merge(const TAttnArgs& a, int vid, int h, i
     if (*last) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
+  if (stats) TA_ST(5);
   if (!*last) return;
   const long long pbase = ((long long)vid * a.nh + h) * a.nsplit;
   const float* part = a.ws;
   const float* pm = a.ws + (long long)gridDim.z * a.nh * a.nsplit * 32 * 32;
   const float* pl = pm + (long long)gridDim.z * a.nh * a.nsplit * 32;
-  // every load of the merge at once: this thread's 4 (query, d) elements of every partial, and (forward)
-  // the row statistics of (partial, query) pairs tid, tid + 256
-  float x[4][FOLD_MAX];
+  // every load of the merge at once: this thread's (query, 4 consecutive d) slice of every partial as one
+  // 16-B load each (query tid / 8, d 4 (tid % 8) ..), and (forward) the row statistics of (partial, query)
+  // pairs tid, tid + 256
+  const int mq = tid >> 3, md = (tid & 7) * 4;
+  float4 x[FOLD_MAX];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int e = tid + i * AT;
-#pragma unroll
-    for (int sp = 0; sp < FOLD_MAX; ++sp) x[i][sp] = ldc1(part, (pbase + min(sp, ns - 1)) * 1024 + e);
-  }
+  for (int sp = 0; sp < FOLD_MAX; ++sp) x[sp] = ldc4(part, (pbase + min(sp, ns - 1)) * 1024 + mq * 32 + md);
   if (stats) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -626,15 +649,24 @@ __device__ __forceinline__ void fold_merge(const TAttnArgs& a, int vid, int h, i
     }
     __syncthreads();
   }
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int e = tid + i * AT, q = e >> 5, d = e & 31;
-    float acc = 0.f;
-#pragma unroll
-    for (int sp = 0; sp < FOLD_MAX; ++sp)
-      if (sp < ns) acc += (stats ? wm[sp][q] : 1.f) * x[i][sp];
-    if (q < a.Qv) a.out[(qrow + q) * a.ld_out + h * 32 + d] = acc * mul;
+  for (int sp = 0; sp < FOLD_MAX; ++sp)
+    if (sp < ns) {
+      const float wgt = stats ? wm[sp][mq] : 1.f;
+      acc.x += wgt * x[sp].x;
+      acc.y += wgt * x[sp].y;
+      acc.z += wgt * x[sp].z;
+      acc.w += wgt * x[sp].w;
+    }
+  if (mq < a.Qv) {
+    float* o = a.out + (qrow + mq) * a.ld_out + h * 32 + md;
+    o[0] = acc.x * mul;
+    o[1] = acc.y * mul;
+    o[2] = acc.z * mul;
+    o[3] = acc.w * mul;
   }
+  if (stats) TA_ST(6);
 }
 
 template <int KT>
@@ -643,6 +675,7 @@ __global__ __launch_bounds__(AT) void tattn_fwd32_kernel(TAttnArgs a) {
   __shared__ float xm[4][32], xl[4][32];
   const int c = blockIdx.x, h = blockIdx.y, vid = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 31, lh = lane >> 5;
+  TA_ST(0);
   const int Tv = a.koff[vid + 1] - a.koff[vid];
   const int t0 = c * a.Tc, nk = min(a.Tc, Tv - t0);
   if (nk <= 0) return;
@@ -655,11 +688,16 @@ __global__ __launch_bounds__(AT) void tattn_fwd32_kernel(TAttnArgs a) {
     const float* qp = a.q + (qrow + min(li, a.Qv - 1)) * a.ldq + h * 32 + 16 * lh;
 #pragma unroll
     for (int q = 0; q < 4; ++q) qf[q] = ld4g(qp + 4 * q);
+    // (every K fragment before the first V column: loads complete in issue order, so S = q K^T then waits
+    // for K alone and the V columns arrive behind its MFMAs)
 #pragma unroll
     for (int u = 0; u < KT; ++u) {
       const float* kp = a.k + (krow + min(kw0 + 32 * u + li, nk - 1)) * a.ldk + h * 32 + 16 * lh;
 #pragma unroll
       for (int q = 0; q < 4; ++q) kf[u][q] = ld4g(kp + 4 * q);
+    }
+#pragma unroll
+    for (int u = 0; u < KT; ++u) {
 #pragma unroll
       for (int j = 0; j < 16; ++j)
         vf[u][j] = a.v[(krow + min(kw0 + 32 * u + acc_row(j, lane), nk - 1)) * a.ldv + h * 32 + li];
@@ -685,6 +723,7 @@ __global__ __launch_bounds__(AT) void tattn_fwd32_kernel(TAttnArgs a) {
     }
   }
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  TA_ST(1);
   float l = 0.f;
   f32x16 ou[KT];   // one P V accumulator per key tile: independent MFMA chains, summed after
 #pragma unroll
@@ -711,6 +750,7 @@ __global__ __launch_bounds__(AT) void tattn_fwd32_kernel(TAttnArgs a) {
   }
 #pragma unroll
   for (int r = 0; r < 16; ++r) xo[w][acc_row(r, lane)][li] = o[r];
+  TA_ST(2);
   __syncthreads();
   // the 4 waves' partials, in wave order; thread -> (query q, d) pairs
   const long long pid = ((long long)vid * a.nh + h) * a.nsplit + c;
@@ -721,38 +761,46 @@ __global__ __launch_bounds__(AT) void tattn_fwd32_kernel(TAttnArgs a) {
   // a one-chunk video writes its rows directly, except when a merge launch follows (no fold, more than
   // one chunk in the launch): that launch merges every video, so every video leaves partials
   const bool direct = ns == 1 && (fold || a.nsplit == 1);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int e = tid + i * AT, q = e >> 5, d = e & 31;
+  {   // thread -> (query tid / 8, 4 consecutive d): one 16-B partial store (the merge reads it back the same way)
+    const int q = tid >> 3, d0 = (tid & 7) * 4;
     float M = -INFINITY;
 #pragma unroll
     for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, xm[ww][q]);
-    float O = 0.f, L = 0.f;
+    float4 O = make_float4(0.f, 0.f, 0.f, 0.f);
+    float L = 0.f;
 #pragma unroll
     for (int ww = 0; ww < 4; ++ww) {
       const float f = xm[ww][q] == -INFINITY ? 0.f : __expf(xm[ww][q] - M);
-      O += f * xo[ww][d][q];
+      O.x += f * xo[ww][d0][q];
+      O.y += f * xo[ww][d0 + 1][q];
+      O.z += f * xo[ww][d0 + 2][q];
+      O.w += f * xo[ww][d0 + 3][q];
       L += f * xl[ww][q];
     }
     if (direct) {
       if (q < a.Qv) {
-        a.out[(qrow + q) * a.ld_out + h * 32 + d] = O / L;
-        if (d == 0) a.lse[((long long)vid * a.nh + h) * a.qs + a.q0 + q] = M + __logf(L);
+        float* op = a.out + (qrow + q) * a.ld_out + h * 32 + d0;
+        op[0] = O.x / L;
+        op[1] = O.y / L;
+        op[2] = O.z / L;
+        op[3] = O.w / L;
+        if (d0 == 0) a.lse[((long long)vid * a.nh + h) * a.qs + a.q0 + q] = M + __logf(L);
       }
     } else if (fold) {
-      stc1(a.ws, (pid * 32 + q) * 32 + d, O);
-      if (d == 0) {
+      stc4(a.ws, (pid * 32 + q) * 32 + d0, O);
+      if (d0 == 0) {
         stc1(pm, pid * 32 + q, M);
         stc1(pl, pid * 32 + q, L);
       }
     } else {
-      a.ws[(pid * 32 + q) * 32 + d] = O;
-      if (d == 0) {
+      *reinterpret_cast<float4*>(a.ws + (pid * 32 + q) * 32 + d0) = O;
+      if (d0 == 0) {
         pm[pid * 32 + q] = M;
         pl[pid * 32 + q] = L;
       }
     }
   }
+  TA_ST(3);
   if (ns > 1 && fold) {
     __shared__ int last;
     // (the wave partial images are free now: the merge's weights reuse them)
@@ -880,16 +928,25 @@ __global__ __launch_bounds__(AT) void tattn_bwd32_kernel(TAttnArgs a) {
   const int ns = (Tv + a.Tc - 1) / a.Tc;
   const bool fold = a.cnt != nullptr;
   const bool direct = ns == 1 && (fold || a.nsplit == 1);   // (see the forward)
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int e = tid + i * AT, q = e >> 5, d = e & 31;
-    const float v = (xq[0][q][d] + xq[1][q][d]) + (xq[2][q][d] + xq[3][q][d]);
+  {   // thread -> (query tid / 8, 4 consecutive d): one 16-B partial store (as the forward)
+    const int q = tid >> 3, d0 = (tid & 7) * 4;
+    float4 v;
+    v.x = (xq[0][q][d0] + xq[1][q][d0]) + (xq[2][q][d0] + xq[3][q][d0]);
+    v.y = (xq[0][q][d0 + 1] + xq[1][q][d0 + 1]) + (xq[2][q][d0 + 1] + xq[3][q][d0 + 1]);
+    v.z = (xq[0][q][d0 + 2] + xq[1][q][d0 + 2]) + (xq[2][q][d0 + 2] + xq[3][q][d0 + 2]);
+    v.w = (xq[0][q][d0 + 3] + xq[1][q][d0 + 3]) + (xq[2][q][d0 + 3] + xq[3][q][d0 + 3]);
     if (direct) {
-      if (q < Qv) a.out[(qrow + q) * a.ld_out + h * 32 + d] = v * a.scale;
+      if (q < Qv) {
+        float* op = a.out + (qrow + q) * a.ld_out + h * 32 + d0;
+        op[0] = v.x * a.scale;
+        op[1] = v.y * a.scale;
+        op[2] = v.z * a.scale;
+        op[3] = v.w * a.scale;
+      }
     } else if (fold) {
-      stc1(a.ws, (pid * 32 + q) * 32 + d, v);
+      stc4(a.ws, (pid * 32 + q) * 32 + d0, v);
     } else {
-      a.ws[(pid * 32 + q) * 32 + d] = v;
+      *reinterpret_cast<float4*>(a.ws + (pid * 32 + q) * 32 + d0) = v;
     }
   }
   if (ns > 1 && fold) {
@@ -1116,3 +1173,9 @@ int launch_tattn_bwd(const float* q, long long ldq, const float* k, long long ld
 }
 
 }  // namespace fx
+
+#ifdef TATTN_STAMPS
+extern "C" int fx_debug_tattn_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(fx::g_ta_st), sizeof(fx::g_ta_st)) == hipSuccess ? 0 : -1;
+}
+#endif
