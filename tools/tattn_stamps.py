@@ -53,6 +53,8 @@ def main():
         s0 = rel[:, 0]
         print("  start by block id (16 per (video, head)): " + " ".join(f"{s0[g * 16:(g + 1) * 16].min():.1f}-"
                                                                   f"{s0[g * 16:(g + 1) * 16].max():.1f}" for g in range(16)))
+        print("  start by chunk (mean over the 16 (video, head)): " +
+              " ".join(f"{s0.reshape(16, 16)[:, c].mean():.1f}" for c in range(16)))
         print(f"  arrival spread per (video, head): median "
               f"{np.median([np.ptp(rel[g * 16:(g + 1) * 16, 5]) for g in range(16)]):.2f} us")
 
